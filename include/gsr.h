@@ -1,0 +1,113 @@
+/*
+ * gsr.h -- C ABI of libgsr, the MI355X (gfx950) differentiable Gaussian rasterizer.
+ *
+ * This is the drop-in boundary that replaces the reference's pybind11 module `_C`
+ * (submodules/diff-gaussian-rasterization/ext.cpp:15-19) and its libtorch glue
+ * (rasterize_points.cu:27-217).  Plain pointers and sizes only: no torch types cross it.
+ *
+ * Conventions (identical to the reference binding):
+ *  - every tensor is float32 (radii int32), C-contiguous, on the current HIP device;
+ *  - a NULL pointer means "empty tensor" (the reference passes data_ptr() of torch.Tensor([]),
+ *    i.e. nullptr: rasterize_points.cu:84-110, rasterizer_impl.cu:229-232,321,389,411);
+ *  - images are planar [C,H,W];  the 4x4 matrices are the reference's row-major tensors
+ *    world_view_transform / full_proj_transform (scene/cameras.py:76-81);
+ *  - all work is enqueued on `stream` (a hipStream_t, NULL = legacy default stream); the forward
+ *    performs one 8-byte device->host read of the instance count (as rasterizer_impl.cu:281 does);
+ *  - scratch memory is owned by the caller: the library requests it through `alloc`, mirroring
+ *    resizeFunctional (rasterize_points.cu:27-33); `which` is GSR_BUF_GEOM / _BINNING / _IMAGE.
+ *    The three buffers must be handed back unchanged to the backward;
+ *  - errors are reported as a non-zero gsr_status; gsr_last_error() gives a message
+ *    (thread-local).  No C++ exception crosses the ABI.
+ *
+ * Extended outputs (depth / alpha / language feature / confidence) follow DESIGN.md section 3.
+ */
+#ifndef GSR_H
+#define GSR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GSR_ABI_VERSION 1
+
+typedef enum gsr_status {
+  GSR_OK = 0,
+  GSR_ERR_ARGUMENT = 1,     /* shape / pointer / alignment validation (rasterize_points.cu:57-59) */
+  GSR_ERR_HIP = 2,          /* a HIP runtime call or kernel launch failed */
+  GSR_ERR_ALLOC = 3,        /* the allocator callback returned NULL */
+  GSR_ERR_PREFILTERED = 4,  /* a Gaussian was culled although prefiltered was set (auxiliary.h:156-160) */
+  GSR_ERR_TOO_LARGE = 5     /* problem exceeds the scan/sort capacity */
+} gsr_status;
+
+enum { GSR_BUF_GEOM = 0, GSR_BUF_BINNING = 1, GSR_BUF_IMAGE = 2 };
+
+/* Returns a device pointer to at least `bytes` bytes (16-byte aligned) or NULL. */
+typedef void* (*gsr_alloc_fn)(void* ctx, size_t bytes, int which);
+
+int gsr_abi_version(void);
+const char* gsr_last_error(void);
+
+/* Forward.  Replaces _C.rasterize_gaussians -> RasterizeGaussiansCUDA (rasterize_points.cu:35-115)
+ * -> CudaRasterizer::Rasterizer::forward (rasterizer_impl.cu:198-336); argument order follows the
+ * reference, the extended-API inputs/outputs are appended.  M = sh.size(1) (0 without SH).
+ * Outputs: out_color[3,H,W] (= blend + T*bg), out_depth[1,H,W], out_alpha[1,H,W],
+ * out_feature[3,H,W] (zeros unless include_feature), radii[P] (NULL -> internal),
+ * *num_rendered (the reference's first return value).  With P == 0 nothing is written except
+ * *num_rendered = 0 and out_* are zero-filled (the reference returns its zero-initialised tensors). */
+int gsr_rasterize_gaussians(
+    int P, int M,
+    const float* background, const float* means3D, const float* colors_precomp,
+    const float* opacities, const float* scales, const float* rotations, float scale_modifier,
+    const float* cov3D_precomp, const float* viewmatrix, const float* projmatrix,
+    float tan_fovx, float tan_fovy, int image_height, int image_width,
+    const float* sh, int degree, const float* campos, int prefiltered,
+    const float* sh_language, const float* language_feature_precomp, const float* confidence,
+    int include_feature,
+    float* out_color, float* out_depth, float* out_alpha, float* out_feature, int* radii,
+    int* num_rendered,
+    gsr_alloc_fn alloc, void* alloc_ctx,
+    void* stream, int debug);
+
+/* Backward.  Replaces _C.rasterize_gaussians_backward -> RasterizeGaussiansBackwardCUDA
+ * (rasterize_points.cu:117-196) -> CudaRasterizer::Rasterizer::backward (rasterizer_impl.cu:340-434).
+ * R is the forward's num_rendered; geom/binning/image are the buffers the forward allocated.
+ * Upstream grads dL_dout_depth / _alpha / _feature may be NULL (== zeros).
+ * Every element of every non-NULL grad output is written (culled Gaussians get zeros):
+ *   dL_dmeans2D[P,3] (NDC-scaled x,y; z = 0), dL_dcolors[P,3] (may be NULL), dL_dopacity[P],
+ *   dL_dmeans3D[P,3], dL_dcov3D[P,6] (may be NULL), dL_dsh[P,M,3] (required iff sh),
+ *   dL_dscales[P,3] / dL_drotations[P,4] (required iff scales), dL_dsh_language[P,3],
+ *   dL_dlanguage_feature[P,3]. */
+int gsr_rasterize_gaussians_backward(
+    int P, int M, int R,
+    const float* background, const float* means3D, const int* radii, const float* colors_precomp,
+    const float* scales, const float* rotations, float scale_modifier, const float* cov3D_precomp,
+    const float* viewmatrix, const float* projmatrix, float tan_fovx, float tan_fovy,
+    int image_height, int image_width,
+    const float* dL_dout_color, const float* dL_dout_depth, const float* dL_dout_alpha,
+    const float* dL_dout_feature,
+    const float* sh, int degree, const float* campos,
+    const float* sh_language, const float* language_feature_precomp, const float* confidence,
+    int include_feature,
+    void* geom_buffer, void* binning_buffer, void* image_buffer,
+    float* dL_dmeans2D, float* dL_dcolors, float* dL_dopacity, float* dL_dmeans3D,
+    float* dL_dcov3D, float* dL_dsh, float* dL_dscales, float* dL_drotations,
+    float* dL_dsh_language, float* dL_dlanguage_feature,
+    void* stream, int debug);
+
+/* Replaces _C.mark_visible -> markVisible (rasterize_points.cu:198-217) -> checkFrustum
+ * (rasterizer_impl.cu:54-66): present[i] = view-space z > 0.2 (bool as uint8). */
+int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
+                     uint8_t* present, void* stream);
+
+/* Byte sizes of the three scratch buffers (for callers that pre-allocate). */
+size_t gsr_geom_buffer_bytes(int P);
+size_t gsr_binning_buffer_bytes(int R);
+size_t gsr_image_buffer_bytes(int image_height, int image_width);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GSR_H */

@@ -1,0 +1,881 @@
+/*
+ * gsr_oracle.c -- CPU restatement of the reference differentiable Gaussian rasterizer.
+ *
+ * TEST INFRASTRUCTURE ONLY (see gsr_oracle.h).  Never linked into the product.
+ *
+ * Every function cites the reference file:line it restates; paths are relative to
+ * /root/reference/submodules/diff-gaussian-rasterization/.  Parity pinning: the reference ships no
+ * tests or golden vectors for this path and its CUDA sources cannot be built
+ * here (no nvcc, un-vendored glm: SURVEY.md 8(c)), so this restatement is pinned by (a) golden
+ * vectors generated from the importable reference Python maths (eval_sh, getProjectionMatrix,
+ * getWorld2View2) in tests/golden/, (b) analytic known-answer cases, and (c) a float64 autograd
+ * cross-check of the backward (tests/test_oracle_autograd.py).
+ */
+#include "gsr_oracle.h"
+
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define BLOCK_X 16 /* config.h:16 */
+#define BLOCK_Y 16 /* config.h:17 */
+#define NCH 8      /* blend channels: r g b | depth | alpha | f0 f1 f2 */
+
+/* SH constants, auxiliary.h:22-39 */
+static const float SH_C0 = 0.28209479177387814f;
+static const float SH_C1 = 0.4886025119029199f;
+static const float SH_C2[5] = {1.0925484305920792f, -1.0925484305920792f, 0.31539156525252005f,
+                               -1.0925484305920792f, 0.5462742152960396f};
+static const float SH_C3[7] = {-0.5900435899266435f, 2.890611442640554f, -0.4570457994644658f,
+                               0.3731763325901154f,  -0.4570457994644658f, 1.445305721320277f,
+                               -0.5900435899266435f};
+
+/* ------------------------------------------------------------------------------------------ */
+/* glm-like column-major 3x3 maths with glm's evaluation order (the reference uses glm, which  */
+/* is un-vendored; column-major constructor semantics matter).                   */
+/* ------------------------------------------------------------------------------------------ */
+typedef struct { float x, y, z; } v3;
+typedef struct { float m[3][3]; } m3; /* m[col][row] like glm::mat3 */
+
+static m3 m3_cols(float a0, float a1, float a2, float b0, float b1, float b2, float c0, float c1,
+                  float c2) {
+    m3 r;
+    r.m[0][0] = a0; r.m[0][1] = a1; r.m[0][2] = a2;
+    r.m[1][0] = b0; r.m[1][1] = b1; r.m[1][2] = b2;
+    r.m[2][0] = c0; r.m[2][1] = c1; r.m[2][2] = c2;
+    return r;
+}
+/* glm operator*(mat3, mat3): R[c][r] = A[0][r]*B[c][0] + A[1][r]*B[c][1] + A[2][r]*B[c][2] */
+static m3 m3_mul(m3 a, m3 b) {
+    m3 r;
+    for (int c = 0; c < 3; c++)
+        for (int w = 0; w < 3; w++) {
+            float t0 = a.m[0][w] * b.m[c][0];
+            float t1 = a.m[1][w] * b.m[c][1];
+            float t2 = a.m[2][w] * b.m[c][2];
+            r.m[c][w] = t0 + t1 + t2;
+        }
+    return r;
+}
+static m3 m3_T(m3 a) {
+    m3 r;
+    for (int c = 0; c < 3; c++)
+        for (int w = 0; w < 3; w++) r.m[c][w] = a.m[w][c];
+    return r;
+}
+static m3 m3_scale(float s, m3 a) {
+    m3 r;
+    for (int c = 0; c < 3; c++)
+        for (int w = 0; w < 3; w++) r.m[c][w] = s * a.m[c][w];
+    return r;
+}
+static float v3_dot(v3 a, v3 b) {
+    float tx = a.x * b.x, ty = a.y * b.y, tz = a.z * b.z;
+    return tx + ty + tz;
+}
+static v3 v3_mk(float x, float y, float z) { v3 r = {x, y, z}; return r; }
+static v3 v3_add(v3 a, v3 b) { return v3_mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+static v3 v3_sub(v3 a, v3 b) { return v3_mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+static v3 v3_muls(float s, v3 a) { return v3_mk(s * a.x, s * a.y, s * a.z); }
+static v3 v3_mul_s(v3 a, float s) { return v3_mk(a.x * s, a.y * s, a.z * s); }
+
+/* CUDA/HIP float->int conversion semantics: round toward zero, saturate, NaN -> 0. */
+static int f2i_sat(float f) {
+    if (f != f) return 0;
+    if (f >= 2147483648.0f) return 2147483647;
+    if (f <= -2147483648.0f) return (-2147483647 - 1);
+    return (int)f;
+}
+static float fminf_cuda(float a, float b) { return fminf(a, b); }
+static float fmaxf_cuda(float a, float b) { return fmaxf(a, b); }
+
+/* auxiliary.h:41-44: promoted to double */
+static float ndc2Pix(float v, int S) { return (float)((((double)v + 1.0) * S - 1.0) * 0.5); }
+
+typedef struct { unsigned x, y; } u2;
+/* auxiliary.h:46-56 */
+static void getRect(float px, float py, int max_radius, u2* rmin, u2* rmax, unsigned gx,
+                    unsigned gy) {
+    int a = f2i_sat((px - (float)max_radius) / (float)BLOCK_X);
+    int b = f2i_sat((py - (float)max_radius) / (float)BLOCK_Y);
+    int c = f2i_sat((((px + (float)max_radius) + (float)BLOCK_X) - 1.0f) / (float)BLOCK_X);
+    int d = f2i_sat((((py + (float)max_radius) + (float)BLOCK_Y) - 1.0f) / (float)BLOCK_Y);
+    a = a > 0 ? a : 0; b = b > 0 ? b : 0; c = c > 0 ? c : 0; d = d > 0 ? d : 0;
+    rmin->x = (unsigned)a < gx ? (unsigned)a : gx;
+    rmin->y = (unsigned)b < gy ? (unsigned)b : gy;
+    rmax->x = (unsigned)c < gx ? (unsigned)c : gx;
+    rmax->y = (unsigned)d < gy ? (unsigned)d : gy;
+}
+
+/* auxiliary.h:58-87 */
+static v3 transformPoint4x3(v3 p, const float* m) {
+    return v3_mk(m[0] * p.x + m[4] * p.y + m[8] * p.z + m[12],
+                 m[1] * p.x + m[5] * p.y + m[9] * p.z + m[13],
+                 m[2] * p.x + m[6] * p.y + m[10] * p.z + m[14]);
+}
+static void transformPoint4x4(v3 p, const float* m, float out[4]) {
+    out[0] = m[0] * p.x + m[4] * p.y + m[8] * p.z + m[12];
+    out[1] = m[1] * p.x + m[5] * p.y + m[9] * p.z + m[13];
+    out[2] = m[2] * p.x + m[6] * p.y + m[10] * p.z + m[14];
+    out[3] = m[3] * p.x + m[7] * p.y + m[11] * p.z + m[15];
+}
+/* auxiliary.h:89-97 */
+static v3 transformVec4x3Transpose(v3 p, const float* m) {
+    return v3_mk(m[0] * p.x + m[1] * p.y + m[2] * p.z, m[4] * p.x + m[5] * p.y + m[6] * p.z,
+                 m[8] * p.x + m[9] * p.y + m[10] * p.z);
+}
+/* auxiliary.h:107-117 */
+static v3 dnormvdv(v3 v, v3 dv) {
+    float sum2 = v.x * v.x + v.y * v.y + v.z * v.z;
+    float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
+    v3 r;
+    r.x = ((+sum2 - v.x * v.x) * dv.x - v.y * v.x * dv.y - v.z * v.x * dv.z) * invsum32;
+    r.y = (-v.x * v.y * dv.x + (sum2 - v.y * v.y) * dv.y - v.z * v.y * dv.z) * invsum32;
+    r.z = (-v.x * v.z * dv.x - v.y * v.z * dv.y + (sum2 - v.z * v.z) * dv.z) * invsum32;
+    return r;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* State                                                                                      */
+/* ------------------------------------------------------------------------------------------ */
+struct oracle_state {
+    int P, M, D, W, H, prefiltered, include_feature;
+    unsigned gx, gy;
+    float scale_modifier, tan_fovx, tan_fovy, focal_x, focal_y;
+    float bg[3], view[16], proj[16], campos[3];
+    /* inputs (borrowed: the caller keeps them alive between forward and backward) */
+    const float *means3D, *colors_precomp, *opacities, *scales, *rotations, *cov3D_precomp, *sh,
+        *sh_language, *lang_precomp, *confidence;
+    /* geometry (GeometryState, rasterizer_impl.h:21-37) */
+    float* depths;
+    unsigned char* clamped; /* [P*3] */
+    int* radii;
+    float* means2D;       /* [P*2] */
+    float* cov3D;         /* [P*6] */
+    float* conic_opacity; /* [P*4] (opacity already multiplied by confidence) */
+    float* rgb;           /* [P*3] */
+    float* feat;          /* [P*3] */
+    unsigned* tiles_touched;
+    /* binning */
+    int R;
+    unsigned* point_list;
+    unsigned* ranges; /* [tiles*2] */
+    /* image */
+    float* final_T;
+    unsigned* n_contrib;
+};
+
+/* forward.cu:20-71 computeColorFromSH */
+static v3 color_from_sh(int idx, int deg, int max_coeffs, const float* means, const float* campos,
+                        const float* shs, unsigned char* clamped) {
+    v3 pos = v3_mk(means[3 * idx], means[3 * idx + 1], means[3 * idx + 2]);
+    v3 dir = v3_sub(pos, v3_mk(campos[0], campos[1], campos[2]));
+    float len = sqrtf(v3_dot(dir, dir));
+    dir = v3_mk(dir.x / len, dir.y / len, dir.z / len);
+    const float* s = shs + (size_t)idx * max_coeffs * 3;
+#define SH(k) v3_mk(s[3 * (k)], s[3 * (k) + 1], s[3 * (k) + 2])
+    v3 result = v3_muls(SH_C0, SH(0));
+    if (deg > 0) {
+        float x = dir.x, y = dir.y, z = dir.z;
+        result = v3_sub(v3_add(v3_sub(result, v3_muls(SH_C1 * y, SH(1))), v3_muls(SH_C1 * z, SH(2))),
+                        v3_muls(SH_C1 * x, SH(3)));
+        if (deg > 1) {
+            float xx = x * x, yy = y * y, zz = z * z;
+            float xy = x * y, yz = y * z, xz = x * z;
+            result = v3_add(result, v3_muls(SH_C2[0] * xy, SH(4)));
+            result = v3_add(result, v3_muls(SH_C2[1] * yz, SH(5)));
+            result = v3_add(result, v3_muls(SH_C2[2] * (2.0f * zz - xx - yy), SH(6)));
+            result = v3_add(result, v3_muls(SH_C2[3] * xz, SH(7)));
+            result = v3_add(result, v3_muls(SH_C2[4] * (xx - yy), SH(8)));
+            if (deg > 2) {
+                result = v3_add(result, v3_muls(SH_C3[0] * y * (3.0f * xx - yy), SH(9)));
+                result = v3_add(result, v3_muls(SH_C3[1] * xy * z, SH(10)));
+                result = v3_add(result, v3_muls(SH_C3[2] * y * (4.0f * zz - xx - yy), SH(11)));
+                result = v3_add(result,
+                                v3_muls(SH_C3[3] * z * (2.0f * zz - 3.0f * xx - 3.0f * yy), SH(12)));
+                result = v3_add(result, v3_muls(SH_C3[4] * x * (4.0f * zz - xx - yy), SH(13)));
+                result = v3_add(result, v3_muls(SH_C3[5] * z * (xx - yy), SH(14)));
+                result = v3_add(result, v3_muls(SH_C3[6] * x * (xx - 3.0f * yy), SH(15)));
+            }
+        }
+    }
+#undef SH
+    result = v3_mk(result.x + 0.5f, result.y + 0.5f, result.z + 0.5f);
+    clamped[3 * idx + 0] = result.x < 0;
+    clamped[3 * idx + 1] = result.y < 0;
+    clamped[3 * idx + 2] = result.z < 0;
+    return v3_mk(fmaxf_cuda(result.x, 0.0f), fmaxf_cuda(result.y, 0.0f), fmaxf_cuda(result.z, 0.0f));
+}
+
+/* forward.cu:74-113 computeCov2D */
+static void cov2d(v3 mean, float fx, float fy, float tanx, float tany, const float* c3,
+                  const float* view, float out[3]) {
+    v3 t = transformPoint4x3(mean, view);
+    const float limx = 1.3f * tanx;
+    const float limy = 1.3f * tany;
+    const float txtz = t.x / t.z;
+    const float tytz = t.y / t.z;
+    t.x = fminf_cuda(limx, fmaxf_cuda(-limx, txtz)) * t.z;
+    t.y = fminf_cuda(limy, fmaxf_cuda(-limy, tytz)) * t.z;
+    m3 J = m3_cols(fx / t.z, 0.0f, -(fx * t.x) / (t.z * t.z), 0.0f, fy / t.z,
+                   -(fy * t.y) / (t.z * t.z), 0, 0, 0);
+    m3 W = m3_cols(view[0], view[4], view[8], view[1], view[5], view[9], view[2], view[6],
+                   view[10]);
+    m3 T = m3_mul(W, J);
+    m3 Vrk = m3_cols(c3[0], c3[1], c3[2], c3[1], c3[3], c3[4], c3[2], c3[4], c3[5]);
+    m3 cov = m3_mul(m3_mul(m3_T(T), m3_T(Vrk)), T);
+    cov.m[0][0] += 0.3f;
+    cov.m[1][1] += 0.3f;
+    out[0] = cov.m[0][0];
+    out[1] = cov.m[0][1];
+    out[2] = cov.m[1][1];
+}
+
+/* forward.cu:118-152 computeCov3D (no quaternion normalisation, :127) */
+static void cov3d(const float* scale, float mod, const float* rot, float* out) {
+    m3 S = m3_cols(1, 0, 0, 0, 1, 0, 0, 0, 1);
+    S.m[0][0] = mod * scale[0];
+    S.m[1][1] = mod * scale[1];
+    S.m[2][2] = mod * scale[2];
+    float r = rot[0], x = rot[1], y = rot[2], z = rot[3];
+    m3 R = m3_cols(1.f - 2.f * (y * y + z * z), 2.f * (x * y - r * z), 2.f * (x * z + r * y),
+                   2.f * (x * y + r * z), 1.f - 2.f * (x * x + z * z), 2.f * (y * z - r * x),
+                   2.f * (x * z - r * y), 2.f * (y * z + r * x), 1.f - 2.f * (x * x + y * y));
+    m3 M = m3_mul(S, R);
+    m3 Sigma = m3_mul(m3_T(M), M);
+    out[0] = Sigma.m[0][0];
+    out[1] = Sigma.m[0][1];
+    out[2] = Sigma.m[0][2];
+    out[3] = Sigma.m[1][1];
+    out[4] = Sigma.m[1][2];
+    out[5] = Sigma.m[2][2];
+}
+
+/* auxiliary.h:139-164 in_frustum (near-plane test only) */
+static int in_frustum(int idx, const float* pts, const float* view, v3* p_view) {
+    v3 p = v3_mk(pts[3 * idx], pts[3 * idx + 1], pts[3 * idx + 2]);
+    *p_view = transformPoint4x3(p, view);
+    return !(p_view->z <= 0.2f);
+}
+
+int oracle_mark_visible(int P, const float* means3D, const float* viewmatrix,
+                        const float* projmatrix, unsigned char* present) {
+    (void)projmatrix; /* in_frustum computes p_proj but only uses p_view (auxiliary.h:149-154) */
+    for (int i = 0; i < P; i++) {
+        v3 pv;
+        present[i] = (unsigned char)in_frustum(i, means3D, viewmatrix, &pv);
+    }
+    return 0;
+}
+
+typedef struct { uint64_t key; uint32_t seq; uint32_t val; } inst_t;
+static int inst_cmp(const void* a, const void* b) {
+    const inst_t* x = (const inst_t*)a;
+    const inst_t* y = (const inst_t*)b;
+    if (x->key != y->key) return x->key < y->key ? -1 : 1;
+    return x->seq < y->seq ? -1 : (x->seq > y->seq ? 1 : 0); /* stable: SortPairs is stable */
+}
+
+static void* xcalloc(size_t n, size_t s) { return calloc(n ? n : 1, s); }
+
+oracle_state* oracle_forward(int P, int M, const float* background, const float* means3D,
+                             const float* colors_precomp, const float* opacities,
+                             const float* scales, const float* rotations, float scale_modifier,
+                             const float* cov3D_precomp, const float* viewmatrix,
+                             const float* projmatrix, float tan_fovx, float tan_fovy,
+                             int image_height, int image_width, const float* sh, int degree,
+                             const float* campos, int prefiltered, const float* sh_language,
+                             const float* language_feature_precomp, const float* confidence,
+                             int include_feature, float* out_color, float* out_depth,
+                             float* out_alpha, float* out_feature, int* radii_out,
+                             int* num_rendered) {
+    if (P < 0 || image_height <= 0 || image_width <= 0) return NULL;
+    if (!colors_precomp && !sh) return NULL;
+    if (!cov3D_precomp && (!scales || !rotations)) return NULL;
+    oracle_state* st = (oracle_state*)calloc(1, sizeof(oracle_state));
+    const int W = image_width, H = image_height;
+    st->P = P; st->M = M; st->D = degree; st->W = W; st->H = H;
+    st->prefiltered = prefiltered; st->include_feature = include_feature;
+    st->scale_modifier = scale_modifier; st->tan_fovx = tan_fovx; st->tan_fovy = tan_fovy;
+    /* rasterizer_impl.cu:222-223 */
+    st->focal_y = (float)H / (2.0f * tan_fovy);
+    st->focal_x = (float)W / (2.0f * tan_fovx);
+    memcpy(st->bg, background, sizeof(st->bg));
+    memcpy(st->view, viewmatrix, sizeof(st->view));
+    memcpy(st->proj, projmatrix, sizeof(st->proj));
+    memcpy(st->campos, campos, sizeof(st->campos));
+    st->means3D = means3D; st->colors_precomp = colors_precomp; st->opacities = opacities;
+    st->scales = scales; st->rotations = rotations; st->cov3D_precomp = cov3D_precomp;
+    st->sh = sh; st->sh_language = sh_language; st->lang_precomp = language_feature_precomp;
+    st->confidence = confidence;
+    /* rasterizer_impl.cu:234 */
+    st->gx = (unsigned)((W + BLOCK_X - 1) / BLOCK_X);
+    st->gy = (unsigned)((H + BLOCK_Y - 1) / BLOCK_Y);
+    const unsigned gx = st->gx, gy = st->gy;
+
+    st->depths = (float*)xcalloc(P, sizeof(float));
+    st->clamped = (unsigned char*)xcalloc((size_t)P * 3, 1);
+    st->radii = (int*)xcalloc(P, sizeof(int));
+    st->means2D = (float*)xcalloc((size_t)P * 2, sizeof(float));
+    st->cov3D = (float*)xcalloc((size_t)P * 6, sizeof(float));
+    st->conic_opacity = (float*)xcalloc((size_t)P * 4, sizeof(float));
+    st->rgb = (float*)xcalloc((size_t)P * 3, sizeof(float));
+    st->feat = (float*)xcalloc((size_t)P * 3, sizeof(float));
+    st->tiles_touched = (unsigned*)xcalloc(P, sizeof(unsigned));
+
+    /* ---- preprocessCUDA, forward.cu:155-256 ---- */
+    for (int idx = 0; idx < P; idx++) {
+        st->radii[idx] = 0;
+        st->tiles_touched[idx] = 0;
+        v3 p_view;
+        if (!in_frustum(idx, means3D, viewmatrix, &p_view)) continue;
+        v3 p_orig = v3_mk(means3D[3 * idx], means3D[3 * idx + 1], means3D[3 * idx + 2]);
+        float p_hom[4];
+        transformPoint4x4(p_orig, projmatrix, p_hom);
+        float p_w = 1.0f / (p_hom[3] + 0.0000001f);
+        float p_proj_x = p_hom[0] * p_w, p_proj_y = p_hom[1] * p_w;
+        const float* c3;
+        if (cov3D_precomp) {
+            c3 = cov3D_precomp + (size_t)idx * 6;
+        } else {
+            cov3d(scales + 3 * (size_t)idx, scale_modifier, rotations + 4 * (size_t)idx,
+                  st->cov3D + (size_t)idx * 6);
+            c3 = st->cov3D + (size_t)idx * 6;
+        }
+        float cov[3];
+        cov2d(p_orig, st->focal_x, st->focal_y, tan_fovx, tan_fovy, c3, viewmatrix, cov);
+        float det = (cov[0] * cov[2] - cov[1] * cov[1]);
+        if (det == 0.0f) continue;
+        float det_inv = 1.f / det;
+        float conic[3] = {cov[2] * det_inv, -cov[1] * det_inv, cov[0] * det_inv};
+        float mid = 0.5f * (cov[0] + cov[2]);
+        float lambda1 = mid + sqrtf(fmaxf_cuda(0.1f, mid * mid - det));
+        float lambda2 = mid - sqrtf(fmaxf_cuda(0.1f, mid * mid - det));
+        float my_radius = ceilf(3.f * sqrtf(fmaxf_cuda(lambda1, lambda2)));
+        float pix_x = ndc2Pix(p_proj_x, W), pix_y = ndc2Pix(p_proj_y, H);
+        u2 rmin, rmax;
+        getRect(pix_x, pix_y, f2i_sat(my_radius), &rmin, &rmax, gx, gy);
+        if ((rmax.x - rmin.x) * (rmax.y - rmin.y) == 0) continue;
+        if (!colors_precomp) {
+            v3 c = color_from_sh(idx, degree, M, means3D, campos, sh, st->clamped);
+            st->rgb[3 * idx + 0] = c.x;
+            st->rgb[3 * idx + 1] = c.y;
+            st->rgb[3 * idx + 2] = c.z;
+        }
+        st->depths[idx] = p_view.z;
+        st->radii[idx] = f2i_sat(my_radius);
+        st->means2D[2 * idx] = pix_x;
+        st->means2D[2 * idx + 1] = pix_y;
+        float op = opacities[idx];
+        if (confidence) op = op * confidence[idx]; /* confidence = opacity multiplier */
+        st->conic_opacity[4 * idx + 0] = conic[0];
+        st->conic_opacity[4 * idx + 1] = conic[1];
+        st->conic_opacity[4 * idx + 2] = conic[2];
+        st->conic_opacity[4 * idx + 3] = op;
+        st->tiles_touched[idx] = (rmax.y - rmin.y) * (rmax.x - rmin.x);
+        if (include_feature) { /* language feature channels */
+            if (language_feature_precomp) {
+                for (int k = 0; k < 3; k++) st->feat[3 * idx + k] = language_feature_precomp[3 * idx + k];
+            } else if (sh_language) {
+                float u0 = SH_C0 * sh_language[3 * idx], u1 = SH_C0 * sh_language[3 * idx + 1],
+                      u2v = SH_C0 * sh_language[3 * idx + 2];
+                float n = sqrtf(u0 * u0 + u1 * u1 + u2v * u2v);
+                float den = n + 1e-9f;
+                st->feat[3 * idx + 0] = u0 / den;
+                st->feat[3 * idx + 1] = u1 / den;
+                st->feat[3 * idx + 2] = u2v / den;
+            }
+        }
+    }
+    if (radii_out) memcpy(radii_out, st->radii, sizeof(int) * (size_t)P);
+
+    /* ---- scan + duplicateWithKeys + stable SortPairs, rasterizer_impl.cu:70-111, 277-308 ---- */
+    uint64_t R64 = 0;
+    for (int i = 0; i < P; i++) R64 += st->tiles_touched[i];
+    int R = (int)R64;
+    st->R = R;
+    inst_t* inst = (inst_t*)xcalloc((size_t)R, sizeof(inst_t));
+    uint32_t off = 0;
+    for (int idx = 0; idx < P; idx++) {
+        if (st->radii[idx] > 0) {
+            u2 rmin, rmax;
+            getRect(st->means2D[2 * idx], st->means2D[2 * idx + 1], st->radii[idx], &rmin, &rmax,
+                    gx, gy);
+            uint32_t dbits;
+            memcpy(&dbits, &st->depths[idx], 4);
+            for (unsigned y = rmin.y; y < rmax.y; y++)
+                for (unsigned x = rmin.x; x < rmax.x; x++) {
+                    uint64_t key = (uint64_t)(y * gx + x);
+                    key <<= 32;
+                    key |= dbits;
+                    inst[off].key = key;
+                    inst[off].seq = off;
+                    inst[off].val = (uint32_t)idx;
+                    off++;
+                }
+        }
+    }
+    qsort(inst, (size_t)R, sizeof(inst_t), inst_cmp);
+    st->point_list = (unsigned*)xcalloc((size_t)R, sizeof(unsigned));
+    for (int i = 0; i < R; i++) st->point_list[i] = inst[i].val;
+    /* identifyTileRanges, rasterizer_impl.cu:116-138 (ranges zeroed first, :310) */
+    const unsigned ntiles = gx * gy;
+    st->ranges = (unsigned*)xcalloc((size_t)ntiles * 2, sizeof(unsigned));
+    for (int i = 0; i < R; i++) {
+        unsigned cur = (unsigned)(inst[i].key >> 32);
+        if (i == 0) st->ranges[2 * cur] = 0;
+        else {
+            unsigned prev = (unsigned)(inst[i - 1].key >> 32);
+            if (cur != prev) {
+                st->ranges[2 * prev + 1] = (unsigned)i;
+                st->ranges[2 * cur] = (unsigned)i;
+            }
+        }
+        if (i == R - 1) st->ranges[2 * cur + 1] = (unsigned)R;
+    }
+    free(inst);
+    if (num_rendered) *num_rendered = R;
+
+    /* ---- renderCUDA (fwd), forward.cu:261-374, extended to NCH channels ---- */
+    st->final_T = (float*)xcalloc((size_t)W * H, sizeof(float));
+    st->n_contrib = (unsigned*)xcalloc((size_t)W * H, sizeof(unsigned));
+    const float* feat_ptr = colors_precomp ? colors_precomp : st->rgb;
+    const int nch = include_feature ? NCH : 5;
+    for (int py = 0; py < H; py++)
+        for (int px = 0; px < W; px++) {
+            const unsigned tile = (unsigned)(py / BLOCK_Y) * gx + (unsigned)(px / BLOCK_X);
+            const unsigned rs = st->ranges[2 * tile], re = st->ranges[2 * tile + 1];
+            const float pfx = (float)px, pfy = (float)py;
+            float T = 1.0f;
+            unsigned contributor = 0, last_contributor = 0;
+            float C[NCH] = {0};
+            for (unsigned k = rs; k < re; k++) {
+                contributor++;
+                const unsigned g = st->point_list[k];
+                const float dx = st->means2D[2 * g] - pfx, dy = st->means2D[2 * g + 1] - pfy;
+                const float* co = st->conic_opacity + 4 * (size_t)g;
+                float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
+                if (power > 0.0f) continue;
+                float alpha = fminf_cuda(0.99f, co[3] * expf(power));
+                if (alpha < 1.0f / 255.0f) continue;
+                float test_T = T * (1 - alpha);
+                if (test_T < 0.0001f) break; /* done: nothing later changes this pixel */
+                float v[NCH];
+                v[0] = feat_ptr[3 * g]; v[1] = feat_ptr[3 * g + 1]; v[2] = feat_ptr[3 * g + 2];
+                v[3] = st->depths[g]; v[4] = 1.0f;
+                v[5] = st->feat[3 * g]; v[6] = st->feat[3 * g + 1]; v[7] = st->feat[3 * g + 2];
+                for (int ch = 0; ch < nch; ch++) C[ch] += v[ch] * alpha * T;
+                T = test_T;
+                last_contributor = contributor;
+            }
+            const size_t pix = (size_t)py * W + px, HW = (size_t)W * H;
+            st->final_T[pix] = T;
+            st->n_contrib[pix] = last_contributor;
+            for (int ch = 0; ch < 3; ch++) out_color[ch * HW + pix] = C[ch] + T * background[ch];
+            if (out_depth) out_depth[pix] = C[3];
+            if (out_alpha) out_alpha[pix] = C[4];
+            if (out_feature)
+                for (int ch = 0; ch < 3; ch++) out_feature[ch * HW + pix] = include_feature ? C[5 + ch] : 0.0f;
+        }
+    return st;
+}
+
+/* backward.cu:20-139 computeColorFromSH (bwd) */
+static void sh_backward(int idx, int deg, int max_coeffs, const float* means, const float* campos,
+                        const float* shs, const unsigned char* clamped, const float* dL_dcolor,
+                        float* dL_dmeans, float* dL_dshs) {
+    v3 pos = v3_mk(means[3 * idx], means[3 * idx + 1], means[3 * idx + 2]);
+    v3 dir_orig = v3_sub(pos, v3_mk(campos[0], campos[1], campos[2]));
+    float len = sqrtf(v3_dot(dir_orig, dir_orig));
+    v3 dir = v3_mk(dir_orig.x / len, dir_orig.y / len, dir_orig.z / len);
+    const float* s = shs + (size_t)idx * max_coeffs * 3;
+#define SH(k) v3_mk(s[3 * (k)], s[3 * (k) + 1], s[3 * (k) + 2])
+    v3 dL_dRGB = v3_mk(dL_dcolor[3 * idx], dL_dcolor[3 * idx + 1], dL_dcolor[3 * idx + 2]);
+    dL_dRGB.x *= clamped[3 * idx + 0] ? 0 : 1;
+    dL_dRGB.y *= clamped[3 * idx + 1] ? 0 : 1;
+    dL_dRGB.z *= clamped[3 * idx + 2] ? 0 : 1;
+    v3 dRGBdx = v3_mk(0, 0, 0), dRGBdy = v3_mk(0, 0, 0), dRGBdz = v3_mk(0, 0, 0);
+    float x = dir.x, y = dir.y, z = dir.z;
+    float* d = dL_dshs + (size_t)idx * max_coeffs * 3;
+#define PUT(k, v) do { v3 _t = (v); d[3 * (k)] = _t.x; d[3 * (k) + 1] = _t.y; d[3 * (k) + 2] = _t.z; } while (0)
+    float dRGBdsh0 = SH_C0;
+    PUT(0, v3_muls(dRGBdsh0, dL_dRGB));
+    if (deg > 0) {
+        float dRGBdsh1 = -SH_C1 * y;
+        float dRGBdsh2 = SH_C1 * z;
+        float dRGBdsh3 = -SH_C1 * x;
+        PUT(1, v3_muls(dRGBdsh1, dL_dRGB));
+        PUT(2, v3_muls(dRGBdsh2, dL_dRGB));
+        PUT(3, v3_muls(dRGBdsh3, dL_dRGB));
+        dRGBdx = v3_muls(-SH_C1, SH(3));
+        dRGBdy = v3_muls(-SH_C1, SH(1));
+        dRGBdz = v3_muls(SH_C1, SH(2));
+        if (deg > 1) {
+            float xx = x * x, yy = y * y, zz = z * z;
+            float xy = x * y, yz = y * z, xz = x * z;
+            float dRGBdsh4 = SH_C2[0] * xy;
+            float dRGBdsh5 = SH_C2[1] * yz;
+            float dRGBdsh6 = SH_C2[2] * (2.f * zz - xx - yy);
+            float dRGBdsh7 = SH_C2[3] * xz;
+            float dRGBdsh8 = SH_C2[4] * (xx - yy);
+            PUT(4, v3_muls(dRGBdsh4, dL_dRGB));
+            PUT(5, v3_muls(dRGBdsh5, dL_dRGB));
+            PUT(6, v3_muls(dRGBdsh6, dL_dRGB));
+            PUT(7, v3_muls(dRGBdsh7, dL_dRGB));
+            PUT(8, v3_muls(dRGBdsh8, dL_dRGB));
+            v3 tx = v3_add(v3_add(v3_add(v3_muls(SH_C2[0] * y, SH(4)), v3_muls(SH_C2[2] * 2.f * -x, SH(6))),
+                                  v3_muls(SH_C2[3] * z, SH(7))),
+                           v3_muls(SH_C2[4] * 2.f * x, SH(8)));
+            v3 ty = v3_add(v3_add(v3_add(v3_muls(SH_C2[0] * x, SH(4)), v3_muls(SH_C2[1] * z, SH(5))),
+                                  v3_muls(SH_C2[2] * 2.f * -y, SH(6))),
+                           v3_muls(SH_C2[4] * 2.f * -y, SH(8)));
+            v3 tz = v3_add(v3_add(v3_muls(SH_C2[1] * y, SH(5)), v3_muls(SH_C2[2] * 2.f * 2.f * z, SH(6))),
+                           v3_muls(SH_C2[3] * x, SH(7)));
+            dRGBdx = v3_add(dRGBdx, tx);
+            dRGBdy = v3_add(dRGBdy, ty);
+            dRGBdz = v3_add(dRGBdz, tz);
+            if (deg > 2) {
+                float dRGBdsh9 = SH_C3[0] * y * (3.f * xx - yy);
+                float dRGBdsh10 = SH_C3[1] * xy * z;
+                float dRGBdsh11 = SH_C3[2] * y * (4.f * zz - xx - yy);
+                float dRGBdsh12 = SH_C3[3] * z * (2.f * zz - 3.f * xx - 3.f * yy);
+                float dRGBdsh13 = SH_C3[4] * x * (4.f * zz - xx - yy);
+                float dRGBdsh14 = SH_C3[5] * z * (xx - yy);
+                float dRGBdsh15 = SH_C3[6] * x * (xx - 3.f * yy);
+                PUT(9, v3_muls(dRGBdsh9, dL_dRGB));
+                PUT(10, v3_muls(dRGBdsh10, dL_dRGB));
+                PUT(11, v3_muls(dRGBdsh11, dL_dRGB));
+                PUT(12, v3_muls(dRGBdsh12, dL_dRGB));
+                PUT(13, v3_muls(dRGBdsh13, dL_dRGB));
+                PUT(14, v3_muls(dRGBdsh14, dL_dRGB));
+                PUT(15, v3_muls(dRGBdsh15, dL_dRGB));
+                /* backward.cu:99-122: (scalar*vec3) then chained vec3*scalar products */
+                v3 ax = v3_mul_s(v3_mul_s(v3_mul_s(v3_muls(SH_C3[0], SH(9)), 3.f), 2.f), xy);
+                ax = v3_add(ax, v3_mul_s(v3_muls(SH_C3[1], SH(10)), yz));
+                ax = v3_add(ax, v3_mul_s(v3_mul_s(v3_muls(SH_C3[2], SH(11)), -2.f), xy));
+                ax = v3_add(ax, v3_mul_s(v3_mul_s(v3_mul_s(v3_muls(SH_C3[3], SH(12)), -3.f), 2.f), xz));
+                ax = v3_add(ax, v3_mul_s(v3_muls(SH_C3[4], SH(13)), (-3.f * xx + 4.f * zz - yy)));
+                ax = v3_add(ax, v3_mul_s(v3_mul_s(v3_muls(SH_C3[5], SH(14)), 2.f), xz));
+                ax = v3_add(ax, v3_mul_s(v3_mul_s(v3_muls(SH_C3[6], SH(15)), 3.f), (xx - yy)));
+                v3 ay = v3_mul_s(v3_mul_s(v3_muls(SH_C3[0], SH(9)), 3.f), (xx - yy));
+                ay = v3_add(ay, v3_mul_s(v3_muls(SH_C3[1], SH(10)), xz));
+                ay = v3_add(ay, v3_mul_s(v3_muls(SH_C3[2], SH(11)), (-3.f * yy + 4.f * zz - xx)));
+                ay = v3_add(ay, v3_mul_s(v3_mul_s(v3_mul_s(v3_muls(SH_C3[3], SH(12)), -3.f), 2.f), yz));
+                ay = v3_add(ay, v3_mul_s(v3_mul_s(v3_muls(SH_C3[4], SH(13)), -2.f), xy));
+                ay = v3_add(ay, v3_mul_s(v3_mul_s(v3_muls(SH_C3[5], SH(14)), -2.f), yz));
+                ay = v3_add(ay, v3_mul_s(v3_mul_s(v3_mul_s(v3_muls(SH_C3[6], SH(15)), -3.f), 2.f), xy));
+                v3 az = v3_mul_s(v3_muls(SH_C3[1], SH(10)), xy);
+                az = v3_add(az, v3_mul_s(v3_mul_s(v3_mul_s(v3_muls(SH_C3[2], SH(11)), 4.f), 2.f), yz));
+                az = v3_add(az, v3_mul_s(v3_mul_s(v3_muls(SH_C3[3], SH(12)), 3.f), (2.f * zz - xx - yy)));
+                az = v3_add(az, v3_mul_s(v3_mul_s(v3_mul_s(v3_muls(SH_C3[4], SH(13)), 4.f), 2.f), xz));
+                az = v3_add(az, v3_mul_s(v3_muls(SH_C3[5], SH(14)), (xx - yy)));
+                dRGBdx = v3_add(dRGBdx, ax);
+                dRGBdy = v3_add(dRGBdy, ay);
+                dRGBdz = v3_add(dRGBdz, az);
+            }
+        }
+    }
+#undef PUT
+#undef SH
+    v3 dL_ddir = v3_mk(v3_dot(dRGBdx, dL_dRGB), v3_dot(dRGBdy, dL_dRGB), v3_dot(dRGBdz, dL_dRGB));
+    v3 dm = dnormvdv(dir_orig, dL_ddir);
+    dL_dmeans[3 * idx + 0] += dm.x;
+    dL_dmeans[3 * idx + 1] += dm.y;
+    dL_dmeans[3 * idx + 2] += dm.z;
+}
+
+/* backward.cu:144-274 computeCov2DCUDA (per Gaussian) */
+static void cov2d_backward(int idx, const float* means, const float* cov3D, float h_x, float h_y,
+                           float tan_fovx, float tan_fovy, const float* view,
+                           const float* dL_dconics, float* dL_dmeans, float* dL_dcov) {
+    const float* c3 = cov3D + 6 * (size_t)idx;
+    v3 mean = v3_mk(means[3 * idx], means[3 * idx + 1], means[3 * idx + 2]);
+    float dcx = dL_dconics[4 * idx], dcy = dL_dconics[4 * idx + 1], dcz = dL_dconics[4 * idx + 3];
+    v3 t = transformPoint4x3(mean, view);
+    const float limx = 1.3f * tan_fovx;
+    const float limy = 1.3f * tan_fovy;
+    const float txtz = t.x / t.z;
+    const float tytz = t.y / t.z;
+    t.x = fminf_cuda(limx, fmaxf_cuda(-limx, txtz)) * t.z;
+    t.y = fminf_cuda(limy, fmaxf_cuda(-limy, tytz)) * t.z;
+    const float x_grad_mul = txtz < -limx || txtz > limx ? 0 : 1;
+    const float y_grad_mul = tytz < -limy || tytz > limy ? 0 : 1;
+    m3 J = m3_cols(h_x / t.z, 0.0f, -(h_x * t.x) / (t.z * t.z), 0.0f, h_y / t.z,
+                   -(h_y * t.y) / (t.z * t.z), 0, 0, 0);
+    m3 Wm = m3_cols(view[0], view[4], view[8], view[1], view[5], view[9], view[2], view[6],
+                    view[10]);
+    m3 Vrk = m3_cols(c3[0], c3[1], c3[2], c3[1], c3[3], c3[4], c3[2], c3[4], c3[5]);
+    m3 T = m3_mul(Wm, J);
+    m3 cov2D = m3_mul(m3_mul(m3_T(T), m3_T(Vrk)), T);
+    float a = cov2D.m[0][0] += 0.3f;
+    float b = cov2D.m[0][1];
+    float c = cov2D.m[1][1] += 0.3f;
+    float denom = a * c - b * b;
+    float dL_da = 0, dL_db = 0, dL_dc = 0;
+    float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
+    float* dc = dL_dcov + 6 * (size_t)idx;
+#define Tm(cc, rr) T.m[cc][rr]
+#define V(cc, rr) Vrk.m[cc][rr]
+    if (denom2inv != 0) {
+        dL_da = denom2inv * (-c * c * dcx + 2 * b * c * dcy + (denom - a * c) * dcz);
+        dL_dc = denom2inv * (-a * a * dcz + 2 * a * b * dcy + (denom - a * c) * dcx);
+        dL_db = denom2inv * 2 * (b * c * dcx - (denom + 2 * b * b) * dcy + a * b * dcz);
+        dc[0] = (Tm(0, 0) * Tm(0, 0) * dL_da + Tm(0, 0) * Tm(1, 0) * dL_db + Tm(1, 0) * Tm(1, 0) * dL_dc);
+        dc[3] = (Tm(0, 1) * Tm(0, 1) * dL_da + Tm(0, 1) * Tm(1, 1) * dL_db + Tm(1, 1) * Tm(1, 1) * dL_dc);
+        dc[5] = (Tm(0, 2) * Tm(0, 2) * dL_da + Tm(0, 2) * Tm(1, 2) * dL_db + Tm(1, 2) * Tm(1, 2) * dL_dc);
+        dc[1] = 2 * Tm(0, 0) * Tm(0, 1) * dL_da + (Tm(0, 0) * Tm(1, 1) + Tm(0, 1) * Tm(1, 0)) * dL_db +
+                2 * Tm(1, 0) * Tm(1, 1) * dL_dc;
+        dc[2] = 2 * Tm(0, 0) * Tm(0, 2) * dL_da + (Tm(0, 0) * Tm(1, 2) + Tm(0, 2) * Tm(1, 0)) * dL_db +
+                2 * Tm(1, 0) * Tm(1, 2) * dL_dc;
+        dc[4] = 2 * Tm(0, 2) * Tm(0, 1) * dL_da + (Tm(0, 1) * Tm(1, 2) + Tm(0, 2) * Tm(1, 1)) * dL_db +
+                2 * Tm(1, 1) * Tm(1, 2) * dL_dc;
+    } else {
+        for (int i = 0; i < 6; i++) dc[i] = 0;
+    }
+    float dL_dT00 = 2 * (Tm(0, 0) * V(0, 0) + Tm(0, 1) * V(0, 1) + Tm(0, 2) * V(0, 2)) * dL_da +
+                    (Tm(1, 0) * V(0, 0) + Tm(1, 1) * V(0, 1) + Tm(1, 2) * V(0, 2)) * dL_db;
+    float dL_dT01 = 2 * (Tm(0, 0) * V(1, 0) + Tm(0, 1) * V(1, 1) + Tm(0, 2) * V(1, 2)) * dL_da +
+                    (Tm(1, 0) * V(1, 0) + Tm(1, 1) * V(1, 1) + Tm(1, 2) * V(1, 2)) * dL_db;
+    float dL_dT02 = 2 * (Tm(0, 0) * V(2, 0) + Tm(0, 1) * V(2, 1) + Tm(0, 2) * V(2, 2)) * dL_da +
+                    (Tm(1, 0) * V(2, 0) + Tm(1, 1) * V(2, 1) + Tm(1, 2) * V(2, 2)) * dL_db;
+    float dL_dT10 = 2 * (Tm(1, 0) * V(0, 0) + Tm(1, 1) * V(0, 1) + Tm(1, 2) * V(0, 2)) * dL_dc +
+                    (Tm(0, 0) * V(0, 0) + Tm(0, 1) * V(0, 1) + Tm(0, 2) * V(0, 2)) * dL_db;
+    float dL_dT11 = 2 * (Tm(1, 0) * V(1, 0) + Tm(1, 1) * V(1, 1) + Tm(1, 2) * V(1, 2)) * dL_dc +
+                    (Tm(0, 0) * V(1, 0) + Tm(0, 1) * V(1, 1) + Tm(0, 2) * V(1, 2)) * dL_db;
+    float dL_dT12 = 2 * (Tm(1, 0) * V(2, 0) + Tm(1, 1) * V(2, 1) + Tm(1, 2) * V(2, 2)) * dL_dc +
+                    (Tm(0, 0) * V(2, 0) + Tm(0, 1) * V(2, 1) + Tm(0, 2) * V(2, 2)) * dL_db;
+#undef Tm
+#undef V
+    float dL_dJ00 = Wm.m[0][0] * dL_dT00 + Wm.m[0][1] * dL_dT01 + Wm.m[0][2] * dL_dT02;
+    float dL_dJ02 = Wm.m[2][0] * dL_dT00 + Wm.m[2][1] * dL_dT01 + Wm.m[2][2] * dL_dT02;
+    float dL_dJ11 = Wm.m[1][0] * dL_dT10 + Wm.m[1][1] * dL_dT11 + Wm.m[1][2] * dL_dT12;
+    float dL_dJ12 = Wm.m[2][0] * dL_dT10 + Wm.m[2][1] * dL_dT11 + Wm.m[2][2] * dL_dT12;
+    float tz = 1.f / t.z;
+    float tz2 = tz * tz;
+    float tz3 = tz2 * tz;
+    float dL_dtx = x_grad_mul * -h_x * tz2 * dL_dJ02;
+    float dL_dty = y_grad_mul * -h_y * tz2 * dL_dJ12;
+    float dL_dtz = -h_x * tz2 * dL_dJ00 - h_y * tz2 * dL_dJ11 + (2 * h_x * t.x) * tz3 * dL_dJ02 +
+                   (2 * h_y * t.y) * tz3 * dL_dJ12;
+    v3 dm = transformVec4x3Transpose(v3_mk(dL_dtx, dL_dty, dL_dtz), view);
+    dL_dmeans[3 * idx + 0] = dm.x; /* assigned, backward.cu:273 */
+    dL_dmeans[3 * idx + 1] = dm.y;
+    dL_dmeans[3 * idx + 2] = dm.z;
+}
+
+/* backward.cu:278-341 computeCov3D (bwd) */
+static void cov3d_backward(int idx, const float* scale, float mod, const float* rot,
+                           const float* dL_dcov3Ds, float* dL_dscales, float* dL_drots) {
+    float r = rot[0], x = rot[1], y = rot[2], z = rot[3];
+    m3 R = m3_cols(1.f - 2.f * (y * y + z * z), 2.f * (x * y - r * z), 2.f * (x * z + r * y),
+                   2.f * (x * y + r * z), 1.f - 2.f * (x * x + z * z), 2.f * (y * z - r * x),
+                   2.f * (x * z - r * y), 2.f * (y * z + r * x), 1.f - 2.f * (x * x + y * y));
+    m3 S = m3_cols(1, 0, 0, 0, 1, 0, 0, 0, 1);
+    v3 s = v3_muls(mod, v3_mk(scale[0], scale[1], scale[2]));
+    S.m[0][0] = s.x; S.m[1][1] = s.y; S.m[2][2] = s.z;
+    m3 M = m3_mul(S, R);
+    const float* g = dL_dcov3Ds + 6 * (size_t)idx;
+    m3 dL_dSigma = m3_cols(g[0], 0.5f * g[1], 0.5f * g[2], 0.5f * g[1], g[3], 0.5f * g[4],
+                           0.5f * g[2], 0.5f * g[4], g[5]);
+    m3 dL_dM = m3_mul(m3_scale(2.0f, M), dL_dSigma);
+    m3 Rt = m3_T(R);
+    m3 dL_dMt = m3_T(dL_dM);
+    float* ds = dL_dscales + 3 * (size_t)idx;
+    for (int k = 0; k < 3; k++) {
+        v3 a = v3_mk(Rt.m[k][0], Rt.m[k][1], Rt.m[k][2]);
+        v3 b = v3_mk(dL_dMt.m[k][0], dL_dMt.m[k][1], dL_dMt.m[k][2]);
+        ds[k] = v3_dot(a, b);
+    }
+    for (int w = 0; w < 3; w++) {
+        dL_dMt.m[0][w] *= s.x;
+        dL_dMt.m[1][w] *= s.y;
+        dL_dMt.m[2][w] *= s.z;
+    }
+#define D(cc, rr) dL_dMt.m[cc][rr]
+    float* dq = dL_drots + 4 * (size_t)idx;
+    dq[0] = 2 * z * (D(0, 1) - D(1, 0)) + 2 * y * (D(2, 0) - D(0, 2)) + 2 * x * (D(1, 2) - D(2, 1));
+    dq[1] = 2 * y * (D(1, 0) + D(0, 1)) + 2 * z * (D(2, 0) + D(0, 2)) + 2 * r * (D(1, 2) - D(2, 1)) -
+            4 * x * (D(2, 2) + D(1, 1));
+    dq[2] = 2 * x * (D(1, 0) + D(0, 1)) + 2 * r * (D(2, 0) - D(0, 2)) + 2 * z * (D(1, 2) + D(2, 1)) -
+            4 * y * (D(2, 2) + D(0, 0));
+    dq[3] = 2 * r * (D(0, 1) - D(1, 0)) + 2 * x * (D(2, 0) + D(0, 2)) + 2 * y * (D(1, 2) + D(2, 1)) -
+            4 * z * (D(1, 1) + D(0, 0));
+#undef D
+}
+
+int oracle_backward(oracle_state* st, const float* dL_dout_color, const float* dL_dout_depth,
+                    const float* dL_dout_alpha, const float* dL_dout_feature, float* dL_dmeans2D,
+                    float* dL_dcolors, float* dL_dopacity, float* dL_dmeans3D, float* dL_dcov3D,
+                    float* dL_dsh, float* dL_dscales, float* dL_drotations,
+                    float* dL_dsh_language, float* dL_dlanguage_feature) {
+    if (!st) return 1;
+    const int P = st->P, M = st->M, W = st->W, H = st->H;
+    const size_t HW = (size_t)W * H;
+    const unsigned gx = st->gx;
+    /* rasterize_points.cu:151-159 zero-initialised grads */
+    memset(dL_dmeans2D, 0, sizeof(float) * 3 * (size_t)P);
+    memset(dL_dcolors, 0, sizeof(float) * 3 * (size_t)P);
+    memset(dL_dopacity, 0, sizeof(float) * (size_t)P);
+    memset(dL_dmeans3D, 0, sizeof(float) * 3 * (size_t)P);
+    memset(dL_dcov3D, 0, sizeof(float) * 6 * (size_t)P);
+    if (dL_dsh) memset(dL_dsh, 0, sizeof(float) * 3 * (size_t)P * M);
+    if (dL_dscales) memset(dL_dscales, 0, sizeof(float) * 3 * (size_t)P);
+    if (dL_drotations) memset(dL_drotations, 0, sizeof(float) * 4 * (size_t)P);
+    if (dL_dsh_language) memset(dL_dsh_language, 0, sizeof(float) * 3 * (size_t)P);
+    if (dL_dlanguage_feature) memset(dL_dlanguage_feature, 0, sizeof(float) * 3 * (size_t)P);
+    float* dconic = (float*)xcalloc((size_t)P * 4, sizeof(float));
+    float* ddepth = (float*)xcalloc((size_t)P, sizeof(float));
+    float* dfeat = (float*)xcalloc((size_t)P * 3, sizeof(float));
+    const float* color_ptr = st->colors_precomp ? st->colors_precomp : st->rgb;
+    const int nch = st->include_feature ? NCH : 5;
+
+    /* ---- renderCUDA (bwd), backward.cu:399-557, per pixel, extended to NCH channels ---- */
+    const float ddelx_dx = (float)(0.5 * W);
+    const float ddely_dy = (float)(0.5 * H);
+    for (int py = 0; py < H; py++)
+        for (int px = 0; px < W; px++) {
+            const unsigned tile = (unsigned)(py / BLOCK_Y) * gx + (unsigned)(px / BLOCK_X);
+            const unsigned rs = st->ranges[2 * tile], re = st->ranges[2 * tile + 1];
+            const size_t pix = (size_t)py * W + px;
+            const float pfx = (float)px, pfy = (float)py;
+            const float T_final = st->final_T[pix];
+            float T = T_final;
+            unsigned contributor = re - rs;
+            const unsigned last_contributor = st->n_contrib[pix];
+            float accum_rec[NCH] = {0}, last_color[NCH] = {0}, dL_dpixel[NCH] = {0};
+            for (int i = 0; i < 3; i++) dL_dpixel[i] = dL_dout_color[i * HW + pix];
+            dL_dpixel[3] = dL_dout_depth ? dL_dout_depth[pix] : 0.0f;
+            dL_dpixel[4] = dL_dout_alpha ? dL_dout_alpha[pix] : 0.0f;
+            for (int i = 0; i < 3; i++) dL_dpixel[5 + i] = dL_dout_feature ? dL_dout_feature[i * HW + pix] : 0.0f;
+            float last_alpha = 0;
+            for (unsigned k = re; k-- > rs;) {
+                contributor--;
+                if (contributor >= last_contributor) continue;
+                const unsigned g = st->point_list[k];
+                const float dx = st->means2D[2 * g] - pfx, dy = st->means2D[2 * g + 1] - pfy;
+                const float* co = st->conic_opacity + 4 * (size_t)g;
+                const float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
+                if (power > 0.0f) continue;
+                const float G = expf(power);
+                const float alpha = fminf_cuda(0.99f, co[3] * G);
+                if (alpha < 1.0f / 255.0f) continue;
+                T = T / (1.f - alpha);
+                const float dchannel_dcolor = alpha * T;
+                float dL_dalpha = 0.0f;
+                float v[NCH];
+                v[0] = color_ptr[3 * g]; v[1] = color_ptr[3 * g + 1]; v[2] = color_ptr[3 * g + 2];
+                v[3] = st->depths[g]; v[4] = 1.0f;
+                v[5] = st->feat[3 * g]; v[6] = st->feat[3 * g + 1]; v[7] = st->feat[3 * g + 2];
+                for (int ch = 0; ch < nch; ch++) {
+                    const float c = v[ch];
+                    accum_rec[ch] = last_alpha * last_color[ch] + (1.f - last_alpha) * accum_rec[ch];
+                    last_color[ch] = c;
+                    const float dL_dchannel = dL_dpixel[ch];
+                    dL_dalpha += (c - accum_rec[ch]) * dL_dchannel;
+                    const float gv = dchannel_dcolor * dL_dchannel;
+                    if (ch < 3) dL_dcolors[3 * (size_t)g + ch] += gv;
+                    else if (ch == 3) ddepth[g] += gv;
+                    else if (ch >= 5) dfeat[3 * (size_t)g + ch - 5] += gv;
+                }
+                dL_dalpha *= T;
+                last_alpha = alpha;
+                float bg_dot_dpixel = 0;
+                for (int i = 0; i < 3; i++) bg_dot_dpixel += st->bg[i] * dL_dpixel[i];
+                dL_dalpha += (-T_final / (1.f - alpha)) * bg_dot_dpixel;
+                const float dL_dG = co[3] * dL_dalpha;
+                const float gdx = G * dx;
+                const float gdy = G * dy;
+                const float dG_ddelx = -gdx * co[0] - gdy * co[1];
+                const float dG_ddely = -gdy * co[2] - gdx * co[1];
+                dL_dmeans2D[3 * (size_t)g + 0] += dL_dG * dG_ddelx * ddelx_dx;
+                dL_dmeans2D[3 * (size_t)g + 1] += dL_dG * dG_ddely * ddely_dy;
+                dconic[4 * (size_t)g + 0] += -0.5f * gdx * dx * dL_dG;
+                dconic[4 * (size_t)g + 1] += -0.5f * gdx * dy * dL_dG;
+                dconic[4 * (size_t)g + 3] += -0.5f * gdy * dy * dL_dG;
+                dL_dopacity[g] += G * dL_dalpha;
+            }
+        }
+
+    /* ---- BACKWARD::preprocess, backward.cu:559-622 ---- */
+    const float* cov3D_ptr = st->cov3D_precomp ? st->cov3D_precomp : st->cov3D;
+    for (int idx = 0; idx < P; idx++) {
+        if (!(st->radii[idx] > 0)) continue;
+        cov2d_backward(idx, st->means3D, cov3D_ptr, st->focal_x, st->focal_y, st->tan_fovx,
+                       st->tan_fovy, st->view, dconic, dL_dmeans3D, dL_dcov3D);
+    }
+    const float* proj = st->proj;
+    for (int idx = 0; idx < P; idx++) {
+        if (!(st->radii[idx] > 0)) continue;
+        /* backward.cu:370-387 */
+        v3 m = v3_mk(st->means3D[3 * idx], st->means3D[3 * idx + 1], st->means3D[3 * idx + 2]);
+        float m_hom[4];
+        transformPoint4x4(m, proj, m_hom);
+        float m_w = 1.0f / (m_hom[3] + 0.0000001f);
+        float mul1 = (proj[0] * m.x + proj[4] * m.y + proj[8] * m.z + proj[12]) * m_w * m_w;
+        float mul2 = (proj[1] * m.x + proj[5] * m.y + proj[9] * m.z + proj[13]) * m_w * m_w;
+        const float gx2 = dL_dmeans2D[3 * idx], gy2 = dL_dmeans2D[3 * idx + 1];
+        v3 dm;
+        dm.x = (proj[0] * m_w - proj[3] * mul1) * gx2 + (proj[1] * m_w - proj[3] * mul2) * gy2;
+        dm.y = (proj[4] * m_w - proj[7] * mul1) * gx2 + (proj[5] * m_w - proj[7] * mul2) * gy2;
+        dm.z = (proj[8] * m_w - proj[11] * mul1) * gx2 + (proj[9] * m_w - proj[11] * mul2) * gy2;
+        dL_dmeans3D[3 * idx + 0] += dm.x;
+        dL_dmeans3D[3 * idx + 1] += dm.y;
+        dL_dmeans3D[3 * idx + 2] += dm.z;
+        if (st->sh && dL_dsh)
+            sh_backward(idx, st->D, M, st->means3D, st->campos, st->sh, st->clamped, dL_dcolors,
+                        dL_dmeans3D, dL_dsh);
+        if (st->scales && dL_dscales && dL_drotations)
+            cov3d_backward(idx, st->scales + 3 * (size_t)idx, st->scale_modifier,
+                           st->rotations + 4 * (size_t)idx, dL_dcov3D, dL_dscales, dL_drotations);
+        /* depth channel -> view-space z = view[2]x + view[6]y + view[10]z + view[14] */
+        const float dz = ddepth[idx];
+        dL_dmeans3D[3 * idx + 0] += dz * st->view[2];
+        dL_dmeans3D[3 * idx + 1] += dz * st->view[6];
+        dL_dmeans3D[3 * idx + 2] += dz * st->view[10];
+        /* confidence is an opacity multiplier */
+        if (st->confidence) dL_dopacity[idx] = dL_dopacity[idx] * st->confidence[idx];
+        if (st->include_feature) {
+            const float* gf = dfeat + 3 * (size_t)idx;
+            if (st->lang_precomp) {
+                if (dL_dlanguage_feature)
+                    for (int k = 0; k < 3; k++) dL_dlanguage_feature[3 * idx + k] = gf[k];
+            } else if (st->sh_language && dL_dsh_language) {
+                /* f = u / (|u| + 1e-9), u = SH_C0 * l */
+                const float* l = st->sh_language + 3 * (size_t)idx;
+                float u0 = SH_C0 * l[0], u1 = SH_C0 * l[1], u2v = SH_C0 * l[2];
+                float n = sqrtf(u0 * u0 + u1 * u1 + u2v * u2v);
+                float den = n + 1e-9f;
+                float ug = u0 * gf[0] + u1 * gf[1] + u2v * gf[2];
+                float k2 = n > 0.0f ? ug / (den * den * n) : 0.0f;
+                dL_dsh_language[3 * idx + 0] = SH_C0 * (gf[0] / den - u0 * k2);
+                dL_dsh_language[3 * idx + 1] = SH_C0 * (gf[1] / den - u1 * k2);
+                dL_dsh_language[3 * idx + 2] = SH_C0 * (gf[2] / den - u2v * k2);
+            }
+        }
+    }
+    /* invisible Gaussians: the grads of the colour channels etc. are already zero. */
+    free(dconic);
+    free(ddepth);
+    free(dfeat);
+    return 0;
+}
+
+void oracle_free(oracle_state* st) {
+    if (!st) return;
+    free(st->depths); free(st->clamped); free(st->radii); free(st->means2D); free(st->cov3D);
+    free(st->conic_opacity); free(st->rgb); free(st->feat); free(st->tiles_touched);
+    free(st->point_list); free(st->ranges); free(st->final_T); free(st->n_contrib);
+    free(st);
+}
+
+int oracle_get_point_list(const oracle_state* st, unsigned* out) { memcpy(out, st->point_list, sizeof(unsigned) * (size_t)st->R); return st->R; }
+int oracle_get_ranges(const oracle_state* st, unsigned* out) { memcpy(out, st->ranges, sizeof(unsigned) * 2 * (size_t)st->gx * st->gy); return 0; }
+int oracle_get_final_T(const oracle_state* st, float* out) { memcpy(out, st->final_T, sizeof(float) * (size_t)st->W * st->H); return 0; }
+int oracle_get_n_contrib(const oracle_state* st, unsigned* out) { memcpy(out, st->n_contrib, sizeof(unsigned) * (size_t)st->W * st->H); return 0; }
+int oracle_get_means2D(const oracle_state* st, float* out) { memcpy(out, st->means2D, sizeof(float) * 2 * (size_t)st->P); return 0; }
+int oracle_get_conic_opacity(const oracle_state* st, float* out) { memcpy(out, st->conic_opacity, sizeof(float) * 4 * (size_t)st->P); return 0; }
+int oracle_get_depths(const oracle_state* st, float* out) { memcpy(out, st->depths, sizeof(float) * (size_t)st->P); return 0; }
+int oracle_get_rgb(const oracle_state* st, float* out) { memcpy(out, st->rgb, sizeof(float) * 3 * (size_t)st->P); return 0; }
+int oracle_get_tiles_touched(const oracle_state* st, unsigned* out) { memcpy(out, st->tiles_touched, sizeof(unsigned) * (size_t)st->P); return 0; }
+int oracle_get_cov3D(const oracle_state* st, float* out) { memcpy(out, st->cov3D, sizeof(float) * 6 * (size_t)st->P); return 0; }

@@ -1,0 +1,108 @@
+/*
+ * gsr_oracle.h -- CPU restatement of the reference differentiable Gaussian rasterizer.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+ * leg may load this library, and only as the checker / CPU baseline.  The product path
+ * (sdp-gs_amd/) never links, loads or calls it.
+ *
+ * What it restates (all citations relative to /root/reference/submodules/diff-gaussian-rasterization):
+ *   forward : Rasterizer::forward            cuda_rasterizer/rasterizer_impl.cu:198-336
+ *             preprocessCUDA (fwd)           cuda_rasterizer/forward.cu:155-256
+ *             duplicateWithKeys + SortPairs  cuda_rasterizer/rasterizer_impl.cu:70-111, 300-318
+ *             renderCUDA (fwd)               cuda_rasterizer/forward.cu:261-374
+ *   backward: Rasterizer::backward           cuda_rasterizer/rasterizer_impl.cu:340-434
+ *             renderCUDA (bwd)               cuda_rasterizer/backward.cu:399-557
+ *             computeCov2DCUDA               cuda_rasterizer/backward.cu:144-274
+ *             preprocessCUDA (bwd)           cuda_rasterizer/backward.cu:346-396
+ *   visible : checkFrustum / in_frustum      rasterizer_impl.cu:54-66, auxiliary.h:139-164
+ *
+ * Extended outputs (depth / alpha / language feature / confidence) are not in the reference
+ * tree; they are defined in DESIGN.md section 3 and restated
+ * here as extra blend channels on the reference's blend arithmetic.
+ *
+ * Arithmetic: float32, reference expression order, glm column-major conventions, compiled
+ * with -ffp-contract=off (no silent FMA contraction); ndc2Pix in double as auxiliary.h:41-44.
+ * Single-threaded and deterministic (fixed accumulation order).
+ */
+#ifndef GSR_ORACLE_H
+#define GSR_ORACLE_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct oracle_state oracle_state;
+
+/* Forward.  Argument order mirrors _C.rasterize_gaussians (rasterize_points.cu:35-55) plus the
+ * extended-API inputs.  NULL means "empty tensor" exactly like the reference's nullptr
+ * convention (rasterize_points.cu:84-110, rasterizer_impl.cu:229-232,321).  Output images are
+ * planar [C,H,W].  Returns a state handle consumed by oracle_backward (NULL on error). */
+oracle_state* oracle_forward(
+    int P, int M,
+    const float* background,                 /* [3] */
+    const float* means3D,                    /* [P,3] */
+    const float* colors_precomp,             /* [P,3] or NULL */
+    const float* opacities,                  /* [P] */
+    const float* scales,                     /* [P,3] or NULL */
+    const float* rotations,                  /* [P,4] or NULL */
+    float scale_modifier,
+    const float* cov3D_precomp,              /* [P,6] or NULL */
+    const float* viewmatrix,                 /* [16] */
+    const float* projmatrix,                 /* [16] */
+    float tan_fovx, float tan_fovy,
+    int image_height, int image_width,
+    const float* sh,                         /* [P,M,3] or NULL */
+    int degree,
+    const float* campos,                     /* [3] */
+    int prefiltered,
+    const float* sh_language,                /* [P,3] or NULL */
+    const float* language_feature_precomp,   /* [P,3] or NULL */
+    const float* confidence,                 /* [P] or NULL (== all ones) */
+    int include_feature,
+    float* out_color,                        /* [3,H,W] */
+    float* out_depth,                        /* [1,H,W] */
+    float* out_alpha,                        /* [1,H,W] */
+    float* out_feature,                      /* [3,H,W] */
+    int* radii,                              /* [P] */
+    int* num_rendered);
+
+/* Backward.  Consumes the forward state; upstream grads may be NULL (== zeros).
+ * Every grad buffer that is non-NULL is fully written. */
+int oracle_backward(
+    oracle_state* st,
+    const float* dL_dout_color,              /* [3,H,W] */
+    const float* dL_dout_depth,              /* [1,H,W] or NULL */
+    const float* dL_dout_alpha,              /* [1,H,W] or NULL */
+    const float* dL_dout_feature,            /* [3,H,W] or NULL */
+    float* dL_dmeans2D,                      /* [P,3] */
+    float* dL_dcolors,                       /* [P,3] */
+    float* dL_dopacity,                      /* [P] */
+    float* dL_dmeans3D,                      /* [P,3] */
+    float* dL_dcov3D,                        /* [P,6] */
+    float* dL_dsh,                           /* [P,M,3] or NULL */
+    float* dL_dscales,                       /* [P,3] or NULL */
+    float* dL_drotations,                    /* [P,4] or NULL */
+    float* dL_dsh_language,                  /* [P,3] or NULL */
+    float* dL_dlanguage_feature);            /* [P,3] or NULL */
+
+void oracle_free(oracle_state* st);
+
+int oracle_mark_visible(int P, const float* means3D, const float* viewmatrix,
+                        const float* projmatrix, unsigned char* present);
+
+/* Introspection for parity tests (copies internal state out). */
+int oracle_get_point_list(const oracle_state* st, unsigned* out);   /* [num_rendered] */
+int oracle_get_ranges(const oracle_state* st, unsigned* out);       /* [tiles*2] */
+int oracle_get_final_T(const oracle_state* st, float* out);         /* [H*W] */
+int oracle_get_n_contrib(const oracle_state* st, unsigned* out);    /* [H*W] */
+int oracle_get_means2D(const oracle_state* st, float* out);         /* [P*2] */
+int oracle_get_conic_opacity(const oracle_state* st, float* out);   /* [P*4] */
+int oracle_get_depths(const oracle_state* st, float* out);          /* [P] */
+int oracle_get_rgb(const oracle_state* st, float* out);             /* [P*3] */
+int oracle_get_tiles_touched(const oracle_state* st, unsigned* out);/* [P] */
+int oracle_get_cov3D(const oracle_state* st, float* out);           /* [P*6] */
+
+#ifdef __cplusplus
+}
+#endif
+#endif

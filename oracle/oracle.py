@@ -1,0 +1,197 @@
+"""ctypes front-end of the CPU restatement (oracle/gsr_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+leg, always as the checker / CPU baseline -- never by the product package (sdp-gs_amd/).
+
+The arrays follow the reference rasterizer's tensor conventions
+(submodules/diff-gaussian-rasterization/rasterize_points.cu:35-196): float32, C-contiguous,
+images planar [C,H,W], `None` == empty tensor == nullptr.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "libgsr_oracle.so")
+_lib = None
+
+_f = ctypes.c_float
+_i = ctypes.c_int
+_p = ctypes.c_void_p
+
+
+def build() -> str:
+    """Compile the oracle with gcc (seconds)."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        L.oracle_forward.restype = _p
+        L.oracle_forward.argtypes = [
+            _i, _i, _p, _p, _p, _p, _p, _p, _f, _p, _p, _p, _f, _f, _i, _i, _p, _i, _p, _i,
+            _p, _p, _p, _i, _p, _p, _p, _p, _p, ctypes.POINTER(_i)]
+        L.oracle_backward.restype = _i
+        L.oracle_backward.argtypes = [_p] + [_p] * 14
+        L.oracle_free.restype = None
+        L.oracle_free.argtypes = [_p]
+        L.oracle_mark_visible.restype = _i
+        L.oracle_mark_visible.argtypes = [_i, _p, _p, _p, _p]
+        for name in ("point_list", "ranges", "final_T", "n_contrib", "means2D", "conic_opacity",
+                     "depths", "rgb", "tiles_touched", "cov3D"):
+            fn = getattr(L, "oracle_get_" + name)
+            fn.restype = _i
+            fn.argtypes = [_p, _p]
+        _lib = L
+    return _lib
+
+
+def _arr(x, dtype=np.float32):
+    if x is None:
+        return None
+    a = np.ascontiguousarray(np.asarray(x, dtype=dtype))
+    return a
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data
+
+
+class OracleRaster:
+    """One forward (+ optional backward) of the restated rasterizer on host arrays."""
+
+    def __init__(self, *, means3D, opacities, viewmatrix, projmatrix, campos, tanfovx, tanfovy,
+                 image_height, image_width, bg, scale_modifier=1.0, sh_degree=0, shs=None,
+                 colors_precomp=None, scales=None, rotations=None, cov3D_precomp=None,
+                 shs_language=None, language_feature_precomp=None, confidence=None,
+                 include_feature=True, prefiltered=False):
+        L = lib()
+        self._keep = {}
+        k = self._keep
+        k["means3D"] = _arr(means3D).reshape(-1, 3)
+        P = k["means3D"].shape[0]
+        k["opac"] = _arr(opacities).reshape(P)
+        k["view"] = _arr(viewmatrix).reshape(16)
+        k["proj"] = _arr(projmatrix).reshape(16)
+        k["campos"] = _arr(campos).reshape(3)
+        k["bg"] = _arr(bg).reshape(3)
+        k["shs"] = None if shs is None else _arr(shs).reshape(P, -1, 3)
+        M = 0 if k["shs"] is None else k["shs"].shape[1]
+        k["colors"] = None if colors_precomp is None else _arr(colors_precomp).reshape(P, 3)
+        k["scales"] = None if scales is None else _arr(scales).reshape(P, 3)
+        k["rot"] = None if rotations is None else _arr(rotations).reshape(P, 4)
+        k["cov"] = None if cov3D_precomp is None else _arr(cov3D_precomp).reshape(P, 6)
+        k["shl"] = None if shs_language is None else _arr(shs_language).reshape(P, 3)
+        k["lfp"] = None if language_feature_precomp is None else _arr(language_feature_precomp).reshape(P, 3)
+        k["conf"] = None if confidence is None else _arr(confidence).reshape(P)
+        H, W = int(image_height), int(image_width)
+        self.P, self.M, self.H, self.W = P, M, H, W
+        self.color = np.zeros((3, H, W), np.float32)
+        self.depth = np.zeros((1, H, W), np.float32)
+        self.alpha = np.zeros((1, H, W), np.float32)
+        self.feature = np.zeros((3, H, W), np.float32)
+        self.radii = np.zeros((P,), np.int32)
+        nr = _i(0)
+        self._st = L.oracle_forward(
+            P, M, _ptr(k["bg"]), _ptr(k["means3D"]), _ptr(k["colors"]), _ptr(k["opac"]),
+            _ptr(k["scales"]), _ptr(k["rot"]), float(scale_modifier), _ptr(k["cov"]),
+            _ptr(k["view"]), _ptr(k["proj"]), float(tanfovx), float(tanfovy), H, W,
+            _ptr(k["shs"]), int(sh_degree), _ptr(k["campos"]), int(bool(prefiltered)),
+            _ptr(k["shl"]), _ptr(k["lfp"]), _ptr(k["conf"]), int(bool(include_feature)),
+            _ptr(self.color), _ptr(self.depth), _ptr(self.alpha), _ptr(self.feature),
+            _ptr(self.radii), ctypes.byref(nr))
+        if not self._st:
+            raise RuntimeError("oracle_forward rejected its arguments")
+        self.num_rendered = int(nr.value)
+        self.gx = (W + 15) // 16
+        self.gy = (H + 15) // 16
+
+    def __del__(self):
+        st = getattr(self, "_st", None)
+        if st:
+            lib().oracle_free(st)
+            self._st = None
+
+    # ---- state introspection -------------------------------------------------------------
+    def _get(self, name, shape, dtype):
+        out = np.zeros(shape, dtype)
+        getattr(lib(), "oracle_get_" + name)(self._st, _ptr(out))
+        return out
+
+    def point_list(self):
+        return self._get("point_list", (self.num_rendered,), np.uint32)
+
+    def ranges(self):
+        return self._get("ranges", (self.gx * self.gy, 2), np.uint32)
+
+    def final_T(self):
+        return self._get("final_T", (self.H, self.W), np.float32)
+
+    def n_contrib(self):
+        return self._get("n_contrib", (self.H, self.W), np.uint32)
+
+    def means2D(self):
+        return self._get("means2D", (self.P, 2), np.float32)
+
+    def conic_opacity(self):
+        return self._get("conic_opacity", (self.P, 4), np.float32)
+
+    def depths(self):
+        return self._get("depths", (self.P,), np.float32)
+
+    def rgb(self):
+        return self._get("rgb", (self.P, 3), np.float32)
+
+    def tiles_touched(self):
+        return self._get("tiles_touched", (self.P,), np.uint32)
+
+    def cov3D(self):
+        return self._get("cov3D", (self.P, 6), np.float32)
+
+    # ---- backward --------------------------------------------------------------------------
+    def backward(self, dL_dcolor, dL_ddepth=None, dL_dalpha=None, dL_dfeature=None):
+        k = self._keep
+        P, M = self.P, self.M
+        dc = _arr(dL_dcolor).reshape(3, self.H, self.W)
+        dd = None if dL_ddepth is None else _arr(dL_ddepth).reshape(1, self.H, self.W)
+        da = None if dL_dalpha is None else _arr(dL_dalpha).reshape(1, self.H, self.W)
+        df = None if dL_dfeature is None else _arr(dL_dfeature).reshape(3, self.H, self.W)
+        g = {
+            "means2D": np.zeros((P, 3), np.float32),
+            "colors": np.zeros((P, 3), np.float32),
+            "opacity": np.zeros((P, 1), np.float32),
+            "means3D": np.zeros((P, 3), np.float32),
+            "cov3D": np.zeros((P, 6), np.float32),
+            "sh": np.zeros((P, M, 3), np.float32) if k["shs"] is not None else None,
+            "scales": np.zeros((P, 3), np.float32) if k["scales"] is not None else None,
+            "rotations": np.zeros((P, 4), np.float32) if k["rot"] is not None else None,
+            "sh_language": np.zeros((P, 3), np.float32) if k["shl"] is not None else None,
+            "language_feature": np.zeros((P, 3), np.float32) if k["lfp"] is not None else None,
+        }
+        self._keep_bwd = (dc, dd, da, df)
+        rc = lib().oracle_backward(
+            self._st, _ptr(dc), _ptr(dd), _ptr(da), _ptr(df), _ptr(g["means2D"]), _ptr(g["colors"]),
+            _ptr(g["opacity"]), _ptr(g["means3D"]), _ptr(g["cov3D"]), _ptr(g["sh"]),
+            _ptr(g["scales"]), _ptr(g["rotations"]), _ptr(g["sh_language"]),
+            _ptr(g["language_feature"]))
+        if rc != 0:
+            raise RuntimeError("oracle_backward failed")
+        return g
+
+
+def mark_visible(means3D, viewmatrix, projmatrix):
+    m = _arr(means3D).reshape(-1, 3)
+    v = _arr(viewmatrix).reshape(16)
+    p = _arr(projmatrix).reshape(16)
+    out = np.zeros((m.shape[0],), np.uint8)
+    lib().oracle_mark_visible(m.shape[0], _ptr(m), _ptr(v), _ptr(p), _ptr(out))
+    return out.astype(bool)

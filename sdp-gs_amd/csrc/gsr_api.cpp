@@ -1,0 +1,326 @@
+// gsr_api.cpp -- host orchestration behind the C ABI (include/gsr.h).
+//
+// Sequence per view (reference: Rasterizer::forward, cuda_rasterizer/rasterizer_impl.cu:198-336):
+//   preprocess -> stable depth sort of the P splats -> inclusive scan of tile counts in depth
+//   order -> 8-byte readback of the instance count R (+ error flag) -> duplicate tile ids in depth
+//   order -> stable radix sort of the R tile ids over ceil(log2(tiles)) bits -> tile ranges ->
+//   blend.  Backward (rasterizer_impl.cu:340-434): zero the accumulators -> backward blend ->
+//   fused per-Gaussian backward.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/gsr.h"
+#include "gsr_internal.h"
+
+namespace gsr {
+
+GeomState carve_geom(char* base, size_t P) {
+  Carver c(base);
+  GeomState g{};
+  g.flags = c.take<uint32_t>(4);
+  g.depths = c.take<float>(P);
+  g.dkey_a = c.take<uint32_t>(P);
+  g.dval_a = c.take<uint32_t>(P);
+  g.dkey_b = c.take<uint32_t>(P);
+  g.dval_b = c.take<uint32_t>(P);
+  g.clamped = c.take<uint8_t>(P);
+  g.radii = c.take<int32_t>(P);
+  g.cov3D = c.take<float>(6 * P);
+  g.rec = c.take<float4>(4 * P);
+  g.tiles_touched = c.take<uint32_t>(P);
+  g.offsets = c.take<uint32_t>(P);
+  g.acc = c.take<float>((size_t)kAccFloats * P);
+  g.sort_hist = c.take<uint32_t>(sort_hist_len(P));
+  g.sort_parts = c.take<uint32_t>(scan_parts(sort_hist_len(P)) + 1);
+  g.scan_parts = c.take<uint32_t>(scan_parts(P) + 1);
+  g.bytes = c.size();
+  return g;
+}
+
+BinState carve_bin(char* base, size_t R) {
+  Carver c(base);
+  BinState b{};
+  b.tkey_a = c.take<uint32_t>(R);
+  b.tval_a = c.take<uint32_t>(R);
+  b.tkey_b = c.take<uint32_t>(R);
+  b.tval_b = c.take<uint32_t>(R);
+  b.hist = c.take<uint32_t>(sort_hist_len(R));
+  b.parts = c.take<uint32_t>(scan_parts(sort_hist_len(R)) + 1);
+  b.bytes = c.size();
+  return b;
+}
+
+ImgState carve_img(char* base, size_t W, size_t H) {
+  Carver c(base);
+  ImgState s{};
+  const size_t gx = (W + kTile - 1) / kTile, gy = (H + kTile - 1) / kTile;
+  s.final_T = c.take<float>(W * H);
+  s.n_contrib = c.take<uint32_t>(W * H);
+  s.ranges = c.take<uint2>(gx * gy);
+  s.tile_last = c.take<uint32_t>(gx * gy);
+  s.bytes = c.size();
+  return s;
+}
+
+}  // namespace gsr
+
+using namespace gsr;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define GSR_CHECK(expr)                                                                     \
+  do {                                                                                      \
+    hipError_t e_ = (expr);                                                                 \
+    if (e_ != hipSuccess) return fail(GSR_ERR_HIP, "%s failed: %s", #expr, hipGetErrorString(e_)); \
+    if (debug) {                                                                            \
+      e_ = hipStreamSynchronize(stream);                                                    \
+      if (e_ == hipSuccess) e_ = hipGetLastError();                                         \
+      if (e_ != hipSuccess)                                                                 \
+        return fail(GSR_ERR_HIP, "[debug] after %s: %s", #expr, hipGetErrorString(e_));     \
+    }                                                                                       \
+  } while (0)
+
+// Bits needed to hold tile ids 0 .. ntiles-1 (the reference sorts 32 + getHigherMsb(ntiles)
+// bits of a 64-bit key, rasterizer_impl.cu:35-50,300; our tile sort only needs the tile part).
+int tile_bits(uint32_t ntiles) {
+  if (ntiles <= 1) return 0;
+  return 32 - __builtin_clz(ntiles - 1);
+}
+
+// Pinned 16-byte landing zone for the one device->host read per forward.
+uint32_t* pinned_slot() {
+  thread_local uint32_t* p = nullptr;
+  if (!p) {
+    if (hipHostMalloc((void**)&p, 16, hipHostMallocDefault) != hipSuccess) p = nullptr;
+  }
+  return p;
+}
+
+bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+}  // namespace
+
+extern "C" {
+
+int gsr_abi_version(void) { return GSR_ABI_VERSION; }
+const char* gsr_last_error(void) { return g_err.c_str(); }
+
+size_t gsr_geom_buffer_bytes(int P) { return carve_geom(nullptr, (size_t)(P > 0 ? P : 0)).bytes; }
+size_t gsr_binning_buffer_bytes(int R) { return carve_bin(nullptr, (size_t)(R > 0 ? R : 0)).bytes; }
+size_t gsr_image_buffer_bytes(int H, int W) {
+  return carve_img(nullptr, (size_t)(W > 0 ? W : 0), (size_t)(H > 0 ? H : 0)).bytes;
+}
+
+int gsr_rasterize_gaussians(int P, int M, const float* background, const float* means3D,
+                            const float* colors_precomp, const float* opacities,
+                            const float* scales, const float* rotations, float scale_modifier,
+                            const float* cov3D_precomp, const float* viewmatrix,
+                            const float* projmatrix, float tan_fovx, float tan_fovy,
+                            int image_height, int image_width, const float* sh, int degree,
+                            const float* campos, int prefiltered, const float* sh_language,
+                            const float* language_feature_precomp, const float* confidence,
+                            int include_feature, float* out_color, float* out_depth,
+                            float* out_alpha, float* out_feature, int* radii, int* num_rendered,
+                            gsr_alloc_fn alloc, void* alloc_ctx, void* stream_ptr, int debug) {
+  g_err.clear();
+  hipStream_t stream = (hipStream_t)stream_ptr;
+  const int W = image_width, H = image_height;
+  if (P < 0) return fail(GSR_ERR_ARGUMENT, "means3D must have dimensions (num_points, 3)");
+  if (W <= 0 || H <= 0) return fail(GSR_ERR_ARGUMENT, "image size must be positive (got %dx%d)", W, H);
+  if (!num_rendered || !out_color) return fail(GSR_ERR_ARGUMENT, "out_color / num_rendered missing");
+  const size_t HW = (size_t)W * H;
+  if (P == 0) {
+    *num_rendered = 0;
+    GSR_CHECK(hipMemsetAsync(out_color, 0, 3 * HW * sizeof(float), stream));
+    if (out_depth) GSR_CHECK(hipMemsetAsync(out_depth, 0, HW * sizeof(float), stream));
+    if (out_alpha) GSR_CHECK(hipMemsetAsync(out_alpha, 0, HW * sizeof(float), stream));
+    if (out_feature) GSR_CHECK(hipMemsetAsync(out_feature, 0, 3 * HW * sizeof(float), stream));
+    return GSR_OK;
+  }
+  if (!background || !means3D || !opacities || !viewmatrix || !projmatrix || !campos)
+    return fail(GSR_ERR_ARGUMENT, "background/means3D/opacities/viewmatrix/projmatrix/campos required");
+  if ((colors_precomp == nullptr) == (sh == nullptr))
+    return fail(GSR_ERR_ARGUMENT, "Please provide excatly one of either SHs or precomputed colors!");
+  if ((cov3D_precomp == nullptr) == (scales == nullptr || rotations == nullptr))
+    return fail(GSR_ERR_ARGUMENT,
+                "Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!");
+  if (sh) {
+    if (degree < 0 || degree > 3) return fail(GSR_ERR_ARGUMENT, "sh_degree must be in [0, 3] (got %d)", degree);
+    if ((degree + 1) * (degree + 1) > M)
+      return fail(GSR_ERR_ARGUMENT, "sh has %d coefficients but degree %d needs %d", M, degree,
+                  (degree + 1) * (degree + 1));
+  }
+  if (rotations && !aligned16(rotations)) return fail(GSR_ERR_ARGUMENT, "rotations must be 16-byte aligned");
+  if (!alloc) return fail(GSR_ERR_ARGUMENT, "allocator callback missing");
+
+  const uint32_t gx = (uint32_t)((W + kTile - 1) / kTile), gy = (uint32_t)((H + kTile - 1) / kTile);
+  const uint32_t ntiles = gx * gy;
+  if (scan_parts((size_t)P) > (size_t)kScanMaxParts ||
+      scan_parts(sort_hist_len((size_t)P)) > (size_t)kScanMaxParts)
+    return fail(GSR_ERR_TOO_LARGE, "P = %d exceeds the scan capacity", P);
+
+  const size_t gbytes = carve_geom(nullptr, (size_t)P).bytes;
+  char* gbase = (char*)alloc(alloc_ctx, gbytes, GSR_BUF_GEOM);
+  if (!gbase) return fail(GSR_ERR_ALLOC, "geometry buffer allocation of %zu bytes failed", gbytes);
+  const size_t ibytes = carve_img(nullptr, (size_t)W, (size_t)H).bytes;
+  char* ibase = (char*)alloc(alloc_ctx, ibytes, GSR_BUF_IMAGE);
+  if (!ibase) return fail(GSR_ERR_ALLOC, "image buffer allocation of %zu bytes failed", ibytes);
+  GeomState g = carve_geom(gbase, (size_t)P);
+  ImgState im = carve_img(ibase, (size_t)W, (size_t)H);
+  int32_t* radii_ptr = radii ? radii : g.radii;
+
+  GSR_CHECK(hipMemsetAsync(g.flags, 0, 4 * sizeof(uint32_t), stream));
+  PreArgs pa{};
+  pa.P = P; pa.D = degree; pa.M = M; pa.W = W; pa.H = H; pa.gx = gx; pa.gy = gy;
+  pa.means3D = means3D; pa.scales = scales; pa.rotations = rotations; pa.opacities = opacities;
+  pa.shs = sh; pa.cov3D_precomp = cov3D_precomp; pa.colors_precomp = colors_precomp;
+  pa.sh_language = sh_language; pa.lang_precomp = language_feature_precomp;
+  pa.confidence = confidence;
+  pa.view = viewmatrix; pa.proj = projmatrix; pa.campos = campos;
+  pa.scale_modifier = scale_modifier; pa.tanx = tan_fovx; pa.tany = tan_fovy;
+  pa.fy = (float)H / (2.0f * tan_fovy);  // rasterizer_impl.cu:222-223
+  pa.fx = (float)W / (2.0f * tan_fovx);
+  pa.prefiltered = prefiltered; pa.include_feature = include_feature;
+  pa.radii = radii_ptr; pa.g = g;
+  GSR_CHECK(launch_preprocess(pa, stream));
+
+  bool in_b = false;
+  GSR_CHECK(radix_sort_pairs(g.dkey_a, g.dval_a, g.dkey_b, g.dval_b, (size_t)P, 32,
+                             SortScratch{g.sort_hist, g.sort_parts}, &in_b, stream));
+  const uint32_t* order = in_b ? g.dval_b : g.dval_a;
+  GSR_CHECK(scan_u32(g.tiles_touched, order, g.offsets, (size_t)P, true, g.scan_parts, stream));
+
+  uint32_t* host = pinned_slot();
+  if (!host) return fail(GSR_ERR_HIP, "pinned host allocation failed");
+  GSR_CHECK(hipMemcpyAsync(host, g.offsets + (P - 1), 4, hipMemcpyDeviceToHost, stream));
+  GSR_CHECK(hipMemcpyAsync(host + 1, g.flags, 4, hipMemcpyDeviceToHost, stream));
+  GSR_CHECK(hipStreamSynchronize(stream));
+  const uint32_t R = host[0];
+  if (host[1]) return fail(GSR_ERR_PREFILTERED,
+                           "Point is filtered although prefiltered is set. This shouldn't happen!");
+  if (R > 0x7fffffffu || scan_parts(sort_hist_len(R)) > (size_t)kScanMaxParts)
+    return fail(GSR_ERR_TOO_LARGE, "num_rendered = %u exceeds the sort capacity", R);
+
+  const size_t bbytes = carve_bin(nullptr, R).bytes;
+  char* bbase = (char*)alloc(alloc_ctx, bbytes, GSR_BUF_BINNING);
+  if (!bbase) return fail(GSR_ERR_ALLOC, "binning buffer allocation of %zu bytes failed", bbytes);
+  BinState b = carve_bin(bbase, R);
+
+  GSR_CHECK(launch_duplicate(P, order, g.offsets, radii_ptr, g.rec, gx, gy, b.tkey_a, b.tval_a, stream));
+  bool t_in_b = false;
+  GSR_CHECK(radix_sort_pairs(b.tkey_a, b.tval_a, b.tkey_b, b.tval_b, R, tile_bits(ntiles),
+                             SortScratch{b.hist, b.parts}, &t_in_b, stream));
+  const uint32_t* tiles_sorted = t_in_b ? b.tkey_b : b.tkey_a;
+  const uint32_t* point_list = t_in_b ? b.tval_b : b.tval_a;
+  GSR_CHECK(launch_tile_ranges(R, tiles_sorted, im.ranges, ntiles, stream));
+
+  RenderArgs ra{};
+  ra.W = W; ra.H = H; ra.gx = gx; ra.gy = gy;
+  ra.ranges = im.ranges; ra.point_list = point_list; ra.rec = g.rec; ra.bg = background;
+  ra.final_T = im.final_T; ra.n_contrib = im.n_contrib; ra.tile_last = im.tile_last;
+  ra.out_color = out_color; ra.out_depth = out_depth; ra.out_alpha = out_alpha;
+  ra.out_feature = out_feature; ra.include_feature = include_feature;
+  GSR_CHECK(launch_render_forward(ra, stream));
+  *num_rendered = (int)R;
+  return GSR_OK;
+}
+
+int gsr_rasterize_gaussians_backward(
+    int P, int M, int R, const float* background, const float* means3D, const int* radii,
+    const float* colors_precomp, const float* scales, const float* rotations, float scale_modifier,
+    const float* cov3D_precomp, const float* viewmatrix, const float* projmatrix, float tan_fovx,
+    float tan_fovy, int image_height, int image_width, const float* dL_dout_color,
+    const float* dL_dout_depth, const float* dL_dout_alpha, const float* dL_dout_feature,
+    const float* sh, int degree, const float* campos, const float* sh_language,
+    const float* language_feature_precomp, const float* confidence, int include_feature,
+    void* geom_buffer, void* binning_buffer, void* image_buffer, float* dL_dmeans2D,
+    float* dL_dcolors, float* dL_dopacity, float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh,
+    float* dL_dscales, float* dL_drotations, float* dL_dsh_language, float* dL_dlanguage_feature,
+    void* stream_ptr, int debug) {
+  g_err.clear();
+  hipStream_t stream = (hipStream_t)stream_ptr;
+  const int W = image_width, H = image_height;
+  if (P < 0 || R < 0 || W <= 0 || H <= 0) return fail(GSR_ERR_ARGUMENT, "invalid sizes");
+  if (P == 0) return GSR_OK;
+  if (!geom_buffer || !image_buffer || (R > 0 && !binning_buffer))
+    return fail(GSR_ERR_ARGUMENT, "forward scratch buffers missing");
+  if (!dL_dout_color || !dL_dmeans2D || !dL_dopacity || !dL_dmeans3D)
+    return fail(GSR_ERR_ARGUMENT, "required gradient buffers missing");
+  if (sh && !dL_dsh) return fail(GSR_ERR_ARGUMENT, "dL_dsh required when sh is given");
+  if (scales && (!dL_dscales || !dL_drotations || !rotations))
+    return fail(GSR_ERR_ARGUMENT, "dL_dscales / dL_drotations required when scales are given");
+  if ((rotations && !aligned16(rotations)) || (dL_drotations && !aligned16(dL_drotations)))
+    return fail(GSR_ERR_ARGUMENT, "rotations / dL_drotations must be 16-byte aligned");
+  if (sh && (degree < 0 || degree > 3 || (degree + 1) * (degree + 1) > M))
+    return fail(GSR_ERR_ARGUMENT, "invalid sh degree %d for M = %d", degree, M);
+  if (dL_dsh_language && !sh_language && !language_feature_precomp && include_feature)
+    ;  // nothing to differentiate: zeros are written
+
+  const uint32_t gx = (uint32_t)((W + kTile - 1) / kTile), gy = (uint32_t)((H + kTile - 1) / kTile);
+  const uint32_t ntiles = gx * gy;
+  GeomState g = carve_geom((char*)geom_buffer, (size_t)P);
+  ImgState im = carve_img((char*)image_buffer, (size_t)W, (size_t)H);
+  BinState b = carve_bin((char*)binning_buffer, (size_t)R);
+  const int passes = sort_passes(tile_bits(ntiles));
+  const uint32_t* point_list = (passes & 1) ? b.tval_b : b.tval_a;
+  const int32_t* radii_ptr = radii ? radii : g.radii;
+
+  GSR_CHECK(hipMemsetAsync(g.acc, 0, sizeof(float) * kAccFloats * (size_t)P, stream));
+  if (R > 0) {
+    RenderBwdArgs rb{};
+    rb.W = W; rb.H = H; rb.gx = gx; rb.gy = gy;
+    rb.ranges = im.ranges; rb.point_list = point_list; rb.rec = g.rec; rb.bg = background;
+    rb.final_T = im.final_T; rb.n_contrib = im.n_contrib; rb.tile_last = im.tile_last;
+    rb.dL_dcolor = dL_dout_color; rb.dL_ddepth = dL_dout_depth; rb.dL_dalpha = dL_dout_alpha;
+    rb.dL_dfeature = dL_dout_feature; rb.acc = g.acc; rb.include_feature = include_feature;
+    GSR_CHECK(launch_render_backward(rb, stream));
+  }
+  BwdPreArgs ba{};
+  ba.P = P; ba.D = degree; ba.M = M;
+  ba.means3D = means3D; ba.scales = scales; ba.rotations = rotations; ba.shs = sh;
+  ba.cov3D = cov3D_precomp ? cov3D_precomp : g.cov3D; ba.colors_precomp = colors_precomp;
+  ba.sh_language = sh_language; ba.lang_precomp = language_feature_precomp;
+  ba.confidence = confidence;
+  ba.view = viewmatrix; ba.proj = projmatrix; ba.campos = campos;
+  ba.scale_modifier = scale_modifier; ba.tanx = tan_fovx; ba.tany = tan_fovy;
+  ba.fy = (float)H / (2.0f * tan_fovy);  // rasterizer_impl.cu:380-381
+  ba.fx = (float)W / (2.0f * tan_fovx);
+  ba.include_feature = include_feature;
+  ba.radii = radii_ptr; ba.clamped = g.clamped; ba.acc = g.acc;
+  ba.dL_dmeans2D = dL_dmeans2D; ba.dL_dcolors = dL_dcolors; ba.dL_dopacity = dL_dopacity;
+  ba.dL_dmeans3D = dL_dmeans3D; ba.dL_dcov3D = dL_dcov3D; ba.dL_dsh = sh ? dL_dsh : nullptr;
+  ba.dL_dscales = scales ? dL_dscales : nullptr; ba.dL_drotations = scales ? dL_drotations : nullptr;
+  ba.dL_dsh_language = dL_dsh_language; ba.dL_dlanguage_feature = dL_dlanguage_feature;
+  GSR_CHECK(launch_preprocess_backward(ba, stream));
+  return GSR_OK;
+}
+
+int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
+                     uint8_t* present, void* stream_ptr) {
+  g_err.clear();
+  (void)projmatrix;  // in_frustum projects but only tests view-space z (auxiliary.h:149-154)
+  if (P < 0) return fail(GSR_ERR_ARGUMENT, "means3D must have dimensions (num_points, 3)");
+  if (P == 0) return GSR_OK;
+  if (!means3D || !viewmatrix || !present) return fail(GSR_ERR_ARGUMENT, "null pointer");
+  hipError_t e = launch_mark_visible(P, means3D, viewmatrix, present, (hipStream_t)stream_ptr);
+  if (e != hipSuccess) return fail(GSR_ERR_HIP, "mark_visible launch failed: %s", hipGetErrorString(e));
+  return GSR_OK;
+}
+
+}  // extern "C"

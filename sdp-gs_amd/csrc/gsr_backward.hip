@@ -1,0 +1,316 @@
+// gsr_backward.hip -- fused per-Gaussian backward preprocess for gfx950.
+//
+// One launch replaces the reference's two per-Gaussian backward kernels, computeCov2DCUDA
+// (cuda_rasterizer/backward.cu:144-274) and preprocessCUDA (:346-396, with
+// computeColorFromSH-bwd :20-139 and computeCov3D-bwd :278-341), plus the grad zero-fill of
+// RasterizeGaussiansBackwardCUDA (rasterize_points.cu:151-159): every output element is written
+// exactly once (zeros for culled Gaussians), so the caller may hand in uninitialised buffers.
+// Inputs come from the 64-byte accumulator row the backward blend filled (gsr_internal.h AccSlot).
+#include "gsr_device.h"
+#include "gsr_internal.h"
+
+namespace gsr {
+namespace {
+
+constexpr int kThreads = 256;
+
+__device__ __forceinline__ void put3(float* p, size_t i, V3 v) {
+  p[3 * i] = v.x; p[3 * i + 1] = v.y; p[3 * i + 2] = v.z;
+}
+
+// backward.cu:20-139: writes dL/dsh for coefficient k < (deg+1)^2 and returns dL/dmean.
+__device__ V3 sh_backward(const float* __restrict__ s, int deg, V3 dir_orig, V3 dL_dRGB,
+                          float* __restrict__ d) {
+#define SH(k) v3(s[3 * (k)], s[3 * (k) + 1], s[3 * (k) + 2])
+#define PUT(k, v) do { V3 _t = (v); d[3 * (k)] = _t.x; d[3 * (k) + 1] = _t.y; d[3 * (k) + 2] = _t.z; } while (0)
+  const float len = sqrtf(dot3(dir_orig, dir_orig));
+  const V3 dir = v3(dir_orig.x / len, dir_orig.y / len, dir_orig.z / len);
+  V3 dRGBdx = v3(0, 0, 0), dRGBdy = v3(0, 0, 0), dRGBdz = v3(0, 0, 0);
+  const float x = dir.x, y = dir.y, z = dir.z;
+  const float dRGBdsh0 = SH_C0;
+  PUT(0, dRGBdsh0 * dL_dRGB);
+  if (deg > 0) {
+    const float dRGBdsh1 = -SH_C1 * y;
+    const float dRGBdsh2 = SH_C1 * z;
+    const float dRGBdsh3 = -SH_C1 * x;
+    PUT(1, dRGBdsh1 * dL_dRGB);
+    PUT(2, dRGBdsh2 * dL_dRGB);
+    PUT(3, dRGBdsh3 * dL_dRGB);
+    dRGBdx = -SH_C1 * SH(3);
+    dRGBdy = -SH_C1 * SH(1);
+    dRGBdz = SH_C1 * SH(2);
+    if (deg > 1) {
+      const float xx = x * x, yy = y * y, zz = z * z;
+      const float xy = x * y, yz = y * z, xz = x * z;
+      const float dRGBdsh4 = SH_C2_0 * xy;
+      const float dRGBdsh5 = SH_C2_1 * yz;
+      const float dRGBdsh6 = SH_C2_2 * (2.f * zz - xx - yy);
+      const float dRGBdsh7 = SH_C2_3 * xz;
+      const float dRGBdsh8 = SH_C2_4 * (xx - yy);
+      PUT(4, dRGBdsh4 * dL_dRGB);
+      PUT(5, dRGBdsh5 * dL_dRGB);
+      PUT(6, dRGBdsh6 * dL_dRGB);
+      PUT(7, dRGBdsh7 * dL_dRGB);
+      PUT(8, dRGBdsh8 * dL_dRGB);
+      const V3 tx = (((SH_C2_0 * y) * SH(4) + (SH_C2_2 * 2.f * -x) * SH(6)) + (SH_C2_3 * z) * SH(7)) +
+                    (SH_C2_4 * 2.f * x) * SH(8);
+      const V3 ty = (((SH_C2_0 * x) * SH(4) + (SH_C2_1 * z) * SH(5)) + (SH_C2_2 * 2.f * -y) * SH(6)) +
+                    (SH_C2_4 * 2.f * -y) * SH(8);
+      const V3 tz = ((SH_C2_1 * y) * SH(5) + (SH_C2_2 * 2.f * 2.f * z) * SH(6)) + (SH_C2_3 * x) * SH(7);
+      dRGBdx = dRGBdx + tx;
+      dRGBdy = dRGBdy + ty;
+      dRGBdz = dRGBdz + tz;
+      if (deg > 2) {
+        const float dRGBdsh9 = SH_C3_0 * y * (3.f * xx - yy);
+        const float dRGBdsh10 = SH_C3_1 * xy * z;
+        const float dRGBdsh11 = SH_C3_2 * y * (4.f * zz - xx - yy);
+        const float dRGBdsh12 = SH_C3_3 * z * (2.f * zz - 3.f * xx - 3.f * yy);
+        const float dRGBdsh13 = SH_C3_4 * x * (4.f * zz - xx - yy);
+        const float dRGBdsh14 = SH_C3_5 * z * (xx - yy);
+        const float dRGBdsh15 = SH_C3_6 * x * (xx - 3.f * yy);
+        PUT(9, dRGBdsh9 * dL_dRGB);
+        PUT(10, dRGBdsh10 * dL_dRGB);
+        PUT(11, dRGBdsh11 * dL_dRGB);
+        PUT(12, dRGBdsh12 * dL_dRGB);
+        PUT(13, dRGBdsh13 * dL_dRGB);
+        PUT(14, dRGBdsh14 * dL_dRGB);
+        PUT(15, dRGBdsh15 * dL_dRGB);
+        // backward.cu:99-122: (scalar * vec3) followed by vec3 * scalar products, summed left to right
+        V3 ax = (((SH_C3_0 * SH(9)) * 3.f) * 2.f) * xy;
+        ax = ax + (SH_C3_1 * SH(10)) * yz;
+        ax = ax + ((SH_C3_2 * SH(11)) * -2.f) * xy;
+        ax = ax + (((SH_C3_3 * SH(12)) * -3.f) * 2.f) * xz;
+        ax = ax + (SH_C3_4 * SH(13)) * (-3.f * xx + 4.f * zz - yy);
+        ax = ax + ((SH_C3_5 * SH(14)) * 2.f) * xz;
+        ax = ax + ((SH_C3_6 * SH(15)) * 3.f) * (xx - yy);
+        V3 ay = ((SH_C3_0 * SH(9)) * 3.f) * (xx - yy);
+        ay = ay + (SH_C3_1 * SH(10)) * xz;
+        ay = ay + (SH_C3_2 * SH(11)) * (-3.f * yy + 4.f * zz - xx);
+        ay = ay + (((SH_C3_3 * SH(12)) * -3.f) * 2.f) * yz;
+        ay = ay + ((SH_C3_4 * SH(13)) * -2.f) * xy;
+        ay = ay + ((SH_C3_5 * SH(14)) * -2.f) * yz;
+        ay = ay + (((SH_C3_6 * SH(15)) * -3.f) * 2.f) * xy;
+        V3 az = (SH_C3_1 * SH(10)) * xy;
+        az = az + (((SH_C3_2 * SH(11)) * 4.f) * 2.f) * yz;
+        az = az + ((SH_C3_3 * SH(12)) * 3.f) * (2.f * zz - xx - yy);
+        az = az + (((SH_C3_4 * SH(13)) * 4.f) * 2.f) * xz;
+        az = az + (SH_C3_5 * SH(14)) * (xx - yy);
+        dRGBdx = dRGBdx + ax;
+        dRGBdy = dRGBdy + ay;
+        dRGBdz = dRGBdz + az;
+      }
+    }
+  }
+#undef PUT
+#undef SH
+  const V3 dL_ddir = v3(dot3(dRGBdx, dL_dRGB), dot3(dRGBdy, dL_dRGB), dot3(dRGBdz, dL_dRGB));
+  // auxiliary.h:107-117 dnormvdv
+  const V3 v = dir_orig, dv = dL_ddir;
+  const float sum2 = v.x * v.x + v.y * v.y + v.z * v.z;
+  const float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
+  return v3(((+sum2 - v.x * v.x) * dv.x - v.y * v.x * dv.y - v.z * v.x * dv.z) * invsum32,
+            (-v.x * v.y * dv.x + (sum2 - v.y * v.y) * dv.y - v.z * v.y * dv.z) * invsum32,
+            (-v.x * v.z * dv.x - v.y * v.z * dv.y + (sum2 - v.z * v.z) * dv.z) * invsum32);
+}
+
+__global__ __launch_bounds__(kThreads) void preprocess_bwd_kernel(BwdPreArgs a) {
+  const int idx = (int)(blockIdx.x * kThreads + threadIdx.x);
+  if (idx >= a.P) return;
+  const size_t i = (size_t)idx;
+  const int ncoef = a.M * 3;
+  if (!(a.radii[idx] > 0)) {
+    put3(a.dL_dmeans2D, i, v3(0, 0, 0));
+    if (a.dL_dcolors) put3(a.dL_dcolors, i, v3(0, 0, 0));
+    a.dL_dopacity[i] = 0.0f;
+    put3(a.dL_dmeans3D, i, v3(0, 0, 0));
+    if (a.dL_dcov3D) for (int k = 0; k < 6; k++) a.dL_dcov3D[6 * i + k] = 0.0f;
+    if (a.dL_dsh) for (int k = 0; k < ncoef; k++) a.dL_dsh[i * ncoef + k] = 0.0f;
+    if (a.dL_dscales) put3(a.dL_dscales, i, v3(0, 0, 0));
+    if (a.dL_drotations) reinterpret_cast<float4*>(a.dL_drotations)[i] = make_float4(0, 0, 0, 0);
+    if (a.dL_dsh_language) put3(a.dL_dsh_language, i, v3(0, 0, 0));
+    if (a.dL_dlanguage_feature) put3(a.dL_dlanguage_feature, i, v3(0, 0, 0));
+    return;
+  }
+  const float4* accp = reinterpret_cast<const float4*>(a.acc + i * kAccFloats);
+  const float4 q0 = accp[0], q1 = accp[1], q2 = accp[2], q3 = accp[3];
+  // slots: q0 = {mx, my, ca, cb}, q1 = {cc, op, r, g}, q2 = {b, depth, f0, f1}, q3 = {f2, used, -, -}
+  const float gmx = q0.x, gmy = q0.y;
+  const float dcx = q0.z, dcy = q0.w, dcz = q1.x;
+  put3(a.dL_dmeans2D, i, v3(gmx, gmy, 0.0f));
+  const V3 dL_dcolor = v3(q1.z, q1.w, q2.x);
+  if (a.dL_dcolors) put3(a.dL_dcolors, i, dL_dcolor);
+  a.dL_dopacity[i] = a.confidence ? q1.y * a.confidence[i] : q1.y;
+
+  const V3 mean = v3(a.means3D[3 * i], a.means3D[3 * i + 1], a.means3D[3 * i + 2]);
+  const float* c3 = a.cov3D + 6 * i;
+
+  // ---- computeCov2DCUDA, backward.cu:164-273 ----
+  const Ewa e = ewa_project(mean, a.fx, a.fy, a.tanx, a.tany, c3, a.view);
+  const float x_grad_mul = e.txtz < -e.limx || e.txtz > e.limx ? 0 : 1;
+  const float y_grad_mul = e.tytz < -e.limy || e.tytz > e.limy ? 0 : 1;
+  const float ca = e.a, cb = e.b, cc = e.c;
+  const float denom = ca * cc - cb * cb;
+  float dL_da = 0, dL_db = 0, dL_dc = 0;
+  const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
+  float dcov[6];
+#define Tm(c_, r_) e.T.m[c_][r_]
+#define Vk(c_, r_) e.Vrk.m[c_][r_]
+  if (denom2inv != 0) {
+    dL_da = denom2inv * (-cc * cc * dcx + 2 * cb * cc * dcy + (denom - ca * cc) * dcz);
+    dL_dc = denom2inv * (-ca * ca * dcz + 2 * ca * cb * dcy + (denom - ca * cc) * dcx);
+    dL_db = denom2inv * 2 * (cb * cc * dcx - (denom + 2 * cb * cb) * dcy + ca * cb * dcz);
+    dcov[0] = (Tm(0, 0) * Tm(0, 0) * dL_da + Tm(0, 0) * Tm(1, 0) * dL_db + Tm(1, 0) * Tm(1, 0) * dL_dc);
+    dcov[3] = (Tm(0, 1) * Tm(0, 1) * dL_da + Tm(0, 1) * Tm(1, 1) * dL_db + Tm(1, 1) * Tm(1, 1) * dL_dc);
+    dcov[5] = (Tm(0, 2) * Tm(0, 2) * dL_da + Tm(0, 2) * Tm(1, 2) * dL_db + Tm(1, 2) * Tm(1, 2) * dL_dc);
+    dcov[1] = 2 * Tm(0, 0) * Tm(0, 1) * dL_da + (Tm(0, 0) * Tm(1, 1) + Tm(0, 1) * Tm(1, 0)) * dL_db +
+              2 * Tm(1, 0) * Tm(1, 1) * dL_dc;
+    dcov[2] = 2 * Tm(0, 0) * Tm(0, 2) * dL_da + (Tm(0, 0) * Tm(1, 2) + Tm(0, 2) * Tm(1, 0)) * dL_db +
+              2 * Tm(1, 0) * Tm(1, 2) * dL_dc;
+    dcov[4] = 2 * Tm(0, 2) * Tm(0, 1) * dL_da + (Tm(0, 1) * Tm(1, 2) + Tm(0, 2) * Tm(1, 1)) * dL_db +
+              2 * Tm(1, 1) * Tm(1, 2) * dL_dc;
+  } else {
+#pragma unroll
+    for (int k = 0; k < 6; k++) dcov[k] = 0.0f;
+  }
+#pragma unroll
+  if (a.dL_dcov3D)
+    for (int k = 0; k < 6; k++) a.dL_dcov3D[6 * i + k] = dcov[k];
+  const float dL_dT00 = 2 * (Tm(0, 0) * Vk(0, 0) + Tm(0, 1) * Vk(0, 1) + Tm(0, 2) * Vk(0, 2)) * dL_da +
+                        (Tm(1, 0) * Vk(0, 0) + Tm(1, 1) * Vk(0, 1) + Tm(1, 2) * Vk(0, 2)) * dL_db;
+  const float dL_dT01 = 2 * (Tm(0, 0) * Vk(1, 0) + Tm(0, 1) * Vk(1, 1) + Tm(0, 2) * Vk(1, 2)) * dL_da +
+                        (Tm(1, 0) * Vk(1, 0) + Tm(1, 1) * Vk(1, 1) + Tm(1, 2) * Vk(1, 2)) * dL_db;
+  const float dL_dT02 = 2 * (Tm(0, 0) * Vk(2, 0) + Tm(0, 1) * Vk(2, 1) + Tm(0, 2) * Vk(2, 2)) * dL_da +
+                        (Tm(1, 0) * Vk(2, 0) + Tm(1, 1) * Vk(2, 1) + Tm(1, 2) * Vk(2, 2)) * dL_db;
+  const float dL_dT10 = 2 * (Tm(1, 0) * Vk(0, 0) + Tm(1, 1) * Vk(0, 1) + Tm(1, 2) * Vk(0, 2)) * dL_dc +
+                        (Tm(0, 0) * Vk(0, 0) + Tm(0, 1) * Vk(0, 1) + Tm(0, 2) * Vk(0, 2)) * dL_db;
+  const float dL_dT11 = 2 * (Tm(1, 0) * Vk(1, 0) + Tm(1, 1) * Vk(1, 1) + Tm(1, 2) * Vk(1, 2)) * dL_dc +
+                        (Tm(0, 0) * Vk(1, 0) + Tm(0, 1) * Vk(1, 1) + Tm(0, 2) * Vk(1, 2)) * dL_db;
+  const float dL_dT12 = 2 * (Tm(1, 0) * Vk(2, 0) + Tm(1, 1) * Vk(2, 1) + Tm(1, 2) * Vk(2, 2)) * dL_dc +
+                        (Tm(0, 0) * Vk(2, 0) + Tm(0, 1) * Vk(2, 1) + Tm(0, 2) * Vk(2, 2)) * dL_db;
+#undef Tm
+#undef Vk
+  const M3& Wm = e.W;
+  const float dL_dJ00 = Wm.m[0][0] * dL_dT00 + Wm.m[0][1] * dL_dT01 + Wm.m[0][2] * dL_dT02;
+  const float dL_dJ02 = Wm.m[2][0] * dL_dT00 + Wm.m[2][1] * dL_dT01 + Wm.m[2][2] * dL_dT02;
+  const float dL_dJ11 = Wm.m[1][0] * dL_dT10 + Wm.m[1][1] * dL_dT11 + Wm.m[1][2] * dL_dT12;
+  const float dL_dJ12 = Wm.m[2][0] * dL_dT10 + Wm.m[2][1] * dL_dT11 + Wm.m[2][2] * dL_dT12;
+  const float h_x = a.fx, h_y = a.fy;
+  const float tz = 1.f / e.t.z;
+  const float tz2 = tz * tz;
+  const float tz3 = tz2 * tz;
+  const float dL_dtx = x_grad_mul * -h_x * tz2 * dL_dJ02;
+  const float dL_dty = y_grad_mul * -h_y * tz2 * dL_dJ12;
+  const float dL_dtz = -h_x * tz2 * dL_dJ00 - h_y * tz2 * dL_dJ11 + (2 * h_x * e.t.x) * tz3 * dL_dJ02 +
+                       (2 * h_y * e.t.y) * tz3 * dL_dJ12;
+  V3 dmean = xform_vec43_T(v3(dL_dtx, dL_dty, dL_dtz), a.view);
+
+  // ---- preprocessCUDA (bwd), backward.cu:370-387: screen-space mean gradient ----
+  const float* proj = a.proj;
+  const float m_w = 1.0f / (xform_w(mean, proj) + 0.0000001f);
+  const float mul1 = (proj[0] * mean.x + proj[4] * mean.y + proj[8] * mean.z + proj[12]) * m_w * m_w;
+  const float mul2 = (proj[1] * mean.x + proj[5] * mean.y + proj[9] * mean.z + proj[13]) * m_w * m_w;
+  V3 dm2;
+  dm2.x = (proj[0] * m_w - proj[3] * mul1) * gmx + (proj[1] * m_w - proj[3] * mul2) * gmy;
+  dm2.y = (proj[4] * m_w - proj[7] * mul1) * gmx + (proj[5] * m_w - proj[7] * mul2) * gmy;
+  dm2.z = (proj[8] * m_w - proj[11] * mul1) * gmx + (proj[9] * m_w - proj[11] * mul2) * gmy;
+  dmean = dmean + dm2;
+
+  // ---- SH colour backward (backward.cu:390-391) ----
+  if (a.shs) {
+    float* d = a.dL_dsh + i * ncoef;
+    const uint8_t cl = a.clamped[i];
+    V3 dRGB = dL_dcolor;
+    dRGB.x *= (cl & 1) ? 0 : 1;
+    dRGB.y *= (cl & 2) ? 0 : 1;
+    dRGB.z *= (cl & 4) ? 0 : 1;
+    const V3 dir_orig = mean - v3(a.campos[0], a.campos[1], a.campos[2]);
+    const int deg = a.D;
+    const int used = (deg + 1) * (deg + 1) * 3;
+    for (int k = used; k < ncoef; k++) d[k] = 0.0f;
+    dmean = dmean + sh_backward(a.shs + i * ncoef, deg, dir_orig, dRGB, d);
+  }
+
+  // ---- cov3D -> scale / rotation (backward.cu:278-341, 393-395) ----
+  if (a.scales) {
+    const float4 q = reinterpret_cast<const float4*>(a.rotations)[i];
+    const float r = q.x, x = q.y, y = q.z, z = q.w;
+    M3 R = m3_cols(1.f - 2.f * (y * y + z * z), 2.f * (x * y - r * z), 2.f * (x * z + r * y),
+                   2.f * (x * y + r * z), 1.f - 2.f * (x * x + z * z), 2.f * (y * z - r * x),
+                   2.f * (x * z - r * y), 2.f * (y * z + r * x), 1.f - 2.f * (x * x + y * y));
+    M3 S = m3_cols(1, 0, 0, 0, 1, 0, 0, 0, 1);
+    const V3 s = a.scale_modifier * v3(a.scales[3 * i], a.scales[3 * i + 1], a.scales[3 * i + 2]);
+    S.m[0][0] = s.x; S.m[1][1] = s.y; S.m[2][2] = s.z;
+    const M3 Mm = m3_mul(S, R);
+    const float* g6 = dcov;
+    const M3 dL_dSigma = m3_cols(g6[0], 0.5f * g6[1], 0.5f * g6[2], 0.5f * g6[1], g6[3], 0.5f * g6[4],
+                                 0.5f * g6[2], 0.5f * g6[4], g6[5]);
+    M3 M2;
+#pragma unroll
+    for (int c = 0; c < 3; c++)
+#pragma unroll
+      for (int w = 0; w < 3; w++) M2.m[c][w] = 2.0f * Mm.m[c][w];
+    const M3 dL_dM = m3_mul(M2, dL_dSigma);
+    const M3 Rt = m3_T(R);
+    M3 Dt = m3_T(dL_dM);
+    V3 ds;
+    ds.x = dot3(v3(Rt.m[0][0], Rt.m[0][1], Rt.m[0][2]), v3(Dt.m[0][0], Dt.m[0][1], Dt.m[0][2]));
+    ds.y = dot3(v3(Rt.m[1][0], Rt.m[1][1], Rt.m[1][2]), v3(Dt.m[1][0], Dt.m[1][1], Dt.m[1][2]));
+    ds.z = dot3(v3(Rt.m[2][0], Rt.m[2][1], Rt.m[2][2]), v3(Dt.m[2][0], Dt.m[2][1], Dt.m[2][2]));
+    put3(a.dL_dscales, i, ds);
+#pragma unroll
+    for (int w = 0; w < 3; w++) {
+      Dt.m[0][w] *= s.x;
+      Dt.m[1][w] *= s.y;
+      Dt.m[2][w] *= s.z;
+    }
+#define D(c_, r_) Dt.m[c_][r_]
+    float4 dq;
+    dq.x = 2 * z * (D(0, 1) - D(1, 0)) + 2 * y * (D(2, 0) - D(0, 2)) + 2 * x * (D(1, 2) - D(2, 1));
+    dq.y = 2 * y * (D(1, 0) + D(0, 1)) + 2 * z * (D(2, 0) + D(0, 2)) + 2 * r * (D(1, 2) - D(2, 1)) -
+           4 * x * (D(2, 2) + D(1, 1));
+    dq.z = 2 * x * (D(1, 0) + D(0, 1)) + 2 * r * (D(2, 0) - D(0, 2)) + 2 * z * (D(1, 2) + D(2, 1)) -
+           4 * y * (D(2, 2) + D(0, 0));
+    dq.w = 2 * r * (D(0, 1) - D(1, 0)) + 2 * x * (D(2, 0) + D(0, 2)) + 2 * y * (D(1, 2) + D(2, 1)) -
+           4 * z * (D(1, 1) + D(0, 0));
+#undef D
+    reinterpret_cast<float4*>(a.dL_drotations)[i] = dq;
+  }
+
+  // ---- depth channel: z_view = view[2] x + view[6] y + view[10] z + view[14] ----
+  const float dz = q2.y;
+  dmean.x += dz * a.view[2];
+  dmean.y += dz * a.view[6];
+  dmean.z += dz * a.view[10];
+  put3(a.dL_dmeans3D, i, dmean);
+
+  // ---- language feature channels ----
+  if (a.dL_dlanguage_feature) {
+    put3(a.dL_dlanguage_feature, i,
+         (a.include_feature && a.lang_precomp) ? v3(q2.z, q2.w, q3.x) : v3(0, 0, 0));
+  }
+  if (a.dL_dsh_language) {
+    V3 out = v3(0, 0, 0);
+    if (a.include_feature && a.lang_precomp == nullptr) {
+      const float* l = a.sh_language + 3 * i;
+      const float u0 = SH_C0 * l[0], u1 = SH_C0 * l[1], u2 = SH_C0 * l[2];
+      const float n = sqrtf(u0 * u0 + u1 * u1 + u2 * u2);
+      const float den = n + 1e-9f;
+      const float g0 = q2.z, g1 = q2.w, g2 = q3.x;
+      const float ug = u0 * g0 + u1 * g1 + u2 * g2;
+      const float k2 = n > 0.0f ? ug / (den * den * n) : 0.0f;
+      out = v3(SH_C0 * (g0 / den - u0 * k2), SH_C0 * (g1 / den - u1 * k2), SH_C0 * (g2 / den - u2 * k2));
+    }
+    put3(a.dL_dsh_language, i, out);
+  }
+}
+
+}  // namespace
+
+hipError_t launch_preprocess_backward(const BwdPreArgs& a, hipStream_t s) {
+  if (a.P == 0) return hipSuccess;
+  hipLaunchKernelGGL(preprocess_bwd_kernel, dim3((a.P + kThreads - 1) / kThreads), dim3(kThreads),
+                     0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace gsr

@@ -1,0 +1,87 @@
+// gsr_binning.hip -- tile binning: key duplication and per-tile ranges.
+//
+// Reference behaviour: duplicateWithKeys (cuda_rasterizer/rasterizer_impl.cu:70-111) emits one
+// (tile << 32 | depth_bits, gaussian_id) pair per overlapped tile, SortPairs sorts them stably over
+// 32 + bit bits (:300-308) and identifyTileRanges (:116-138) finds each tile's [start, end).
+//
+// gfx950 design: the order (tile, depth_bits, gaussian_id) is produced by a
+// depth-first two-stage sort instead of one 45-bit sort of R 12-byte pairs:
+//   1. stable 32-bit radix sort of the P depth keys (ties keep Gaussian order),
+//   2. duplication in depth order (this file), emitting 4-byte tile ids,
+//   3. stable radix sort of the R tile ids over `bit` bits (2 passes at 1080p instead of 6).
+// Stage 3 is stable, so instances with equal tile keep the depth-sorted emission order; the
+// resulting point_list is identical to the reference's.
+#include "gsr_device.h"
+#include "gsr_internal.h"
+
+namespace gsr {
+namespace {
+
+constexpr int kThreads = 256;
+
+// One lane per depth-sorted Gaussian; the lane writes its tile ids row-major over its tile
+// rectangle (the reference's emission order inside one Gaussian, rasterizer_impl.cu:98-109).
+__global__ __launch_bounds__(kThreads) void duplicate_kernel(int P,
+                                                             const uint32_t* __restrict__ order,
+                                                             const uint32_t* __restrict__ offsets,
+                                                             const int32_t* __restrict__ radii,
+                                                             const float4* __restrict__ rec,
+                                                             uint32_t gx, uint32_t gy,
+                                                             uint32_t* __restrict__ tkey,
+                                                             uint32_t* __restrict__ tval) {
+  const int s = (int)(blockIdx.x * kThreads + threadIdx.x);
+  if (s >= P) return;
+  const uint32_t gid = order[s];
+  const int r = radii[gid];
+  if (!(r > 0)) return;
+  uint32_t off = (s == 0) ? 0u : offsets[s - 1];
+  const float4 r0 = rec[4 * (size_t)gid];
+  uint32_t x0, y0, x1, y1;
+  tile_rect(r0.x, r0.y, r, gx, gy, x0, y0, x1, y1);
+  for (uint32_t y = y0; y < y1; y++)
+    for (uint32_t x = x0; x < x1; x++) {
+      tkey[off] = y * gx + x;
+      tval[off] = gid;
+      off++;
+    }
+}
+
+__global__ __launch_bounds__(kThreads) void tile_ranges_kernel(size_t R,
+                                                               const uint32_t* __restrict__ tiles,
+                                                               uint2* __restrict__ ranges) {
+  const size_t idx = (size_t)blockIdx.x * kThreads + threadIdx.x;
+  if (idx >= R) return;
+  const uint32_t cur = tiles[idx];
+  if (idx == 0) {
+    ranges[cur].x = 0;
+  } else {
+    const uint32_t prev = tiles[idx - 1];
+    if (cur != prev) {
+      ranges[prev].y = (uint32_t)idx;
+      ranges[cur].x = (uint32_t)idx;
+    }
+  }
+  if (idx == R - 1) ranges[cur].y = (uint32_t)R;
+}
+
+}  // namespace
+
+hipError_t launch_duplicate(int P, const uint32_t* order, const uint32_t* offsets,
+                            const int32_t* radii, const float4* rec, uint32_t gx, uint32_t gy,
+                            uint32_t* tkey, uint32_t* tval, hipStream_t s) {
+  if (P == 0) return hipSuccess;
+  hipLaunchKernelGGL(duplicate_kernel, dim3((P + kThreads - 1) / kThreads), dim3(kThreads), 0, s,
+                     P, order, offsets, radii, rec, gx, gy, tkey, tval);
+  return hipGetLastError();
+}
+
+hipError_t launch_tile_ranges(size_t R, const uint32_t* sorted_tiles, uint2* ranges,
+                              uint32_t ntiles, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(ranges, 0, sizeof(uint2) * ntiles, s);
+  if (e != hipSuccess || R == 0) return e;
+  hipLaunchKernelGGL(tile_ranges_kernel, dim3((unsigned)((R + kThreads - 1) / kThreads)),
+                     dim3(kThreads), 0, s, R, sorted_tiles, ranges);
+  return hipGetLastError();
+}
+
+}  // namespace gsr

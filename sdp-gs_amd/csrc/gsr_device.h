@@ -1,0 +1,167 @@
+// gsr_device.h -- per-Gaussian device maths for the gfx950 rasterizer.
+//
+// Semantics follow the reference CUDA rasterizer (paths relative to
+// /root/reference/submodules/diff-gaussian-rasterization/): auxiliary.h:21-164 (helpers, SH
+// constants), forward.cu:20-152 (SH colour, 2D/3D covariance) and backward.cu:20-341 (their
+// gradients).  The reference evaluates its 3x3 maths with glm (column-major, left-to-right sums);
+// the helpers below keep that evaluation order so float32 results match the CPU restatement in
+// oracle/ bit for bit (the library is compiled with -ffp-contract=off; expf is the only libm call
+// whose last bit may differ).  This is fresh code for wave64 CDNA4, not a translation of the
+// reference's glm-based device functions.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "gsr_internal.h"
+
+namespace gsr {
+
+__device__ constexpr float SH_C0 = 0.28209479177387814f;
+__device__ constexpr float SH_C1 = 0.4886025119029199f;
+__device__ constexpr float SH_C2_0 = 1.0925484305920792f;
+__device__ constexpr float SH_C2_1 = -1.0925484305920792f;
+__device__ constexpr float SH_C2_2 = 0.31539156525252005f;
+__device__ constexpr float SH_C2_3 = -1.0925484305920792f;
+__device__ constexpr float SH_C2_4 = 0.5462742152960396f;
+__device__ constexpr float SH_C3_0 = -0.5900435899266435f;
+__device__ constexpr float SH_C3_1 = 2.890611442640554f;
+__device__ constexpr float SH_C3_2 = -0.4570457994644658f;
+__device__ constexpr float SH_C3_3 = 0.3731763325901154f;
+__device__ constexpr float SH_C3_4 = -0.4570457994644658f;
+__device__ constexpr float SH_C3_5 = 1.445305721320277f;
+__device__ constexpr float SH_C3_6 = -0.5900435899266435f;
+
+struct V3 { float x, y, z; };
+struct M3 { float m[3][3]; };  // m[col][row], glm::mat3 convention
+
+__device__ __forceinline__ V3 v3(float x, float y, float z) { return V3{x, y, z}; }
+__device__ __forceinline__ V3 operator+(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ V3 operator-(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ V3 operator*(float s, V3 a) { return v3(s * a.x, s * a.y, s * a.z); }
+__device__ __forceinline__ V3 operator*(V3 a, float s) { return v3(a.x * s, a.y * s, a.z * s); }
+__device__ __forceinline__ float dot3(V3 a, V3 b) {
+  float tx = a.x * b.x, ty = a.y * b.y, tz = a.z * b.z;
+  return tx + ty + tz;
+}
+
+__device__ __forceinline__ M3 m3_cols(float a0, float a1, float a2, float b0, float b1, float b2,
+                                      float c0, float c1, float c2) {
+  M3 r;
+  r.m[0][0] = a0; r.m[0][1] = a1; r.m[0][2] = a2;
+  r.m[1][0] = b0; r.m[1][1] = b1; r.m[1][2] = b2;
+  r.m[2][0] = c0; r.m[2][1] = c1; r.m[2][2] = c2;
+  return r;
+}
+// glm mat3*mat3: R[c][r] = A[0][r]*B[c][0] + A[1][r]*B[c][1] + A[2][r]*B[c][2]
+__device__ __forceinline__ M3 m3_mul(const M3& a, const M3& b) {
+  M3 r;
+#pragma unroll
+  for (int c = 0; c < 3; c++)
+#pragma unroll
+    for (int w = 0; w < 3; w++) {
+      float t0 = a.m[0][w] * b.m[c][0];
+      float t1 = a.m[1][w] * b.m[c][1];
+      float t2 = a.m[2][w] * b.m[c][2];
+      r.m[c][w] = t0 + t1 + t2;
+    }
+  return r;
+}
+__device__ __forceinline__ M3 m3_T(const M3& a) {
+  M3 r;
+#pragma unroll
+  for (int c = 0; c < 3; c++)
+#pragma unroll
+    for (int w = 0; w < 3; w++) r.m[c][w] = a.m[w][c];
+  return r;
+}
+
+// HIP float->int conversion (v_cvt_i32_f32) truncates and saturates, NaN -> 0: the same as the
+// reference's CUDA cvt.rzi; written explicitly so the compiler cannot assume an in-range value.
+__device__ __forceinline__ int f2i_sat(float f) {
+  if (f != f) return 0;
+  if (f >= 2147483648.0f) return 2147483647;
+  if (f <= -2147483648.0f) return -2147483647 - 1;
+  return (int)f;
+}
+
+// auxiliary.h:41-44 (double promotion is part of the reference's numerics)
+__device__ __forceinline__ float ndc2pix(float v, int S) {
+  return (float)((((double)v + 1.0) * S - 1.0) * 0.5);
+}
+
+// auxiliary.h:46-56: tile rectangle [min, max) of a splat, clamped to the tile grid.
+__device__ __forceinline__ void tile_rect(float px, float py, int r, uint32_t gx, uint32_t gy,
+                                          uint32_t& x0, uint32_t& y0, uint32_t& x1, uint32_t& y1) {
+  int a = f2i_sat((px - (float)r) / (float)kTile);
+  int b = f2i_sat((py - (float)r) / (float)kTile);
+  int c = f2i_sat((((px + (float)r) + (float)kTile) - 1.0f) / (float)kTile);
+  int d = f2i_sat((((py + (float)r) + (float)kTile) - 1.0f) / (float)kTile);
+  a = a > 0 ? a : 0; b = b > 0 ? b : 0; c = c > 0 ? c : 0; d = d > 0 ? d : 0;
+  x0 = min((uint32_t)a, gx); y0 = min((uint32_t)b, gy);
+  x1 = min((uint32_t)c, gx); y1 = min((uint32_t)d, gy);
+}
+
+// auxiliary.h:58-77 (the 4x4 matrices are row-major tensors read as column-major)
+__device__ __forceinline__ V3 xform_point43(V3 p, const float* m) {
+  return v3(m[0] * p.x + m[4] * p.y + m[8] * p.z + m[12],
+            m[1] * p.x + m[5] * p.y + m[9] * p.z + m[13],
+            m[2] * p.x + m[6] * p.y + m[10] * p.z + m[14]);
+}
+__device__ __forceinline__ float xform_w(V3 p, const float* m) {
+  return m[3] * p.x + m[7] * p.y + m[11] * p.z + m[15];
+}
+// auxiliary.h:89-97
+__device__ __forceinline__ V3 xform_vec43_T(V3 p, const float* m) {
+  return v3(m[0] * p.x + m[1] * p.y + m[2] * p.z, m[4] * p.x + m[5] * p.y + m[6] * p.z,
+            m[8] * p.x + m[9] * p.y + m[10] * p.z);
+}
+
+// forward.cu:118-152: Sigma = (S R)^T (S R), quaternion (w,x,y,z) NOT normalised in-kernel.
+__device__ __forceinline__ void cov3d_from_scale_rot(float sx, float sy, float sz, float mod,
+                                                     float r, float x, float y, float z,
+                                                     float out[6]) {
+  M3 S = m3_cols(1, 0, 0, 0, 1, 0, 0, 0, 1);
+  S.m[0][0] = mod * sx;
+  S.m[1][1] = mod * sy;
+  S.m[2][2] = mod * sz;
+  M3 R = m3_cols(1.f - 2.f * (y * y + z * z), 2.f * (x * y - r * z), 2.f * (x * z + r * y),
+                 2.f * (x * y + r * z), 1.f - 2.f * (x * x + z * z), 2.f * (y * z - r * x),
+                 2.f * (x * z - r * y), 2.f * (y * z + r * x), 1.f - 2.f * (x * x + y * y));
+  M3 M = m3_mul(S, R);
+  M3 Sig = m3_mul(m3_T(M), M);
+  out[0] = Sig.m[0][0]; out[1] = Sig.m[0][1]; out[2] = Sig.m[0][2];
+  out[3] = Sig.m[1][1]; out[4] = Sig.m[1][2]; out[5] = Sig.m[2][2];
+}
+
+// EWA projection of a world covariance (forward.cu:74-113 and the recomputation at
+// backward.cu:166-199).  Returns T = W*J (for the backward) and the un-filtered 2D covariance.
+struct Ewa {
+  M3 T, W, Vrk;
+  V3 t;             // clamped view-space mean
+  float txtz, tytz, limx, limy;
+  float a, b, c;    // 2D covariance with the +0.3 low-pass on the diagonal
+};
+__device__ __forceinline__ Ewa ewa_project(V3 mean, float fx, float fy, float tanx, float tany,
+                                           const float* c3, const float* view) {
+  Ewa e;
+  V3 t = xform_point43(mean, view);
+  e.limx = 1.3f * tanx;
+  e.limy = 1.3f * tany;
+  e.txtz = t.x / t.z;
+  e.tytz = t.y / t.z;
+  t.x = fminf(e.limx, fmaxf(-e.limx, e.txtz)) * t.z;
+  t.y = fminf(e.limy, fmaxf(-e.limy, e.tytz)) * t.z;
+  e.t = t;
+  M3 J = m3_cols(fx / t.z, 0.0f, -(fx * t.x) / (t.z * t.z), 0.0f, fy / t.z,
+                 -(fy * t.y) / (t.z * t.z), 0, 0, 0);
+  e.W = m3_cols(view[0], view[4], view[8], view[1], view[5], view[9], view[2], view[6], view[10]);
+  e.T = m3_mul(e.W, J);
+  e.Vrk = m3_cols(c3[0], c3[1], c3[2], c3[1], c3[3], c3[4], c3[2], c3[4], c3[5]);
+  M3 cov = m3_mul(m3_mul(m3_T(e.T), m3_T(e.Vrk)), e.T);
+  e.a = cov.m[0][0] + 0.3f;
+  e.b = cov.m[0][1];
+  e.c = cov.m[1][1] + 0.3f;
+  return e;
+}
+
+}  // namespace gsr

@@ -1,0 +1,184 @@
+// gsr_internal.h -- private buffer layouts and kernel launchers of libgsr (not part of the C-ABI).
+//
+// The three scratch byte buffers play the role of the reference's GeometryState / BinningState /
+// ImageState (cuda_rasterizer/rasterizer_impl.h:21-73, rasterizer_impl.cu:155-194): the forward
+// carves them, Python keeps them alive in the autograd context, and the backward re-carves the
+// same offsets from the same bytes.  The layout itself is ours (a per-splat 64-byte record packed
+// for the tile gather, a depth-first two-stage sort, per-splat gradient accumulators).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace gsr {
+
+constexpr int kTile = 16;                 // config.h:16-17 (BLOCK_X = BLOCK_Y = 16)
+constexpr int kTilePix = kTile * kTile;   // 256 pixels = 4 waves of 64 lanes
+constexpr size_t kAlign = 256;
+constexpr int kRecFloats = 16;        // 4 x float4 splat record (see gsr_preprocess.hip)
+constexpr int kAccFloats = 16;        // per-splat gradient accumulator row (64 B)
+// Accumulator slots (one 64-byte row per Gaussian, filled by the backward blend)
+enum AccSlot : int {
+  kAccMx = 0, kAccMy = 1,                 // dL/dmean2D (NDC-scaled, backward.cu:545-546)
+  kAccCa = 2, kAccCb = 3, kAccCc = 4,     // dL/dconic (x, y, w of the reference's float4)
+  kAccOp = 5,                             // dL/dopacity (effective opacity)
+  kAccR = 6, kAccG = 7, kAccB = 8,        // dL/dcolor
+  kAccDepth = 9,                          // dL/ddepth (view-space z)
+  kAccF0 = 10, kAccF1 = 11, kAccF2 = 12,  // dL/dfeature
+  kAccUsed = 13
+};
+
+inline size_t align_up(size_t x) { return (x + kAlign - 1) & ~(kAlign - 1); }
+
+struct Carver {
+  char* base;
+  size_t off = 0;
+  explicit Carver(char* b) : base(b) {}
+  template <class T>
+  T* take(size_t n) {
+    off = align_up(off);
+    T* p = base ? reinterpret_cast<T*>(base + off) : nullptr;
+    off += n * sizeof(T);
+    return p;
+  }
+  size_t size() const { return align_up(off); }
+};
+
+// ---- device-wide primitives (gsr_sort.hip) -----------------------------------------------------
+constexpr int kScanTile = 2048;       // elements per scan workgroup (256 threads x 8)
+constexpr int kScanMaxParts = 8192;   // partials scanned by the single-workgroup middle pass
+constexpr int kSortTile = 4096;       // keys per radix-sort workgroup (256 threads x 16)
+
+inline size_t scan_parts(size_t n) { return (n + kScanTile - 1) / kScanTile; }
+inline size_t sort_blocks(size_t n) { return (n + kSortTile - 1) / kSortTile; }
+inline size_t sort_hist_len(size_t n) { return 256 * sort_blocks(n); }
+inline int sort_passes(int bits) { return (bits + 7) / 8; }
+
+struct SortScratch {
+  uint32_t* hist;   // [256 * blocks]
+  uint32_t* parts;  // scan partials of hist
+};
+
+// Exclusive (inclusive=false) or inclusive prefix sum of n u32 values; if gather != nullptr the
+// input element i is in[gather[i]].  parts: scratch of scan_parts(n) u32.
+hipError_t scan_u32(const uint32_t* in, const uint32_t* gather, uint32_t* out, size_t n,
+                    bool inclusive, uint32_t* parts, hipStream_t s);
+// Stable LSD radix sort of (key, value) u32 pairs over key bits [0, bits).  Ping-pongs between
+// (ka, va) and (kb, vb); returns through *result_in_b whether the sorted data ended in (kb, vb).
+hipError_t radix_sort_pairs(uint32_t* ka, uint32_t* va, uint32_t* kb, uint32_t* vb, size_t n,
+                            int bits, SortScratch scratch, bool* result_in_b, hipStream_t s);
+
+// ---- layouts -------------------------------------------------------------------------------------
+struct GeomState {
+  float* depths;            // [P] view-space z (valid where radii > 0)
+  uint32_t* dkey_a;         // [P] depth-sort keys (float bits of z; 0xffffffff if culled)
+  uint32_t* dval_a;         // [P] Gaussian ids, depth-sorted after the sort (see depth_sorted())
+  uint32_t* dkey_b;
+  uint32_t* dval_b;
+  uint8_t* clamped;         // [P] bit c set <=> SH colour channel c clamped (forward.cu:67-69)
+  int32_t* radii;           // [P] internal radii (used when the caller passes none)
+  float* cov3D;             // [P*6]
+  float4* rec;              // [P*4] splat record for the blend
+  uint32_t* tiles_touched;  // [P]
+  uint32_t* offsets;        // [P] inclusive scan of tiles_touched in depth order
+  float* acc;               // [P*16] backward accumulators
+  uint32_t* flags;          // [4]  [0]: prefiltered violation
+  uint32_t* sort_hist;
+  uint32_t* sort_parts;
+  uint32_t* scan_parts;
+  size_t bytes;
+};
+GeomState carve_geom(char* base, size_t P);
+
+struct BinState {
+  uint32_t* tkey_a;  // [R] tile ids of the duplicated instances
+  uint32_t* tval_a;  // [R] Gaussian ids
+  uint32_t* tkey_b;
+  uint32_t* tval_b;
+  uint32_t* hist;
+  uint32_t* parts;
+  size_t bytes;
+};
+BinState carve_bin(char* base, size_t R);
+
+struct ImgState {
+  float* final_T;       // [H*W]
+  uint32_t* n_contrib;  // [H*W]
+  uint2* ranges;        // [tiles]
+  uint32_t* tile_last;  // [tiles] max n_contrib over the tile's pixels
+  size_t bytes;
+};
+ImgState carve_img(char* base, size_t W, size_t H);
+
+// ---- per-Gaussian kernels (gsr_preprocess.hip, gsr_backward.hip) ----------------------------------
+struct PreArgs {
+  int P, D, M, W, H;
+  uint32_t gx, gy;
+  const float *means3D, *scales, *rotations, *opacities, *shs, *cov3D_precomp, *colors_precomp;
+  const float *sh_language, *lang_precomp, *confidence;
+  const float *view, *proj, *campos;
+  float scale_modifier, tanx, tany, fx, fy;
+  int prefiltered, include_feature;
+  int32_t* radii;
+  GeomState g;
+};
+hipError_t launch_preprocess(const PreArgs& a, hipStream_t s);
+hipError_t launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present,
+                               hipStream_t s);
+
+struct BwdPreArgs {
+  int P, D, M;
+  const float *means3D, *scales, *rotations, *shs, *cov3D, *colors_precomp;
+  const float *sh_language, *lang_precomp, *confidence;
+  const float *view, *proj, *campos;
+  float scale_modifier, tanx, tany, fx, fy;
+  int include_feature;
+  const int32_t* radii;
+  const uint8_t* clamped;
+  const float* acc;
+  // outputs (every element written)
+  float *dL_dmeans2D, *dL_dcolors, *dL_dopacity, *dL_dmeans3D, *dL_dcov3D, *dL_dsh, *dL_dscales,
+      *dL_drotations, *dL_dsh_language, *dL_dlanguage_feature;
+};
+hipError_t launch_preprocess_backward(const BwdPreArgs& a, hipStream_t s);
+
+// ---- binning (gsr_binning.hip) -------------------------------------------------------------------
+hipError_t launch_duplicate(int P, const uint32_t* order, const uint32_t* offsets,
+                            const int32_t* radii, const float4* rec, uint32_t gx, uint32_t gy,
+                            uint32_t* tkey, uint32_t* tval, hipStream_t s);
+hipError_t launch_tile_ranges(size_t R, const uint32_t* sorted_tiles, uint2* ranges,
+                              uint32_t ntiles, hipStream_t s);
+
+// ---- blend (gsr_render.hip) ----------------------------------------------------------------------
+struct RenderArgs {
+  int W, H;
+  uint32_t gx, gy;
+  const uint2* ranges;
+  const uint32_t* point_list;
+  const float4* rec;
+  const float* bg;
+  float* final_T;
+  uint32_t* n_contrib;
+  uint32_t* tile_last;
+  float *out_color, *out_depth, *out_alpha, *out_feature;
+  int include_feature;
+};
+hipError_t launch_render_forward(const RenderArgs& a, hipStream_t s);
+
+struct RenderBwdArgs {
+  int W, H;
+  uint32_t gx, gy;
+  const uint2* ranges;
+  const uint32_t* point_list;
+  const float4* rec;
+  const float* bg;
+  const float* final_T;
+  const uint32_t* n_contrib;
+  const uint32_t* tile_last;
+  const float *dL_dcolor, *dL_ddepth, *dL_dalpha, *dL_dfeature;
+  float* acc;
+  int include_feature;
+};
+hipError_t launch_render_backward(const RenderBwdArgs& a, hipStream_t s);
+
+}  // namespace gsr

@@ -1,0 +1,170 @@
+// gsr_preprocess.hip -- per-Gaussian forward preprocess and the near-plane visibility test.
+//
+// Behaviour follows preprocessCUDA (cuda_rasterizer/forward.cu:155-256), computeColorFromSH
+// (:20-71), in_frustum (auxiliary.h:139-164) and checkFrustum (rasterizer_impl.cu:54-66).
+// gfx950 design: one lane per Gaussian over the SoA inputs; the kernel writes everything the
+// later stages need in one pass -- the depth-sort key (float bits of view z, which sort
+// monotonically because z > 0.2), the tile count, and a 64-byte "splat record" packed for the
+// blend's tile gather:
+//   rec[4g+0] = {x_px, y_px, conic.a, conic.b}
+//   rec[4g+1] = {conic.c, opacity*confidence, depth, r}
+//   rec[4g+2] = {g, b, f0, f1}
+//   rec[4g+3] = {f2, 0, 0, 0}
+// so the blend reads one contiguous record per instance instead of five scattered arrays.
+#include "gsr_device.h"
+#include "gsr_internal.h"
+
+namespace gsr {
+namespace {
+
+constexpr int kThreads = 256;
+
+// forward.cu:20-71 (float32, same evaluation order as the CPU restatement)
+__device__ __forceinline__ V3 sh_to_rgb(const float* __restrict__ s, int deg, V3 dir,
+                                        uint8_t& clamped) {
+#define SH(k) v3(s[3 * (k)], s[3 * (k) + 1], s[3 * (k) + 2])
+  V3 result = SH_C0 * SH(0);
+  if (deg > 0) {
+    const float x = dir.x, y = dir.y, z = dir.z;
+    result = ((result - (SH_C1 * y) * SH(1)) + (SH_C1 * z) * SH(2)) - (SH_C1 * x) * SH(3);
+    if (deg > 1) {
+      const float xx = x * x, yy = y * y, zz = z * z;
+      const float xy = x * y, yz = y * z, xz = x * z;
+      result = result + (SH_C2_0 * xy) * SH(4);
+      result = result + (SH_C2_1 * yz) * SH(5);
+      result = result + (SH_C2_2 * (2.0f * zz - xx - yy)) * SH(6);
+      result = result + (SH_C2_3 * xz) * SH(7);
+      result = result + (SH_C2_4 * (xx - yy)) * SH(8);
+      if (deg > 2) {
+        result = result + (SH_C3_0 * y * (3.0f * xx - yy)) * SH(9);
+        result = result + (SH_C3_1 * xy * z) * SH(10);
+        result = result + (SH_C3_2 * y * (4.0f * zz - xx - yy)) * SH(11);
+        result = result + (SH_C3_3 * z * (2.0f * zz - 3.0f * xx - 3.0f * yy)) * SH(12);
+        result = result + (SH_C3_4 * x * (4.0f * zz - xx - yy)) * SH(13);
+        result = result + (SH_C3_5 * z * (xx - yy)) * SH(14);
+        result = result + (SH_C3_6 * x * (xx - 3.0f * yy)) * SH(15);
+      }
+    }
+  }
+#undef SH
+  result = v3(result.x + 0.5f, result.y + 0.5f, result.z + 0.5f);
+  clamped = (uint8_t)((result.x < 0) | ((result.y < 0) << 1) | ((result.z < 0) << 2));
+  return v3(fmaxf(result.x, 0.0f), fmaxf(result.y, 0.0f), fmaxf(result.z, 0.0f));
+}
+
+__global__ __launch_bounds__(kThreads) void preprocess_kernel(PreArgs a) {
+  const int idx = (int)(blockIdx.x * kThreads + threadIdx.x);
+  if (idx >= a.P) return;
+  const GeomState& g = a.g;
+  a.radii[idx] = 0;
+  g.tiles_touched[idx] = 0;
+  g.dkey_a[idx] = 0xffffffffu;
+  g.dval_a[idx] = (uint32_t)idx;
+
+  const V3 p_orig = v3(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
+  // in_frustum: near-plane test only (auxiliary.h:154)
+  const V3 p_view = xform_point43(p_orig, a.view);
+  if (p_view.z <= 0.2f) {
+    if (a.prefiltered) atomicOr(&g.flags[0], 1u);  // reference __trap()s (auxiliary.h:156-160)
+    return;
+  }
+  const V3 ph = xform_point43(p_orig, a.proj);
+  const float pw = 1.0f / (xform_w(p_orig, a.proj) + 0.0000001f);
+  const float pproj_x = ph.x * pw, pproj_y = ph.y * pw;
+
+  float c3buf[6];
+  const float* c3;
+  if (a.cov3D_precomp) {
+    c3 = a.cov3D_precomp + 6 * (size_t)idx;
+  } else {
+    const float4 q = reinterpret_cast<const float4*>(a.rotations)[idx];
+    cov3d_from_scale_rot(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2],
+                         a.scale_modifier, q.x, q.y, q.z, q.w, c3buf);
+    float* dst = g.cov3D + 6 * (size_t)idx;
+#pragma unroll
+    for (int k = 0; k < 6; k++) dst[k] = c3buf[k];
+    c3 = c3buf;
+  }
+  const Ewa e = ewa_project(p_orig, a.fx, a.fy, a.tanx, a.tany, c3, a.view);
+  const float det = (e.a * e.c - e.b * e.b);
+  if (det == 0.0f) return;
+  const float det_inv = 1.f / det;
+  const float con_a = e.c * det_inv, con_b = -e.b * det_inv, con_c = e.a * det_inv;
+  const float mid = 0.5f * (e.a + e.c);
+  const float lambda1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
+  const float lambda2 = mid - sqrtf(fmaxf(0.1f, mid * mid - det));
+  const float my_radius = ceilf(3.f * sqrtf(fmaxf(lambda1, lambda2)));
+  const float px = ndc2pix(pproj_x, a.W), py = ndc2pix(pproj_y, a.H);
+  const int r = f2i_sat(my_radius);
+  uint32_t x0, y0, x1, y1;
+  tile_rect(px, py, r, a.gx, a.gy, x0, y0, x1, y1);
+  if ((x1 - x0) * (y1 - y0) == 0) return;
+
+  float cr, cg, cb;
+  if (a.colors_precomp == nullptr) {
+    V3 dir = p_orig - v3(a.campos[0], a.campos[1], a.campos[2]);
+    const float len = sqrtf(dot3(dir, dir));
+    dir = v3(dir.x / len, dir.y / len, dir.z / len);
+    uint8_t cl;
+    const V3 c = sh_to_rgb(a.shs + (size_t)idx * a.M * 3, a.D, dir, cl);
+    g.clamped[idx] = cl;
+    cr = c.x; cg = c.y; cb = c.z;
+  } else {
+    cr = a.colors_precomp[3 * idx];
+    cg = a.colors_precomp[3 * idx + 1];
+    cb = a.colors_precomp[3 * idx + 2];
+  }
+  float op = a.opacities[idx];
+  if (a.confidence) op = op * a.confidence[idx];
+  float f0 = 0.f, f1 = 0.f, f2 = 0.f;
+  if (a.include_feature) {
+    if (a.lang_precomp) {
+      f0 = a.lang_precomp[3 * idx]; f1 = a.lang_precomp[3 * idx + 1]; f2 = a.lang_precomp[3 * idx + 2];
+    } else if (a.sh_language) {
+      const float u0 = SH_C0 * a.sh_language[3 * idx];
+      const float u1 = SH_C0 * a.sh_language[3 * idx + 1];
+      const float u2 = SH_C0 * a.sh_language[3 * idx + 2];
+      const float n = sqrtf(u0 * u0 + u1 * u1 + u2 * u2);
+      const float den = n + 1e-9f;
+      f0 = u0 / den; f1 = u1 / den; f2 = u2 / den;
+    }
+  }
+  const float depth = p_view.z;
+  g.depths[idx] = depth;
+  a.radii[idx] = r;
+  g.tiles_touched[idx] = (y1 - y0) * (x1 - x0);
+  g.dkey_a[idx] = __float_as_uint(depth);
+  float4* rec = g.rec + 4 * (size_t)idx;
+  rec[0] = make_float4(px, py, con_a, con_b);
+  rec[1] = make_float4(con_c, op, depth, cr);
+  rec[2] = make_float4(cg, cb, f0, f1);
+  rec[3] = make_float4(f2, 0.f, 0.f, 0.f);
+}
+
+__global__ __launch_bounds__(kThreads) void mark_visible_kernel(int P, const float* __restrict__ m,
+                                                                const float* __restrict__ view,
+                                                                uint8_t* __restrict__ present) {
+  const int idx = (int)(blockIdx.x * kThreads + threadIdx.x);
+  if (idx >= P) return;
+  const V3 pv = xform_point43(v3(m[3 * idx], m[3 * idx + 1], m[3 * idx + 2]), view);
+  present[idx] = !(pv.z <= 0.2f);
+}
+
+}  // namespace
+
+hipError_t launch_preprocess(const PreArgs& a, hipStream_t s) {
+  if (a.P == 0) return hipSuccess;
+  hipLaunchKernelGGL(preprocess_kernel, dim3((a.P + kThreads - 1) / kThreads), dim3(kThreads), 0,
+                     s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present,
+                               hipStream_t s) {
+  if (P == 0) return hipSuccess;
+  hipLaunchKernelGGL(mark_visible_kernel, dim3((P + kThreads - 1) / kThreads), dim3(kThreads), 0,
+                     s, P, means3D, view, present);
+  return hipGetLastError();
+}
+
+}  // namespace gsr

@@ -1,0 +1,285 @@
+"""MI355X drop-in for the `diff_gaussian_rasterization` package.
+
+Mirrors the Python surface of submodules/diff-gaussian-rasterization/diff_gaussian_rasterization/
+__init__.py (GaussianRasterizationSettings :157-169, GaussianRasterizer :171-220,
+_RasterizeGaussians :44-155) in its *extended* form -- the one gaussian_renderer/__init__.py:228-243
+and :315-326 actually calls (include_feature / confidence settings, shs_language /
+language_feature_precomp inputs, five outputs image/depth/alpha/feature/radii).
+The native side is libgsr.so (include/gsr.h), hand-written HIP for gfx950; there is no CPU path.
+"""
+from __future__ import annotations
+
+import os
+import sys
+from typing import NamedTuple, Optional
+
+import torch
+import torch.nn as nn
+
+_PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if _PKG_ROOT not in sys.path:
+    sys.path.insert(0, _PKG_ROOT)
+
+from gsr_amd import _lib  # noqa: E402
+
+__all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians",
+           "rasterize_gaussians_extended", "mark_visible"]
+
+
+def cpu_deep_copy_tuple(input_tuple):
+    # diff_gaussian_rasterization/__init__.py:17-19
+    return tuple(item.cpu().clone() if isinstance(item, torch.Tensor) else item for item in input_tuple)
+
+
+def _opt(t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+    """None or an empty tensor (the reference's torch.Tensor([]) placeholder) -> None."""
+    if t is None or (isinstance(t, torch.Tensor) and t.numel() == 0):
+        return None
+    return t
+
+
+def _dev_f32(t: Optional[torch.Tensor], name: str, device) -> Optional[torch.Tensor]:
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise RuntimeError(f"{name} must be a tensor on the HIP device (got {t.device}); "
+                           "libgsr has no CPU path")
+    if t.device != device:
+        raise RuntimeError(f"{name} is on {t.device}, expected {device}")
+    if t.dtype != torch.float32:
+        t = t.float()
+    return t.contiguous()
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else t.data_ptr()
+
+
+def rasterize_gaussians(means3D, means2D, sh, colors_precomp, opacities, scales, rotations,
+                        cov3Ds_precomp, raster_settings):
+    """Vendored 2-output entry point (diff_gaussian_rasterization/__init__.py:21-42): (color, radii)."""
+    color, _depth, _alpha, _feature, radii = _RasterizeGaussians.apply(
+        means3D, means2D, sh, None, colors_precomp, None, opacities, scales, rotations,
+        cov3Ds_precomp, raster_settings)
+    return color, radii
+
+
+def rasterize_gaussians_extended(means3D, means2D, sh, sh_language, colors_precomp,
+                                 language_feature_precomp, opacities, scales, rotations,
+                                 cov3Ds_precomp, raster_settings):
+    """Extended entry point: (color, depth, alpha, feature, radii)."""
+    return _RasterizeGaussians.apply(means3D, means2D, sh, sh_language, colors_precomp,
+                                     language_feature_precomp, opacities, scales, rotations,
+                                     cov3Ds_precomp, raster_settings)
+
+
+class _RasterizeGaussians(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, means3D, means2D, sh, sh_language, colors_precomp, language_feature_precomp,
+                opacities, scales, rotations, cov3Ds_precomp, raster_settings):
+        rs = raster_settings
+        if means3D.ndim != 2 or means3D.shape[1] != 3:
+            raise RuntimeError("means3D must have dimensions (num_points, 3)")
+        dev = means3D.device
+        P = int(means3D.shape[0])
+        H, W = int(rs.image_height), int(rs.image_width)
+        include_feature = bool(getattr(rs, "include_feature", False))
+
+        m3 = _dev_f32(means3D, "means3D", dev)
+        shs = _dev_f32(_opt(sh), "shs", dev)
+        shl = _dev_f32(_opt(sh_language), "shs_language", dev) if include_feature else None
+        col = _dev_f32(_opt(colors_precomp), "colors_precomp", dev)
+        lfp = _dev_f32(_opt(language_feature_precomp), "language_feature_precomp", dev) if include_feature else None
+        if lfp is not None:
+            shl = None  # precomputed features take precedence over in-kernel evaluation
+        op = _dev_f32(opacities, "opacities", dev)
+        sc = _dev_f32(_opt(scales), "scales", dev)
+        rot = _dev_f32(_opt(rotations), "rotations", dev)
+        cov = _dev_f32(_opt(cov3Ds_precomp), "cov3D_precomp", dev)
+        conf = _opt(getattr(rs, "confidence", None))
+        conf = _dev_f32(conf, "confidence", dev)
+        bg = _dev_f32(rs.bg, "bg", dev)
+        view = _dev_f32(rs.viewmatrix, "viewmatrix", dev)
+        proj = _dev_f32(rs.projmatrix, "projmatrix", dev)
+        campos = _dev_f32(rs.campos, "campos", dev)
+        M = int(shs.shape[1]) if shs is not None and shs.ndim >= 2 else 0
+        if shs is not None and shs.ndim == 2:  # [P, 3*M] flat layout
+            M = shs.shape[1] // 3
+
+        fopts = dict(dtype=torch.float32, device=dev)
+        color = torch.empty((3, H, W), **fopts)
+        depth = torch.empty((1, H, W), **fopts)
+        alpha = torch.empty((1, H, W), **fopts)
+        feature = torch.empty((3, H, W), **fopts)
+        radii = torch.empty((P,), dtype=torch.int32, device=dev)
+        holder = _lib.BufferHolder(dev)
+        L = _lib.load()
+        nr = _lib.ctypes.c_int(0)
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        args = (P, M, _ptr(bg), _ptr(m3), _ptr(col), _ptr(op), _ptr(sc), _ptr(rot),
+                float(rs.scale_modifier), _ptr(cov), _ptr(view), _ptr(proj), float(rs.tanfovx),
+                float(rs.tanfovy), H, W, _ptr(shs), int(rs.sh_degree), _ptr(campos),
+                int(bool(rs.prefiltered)), _ptr(shl), _ptr(lfp), _ptr(conf), int(include_feature),
+                _ptr(color), _ptr(depth), _ptr(alpha), _ptr(feature), _ptr(radii),
+                _lib.ctypes.byref(nr), _lib.alloc_callback(), holder.key, stream,
+                int(bool(rs.debug)))
+        try:
+            with torch.cuda.device(dev):
+                rc = L.gsr_rasterize_gaussians(*args)
+            _lib.check(rc)
+        except Exception:
+            if rs.debug:
+                cpu_args = cpu_deep_copy_tuple((rs.bg, means3D, colors_precomp, opacities, scales,
+                                                rotations, rs.scale_modifier, cov3Ds_precomp,
+                                                rs.viewmatrix, rs.projmatrix, rs.tanfovx,
+                                                rs.tanfovy, H, W, sh, rs.sh_degree, rs.campos,
+                                                rs.prefiltered, rs.debug))
+                torch.save(cpu_args, "snapshot_fw.dump")
+                print("\nAn error occured in forward. Please forward snapshot_fw.dump for debugging.")
+            raise
+        finally:
+            holder.release()
+        num_rendered = int(nr.value)
+
+        ctx.raster_settings = rs
+        ctx.num_rendered = num_rendered
+        ctx.meta = dict(P=P, M=M, H=H, W=W, include_feature=include_feature,
+                        has_shs=shs is not None, has_shl=shl is not None,
+                        has_col=col is not None, has_lfp=lfp is not None,
+                        has_sc=sc is not None, has_cov=cov is not None,
+                        op_shape=tuple(opacities.shape))
+        empty = torch.empty(0, device=dev)
+        geom, binning, image = (b if b is not None else torch.empty(0, dtype=torch.uint8, device=dev)
+                                for b in holder.bufs)
+        ctx.save_for_backward(m3, radii, shs if shs is not None else empty,
+                              shl if shl is not None else empty, col if col is not None else empty,
+                              lfp if lfp is not None else empty, sc if sc is not None else empty,
+                              rot if rot is not None else empty, cov if cov is not None else empty,
+                              conf if conf is not None else empty, bg, view, proj, campos,
+                              geom, binning, image)
+        ctx.mark_non_differentiable(radii)
+        return color, depth, alpha, feature, radii
+
+    @staticmethod
+    def backward(ctx, grad_color, grad_depth, grad_alpha, grad_feature, _grad_radii):
+        rs = ctx.raster_settings
+        mt = ctx.meta
+        (m3, radii, shs, shl, col, lfp, sc, rot, cov, conf, bg, view, proj, campos, geom, binning,
+         image) = ctx.saved_tensors
+        o = lambda t, flag: t if flag else None  # noqa: E731
+        shs, shl, col, lfp = o(shs, mt["has_shs"]), o(shl, mt["has_shl"]), o(col, mt["has_col"]), o(lfp, mt["has_lfp"])
+        sc, rot, cov = o(sc, mt["has_sc"]), o(rot, mt["has_sc"]), o(cov, mt["has_cov"])
+        conf = conf if conf.numel() > 0 else None
+        P, M, H, W = mt["P"], mt["M"], mt["H"], mt["W"]
+        dev = m3.device
+
+        def g(t):
+            return None if t is None else t.contiguous().float()
+
+        dcol = g(grad_color)
+        if dcol is None:
+            dcol = torch.zeros((3, H, W), dtype=torch.float32, device=dev)
+        ddep, dalp = g(grad_depth), g(grad_alpha)
+        dfeat = g(grad_feature) if mt["include_feature"] else None
+
+        fopts = dict(dtype=torch.float32, device=dev)
+        d_means2D = torch.empty((P, 3), **fopts)
+        d_colors = torch.empty((P, 3), **fopts) if col is not None else None
+        d_opac = torch.empty((P, 1), **fopts)
+        d_means3D = torch.empty((P, 3), **fopts)
+        d_cov = torch.empty((P, 6), **fopts) if cov is not None else None
+        d_sh = torch.empty((P, M, 3), **fopts) if shs is not None else None
+        d_sc = torch.empty((P, 3), **fopts) if sc is not None else None
+        d_rot = torch.empty((P, 4), **fopts) if sc is not None else None
+        d_shl = torch.empty((P, 3), **fopts) if shl is not None else None
+        d_lfp = torch.empty((P, 3), **fopts) if lfp is not None else None
+
+        L = _lib.load()
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        args = (P, M, ctx.num_rendered, _ptr(bg), _ptr(m3), _ptr(radii), _ptr(col), _ptr(sc),
+                _ptr(rot), float(rs.scale_modifier), _ptr(cov), _ptr(view), _ptr(proj),
+                float(rs.tanfovx), float(rs.tanfovy), H, W, _ptr(dcol), _ptr(ddep), _ptr(dalp),
+                _ptr(dfeat), _ptr(shs), int(rs.sh_degree), _ptr(campos), _ptr(shl), _ptr(lfp),
+                _ptr(conf), int(mt["include_feature"]), _ptr(geom) if geom.numel() else None,
+                _ptr(binning) if binning.numel() else None, _ptr(image) if image.numel() else None,
+                _ptr(d_means2D), _ptr(d_colors), _ptr(d_opac), _ptr(d_means3D), _ptr(d_cov),
+                _ptr(d_sh), _ptr(d_sc), _ptr(d_rot), _ptr(d_shl), _ptr(d_lfp), stream,
+                int(bool(rs.debug)))
+        try:
+            with torch.cuda.device(dev):
+                rc = L.gsr_rasterize_gaussians_backward(*args)
+            _lib.check(rc)
+        except Exception:
+            if rs.debug:
+                torch.save(cpu_deep_copy_tuple((rs.bg, m3, radii, col, sc, rot, rs.scale_modifier,
+                                                cov, rs.viewmatrix, rs.projmatrix, rs.tanfovx,
+                                                rs.tanfovy, grad_color, shs, rs.sh_degree,
+                                                rs.campos, geom, ctx.num_rendered, binning, image,
+                                                rs.debug)), "snapshot_bw.dump")
+                print("\nAn error occured in backward. Writing snapshot_bw.dump for debugging.\n")
+            raise
+        # order of forward inputs: means3D, means2D, sh, sh_language, colors_precomp,
+        # language_feature_precomp, opacities, scales, rotations, cov3Ds_precomp, raster_settings
+        d_opac = d_opac.view(mt["op_shape"])
+        return (d_means3D, d_means2D, d_sh, d_shl, d_colors, d_lfp, d_opac, d_sc, d_rot, d_cov, None)
+
+
+class GaussianRasterizationSettings(NamedTuple):
+    # vendored fields (diff_gaussian_rasterization/__init__.py:157-169)
+    image_height: int
+    image_width: int
+    tanfovx: float
+    tanfovy: float
+    bg: torch.Tensor
+    scale_modifier: float
+    viewmatrix: torch.Tensor
+    projmatrix: torch.Tensor
+    sh_degree: int
+    campos: torch.Tensor
+    prefiltered: bool
+    debug: bool = False
+    # extended fields used by gaussian_renderer/__init__.py:241-242
+    include_feature: bool = False
+    confidence: Optional[torch.Tensor] = None
+
+
+class GaussianRasterizer(nn.Module):
+    def __init__(self, raster_settings):
+        super().__init__()
+        self.raster_settings = raster_settings
+
+    def markVisible(self, positions):
+        # diff_gaussian_rasterization/__init__.py:176-185
+        with torch.no_grad():
+            rs = self.raster_settings
+            return mark_visible(positions, rs.viewmatrix, rs.projmatrix)
+
+    def forward(self, means3D, means2D, opacities, shs=None, colors_precomp=None, scales=None,
+                rotations=None, cov3D_precomp=None, shs_language=None,
+                language_feature_precomp=None):
+        rs = self.raster_settings
+        # argument checks of diff_gaussian_rasterization/__init__.py:191-195
+        if (shs is None and colors_precomp is None) or (shs is not None and colors_precomp is not None):
+            raise Exception('Please provide excatly one of either SHs or precomputed colors!')
+        if ((scales is None or rotations is None) and cov3D_precomp is None) or \
+                ((scales is not None or rotations is not None) and cov3D_precomp is not None):
+            raise Exception('Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!')
+        return rasterize_gaussians_extended(means3D, means2D, shs, shs_language, colors_precomp,
+                                            language_feature_precomp, opacities, scales, rotations,
+                                            cov3D_precomp, rs)
+
+
+def mark_visible(positions, viewmatrix, projmatrix):
+    """_C.mark_visible (rasterize_points.cu:198-217): bool[P], view-space z > 0.2."""
+    dev = positions.device
+    m3 = _dev_f32(positions, "positions", dev)
+    view = _dev_f32(viewmatrix, "viewmatrix", dev)
+    proj = _dev_f32(projmatrix, "projmatrix", dev)
+    P = int(m3.shape[0])
+    present = torch.zeros((P,), dtype=torch.bool, device=dev)
+    if P:
+        with torch.cuda.device(dev):
+            _lib.check(_lib.load().gsr_mark_visible(P, _ptr(m3), _ptr(view), _ptr(proj),
+                                                   _ptr(present),
+                                                   torch.cuda.current_stream(dev).cuda_stream))
+    return present

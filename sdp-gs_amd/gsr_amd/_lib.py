@@ -1,0 +1,134 @@
+"""ctypes binding of libgsr.so (include/gsr.h), the hand-written gfx950 rasterizer.
+
+There is no CPU fallback: if the shared library is missing or the tensors are not on a HIP device
+the calls raise.  `import torch` happens first so that libgsr resolves libamdhip64.so.7 to the HIP
+runtime torch already loaded (same soname), which makes torch's hipStream_t valid here.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libgsr.so")
+
+_f = ctypes.c_float
+_i = ctypes.c_int
+_p = ctypes.c_void_p
+_sz = ctypes.c_size_t
+
+ALLOC_FN = ctypes.CFUNCTYPE(_p, _p, _sz, _i)
+
+_lib = None
+_lock = threading.Lock()
+
+
+class GsrError(RuntimeError):
+    pass
+
+
+def load():
+    """Load libgsr.so (raises ImportError with the build hint if it is absent)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"libgsr.so not found at {LIB_PATH}: build it with "
+                "`make -C sdp-gs_amd/csrc` or `python -c 'import __graft_entry__ as g; g.build()'`")
+        L = ctypes.CDLL(LIB_PATH)
+        L.gsr_abi_version.restype = _i
+        L.gsr_abi_version.argtypes = []
+        L.gsr_last_error.restype = ctypes.c_char_p
+        L.gsr_last_error.argtypes = []
+        L.gsr_rasterize_gaussians.restype = _i
+        L.gsr_rasterize_gaussians.argtypes = [
+            _i, _i,                      # P, M
+            _p, _p, _p, _p, _p, _p, _f,  # bg, means3D, colors, opacities, scales, rotations, scale_mod
+            _p, _p, _p,                  # cov3D_precomp, view, proj
+            _f, _f, _i, _i,              # tanfovx, tanfovy, H, W
+            _p, _i, _p, _i,              # sh, degree, campos, prefiltered
+            _p, _p, _p, _i,              # sh_language, lang_precomp, confidence, include_feature
+            _p, _p, _p, _p, _p,          # out_color, out_depth, out_alpha, out_feature, radii
+            ctypes.POINTER(_i),          # num_rendered
+            ALLOC_FN, _p,                # alloc, alloc_ctx
+            _p, _i]                      # stream, debug
+        L.gsr_rasterize_gaussians_backward.restype = _i
+        L.gsr_rasterize_gaussians_backward.argtypes = [
+            _i, _i, _i,                  # P, M, R
+            _p, _p, _p, _p,              # bg, means3D, radii, colors
+            _p, _p, _f, _p,              # scales, rotations, scale_mod, cov3D_precomp
+            _p, _p, _f, _f, _i, _i,      # view, proj, tanfovx, tanfovy, H, W
+            _p, _p, _p, _p,              # dL_dcolor, dL_ddepth, dL_dalpha, dL_dfeature
+            _p, _i, _p,                  # sh, degree, campos
+            _p, _p, _p, _i,              # sh_language, lang_precomp, confidence, include_feature
+            _p, _p, _p,                  # geom, binning, image buffers
+            _p, _p, _p, _p, _p, _p, _p, _p, _p, _p,  # grads
+            _p, _i]                      # stream, debug
+        L.gsr_mark_visible.restype = _i
+        L.gsr_mark_visible.argtypes = [_i, _p, _p, _p, _p, _p]
+        for n in ("gsr_geom_buffer_bytes", "gsr_binning_buffer_bytes"):
+            getattr(L, n).restype = _sz
+            getattr(L, n).argtypes = [_i]
+        L.gsr_image_buffer_bytes.restype = _sz
+        L.gsr_image_buffer_bytes.argtypes = [_i, _i]
+        _lib = L
+    return _lib
+
+
+def check(rc: int):
+    if rc != 0:
+        msg = load().gsr_last_error().decode(errors="replace")
+        raise GsrError(f"libgsr error {rc}: {msg}")
+
+
+# --- allocator callback: the library asks for its three scratch buffers through it ---------------
+_holders: dict[int, "BufferHolder"] = {}
+_holder_lock = threading.Lock()
+_holder_seq = [0]
+
+
+class BufferHolder:
+    """Owns the geometry / binning / image byte tensors of one forward (the reference keeps the
+    same three tensors in the autograd context, diff_gaussian_rasterization/__init__.py:97)."""
+
+    def __init__(self, device: torch.device):
+        self.device = device
+        self.bufs = [None, None, None]
+        with _holder_lock:
+            _holder_seq[0] += 1
+            self.key = _holder_seq[0]
+            _holders[self.key] = self
+
+    def release(self):
+        with _holder_lock:
+            _holders.pop(self.key, None)
+
+    def ptr(self, which: int):
+        b = self.bufs[which]
+        return None if b is None else b.data_ptr()
+
+
+def _alloc_cb(ctx, nbytes, which):
+    h = _holders.get(int(ctx or 0))
+    if h is None:
+        return None
+    try:
+        t = torch.empty((max(int(nbytes), 1),), dtype=torch.uint8, device=h.device)
+    except Exception:  # out of memory: the library reports GSR_ERR_ALLOC
+        return None
+    h.bufs[which] = t
+    return t.data_ptr()
+
+
+_ALLOC_CB = ALLOC_FN(_alloc_cb)
+
+
+def alloc_callback():
+    return _ALLOC_CB
