@@ -1,0 +1,259 @@
+#!/usr/bin/env python3
+"""Benchmark: rasterized views/sec (fwd+bwd) of the MI355X Gaussian rasterizer.
+
+Workload (BASELINE.json configs[2] at N=1, configs[3] at N=8): 1,000,000 synthetic Gaussians
+(SH degree 3 evaluated in-kernel, language features on), LLFF-style cameras at 1008x756, and
+`--views-per-gpu` (default 6) camera views per GPU per step.  One step = for each of this rank's
+views: render() (activations + rasterizer forward with colour/depth/alpha/feature outputs) and the
+backward of fixed synthetic upstream gradients, accumulating per-Gaussian gradients; then, with
+N > 1, one bucketed SUM all-reduce of all gradients over RCCL.  Weak scaling: views per GPU fixed.
+
+    python bench.py --gpus N --steps K --warmup W
+
+Prints ONE JSON line on rank 0 (see DESIGN.md section 7 for the roofline byte model).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import platform
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "sdp-gs_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md chip table (spec)
+FP32_PEAK_TFLOPS = 157.3  # vector FP32 (spec)
+
+WORKLOADS = {
+    # name: (P, W, H, sh_degree)
+    "llff_1m_1008x756": (1_000_000, 1008, 756, 3),
+    "cfg2_100k_800x800": (100_000, 800, 800, 3),
+    "cfg5_5m_1920x1080": (5_000_000, 1920, 1080, 3),
+}
+
+
+class Pipe:
+    convert_SHs_python = False   # colour from SH inside the HIP preprocess (the rasterizer's work)
+    compute_cov3D_python = False
+    debug = False
+    use_confidence = False
+
+
+class Opt:
+    include_feature = True
+
+
+def algorithmic_bytes(stage, P, Pv, R, T, HW, D=3, C=8, tile_passes=2):
+    """Bytes each stage must move per launch."""
+    sh = 12 * (D + 1) ** 2
+    return {
+        "preprocess": P * 12 + Pv * (12 + 16 + 4 + sh + 12) + P * 16 + Pv * (64 + 24 + 4 + 1),
+        "depth_sort": 4 * P * 20,
+        "scan": P * 12,
+        "duplicate": P * 12 + Pv * 16 + R * 8,
+        "tile_sort": tile_passes * R * 20,
+        "ranges": R * 4 + T * 8,
+        "render_fwd": R * (4 + 8 + 16 + 4 * (C - 1)) + T * 8 + HW * (4 * C + 8),
+        "acc_zero": P * 64,
+        "render_bwd": R * (4 + 8 + 16 + 4 * C) + HW * (4 * C + 8) + Pv * 64,
+        "preprocess_bwd": Pv * (12 + 24 + 16 + 12 + sh + 64 + 12 + 1 + 4)
+                          + P * (12 + 4 + 12 + sh + 12 + 16 + 12),
+    }[stage]
+
+
+# per (pixel, splat) pair FLOP model of the blend kernels
+FLOP_PER_PAIR = {"render_fwd": 45.0, "render_bwd": 110.0}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", default="llff_1m_1008x756", choices=sorted(WORKLOADS))
+    ap.add_argument("--views-per-gpu", type=int, default=6)
+    ap.add_argument("--cpu-baseline-views", type=int, default=2)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-stage-timing", action="store_true")
+    ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_r01.json"))
+    args = ap.parse_args()
+
+    from gsr_amd import _lib
+    from gsr_amd.model import SplatModel
+    from gsr_amd.parallel import GradAllReducer, init_from_env, shard_views
+    from gsr_amd.synthetic import make_cameras, make_gaussians, upstream_grads
+    import diff_gaussian_rasterization as dgr
+    from gaussian_renderer import render
+
+    rank, world, local = init_from_env("nccl")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    P, W, H, deg = WORKLOADS[args.workload]
+
+    params = make_gaussians(P, sh_degree=deg, seed=0)
+    model = SplatModel(params, device=dev)
+    n_views = args.views_per_gpu * world
+    cams_all = make_cameras(n_views, W, H, seed=0)
+    my_cams = [cams_all[i].to(dev) for i in shard_views(n_views, rank, world)]
+    dimg, ddep, dfeat = upstream_grads(H, W, seed=1, device=dev)
+    bg = torch.zeros(3, device=dev)
+    reducer = GradAllReducer(model.parameters()) if world > 1 else None
+    pipe, opt = Pipe(), Opt()
+    stats = {"R": [], "Pv": []}
+
+    def step(record=False):
+        for p in model.parameters():
+            p.grad = None
+        for cam in my_cams:
+            pkg = render(cam, model, pipe, bg, opt)
+            torch.autograd.backward([pkg["render"], pkg["depth"], pkg["feature"]],
+                                    [dimg, ddep, dfeat])
+            if record:
+                stats["R"].append(dgr.LAST_STATS["num_rendered"])
+                stats["Pv"].append(int(pkg["visibility_filter"].sum()))
+        if reducer is not None:
+            reducer.allreduce()
+
+    for _ in range(args.warmup):
+        step()
+    step(record=True)  # one recorded step for the per-view statistics (not timed)
+    timer = _lib.StageTimer()
+    timer.reset()
+    if not args.no_stage_timing:
+        timer.enable(True)
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    timer.enable(False)
+    stages = timer.collect() if not args.no_stage_timing else {}
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    total_views = args.steps * n_views
+    value = total_views / elapsed
+    ms_per_step = 1000.0 * elapsed / args.steps
+
+    R = float(np.mean(stats["R"]))
+    Pv = float(np.mean(stats["Pv"]))
+    T = ((W + 15) // 16) * ((H + 15) // 16)
+    HW = W * H
+    kernels = {}
+    for name, (ms, calls) in stages.items():
+        if calls == 0:
+            continue
+        avg_ms = ms / calls
+        b = algorithmic_bytes(name, P, Pv, R, T, HW, D=deg)
+        k = {"avg_ms": round(avg_ms, 4), "calls": int(calls), "bytes": int(b),
+             "gbs": round(b / (avg_ms * 1e-3) / 1e9, 1)}
+        if name in FLOP_PER_PAIR:
+            pairs = 256.0 * R  # every splat instance is evaluated by the 256 pixels of its tile
+            k["pair_evals_per_s"] = round(pairs / (avg_ms * 1e-3) / 1e9, 2)
+            k["tflops_est"] = round(pairs * FLOP_PER_PAIR[name] / (avg_ms * 1e-3) / 1e12, 2)
+        kernels[name] = k
+    roofline = None
+    if kernels:
+        dom = max(kernels, key=lambda n: kernels[n]["avg_ms"] * kernels[n]["calls"])
+        kd = kernels[dom]
+        achieved = kd["gbs"]
+        traffic = None
+        try:
+            with open(args.pmc_file) as fh:
+                pmc = json.load(fh)
+            if pmc.get("workload") == args.workload and dom in pmc.get("kernels", {}):
+                traffic = pmc["kernels"][dom].get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            pass
+        roofline = {"kernel": dom, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                    "algorithmic_bytes": kd["bytes"], "avg_ms": kd["avg_ms"]}
+        if "tflops_est" in kd:
+            roofline["valu"] = {"achieved_tflops": kd["tflops_est"], "peak_tflops": FP32_PEAK_TFLOPS,
+                                "frac": round(kd["tflops_est"] / FP32_PEAK_TFLOPS, 4)}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_baseline_views > 0:
+        cpu = cpu_baseline(model, cams_all[: args.cpu_baseline_views], dimg, ddep, dfeat, deg)
+
+    if rank == 0:
+        line = {
+            "metric": "rasterized views/sec (fwd+bwd)",
+            "value": round(value, 3),
+            "unit": "views/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic (seeded Gaussians + LLFF-style cameras, SURVEY.md 8(d))",
+            "config": {"workload": args.workload, "gaussians": P, "width": W, "height": H,
+                       "sh_degree": deg, "views_per_gpu": args.views_per_gpu,
+                       "views_per_step": n_views, "outputs": "rgb+depth+alpha+feature",
+                       "parallelism": f"camera-sharded dp{world}",
+                       "num_rendered_mean": int(R), "visible_mean": int(Pv), "tiles": T},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "kernels": kernels,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(model, cams, dimg, ddep, dfeat, deg):
+    """The CPU restatement (oracle/, single-threaded C) on a bounded sample of the same workload:
+    `len(cams)` full views (forward + backward).  Rank 0 at N = 1 only."""
+    try:
+        from oracle.oracle import OracleRaster, build
+        build()
+    except Exception as exc:  # pragma: no cover - reported, not fatal
+        return {"value": None, "error": repr(exc)[:200]}
+    with torch.no_grad():
+        xyz = model.get_xyz.detach().cpu().numpy()
+        kw_common = dict(
+            means3D=xyz, opacities=model.get_opacity.detach().cpu().numpy(),
+            shs=model.get_features.detach().cpu().numpy(), sh_degree=deg,
+            scales=model.get_scaling.detach().cpu().numpy(),
+            rotations=model.get_rotation.detach().cpu().numpy(),
+            shs_language=model.get_language_feature.detach().cpu().numpy(), include_feature=True,
+            bg=np.zeros(3, np.float32))
+        dimg_n, ddep_n, dfeat_n = (t.detach().cpu().numpy() for t in (dimg, ddep, dfeat))
+    t0 = time.perf_counter()
+    for cam in cams:
+        orc = OracleRaster(viewmatrix=cam.world_view_transform.cpu().numpy(),
+                           projmatrix=cam.full_proj_transform.cpu().numpy(),
+                           campos=cam.camera_center.cpu().numpy(),
+                           tanfovx=math.tan(cam.FoVx * 0.5), tanfovy=math.tan(cam.FoVy * 0.5),
+                           image_height=cam.image_height, image_width=cam.image_width, **kw_common)
+        orc.backward(dimg_n, ddep_n, None, dfeat_n)
+        del orc
+    dt = time.perf_counter() - t0
+    return {"value": round(len(cams) / dt, 4), "unit": "views/s", "cores": 1, "kind": "port",
+            "sample": f"{len(cams)} full views (fwd+bwd) of the same workload on the oracle "
+                      f"(single-threaded C restatement), {dt:.1f} s",
+            "cpu": platform.processor() or platform.machine()}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,47 @@
+/*
+ * gsr_testing.h -- test hooks of libgsr (NOT part of the drop-in boundary in gsr.h).
+ *
+ * They expose the device-wide primitives that replace the reference's CUB calls
+ * (cub::DeviceScan::InclusiveSum, rasterizer_impl.cu:277; cub::DeviceRadixSort::SortPairs,
+ * :303-308) so that tests/ can check sortedness, stability and prefix sums at full size.
+ */
+#ifndef GSR_TESTING_H
+#define GSR_TESTING_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Scratch bytes needed by gsr_test_radix_sort_pairs for n pairs. */
+size_t gsr_test_sort_scratch_bytes(size_t n);
+/* Stable LSD radix sort of (keys, vals) over key bits [0, bits), in place (device pointers). */
+int gsr_test_radix_sort_pairs(uint32_t* keys, uint32_t* vals, size_t n, int bits, void* scratch,
+                              void* stream);
+/* Scratch bytes needed by gsr_test_scan for n elements. */
+size_t gsr_test_scan_scratch_bytes(size_t n);
+/* out = inclusive (or exclusive) prefix sum of in (device pointers). */
+int gsr_test_scan(const uint32_t* in, uint32_t* out, size_t n, int inclusive, void* scratch,
+                  void* stream);
+
+/* Stage timing with hipEvents recorded on the caller's stream around every kernel of the forward
+ * and backward (used by bench.py for the per-kernel roofline).  Off by default; when on, each
+ * stage launch is bracketed by two events, which costs a few microseconds per view. */
+enum {
+  GSR_STAGE_PREPROCESS = 0, GSR_STAGE_DEPTH_SORT, GSR_STAGE_SCAN, GSR_STAGE_DUPLICATE,
+  GSR_STAGE_TILE_SORT, GSR_STAGE_RANGES, GSR_STAGE_RENDER_FWD, GSR_STAGE_ACC_ZERO,
+  GSR_STAGE_RENDER_BWD, GSR_STAGE_PREPROCESS_BWD, GSR_NUM_STAGES
+};
+void gsr_profile_enable(int on);
+/* Waits for the recorded events, adds their durations into ms[GSR_NUM_STAGES] and
+ * calls[GSR_NUM_STAGES] (accumulating since the last reset) and recycles the events. */
+int gsr_profile_collect(double* ms, long long* calls);
+void gsr_profile_reset(void);
+const char* gsr_profile_stage_name(int stage);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GSR_TESTING_H */

@@ -8,12 +8,16 @@
 //   fused per-Gaussian backward.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <string>
+#include <vector>
 
 #include "../../include/gsr.h"
+#include "../../include/gsr_testing.h"
 #include "gsr_internal.h"
 
 namespace gsr {
@@ -114,6 +118,53 @@ uint32_t* pinned_slot() {
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
+// ---- optional per-stage hipEvent timing (include/gsr_testing.h) ----------------------------------
+struct Profiler {
+  std::mutex mu;
+  std::atomic<bool> on{false};
+  std::vector<hipEvent_t> pool;
+  struct Rec { int stage; hipEvent_t a, b; };
+  std::vector<Rec> pending;
+  double ms[GSR_NUM_STAGES] = {0};
+  long long calls[GSR_NUM_STAGES] = {0};
+};
+Profiler& prof() {
+  static Profiler p;
+  return p;
+}
+hipEvent_t prof_take() {
+  Profiler& p = prof();
+  std::lock_guard<std::mutex> g(p.mu);
+  if (!p.pool.empty()) {
+    hipEvent_t e = p.pool.back();
+    p.pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+hipEvent_t prof_begin(hipStream_t s) {
+  if (!prof().on.load(std::memory_order_relaxed)) return nullptr;
+  hipEvent_t a = prof_take();
+  if (a && hipEventRecord(a, s) != hipSuccess) return nullptr;
+  return a;
+}
+void prof_end(int stage, hipEvent_t a, hipStream_t s) {
+  if (!a) return;
+  hipEvent_t b = prof_take();
+  if (!b || hipEventRecord(b, s) != hipSuccess) return;
+  Profiler& p = prof();
+  std::lock_guard<std::mutex> g(p.mu);
+  p.pending.push_back({stage, a, b});
+}
+#define PROF_BEGIN(st) hipEvent_t prof_ev_##st = prof_begin(stream)
+#define PROF_END(st) prof_end(GSR_STAGE_##st, prof_ev_##st, stream)
+
+const char* kStageNames[GSR_NUM_STAGES] = {"preprocess", "depth_sort", "scan", "duplicate",
+                                          "tile_sort", "ranges", "render_fwd", "acc_zero",
+                                          "render_bwd", "preprocess_bwd"};
+
 }  // namespace
 
 extern "C" {
@@ -198,13 +249,19 @@ int gsr_rasterize_gaussians(int P, int M, const float* background, const float* 
   pa.fx = (float)W / (2.0f * tan_fovx);
   pa.prefiltered = prefiltered; pa.include_feature = include_feature;
   pa.radii = radii_ptr; pa.g = g;
+  PROF_BEGIN(PREPROCESS);
   GSR_CHECK(launch_preprocess(pa, stream));
+  PROF_END(PREPROCESS);
 
   bool in_b = false;
+  PROF_BEGIN(DEPTH_SORT);
   GSR_CHECK(radix_sort_pairs(g.dkey_a, g.dval_a, g.dkey_b, g.dval_b, (size_t)P, 32,
                              SortScratch{g.sort_hist, g.sort_parts}, &in_b, stream));
+  PROF_END(DEPTH_SORT);
   const uint32_t* order = in_b ? g.dval_b : g.dval_a;
+  PROF_BEGIN(SCAN);
   GSR_CHECK(scan_u32(g.tiles_touched, order, g.offsets, (size_t)P, true, g.scan_parts, stream));
+  PROF_END(SCAN);
 
   uint32_t* host = pinned_slot();
   if (!host) return fail(GSR_ERR_HIP, "pinned host allocation failed");
@@ -222,13 +279,19 @@ int gsr_rasterize_gaussians(int P, int M, const float* background, const float* 
   if (!bbase) return fail(GSR_ERR_ALLOC, "binning buffer allocation of %zu bytes failed", bbytes);
   BinState b = carve_bin(bbase, R);
 
+  PROF_BEGIN(DUPLICATE);
   GSR_CHECK(launch_duplicate(P, order, g.offsets, radii_ptr, g.rec, gx, gy, b.tkey_a, b.tval_a, stream));
+  PROF_END(DUPLICATE);
   bool t_in_b = false;
+  PROF_BEGIN(TILE_SORT);
   GSR_CHECK(radix_sort_pairs(b.tkey_a, b.tval_a, b.tkey_b, b.tval_b, R, tile_bits(ntiles),
                              SortScratch{b.hist, b.parts}, &t_in_b, stream));
+  PROF_END(TILE_SORT);
   const uint32_t* tiles_sorted = t_in_b ? b.tkey_b : b.tkey_a;
   const uint32_t* point_list = t_in_b ? b.tval_b : b.tval_a;
+  PROF_BEGIN(RANGES);
   GSR_CHECK(launch_tile_ranges(R, tiles_sorted, im.ranges, ntiles, stream));
+  PROF_END(RANGES);
 
   RenderArgs ra{};
   ra.W = W; ra.H = H; ra.gx = gx; ra.gy = gy;
@@ -236,7 +299,9 @@ int gsr_rasterize_gaussians(int P, int M, const float* background, const float* 
   ra.final_T = im.final_T; ra.n_contrib = im.n_contrib; ra.tile_last = im.tile_last;
   ra.out_color = out_color; ra.out_depth = out_depth; ra.out_alpha = out_alpha;
   ra.out_feature = out_feature; ra.include_feature = include_feature;
+  PROF_BEGIN(RENDER_FWD);
   GSR_CHECK(launch_render_forward(ra, stream));
+  PROF_END(RENDER_FWD);
   *num_rendered = (int)R;
   return GSR_OK;
 }
@@ -281,7 +346,9 @@ int gsr_rasterize_gaussians_backward(
   const uint32_t* point_list = (passes & 1) ? b.tval_b : b.tval_a;
   const int32_t* radii_ptr = radii ? radii : g.radii;
 
+  PROF_BEGIN(ACC_ZERO);
   GSR_CHECK(hipMemsetAsync(g.acc, 0, sizeof(float) * kAccFloats * (size_t)P, stream));
+  PROF_END(ACC_ZERO);
   if (R > 0) {
     RenderBwdArgs rb{};
     rb.W = W; rb.H = H; rb.gx = gx; rb.gy = gy;
@@ -289,7 +356,9 @@ int gsr_rasterize_gaussians_backward(
     rb.final_T = im.final_T; rb.n_contrib = im.n_contrib; rb.tile_last = im.tile_last;
     rb.dL_dcolor = dL_dout_color; rb.dL_ddepth = dL_dout_depth; rb.dL_dalpha = dL_dout_alpha;
     rb.dL_dfeature = dL_dout_feature; rb.acc = g.acc; rb.include_feature = include_feature;
+    PROF_BEGIN(RENDER_BWD);
     GSR_CHECK(launch_render_backward(rb, stream));
+    PROF_END(RENDER_BWD);
   }
   BwdPreArgs ba{};
   ba.P = P; ba.D = degree; ba.M = M;
@@ -307,8 +376,100 @@ int gsr_rasterize_gaussians_backward(
   ba.dL_dmeans3D = dL_dmeans3D; ba.dL_dcov3D = dL_dcov3D; ba.dL_dsh = sh ? dL_dsh : nullptr;
   ba.dL_dscales = scales ? dL_dscales : nullptr; ba.dL_drotations = scales ? dL_drotations : nullptr;
   ba.dL_dsh_language = dL_dsh_language; ba.dL_dlanguage_feature = dL_dlanguage_feature;
+  PROF_BEGIN(PREPROCESS_BWD);
   GSR_CHECK(launch_preprocess_backward(ba, stream));
+  PROF_END(PREPROCESS_BWD);
   return GSR_OK;
+}
+
+// ---- test hooks (include/gsr_testing.h) -----------------------------------------------------------
+static size_t sort_scratch_layout(char* base, size_t n, uint32_t** kb, uint32_t** vb,
+                                  SortScratch* sc) {
+  Carver c(base);
+  uint32_t* a = c.take<uint32_t>(n);
+  uint32_t* b = c.take<uint32_t>(n);
+  uint32_t* h = c.take<uint32_t>(sort_hist_len(n));
+  uint32_t* p = c.take<uint32_t>(scan_parts(sort_hist_len(n)) + 1);
+  if (kb) *kb = a;
+  if (vb) *vb = b;
+  if (sc) *sc = SortScratch{h, p};
+  return c.size();
+}
+
+size_t gsr_test_sort_scratch_bytes(size_t n) {
+  return sort_scratch_layout(nullptr, n, nullptr, nullptr, nullptr);
+}
+
+int gsr_test_radix_sort_pairs(uint32_t* keys, uint32_t* vals, size_t n, int bits, void* scratch,
+                              void* stream_ptr) {
+  g_err.clear();
+  hipStream_t stream = (hipStream_t)stream_ptr;
+  const int debug = 0;
+  if (n == 0) return GSR_OK;
+  if (!keys || !vals || !scratch || bits < 0 || bits > 32) return fail(GSR_ERR_ARGUMENT, "bad args");
+  if (scan_parts(sort_hist_len(n)) > (size_t)kScanMaxParts) return fail(GSR_ERR_TOO_LARGE, "n too large");
+  uint32_t *kb, *vb;
+  SortScratch sc;
+  sort_scratch_layout((char*)scratch, n, &kb, &vb, &sc);
+  bool in_b = false;
+  GSR_CHECK(radix_sort_pairs(keys, vals, kb, vb, n, bits, sc, &in_b, stream));
+  if (in_b) {
+    GSR_CHECK(hipMemcpyAsync(keys, kb, n * 4, hipMemcpyDeviceToDevice, stream));
+    GSR_CHECK(hipMemcpyAsync(vals, vb, n * 4, hipMemcpyDeviceToDevice, stream));
+  }
+  return GSR_OK;
+}
+
+size_t gsr_test_scan_scratch_bytes(size_t n) { return align_up((scan_parts(n) + 1) * 4); }
+
+int gsr_test_scan(const uint32_t* in, uint32_t* out, size_t n, int inclusive, void* scratch,
+                  void* stream_ptr) {
+  g_err.clear();
+  hipStream_t stream = (hipStream_t)stream_ptr;
+  const int debug = 0;
+  if (n == 0) return GSR_OK;
+  if (scan_parts(n) > (size_t)kScanMaxParts) return fail(GSR_ERR_TOO_LARGE, "n too large");
+  GSR_CHECK(scan_u32(in, nullptr, out, n, inclusive != 0, (uint32_t*)scratch, stream));
+  return GSR_OK;
+}
+
+void gsr_profile_enable(int on) { prof().on.store(on != 0); }
+
+int gsr_profile_collect(double* ms, long long* calls) {
+  Profiler& p = prof();
+  std::vector<Profiler::Rec> recs;
+  {
+    std::lock_guard<std::mutex> g(p.mu);
+    recs.swap(p.pending);
+  }
+  int rc = GSR_OK;
+  for (auto& r : recs) {
+    float t = 0.f;
+    if (hipEventSynchronize(r.b) == hipSuccess && hipEventElapsedTime(&t, r.a, r.b) == hipSuccess) {
+      p.ms[r.stage] += t;
+      p.calls[r.stage] += 1;
+    } else {
+      rc = fail(GSR_ERR_HIP, "event timing failed");
+    }
+  }
+  std::lock_guard<std::mutex> g(p.mu);
+  for (auto& r : recs) { p.pool.push_back(r.a); p.pool.push_back(r.b); }
+  for (int i = 0; i < GSR_NUM_STAGES; i++) {
+    if (ms) ms[i] = p.ms[i];
+    if (calls) calls[i] = p.calls[i];
+  }
+  return rc;
+}
+
+void gsr_profile_reset(void) {
+  Profiler& p = prof();
+  gsr_profile_collect(nullptr, nullptr);
+  std::lock_guard<std::mutex> g(p.mu);
+  for (int i = 0; i < GSR_NUM_STAGES; i++) { p.ms[i] = 0; p.calls[i] = 0; }
+}
+
+const char* gsr_profile_stage_name(int stage) {
+  return (stage >= 0 && stage < GSR_NUM_STAGES) ? kStageNames[stage] : "";
 }
 
 int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,

@@ -172,9 +172,10 @@ __global__ __launch_bounds__(kThreads) void preprocess_bwd_kernel(BwdPreArgs a) 
 #pragma unroll
     for (int k = 0; k < 6; k++) dcov[k] = 0.0f;
   }
+  if (a.dL_dcov3D) {
 #pragma unroll
-  if (a.dL_dcov3D)
     for (int k = 0; k < 6; k++) a.dL_dcov3D[6 * i + k] = dcov[k];
+  }
   const float dL_dT00 = 2 * (Tm(0, 0) * Vk(0, 0) + Tm(0, 1) * Vk(0, 1) + Tm(0, 2) * Vk(0, 2)) * dL_da +
                         (Tm(1, 0) * Vk(0, 0) + Tm(1, 1) * Vk(0, 1) + Tm(1, 2) * Vk(0, 2)) * dL_db;
   const float dL_dT01 = 2 * (Tm(0, 0) * Vk(1, 0) + Tm(0, 1) * Vk(1, 1) + Tm(0, 2) * Vk(1, 2)) * dL_da +

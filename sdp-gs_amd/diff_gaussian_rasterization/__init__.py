@@ -25,6 +25,10 @@ from gsr_amd import _lib  # noqa: E402
 __all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians",
            "rasterize_gaussians_extended", "mark_visible"]
 
+# instance count of the most recent forward (the reference keeps it in ctx.num_rendered only);
+# read by bench.py to compute per-kernel algorithmic bytes
+LAST_STATS = {"num_rendered": 0, "P": 0}
+
 
 def cpu_deep_copy_tuple(input_tuple):
     # diff_gaussian_rasterization/__init__.py:17-19
@@ -140,6 +144,8 @@ class _RasterizeGaussians(torch.autograd.Function):
         finally:
             holder.release()
         num_rendered = int(nr.value)
+        LAST_STATS["num_rendered"] = num_rendered
+        LAST_STATS["P"] = P
 
         ctx.raster_settings = rs
         ctx.num_rendered = num_rendered

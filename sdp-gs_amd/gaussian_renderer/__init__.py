@@ -1,0 +1,113 @@
+"""Drop-in counterpart of gaussian_renderer/__init__.py::render() (:209-338), the caller of the hot
+path.  Same signature, same flag-driven input assembly (compute_cov3D_python, convert_SHs_python,
+use_confidence, opt.include_feature, override_color / override_language) and the same returned
+dict; the only deliberate difference is that screenspace_points follows the model's device
+instead of a hard-coded "cuda" (:217), so the function is device-agnostic.
+"""
+from __future__ import annotations
+
+import math
+import os
+import sys
+
+import torch
+
+_PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if _PKG_ROOT not in sys.path:
+    sys.path.insert(0, _PKG_ROOT)
+
+from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer  # noqa: E402
+from gsr_amd.sh import eval_sh  # noqa: E402
+
+
+def render(viewpoint_camera, pc, pipe, bg_color: torch.Tensor, opt, scaling_modifier=1.0,
+           override_color=None, override_language=None):
+    xyz = pc.get_xyz
+    screenspace_points = torch.zeros_like(xyz, dtype=xyz.dtype, requires_grad=True,
+                                          device=xyz.device) + 0
+    try:
+        screenspace_points.retain_grad()
+    except Exception:
+        pass
+
+    tanfovx = math.tan(viewpoint_camera.FoVx * 0.5)
+    tanfovy = math.tan(viewpoint_camera.FoVy * 0.5)
+    confidence = pc.confidence if pipe.use_confidence else torch.ones_like(pc.confidence)
+    raster_settings = GaussianRasterizationSettings(
+        image_height=int(viewpoint_camera.image_height),
+        image_width=int(viewpoint_camera.image_width),
+        tanfovx=tanfovx,
+        tanfovy=tanfovy,
+        bg=bg_color,
+        scale_modifier=scaling_modifier,
+        viewmatrix=viewpoint_camera.world_view_transform,
+        projmatrix=viewpoint_camera.full_proj_transform,
+        sh_degree=pc.active_sh_degree,
+        campos=viewpoint_camera.camera_center,
+        prefiltered=False,
+        include_feature=True,
+        confidence=confidence,
+        debug=pipe.debug)
+    rasterizer = GaussianRasterizer(raster_settings=raster_settings)
+
+    means3D = xyz
+    means2D = screenspace_points
+    opacity = pc.get_opacity
+
+    scales = rotations = cov3D_precomp = None
+    if pipe.compute_cov3D_python:
+        cov3D_precomp = pc.get_covariance(scaling_modifier)
+    else:
+        scales = pc.get_scaling
+        rotations = pc.get_rotation
+
+    shs = shs_language = colors_precomp = language_feature_precomp = None
+    if override_color is None:
+        if pipe.convert_SHs_python:
+            shs_view = pc.get_features.transpose(1, 2).view(-1, 3, (pc.max_sh_degree + 1) ** 2)
+            dir_pp = (xyz - viewpoint_camera.camera_center.repeat(pc.get_features.shape[0], 1))
+            dir_pp_normalized = dir_pp / dir_pp.norm(dim=1, keepdim=True)
+            sh2rgb = eval_sh(pc.active_sh_degree, shs_view, dir_pp_normalized)
+            colors_precomp = torch.clamp_min(sh2rgb + 0.5, 0.0)
+        else:
+            shs = pc.get_features
+    else:
+        colors_precomp = override_color
+
+    if opt.include_feature:
+        if override_language is None:
+            if pipe.convert_SHs_python:
+                lf = pc.get_language_feature
+                shs_view = lf.view(-1, 3, 1)
+                dir_pp = (xyz - viewpoint_camera.camera_center.repeat(lf.shape[0], 1))
+                dir_pp_normalized = dir_pp / dir_pp.norm(dim=1, keepdim=True)
+                sh2language = eval_sh(0, shs_view, dir_pp_normalized)
+                language_feature_precomp = sh2language / (sh2language.norm(dim=-1, keepdim=True) + 1e-9)
+            else:
+                shs_language = pc.get_language_feature
+        else:
+            language_feature_precomp = override_language
+    else:
+        language_feature_precomp = colors_precomp
+
+    rendered_image, rendered_depth, rendered_alpha, language_feature_image, radii = rasterizer(
+        means3D=means3D,
+        means2D=means2D,
+        shs=shs,
+        shs_language=shs_language,
+        colors_precomp=colors_precomp,
+        language_feature_precomp=language_feature_precomp,
+        opacities=opacity,
+        scales=scales,
+        rotations=rotations,
+        cov3D_precomp=cov3D_precomp)
+
+    return {"render": rendered_image,
+            "depth": rendered_depth,
+            "alpha": rendered_alpha,
+            "opacity": opacity,
+            "feature": language_feature_image,
+            "viewspace_points": screenspace_points,
+            "visibility_filter": radii > 0,
+            "radii": radii,
+            "color": colors_precomp}

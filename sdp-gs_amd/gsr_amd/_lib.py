@@ -78,6 +78,24 @@ def load():
             getattr(L, n).argtypes = [_i]
         L.gsr_image_buffer_bytes.restype = _sz
         L.gsr_image_buffer_bytes.argtypes = [_i, _i]
+        # test hooks (include/gsr_testing.h); every pointer is typed so ctypes never truncates it
+        L.gsr_test_sort_scratch_bytes.restype = _sz
+        L.gsr_test_sort_scratch_bytes.argtypes = [_sz]
+        L.gsr_test_radix_sort_pairs.restype = _i
+        L.gsr_test_radix_sort_pairs.argtypes = [_p, _p, _sz, _i, _p, _p]
+        L.gsr_test_scan_scratch_bytes.restype = _sz
+        L.gsr_test_scan_scratch_bytes.argtypes = [_sz]
+        L.gsr_test_scan.restype = _i
+        L.gsr_test_scan.argtypes = [_p, _p, _sz, _i, _p, _p]
+        L.gsr_profile_enable.restype = None
+        L.gsr_profile_enable.argtypes = [_i]
+        L.gsr_profile_collect.restype = _i
+        L.gsr_profile_collect.argtypes = [ctypes.POINTER(ctypes.c_double),
+                                          ctypes.POINTER(ctypes.c_longlong)]
+        L.gsr_profile_reset.restype = None
+        L.gsr_profile_reset.argtypes = []
+        L.gsr_profile_stage_name.restype = ctypes.c_char_p
+        L.gsr_profile_stage_name.argtypes = [_i]
         _lib = L
     return _lib
 
@@ -132,3 +150,26 @@ _ALLOC_CB = ALLOC_FN(_alloc_cb)
 
 def alloc_callback():
     return _ALLOC_CB
+
+
+NUM_STAGES = 10
+
+
+class StageTimer:
+    """Per-stage device time from the library's hipEvent instrumentation (gsr_testing.h)."""
+
+    def __init__(self):
+        self.L = load()
+
+    def enable(self, on=True):
+        self.L.gsr_profile_enable(int(on))
+
+    def reset(self):
+        self.L.gsr_profile_reset()
+
+    def collect(self):
+        ms = (ctypes.c_double * NUM_STAGES)()
+        calls = (ctypes.c_longlong * NUM_STAGES)()
+        check(self.L.gsr_profile_collect(ms, calls))
+        return {self.L.gsr_profile_stage_name(i).decode(): (ms[i], calls[i])
+                for i in range(NUM_STAGES)}

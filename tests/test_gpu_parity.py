@@ -1,0 +1,189 @@
+"""HIP path (libgsr.so through the drop-in diff_gaussian_rasterization API) vs the CPU oracle.
+
+Tolerances: the library and the oracle evaluate the same float32 expressions in the same order
+(-ffp-contract=off on both sides), so the forward agrees to the last bits except where expf's last
+ulp differs; images are compared at atol 1e-5 (north_star: <= 1e-5).  Backward gradients are summed
+with float atomics in a different order than the oracle's sequential loop, so they are compared
+as max|gpu - oracle| / max|oracle| <= 1e-5 per tensor.  Integer outputs (radii, num_rendered,
+sort results) must match exactly.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle.oracle import OracleRaster, mark_visible as oracle_mark_visible
+from scenes import scene, to_torch_call
+
+pytestmark = pytest.mark.gpu
+
+FWD_ATOL = 1e-5
+GRAD_REL = 1e-5
+
+
+def run_gpu(kw, grads=None, bwd=True):
+    from diff_gaussian_rasterization import GaussianRasterizer
+    settings, inp = to_torch_call(kw)
+    rast = GaussianRasterizer(settings)
+    outs = rast(means3D=inp["means3D"], means2D=inp["means2D"], opacities=inp["opacities"],
+                shs=inp.get("shs"), colors_precomp=inp.get("colors_precomp"),
+                scales=inp.get("scales"), rotations=inp.get("rotations"),
+                cov3D_precomp=inp.get("cov3D_precomp"), shs_language=inp.get("shs_language"),
+                language_feature_precomp=inp.get("language_feature_precomp"))
+    color, depth, alpha, feature, radii = outs
+    res = dict(color=color.detach().cpu().numpy(), depth=depth.detach().cpu().numpy(),
+               alpha=alpha.detach().cpu().numpy(), feature=feature.detach().cpu().numpy(),
+               radii=radii.cpu().numpy())
+    if bwd and grads is not None:
+        dimg, ddep, dalp, dfea = [None if g is None else torch.tensor(g, device="cuda") for g in grads]
+        loss = (color * dimg).sum()
+        if ddep is not None:
+            loss = loss + (depth * ddep).sum()
+        if dalp is not None:
+            loss = loss + (alpha * dalp).sum()
+        if dfea is not None and kw["include_feature"]:
+            loss = loss + (feature * dfea).sum()
+        loss.backward()
+        res["grads"] = {k: (None if v.grad is None else v.grad.detach().cpu().numpy())
+                        for k, v in inp.items()}
+    torch.cuda.synchronize()
+    return res
+
+
+GRAD_MAP = [("means3D", "means3D"), ("means2D", "means2D"), ("opacity", "opacities"),
+            ("colors", "colors_precomp"), ("sh", "shs"), ("scales", "scales"),
+            ("rotations", "rotations"), ("cov3D", "cov3D_precomp"), ("sh_language", "shs_language"),
+            ("language_feature", "language_feature_precomp")]
+
+
+def compare(kw, with_bwd=True, seed=5, extra_grads=True):
+    H, W = kw["image_height"], kw["image_width"]
+    rng = np.random.default_rng(seed)
+    dimg = rng.standard_normal((3, H, W)).astype(np.float32)
+    ddep = rng.standard_normal((1, H, W)).astype(np.float32) * 0.3 if extra_grads else None
+    dalp = rng.standard_normal((1, H, W)).astype(np.float32) if extra_grads else None
+    dfea = rng.standard_normal((3, H, W)).astype(np.float32) if extra_grads else None
+    orc = OracleRaster(**kw)
+    gpu = run_gpu(kw, (dimg, ddep, dalp, dfea), bwd=with_bwd)
+    np.testing.assert_array_equal(gpu["radii"], orc.radii)
+    for name in ("color", "depth", "alpha", "feature"):
+        np.testing.assert_allclose(gpu[name], getattr(orc, name), atol=FWD_ATOL, rtol=0,
+                                   err_msg=name)
+    if not with_bwd:
+        return orc, gpu
+    og = orc.backward(dimg, ddep, dalp, dfea if kw["include_feature"] else None)
+    checked = 0
+    for oname, iname in GRAD_MAP:
+        if og.get(oname) is None or iname not in gpu["grads"]:
+            continue
+        got = gpu["grads"][iname].reshape(og[oname].shape)
+        ref = og[oname]
+        scale = max(float(np.abs(ref).max()), 1e-6)
+        err = float(np.abs(got - ref).max()) / scale
+        assert err <= GRAD_REL, f"{iname}: rel err {err:.2e} (scale {scale:.2e})"
+        checked += 1
+    assert checked >= 5
+    return orc, gpu
+
+
+CONFIGS = [
+    dict(P=64, W=64, H=48, mode="sh", cov_mode="scale_rot", feature="sh"),
+    dict(P=1024, W=97, H=61, mode="sh", cov_mode="scale_rot", feature="sh"),
+    dict(P=1024, W=97, H=61, mode="colors", cov_mode="scale_rot", feature="precomp"),
+    dict(P=1024, W=64, H=48, mode="sh", cov_mode="cov3D", feature=None),
+    dict(P=4096, W=128, H=96, mode="colors", cov_mode="cov3D", feature="sh", bg=(0, 0, 0)),
+    dict(P=4096, W=200, H=120, mode="sh", cov_mode="scale_rot", feature="sh", active_degree=1),
+    dict(P=1, W=64, H=48, mode="sh", cov_mode="scale_rot", feature="sh", cam=0),
+    dict(P=2000, W=64, H=48, mode="sh", cov_mode="scale_rot", feature="sh", scale_mult=6.0),
+]
+
+
+@pytest.mark.parametrize("i", range(len(CONFIGS)))
+def test_forward_backward_parity(i):
+    compare(scene(seed=i, **CONFIGS[i]))
+
+
+def test_parity_without_extra_upstream_grads():
+    compare(scene(P=2048, W=96, H=80, seed=9, feature="sh"), extra_grads=False)
+
+
+def test_confidence_parity():
+    P = 1024
+    conf = np.random.default_rng(0).uniform(0.2, 1.0, P)
+    compare(scene(P=P, W=80, H=64, seed=4, confidence=conf))
+
+
+def test_empty_scene_returns_zero_images():
+    kw = scene(P=1, W=32, H=16)
+    for k in ("means3D", "shs", "scales", "rotations", "shs_language"):
+        kw[k] = kw[k][:0]
+    kw["opacities"] = kw["opacities"][:0]
+    gpu = run_gpu(kw, bwd=False)
+    assert np.all(gpu["color"] == 0) and gpu["radii"].shape == (0,)
+
+
+def test_mark_visible_parity():
+    from diff_gaussian_rasterization import mark_visible
+    kw = scene(P=5000, W=64, H=48, cam=2)
+    xyz = kw["means3D"].copy()
+    xyz[::7, 2] = -3.95  # behind the near plane of the jittered camera
+    got = mark_visible(torch.tensor(xyz, device="cuda"), torch.tensor(kw["viewmatrix"], device="cuda"),
+                       torch.tensor(kw["projmatrix"], device="cuda")).cpu().numpy()
+    np.testing.assert_array_equal(got, oracle_mark_visible(xyz, kw["viewmatrix"], kw["projmatrix"]))
+
+
+def test_forward_is_deterministic():
+    kw = scene(P=20000, W=160, H=120, seed=2)
+    a = run_gpu(kw, bwd=False)
+    b = run_gpu(kw, bwd=False)
+    for name in ("color", "depth", "alpha", "feature", "radii"):
+        np.testing.assert_array_equal(a[name], b[name])
+
+
+@pytest.mark.parametrize("n,bits", [(1, 8), (4095, 13), (4097, 32), (1_000_003, 32), (3_000_000, 13)])
+def test_radix_sort_sorted_and_stable(n, bits):
+    from gsr_amd import _lib
+    L = _lib.load()
+    rng = np.random.default_rng(n)
+    keys = rng.integers(0, 1 << min(bits, 31), size=n, dtype=np.int64).astype(np.uint32)
+    if bits < 32:
+        keys &= np.uint32((1 << bits) - 1)
+    keys[: n // 3] = keys[0]  # many ties
+    vals = np.arange(n, dtype=np.uint32)
+    k = torch.tensor(keys.view(np.int32), device="cuda")
+    v = torch.tensor(vals.view(np.int32), device="cuda")
+    scratch = torch.empty(int(L.gsr_test_sort_scratch_bytes(n)), dtype=torch.uint8, device="cuda")
+    _lib.check(L.gsr_test_radix_sort_pairs(k.data_ptr(), v.data_ptr(), n, bits, scratch.data_ptr(),
+                                           torch.cuda.current_stream().cuda_stream))
+    order = np.argsort(keys, kind="stable")
+    np.testing.assert_array_equal(k.cpu().numpy().view(np.uint32), keys[order])
+    np.testing.assert_array_equal(v.cpu().numpy().view(np.uint32), vals[order])
+
+
+@pytest.mark.parametrize("n", [1, 2047, 2049, 5_000_001])
+def test_scan(n):
+    from gsr_amd import _lib
+    L = _lib.load()
+    x = np.random.default_rng(n).integers(0, 50, size=n).astype(np.uint32)
+    xi = torch.tensor(x.view(np.int32), device="cuda")
+    out = torch.empty_like(xi)
+    scratch = torch.empty(int(L.gsr_test_scan_scratch_bytes(n)), dtype=torch.uint8, device="cuda")
+    for inclusive in (1, 0):
+        _lib.check(L.gsr_test_scan(xi.data_ptr(), out.data_ptr(), n, inclusive, scratch.data_ptr(),
+                                   torch.cuda.current_stream().cuda_stream))
+        c = np.cumsum(x, dtype=np.uint64).astype(np.uint32)
+        ref = c if inclusive else np.concatenate([[0], c[:-1]]).astype(np.uint32)
+        np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), ref)
+
+
+@pytest.mark.parametrize("P,W,H", [(100_000, 800, 800)])
+def test_config2_full_size_parity(P, W, H):
+    """BASELINE config 2 at full size (100k Gaussians, 800x800, SH degree 3), fwd + bwd."""
+    compare(scene(P=P, W=W, H=H, seed=0, cam=0, mode="sh", feature="sh"))
+
+
+def test_config3_full_size_forward_parity():
+    """BASELINE config 3 scale (1M Gaussians, 1008x756): forward parity vs the oracle."""
+    kw = scene(P=1_000_000, W=1008, H=756, seed=0, cam=1, mode="sh", feature="sh")
+    compare(kw, with_bwd=False)
