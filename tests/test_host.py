@@ -1,0 +1,72 @@
+"""Host-side pieces of the path (CPU): SH evaluation, activations, settings API."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from gsr_amd.sh import eval_sh
+from gsr_amd.synthetic import make_gaussians
+from gsr_amd.model import SplatModel, build_covariance_from_scaling_rotation
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.mark.parametrize("deg", [0, 1, 2, 3])
+def test_eval_sh_matches_reference_golden(deg):
+    d = np.load(os.path.join(GOLD, "sh_golden.npz"))
+    xyz, campos = torch.tensor(d["xyz"]), torch.tensor(d["campos"])
+    feats = torch.tensor(d["features"])
+    dir_pp = xyz - campos.repeat(xyz.shape[0], 1)
+    dirs = dir_pp / dir_pp.norm(dim=1, keepdim=True)
+    out = eval_sh(deg, feats.transpose(1, 2).view(-1, 3, 16), dirs)
+    np.testing.assert_allclose(out.numpy(), d[f"eval_sh_deg{deg}"], atol=1e-6, rtol=0)
+
+
+def test_language_feature_prepass_matches_reference_golden():
+    d = np.load(os.path.join(GOLD, "sh_golden.npz"))
+    xyz, campos = torch.tensor(d["xyz"]), torch.tensor(d["campos"])
+    lang = torch.tensor(d["language_feature"])
+    dir_pp = xyz - campos.repeat(xyz.shape[0], 1)
+    dirs = dir_pp / dir_pp.norm(dim=1, keepdim=True)
+    s2l = eval_sh(0, lang.view(-1, 3, 1), dirs)
+    f = s2l / (s2l.norm(dim=-1, keepdim=True) + 1e-9)
+    np.testing.assert_allclose(f.numpy(), d["language_feature_precomp"], atol=1e-6, rtol=0)
+
+
+def test_model_getters_and_covariance():
+    g = make_gaussians(500, seed=3)
+    m = SplatModel(g, device="cpu")
+    assert torch.allclose(m.get_scaling, torch.exp(g.scaling))
+    assert torch.allclose(m.get_rotation.norm(dim=1), torch.ones(500), atol=1e-6)
+    assert m.get_features.shape == (500, 16, 3)
+    cov = build_covariance_from_scaling_rotation(m.get_scaling, 1.0, m._rotation)
+    # symmetric PSD reconstruction
+    S = torch.stack([cov[:, 0], cov[:, 1], cov[:, 2], cov[:, 1], cov[:, 3], cov[:, 4], cov[:, 2],
+                     cov[:, 4], cov[:, 5]], 1).view(-1, 3, 3)
+    ev = torch.linalg.eigvalsh(S.double())
+    assert torch.all(ev > -1e-9)
+    s2 = torch.sort(m.get_scaling.double() ** 2, dim=1).values
+    torch.testing.assert_close(ev, s2, rtol=1e-4, atol=1e-9)
+
+
+def test_settings_namedtuple_is_backward_compatible():
+    from diff_gaussian_rasterization import GaussianRasterizationSettings
+    fields = GaussianRasterizationSettings._fields
+    assert fields[:12] == ("image_height", "image_width", "tanfovx", "tanfovy", "bg",
+                           "scale_modifier", "viewmatrix", "projmatrix", "sh_degree", "campos",
+                           "prefiltered", "debug")
+    assert "include_feature" in fields and "confidence" in fields
+    s = GaussianRasterizationSettings(10, 10, 1.0, 1.0, None, 1.0, None, None, 0, None, False, False)
+    assert s.include_feature is False and s.confidence is None
+
+
+def test_cpu_tensors_are_rejected_not_rasterized_on_cpu():
+    """The product path has no CPU fallback: CPU tensors must raise."""
+    from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+    s = GaussianRasterizationSettings(8, 8, 1.0, 1.0, torch.zeros(3), 1.0, torch.eye(4),
+                                      torch.eye(4), 0, torch.zeros(3), False, False)
+    with pytest.raises(RuntimeError):
+        GaussianRasterizer(s)(means3D=torch.zeros((1, 3)), means2D=torch.zeros((1, 3)),
+                              opacities=torch.ones((1, 1)), colors_precomp=torch.ones((1, 3)),
+                              scales=torch.ones((1, 3)), rotations=torch.tensor([[1., 0, 0, 0]]))
