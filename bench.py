@@ -70,10 +70,6 @@ def algorithmic_bytes(stage, P, Pv, R, T, HW, D=3, C=8, tile_passes=2):
     }[stage]
 
 
-# per (pixel, splat) pair FLOP model of the blend kernels
-FLOP_PER_PAIR = {"render_fwd": 45.0, "render_bwd": 110.0}
-
-
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -164,10 +160,9 @@ def main():
         b = algorithmic_bytes(name, P, Pv, R, T, HW, D=deg)
         k = {"avg_ms": round(avg_ms, 4), "calls": int(calls), "bytes": int(b),
              "gbs": round(b / (avg_ms * 1e-3) / 1e9, 1)}
-        if name in FLOP_PER_PAIR:
-            pairs = 256.0 * R  # every splat instance is evaluated by the 256 pixels of its tile
-            k["pair_evals_per_s"] = round(pairs / (avg_ms * 1e-3) / 1e9, 2)
-            k["tflops_est"] = round(pairs * FLOP_PER_PAIR[name] / (avg_ms * 1e-3) / 1e12, 2)
+        if name in ("render_fwd", "render_bwd"):
+            # (pixel, instance) candidate pairs per second: 256 pixels x R instances per view
+            k["pair_candidates_per_s_G"] = round(256.0 * R / (avg_ms * 1e-3) / 1e9, 1)
         kernels[name] = k
     roofline = None
     if kernels:
@@ -185,9 +180,14 @@ def main():
         roofline = {"kernel": dom, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                     "algorithmic_bytes": kd["bytes"], "avg_ms": kd["avg_ms"]}
-        if "tflops_est" in kd:
-            roofline["valu"] = {"achieved_tflops": kd["tflops_est"], "peak_tflops": FP32_PEAK_TFLOPS,
-                                "frac": round(kd["tflops_est"] / FP32_PEAK_TFLOPS, 4)}
+        try:
+            with open(args.pmc_file) as fh:
+                pmc = json.load(fh)
+            v = pmc.get("kernels", {}).get(dom, {}).get("valu_busy_frac")
+            if v is not None and pmc.get("workload") == args.workload:
+                roofline["valu_busy_frac_pmc"] = v
+        except (OSError, ValueError):
+            pass
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_baseline_views > 0:

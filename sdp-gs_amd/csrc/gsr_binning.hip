@@ -35,11 +35,22 @@ __global__ __launch_bounds__(kThreads) void duplicate_kernel(int P,
   const int r = radii[gid];
   if (!(r > 0)) return;
   uint32_t off = (s == 0) ? 0u : offsets[s - 1];
+  const uint32_t end = offsets[s];
+  if (off == end) return;
   const float4 r0 = rec[4 * (size_t)gid];
+  const float4 r1 = rec[4 * (size_t)gid + 1];
+  const float qc = splat_q_cut(r0.z, r0.w, r1.x, r1.y);
   uint32_t x0, y0, x1, y1;
   tile_rect(r0.x, r0.y, r, gx, gy, x0, y0, x1, y1);
-  for (uint32_t y = y0; y < y1; y++)
-    for (uint32_t x = x0; x < x1; x++) {
+  // the same conservative tile test as the preprocess count (gsr_device.h), so exactly
+  // tiles_touched ids are written
+  for (uint32_t y = y0; y < y1 && off < end; y++)
+    for (uint32_t x = x0; x < x1 && off < end; x++) {
+      if (qc >= 0.0f &&
+          !splat_touches_rect(r0.x, r0.y, r0.z, r0.w, r1.x, qc, (float)(x * kTile),
+                              (float)(x * kTile + kTile - 1), (float)(y * kTile),
+                              (float)(y * kTile + kTile - 1)))
+        continue;
       tkey[off] = y * gx + x;
       tval[off] = gid;
       off++;

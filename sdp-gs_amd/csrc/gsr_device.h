@@ -101,6 +101,49 @@ __device__ __forceinline__ void tile_rect(float px, float py, int r, uint32_t gx
   x1 = min((uint32_t)c, gx); y1 = min((uint32_t)d, gy);
 }
 
+// ---- conservative splat / pixel-rectangle culling ----------------------------------------------
+// The blend skips a (splat, pixel) pair when alpha = min(0.99, op * exp(power)) < 1/255 with
+// power = -q/2, q = ca dx^2 + 2 cb dx dy + cc dy^2 (forward.cu:335-345).  A splat that fails that
+// test at EVERY pixel centre of a rectangle changes no output bit there, so it may be dropped from
+// the rectangle's list.  `q_cut` is the squared Mahalanobis radius beyond which alpha < 1/255,
+// or a negative value when nothing can be culled (conic not positive definite) and -2 when the
+// splat can never reach 1/255 (op < 1/255: max alpha is op at power = 0).
+__device__ __forceinline__ float splat_q_cut(float ca, float cb, float cc, float op) {
+  if (!(op >= 1.0f / 255.0f)) return -2.0f;
+  if (!(ca > 0.0f && cc > 0.0f && ca * cc - cb * cb > 0.0f)) return -1.0f;
+  return (float)(2.0 * log(255.0 * (double)op));
+}
+
+// True unless q > q_cut (plus a safety margin) on the whole rectangle of pixel centres
+// [x0, x1] x [y0, y1].  The minimum of the positive-definite form over a rectangle is 0 when the
+// centre is inside, else it lies on an edge; each edge is a clamped 1-D quadratic minimisation.
+__device__ __forceinline__ bool splat_touches_rect(float mx, float my, float ca, float cb, float cc,
+                                                   float q_cut, float x0, float x1, float y0,
+                                                   float y1) {
+  if (q_cut == -2.0f) return false;
+  if (q_cut < 0.0f) return true;
+  const float dx0 = x0 - mx, dx1 = x1 - mx, dy0 = y0 - my, dy1 = y1 - my;
+  if (dx0 <= 0.0f && dx1 >= 0.0f && dy0 <= 0.0f && dy1 >= 0.0f) return true;
+  float qmin = 3.0e38f, tabs = 0.0f;
+#pragma unroll
+  for (int e = 0; e < 4; e++) {
+    float dx, dy;
+    if (e < 2) {
+      dx = (e == 0) ? dx0 : dx1;
+      dy = fminf(fmaxf(-cb * dx / cc, dy0), dy1);
+    } else {
+      dy = (e == 2) ? dy0 : dy1;
+      dx = fminf(fmaxf(-cb * dy / ca, dx0), dx1);
+    }
+    const float t1 = ca * dx * dx, t2 = cc * dy * dy, t3 = 2.0f * cb * dx * dy;
+    const float q = t1 + t2 + t3;
+    if (q < qmin) { qmin = q; tabs = t1 + t2 + fabsf(t3); }
+  }
+  // margin >> the float error of the blend's own evaluation: dx = mx - px carries up to
+  // ulp(2048) = 2.4e-4 px, i.e. |dq| <= 2 sqrt(ca q) * 2.4e-4 < 3e-3 for q <= 11, ca <= 1/0.3
+  return qmin <= q_cut + 2e-2f + 1e-4f * tabs;
+}
+
 // auxiliary.h:58-77 (the 4x4 matrices are row-major tensors read as column-major)
 __device__ __forceinline__ V3 xform_point43(V3 p, const float* m) {
   return v3(m[0] * p.x + m[4] * p.y + m[8] * p.z + m[12],

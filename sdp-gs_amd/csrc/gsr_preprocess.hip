@@ -132,7 +132,20 @@ __global__ __launch_bounds__(kThreads) void preprocess_kernel(PreArgs a) {
   const float depth = p_view.z;
   g.depths[idx] = depth;
   a.radii[idx] = r;
-  g.tiles_touched[idx] = (y1 - y0) * (x1 - x0);
+  // Exact tile list: the reference emits every tile of the 3-sigma square (forward.cu:255); tiles
+  // in which no pixel can reach alpha >= 1/255 are dropped here (no output bit changes)
+  const float qc = splat_q_cut(con_a, con_b, con_c, op);
+  uint32_t count = 0;
+  if (qc == -1.0f) {
+    count = (y1 - y0) * (x1 - x0);
+  } else if (qc >= 0.0f) {
+    for (uint32_t ty = y0; ty < y1; ty++)
+      for (uint32_t tx = x0; tx < x1; tx++)
+        count += splat_touches_rect(px, py, con_a, con_b, con_c, qc, (float)(tx * kTile),
+                                    (float)(tx * kTile + kTile - 1), (float)(ty * kTile),
+                                    (float)(ty * kTile + kTile - 1));
+  }
+  g.tiles_touched[idx] = count;
   g.dkey_a[idx] = __float_as_uint(depth);
   float4* rec = g.rec + 4 * (size_t)idx;
   rec[0] = make_float4(px, py, con_a, con_b);

@@ -32,13 +32,50 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t ntiles) {
   return start + local;
 }
 
+// Which of the 4 waves (pixel rows 4w..4w+3 of the tile) a splat can reach: bit w set unless the
+// conservative test of gsr_device.h proves alpha < 1/255 on all 64 pixels of wave w.
+__device__ __forceinline__ uint32_t wave_mask(float4 r0, float4 r1, uint32_t tx, uint32_t ty) {
+  const float qc = splat_q_cut(r0.z, r0.w, r1.x, r1.y);
+  if (qc == -1.0f) return 0xfu;
+  if (qc == -2.0f) return 0u;
+  const float x0 = (float)(tx * kTile), x1 = (float)(tx * kTile + kTile - 1);
+  uint32_t m = 0;
+#pragma unroll
+  for (int w = 0; w < 4; w++) {
+    const float y0 = (float)(ty * kTile + 4 * w);
+    m |= splat_touches_rect(r0.x, r0.y, r0.z, r0.w, r1.x, qc, x0, x1, y0, y0 + 3.0f) ? (1u << w) : 0u;
+  }
+  return m;
+}
+
+// Per-wave compaction of the batch: the wave's list holds, in batch order, the entries whose
+// mask has this wave's bit.  Returns the list length (wave-uniform).
+__device__ __forceinline__ uint32_t build_wave_list(const uint8_t* s_mask, uint8_t* list,
+                                                    uint32_t cnt, int wid, int lane) {
+  const uint64_t lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
+  uint32_t n = 0;
+#pragma unroll
+  for (int c = 0; c < kThreads / 64; c++) {
+    const uint32_t j = (uint32_t)(c * 64 + lane);
+    const bool bit = j < cnt && ((s_mask[j] >> wid) & 1u);
+    const uint64_t b = __ballot(bit);
+    if (bit) list[n + (uint32_t)__popcll(b & lt)] = (uint8_t)j;
+    n += (uint32_t)__popcll(b);
+  }
+  return n;
+}
+
 template <bool FEAT>
 __global__ __launch_bounds__(kThreads) void render_fwd_kernel(RenderArgs a) {
   __shared__ float4 s_r0[kThreads];
   __shared__ float4 s_r1[kThreads];
   __shared__ float4 s_r2[kThreads];
   __shared__ float4 s_r3[FEAT ? kThreads : 1];
+  __shared__ uint8_t s_mask[kThreads];
+  __shared__ uint8_t s_list[kThreads / 64][kThreads];
   __shared__ uint32_t s_max;
+  const int lane = (int)(threadIdx.x & 63);
+  const int wid = (int)(threadIdx.x >> 6);
 
   const uint32_t ntiles = a.gx * a.gy;
   const uint32_t tile = xcd_tile(blockIdx.x, ntiles);
@@ -65,15 +102,20 @@ __global__ __launch_bounds__(kThreads) void render_fwd_kernel(RenderArgs a) {
     if (i < range.y) {
       const uint32_t gid = a.point_list[i];
       const float4* rec = a.rec + 4 * (size_t)gid;
-      s_r0[threadIdx.x] = rec[0];
-      s_r1[threadIdx.x] = rec[1];
+      const float4 q0 = rec[0], q1 = rec[1];
+      s_r0[threadIdx.x] = q0;
+      s_r1[threadIdx.x] = q1;
       s_r2[threadIdx.x] = rec[2];
       if (FEAT) s_r3[threadIdx.x] = rec[3];
+      s_mask[threadIdx.x] = (uint8_t)wave_mask(q0, q1, tx, ty);
     }
     __syncthreads();
     const uint32_t cnt = min((uint32_t)kThreads, range.y - base);
-    for (uint32_t j = 0; !done && j < cnt; j++) {
-      contributor++;
+    const uint32_t nlist = build_wave_list(s_mask, s_list[wid], cnt, wid, lane);
+    for (uint32_t k = 0; !done && k < nlist; k++) {
+      const uint32_t j = s_list[wid][k];
+      // the reference counts every list position (forward.cu:328); skipped entries cannot blend
+      contributor = base - range.x + j + 1;
       const float4 r0 = s_r0[j];
       const float dx = r0.x - pfx, dy = r0.y - pfy;
       const float4 r1 = s_r1[j];
@@ -180,8 +222,11 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
   __shared__ float4 s_r3[FEAT ? kThreads : 1];
   __shared__ uint32_t s_gid[kThreads];
   __shared__ float s_acc[kThreads][kAccFloats];
+  __shared__ uint8_t s_mask[kThreads];
+  __shared__ uint8_t s_list[kThreads / 64][kThreads];
 
   const int lane = (int)(threadIdx.x & 63);
+  const int wid = (int)(threadIdx.x >> 6);
   const uint32_t ntiles = a.gx * a.gy;
   const uint32_t tile = xcd_tile(blockIdx.x, ntiles);
   const uint32_t tx = tile % a.gx, ty = tile / a.gx;
@@ -197,6 +242,9 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
   const float T_final = inside ? a.final_T[pix] : 0.0f;
   float T = T_final;
   const uint32_t last_contributor = inside ? a.n_contrib[pix] : 0u;
+  uint32_t wave_last = last_contributor;
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) wave_last = max(wave_last, (uint32_t)__shfl_xor((int)wave_last, d, 64));
 
   constexpr int NC = FEAT ? 8 : (EXTRA ? 5 : 3);
   float dpix[NC];
@@ -238,14 +286,19 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
       const uint32_t gid = a.point_list[range.x + rel];
       s_gid[threadIdx.x] = gid;
       const float4* rec = a.rec + 4 * (size_t)gid;
-      s_r0[threadIdx.x] = rec[0];
-      s_r1[threadIdx.x] = rec[1];
+      const float4 q0 = rec[0], q1 = rec[1];
+      s_r0[threadIdx.x] = q0;
+      s_r1[threadIdx.x] = q1;
+      s_mask[threadIdx.x] = (uint8_t)wave_mask(q0, q1, tx, ty);
       s_r2[threadIdx.x] = rec[2];
       if (FEAT) s_r3[threadIdx.x] = rec[3];
     }
     __syncthreads();
-    for (uint32_t j = 0; j < cnt; j++) {
+    const uint32_t nlist = build_wave_list(s_mask, s_list[wid], cnt, wid, lane);
+    for (uint32_t k = 0; k < nlist; k++) {
+      const uint32_t j = s_list[wid][k];
       const uint32_t rel = tile_last - 1 - done_cnt - j;
+      if (rel >= wave_last) continue;  // wave-uniform: behind every pixel of this wave
       const float4 r0 = s_r0[j];
       const float4 r1 = s_r1[j];
       const float dx = r0.x - pfx, dy = r0.y - pfy;
