@@ -10,6 +10,7 @@
 
 #include <atomic>
 #include <cstdarg>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -66,8 +67,19 @@ ImgState carve_img(char* base, size_t W, size_t H) {
   s.n_contrib = c.take<uint32_t>(W * H);
   s.ranges = c.take<uint2>(gx * gy);
   s.tile_last = c.take<uint32_t>(gx * gy);
+  s.order = c.take<uint32_t>(gx * gy);
   s.bytes = c.size();
   return s;
+}
+
+int tile_schedule_mode() {
+  static const int mode = [] {
+    const char* e = getenv("GSR_TILE_ORDER");
+    if (e && strcmp(e, "natural") == 0) return 0;
+    if (e && strcmp(e, "xcd") == 0) return 1;
+    return 2;  // heaviest first
+  }();
+  return mode;
 }
 
 }  // namespace gsr
@@ -299,6 +311,7 @@ int gsr_rasterize_gaussians(int P, int M, const float* background, const float* 
   ra.final_T = im.final_T; ra.n_contrib = im.n_contrib; ra.tile_last = im.tile_last;
   ra.out_color = out_color; ra.out_depth = out_depth; ra.out_alpha = out_alpha;
   ra.out_feature = out_feature; ra.include_feature = include_feature;
+  ra.order = im.order; ra.sched = tile_schedule_mode();
   PROF_BEGIN(RENDER_FWD);
   GSR_CHECK(launch_render_forward(ra, stream));
   PROF_END(RENDER_FWD);
@@ -356,6 +369,7 @@ int gsr_rasterize_gaussians_backward(
     rb.final_T = im.final_T; rb.n_contrib = im.n_contrib; rb.tile_last = im.tile_last;
     rb.dL_dcolor = dL_dout_color; rb.dL_ddepth = dL_dout_depth; rb.dL_dalpha = dL_dout_alpha;
     rb.dL_dfeature = dL_dout_feature; rb.acc = g.acc; rb.include_feature = include_feature;
+    rb.order = im.order; rb.sched = tile_schedule_mode();
     PROF_BEGIN(RENDER_BWD);
     GSR_CHECK(launch_render_backward(rb, stream));
     PROF_END(RENDER_BWD);

@@ -106,9 +106,13 @@ struct ImgState {
   uint32_t* n_contrib;  // [H*W]
   uint2* ranges;        // [tiles]
   uint32_t* tile_last;  // [tiles] max n_contrib over the tile's pixels
+  uint32_t* order;      // [tiles] workgroup -> tile schedule (heaviest first)
   size_t bytes;
 };
 ImgState carve_img(char* base, size_t W, size_t H);
+
+// workgroup -> tile schedule of the blend kernels (env GSR_TILE_ORDER: natural | xcd | lpt)
+int tile_schedule_mode();
 
 // ---- per-Gaussian kernels (gsr_preprocess.hip, gsr_backward.hip) ----------------------------------
 struct PreArgs {
@@ -162,6 +166,8 @@ struct RenderArgs {
   uint32_t* tile_last;
   float *out_color, *out_depth, *out_alpha, *out_feature;
   int include_feature;
+  uint32_t* order;
+  int sched;
 };
 hipError_t launch_render_forward(const RenderArgs& a, hipStream_t s);
 
@@ -178,6 +184,8 @@ struct RenderBwdArgs {
   const float *dL_dcolor, *dL_ddepth, *dL_dalpha, *dL_dfeature;
   float* acc;
   int include_feature;
+  uint32_t* order;
+  int sched;
 };
 hipError_t launch_render_backward(const RenderBwdArgs& a, hipStream_t s);
 

@@ -32,6 +32,45 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t ntiles) {
   return start + local;
 }
 
+// Tile schedule: 0 = natural order (round-robin over XCDs by the dispatcher), 1 = contiguous
+// band per XCD (L2 locality), 2 = heaviest tiles first (order[] computed on device by
+// tile_schedule_kernel; a schedule only, results do not depend on it).
+__device__ __forceinline__ uint32_t sched_tile(uint32_t b, uint32_t ntiles, int mode,
+                                               const uint32_t* order) {
+  if (mode == 2 && order) return order[b];
+  if (mode == 1) return xcd_tile(b, ntiles);
+  return b;
+}
+
+// One workgroup: bucket the tiles by log2 of their work (list length) and write them heaviest
+// bucket first.  Order inside a bucket is whatever the LDS atomics produce -- only a schedule.
+constexpr int kSchedThreads = 1024;
+__global__ __launch_bounds__(kSchedThreads) void tile_schedule_kernel(const uint2* __restrict__ ranges,
+                                                                      const uint32_t* __restrict__ work,
+                                                                      uint32_t ntiles,
+                                                                      uint32_t* __restrict__ order) {
+  __shared__ uint32_t cnt[33];
+  __shared__ uint32_t off[33];
+  if (threadIdx.x < 33) cnt[threadIdx.x] = 0;
+  __syncthreads();
+  for (uint32_t t = threadIdx.x; t < ntiles; t += kSchedThreads) {
+    const uint32_t w = work ? work[t] : ranges[t].y - ranges[t].x;
+    const uint32_t bkt = 32u - (uint32_t)__clz((int)w);  // 0 for empty, 32 for >= 2^31
+    atomicAdd(&cnt[32 - bkt], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t s = 0;
+    for (int i = 0; i < 33; i++) { off[i] = s; s += cnt[i]; }
+  }
+  __syncthreads();
+  for (uint32_t t = threadIdx.x; t < ntiles; t += kSchedThreads) {
+    const uint32_t w = work ? work[t] : ranges[t].y - ranges[t].x;
+    const uint32_t bkt = 32u - (uint32_t)__clz((int)w);
+    order[atomicAdd(&off[32 - bkt], 1u)] = t;
+  }
+}
+
 // Which of the 4 waves (pixel rows 4w..4w+3 of the tile) a splat can reach: bit w set unless the
 // conservative test of gsr_device.h proves alpha < 1/255 on all 64 pixels of wave w.
 __device__ __forceinline__ uint32_t wave_mask(float4 r0, float4 r1, uint32_t tx, uint32_t ty) {
@@ -78,7 +117,7 @@ __global__ __launch_bounds__(kThreads) void render_fwd_kernel(RenderArgs a) {
   const int wid = (int)(threadIdx.x >> 6);
 
   const uint32_t ntiles = a.gx * a.gy;
-  const uint32_t tile = xcd_tile(blockIdx.x, ntiles);
+  const uint32_t tile = sched_tile(blockIdx.x, ntiles, a.sched, a.order);
   const uint32_t tx = tile % a.gx, ty = tile / a.gx;
   const uint32_t px = tx * kTile + (threadIdx.x & (kTile - 1));
   const uint32_t py = ty * kTile + (threadIdx.x >> 4);
@@ -89,7 +128,7 @@ __global__ __launch_bounds__(kThreads) void render_fwd_kernel(RenderArgs a) {
 
   const uint2 range = a.ranges[tile];
   float T = 1.0f;
-  uint32_t contributor = 0, last_contributor = 0;
+  uint32_t last_contributor = 0;
   constexpr int NC = FEAT ? 8 : 5;
   float C[NC];
 #pragma unroll
@@ -112,36 +151,55 @@ __global__ __launch_bounds__(kThreads) void render_fwd_kernel(RenderArgs a) {
     __syncthreads();
     const uint32_t cnt = min((uint32_t)kThreads, range.y - base);
     const uint32_t nlist = build_wave_list(s_mask, s_list[wid], cnt, wid, lane);
-    for (uint32_t k = 0; !done && k < nlist; k++) {
-      const uint32_t j = s_list[wid][k];
-      // the reference counts every list position (forward.cu:328); skipped entries cannot blend
-      contributor = base - range.x + j + 1;
-      const float4 r0 = s_r0[j];
-      const float dx = r0.x - pfx, dy = r0.y - pfy;
-      const float4 r1 = s_r1[j];
-      const float power = -0.5f * (r0.z * dx * dx + r1.x * dy * dy) - r0.w * dx * dy;
-      if (power > 0.0f) continue;
-      const float alpha = fminf(0.99f, r1.y * expf(power));
-      if (alpha < 1.0f / 255.0f) continue;
-      const float test_T = T * (1 - alpha);
-      if (test_T < 0.0001f) {
-        done = true;
-        continue;
+    const uint32_t rel0 = base - range.x;
+    // Four list entries per iteration: their (independent) Gaussian weights are evaluated
+    // together, then composited in list order exactly as the reference's per-splat loop
+    // (forward.cu:325-362) -- same operations, same order, per pixel.
+    for (uint32_t k = 0; k < nlist; k += 4) {
+      if (__ballot(!done) == 0ull) break;  // wave-uniform
+      const uint32_t packed = *reinterpret_cast<const uint32_t*>(&s_list[wid][k]);
+      uint32_t jj[4];
+      float pw[4], al[4];
+      float4 r1v[4], r2v[4];
+      float f2v[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        jj[u] = (packed >> (8 * u)) & 0xffu;
+        const float4 r0 = s_r0[jj[u]];
+        r1v[u] = s_r1[jj[u]];
+        r2v[u] = s_r2[jj[u]];
+        f2v[u] = FEAT ? s_r3[jj[u]].x : 0.0f;
+        const float dx = r0.x - pfx, dy = r0.y - pfy;
+        const float power = -0.5f * (r0.z * dx * dx + r1v[u].x * dy * dy) - r0.w * dx * dy;
+        // entries past the list end get power = +1 and are skipped like any power > 0 pair
+        pw[u] = (k + u < nlist) ? power : 1.0f;
+        al[u] = fminf(0.99f, r1v[u].y * expf(pw[u]));
       }
-      const float4 r2 = s_r2[j];
-      C[0] += r1.w * alpha * T;
-      C[1] += r2.x * alpha * T;
-      C[2] += r2.y * alpha * T;
-      C[3] += r1.z * alpha * T;
-      C[4] += alpha * T;
-      if (FEAT) {
-        const float4 r3 = s_r3[j];
-        C[5] += r2.z * alpha * T;
-        C[6] += r2.w * alpha * T;
-        C[7] += r3.x * alpha * T;
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        if (done) continue;
+        if (pw[u] > 0.0f) continue;
+        const float alpha = al[u];
+        if (alpha < 1.0f / 255.0f) continue;
+        const float test_T = T * (1 - alpha);
+        if (test_T < 0.0001f) {
+          done = true;
+          continue;
+        }
+        C[0] += r1v[u].w * alpha * T;
+        C[1] += r2v[u].x * alpha * T;
+        C[2] += r2v[u].y * alpha * T;
+        C[3] += r1v[u].z * alpha * T;
+        C[4] += alpha * T;
+        if (FEAT) {
+          C[5 % NC] += r2v[u].z * alpha * T;
+          C[6 % NC] += r2v[u].w * alpha * T;
+          C[7 % NC] += f2v[u] * alpha * T;
+        }
+        T = test_T;
+        // the reference counts every list position (forward.cu:328); skipped entries cannot blend
+        last_contributor = rel0 + jj[u] + 1;
       }
-      T = test_T;
-      last_contributor = contributor;
     }
   }
 
@@ -170,6 +228,74 @@ __global__ __launch_bounds__(kThreads) void render_fwd_kernel(RenderArgs a) {
       a.out_feature[2 * HW + pix] = FEAT ? C[FEAT ? 7 : 0] : 0.0f;
     }
   }
+}
+
+template <int CTRL>
+__device__ __forceinline__ float dpp(float x) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), CTRL, 0xf, 0xf, false));
+}
+
+// Orientation of gfx950's v_permlane32_swap / v_permlane16_swap (which half of the pair keeps
+// the first operand), probed once per kernel so the value->lane map below does not rest on an
+// assumption about the ISA description.
+struct SwapOrient {
+  uint32_t flip32, flip16;  // 1 if the low half ends up holding the second operand's pair
+};
+__device__ __forceinline__ SwapOrient probe_swaps(int lane) {
+  const uint32_t a = (uint32_t)lane, b = (uint32_t)lane + 64u;
+  const auto r32 = __builtin_amdgcn_permlane32_swap(a, b, false, false);
+  const auto r16 = __builtin_amdgcn_permlane16_swap(a, b, false, false);
+  SwapOrient o;
+  o.flip32 = (__builtin_amdgcn_readfirstlane(r32[0]) == 0u) ? 0u : 1u;
+  o.flip16 = (__builtin_amdgcn_readfirstlane(r16[0]) == 0u) ? 0u : 1u;
+  return o;
+}
+
+// Halving butterfly on VALU only: on entry every lane holds 16 partial values; on exit every
+// lane holds the full wave sum of ONE value, index k = 8*b5' + 4*b4' + 2*b3 + b2 (b = lane bits,
+// b5'/b4' corrected by the probed swap orientation), 4 lanes per value.  Steps: permlane32_swap
+// (pairs lane l with l^32, 8 values -> 8 adds), permlane16_swap (l^16, 4 adds), DPP row_mirror
+// (l^15 within a row), DPP row_half_mirror (l^7), quad_perm xor 2, xor 1.  The partner maps
+// {^15, ^7, ^2, ^1} are linearly independent over the low 4 lane bits, so every lane of the
+// 16-lane row is summed exactly once; no LDS traffic (the previous form used 17 ds_bpermute).
+__device__ __forceinline__ float wave_reduce16_dpp(float (&v)[16], int lane) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[i]), __float_as_uint(v[i + 8]),
+                                                    false, false);
+    v[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[i]), __float_as_uint(v[i + 4]),
+                                                    false, false);
+    v[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+  {
+    const bool hi = lane & 8;
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+      const float send = hi ? v[i] : v[i + 2];
+      const float keep = hi ? v[i + 2] : v[i];
+      v[i] = keep + dpp<0x140>(send);  // row_mirror
+    }
+  }
+  float x;
+  {
+    const bool hi = lane & 4;
+    const float send = hi ? v[0] : v[1];
+    const float keep = hi ? v[1] : v[0];
+    x = keep + dpp<0x141>(send);  // row_half_mirror
+  }
+  x += dpp<0x4E>(x);  // quad_perm [2,3,0,1]
+  x += dpp<0xB1>(x);  // quad_perm [1,0,3,2]
+  return x;
+}
+
+__device__ __forceinline__ int reduce16_slot(int lane, SwapOrient o) {
+  const int b5 = ((lane >> 5) & 1) ^ (int)o.flip32;
+  const int b4 = ((lane >> 4) & 1) ^ (int)o.flip16;
+  return b5 * 8 + b4 * 4 + ((lane >> 3) & 1) * 2 + ((lane >> 2) & 1);
 }
 
 // Halving butterfly: on entry every lane holds 16 partial values; on exit lane l holds the wave
@@ -214,7 +340,7 @@ __device__ __forceinline__ float wave_reduce16(float (&v)[16], int lane) {
   return x;
 }
 
-template <bool EXTRA, bool FEAT>
+template <bool EXTRA, bool FEAT, int GROUP>
 __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
   __shared__ float4 s_r0[kThreads];
   __shared__ float4 s_r1[kThreads];
@@ -227,8 +353,9 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
 
   const int lane = (int)(threadIdx.x & 63);
   const int wid = (int)(threadIdx.x >> 6);
+  const SwapOrient swap_orient = probe_swaps(lane);
   const uint32_t ntiles = a.gx * a.gy;
-  const uint32_t tile = xcd_tile(blockIdx.x, ntiles);
+  const uint32_t tile = sched_tile(blockIdx.x, ntiles, a.sched, a.order);
   const uint32_t tx = tile % a.gx, ty = tile / a.gx;
   const uint32_t px = tx * kTile + (threadIdx.x & (kTile - 1));
   const uint32_t py = ty * kTile + (threadIdx.x >> 4);
@@ -295,20 +422,43 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
     }
     __syncthreads();
     const uint32_t nlist = build_wave_list(s_mask, s_list[wid], cnt, wid, lane);
-    for (uint32_t k = 0; k < nlist; k++) {
-      const uint32_t j = s_list[wid][k];
+    // Four list entries per group: the cheap per-pair test (power, G, alpha) of all four is
+    // evaluated first (independent work), then the entries are replayed in list order.
+    for (uint32_t k0 = 0; k0 < nlist; k0 += GROUP) {
+    const uint32_t packed = GROUP == 4 ? *reinterpret_cast<const uint32_t*>(&s_list[wid][k0])
+                                       : (uint32_t)s_list[wid][k0];
+    {
+      // list order is back to front: if even the group's front-most entry lies behind every
+      // pixel's last contributor in this wave, nothing in the group can contribute
+      const uint32_t ulast = min((uint32_t)GROUP - 1u, nlist - 1 - k0);
+      const uint32_t jl = (packed >> (8 * ulast)) & 0xffu;
+      if (tile_last - 1 - done_cnt - jl >= wave_last) continue;  // wave-uniform
+    }
+    float Gv[GROUP], av[GROUP];
+    bool cv[GROUP];
+#pragma unroll
+    for (int u = 0; u < GROUP; u++) {
+      const uint32_t j = (packed >> (8 * u)) & 0xffu;
       const uint32_t rel = tile_last - 1 - done_cnt - j;
-      if (rel >= wave_last) continue;  // wave-uniform: behind every pixel of this wave
       const float4 r0 = s_r0[j];
       const float4 r1 = s_r1[j];
       const float dx = r0.x - pfx, dy = r0.y - pfy;
-      bool contrib = rel < last_contributor;
       const float power = -0.5f * (r0.z * dx * dx + r1.x * dy * dy) - r0.w * dx * dy;
-      contrib = contrib && !(power > 0.0f);
-      const float G = expf(power);
-      const float alpha = fminf(0.99f, r1.y * G);
-      contrib = contrib && !(alpha < 1.0f / 255.0f);
+      Gv[u] = expf(power);
+      av[u] = fminf(0.99f, r1.y * Gv[u]);
+      cv[u] = (k0 + u < nlist) && rel < last_contributor && !(power > 0.0f) &&
+              !(av[u] < 1.0f / 255.0f);
+    }
+#pragma unroll
+    for (int u = 0; u < GROUP; u++) {
+      const bool contrib = cv[u];
       if (__ballot(contrib) == 0ull) continue;  // wave-uniform skip
+      const uint32_t j = (packed >> (8 * u)) & 0xffu;
+      const float G = Gv[u];
+      const float alpha = av[u];
+      const float4 r0 = s_r0[j];
+      const float4 r1 = s_r1[j];
+      const float dx = r0.x - pfx, dy = r0.y - pfy;
 
       float g[kAccFloats];
 #pragma unroll
@@ -356,12 +506,12 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
         g[kAccOp] = G * dL_dalpha;
         g[kAccUsed] = 1.0f;
       }
-      const float sum = wave_reduce16(g, lane);
+      const float sum = wave_reduce16_dpp(g, lane);
       if ((lane & 3) == 0) {
-        const int k = ((lane >> 5) & 1) * 8 + ((lane >> 4) & 1) * 4 + ((lane >> 3) & 1) * 2 +
-                      ((lane >> 2) & 1);
+        const int k = reduce16_slot(lane, swap_orient);
         if (sum != 0.0f) atomicAdd(&s_acc[j][k], sum);
       }
+    }
     }
     __syncthreads();
     // flush: lane l of wave-instruction `it` handles splat (it*16 + tid/16), slot tid%16
@@ -385,6 +535,9 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
 hipError_t launch_render_forward(const RenderArgs& a, hipStream_t s) {
   const uint32_t ntiles = a.gx * a.gy;
   if (ntiles == 0) return hipSuccess;
+  if (a.sched == 2)
+    hipLaunchKernelGGL(tile_schedule_kernel, dim3(1), dim3(kSchedThreads), 0, s, a.ranges,
+                       (const uint32_t*)nullptr, ntiles, a.order);
   if (a.include_feature)
     hipLaunchKernelGGL(render_fwd_kernel<true>, dim3(ntiles), dim3(kThreads), 0, s, a);
   else
@@ -397,12 +550,24 @@ hipError_t launch_render_backward(const RenderBwdArgs& a, hipStream_t s) {
   if (ntiles == 0) return hipSuccess;
   const bool extra = a.dL_ddepth != nullptr || a.dL_dalpha != nullptr;
   const bool feat = a.include_feature && a.dL_dfeature != nullptr;
-  if (feat)
-    hipLaunchKernelGGL((render_bwd_kernel<true, true>), dim3(ntiles), dim3(kThreads), 0, s, a);
-  else if (extra)
-    hipLaunchKernelGGL((render_bwd_kernel<true, false>), dim3(ntiles), dim3(kThreads), 0, s, a);
-  else
-    hipLaunchKernelGGL((render_bwd_kernel<false, false>), dim3(ntiles), dim3(kThreads), 0, s, a);
+  static const int group = [] {
+    const char* e = getenv("GSR_BWD_GROUP");
+    return (e && atoi(e) == 1) ? 1 : 4;
+  }();
+  if (a.sched == 2)  // backward work per tile ~ the replayed prefix (max n_contrib)
+    hipLaunchKernelGGL(tile_schedule_kernel, dim3(1), dim3(kSchedThreads), 0, s, a.ranges,
+                       a.tile_last, ntiles, a.order);
+#define GSR_BWD(E, F)                                                                             \
+  do {                                                                                           \
+    if (group == 1)                                                                              \
+      hipLaunchKernelGGL((render_bwd_kernel<E, F, 1>), dim3(ntiles), dim3(kThreads), 0, s, a);   \
+    else                                                                                         \
+      hipLaunchKernelGGL((render_bwd_kernel<E, F, 4>), dim3(ntiles), dim3(kThreads), 0, s, a);   \
+  } while (0)
+  if (feat) GSR_BWD(true, true);
+  else if (extra) GSR_BWD(true, false);
+  else GSR_BWD(false, false);
+#undef GSR_BWD
   return hipGetLastError();
 }
 
