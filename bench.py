@@ -4,8 +4,9 @@
 Workload (BASELINE.json configs[2] at N=1, configs[3] at N=8): 1,000,000 synthetic Gaussians
 (SH degree 3 evaluated in-kernel, language features on), LLFF-style cameras at 1008x756, and
 `--views-per-gpu` (default 6) camera views per GPU per step.  One step = for each of this rank's
-views: render() (activations + rasterizer forward with colour/depth/alpha/feature outputs) and the
-backward of fixed synthetic upstream gradients, accumulating per-Gaussian gradients; then, with
+views: render() (rasterizer forward with colour/depth/alpha/feature outputs; GaussianModel's
+activations fused into the kernels) and the backward of fixed synthetic upstream gradients,
+accumulating the raw parameters' gradients into their .grad; then, with
 N > 1, one bucketed SUM all-reduce of all gradients over RCCL.  Weak scaling: views per GPU fixed.
 
     python bench.py --gpus N --steps K --warmup W
@@ -80,6 +81,8 @@ def main():
     ap.add_argument("--cpu-baseline-views", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stage-timing", action="store_true")
+    ap.add_argument("--autograd-grads", action="store_true",
+                    help="return per-view raw grads to autograd instead of adding them into .grad")
     ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_r01.json"))
     args = ap.parse_args()
 
@@ -90,6 +93,7 @@ def main():
     import diff_gaussian_rasterization as dgr
     from gaussian_renderer import render
 
+    dgr.grad_into_leaves(not args.autograd_grads)
     rank, world, local = init_from_env("nccl")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
@@ -211,6 +215,9 @@ def main():
                        "sh_degree": deg, "views_per_gpu": args.views_per_gpu,
                        "views_per_step": n_views, "outputs": "rgb+depth+alpha+feature",
                        "parallelism": f"camera-sharded dp{world}",
+                       "raster_path": ("fused" if os.environ.get("GSR_FUSED", "1") != "0"
+                                       else "unfused"),
+                       "grad_mode": "autograd" if args.autograd_grads else "into_leaves",
                        "num_rendered_mean": int(R), "visible_mean": int(Pv), "tiles": T},
             "roofline": roofline,
             "cpu_baseline": cpu,

@@ -97,6 +97,55 @@ int gsr_rasterize_gaussians_backward(
     float* dL_dsh_language, float* dL_dlanguage_feature,
     void* stream, int debug);
 
+/* Fused-activation forward.  Same rasterization as gsr_rasterize_gaussians for the
+ * render() configuration that the reference runs by default (pipe.convert_SHs_python = False,
+ * pipe.compute_cov3D_python = False, override_color/override_language = None;
+ * gaussian_renderer/__init__.py:209-290), but reading GaussianModel's raw leaves directly:
+ *   features_dc[P,1,3], features_rest[P,M-1,3]   (instead of get_features = cat(...),
+ *                                                  scene/gaussian_model.py:159-162)
+ *   opacity_raw[P]      sigmoid in-kernel          (get_opacity, gaussian_model.py:38,172-173)
+ *   scaling_raw[P,3]    exp in-kernel              (get_scaling, gaussian_model.py:33,147-148)
+ *   rotation_raw[P,4]   normalize in-kernel        (get_rotation, gaussian_model.py:41,151-152;
+ *                                                  r / max(|r|, 1e-12) as F.normalize)
+ *   language_feature[P,3]  = shs_language           (get_language_feature, :175)
+ * Removes the cat/activation kernels PyTorch would launch around every view.  Outputs as above. */
+int gsr_rasterize_gaussians_fused(
+    int P, int M,
+    const float* background, const float* means3D,
+    const float* features_dc, const float* features_rest, const float* opacity_raw,
+    const float* scaling_raw, const float* rotation_raw, float scale_modifier,
+    const float* viewmatrix, const float* projmatrix,
+    float tan_fovx, float tan_fovy, int image_height, int image_width,
+    int degree, const float* campos, int prefiltered,
+    const float* language_feature, const float* confidence, int include_feature,
+    float* out_color, float* out_depth, float* out_alpha, float* out_feature, int* radii,
+    int* num_rendered,
+    gsr_alloc_fn alloc, void* alloc_ctx,
+    void* stream, int debug);
+
+/* Backward of gsr_rasterize_gaussians_fused: writes the gradients of the raw leaves
+ * (the chain through sigmoid / exp / normalize / cat is applied in-kernel).
+ * accumulate = 0: every element written (zeros for culled Gaussians), as the plain backward.
+ * accumulate = 1: visible Gaussians' grads are ADDED into the buffers and culled ones are left
+ *   untouched, so the buffers may be the leaves' .grad tensors across views of one step.
+ * dL_dmeans2D[P,3] is the screen-space gradient (the reference's means2D.grad). */
+int gsr_rasterize_gaussians_fused_backward(
+    int P, int M, int R,
+    const float* background, const float* means3D, const int* radii,
+    const float* features_dc, const float* features_rest, const float* opacity_raw,
+    const float* scaling_raw, const float* rotation_raw, float scale_modifier,
+    const float* viewmatrix, const float* projmatrix, float tan_fovx, float tan_fovy,
+    int image_height, int image_width,
+    const float* dL_dout_color, const float* dL_dout_depth, const float* dL_dout_alpha,
+    const float* dL_dout_feature,
+    int degree, const float* campos,
+    const float* language_feature, const float* confidence, int include_feature,
+    void* geom_buffer, void* binning_buffer, void* image_buffer,
+    float* dL_dmeans2D, float* dL_dmeans3D, float* dL_dfeatures_dc, float* dL_dfeatures_rest,
+    float* dL_dopacity_raw, float* dL_dscaling_raw, float* dL_drotation_raw,
+    float* dL_dlanguage_feature, int accumulate,
+    void* stream, int debug);
+
 /* Replaces _C.mark_visible -> markVisible (rasterize_points.cu:198-217) -> checkFrustum
  * (rasterizer_impl.cu:54-66): present[i] = view-space z > 0.2 (bool as uint8). */
 int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,

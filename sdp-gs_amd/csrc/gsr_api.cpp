@@ -190,18 +190,25 @@ size_t gsr_image_buffer_bytes(int H, int W) {
   return carve_img(nullptr, (size_t)(W > 0 ? W : 0), (size_t)(H > 0 ? H : 0)).bytes;
 }
 
-int gsr_rasterize_gaussians(int P, int M, const float* background, const float* means3D,
-                            const float* colors_precomp, const float* opacities,
-                            const float* scales, const float* rotations, float scale_modifier,
-                            const float* cov3D_precomp, const float* viewmatrix,
-                            const float* projmatrix, float tan_fovx, float tan_fovy,
-                            int image_height, int image_width, const float* sh, int degree,
-                            const float* campos, int prefiltered, const float* sh_language,
-                            const float* language_feature_precomp, const float* confidence,
-                            int include_feature, float* out_color, float* out_depth,
-                            float* out_alpha, float* out_feature, int* radii, int* num_rendered,
-                            gsr_alloc_fn alloc, void* alloc_ctx, void* stream_ptr, int debug) {
+// Shared forward.  fused != 0: opacities / scales / rotations are GaussianModel's raw
+// _opacity / _scaling / _rotation and the SH come split as sh_dc + sh_rest (activations in-kernel).
+static int forward_impl(int P, int M, const float* background, const float* means3D,
+                        const float* colors_precomp, const float* opacities, const float* scales,
+                        const float* rotations, float scale_modifier, const float* cov3D_precomp,
+                        const float* viewmatrix, const float* projmatrix, float tan_fovx,
+                        float tan_fovy, int image_height, int image_width, const float* sh,
+                        int degree, const float* campos, int prefiltered, const float* sh_language,
+                        const float* language_feature_precomp, const float* confidence,
+                        int include_feature, float* out_color, float* out_depth, float* out_alpha,
+                        float* out_feature, int* radii, int* num_rendered, gsr_alloc_fn alloc,
+                        void* alloc_ctx, void* stream_ptr, int debug, int fused,
+                        const float* sh_dc, const float* sh_rest) {
   g_err.clear();
+  if (fused) {
+    if (!sh_dc || (M > 1 && !sh_rest) || !scales || !rotations)
+      return fail(GSR_ERR_ARGUMENT, "fused path needs features_dc/_rest, _scaling, _rotation");
+    sh = sh_dc;  // "SH present" for the checks below; the kernels read sh_dc / sh_rest
+  }
   hipStream_t stream = (hipStream_t)stream_ptr;
   const int W = image_width, H = image_height;
   if (P < 0) return fail(GSR_ERR_ARGUMENT, "means3D must have dimensions (num_points, 3)");
@@ -261,6 +268,7 @@ int gsr_rasterize_gaussians(int P, int M, const float* background, const float* 
   pa.fx = (float)W / (2.0f * tan_fovx);
   pa.prefiltered = prefiltered; pa.include_feature = include_feature;
   pa.radii = radii_ptr; pa.g = g;
+  pa.fused = fused; pa.sh_dc = sh_dc; pa.sh_rest = sh_rest;
   PROF_BEGIN(PREPROCESS);
   GSR_CHECK(launch_preprocess(pa, stream));
   PROF_END(PREPROCESS);
@@ -319,7 +327,46 @@ int gsr_rasterize_gaussians(int P, int M, const float* background, const float* 
   return GSR_OK;
 }
 
-int gsr_rasterize_gaussians_backward(
+int gsr_rasterize_gaussians(int P, int M, const float* background, const float* means3D,
+                            const float* colors_precomp, const float* opacities,
+                            const float* scales, const float* rotations, float scale_modifier,
+                            const float* cov3D_precomp, const float* viewmatrix,
+                            const float* projmatrix, float tan_fovx, float tan_fovy,
+                            int image_height, int image_width, const float* sh, int degree,
+                            const float* campos, int prefiltered, const float* sh_language,
+                            const float* language_feature_precomp, const float* confidence,
+                            int include_feature, float* out_color, float* out_depth,
+                            float* out_alpha, float* out_feature, int* radii, int* num_rendered,
+                            gsr_alloc_fn alloc, void* alloc_ctx, void* stream_ptr, int debug) {
+  return forward_impl(P, M, background, means3D, colors_precomp, opacities, scales, rotations,
+                      scale_modifier, cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy,
+                      image_height, image_width, sh, degree, campos, prefiltered, sh_language,
+                      language_feature_precomp, confidence, include_feature, out_color, out_depth,
+                      out_alpha, out_feature, radii, num_rendered, alloc, alloc_ctx, stream_ptr,
+                      debug, 0, nullptr, nullptr);
+}
+
+int gsr_rasterize_gaussians_fused(int P, int M, const float* background, const float* means3D,
+                                  const float* features_dc, const float* features_rest,
+                                  const float* opacity_raw, const float* scaling_raw,
+                                  const float* rotation_raw, float scale_modifier,
+                                  const float* viewmatrix, const float* projmatrix, float tan_fovx,
+                                  float tan_fovy, int image_height, int image_width, int degree,
+                                  const float* campos, int prefiltered,
+                                  const float* language_feature, const float* confidence,
+                                  int include_feature, float* out_color, float* out_depth,
+                                  float* out_alpha, float* out_feature, int* radii,
+                                  int* num_rendered, gsr_alloc_fn alloc, void* alloc_ctx,
+                                  void* stream_ptr, int debug) {
+  return forward_impl(P, M, background, means3D, nullptr, opacity_raw, scaling_raw, rotation_raw,
+                      scale_modifier, nullptr, viewmatrix, projmatrix, tan_fovx, tan_fovy,
+                      image_height, image_width, nullptr, degree, campos, prefiltered,
+                      language_feature, nullptr, confidence, include_feature, out_color, out_depth,
+                      out_alpha, out_feature, radii, num_rendered, alloc, alloc_ctx, stream_ptr,
+                      debug, 1, features_dc, features_rest);
+}
+
+static int backward_impl(
     int P, int M, int R, const float* background, const float* means3D, const int* radii,
     const float* colors_precomp, const float* scales, const float* rotations, float scale_modifier,
     const float* cov3D_precomp, const float* viewmatrix, const float* projmatrix, float tan_fovx,
@@ -330,8 +377,14 @@ int gsr_rasterize_gaussians_backward(
     void* geom_buffer, void* binning_buffer, void* image_buffer, float* dL_dmeans2D,
     float* dL_dcolors, float* dL_dopacity, float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh,
     float* dL_dscales, float* dL_drotations, float* dL_dsh_language, float* dL_dlanguage_feature,
-    void* stream_ptr, int debug) {
+    void* stream_ptr, int debug, int fused, const float* sh_dc, const float* sh_rest,
+    const float* opacity_raw, float* dL_dsh_rest, int accumulate) {
   g_err.clear();
+  if (fused) {
+    if (!sh_dc || (M > 1 && (!sh_rest || !dL_dsh_rest)) || !scales || !rotations || !opacity_raw)
+      return fail(GSR_ERR_ARGUMENT, "fused backward needs the raw parameters and their grads");
+    sh = sh_dc;
+  }
   hipStream_t stream = (hipStream_t)stream_ptr;
   const int W = image_width, H = image_height;
   if (P < 0 || R < 0 || W <= 0 || H <= 0) return fail(GSR_ERR_ARGUMENT, "invalid sizes");
@@ -390,10 +443,57 @@ int gsr_rasterize_gaussians_backward(
   ba.dL_dmeans3D = dL_dmeans3D; ba.dL_dcov3D = dL_dcov3D; ba.dL_dsh = sh ? dL_dsh : nullptr;
   ba.dL_dscales = scales ? dL_dscales : nullptr; ba.dL_drotations = scales ? dL_drotations : nullptr;
   ba.dL_dsh_language = dL_dsh_language; ba.dL_dlanguage_feature = dL_dlanguage_feature;
+  ba.fused = fused; ba.accumulate = accumulate; ba.sh_dc = sh_dc; ba.sh_rest = sh_rest;
+  ba.opacities_raw = opacity_raw; ba.dL_dsh_rest = dL_dsh_rest;
   PROF_BEGIN(PREPROCESS_BWD);
   GSR_CHECK(launch_preprocess_backward(ba, stream));
   PROF_END(PREPROCESS_BWD);
   return GSR_OK;
+}
+
+int gsr_rasterize_gaussians_backward(
+    int P, int M, int R, const float* background, const float* means3D, const int* radii,
+    const float* colors_precomp, const float* scales, const float* rotations, float scale_modifier,
+    const float* cov3D_precomp, const float* viewmatrix, const float* projmatrix, float tan_fovx,
+    float tan_fovy, int image_height, int image_width, const float* dL_dout_color,
+    const float* dL_dout_depth, const float* dL_dout_alpha, const float* dL_dout_feature,
+    const float* sh, int degree, const float* campos, const float* sh_language,
+    const float* language_feature_precomp, const float* confidence, int include_feature,
+    void* geom_buffer, void* binning_buffer, void* image_buffer, float* dL_dmeans2D,
+    float* dL_dcolors, float* dL_dopacity, float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh,
+    float* dL_dscales, float* dL_drotations, float* dL_dsh_language, float* dL_dlanguage_feature,
+    void* stream_ptr, int debug) {
+  return backward_impl(P, M, R, background, means3D, radii, colors_precomp, scales, rotations,
+                       scale_modifier, cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy,
+                       image_height, image_width, dL_dout_color, dL_dout_depth, dL_dout_alpha,
+                       dL_dout_feature, sh, degree, campos, sh_language, language_feature_precomp,
+                       confidence, include_feature, geom_buffer, binning_buffer, image_buffer,
+                       dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh,
+                       dL_dscales, dL_drotations, dL_dsh_language, dL_dlanguage_feature, stream_ptr,
+                       debug, 0, nullptr, nullptr, nullptr, nullptr, 0);
+}
+
+int gsr_rasterize_gaussians_fused_backward(
+    int P, int M, int R, const float* background, const float* means3D, const int* radii,
+    const float* features_dc, const float* features_rest, const float* opacity_raw,
+    const float* scaling_raw, const float* rotation_raw, float scale_modifier,
+    const float* viewmatrix, const float* projmatrix, float tan_fovx, float tan_fovy,
+    int image_height, int image_width, const float* dL_dout_color, const float* dL_dout_depth,
+    const float* dL_dout_alpha, const float* dL_dout_feature, int degree, const float* campos,
+    const float* language_feature, const float* confidence, int include_feature,
+    void* geom_buffer, void* binning_buffer, void* image_buffer, float* dL_dmeans2D,
+    float* dL_dmeans3D, float* dL_dfeatures_dc, float* dL_dfeatures_rest, float* dL_dopacity_raw,
+    float* dL_dscaling_raw, float* dL_drotation_raw, float* dL_dlanguage_feature, int accumulate,
+    void* stream_ptr, int debug) {
+  return backward_impl(P, M, R, background, means3D, radii, nullptr, scaling_raw, rotation_raw,
+                       scale_modifier, nullptr, viewmatrix, projmatrix, tan_fovx, tan_fovy,
+                       image_height, image_width, dL_dout_color, dL_dout_depth, dL_dout_alpha,
+                       dL_dout_feature, nullptr, degree, campos, language_feature, nullptr,
+                       confidence, include_feature, geom_buffer, binning_buffer, image_buffer,
+                       dL_dmeans2D, nullptr, dL_dopacity_raw, dL_dmeans3D, nullptr,
+                       dL_dfeatures_dc, dL_dscaling_raw, dL_drotation_raw, dL_dlanguage_feature,
+                       nullptr, stream_ptr, debug, 1, features_dc, features_rest, opacity_raw,
+                       dL_dfeatures_rest, accumulate);
 }
 
 // ---- test hooks (include/gsr_testing.h) -----------------------------------------------------------

@@ -17,12 +17,30 @@ constexpr int kThreads = 256;
 __device__ __forceinline__ void put3(float* p, size_t i, V3 v) {
   p[3 * i] = v.x; p[3 * i + 1] = v.y; p[3 * i + 2] = v.z;
 }
+// store or accumulate (fused path with accumulate = 1 adds into existing .grad buffers)
+template <bool ACC>
+__device__ __forceinline__ void st(float* p, float v) {
+  if (ACC) *p += v; else *p = v;
+}
+template <bool ACC>
+__device__ __forceinline__ void st3(float* p, size_t i, V3 v) {
+  st<ACC>(p + 3 * i, v.x); st<ACC>(p + 3 * i + 1, v.y); st<ACC>(p + 3 * i + 2, v.z);
+}
 
 // backward.cu:20-139: writes dL/dsh for coefficient k < (deg+1)^2 and returns dL/dmean.
-__device__ V3 sh_backward(const float* __restrict__ s, int deg, V3 dir_orig, V3 dL_dRGB,
-                          float* __restrict__ d) {
-#define SH(k) v3(s[3 * (k)], s[3 * (k) + 1], s[3 * (k) + 2])
-#define PUT(k, v) do { V3 _t = (v); d[3 * (k)] = _t.x; d[3 * (k) + 1] = _t.y; d[3 * (k) + 2] = _t.z; } while (0)
+// s0/d0: coefficient 0 of this Gaussian, s1/d1: its coefficients 1.. (see sh_to_rgb).
+template <bool ACC>
+__device__ V3 sh_backward(const float* __restrict__ s0, const float* __restrict__ s1, int deg,
+                          V3 dir_orig, V3 dL_dRGB, float* __restrict__ d0,
+                          float* __restrict__ d1) {
+#define SH(k) ((k) == 0 ? v3(s0[0], s0[1], s0[2]) \
+                        : v3(s1[3 * ((k) - 1)], s1[3 * ((k) - 1) + 1], s1[3 * ((k) - 1) + 2]))
+#define PUT(k, v)                                                   \
+  do {                                                              \
+    V3 _t = (v);                                                    \
+    float* _d = (k) == 0 ? d0 : d1 + 3 * ((k) - 1);                 \
+    st<ACC>(_d, _t.x); st<ACC>(_d + 1, _t.y); st<ACC>(_d + 2, _t.z); \
+  } while (0)
   const float len = sqrtf(dot3(dir_orig, dir_orig));
   const V3 dir = v3(dir_orig.x / len, dir_orig.y / len, dir_orig.z / len);
   V3 dRGBdx = v3(0, 0, 0), dRGBdy = v3(0, 0, 0), dRGBdz = v3(0, 0, 0);
@@ -113,18 +131,26 @@ __device__ V3 sh_backward(const float* __restrict__ s, int deg, V3 dir_orig, V3 
             (-v.x * v.z * dv.x - v.y * v.z * dv.y + (sum2 - v.z * v.z) * dv.z) * invsum32);
 }
 
+template <bool ACC>
 __global__ __launch_bounds__(kThreads) void preprocess_bwd_kernel(BwdPreArgs a) {
   const int idx = (int)(blockIdx.x * kThreads + threadIdx.x);
   if (idx >= a.P) return;
   const size_t i = (size_t)idx;
   const int ncoef = a.M * 3;
   if (!(a.radii[idx] > 0)) {
+    if (ACC) return;  // nothing to add for a culled Gaussian
     put3(a.dL_dmeans2D, i, v3(0, 0, 0));
     if (a.dL_dcolors) put3(a.dL_dcolors, i, v3(0, 0, 0));
     a.dL_dopacity[i] = 0.0f;
     put3(a.dL_dmeans3D, i, v3(0, 0, 0));
     if (a.dL_dcov3D) for (int k = 0; k < 6; k++) a.dL_dcov3D[6 * i + k] = 0.0f;
-    if (a.dL_dsh) for (int k = 0; k < ncoef; k++) a.dL_dsh[i * ncoef + k] = 0.0f;
+    if (a.fused) {
+      if (a.dL_dsh) put3(a.dL_dsh, i, v3(0, 0, 0));
+      if (a.dL_dsh_rest)
+        for (int k = 0; k < ncoef - 3; k++) a.dL_dsh_rest[i * (ncoef - 3) + k] = 0.0f;
+    } else if (a.dL_dsh) {
+      for (int k = 0; k < ncoef; k++) a.dL_dsh[i * ncoef + k] = 0.0f;
+    }
     if (a.dL_dscales) put3(a.dL_dscales, i, v3(0, 0, 0));
     if (a.dL_drotations) reinterpret_cast<float4*>(a.dL_drotations)[i] = make_float4(0, 0, 0, 0);
     if (a.dL_dsh_language) put3(a.dL_dsh_language, i, v3(0, 0, 0));
@@ -136,10 +162,17 @@ __global__ __launch_bounds__(kThreads) void preprocess_bwd_kernel(BwdPreArgs a) 
   // slots: q0 = {mx, my, ca, cb}, q1 = {cc, op, r, g}, q2 = {b, depth, f0, f1}, q3 = {f2, used, -, -}
   const float gmx = q0.x, gmy = q0.y;
   const float dcx = q0.z, dcy = q0.w, dcz = q1.x;
-  put3(a.dL_dmeans2D, i, v3(gmx, gmy, 0.0f));
+  st3<ACC>(a.dL_dmeans2D, i, v3(gmx, gmy, 0.0f));
   const V3 dL_dcolor = v3(q1.z, q1.w, q2.x);
-  if (a.dL_dcolors) put3(a.dL_dcolors, i, dL_dcolor);
-  a.dL_dopacity[i] = a.confidence ? q1.y * a.confidence[i] : q1.y;
+  if (a.dL_dcolors) st3<ACC>(a.dL_dcolors, i, dL_dcolor);
+  {
+    float dop = a.confidence ? q1.y * a.confidence[i] : q1.y;
+    if (a.fused) {  // through get_opacity = sigmoid(_opacity): go * (1 - y) * y
+      const float y = sigmoid_f(a.opacities_raw[i]);
+      dop = dop * (1.0f - y) * y;
+    }
+    st<ACC>(a.dL_dopacity + i, dop);
+  }
 
   const V3 mean = v3(a.means3D[3 * i], a.means3D[3 * i + 1], a.means3D[3 * i + 2]);
   const float* c3 = a.cov3D + 6 * i;
@@ -174,7 +207,7 @@ __global__ __launch_bounds__(kThreads) void preprocess_bwd_kernel(BwdPreArgs a) 
   }
   if (a.dL_dcov3D) {
 #pragma unroll
-    for (int k = 0; k < 6; k++) a.dL_dcov3D[6 * i + k] = dcov[k];
+    for (int k = 0; k < 6; k++) st<ACC>(a.dL_dcov3D + 6 * i + k, dcov[k]);
   }
   const float dL_dT00 = 2 * (Tm(0, 0) * Vk(0, 0) + Tm(0, 1) * Vk(0, 1) + Tm(0, 2) * Vk(0, 2)) * dL_da +
                         (Tm(1, 0) * Vk(0, 0) + Tm(1, 1) * Vk(0, 1) + Tm(1, 2) * Vk(0, 2)) * dL_db;
@@ -217,8 +250,11 @@ __global__ __launch_bounds__(kThreads) void preprocess_bwd_kernel(BwdPreArgs a) 
   dmean = dmean + dm2;
 
   // ---- SH colour backward (backward.cu:390-391) ----
-  if (a.shs) {
-    float* d = a.dL_dsh + i * ncoef;
+  if (a.shs || a.fused) {
+    const float* s0 = a.fused ? a.sh_dc + 3 * i : a.shs + i * ncoef;
+    const float* s1 = a.fused ? a.sh_rest + i * (ncoef - 3) : s0 + 3;
+    float* d0 = a.fused ? a.dL_dsh + 3 * i : a.dL_dsh + i * ncoef;
+    float* d1 = a.fused ? a.dL_dsh_rest + i * (ncoef - 3) : d0 + 3;
     const uint8_t cl = a.clamped[i];
     V3 dRGB = dL_dcolor;
     dRGB.x *= (cl & 1) ? 0 : 1;
@@ -227,19 +263,24 @@ __global__ __launch_bounds__(kThreads) void preprocess_bwd_kernel(BwdPreArgs a) 
     const V3 dir_orig = mean - v3(a.campos[0], a.campos[1], a.campos[2]);
     const int deg = a.D;
     const int used = (deg + 1) * (deg + 1) * 3;
-    for (int k = used; k < ncoef; k++) d[k] = 0.0f;
-    dmean = dmean + sh_backward(a.shs + i * ncoef, deg, dir_orig, dRGB, d);
+    if (!ACC)
+      for (int k = used; k < ncoef; k++) d1[k - 3] = 0.0f;
+    dmean = dmean + sh_backward<ACC>(s0, s1, deg, dir_orig, dRGB, d0, d1);
   }
 
   // ---- cov3D -> scale / rotation (backward.cu:278-341, 393-395) ----
   if (a.scales) {
-    const float4 q = reinterpret_cast<const float4*>(a.rotations)[i];
+    const float4 qraw = reinterpret_cast<const float4*>(a.rotations)[i];
+    // fused: the kernel saw normalize(_rotation) and exp(_scaling) (gsr_preprocess.hip)
+    const float4 q = a.fused ? normalize_quat(qraw) : qraw;
     const float r = q.x, x = q.y, y = q.z, z = q.w;
     M3 R = m3_cols(1.f - 2.f * (y * y + z * z), 2.f * (x * y - r * z), 2.f * (x * z + r * y),
                    2.f * (x * y + r * z), 1.f - 2.f * (x * x + z * z), 2.f * (y * z - r * x),
                    2.f * (x * z - r * y), 2.f * (y * z + r * x), 1.f - 2.f * (x * x + y * y));
     M3 S = m3_cols(1, 0, 0, 0, 1, 0, 0, 0, 1);
-    const V3 s = a.scale_modifier * v3(a.scales[3 * i], a.scales[3 * i + 1], a.scales[3 * i + 2]);
+    V3 sc = v3(a.scales[3 * i], a.scales[3 * i + 1], a.scales[3 * i + 2]);
+    if (a.fused) sc = v3(expf(sc.x), expf(sc.y), expf(sc.z));
+    const V3 s = a.scale_modifier * sc;
     S.m[0][0] = s.x; S.m[1][1] = s.y; S.m[2][2] = s.z;
     const M3 Mm = m3_mul(S, R);
     const float* g6 = dcov;
@@ -257,7 +298,8 @@ __global__ __launch_bounds__(kThreads) void preprocess_bwd_kernel(BwdPreArgs a) 
     ds.x = dot3(v3(Rt.m[0][0], Rt.m[0][1], Rt.m[0][2]), v3(Dt.m[0][0], Dt.m[0][1], Dt.m[0][2]));
     ds.y = dot3(v3(Rt.m[1][0], Rt.m[1][1], Rt.m[1][2]), v3(Dt.m[1][0], Dt.m[1][1], Dt.m[1][2]));
     ds.z = dot3(v3(Rt.m[2][0], Rt.m[2][1], Rt.m[2][2]), v3(Dt.m[2][0], Dt.m[2][1], Dt.m[2][2]));
-    put3(a.dL_dscales, i, ds);
+    // fused: through exp (torch exp backward: grad * result)
+    st3<ACC>(a.dL_dscales, i, a.fused ? v3(ds.x * sc.x, ds.y * sc.y, ds.z * sc.z) : ds);
 #pragma unroll
     for (int w = 0; w < 3; w++) {
       Dt.m[0][w] *= s.x;
@@ -274,7 +316,14 @@ __global__ __launch_bounds__(kThreads) void preprocess_bwd_kernel(BwdPreArgs a) 
     dq.w = 2 * r * (D(0, 1) - D(1, 0)) + 2 * x * (D(2, 0) + D(0, 2)) + 2 * y * (D(1, 2) + D(2, 1)) -
            4 * z * (D(1, 1) + D(0, 0));
 #undef D
-    reinterpret_cast<float4*>(a.dL_drotations)[i] = dq;
+    if (a.fused) dq = normalize_quat_backward(qraw, dq);  // through F.normalize
+    float4* dr = reinterpret_cast<float4*>(a.dL_drotations) + i;
+    if (ACC) {
+      const float4 o = *dr;
+      *dr = make_float4(o.x + dq.x, o.y + dq.y, o.z + dq.z, o.w + dq.w);
+    } else {
+      *dr = dq;
+    }
   }
 
   // ---- depth channel: z_view = view[2] x + view[6] y + view[10] z + view[14] ----
@@ -282,12 +331,12 @@ __global__ __launch_bounds__(kThreads) void preprocess_bwd_kernel(BwdPreArgs a) 
   dmean.x += dz * a.view[2];
   dmean.y += dz * a.view[6];
   dmean.z += dz * a.view[10];
-  put3(a.dL_dmeans3D, i, dmean);
+  st3<ACC>(a.dL_dmeans3D, i, dmean);
 
   // ---- language feature channels ----
   if (a.dL_dlanguage_feature) {
-    put3(a.dL_dlanguage_feature, i,
-         (a.include_feature && a.lang_precomp) ? v3(q2.z, q2.w, q3.x) : v3(0, 0, 0));
+    st3<ACC>(a.dL_dlanguage_feature, i,
+             (a.include_feature && a.lang_precomp) ? v3(q2.z, q2.w, q3.x) : v3(0, 0, 0));
   }
   if (a.dL_dsh_language) {
     V3 out = v3(0, 0, 0);
@@ -301,7 +350,7 @@ __global__ __launch_bounds__(kThreads) void preprocess_bwd_kernel(BwdPreArgs a) 
       const float k2 = n > 0.0f ? ug / (den * den * n) : 0.0f;
       out = v3(SH_C0 * (g0 / den - u0 * k2), SH_C0 * (g1 / den - u1 * k2), SH_C0 * (g2 / den - u2 * k2));
     }
-    put3(a.dL_dsh_language, i, out);
+    st3<ACC>(a.dL_dsh_language, i, out);
   }
 }
 
@@ -309,8 +358,11 @@ __global__ __launch_bounds__(kThreads) void preprocess_bwd_kernel(BwdPreArgs a) 
 
 hipError_t launch_preprocess_backward(const BwdPreArgs& a, hipStream_t s) {
   if (a.P == 0) return hipSuccess;
-  hipLaunchKernelGGL(preprocess_bwd_kernel, dim3((a.P + kThreads - 1) / kThreads), dim3(kThreads),
-                     0, s, a);
+  const dim3 grid((a.P + kThreads - 1) / kThreads);
+  if (a.accumulate)
+    hipLaunchKernelGGL(preprocess_bwd_kernel<true>, grid, dim3(kThreads), 0, s, a);
+  else
+    hipLaunchKernelGGL(preprocess_bwd_kernel<false>, grid, dim3(kThreads), 0, s, a);
   return hipGetLastError();
 }
 

@@ -101,6 +101,27 @@ __device__ __forceinline__ void tile_rect(float px, float py, int r, uint32_t gx
   x1 = min((uint32_t)c, gx); y1 = min((uint32_t)d, gy);
 }
 
+// ---- GaussianModel activations (scene/gaussian_model.py:33-41), for the fused-activation path ----
+// torch.nn.functional.normalize(r, dim=1): r / max(||r||_2, 1e-12)
+__device__ __forceinline__ float quat_norm(float4 r) {
+  return sqrtf(r.x * r.x + r.y * r.y + r.z * r.z + r.w * r.w);
+}
+__device__ __forceinline__ float4 normalize_quat(float4 r) {
+  const float d = fmaxf(quat_norm(r), 1e-12f);
+  return make_float4(r.x / d, r.y / d, r.z / d, r.w / d);
+}
+// backward of normalize: dL/dr = go/d - (sum(go * r) / d^2) * r / n   (n = ||r||, d = max(n, eps))
+__device__ __forceinline__ float4 normalize_quat_backward(float4 r, float4 go) {
+  const float n = quat_norm(r);
+  const float d = fmaxf(n, 1e-12f);
+  const float s = (go.x * r.x + go.y * r.y + go.z * r.z + go.w * r.w) / (d * d);
+  const float k = (n > 1e-12f && n > 0.0f) ? s / n : 0.0f;
+  return make_float4(go.x / d - k * r.x, go.y / d - k * r.y, go.z / d - k * r.z,
+                     go.w / d - k * r.w);
+}
+// torch.sigmoid on float: 1 / (1 + exp(-x)); backward: go * (1 - y) * y
+__device__ __forceinline__ float sigmoid_f(float x) { return 1.0f / (1.0f + expf(-x)); }
+
 // ---- conservative splat / pixel-rectangle culling ----------------------------------------------
 // The blend skips a (splat, pixel) pair when alpha = min(0.99, op * exp(power)) < 1/255 with
 // power = -q/2, q = ca dx^2 + 2 cb dx dy + cc dy^2 (forward.cu:335-345).  A splat that fails that

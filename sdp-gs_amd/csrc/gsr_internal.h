@@ -125,6 +125,11 @@ struct PreArgs {
   int prefiltered, include_feature;
   int32_t* radii;
   GeomState g;
+  // fused-activation inputs (gsr_rasterize_gaussians_fused): when fused != 0, scales / rotations /
+  // opacities hold GaussianModel's raw _scaling (log), _rotation (unnormalised), _opacity (logit)
+  // and the SH coefficients come split as sh_dc [P,1,3] + sh_rest [P,M-1,3]
+  int fused;
+  const float *sh_dc, *sh_rest;
 };
 hipError_t launch_preprocess(const PreArgs& a, hipStream_t s);
 hipError_t launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present,
@@ -140,9 +145,16 @@ struct BwdPreArgs {
   const int32_t* radii;
   const uint8_t* clamped;
   const float* acc;
-  // outputs (every element written)
+  // outputs (every element written; with accumulate != 0 the grads of visible Gaussians are
+  // added into the buffers and culled Gaussians are left untouched)
   float *dL_dmeans2D, *dL_dcolors, *dL_dopacity, *dL_dmeans3D, *dL_dcov3D, *dL_dsh, *dL_dscales,
       *dL_drotations, *dL_dsh_language, *dL_dlanguage_feature;
+  // fused mode: inputs are raw parameters (see PreArgs) and the outputs are the raw-parameter
+  // grads: dL_dopacity -> d _opacity, dL_dscales -> d _scaling, dL_drotations -> d _rotation,
+  // dL_dsh -> d features_dc, dL_dsh_rest -> d features_rest
+  int fused, accumulate;
+  const float *sh_dc, *sh_rest, *opacities_raw;
+  float* dL_dsh_rest;
 };
 hipError_t launch_preprocess_backward(const BwdPreArgs& a, hipStream_t s);
 

@@ -20,9 +20,12 @@ namespace {
 constexpr int kThreads = 256;
 
 // forward.cu:20-71 (float32, same evaluation order as the CPU restatement)
-__device__ __forceinline__ V3 sh_to_rgb(const float* __restrict__ s, int deg, V3 dir,
-                                        uint8_t& clamped) {
-#define SH(k) v3(s[3 * (k)], s[3 * (k) + 1], s[3 * (k) + 2])
+// s0: coefficient 0 of this Gaussian, s1: its coefficients 1.. (contiguous); for the reference's
+// [P,M,3] layout s1 = s0 + 3, for the fused split layout s0 = features_dc, s1 = features_rest.
+__device__ __forceinline__ V3 sh_to_rgb(const float* __restrict__ s0, const float* __restrict__ s1,
+                                        int deg, V3 dir, uint8_t& clamped) {
+#define SH(k) ((k) == 0 ? v3(s0[0], s0[1], s0[2]) \
+                        : v3(s1[3 * ((k) - 1)], s1[3 * ((k) - 1) + 1], s1[3 * ((k) - 1) + 2]))
   V3 result = SH_C0 * SH(0);
   if (deg > 0) {
     const float x = dir.x, y = dir.y, z = dir.z;
@@ -77,9 +80,13 @@ __global__ __launch_bounds__(kThreads) void preprocess_kernel(PreArgs a) {
   if (a.cov3D_precomp) {
     c3 = a.cov3D_precomp + 6 * (size_t)idx;
   } else {
-    const float4 q = reinterpret_cast<const float4*>(a.rotations)[idx];
-    cov3d_from_scale_rot(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2],
-                         a.scale_modifier, q.x, q.y, q.z, q.w, c3buf);
+    float4 q = reinterpret_cast<const float4*>(a.rotations)[idx];
+    float sx = a.scales[3 * idx], sy = a.scales[3 * idx + 1], sz = a.scales[3 * idx + 2];
+    if (a.fused) {  // GaussianModel activations: exp(_scaling), normalize(_rotation)
+      sx = expf(sx); sy = expf(sy); sz = expf(sz);
+      q = normalize_quat(q);
+    }
+    cov3d_from_scale_rot(sx, sy, sz, a.scale_modifier, q.x, q.y, q.z, q.w, c3buf);
     float* dst = g.cov3D + 6 * (size_t)idx;
 #pragma unroll
     for (int k = 0; k < 6; k++) dst[k] = c3buf[k];
@@ -106,7 +113,9 @@ __global__ __launch_bounds__(kThreads) void preprocess_kernel(PreArgs a) {
     const float len = sqrtf(dot3(dir, dir));
     dir = v3(dir.x / len, dir.y / len, dir.z / len);
     uint8_t cl;
-    const V3 c = sh_to_rgb(a.shs + (size_t)idx * a.M * 3, a.D, dir, cl);
+    const float* s0 = a.fused ? a.sh_dc + 3 * (size_t)idx : a.shs + (size_t)idx * a.M * 3;
+    const float* s1 = a.fused ? a.sh_rest + (size_t)idx * (a.M - 1) * 3 : s0 + 3;
+    const V3 c = sh_to_rgb(s0, s1, a.D, dir, cl);
     g.clamped[idx] = cl;
     cr = c.x; cg = c.y; cb = c.z;
   } else {
@@ -115,6 +124,7 @@ __global__ __launch_bounds__(kThreads) void preprocess_kernel(PreArgs a) {
     cb = a.colors_precomp[3 * idx + 2];
   }
   float op = a.opacities[idx];
+  if (a.fused) op = sigmoid_f(op);  // GaussianModel.get_opacity
   if (a.confidence) op = op * a.confidence[idx];
   float f0 = 0.f, f1 = 0.f, f2 = 0.f;
   if (a.include_feature) {

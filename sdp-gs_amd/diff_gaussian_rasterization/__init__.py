@@ -23,7 +23,7 @@ if _PKG_ROOT not in sys.path:
 from gsr_amd import _lib  # noqa: E402
 
 __all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians",
-           "rasterize_gaussians_extended", "mark_visible"]
+           "rasterize_gaussians_extended", "rasterize_gaussians_fused", "mark_visible"]
 
 # instance count of the most recent forward (the reference keeps it in ctx.num_rendered only);
 # read by bench.py to compute per-kernel algorithmic bytes
@@ -228,6 +228,190 @@ class _RasterizeGaussians(torch.autograd.Function):
         # language_feature_precomp, opacities, scales, rotations, cov3Ds_precomp, raster_settings
         d_opac = d_opac.view(mt["op_shape"])
         return (d_means3D, d_means2D, d_sh, d_shl, d_colors, d_lfp, d_opac, d_sc, d_rot, d_cov, None)
+
+
+def rasterize_gaussians_fused(means3D, means2D, features_dc, features_rest, opacity_raw,
+                              scaling_raw, rotation_raw, language_feature, raster_settings):
+    """Fused-activation entry point (include/gsr.h gsr_rasterize_gaussians_fused).
+
+    Takes GaussianModel's raw leaves (_xyz, _features_dc, _features_rest, _opacity, _scaling,
+    _rotation, _language_feature; scene/gaussian_model.py:147-180) and applies get_features' cat,
+    sigmoid, exp and normalize inside the preprocess kernel; the backward returns the raw leaves'
+    gradients directly.  Same outputs as rasterize_gaussians_extended with
+    shs = get_features, opacities = get_opacity, scales = get_scaling, rotations = get_rotation,
+    shs_language = get_language_feature.
+    """
+    return _RasterizeGaussiansFused.apply(means3D, means2D, features_dc, features_rest, opacity_raw,
+                                          scaling_raw, rotation_raw, language_feature,
+                                          raster_settings)
+
+
+class _RasterizeGaussiansFused(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, means3D, means2D, features_dc, features_rest, opacity_raw, scaling_raw,
+                rotation_raw, language_feature, raster_settings):
+        rs = raster_settings
+        if means3D.ndim != 2 or means3D.shape[1] != 3:
+            raise RuntimeError("means3D must have dimensions (num_points, 3)")
+        dev = means3D.device
+        P = int(means3D.shape[0])
+        H, W = int(rs.image_height), int(rs.image_width)
+        include_feature = bool(getattr(rs, "include_feature", False))
+        m3 = _dev_f32(means3D, "means3D", dev)
+        dc = _dev_f32(features_dc, "features_dc", dev)
+        rest = _dev_f32(_opt(features_rest), "features_rest", dev)
+        op = _dev_f32(opacity_raw, "opacity", dev)
+        sc = _dev_f32(scaling_raw, "scaling", dev)
+        rot = _dev_f32(rotation_raw, "rotation", dev)
+        lf = _dev_f32(_opt(language_feature), "language_feature", dev) if include_feature else None
+        conf = _dev_f32(_opt(getattr(rs, "confidence", None)), "confidence", dev)
+        bg = _dev_f32(rs.bg, "bg", dev)
+        view = _dev_f32(rs.viewmatrix, "viewmatrix", dev)
+        proj = _dev_f32(rs.projmatrix, "projmatrix", dev)
+        campos = _dev_f32(rs.campos, "campos", dev)
+        if dc.numel() != 3 * P or (rest is not None and rest.numel() % (3 * max(P, 1))):
+            raise RuntimeError("features_dc must be [P,1,3] and features_rest [P,K,3]")
+        M = 1 + (rest.numel() // (3 * P) if rest is not None and P else 0)
+
+        fopts = dict(dtype=torch.float32, device=dev)
+        color = torch.empty((3, H, W), **fopts)
+        depth = torch.empty((1, H, W), **fopts)
+        alpha = torch.empty((1, H, W), **fopts)
+        feature = torch.empty((3, H, W), **fopts)
+        radii = torch.empty((P,), dtype=torch.int32, device=dev)
+        holder = _lib.BufferHolder(dev)
+        L = _lib.load()
+        nr = _lib.ctypes.c_int(0)
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        try:
+            with torch.cuda.device(dev):
+                rc = L.gsr_rasterize_gaussians_fused(
+                    P, M, _ptr(bg), _ptr(m3), _ptr(dc), _ptr(rest), _ptr(op), _ptr(sc), _ptr(rot),
+                    float(rs.scale_modifier), _ptr(view), _ptr(proj), float(rs.tanfovx),
+                    float(rs.tanfovy), H, W, int(rs.sh_degree), _ptr(campos),
+                    int(bool(rs.prefiltered)), _ptr(lf), _ptr(conf), int(include_feature),
+                    _ptr(color), _ptr(depth), _ptr(alpha), _ptr(feature), _ptr(radii),
+                    _lib.ctypes.byref(nr), _lib.alloc_callback(), holder.key, stream,
+                    int(bool(rs.debug)))
+            _lib.check(rc)
+        finally:
+            holder.release()
+        num_rendered = int(nr.value)
+        LAST_STATS["num_rendered"] = num_rendered
+        LAST_STATS["P"] = P
+
+        ctx.raster_settings = rs
+        ctx.num_rendered = num_rendered
+        # grad-into-leaves mode: only when every differentiable input is itself the float32
+        # contiguous leaf (then the kernel's pointer IS the parameter's storage)
+        leaves = (means3D, features_dc, features_rest, opacity_raw, scaling_raw, rotation_raw,
+                  language_feature)
+        used = (m3, dc, rest, op, sc, rot, lf)
+        ctx.leaves = None
+        if grad_into_leaves() and all(
+                t is None or (t.is_leaf and t.requires_grad and u is not None
+                              and u.data_ptr() == t.data_ptr())
+                for t, u in zip(leaves, used)):
+            ctx.leaves = leaves
+        ctx.meta = dict(P=P, M=M, H=H, W=W, include_feature=include_feature,
+                        has_rest=rest is not None, has_lf=lf is not None,
+                        shapes=(tuple(features_dc.shape),
+                                None if rest is None else tuple(features_rest.shape),
+                                tuple(opacity_raw.shape), tuple(scaling_raw.shape),
+                                tuple(rotation_raw.shape)))
+        empty = torch.empty(0, device=dev)
+        geom, binning, image = (b if b is not None else torch.empty(0, dtype=torch.uint8, device=dev)
+                                for b in holder.bufs)
+        ctx.save_for_backward(m3, radii, dc, rest if rest is not None else empty, op, sc, rot,
+                              lf if lf is not None else empty,
+                              conf if conf is not None else empty, bg, view, proj, campos,
+                              geom, binning, image)
+        ctx.mark_non_differentiable(radii)
+        return color, depth, alpha, feature, radii
+
+    @staticmethod
+    def backward(ctx, grad_color, grad_depth, grad_alpha, grad_feature, _grad_radii):
+        rs = ctx.raster_settings
+        mt = ctx.meta
+        (m3, radii, dc, rest, op, sc, rot, lf, conf, bg, view, proj, campos, geom, binning,
+         image) = ctx.saved_tensors
+        rest = rest if mt["has_rest"] else None
+        lf = lf if mt["has_lf"] else None
+        conf = conf if conf.numel() > 0 else None
+        P, M, H, W = mt["P"], mt["M"], mt["H"], mt["W"]
+        dev = m3.device
+
+        def g(t):
+            return None if t is None else t.contiguous().float()
+
+        dcol = g(grad_color)
+        if dcol is None:
+            dcol = torch.zeros((3, H, W), dtype=torch.float32, device=dev)
+        ddep, dalp = g(grad_depth), g(grad_alpha)
+        dfeat = g(grad_feature) if mt["include_feature"] else None
+        s_dc, s_rest, s_op, s_sc, s_rot = mt["shapes"]
+        fopts = dict(dtype=torch.float32, device=dev)
+        accumulate = ctx.leaves is not None
+        if accumulate:
+            # add straight into the parameters' .grad (created as zeros when absent, as
+            # AccumulateGrad would); culled Gaussians are not touched at all
+            grads = []
+            for t in ctx.leaves:
+                if t is not None and t.grad is None:
+                    t.grad = torch.zeros_like(t, memory_format=torch.contiguous_format)
+                grads.append(None if t is None else t.grad)
+            if any(gr is not None and not gr.is_contiguous() for gr in grads):
+                raise RuntimeError("grad-into-leaves needs contiguous .grad tensors")
+            d_means3D, d_dc, d_rest, d_op, d_sc, d_rot, d_lf = grads
+            d_means2D = torch.zeros((P, 3), **fopts)
+        else:
+            d_means2D = torch.empty((P, 3), **fopts)
+            d_means3D = torch.empty((P, 3), **fopts)
+            d_dc = torch.empty(s_dc, **fopts)
+            d_rest = torch.empty(s_rest, **fopts) if rest is not None else None
+            d_op = torch.empty(s_op, **fopts)
+            d_sc = torch.empty(s_sc, **fopts)
+            d_rot = torch.empty(s_rot, **fopts)
+            d_lf = torch.empty((P, 3), **fopts) if lf is not None else None
+        L = _lib.load()
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        with torch.cuda.device(dev):
+            rc = L.gsr_rasterize_gaussians_fused_backward(
+                P, M, ctx.num_rendered, _ptr(bg), _ptr(m3), _ptr(radii), _ptr(dc), _ptr(rest),
+                _ptr(op), _ptr(sc), _ptr(rot), float(rs.scale_modifier), _ptr(view), _ptr(proj),
+                float(rs.tanfovx), float(rs.tanfovy), H, W, _ptr(dcol), _ptr(ddep), _ptr(dalp),
+                _ptr(dfeat), int(rs.sh_degree), _ptr(campos), _ptr(lf), _ptr(conf),
+                int(mt["include_feature"]), _ptr(geom) if geom.numel() else None,
+                _ptr(binning) if binning.numel() else None, _ptr(image) if image.numel() else None,
+                _ptr(d_means2D), _ptr(d_means3D), _ptr(d_dc), _ptr(d_rest), _ptr(d_op),
+                _ptr(d_sc), _ptr(d_rot), _ptr(d_lf), int(accumulate), stream,
+                int(bool(rs.debug)))
+        _lib.check(rc)
+        # forward inputs: means3D, means2D, features_dc, features_rest, opacity_raw, scaling_raw,
+        # rotation_raw, language_feature, raster_settings
+        if accumulate:
+            return None, d_means2D, None, None, None, None, None, None, None
+        return d_means3D, d_means2D, d_dc, d_rest, d_op, d_sc, d_rot, d_lf, None
+
+
+_GRAD_INTO_LEAVES = None
+
+
+def grad_into_leaves(enable: Optional[bool] = None) -> bool:
+    """Query / set the fused path's grad-into-leaves mode (default: env GSR_GRAD_INTO_LEAVES=1).
+
+    When on, and the fused entry point receives the model's leaf tensors themselves, the backward
+    kernel adds the raw-parameter gradients of the visible Gaussians straight into each leaf's
+    .grad (include/gsr.h accumulate = 1) and returns None for them, instead of materialising
+    fresh [P,...] gradients that autograd then adds view by view.  loss.backward() +
+    optimizer.step() see identical .grad values; torch.autograd.grad() on those leaves and
+    per-leaf grad hooks do not (they are bypassed), hence opt-in."""
+    global _GRAD_INTO_LEAVES
+    if enable is not None:
+        _GRAD_INTO_LEAVES = bool(enable)
+    if _GRAD_INTO_LEAVES is None:
+        _GRAD_INTO_LEAVES = os.environ.get("GSR_GRAD_INTO_LEAVES", "0") == "1"
+    return _GRAD_INTO_LEAVES
 
 
 class GaussianRasterizationSettings(NamedTuple):

@@ -16,8 +16,30 @@ _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if _PKG_ROOT not in sys.path:
     sys.path.insert(0, _PKG_ROOT)
 
-from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer  # noqa: E402
+from diff_gaussian_rasterization import (GaussianRasterizationSettings, GaussianRasterizer,  # noqa: E402
+                                         rasterize_gaussians_fused)
 from gsr_amd.sh import eval_sh  # noqa: E402
+
+_RAW = ("_features_dc", "_features_rest", "_opacity", "_scaling", "_rotation")
+
+
+def _fused_eligible(pc, pipe, opt, override_color, override_language) -> bool:
+    """True when render() would hand the rasterizer exactly get_features / get_opacity /
+    get_scaling / get_rotation / get_language_feature of a model with GaussianModel's standard
+    activations (scene/gaussian_model.py:33-41), so the fused entry point is equivalent.
+    GSR_FUSED=0 forces the unfused path."""
+    if os.environ.get("GSR_FUSED", "1") == "0":
+        return False
+    if pipe.compute_cov3D_python or pipe.convert_SHs_python or override_color is not None:
+        return False
+    if opt.include_feature and (override_language is not None
+                                or getattr(pc, "_language_feature", None) is None):
+        return False
+    if not all(isinstance(getattr(pc, n, None), torch.Tensor) for n in _RAW):
+        return False
+    return (getattr(pc, "scaling_activation", None) is torch.exp
+            and getattr(pc, "opacity_activation", None) is torch.sigmoid
+            and getattr(pc, "rotation_activation", None) is torch.nn.functional.normalize)
 
 
 def render(viewpoint_camera, pc, pipe, bg_color: torch.Tensor, opt, scaling_modifier=1.0,
@@ -49,6 +71,24 @@ def render(viewpoint_camera, pc, pipe, bg_color: torch.Tensor, opt, scaling_modi
         confidence=confidence,
         debug=pipe.debug)
     rasterizer = GaussianRasterizer(raster_settings=raster_settings)
+
+    if _fused_eligible(pc, pipe, opt, override_color, override_language):
+        # Default configuration: the activations / cat of GaussianModel's getters run inside the
+        # preprocess kernel and the backward writes the raw leaves' grads (identical outputs).
+        lang = pc._language_feature if opt.include_feature else None
+        rendered_image, rendered_depth, rendered_alpha, language_feature_image, radii = \
+            rasterize_gaussians_fused(xyz, screenspace_points, pc._features_dc,
+                                      pc._features_rest, pc._opacity, pc._scaling, pc._rotation,
+                                      lang, raster_settings)
+        return {"render": rendered_image,
+                "depth": rendered_depth,
+                "alpha": rendered_alpha,
+                "opacity": pc.get_opacity,
+                "feature": language_feature_image,
+                "viewspace_points": screenspace_points,
+                "visibility_filter": radii > 0,
+                "radii": radii,
+                "color": None}
 
     means3D = xyz
     means2D = screenspace_points

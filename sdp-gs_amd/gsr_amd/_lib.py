@@ -71,6 +71,34 @@ def load():
             _p, _p, _p,                  # geom, binning, image buffers
             _p, _p, _p, _p, _p, _p, _p, _p, _p, _p,  # grads
             _p, _i]                      # stream, debug
+        L.gsr_rasterize_gaussians_fused.restype = _i
+        L.gsr_rasterize_gaussians_fused.argtypes = [
+            _i, _i,                      # P, M
+            _p, _p,                      # bg, means3D
+            _p, _p, _p,                  # features_dc, features_rest, opacity_raw
+            _p, _p, _f,                  # scaling_raw, rotation_raw, scale_modifier
+            _p, _p,                      # view, proj
+            _f, _f, _i, _i,              # tanfovx, tanfovy, H, W
+            _i, _p, _i,                  # degree, campos, prefiltered
+            _p, _p, _i,                  # language_feature, confidence, include_feature
+            _p, _p, _p, _p, _p,          # out_color, out_depth, out_alpha, out_feature, radii
+            ctypes.POINTER(_i),          # num_rendered
+            ALLOC_FN, _p,                # alloc, alloc_ctx
+            _p, _i]                      # stream, debug
+        L.gsr_rasterize_gaussians_fused_backward.restype = _i
+        L.gsr_rasterize_gaussians_fused_backward.argtypes = [
+            _i, _i, _i,                  # P, M, R
+            _p, _p, _p,                  # bg, means3D, radii
+            _p, _p, _p,                  # features_dc, features_rest, opacity_raw
+            _p, _p, _f,                  # scaling_raw, rotation_raw, scale_modifier
+            _p, _p, _f, _f, _i, _i,      # view, proj, tanfovx, tanfovy, H, W
+            _p, _p, _p, _p,              # dL_dcolor, dL_ddepth, dL_dalpha, dL_dfeature
+            _i, _p,                      # degree, campos
+            _p, _p, _i,                  # language_feature, confidence, include_feature
+            _p, _p, _p,                  # geom, binning, image buffers
+            _p, _p, _p, _p, _p, _p, _p, _p,  # grads: means2D, means3D, dc, rest, op, scale, rot, lang
+            _i,                          # accumulate
+            _p, _i]                      # stream, debug
         L.gsr_mark_visible.restype = _i
         L.gsr_mark_visible.argtypes = [_i, _p, _p, _p, _p, _p]
         for n in ("gsr_geom_buffer_bytes", "gsr_binning_buffer_bytes"):

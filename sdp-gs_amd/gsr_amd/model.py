@@ -42,6 +42,11 @@ def build_covariance_from_scaling_rotation(scaling, scaling_modifier, rotation):
 class SplatModel:
     """Leaf tensors in GaussianModel's raw parameterisation with its activation getters."""
 
+    # scene/gaussian_model.py:33-41 (setup_functions)
+    scaling_activation = staticmethod(torch.exp)
+    opacity_activation = staticmethod(torch.sigmoid)
+    rotation_activation = staticmethod(torch.nn.functional.normalize)
+
     def __init__(self, params: GaussianParams, device="cuda", active_sh_degree=None):
         p = params.to(device)
         self.max_sh_degree = p.max_sh_degree
@@ -65,15 +70,15 @@ class SplatModel:
 
     @property
     def get_scaling(self):
-        return torch.exp(self._scaling)
+        return self.scaling_activation(self._scaling)
 
     @property
     def get_rotation(self):
-        return torch.nn.functional.normalize(self._rotation)
+        return self.rotation_activation(self._rotation)
 
     @property
     def get_opacity(self):
-        return torch.sigmoid(self._opacity)
+        return self.opacity_activation(self._opacity)
 
     @property
     def get_features(self):

@@ -43,7 +43,9 @@ def test_render_dict_and_grads():
     assert vs is not None and vs[:, :2].abs().sum() > 0 and torch.all(vs[:, 2] == 0)
 
 
-def test_python_and_kernel_sh_paths_agree():
+def test_python_and_kernel_sh_paths_agree(monkeypatch):
+    # both sides with torch's activations (the fused path's in-kernel sigmoid differs by ulps)
+    monkeypatch.setenv("GSR_FUSED", "0")
     render, m, cam = _setup()
     bg = torch.tensor([0.1, 0.2, 0.3], device="cuda")
     a = render(cam, m, Pipe(sh_py=True), bg, Opt())
@@ -62,3 +64,74 @@ def test_python_covariance_path_agrees():
     same = (a["radii"] == b["radii"]).float().mean().item()
     assert same > 0.999
     assert (a["render"] - b["render"]).abs().mean().item() < 1e-5
+
+
+def _leaf_grads(m):
+    return [p.grad.clone() for p in m.parameters()]
+
+
+def _zero(m):
+    for p in m.parameters():
+        p.grad = None
+
+
+@pytest.mark.parametrize("conf", [False, True])
+def test_fused_activation_path_matches_unfused(monkeypatch, conf):
+    """render() default config -> gsr_rasterize_gaussians_fused (sigmoid / exp / normalize / cat
+    in-kernel) vs GSR_FUSED=0 (torch getters + gsr_rasterize_gaussians): same images, same raw
+    gradients up to the ulp-level difference of torch's vs the kernel's activation arithmetic."""
+    import gaussian_renderer as gr
+    render, m, cam = _setup()
+    if conf:
+        m.confidence = torch.rand_like(m.confidence)
+    bg = torch.tensor([0.1, 0.2, 0.3], device="cuda")
+    pipe = Pipe(sh_py=False, conf=conf)
+    assert gr._fused_eligible(m, pipe, Opt(), None, None)
+    outs = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("GSR_FUSED", fused)
+        _zero(m)
+        pkg = render(cam, m, pipe, bg, Opt())
+        g = torch.Generator(device="cuda").manual_seed(3)
+        loss = ((pkg["render"] * torch.rand(pkg["render"].shape, device="cuda", generator=g)).sum()
+                + (pkg["depth"] * 0.01).sum() + pkg["alpha"].sum() + pkg["feature"].sum())
+        loss.backward()
+        outs.append((pkg, _leaf_grads(m), pkg["viewspace_points"].grad.clone()))
+    (a, ga, va), (b, gb, vb) = outs
+    same = (a["radii"] == b["radii"]).float().mean().item()
+    assert same > 0.9999
+    for k in ("render", "depth", "alpha", "feature"):
+        torch.testing.assert_close(a[k], b[k], atol=1e-4, rtol=1e-4)
+    names = ["xyz", "f_dc", "f_rest", "scaling", "rotation", "opacity", "language"]
+    for n, x, y in zip(names, ga, gb):
+        scale = y.abs().max().item() + 1e-12
+        err = (x - y).abs().max().item() / scale
+        assert err < 2e-3, (n, err)
+    torch.testing.assert_close(va, vb, atol=1e-3 * vb.abs().max().item(), rtol=1e-3)
+
+
+def test_grad_into_leaves_equals_autograd_accumulation():
+    """Fused backward with accumulate = 1 (grads added into the leaves' .grad) over three views
+    equals autograd's own accumulation of the per-view gradients, bit for bit."""
+    import diff_gaussian_rasterization as dgr
+    render, m, _ = _setup()
+    cams = [c.to("cuda") for c in make_cameras(3, 200, 150, seed=1)]
+    bg = torch.zeros(3, device="cuda")
+    res = []
+    try:
+        for mode in (False, True):
+            dgr.grad_into_leaves(mode)
+            _zero(m)
+            vs = []
+            for c in cams:
+                pkg = render(c, m, Pipe(sh_py=False), bg, Opt())
+                (pkg["render"].sum() + pkg["feature"].sum() + pkg["depth"].mean()).backward()
+                vs.append(pkg["viewspace_points"].grad.clone())
+            res.append((_leaf_grads(m), vs))
+    finally:
+        dgr.grad_into_leaves(False)
+    (ga, va), (gb, vb) = res
+    for x, y in zip(ga, gb):
+        assert torch.equal(x, y)
+    for x, y in zip(va, vb):
+        assert torch.equal(x, y)
