@@ -112,7 +112,8 @@ def test_fused_activation_path_matches_unfused(monkeypatch, conf):
 
 def test_grad_into_leaves_equals_autograd_accumulation():
     """Fused backward with accumulate = 1 (grads added into the leaves' .grad) over three views
-    equals autograd's own accumulation of the per-view gradients, bit for bit."""
+    equals autograd's own accumulation of the per-view gradients (to float-atomic ordering: the
+    blend backward's global atomics, like the reference's, are not order-deterministic)."""
     import diff_gaussian_rasterization as dgr
     render, m, _ = _setup()
     cams = [c.to("cuda") for c in make_cameras(3, 200, 150, seed=1)]
@@ -131,7 +132,5 @@ def test_grad_into_leaves_equals_autograd_accumulation():
     finally:
         dgr.grad_into_leaves(False)
     (ga, va), (gb, vb) = res
-    for x, y in zip(ga, gb):
-        assert torch.equal(x, y)
-    for x, y in zip(va, vb):
-        assert torch.equal(x, y)
+    for x, y in zip(ga + va, gb + vb):
+        torch.testing.assert_close(x, y, rtol=1e-4, atol=1e-5 * y.abs().max().item())
