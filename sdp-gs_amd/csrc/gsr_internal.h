@@ -25,7 +25,7 @@ enum AccSlot : int {
   kAccR = 6, kAccG = 7, kAccB = 8,        // dL/dcolor
   kAccDepth = 9,                          // dL/ddepth (view-space z)
   kAccF0 = 10, kAccF1 = 11, kAccF2 = 12,  // dL/dfeature
-  kAccUsed = 13
+  kAccUsed = 13                           // reserved (always 0); slots 14, 15 unused
 };
 
 inline size_t align_up(size_t x) { return (x + kAlign - 1) & ~(kAlign - 1); }

@@ -394,9 +394,16 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
   }
   // backward.cu:531-533: only the colour channels see the background
   const float bg_dot = a.bg[0] * dpix[0] + a.bg[1] * dpix[1] + a.bg[2] * dpix[2];
-  float accum_rec[NC], last_color[NC];
-#pragma unroll
-  for (int c = 0; c < NC; c++) { accum_rec[c] = 0.0f; last_color[c] = 0.0f; }
+  // the bg term of dL/dalpha is -T_final / (1 - alpha) * bg_dot: with a zero background it is a
+  // signed zero, so its division is skipped (bit-identical) -- workgroup-uniform test
+  const bool has_bg = a.bg[0] != 0.0f || a.bg[1] != 0.0f || a.bg[2] != 0.0f;
+  // backward.cu:502-520 keeps one accum_rec per channel and forms
+  //   dL_dalpha = sum_c (col_c - accum_rec_c) * dpix_c.
+  // By linearity only the projection onto dpix is needed:
+  //   acc_dot' = last_alpha * last_cdot + (1 - last_alpha) * acc_dot,  cdot = sum_c col_c dpix_c,
+  //   dL_dalpha = cdot - acc_dot'
+  // (the same recurrence on one scalar instead of NC channels; equal up to float rounding)
+  float acc_dot = 0.0f, last_cdot = 0.0f;
   float last_alpha = 0.0f;
   const float ddelx_dx = (float)(0.5 * a.W);
   const float ddely_dy = (float)(0.5 * a.H);
@@ -474,13 +481,12 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
           const float4 r3 = s_r3[j];
           col[5 % NC] = r2.z; col[6 % NC] = r2.w; col[7 % NC] = r3.x;
         }
-        float dL_dalpha = 0.0f;
+        float cdot = 0.0f;
 #pragma unroll
-        for (int c = 0; c < NC; c++) {
-          accum_rec[c] = last_alpha * last_color[c] + (1.f - last_alpha) * accum_rec[c];
-          last_color[c] = col[c];
-          dL_dalpha += (col[c] - accum_rec[c]) * dpix[c];
-        }
+        for (int c = 0; c < NC; c++) cdot += col[c] * dpix[c];
+        acc_dot = last_alpha * last_cdot + (1.f - last_alpha) * acc_dot;
+        last_cdot = cdot;
+        float dL_dalpha = cdot - acc_dot;
         g[kAccR] = dchannel_dcolor * dpix[0];
         g[kAccG] = dchannel_dcolor * dpix[1];
         g[kAccB] = dchannel_dcolor * dpix[2];
@@ -492,7 +498,7 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
         }
         dL_dalpha *= T;
         last_alpha = alpha;
-        dL_dalpha += (-T_final / (1.f - alpha)) * bg_dot;
+        if (has_bg) dL_dalpha += (-T_final / (1.f - alpha)) * bg_dot;
         const float dL_dG = r1.y * dL_dalpha;
         const float gdx = G * dx;
         const float gdy = G * dy;
@@ -504,7 +510,6 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
         g[kAccCb] = -0.5f * gdx * dy * dL_dG;
         g[kAccCc] = -0.5f * gdy * dy * dL_dG;
         g[kAccOp] = G * dL_dalpha;
-        g[kAccUsed] = 1.0f;
       }
       const float sum = wave_reduce16_dpp(g, lane);
       if ((lane & 3) == 0) {

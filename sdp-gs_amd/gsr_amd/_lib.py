@@ -13,7 +13,8 @@ import threading
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libgsr.so")
+# GSR_LIB_PATH selects an alternative in-tree build (A/B experiments of compile flags)
+LIB_PATH = os.environ.get("GSR_LIB_PATH") or os.path.join(_HERE, "libgsr.so")
 
 _f = ctypes.c_float
 _i = ctypes.c_int
