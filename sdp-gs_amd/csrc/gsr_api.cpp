@@ -39,8 +39,7 @@ GeomState carve_geom(char* base, size_t P) {
   g.tiles_touched = c.take<uint32_t>(P);
   g.offsets = c.take<uint32_t>(P);
   g.acc = c.take<float>((size_t)kAccFloats * P);
-  g.sort_hist = c.take<uint32_t>(sort_hist_len(P));
-  g.sort_parts = c.take<uint32_t>(scan_parts(sort_hist_len(P)) + 1);
+  g.sort = take_sort_scratch(c, P);
   g.scan_parts = c.take<uint32_t>(scan_parts(P) + 1);
   g.bytes = c.size();
   return g;
@@ -53,8 +52,7 @@ BinState carve_bin(char* base, size_t R) {
   b.tval_a = c.take<uint32_t>(R);
   b.tkey_b = c.take<uint32_t>(R);
   b.tval_b = c.take<uint32_t>(R);
-  b.hist = c.take<uint32_t>(sort_hist_len(R));
-  b.parts = c.take<uint32_t>(scan_parts(sort_hist_len(R)) + 1);
+  b.sort = take_sort_scratch(c, R);
   b.bytes = c.size();
   return b;
 }
@@ -241,8 +239,7 @@ static int forward_impl(int P, int M, const float* background, const float* mean
 
   const uint32_t gx = (uint32_t)((W + kTile - 1) / kTile), gy = (uint32_t)((H + kTile - 1) / kTile);
   const uint32_t ntiles = gx * gy;
-  if (scan_parts((size_t)P) > (size_t)kScanMaxParts ||
-      scan_parts(sort_hist_len((size_t)P)) > (size_t)kScanMaxParts)
+  if (scan_parts((size_t)P) > (size_t)kScanMaxParts)
     return fail(GSR_ERR_TOO_LARGE, "P = %d exceeds the scan capacity", P);
 
   const size_t gbytes = carve_geom(nullptr, (size_t)P).bytes;
@@ -276,7 +273,7 @@ static int forward_impl(int P, int M, const float* background, const float* mean
   bool in_b = false;
   PROF_BEGIN(DEPTH_SORT);
   GSR_CHECK(radix_sort_pairs(g.dkey_a, g.dval_a, g.dkey_b, g.dval_b, (size_t)P, 32,
-                             SortScratch{g.sort_hist, g.sort_parts}, &in_b, stream));
+                             g.sort, &in_b, stream));
   PROF_END(DEPTH_SORT);
   const uint32_t* order = in_b ? g.dval_b : g.dval_a;
   PROF_BEGIN(SCAN);
@@ -287,11 +284,13 @@ static int forward_impl(int P, int M, const float* background, const float* mean
   if (!host) return fail(GSR_ERR_HIP, "pinned host allocation failed");
   GSR_CHECK(hipMemcpyAsync(host, g.offsets + (P - 1), 4, hipMemcpyDeviceToHost, stream));
   GSR_CHECK(hipMemcpyAsync(host + 1, g.flags, 4, hipMemcpyDeviceToHost, stream));
+  GSR_CHECK(hipMemcpyAsync(host + 2, g.sort.aux + kSortAuxErr, 4, hipMemcpyDeviceToHost, stream));
   GSR_CHECK(hipStreamSynchronize(stream));
   const uint32_t R = host[0];
+  if (host[2]) return fail(GSR_ERR_HIP, "depth sort look-back timed out");
   if (host[1]) return fail(GSR_ERR_PREFILTERED,
                            "Point is filtered although prefiltered is set. This shouldn't happen!");
-  if (R > 0x7fffffffu || scan_parts(sort_hist_len(R)) > (size_t)kScanMaxParts)
+  if (R > 0x7fffffffu)
     return fail(GSR_ERR_TOO_LARGE, "num_rendered = %u exceeds the sort capacity", R);
 
   const size_t bbytes = carve_bin(nullptr, R).bytes;
@@ -305,8 +304,13 @@ static int forward_impl(int P, int M, const float* background, const float* mean
   bool t_in_b = false;
   PROF_BEGIN(TILE_SORT);
   GSR_CHECK(radix_sort_pairs(b.tkey_a, b.tval_a, b.tkey_b, b.tval_b, R, tile_bits(ntiles),
-                             SortScratch{b.hist, b.parts}, &t_in_b, stream));
+                             b.sort, &t_in_b, stream));
   PROF_END(TILE_SORT);
+  if (debug) {
+    GSR_CHECK(hipMemcpyAsync(host + 2, b.sort.aux + kSortAuxErr, 4, hipMemcpyDeviceToHost, stream));
+    GSR_CHECK(hipStreamSynchronize(stream));
+    if (host[2]) return fail(GSR_ERR_HIP, "tile sort look-back timed out");
+  }
   const uint32_t* tiles_sorted = t_in_b ? b.tkey_b : b.tkey_a;
   const uint32_t* point_list = t_in_b ? b.tval_b : b.tval_a;
   PROF_BEGIN(RANGES);
@@ -502,11 +506,10 @@ static size_t sort_scratch_layout(char* base, size_t n, uint32_t** kb, uint32_t*
   Carver c(base);
   uint32_t* a = c.take<uint32_t>(n);
   uint32_t* b = c.take<uint32_t>(n);
-  uint32_t* h = c.take<uint32_t>(sort_hist_len(n));
-  uint32_t* p = c.take<uint32_t>(scan_parts(sort_hist_len(n)) + 1);
+  SortScratch s = take_sort_scratch(c, n);
   if (kb) *kb = a;
   if (vb) *vb = b;
-  if (sc) *sc = SortScratch{h, p};
+  if (sc) *sc = s;
   return c.size();
 }
 
@@ -521,12 +524,17 @@ int gsr_test_radix_sort_pairs(uint32_t* keys, uint32_t* vals, size_t n, int bits
   const int debug = 0;
   if (n == 0) return GSR_OK;
   if (!keys || !vals || !scratch || bits < 0 || bits > 32) return fail(GSR_ERR_ARGUMENT, "bad args");
-  if (scan_parts(sort_hist_len(n)) > (size_t)kScanMaxParts) return fail(GSR_ERR_TOO_LARGE, "n too large");
+  if (n > 0xffffffffull) return fail(GSR_ERR_TOO_LARGE, "n too large");
   uint32_t *kb, *vb;
   SortScratch sc;
   sort_scratch_layout((char*)scratch, n, &kb, &vb, &sc);
   bool in_b = false;
   GSR_CHECK(radix_sort_pairs(keys, vals, kb, vb, n, bits, sc, &in_b, stream));
+  uint32_t* host = pinned_slot();
+  if (!host) return fail(GSR_ERR_HIP, "pinned host allocation failed");
+  GSR_CHECK(hipMemcpyAsync(host + 2, sc.aux + kSortAuxErr, 4, hipMemcpyDeviceToHost, stream));
+  GSR_CHECK(hipStreamSynchronize(stream));
+  if (host[2]) return fail(GSR_ERR_HIP, "radix sort look-back timed out");
   if (in_b) {
     GSR_CHECK(hipMemcpyAsync(keys, kb, n * 4, hipMemcpyDeviceToDevice, stream));
     GSR_CHECK(hipMemcpyAsync(vals, vb, n * 4, hipMemcpyDeviceToDevice, stream));

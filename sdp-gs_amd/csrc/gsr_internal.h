@@ -51,13 +51,25 @@ constexpr int kSortTile = 4096;       // keys per radix-sort workgroup (256 thre
 
 inline size_t scan_parts(size_t n) { return (n + kScanTile - 1) / kScanTile; }
 inline size_t sort_blocks(size_t n) { return (n + kSortTile - 1) / kSortTile; }
-inline size_t sort_hist_len(size_t n) { return 256 * sort_blocks(n); }
 inline int sort_passes(int bits) { return (bits + 7) / 8; }
+constexpr int kSortMaxPasses = 4;
+// u64 look-back status words: one per (pass, partition, digit)
+inline size_t sort_status_len(size_t n) { return (size_t)kSortMaxPasses * sort_blocks(n) * 256; }
+// u32 aux words: digit totals [kSortMaxPasses][256], partition tickets [kSortMaxPasses][8],
+// error flag
+constexpr size_t kSortAuxTotals = 0, kSortAuxTickets = kSortMaxPasses * 256,
+                 kSortAuxErr = kSortAuxTickets + 8 * kSortMaxPasses, kSortAuxLen = kSortAuxErr + 4;
 
 struct SortScratch {
-  uint32_t* hist;   // [256 * blocks]
-  uint32_t* parts;  // scan partials of hist
+  uint64_t* status;  // [sort_status_len(n)]
+  uint32_t* aux;     // [kSortAuxLen]; aux[kSortAuxErr] != 0 after a sort = look-back timeout
 };
+inline SortScratch take_sort_scratch(Carver& c, size_t n) {
+  SortScratch s;
+  s.aux = c.take<uint32_t>(kSortAuxLen);
+  s.status = c.take<uint64_t>(sort_status_len(n));  // follows aux: one memset clears both
+  return s;
+}
 
 // Exclusive (inclusive=false) or inclusive prefix sum of n u32 values; if gather != nullptr the
 // input element i is in[gather[i]].  parts: scratch of scan_parts(n) u32.
@@ -65,6 +77,7 @@ hipError_t scan_u32(const uint32_t* in, const uint32_t* gather, uint32_t* out, s
                     bool inclusive, uint32_t* parts, hipStream_t s);
 // Stable LSD radix sort of (key, value) u32 pairs over key bits [0, bits).  Ping-pongs between
 // (ka, va) and (kb, vb); returns through *result_in_b whether the sorted data ended in (kb, vb).
+// One-sweep passes: 1 memset + 1 digit-totals launch + 1 launch per 8-bit digit.
 hipError_t radix_sort_pairs(uint32_t* ka, uint32_t* va, uint32_t* kb, uint32_t* vb, size_t n,
                             int bits, SortScratch scratch, bool* result_in_b, hipStream_t s);
 
@@ -83,8 +96,7 @@ struct GeomState {
   uint32_t* offsets;        // [P] inclusive scan of tiles_touched in depth order
   float* acc;               // [P*16] backward accumulators
   uint32_t* flags;          // [4]  [0]: prefiltered violation
-  uint32_t* sort_hist;
-  uint32_t* sort_parts;
+  SortScratch sort;         // depth-sort scratch
   uint32_t* scan_parts;
   size_t bytes;
 };
@@ -95,8 +107,7 @@ struct BinState {
   uint32_t* tval_a;  // [R] Gaussian ids
   uint32_t* tkey_b;
   uint32_t* tval_b;
-  uint32_t* hist;
-  uint32_t* parts;
+  SortScratch sort;  // tile-sort scratch
   size_t bytes;
 };
 BinState carve_bin(char* base, size_t R);

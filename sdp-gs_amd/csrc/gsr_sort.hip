@@ -5,10 +5,10 @@
 // toolkit 11.6 per environment.yml:6).  The sort must be STABLE: the reference breaks equal-depth
 // ties by emission order, i.e. by Gaussian index.
 //
-// Design: reduce-then-scan (3 launches, no inter-workgroup hand-off, hence no agent-scope
-// release/acquire protocol to get wrong), and a 3-launch radix pass (histogram -> scan ->
-// scatter) whose in-workgroup ranking uses wave64 ballots ("match" of the 8-bit digit) instead of
-// shared-memory per-thread counters.
+// Design: the prefix sum is reduce-then-scan (3 launches, no inter-workgroup hand-off); the radix
+// sort is one-sweep (one launch per 8-bit pass with a decoupled look-back over agent-scope status
+// words, see below), whose in-workgroup ranking uses wave64 ballots ("match" of the digit)
+// instead of shared-memory per-thread counters.
 #include "gsr_internal.h"
 
 namespace gsr {
@@ -16,7 +16,6 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kScanItems = kScanTile / kThreads;   // 8
-constexpr int kSortRounds = kSortTile / kThreads;  // 16
 
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
 
@@ -129,72 +128,182 @@ __device__ __forceinline__ uint64_t match_digit(uint32_t d, bool valid, int bits
   return valid ? m : 0ull;
 }
 
-__global__ __launch_bounds__(kThreads) void radix_hist_kernel(const uint32_t* __restrict__ keys,
-                                                              size_t n, int shift, int bits,
-                                                              uint32_t* __restrict__ hist,
-                                                              uint32_t nblocks) {
-  __shared__ uint32_t cnt[256];
-  cnt[threadIdx.x] = 0;
+// ---- one-sweep LSD radix sort ---------------------------------------------------------------------
+// Per sort: one memset (digit totals, partition tickets, look-back status), one launch computing
+// the digit totals of EVERY pass from the unsorted keys (a permutation does not change them), and
+// one launch per 8-bit pass that ranks, scans and scatters in a single sweep:
+//   * a workgroup takes a ticket (atomic counter) = its partition of kSortTile keys, so every
+//     partition it may wait for belongs to a workgroup that is already running;
+//   * it ranks its keys stably (wave64 ballot "match" of the digit, per-wave running counts in
+//     LDS), publishes its per-digit counts as AGGREGATE, then each thread (= one digit) walks back
+//     over the predecessors' status words until an INCLUSIVE prefix, and publishes its own
+//     INCLUSIVE prefix (decoupled look-back);
+//   * the keys are re-ordered in LDS by digit and written out in runs, so that consecutive lanes
+//     store consecutive addresses of one digit bucket.
+// Status word (u64): bits 32-33 flag (0 = not yet published, 1 = aggregate, 2 = inclusive),
+// bits 0-31 count.  Polling is bounded: after kSpinLimit empty polls a thread gives up, raises
+// the error word (checked by the host at its next synchronisation) and proceeds, so no wave can
+// hang the device.
+constexpr uint64_t kStAgg = 1ull << 32, kStIncl = 2ull << 32, kStFlags = 3ull << 32;
+constexpr int kSpinLimit = 1 << 18;
+constexpr int kLookback = 16;
+constexpr int kKeysPerThread = kSortTile / kThreads;  // 16
+constexpr int kKeysPerWave = kKeysPerThread * 64;     // 1024
+
+__global__ __launch_bounds__(kThreads) void radix_totals_kernel(const uint32_t* __restrict__ keys,
+                                                                size_t n, int bits,
+                                                                uint32_t* __restrict__ totals) {
+  __shared__ uint32_t cnt[kSortMaxPasses][256];
+#pragma unroll
+  for (int p = 0; p < kSortMaxPasses; p++) cnt[p][threadIdx.x] = 0;
   __syncthreads();
-  const uint32_t mask = (1u << bits) - 1u;
-  const int lane = lane_id();
+  const int passes = (bits + 7) / 8;
   const size_t base = (size_t)blockIdx.x * kSortTile;
-  for (int r = 0; r < kSortRounds; r++) {
+  // all loads of the partition in flight before any is consumed
+  uint32_t key[kKeysPerThread];
+#pragma unroll
+  for (int r = 0; r < kKeysPerThread; r++) {
     const size_t i = base + (size_t)r * kThreads + threadIdx.x;
-    const bool valid = i < n;
-    const uint32_t d = valid ? (keys[i] >> shift) & mask : 0u;
-    const uint64_t peers = match_digit(d, valid, bits);
-    if (valid && (__ffsll((long long)peers) - 1) == lane) atomicAdd(&cnt[d], (uint32_t)__popcll(peers));
+    key[r] = i < n ? keys[i] : 0u;
+  }
+#pragma unroll
+  for (int r = 0; r < kKeysPerThread; r++) {
+    const bool valid = base + (size_t)r * kThreads + threadIdx.x < n;
+    const uint64_t vmask = __ballot(valid);
+    if (vmask == 0ull) continue;
+    for (int p = 0; p < passes; p++) {
+      const uint32_t d = (key[r] >> (8 * p)) & 0xffu;
+      // typical depth keys share their top byte across a wave: one LDS add instead of 64
+      // serialised same-address atomics
+      const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
+      if (__ballot(valid && d != d0) == 0ull) {
+        if ((threadIdx.x & 63) == 0) atomicAdd(&cnt[p][d0], (uint32_t)__popcll(vmask));
+      } else if (valid) {
+        atomicAdd(&cnt[p][d], 1u);
+      }
+    }
   }
   __syncthreads();
-  hist[(size_t)threadIdx.x * nblocks + blockIdx.x] = cnt[threadIdx.x];
+  for (int p = 0; p < passes; p++) {
+    const uint32_t c = cnt[p][threadIdx.x];
+    if (c) atomicAdd(&totals[p * 256 + threadIdx.x], c);
+  }
 }
 
-__global__ __launch_bounds__(kThreads) void radix_scatter_kernel(
+__device__ __forceinline__ uint64_t status_load(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void status_store(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(kThreads) void radix_onesweep_kernel(
     const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin, size_t n, int shift,
-    int bits, const uint32_t* __restrict__ hist_scanned, uint32_t nblocks,
-    uint32_t* __restrict__ kout, uint32_t* __restrict__ vout) {
-  __shared__ uint32_t running[256];
-  __shared__ uint32_t cnt[4][256];
-  __shared__ uint32_t wbase[4][256];
-  const int lane = lane_id();
-  const int wid = (int)(threadIdx.x >> 6);
+    int bits, const uint32_t* __restrict__ totals, uint32_t* __restrict__ ticket,
+    uint64_t* __restrict__ status, uint32_t* __restrict__ err, uint32_t* __restrict__ kout,
+    uint32_t* __restrict__ vout) {
+  __shared__ uint32_t s_k[kSortTile];
+  __shared__ uint32_t s_v[kSortTile];
+  __shared__ uint32_t s_cnt[kThreads / 64][256];
+  __shared__ uint32_t s_gofs[256];
+  __shared__ uint32_t s_scan[kThreads / 64];
+  __shared__ uint32_t s_part;
+  const int t = (int)threadIdx.x, lane = t & 63, wid = t >> 6;
   const uint32_t mask = (1u << bits) - 1u;
-  running[threadIdx.x] = hist_scanned[(size_t)threadIdx.x * nblocks + blockIdx.x];
-  const size_t base = (size_t)blockIdx.x * kSortTile;
+  // ticket, not blockIdx: a partition can only wait on partitions whose workgroups already run
+  // (a per-XCD ticket variant timed out its look-back on gfx950 -- dispatch order across XCDs
+  // gives no such guarantee)
+  if (t == 0) s_part = atomicAdd(ticket, 1u);
+#pragma unroll
+  for (int w = 0; w < kThreads / 64; w++) s_cnt[w][t] = 0;
+  __syncthreads();
+  const uint32_t part = s_part;
+  const size_t base = (size_t)part * kSortTile;
+  const size_t wbase = base + (size_t)wid * kKeysPerWave;
+
+  uint32_t key[kKeysPerThread], val[kKeysPerThread];
+#pragma unroll
+  for (int r = 0; r < kKeysPerThread; r++) {
+    const size_t i = wbase + (size_t)r * 64 + lane;
+    key[r] = i < n ? kin[i] : 0u;
+    val[r] = i < n ? vin[i] : 0u;
+  }
+  // stable rank inside the wave's 1024 consecutive keys
   const uint64_t lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
-  for (int r = 0; r < kSortRounds; r++) {
-    const size_t i = base + (size_t)r * kThreads + threadIdx.x;
-    if (base + (size_t)r * kThreads >= n) break;  // workgroup-uniform
-    const bool valid = i < n;
-    const uint32_t k = valid ? kin[i] : 0u;
-    const uint32_t v = valid ? vin[i] : 0u;
-    const uint32_t d = (k >> shift) & mask;
-    cnt[0][threadIdx.x] = 0;
-    cnt[1][threadIdx.x] = 0;
-    cnt[2][threadIdx.x] = 0;
-    cnt[3][threadIdx.x] = 0;
-    __syncthreads();
+  uint32_t rk[kKeysPerThread];
+#pragma unroll
+  for (int r = 0; r < kKeysPerThread; r++) {
+    const bool valid = wbase + (size_t)r * 64 + lane < n;
+    const uint32_t d = (key[r] >> shift) & mask;
     const uint64_t peers = match_digit(d, valid, bits);
-    const uint32_t rank = (uint32_t)__popcll(peers & lt);
-    if (valid && (__ffsll((long long)peers) - 1) == lane) cnt[wid][d] = (uint32_t)__popcll(peers);
-    __syncthreads();
-    {
-      const uint32_t dd = threadIdx.x;
-      const uint32_t c0 = cnt[0][dd], c1 = cnt[1][dd], c2 = cnt[2][dd], c3 = cnt[3][dd];
-      const uint32_t b0 = running[dd];
-      wbase[0][dd] = b0;
-      wbase[1][dd] = b0 + c0;
-      wbase[2][dd] = b0 + c0 + c1;
-      wbase[3][dd] = b0 + c0 + c1 + c2;
-      running[dd] = b0 + c0 + c1 + c2 + c3;
+    const uint32_t before = s_cnt[wid][d];
+    rk[r] = before + (uint32_t)__popcll(peers & lt);
+    if (valid && (__ffsll((long long)peers) - 1) == lane) s_cnt[wid][d] = before + (uint32_t)__popcll(peers);
+  }
+  __syncthreads();
+  // thread t <-> digit t
+  const uint32_t c0 = s_cnt[0][t], c1 = s_cnt[1][t], c2 = s_cnt[2][t], c3 = s_cnt[3][t];
+  const uint32_t h = c0 + c1 + c2 + c3;
+  uint64_t* my = status + (size_t)part * 256 + t;
+  status_store(my, (part == 0 ? kStIncl : kStAgg) | (uint64_t)h);
+  uint32_t total_n;
+  const uint32_t lstart = block_excl_scan<kThreads / 64>(h, s_scan, total_n);
+  const uint32_t dbase = block_excl_scan<kThreads / 64>(totals[t], s_scan, total_n);
+  s_cnt[0][t] = lstart;
+  s_cnt[1][t] = lstart + c0;
+  s_cnt[2][t] = lstart + c0 + c1;
+  s_cnt[3][t] = lstart + c0 + c1 + c2;
+  uint32_t excl = 0;
+  if (part > 0) {
+    // windowed look-back: kLookback predecessors' words are loaded together (independent
+    // loads in flight) and consumed in order up to the first INCLUSIVE one or the first word not
+    // yet published (then re-polled from there); partition 0 is always INCLUSIVE, so the walk
+    // ends there at the latest
+    int spins = 0;
+    int64_t q = (int64_t)part - 1;
+    for (;;) {
+      uint64_t w[kLookback];
+#pragma unroll
+      for (int j = 0; j < kLookback; j++)
+        w[j] = (q - j >= 0) ? status_load(status + (size_t)(q - j) * 256 + t) : kStIncl;
+      int used = 0;
+      bool done = false, stop = false;
+#pragma unroll
+      for (int j = 0; j < kLookback; j++) {  // branch-free so that w[] stays in registers
+        const uint64_t f = w[j] & kStFlags;
+        const bool take = !stop && f != 0;
+        excl += take ? (uint32_t)w[j] : 0u;
+        used = take ? j + 1 : used;
+        done = done || (take && f == kStIncl);
+        stop = stop || !take || f == kStIncl;
+      }
+      if (done) break;
+      q -= used;
+      if (used < kLookback) {
+        if (++spins > kSpinLimit) { atomicOr(err, 1u); break; }
+        __builtin_amdgcn_s_sleep(1);
+      }
     }
-    __syncthreads();
-    if (valid) {
-      const uint32_t pos = wbase[wid][d] + rank;
-      kout[pos] = k;
-      vout[pos] = v;
+    status_store(my, kStIncl | (uint64_t)(excl + h));
+  }
+  s_gofs[t] = dbase + excl - lstart;
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < kKeysPerThread; r++) {
+    if (wbase + (size_t)r * 64 + lane < n) {
+      const uint32_t d = (key[r] >> shift) & mask;
+      const uint32_t pos = s_cnt[wid][d] + rk[r];
+      s_k[pos] = key[r];
+      s_v[pos] = val[r];
     }
+  }
+  __syncthreads();
+  const uint32_t nvalid = (uint32_t)min((size_t)kSortTile, n - base);
+  for (uint32_t i = (uint32_t)t; i < nvalid; i += kThreads) {
+    const uint32_t k = s_k[i];
+    const uint32_t o = s_gofs[(k >> shift) & mask] + i;
+    kout[o] = k;
+    vout[o] = s_v[i];
   }
 }
 
@@ -223,18 +332,24 @@ hipError_t radix_sort_pairs(uint32_t* ka, uint32_t* va, uint32_t* kb, uint32_t* 
                             int bits, SortScratch scratch, bool* result_in_b, hipStream_t s) {
   *result_in_b = false;
   if (n == 0 || bits <= 0) return hipSuccess;
+  if (bits > 32 || n > 0xffffffffull) return hipErrorInvalidValue;
+  const int passes = sort_passes(bits);
   const uint32_t nb = (uint32_t)sort_blocks(n);
-  const size_t hl = sort_hist_len(n);
+  // aux (totals, tickets, error word) and the status words of the passes used: one memset
+  const size_t clear = (size_t)((char*)(scratch.status + (size_t)passes * nb * 256) - (char*)scratch.aux);
+  hipError_t e = hipMemsetAsync(scratch.aux, 0, clear, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(radix_totals_kernel, dim3(nb), dim3(kThreads), 0, s, ka, n, bits,
+                     scratch.aux + kSortAuxTotals);
   uint32_t *kin = ka, *vin = va, *kout = kb, *vout = vb;
   bool in_b = false;
-  for (int shift = 0; shift < bits; shift += 8) {
+  for (int p = 0; p < passes; p++) {
+    const int shift = 8 * p;
     const int dbits = (bits - shift) < 8 ? (bits - shift) : 8;
-    hipLaunchKernelGGL(radix_hist_kernel, dim3(nb), dim3(kThreads), 0, s, kin, n, shift, dbits,
-                       scratch.hist, nb);
-    hipError_t e = scan_u32(scratch.hist, nullptr, scratch.hist, hl, false, scratch.parts, s);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(radix_scatter_kernel, dim3(nb), dim3(kThreads), 0, s, kin, vin, n, shift,
-                       dbits, scratch.hist, nb, kout, vout);
+    hipLaunchKernelGGL(radix_onesweep_kernel, dim3(nb), dim3(kThreads), 0, s, kin, vin, n, shift,
+                       dbits, scratch.aux + kSortAuxTotals + 256 * p,
+                       scratch.aux + kSortAuxTickets + 8 * p, scratch.status + (size_t)p * nb * 256,
+                       scratch.aux + kSortAuxErr, kout, vout);
     uint32_t* t;
     t = kin; kin = kout; kout = t;
     t = vin; vin = vout; vout = t;

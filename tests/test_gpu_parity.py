@@ -172,14 +172,22 @@ def test_forward_is_deterministic():
         np.testing.assert_array_equal(a[name], b[name])
 
 
-@pytest.mark.parametrize("n,bits", [(1, 8), (4095, 13), (4097, 32), (1_000_003, 32), (3_000_000, 13)])
-def test_radix_sort_sorted_and_stable(n, bits):
+@pytest.mark.parametrize("n,bits,kind", [(1, 8, "int"), (4095, 13, "int"), (4097, 32, "int"),
+                                         (1_000_003, 32, "int"), (3_000_000, 13, "int"),
+                                         (8191, 4, "int"), (1_000_000, 32, "depth"),
+                                         (2_500_000, 12, "tiles")])
+def test_radix_sort_sorted_and_stable(n, bits, kind):
+    """One-sweep radix sort (gsr_sort.hip) == numpy's stable argsort, bit for bit: full 32-bit
+    keys, float-bit depth keys (shared top bytes), skewed tile ids, partial last partitions."""
     from gsr_amd import _lib
     L = _lib.load()
     rng = np.random.default_rng(n)
-    keys = rng.integers(0, 1 << min(bits, 31), size=n, dtype=np.int64).astype(np.uint32)
-    if bits < 32:
-        keys &= np.uint32((1 << bits) - 1)
+    if kind == "depth":
+        keys = rng.lognormal(1.0, 0.5, size=n).astype(np.float32).view(np.uint32) + 0
+    elif kind == "tiles":
+        keys = np.minimum(rng.exponential(300.0, size=n), (1 << bits) - 1).astype(np.uint32)
+    else:
+        keys = rng.integers(0, 1 << bits, size=n, dtype=np.uint64).astype(np.uint32)
     keys[: n // 3] = keys[0]  # many ties
     vals = np.arange(n, dtype=np.uint32)
     k = torch.tensor(keys.view(np.int32), device="cuda")
