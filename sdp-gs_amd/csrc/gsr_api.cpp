@@ -404,6 +404,8 @@ static int backward_impl(
     return fail(GSR_ERR_ARGUMENT, "rotations / dL_drotations must be 16-byte aligned");
   if (sh && (degree < 0 || degree > 3 || (degree + 1) * (degree + 1) > M))
     return fail(GSR_ERR_ARGUMENT, "invalid sh degree %d for M = %d", degree, M);
+  if (sh && M > 16)  // the backward stages at most 16 coefficients per Gaussian in LDS
+    return fail(GSR_ERR_ARGUMENT, "sh has M = %d coefficients; at most 16 (degree 3) supported", M);
   if (dL_dsh_language && !sh_language && !language_feature_precomp && include_feature)
     ;  // nothing to differentiate: zeros are written
 

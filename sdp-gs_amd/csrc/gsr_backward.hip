@@ -27,21 +27,24 @@ __device__ __forceinline__ void st3(float* p, size_t i, V3 v) {
   st<ACC>(p + 3 * i, v.x); st<ACC>(p + 3 * i + 1, v.y); st<ACC>(p + 3 * i + 2, v.z);
 }
 
-// backward.cu:20-139: writes dL/dsh for coefficient k < (deg+1)^2 into dsh and returns dL/dmean.
-// sh / dsh: this Gaussian's row of the LDS staging buffer (coefficient k at 3k..3k+2).  The used
-// coefficients are read into registers first, so dsh may alias sh (the kernel works in place).
-__device__ __forceinline__ V3 sh_backward(const float* sh, int deg, V3 dir_orig, V3 dL_dRGB,
-                                          float* dsh) {
+// backward.cu:20-139: writes dL/dsh for coefficient k < (deg+1)^2 and returns dL/dmean.
+// s0: coefficient 0 of this Gaussian, s1: its coefficients 1.. (rows of the LDS staging planes);
+// the gradients go to the same places.  The used coefficients are read into registers first, so
+// the computation is in place.
+__device__ __forceinline__ V3 sh_backward(float* s0, float* s1, int deg, V3 dir_orig,
+                                          V3 dL_dRGB) {
   V3 c[16];
   const int ncoef_used = (deg + 1) * (deg + 1);
+  c[0] = v3(s0[0], s0[1], s0[2]);
 #pragma unroll
-  for (int k = 0; k < 16; k++)
-    c[k] = k < ncoef_used ? v3(sh[3 * k], sh[3 * k + 1], sh[3 * k + 2]) : v3(0, 0, 0);
+  for (int k = 1; k < 16; k++)
+    c[k] = k < ncoef_used ? v3(s1[3 * k - 3], s1[3 * k - 2], s1[3 * k - 1]) : v3(0, 0, 0);
 #define SH(k) c[k]
-#define PUT(k, v)                                       \
-  do {                                                  \
-    V3 _t = (v);                                        \
-    dsh[3 * (k)] = _t.x; dsh[3 * (k) + 1] = _t.y; dsh[3 * (k) + 2] = _t.z; \
+#define PUT(k, v)                                                   \
+  do {                                                              \
+    V3 _t = (v);                                                    \
+    float* _d = (k) == 0 ? s0 : s1 + 3 * (k) - 3;                   \
+    _d[0] = _t.x; _d[1] = _t.y; _d[2] = _t.z;                       \
   } while (0)
   const float len = sqrtf(dot3(dir_orig, dir_orig));
   const V3 dir = v3(dir_orig.x / len, dir_orig.y / len, dir_orig.z / len);
@@ -147,10 +150,11 @@ __device__ __forceinline__ void zero_outputs(const BwdPreArgs& a, size_t i) {
   if (a.dL_dlanguage_feature) put3(a.dL_dlanguage_feature, i, v3(0, 0, 0));
 }
 
-// Backward of one visible Gaussian.  shrow: its row of the LDS staging buffer (SH coefficients
-// in, SH gradients out; unused without SH).
+// Backward of one visible Gaussian.  sh0 / sh1: its rows (coefficient 0 / coefficients 1..) of
+// the LDS staging planes: SH coefficients in, SH gradients out; unused without SH.
 template <bool ACC>
-__device__ __forceinline__ void gaussian_bwd(const BwdPreArgs& a, size_t i, float* shrow) {
+__device__ __forceinline__ void gaussian_bwd(const BwdPreArgs& a, size_t i, float* sh0,
+                                             float* sh1) {
   const float4* accp = reinterpret_cast<const float4*>(a.acc + i * kAccFloats);
   const float4 q0 = accp[0], q1 = accp[1], q2 = accp[2], q3 = accp[3];
   // slots: q0 = {mx, my, ca, cb}, q1 = {cc, op, r, g}, q2 = {b, depth, f0, f1}, q3 = {f2, used, -, -}
@@ -251,7 +255,7 @@ __device__ __forceinline__ void gaussian_bwd(const BwdPreArgs& a, size_t i, floa
     dRGB.y *= (cl & 2) ? 0 : 1;
     dRGB.z *= (cl & 4) ? 0 : 1;
     const V3 dir_orig = mean - v3(a.campos[0], a.campos[1], a.campos[2]);
-    dmean = dmean + sh_backward(shrow, a.D, dir_orig, dRGB, shrow);
+    dmean = dmean + sh_backward(sh0, sh1, a.D, dir_orig, dRGB);
   }
 
   // ---- cov3D -> scale / rotation (backward.cu:278-341, 393-395) ----
@@ -340,123 +344,95 @@ __device__ __forceinline__ void gaussian_bwd(const BwdPreArgs& a, size_t i, floa
   }
 }
 
-// Row width of the SH staging buffer: at most 16 coefficients x 3, padded to an odd stride so
-// that lane-strided row accesses (lane t -> row t) hit distinct LDS banks.
-constexpr int kShStride = 49;
+// ---- SH staging ----------------------------------------------------------------------------------
+// A workgroup's SH data is one contiguous segment per plane in global memory (fused: features_dc
+// w = 3 floats per Gaussian and features_rest w = 3(M-1); reference layout: sh w = 3M).  Each plane
+// is copied into LDS with the SAME layout, as 16-byte vectors (ds_write_b128 / ds_read_b128 at
+// consecutive addresses: no bank conflicts, no index arithmetic), kBatch vectors in flight per
+// lane.  The per-Gaussian compute then reads its row at stride w (odd for the fused planes, so
+// lane-strided access is conflict-free), works in place, and the gradient plane goes back the
+// same way (ACC: read-add-write).  A vector spans at most two rows (w >= 3); vectors whose rows
+// are all culled are skipped in ACC mode.
+constexpr int kShMaxFloats = 48;  // 16 coefficients x 3 per Gaussian (M <= 16, checked by the API)
+constexpr int kBatch = 4;
 
-// One "plane" of SH data in global memory: row g of the workgroup's Gaussians holds `w` floats
-// at src + (base + g) * w and maps to columns [col, col + w) of the LDS row; only the first
-// `used` floats of each row take part (coefficients beyond the active degree).
 struct ShPlane {
-  const float* src;
-  float* dst;
-  int w, col, used;
+  const float* src;  // global input plane (row-major [P, w])
+  float* dst;        // global gradient plane
+  int w;             // floats per Gaussian
+  int lds;           // float offset of the plane in the LDS buffer
 };
 
 __device__ __forceinline__ uint32_t div_small(uint32_t e, uint32_t magic) {
   return __umulhi(e, magic);  // e / w for e < 2^32 / w^2 with magic = ceil(2^32 / w)
 }
 
-// The plane segment of a workgroup is contiguous (n * w floats starting at (base * w) floats,
-// 16-byte aligned when the tensor is, since base is a multiple of 256): it is moved as float4
-// vectors, kBatch of them in flight per lane, plus a scalar tail.  A float4 spans at most two
-// rows (w >= 3); vectors whose rows are all culled are skipped.
-constexpr int kBatch = 4;
-
-template <class F>
-__device__ __forceinline__ void for_plane_vectors(int n, int w, const float* gptr, F&& f) {
-  const int total = n * w;
-  const bool vec_ok = (((uintptr_t)gptr) & 15) == 0;
+// global <-> LDS copy of one plane segment; IN: global -> LDS, else LDS -> global (ACC: add)
+template <bool IN, bool ACC>
+__device__ __forceinline__ void stage(const ShPlane& p, int base, int n, const uint8_t* live,
+                                      float* lds) {
+  if (p.w == 0) return;
+  const uint32_t w = (uint32_t)p.w;
+  const uint32_t magic = (uint32_t)((0x100000000ull + w - 1) / w);
+  const size_t gofs = (size_t)base * w;
+  const float* src = p.src + gofs;
+  float* dst = p.dst + gofs;
+  float* l = lds + p.lds;
+  const int total = n * p.w;
+  const bool vec_ok = ((((uintptr_t)(IN ? (const void*)src : (const void*)dst)) & 15) == 0);
   const int nvec = vec_ok ? (total >> 2) : 0;
-  for (int q0 = (int)threadIdx.x; q0 < nvec; q0 += kBatch * kThreads) f(q0, nvec);
-  // scalar tail (or everything when unaligned): element index space [4 * nvec, total)
-  for (int e = 4 * nvec + (int)threadIdx.x; e < total; e += kThreads) f(-1 - e, nvec);
-}
-
-// Cooperative, coalesced copy of a plane into the LDS rows (only the `used` columns).
-__device__ __forceinline__ void stage_in(const ShPlane& p, int base, int n, const uint8_t* live,
-                                         float* lds) {
-  if (p.w == 0 || p.used == 0) return;
-  const uint32_t w = (uint32_t)p.w;
-  const uint32_t magic = (uint32_t)((0x100000000ull + w - 1) / w);
-  const float* src = p.src + (size_t)base * w;
-  auto put = [&](uint32_t e, float v) {
-    const uint32_t g = div_small(e, magic), k = e - g * w;
-    if ((int)k < p.used) lds[g * kShStride + p.col + k] = v;
+  // in ACC mode (or when loading) vectors covering only culled rows are skipped
+  auto needed = [&](int q) {
+    return live[div_small(4u * q, magic)] || live[div_small(4u * q + 3u, magic)];
   };
-  for_plane_vectors(n, p.w, src, [&](int q0, int nvec) {
-    if (q0 < 0) {
-      const uint32_t e = (uint32_t)(-1 - q0);
-      put(e, src[e]);
-      return;
-    }
-    float4 v[kBatch];
+  for (int q0 = (int)threadIdx.x; q0 < nvec; q0 += kBatch * kThreads) {
+    float4 v[kBatch], o[kBatch];
     bool on[kBatch];
 #pragma unroll
     for (int j = 0; j < kBatch; j++) {
       const int q = q0 + j * kThreads;
-      on[j] = q < nvec && (live[div_small(4 * q, magic)] || live[div_small(4 * q + 3, magic)]);
-      if (on[j]) v[j] = reinterpret_cast<const float4*>(src)[q];
-    }
-#pragma unroll
-    for (int j = 0; j < kBatch; j++) {
-      if (!on[j]) continue;
-      const uint32_t e = 4u * (uint32_t)(q0 + j * kThreads);
-      put(e, v[j].x); put(e + 1, v[j].y); put(e + 2, v[j].z); put(e + 3, v[j].w);
-    }
-  });
-}
-
-// Cooperative, coalesced write (ACC: add) of the gradient plane from the LDS rows.  Store mode
-// writes zeros for culled Gaussians and for coefficients above the active degree; ACC mode leaves
-// them unchanged.
-template <bool ACC>
-__device__ __forceinline__ void stage_out(const ShPlane& p, int base, int n, const uint8_t* live,
-                                          const float* lds) {
-  if (p.w == 0 || p.dst == nullptr) return;
-  const uint32_t w = (uint32_t)p.w;
-  const uint32_t magic = (uint32_t)((0x100000000ull + w - 1) / w);
-  float* dst = p.dst + (size_t)base * w;
-  auto get = [&](uint32_t e) {
-    const uint32_t g = div_small(e, magic), k = e - g * w;
-    return (live[g] && (int)k < p.used) ? lds[g * kShStride + p.col + k] : 0.0f;
-  };
-  for_plane_vectors(n, p.w, dst, [&](int q0, int nvec) {
-    if (q0 < 0) {
-      const uint32_t e = (uint32_t)(-1 - q0);
-      if (ACC) dst[e] += get(e); else dst[e] = get(e);
-      return;
-    }
-    float4 v[kBatch];
-    bool on[kBatch];
-#pragma unroll
-    for (int j = 0; j < kBatch; j++) {
-      const int q = q0 + j * kThreads;
-      on[j] = q < nvec;
-      if (ACC) {
-        on[j] = on[j] && (live[div_small(4 * q, magic)] || live[div_small(4 * q + 3, magic)]);
-        if (on[j]) v[j] = reinterpret_cast<const float4*>(dst)[q];
+      on[j] = q < nvec && (!(IN || ACC) || needed(q));
+      v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      o[j] = v[j];
+      if (on[j]) {
+        if (IN) {
+          v[j] = reinterpret_cast<const float4*>(src)[q];
+        } else {
+          v[j] = reinterpret_cast<const float4*>(l)[q];
+          if (ACC) o[j] = reinterpret_cast<const float4*>(dst)[q];
+        }
       }
     }
 #pragma unroll
     for (int j = 0; j < kBatch; j++) {
-      if (!on[j]) continue;
-      const uint32_t e = 4u * (uint32_t)(q0 + j * kThreads);
-      const float4 g4 = make_float4(get(e), get(e + 1), get(e + 2), get(e + 3));
-      float4 o = g4;
-      if (ACC) o = make_float4(v[j].x + g4.x, v[j].y + g4.y, v[j].z + g4.z, v[j].w + g4.w);
-      reinterpret_cast<float4*>(dst)[q0 + j * kThreads] = o;
+      const int q = q0 + j * kThreads;
+      if (on[j]) {
+        if (IN) {
+          reinterpret_cast<float4*>(l)[q] = v[j];
+        } else {
+          float4 r = v[j];
+          if (ACC) r = make_float4(o[j].x + r.x, o[j].y + r.y, o[j].z + r.z, o[j].w + r.w);
+          reinterpret_cast<float4*>(dst)[q] = r;
+        }
+      }
     }
-  });
+  }
+  // scalar tail (everything when the global pointer is not 16-byte aligned)
+  for (int e = 4 * nvec + (int)threadIdx.x; e < total; e += kThreads) {
+    if (IN) l[e] = src[e];
+    else if (ACC) { if (live[div_small((uint32_t)e, magic)]) dst[e] += l[e]; }
+    else dst[e] = l[e];
+  }
 }
 
 // One workgroup = kThreads consecutive Gaussians.  The SH coefficients (48 of the ~60 floats a
-// Gaussian reads, and 48 of the grads it writes) are staged through LDS so that global traffic
-// is coalesced instead of lane-strided by 180-192 bytes.
+// Gaussian reads, and 48 of the grads it writes) go through LDS so that global traffic is
+// coalesced 16-byte vectors instead of lane-strided by 180-192 bytes.
 template <bool ACC>
 __global__ __launch_bounds__(kThreads) void preprocess_bwd_kernel(BwdPreArgs a) {
-  __shared__ float s_sh[kThreads * kShStride];
+  __shared__ float4 s_sh4[kThreads * kShMaxFloats / 4];
   __shared__ uint8_t s_live[kThreads];
+  float* s_sh = reinterpret_cast<float*>(s_sh4);
   const int base = (int)(blockIdx.x * kThreads);
   const int n = min(kThreads, a.P - base);
   const int t = (int)threadIdx.x;
@@ -467,26 +443,37 @@ __global__ __launch_bounds__(kThreads) void preprocess_bwd_kernel(BwdPreArgs a) 
   ShPlane p0{}, p1{};
   if (has_sh) {
     const int ncoef = a.M * 3;
-    const int used = (a.D + 1) * (a.D + 1) * 3;
     if (a.fused) {
-      p0 = ShPlane{a.sh_dc, a.dL_dsh, 3, 0, 3};
-      p1 = ShPlane{a.sh_rest, a.dL_dsh_rest, ncoef - 3, 3, used - 3};
+      p0 = ShPlane{a.sh_dc, a.dL_dsh, 3, 0};
+      p1 = ShPlane{a.sh_rest, a.dL_dsh_rest, ncoef - 3, kThreads * 3};
     } else {
-      p0 = ShPlane{a.shs, a.dL_dsh, ncoef, 0, used};
+      p0 = ShPlane{a.shs, a.dL_dsh, ncoef, 0};
     }
     __syncthreads();
-    stage_in(p0, base, n, s_live, s_sh);
-    stage_in(p1, base, n, s_live, s_sh);
+    stage<true, ACC>(p0, base, n, s_live, s_sh);
+    stage<true, ACC>(p1, base, n, s_live, s_sh);
     __syncthreads();
   }
-  if (live)
-    gaussian_bwd<ACC>(a, i, s_sh + t * kShStride);
-  else if (!ACC && t < n)
-    zero_outputs(a, i);
+  // this Gaussian's rows: coefficient 0 and coefficients 1..
+  float* r0 = s_sh + p0.lds + t * p0.w;
+  float* r1 = a.fused ? s_sh + p1.lds + t * p1.w : r0 + 3;
+  if (live) {
+    gaussian_bwd<ACC>(a, i, r0, r1);
+    if (has_sh) {  // coefficients above the active degree: zero gradient
+      const int used = (a.D + 1) * (a.D + 1) * 3;
+      for (int k = used; k < a.M * 3; k++) r1[k - 3] = 0.0f;
+    }
+  } else {
+    if (!ACC && t < n) zero_outputs(a, i);
+    if (has_sh && t < n) {  // culled: zero rows (written in store mode, skipped or +0 in ACC)
+      for (int k = 0; k < 3; k++) r0[k] = 0.0f;
+      for (int k = 3; k < a.M * 3; k++) r1[k - 3] = 0.0f;
+    }
+  }
   if (has_sh) {
     __syncthreads();
-    stage_out<ACC>(p0, base, n, s_live, s_sh);
-    stage_out<ACC>(p1, base, n, s_live, s_sh);
+    stage<false, ACC>(p0, base, n, s_live, s_sh);
+    stage<false, ACC>(p1, base, n, s_live, s_sh);
   }
 }
 

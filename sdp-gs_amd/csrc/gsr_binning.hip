@@ -31,14 +31,16 @@ __global__ __launch_bounds__(kThreads) void duplicate_kernel(int P,
                                                              uint32_t* __restrict__ tval) {
   const int s = (int)(blockIdx.x * kThreads + threadIdx.x);
   if (s >= P) return;
-  const uint32_t gid = order[s];
-  const int r = radii[gid];
-  if (!(r > 0)) return;
+  // coalesced reads first: culled / tile-less Gaussians (count 0) never touch the random gather
   uint32_t off = (s == 0) ? 0u : offsets[s - 1];
   const uint32_t end = offsets[s];
   if (off == end) return;
+  const uint32_t gid = order[s];
+  // the radius travels in the record (rec[3].y, exact as float): the gather stays inside the
+  // Gaussian's 64-byte record line
   const float4 r0 = rec[4 * (size_t)gid];
   const float4 r1 = rec[4 * (size_t)gid + 1];
+  const int r = (int)rec[4 * (size_t)gid + 3].y;
   const float qc = splat_q_cut(r0.z, r0.w, r1.x, r1.y);
   uint32_t x0, y0, x1, y1;
   tile_rect(r0.x, r0.y, r, gx, gy, x0, y0, x1, y1);

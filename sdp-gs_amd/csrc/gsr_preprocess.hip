@@ -9,7 +9,7 @@
 //   rec[4g+0] = {x_px, y_px, conic.a, conic.b}
 //   rec[4g+1] = {conic.c, opacity*confidence, depth, r}
 //   rec[4g+2] = {g, b, f0, f1}
-//   rec[4g+3] = {f2, 0, 0, 0}
+//   rec[4g+3] = {f2, radius, 0, 0}   (radius as float: exact, read by the duplication)
 // so the blend reads one contiguous record per instance instead of five scattered arrays.
 #include "gsr_device.h"
 #include "gsr_internal.h"
@@ -161,7 +161,7 @@ __global__ __launch_bounds__(kThreads) void preprocess_kernel(PreArgs a) {
   rec[0] = make_float4(px, py, con_a, con_b);
   rec[1] = make_float4(con_c, op, depth, cr);
   rec[2] = make_float4(cg, cb, f0, f1);
-  rec[3] = make_float4(f2, 0.f, 0.f, 0.f);
+  rec[3] = make_float4(f2, (float)r, 0.f, 0.f);
 }
 
 __global__ __launch_bounds__(kThreads) void mark_visible_kernel(int P, const float* __restrict__ m,
