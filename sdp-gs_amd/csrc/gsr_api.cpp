@@ -27,14 +27,12 @@ GeomState carve_geom(char* base, size_t P) {
   Carver c(base);
   GeomState g{};
   g.flags = c.take<uint32_t>(4);
-  g.depths = c.take<float>(P);
   g.dkey_a = c.take<uint32_t>(P);
   g.dval_a = c.take<uint32_t>(P);
   g.dkey_b = c.take<uint32_t>(P);
   g.dval_b = c.take<uint32_t>(P);
   g.clamped = c.take<uint8_t>(P);
   g.radii = c.take<int32_t>(P);
-  g.cov3D = c.take<float>(6 * P);
   g.rec = c.take<float4>(4 * P);
   g.tiles_touched = c.take<uint32_t>(P);
   g.offsets = c.take<uint32_t>(P);
@@ -230,6 +228,8 @@ static int forward_impl(int P, int M, const float* background, const float* mean
                 "Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!");
   if (sh) {
     if (degree < 0 || degree > 3) return fail(GSR_ERR_ARGUMENT, "sh_degree must be in [0, 3] (got %d)", degree);
+    if (M > 16)  // the kernels stage at most 16 coefficients per Gaussian in LDS
+      return fail(GSR_ERR_ARGUMENT, "sh has M = %d coefficients; at most 16 (degree 3) supported", M);
     if ((degree + 1) * (degree + 1) > M)
       return fail(GSR_ERR_ARGUMENT, "sh has %d coefficients but degree %d needs %d", M, degree,
                   (degree + 1) * (degree + 1));
@@ -436,7 +436,7 @@ static int backward_impl(
   BwdPreArgs ba{};
   ba.P = P; ba.D = degree; ba.M = M;
   ba.means3D = means3D; ba.scales = scales; ba.rotations = rotations; ba.shs = sh;
-  ba.cov3D = cov3D_precomp ? cov3D_precomp : g.cov3D; ba.colors_precomp = colors_precomp;
+  ba.cov3D = cov3D_precomp; ba.colors_precomp = colors_precomp;
   ba.sh_language = sh_language; ba.lang_precomp = language_feature_precomp;
   ba.confidence = confidence;
   ba.view = viewmatrix; ba.proj = projmatrix; ba.campos = campos;

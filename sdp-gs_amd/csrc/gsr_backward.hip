@@ -8,6 +8,7 @@
 // Inputs come from the 64-byte accumulator row the backward blend filled (gsr_internal.h AccSlot).
 #include "gsr_device.h"
 #include "gsr_internal.h"
+#include "gsr_stage.h"
 
 namespace gsr {
 namespace {
@@ -173,7 +174,22 @@ __device__ __forceinline__ void gaussian_bwd(const BwdPreArgs& a, size_t i, floa
   }
 
   const V3 mean = v3(a.means3D[3 * i], a.means3D[3 * i + 1], a.means3D[3 * i + 2]);
-  const float* c3 = a.cov3D + 6 * i;
+  // 3D covariance: precomputed, or recomputed from scale / rotation with the forward's own
+  // function and inputs (bit-identical to what the forward projected; not stored in between)
+  float c3buf[6];  // always a register array (a pointer select would force it into scratch)
+  const float* c3 = c3buf;
+  if (a.cov3D) {
+#pragma unroll
+    for (int k = 0; k < 6; k++) c3buf[k] = a.cov3D[6 * i + k];
+  } else {
+    float4 q = reinterpret_cast<const float4*>(a.rotations)[i];
+    float sx = a.scales[3 * i], sy = a.scales[3 * i + 1], sz = a.scales[3 * i + 2];
+    if (a.fused) {
+      sx = expf(sx); sy = expf(sy); sz = expf(sz);
+      q = normalize_quat(q);
+    }
+    cov3d_from_scale_rot(sx, sy, sz, a.scale_modifier, q.x, q.y, q.z, q.w, c3buf);
+  }
 
   // ---- computeCov2DCUDA, backward.cu:164-273 ----
   const Ewa e = ewa_project(mean, a.fx, a.fy, a.tanx, a.tany, c3, a.view);
@@ -344,87 +360,6 @@ __device__ __forceinline__ void gaussian_bwd(const BwdPreArgs& a, size_t i, floa
   }
 }
 
-// ---- SH staging ----------------------------------------------------------------------------------
-// A workgroup's SH data is one contiguous segment per plane in global memory (fused: features_dc
-// w = 3 floats per Gaussian and features_rest w = 3(M-1); reference layout: sh w = 3M).  Each plane
-// is copied into LDS with the SAME layout, as 16-byte vectors (ds_write_b128 / ds_read_b128 at
-// consecutive addresses: no bank conflicts, no index arithmetic), kBatch vectors in flight per
-// lane.  The per-Gaussian compute then reads its row at stride w (odd for the fused planes, so
-// lane-strided access is conflict-free), works in place, and the gradient plane goes back the
-// same way (ACC: read-add-write).  A vector spans at most two rows (w >= 3); vectors whose rows
-// are all culled are skipped in ACC mode.
-constexpr int kShMaxFloats = 48;  // 16 coefficients x 3 per Gaussian (M <= 16, checked by the API)
-constexpr int kBatch = 4;
-
-struct ShPlane {
-  const float* src;  // global input plane (row-major [P, w])
-  float* dst;        // global gradient plane
-  int w;             // floats per Gaussian
-  int lds;           // float offset of the plane in the LDS buffer
-};
-
-__device__ __forceinline__ uint32_t div_small(uint32_t e, uint32_t magic) {
-  return __umulhi(e, magic);  // e / w for e < 2^32 / w^2 with magic = ceil(2^32 / w)
-}
-
-// global <-> LDS copy of one plane segment; IN: global -> LDS, else LDS -> global (ACC: add)
-template <bool IN, bool ACC>
-__device__ __forceinline__ void stage(const ShPlane& p, int base, int n, const uint8_t* live,
-                                      float* lds) {
-  if (p.w == 0) return;
-  const uint32_t w = (uint32_t)p.w;
-  const uint32_t magic = (uint32_t)((0x100000000ull + w - 1) / w);
-  const size_t gofs = (size_t)base * w;
-  const float* src = p.src + gofs;
-  float* dst = p.dst + gofs;
-  float* l = lds + p.lds;
-  const int total = n * p.w;
-  const bool vec_ok = ((((uintptr_t)(IN ? (const void*)src : (const void*)dst)) & 15) == 0);
-  const int nvec = vec_ok ? (total >> 2) : 0;
-  // in ACC mode (or when loading) vectors covering only culled rows are skipped
-  auto needed = [&](int q) {
-    return live[div_small(4u * q, magic)] || live[div_small(4u * q + 3u, magic)];
-  };
-  for (int q0 = (int)threadIdx.x; q0 < nvec; q0 += kBatch * kThreads) {
-    float4 v[kBatch], o[kBatch];
-    bool on[kBatch];
-#pragma unroll
-    for (int j = 0; j < kBatch; j++) {
-      const int q = q0 + j * kThreads;
-      on[j] = q < nvec && (!(IN || ACC) || needed(q));
-      v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-      o[j] = v[j];
-      if (on[j]) {
-        if (IN) {
-          v[j] = reinterpret_cast<const float4*>(src)[q];
-        } else {
-          v[j] = reinterpret_cast<const float4*>(l)[q];
-          if (ACC) o[j] = reinterpret_cast<const float4*>(dst)[q];
-        }
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < kBatch; j++) {
-      const int q = q0 + j * kThreads;
-      if (on[j]) {
-        if (IN) {
-          reinterpret_cast<float4*>(l)[q] = v[j];
-        } else {
-          float4 r = v[j];
-          if (ACC) r = make_float4(o[j].x + r.x, o[j].y + r.y, o[j].z + r.z, o[j].w + r.w);
-          reinterpret_cast<float4*>(dst)[q] = r;
-        }
-      }
-    }
-  }
-  // scalar tail (everything when the global pointer is not 16-byte aligned)
-  for (int e = 4 * nvec + (int)threadIdx.x; e < total; e += kThreads) {
-    if (IN) l[e] = src[e];
-    else if (ACC) { if (live[div_small((uint32_t)e, magic)]) dst[e] += l[e]; }
-    else dst[e] = l[e];
-  }
-}
-
 // One workgroup = kThreads consecutive Gaussians.  The SH coefficients (48 of the ~60 floats a
 // Gaussian reads, and 48 of the grads it writes) go through LDS so that global traffic is
 // coalesced 16-byte vectors instead of lane-strided by 180-192 bytes.
@@ -450,8 +385,8 @@ __global__ __launch_bounds__(kThreads) void preprocess_bwd_kernel(BwdPreArgs a) 
       p0 = ShPlane{a.shs, a.dL_dsh, ncoef, 0};
     }
     __syncthreads();
-    stage<true, ACC>(p0, base, n, s_live, s_sh);
-    stage<true, ACC>(p1, base, n, s_live, s_sh);
+    stage<kThreads, true, ACC>(p0, base, n, s_live, s_sh);
+    stage<kThreads, true, ACC>(p1, base, n, s_live, s_sh);
     __syncthreads();
   }
   // this Gaussian's rows: coefficient 0 and coefficients 1..
@@ -472,8 +407,8 @@ __global__ __launch_bounds__(kThreads) void preprocess_bwd_kernel(BwdPreArgs a) 
   }
   if (has_sh) {
     __syncthreads();
-    stage<false, ACC>(p0, base, n, s_live, s_sh);
-    stage<false, ACC>(p1, base, n, s_live, s_sh);
+    stage<kThreads, false, ACC>(p0, base, n, s_live, s_sh);
+    stage<kThreads, false, ACC>(p1, base, n, s_live, s_sh);
   }
 }
 

@@ -83,14 +83,12 @@ hipError_t radix_sort_pairs(uint32_t* ka, uint32_t* va, uint32_t* kb, uint32_t* 
 
 // ---- layouts -------------------------------------------------------------------------------------
 struct GeomState {
-  float* depths;            // [P] view-space z (valid where radii > 0)
   uint32_t* dkey_a;         // [P] depth-sort keys (float bits of z; 0xffffffff if culled)
   uint32_t* dval_a;         // [P] Gaussian ids, depth-sorted after the sort (see depth_sorted())
   uint32_t* dkey_b;
   uint32_t* dval_b;
   uint8_t* clamped;         // [P] bit c set <=> SH colour channel c clamped (forward.cu:67-69)
   int32_t* radii;           // [P] internal radii (used when the caller passes none)
-  float* cov3D;             // [P*6]
   float4* rec;              // [P*4] splat record for the blend
   uint32_t* tiles_touched;  // [P]
   uint32_t* offsets;        // [P] inclusive scan of tiles_touched in depth order

@@ -56,18 +56,20 @@ __device__ __forceinline__ V3 sh_to_rgb(const float* __restrict__ s0, const floa
 }
 
 __global__ __launch_bounds__(kThreads) void preprocess_kernel(PreArgs a) {
+  // one lane per Gaussian; SH rows are read directly (an LDS-staged variant, gsr_stage.h, measured
+  // slower here: its 48 KB of LDS cut occupancy below what this latency-bound kernel needs)
   const int idx = (int)(blockIdx.x * kThreads + threadIdx.x);
   if (idx >= a.P) return;
+  const V3 p_orig = v3(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
+  const V3 p_view = xform_point43(p_orig, a.view);
+  // in_frustum: near-plane test only (auxiliary.h:154)
+  const bool near_ok = !(p_view.z <= 0.2f);
   const GeomState& g = a.g;
   a.radii[idx] = 0;
   g.tiles_touched[idx] = 0;
   g.dkey_a[idx] = 0xffffffffu;
   g.dval_a[idx] = (uint32_t)idx;
-
-  const V3 p_orig = v3(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
-  // in_frustum: near-plane test only (auxiliary.h:154)
-  const V3 p_view = xform_point43(p_orig, a.view);
-  if (p_view.z <= 0.2f) {
+  if (!near_ok) {
     if (a.prefiltered) atomicOr(&g.flags[0], 1u);  // reference __trap()s (auxiliary.h:156-160)
     return;
   }
@@ -75,10 +77,11 @@ __global__ __launch_bounds__(kThreads) void preprocess_kernel(PreArgs a) {
   const float pw = 1.0f / (xform_w(p_orig, a.proj) + 0.0000001f);
   const float pproj_x = ph.x * pw, pproj_y = ph.y * pw;
 
-  float c3buf[6];
-  const float* c3;
+  float c3buf[6];  // always a register array (a pointer select would force it into scratch)
+  const float* c3 = c3buf;
   if (a.cov3D_precomp) {
-    c3 = a.cov3D_precomp + 6 * (size_t)idx;
+#pragma unroll
+    for (int k = 0; k < 6; k++) c3buf[k] = a.cov3D_precomp[6 * (size_t)idx + k];
   } else {
     float4 q = reinterpret_cast<const float4*>(a.rotations)[idx];
     float sx = a.scales[3 * idx], sy = a.scales[3 * idx + 1], sz = a.scales[3 * idx + 2];
@@ -86,11 +89,8 @@ __global__ __launch_bounds__(kThreads) void preprocess_kernel(PreArgs a) {
       sx = expf(sx); sy = expf(sy); sz = expf(sz);
       q = normalize_quat(q);
     }
+    // not stored: the backward recomputes it bit-identically from the same inputs
     cov3d_from_scale_rot(sx, sy, sz, a.scale_modifier, q.x, q.y, q.z, q.w, c3buf);
-    float* dst = g.cov3D + 6 * (size_t)idx;
-#pragma unroll
-    for (int k = 0; k < 6; k++) dst[k] = c3buf[k];
-    c3 = c3buf;
   }
   const Ewa e = ewa_project(p_orig, a.fx, a.fy, a.tanx, a.tany, c3, a.view);
   const float det = (e.a * e.c - e.b * e.b);
@@ -140,7 +140,6 @@ __global__ __launch_bounds__(kThreads) void preprocess_kernel(PreArgs a) {
     }
   }
   const float depth = p_view.z;
-  g.depths[idx] = depth;
   a.radii[idx] = r;
   // Exact tile list: the reference emits every tile of the 3-sigma square (forward.cu:255); tiles
   // in which no pixel can reach alpha >= 1/255 are dropped here (no output bit changes)

@@ -1,0 +1,92 @@
+// gsr_stage.h -- cooperative global <-> LDS staging of per-Gaussian SH planes (device code).
+//
+// Shared by the forward preprocess (gsr_preprocess.hip, loads only) and the backward preprocess
+// (gsr_backward.hip, loads + gradient stores / accumulation).
+#pragma once
+#include "gsr_internal.h"
+
+namespace gsr {
+
+// ---- SH staging ----------------------------------------------------------------------------------
+// A workgroup's SH data is one contiguous segment per plane in global memory (fused: features_dc
+// w = 3 floats per Gaussian and features_rest w = 3(M-1); reference layout: sh w = 3M).  Each plane
+// is copied into LDS with the SAME layout, as 16-byte vectors (ds_write_b128 / ds_read_b128 at
+// consecutive addresses: no bank conflicts, no index arithmetic), kStageBatch vectors in flight per
+// lane.  The per-Gaussian compute then reads its row at stride w (odd for the fused planes, so
+// lane-strided access is conflict-free), works in place, and the gradient plane goes back the
+// same way (ACC: read-add-write).  A vector spans at most two rows (w >= 3); vectors whose rows
+// are all culled are skipped in ACC mode.
+constexpr int kShMaxFloats = 48;  // 16 coefficients x 3 per Gaussian (M <= 16, checked by the API)
+constexpr int kStageBatch = 4;
+
+struct ShPlane {
+  const float* src;  // global input plane (row-major [P, w])
+  float* dst;        // global gradient plane
+  int w;             // floats per Gaussian
+  int lds;           // float offset of the plane in the LDS buffer
+};
+
+__device__ __forceinline__ uint32_t div_small(uint32_t e, uint32_t magic) {
+  return __umulhi(e, magic);  // e / w for e < 2^32 / w^2 with magic = ceil(2^32 / w)
+}
+
+// global <-> LDS copy of one plane segment; IN: global -> LDS, else LDS -> global (ACC: add)
+template <int NT, bool IN, bool ACC>
+__device__ __forceinline__ void stage(const ShPlane& p, int base, int n, const uint8_t* live,
+                                      float* lds) {
+  if (p.w == 0) return;
+  const uint32_t w = (uint32_t)p.w;
+  const uint32_t magic = (uint32_t)((0x100000000ull + w - 1) / w);
+  const size_t gofs = (size_t)base * w;
+  const float* src = p.src + gofs;
+  float* dst = p.dst + gofs;
+  float* l = lds + p.lds;
+  const int total = n * p.w;
+  const bool vec_ok = ((((uintptr_t)(IN ? (const void*)src : (const void*)dst)) & 15) == 0);
+  const int nvec = vec_ok ? (total >> 2) : 0;
+  // in ACC mode (or when loading) vectors covering only culled rows are skipped
+  auto needed = [&](int q) {
+    return live[div_small(4u * q, magic)] || live[div_small(4u * q + 3u, magic)];
+  };
+  for (int q0 = (int)threadIdx.x; q0 < nvec; q0 += kStageBatch * NT) {
+    float4 v[kStageBatch], o[kStageBatch];
+    bool on[kStageBatch];
+#pragma unroll
+    for (int j = 0; j < kStageBatch; j++) {
+      const int q = q0 + j * NT;
+      on[j] = q < nvec && (!(IN || ACC) || needed(q));
+      v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      o[j] = v[j];
+      if (on[j]) {
+        if (IN) {
+          v[j] = reinterpret_cast<const float4*>(src)[q];
+        } else {
+          v[j] = reinterpret_cast<const float4*>(l)[q];
+          if (ACC) o[j] = reinterpret_cast<const float4*>(dst)[q];
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kStageBatch; j++) {
+      const int q = q0 + j * NT;
+      if (on[j]) {
+        if (IN) {
+          reinterpret_cast<float4*>(l)[q] = v[j];
+        } else {
+          float4 r = v[j];
+          if (ACC) r = make_float4(o[j].x + r.x, o[j].y + r.y, o[j].z + r.z, o[j].w + r.w);
+          reinterpret_cast<float4*>(dst)[q] = r;
+        }
+      }
+    }
+  }
+  // scalar tail (everything when the global pointer is not 16-byte aligned)
+  for (int e = 4 * nvec + (int)threadIdx.x; e < total; e += NT) {
+    if (IN) l[e] = src[e];
+    else if (ACC) { if (live[div_small((uint32_t)e, magic)]) dst[e] += l[e]; }
+    else dst[e] = l[e];
+  }
+}
+
+
+}  // namespace gsr
