@@ -53,21 +53,31 @@ class Opt:
     include_feature = True
 
 
-def algorithmic_bytes(stage, P, Pv, R, T, HW, D=3, C=8, tile_passes=2):
-    """Bytes each stage must move per launch."""
+def algorithmic_bytes(stage, P, Pv, R, T, HW, D=3, C=8, tile_passes=2, acc=True):
+    """Bytes each stage must move per launch.
+    P Gaussians, Pv visible, R instances, T tiles, HW pixels, C blended channels (rgb, depth,
+    alpha, feature x3), acc: the backward adds into existing gradients (read + write)."""
     sh = 12 * (D + 1) ** 2
+    grads = 12 + 12 + 4 + 12 + 16 + 12 + sh  # means2D, means3D, opacity, scale, rot, lang, SH
     return {
-        "preprocess": P * 12 + Pv * (12 + 16 + 4 + sh + 12) + P * 16 + Pv * (64 + 24 + 4 + 1),
-        "depth_sort": 4 * P * 20,
+        # means (all); scale, rot, opacity, SH, language (visible); radii/tiles/key/value (all);
+        # 64-B splat record + clamp bits (visible)
+        "preprocess": P * 12 + Pv * (12 + 16 + 4 + sh + 12) + P * 16 + Pv * (64 + 1),
+        # one-sweep: digit totals read the keys once, each 8-bit pass reads and writes key+value
+        "depth_sort": P * 4 + 4 * P * 16,
         "scan": P * 12,
-        "duplicate": P * 12 + Pv * 16 + R * 8,
-        "tile_sort": tile_passes * R * 20,
+        # offsets (all), order + 48-B record gather (non-empty), R (tile, id) pairs
+        "duplicate": P * 8 + Pv * (4 + 48) + R * 8,
+        "tile_sort": R * 4 + tile_passes * R * 16,
         "ranges": R * 4 + T * 8,
-        "render_fwd": R * (4 + 8 + 16 + 4 * (C - 1)) + T * 8 + HW * (4 * C + 8),
+        # point_list + 64-B record per instance, ranges/tile_last, C outputs + final_T + n_contrib
+        "render_fwd": R * (4 + 64) + T * 12 + HW * (4 * C + 8),
         "acc_zero": P * 64,
-        "render_bwd": R * (4 + 8 + 16 + 4 * C) + HW * (4 * C + 8) + Pv * 64,
-        "preprocess_bwd": Pv * (12 + 24 + 16 + 12 + sh + 64 + 12 + 1 + 4)
-                          + P * (12 + 4 + 12 + sh + 12 + 16 + 12),
+        # same gathers, C upstream grads + final_T + n_contrib, one 64-B accumulator row per Gaussian
+        "render_bwd": R * (4 + 64) + T * 12 + HW * (4 * C + 8) + Pv * 64,
+        # accumulator row + per-Gaussian inputs (visible), radii (all), gradients (RMW when acc)
+        "preprocess_bwd": Pv * (64 + 12 + 12 + 16 + 4 + sh + 12 + 1) + P * 4
+                          + ((2 * Pv) if acc else P) * grads,
     }[stage]
 
 
@@ -161,7 +171,7 @@ def main():
         if calls == 0:
             continue
         avg_ms = ms / calls
-        b = algorithmic_bytes(name, P, Pv, R, T, HW, D=deg)
+        b = algorithmic_bytes(name, P, Pv, R, T, HW, D=deg, acc=not args.autograd_grads)
         k = {"avg_ms": round(avg_ms, 4), "calls": int(calls), "bytes": int(b),
              "gbs": round(b / (avg_ms * 1e-3) / 1e9, 1)}
         if name in ("render_fwd", "render_bwd"):
@@ -187,9 +197,10 @@ def main():
         try:
             with open(args.pmc_file) as fh:
                 pmc = json.load(fh)
-            v = pmc.get("kernels", {}).get(dom, {}).get("valu_busy_frac")
+            v = pmc.get("kernels", {}).get(dom, {}).get("valu_active_per_wave_cycle")
             if v is not None and pmc.get("workload") == args.workload:
-                roofline["valu_busy_frac_pmc"] = v
+                # SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES: the blend kernels are VALU/latency-bound
+                roofline["valu_active_per_wave_cycle_pmc"] = v
         except (OSError, ValueError):
             pass
 
