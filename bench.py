@@ -43,7 +43,9 @@ WORKLOADS = {
 
 
 class Pipe:
-    convert_SHs_python = False   # colour from SH inside the HIP preprocess (the rasterizer's work)
+    # the reference's PipelineParams defaults (arguments/__init__.py:68-71); render() evaluates
+    # the Python SH colour / language pre-pass inside the fused HIP preprocess
+    convert_SHs_python = True
     compute_cov3D_python = False
     debug = False
     use_confidence = False

@@ -24,13 +24,18 @@ _RAW = ("_features_dc", "_features_rest", "_opacity", "_scaling", "_rotation")
 
 
 def _fused_eligible(pc, pipe, opt, override_color, override_language) -> bool:
-    """True when render() would hand the rasterizer exactly get_features / get_opacity /
-    get_scaling / get_rotation / get_language_feature of a model with GaussianModel's standard
-    activations (scene/gaussian_model.py:33-41), so the fused entry point is equivalent.
-    GSR_FUSED=0 forces the unfused path."""
+    """True when the fused entry point computes what render() would: a model with GaussianModel's
+    standard activations (scene/gaussian_model.py:33-41), scales/rotations (not a Python cov3D),
+    no overrides.  Both colour paths qualify: with convert_SHs_python=False render() hands the
+    rasterizer get_features (SH evaluated in-kernel, forward.cu:20-71); with the reference's
+    default convert_SHs_python=True it evaluates the same function in Python
+    (gaussian_renderer/__init__.py:269-287: eval_sh + 0.5, clamp_min 0; language features
+    eval_sh(0)/(norm + 1e-9)), which the fused preprocess evaluates in-kernel with the matching
+    gradient (clamp_min passes the gradient where the value is >= 0, the kernel's `clamped` bit
+    blocks it where it is < 0).  GSR_FUSED=0 forces the unfused path."""
     if os.environ.get("GSR_FUSED", "1") == "0":
         return False
-    if pipe.compute_cov3D_python or pipe.convert_SHs_python or override_color is not None:
+    if pipe.compute_cov3D_python or override_color is not None:
         return False
     if opt.include_feature and (override_language is not None
                                 or getattr(pc, "_language_feature", None) is None):

@@ -75,17 +75,19 @@ def _zero(m):
         p.grad = None
 
 
-@pytest.mark.parametrize("conf", [False, True])
-def test_fused_activation_path_matches_unfused(monkeypatch, conf):
-    """render() default config -> gsr_rasterize_gaussians_fused (sigmoid / exp / normalize / cat
-    in-kernel) vs GSR_FUSED=0 (torch getters + gsr_rasterize_gaussians): same images, same raw
-    gradients up to the ulp-level difference of torch's vs the kernel's activation arithmetic."""
+@pytest.mark.parametrize("conf,sh_py", [(False, False), (True, False), (False, True)])
+def test_fused_activation_path_matches_unfused(monkeypatch, conf, sh_py):
+    """render() -> gsr_rasterize_gaussians_fused (sigmoid / exp / normalize / cat and, for the
+    reference's default convert_SHs_python=True, the Python eval_sh colour + language pre-pass,
+    all in-kernel) vs GSR_FUSED=0 (the torch getters / eval_sh + gsr_rasterize_gaussians): same
+    images, same raw gradients up to the ulp-level difference of torch's vs the kernel's
+    arithmetic."""
     import gaussian_renderer as gr
     render, m, cam = _setup()
     if conf:
         m.confidence = torch.rand_like(m.confidence)
     bg = torch.tensor([0.1, 0.2, 0.3], device="cuda")
-    pipe = Pipe(sh_py=False, conf=conf)
+    pipe = Pipe(sh_py=sh_py, conf=conf)
     assert gr._fused_eligible(m, pipe, Opt(), None, None)
     outs = []
     for fused in ("1", "0"):
