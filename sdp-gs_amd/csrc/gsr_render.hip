@@ -109,7 +109,7 @@ __global__ __launch_bounds__(kThreads) void render_fwd_kernel(RenderArgs a) {
   __shared__ float4 s_r0[kThreads];
   __shared__ float4 s_r1[kThreads];
   __shared__ float4 s_r2[kThreads];
-  __shared__ float4 s_r3[FEAT ? kThreads : 1];
+  __shared__ float s_f2[FEAT ? kThreads : 1];  // rec[3].x (feature 2) only
   __shared__ uint8_t s_mask[kThreads];
   __shared__ uint8_t s_list[kThreads / 64][kThreads];
   __shared__ uint32_t s_max;
@@ -145,7 +145,7 @@ __global__ __launch_bounds__(kThreads) void render_fwd_kernel(RenderArgs a) {
       s_r0[threadIdx.x] = q0;
       s_r1[threadIdx.x] = q1;
       s_r2[threadIdx.x] = rec[2];
-      if (FEAT) s_r3[threadIdx.x] = rec[3];
+      if (FEAT) s_f2[threadIdx.x] = rec[3].x;
       s_mask[threadIdx.x] = (uint8_t)wave_mask(q0, q1, tx, ty);
     }
     __syncthreads();
@@ -168,7 +168,7 @@ __global__ __launch_bounds__(kThreads) void render_fwd_kernel(RenderArgs a) {
         const float4 r0 = s_r0[jj[u]];
         r1v[u] = s_r1[jj[u]];
         r2v[u] = s_r2[jj[u]];
-        f2v[u] = FEAT ? s_r3[jj[u]].x : 0.0f;
+        f2v[u] = FEAT ? s_f2[jj[u]] : 0.0f;
         const float dx = r0.x - pfx, dy = r0.y - pfy;
         const float power = -0.5f * (r0.z * dx * dx + r1v[u].x * dy * dy) - r0.w * dx * dy;
         // entries past the list end get power = +1 and are skipped like any power > 0 pair
@@ -345,7 +345,7 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
   __shared__ float4 s_r0[kThreads];
   __shared__ float4 s_r1[kThreads];
   __shared__ float4 s_r2[kThreads];
-  __shared__ float4 s_r3[FEAT ? kThreads : 1];
+  __shared__ float s_f2[FEAT ? kThreads : 1];  // rec[3].x (feature 2) only
   __shared__ uint32_t s_gid[kThreads];
   __shared__ float s_acc[kThreads][kAccFloats];
   __shared__ uint8_t s_mask[kThreads];
@@ -425,7 +425,7 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
       s_r1[threadIdx.x] = q1;
       s_mask[threadIdx.x] = (uint8_t)wave_mask(q0, q1, tx, ty);
       s_r2[threadIdx.x] = rec[2];
-      if (FEAT) s_r3[threadIdx.x] = rec[3];
+      if (FEAT) s_f2[threadIdx.x] = rec[3].x;
     }
     __syncthreads();
     const uint32_t nlist = build_wave_list(s_mask, s_list[wid], cnt, wid, lane);
@@ -478,8 +478,8 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
         col[0] = r1.w; col[1] = r2.x; col[2] = r2.y;
         if (NC > 3) { col[3 % NC] = r1.z; col[4 % NC] = 1.0f; }
         if (FEAT) {
-          const float4 r3 = s_r3[j];
-          col[5 % NC] = r2.z; col[6 % NC] = r2.w; col[7 % NC] = r3.x;
+          const float f2 = s_f2[j];
+          col[5 % NC] = r2.z; col[6 % NC] = r2.w; col[7 % NC] = f2;
         }
         float cdot = 0.0f;
 #pragma unroll
