@@ -26,15 +26,17 @@ size_t gsr_test_scan_scratch_bytes(size_t n);
 int gsr_test_scan(const uint32_t* in, uint32_t* out, size_t n, int inclusive, void* scratch,
                   void* stream);
 
-/* Stage timing with hipEvents recorded on the caller's stream around every kernel of the forward
- * and backward (used by bench.py for the per-kernel roofline).  Off by default; when on, each
- * stage launch is bracketed by two events, which costs a few microseconds per view. */
+/* Stage timing with hipEvents recorded on the caller's stream around the kernels of the forward
+ * and backward (used by bench.py for the per-kernel roofline).  Off by default; each enabled
+ * stage launch is bracketed by two events (a few microseconds per stage and view, so bench.py
+ * instruments only the dominant stage inside its timed region). */
 enum {
   GSR_STAGE_PREPROCESS = 0, GSR_STAGE_DEPTH_SORT, GSR_STAGE_SCAN, GSR_STAGE_DUPLICATE,
   GSR_STAGE_TILE_SORT, GSR_STAGE_RANGES, GSR_STAGE_RENDER_FWD, GSR_STAGE_ACC_ZERO,
   GSR_STAGE_RENDER_BWD, GSR_STAGE_PREPROCESS_BWD, GSR_NUM_STAGES
 };
-void gsr_profile_enable(int on);
+/* stage_mask: bit GSR_STAGE_x enables that stage; 0 disables; -1 (all bits) enables all. */
+void gsr_profile_enable(int stage_mask);
 /* Waits for the recorded events, adds their durations into ms[GSR_NUM_STAGES] and
  * calls[GSR_NUM_STAGES] (accumulating since the last reset) and recycles the events. */
 int gsr_profile_collect(double* ms, long long* calls);

@@ -124,12 +124,24 @@ uint32_t* pinned_slot() {
   return p;
 }
 
+// Event marking the arrival of the forward's readback in the pinned slot (per host thread; HIP
+// events are device-agnostic for synchronisation).
+hipEvent_t readback_event() {
+  constexpr int kMaxDev = 64;
+  thread_local hipEvent_t ev[kMaxDev] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return nullptr;
+  if (!ev[dev] && hipEventCreateWithFlags(&ev[dev], hipEventDisableTiming) != hipSuccess)
+    ev[dev] = nullptr;
+  return ev[dev];
+}
+
 bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
 // ---- optional per-stage hipEvent timing (include/gsr_testing.h) ----------------------------------
 struct Profiler {
   std::mutex mu;
-  std::atomic<bool> on{false};
+  std::atomic<uint32_t> mask{0};
   std::vector<hipEvent_t> pool;
   struct Rec { int stage; hipEvent_t a, b; };
   std::vector<Rec> pending;
@@ -152,8 +164,8 @@ hipEvent_t prof_take() {
   if (hipEventCreate(&e) != hipSuccess) return nullptr;
   return e;
 }
-hipEvent_t prof_begin(hipStream_t s) {
-  if (!prof().on.load(std::memory_order_relaxed)) return nullptr;
+hipEvent_t prof_begin(int stage, hipStream_t s) {
+  if (!((prof().mask.load(std::memory_order_relaxed) >> stage) & 1u)) return nullptr;
   hipEvent_t a = prof_take();
   if (a && hipEventRecord(a, s) != hipSuccess) return nullptr;
   return a;
@@ -166,7 +178,7 @@ void prof_end(int stage, hipEvent_t a, hipStream_t s) {
   std::lock_guard<std::mutex> g(p.mu);
   p.pending.push_back({stage, a, b});
 }
-#define PROF_BEGIN(st) hipEvent_t prof_ev_##st = prof_begin(stream)
+#define PROF_BEGIN(st) hipEvent_t prof_ev_##st = prof_begin(GSR_STAGE_##st, stream)
 #define PROF_END(st) prof_end(GSR_STAGE_##st, prof_ev_##st, stream)
 
 const char* kStageNames[GSR_NUM_STAGES] = {"preprocess", "depth_sort", "scan", "duplicate",
@@ -268,7 +280,16 @@ static int forward_impl(int P, int M, const float* background, const float* mean
   pa.fused = fused; pa.sh_dc = sh_dc; pa.sh_rest = sh_rest;
   PROF_BEGIN(PREPROCESS);
   GSR_CHECK(launch_preprocess(pa, stream));
+  // R = total tile count (order-independent): reduced right after the preprocess and read back
+  // while the depth sort and the scan are already queued behind it, so the host's wait and the
+  // binning-buffer allocation overlap GPU work instead of draining the stream
+  GSR_CHECK(reduce_u32(g.tiles_touched, (size_t)P, g.scan_parts, g.flags + 1, stream));
   PROF_END(PREPROCESS);
+  uint32_t* host = pinned_slot();
+  hipEvent_t ready = readback_event();
+  if (!host || !ready) return fail(GSR_ERR_HIP, "pinned host slot / event creation failed");
+  GSR_CHECK(hipMemcpyAsync(host, g.flags, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+  GSR_CHECK(hipEventRecord(ready, stream));
 
   bool in_b = false;
   PROF_BEGIN(DEPTH_SORT);
@@ -280,18 +301,17 @@ static int forward_impl(int P, int M, const float* background, const float* mean
   GSR_CHECK(scan_u32(g.tiles_touched, order, g.offsets, (size_t)P, true, g.scan_parts, stream));
   PROF_END(SCAN);
 
-  uint32_t* host = pinned_slot();
-  if (!host) return fail(GSR_ERR_HIP, "pinned host allocation failed");
-  GSR_CHECK(hipMemcpyAsync(host, g.offsets + (P - 1), 4, hipMemcpyDeviceToHost, stream));
-  GSR_CHECK(hipMemcpyAsync(host + 1, g.flags, 4, hipMemcpyDeviceToHost, stream));
-  GSR_CHECK(hipMemcpyAsync(host + 2, g.sort.aux + kSortAuxErr, 4, hipMemcpyDeviceToHost, stream));
-  GSR_CHECK(hipStreamSynchronize(stream));
-  const uint32_t R = host[0];
-  if (host[2]) return fail(GSR_ERR_HIP, "depth sort look-back timed out");
-  if (host[1]) return fail(GSR_ERR_PREFILTERED,
+  GSR_CHECK(hipEventSynchronize(ready));
+  const uint32_t R = host[1];
+  if (host[0]) return fail(GSR_ERR_PREFILTERED,
                            "Point is filtered although prefiltered is set. This shouldn't happen!");
   if (R > 0x7fffffffu)
     return fail(GSR_ERR_TOO_LARGE, "num_rendered = %u exceeds the sort capacity", R);
+  if (debug) {
+    GSR_CHECK(hipMemcpyAsync(host + 2, g.sort.aux + kSortAuxErr, 4, hipMemcpyDeviceToHost, stream));
+    GSR_CHECK(hipStreamSynchronize(stream));
+    if (host[2]) return fail(GSR_ERR_HIP, "depth sort look-back timed out");
+  }
 
   const size_t bbytes = carve_bin(nullptr, R).bytes;
   char* bbase = (char*)alloc(alloc_ctx, bbytes, GSR_BUF_BINNING);
@@ -557,7 +577,7 @@ int gsr_test_scan(const uint32_t* in, uint32_t* out, size_t n, int inclusive, vo
   return GSR_OK;
 }
 
-void gsr_profile_enable(int on) { prof().on.store(on != 0); }
+void gsr_profile_enable(int stage_mask) { prof().mask.store((uint32_t)stage_mask); }
 
 int gsr_profile_collect(double* ms, long long* calls) {
   Profiler& p = prof();

@@ -75,6 +75,9 @@ inline SortScratch take_sort_scratch(Carver& c, size_t n) {
 // input element i is in[gather[i]].  parts: scratch of scan_parts(n) u32.
 hipError_t scan_u32(const uint32_t* in, const uint32_t* gather, uint32_t* out, size_t n,
                     bool inclusive, uint32_t* parts, hipStream_t s);
+// *out = sum of n u32 values (two launches); parts: scratch of scan_parts(n) u32.
+hipError_t reduce_u32(const uint32_t* in, size_t n, uint32_t* parts, uint32_t* out,
+                      hipStream_t s);
 // Stable LSD radix sort of (key, value) u32 pairs over key bits [0, bits).  Ping-pongs between
 // (ka, va) and (kb, vb); returns through *result_in_b whether the sorted data ended in (kb, vb).
 // One-sweep passes: 1 memset + 1 digit-totals launch + 1 launch per 8-bit digit.

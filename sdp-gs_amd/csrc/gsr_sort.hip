@@ -307,7 +307,29 @@ __global__ __launch_bounds__(kThreads) void radix_onesweep_kernel(
   }
 }
 
+// One workgroup: *out = sum of the n partials (n <= kScanMaxParts).
+__global__ __launch_bounds__(1024) void sum_parts_kernel(const uint32_t* __restrict__ parts, int n,
+                                                         uint32_t* __restrict__ out) {
+  __shared__ uint32_t lds[16];
+  uint32_t s = 0;
+  for (int i = (int)threadIdx.x; i < n; i += 1024) s += parts[i];
+  uint32_t total;
+  block_excl_scan<16>(s, lds, total);
+  if (threadIdx.x == 0) *out = total;
+}
+
 }  // namespace
+
+hipError_t reduce_u32(const uint32_t* in, size_t n, uint32_t* parts, uint32_t* out,
+                      hipStream_t s) {
+  if (n == 0) return hipMemsetAsync(out, 0, sizeof(uint32_t), s);
+  const size_t np = scan_parts(n);
+  if (np > (size_t)kScanMaxParts) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(scan_reduce_kernel<false>, dim3((unsigned)np), dim3(kThreads), 0, s, in,
+                     (const uint32_t*)nullptr, n, parts);
+  hipLaunchKernelGGL(sum_parts_kernel, dim3(1), dim3(1024), 0, s, parts, (int)np, out);
+  return hipGetLastError();
+}
 
 hipError_t scan_u32(const uint32_t* in, const uint32_t* gather, uint32_t* out, size_t n,
                     bool inclusive, uint32_t* parts, hipStream_t s) {

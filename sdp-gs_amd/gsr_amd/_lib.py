@@ -190,8 +190,18 @@ class StageTimer:
     def __init__(self):
         self.L = load()
 
-    def enable(self, on=True):
-        self.L.gsr_profile_enable(int(on))
+    def enable(self, on=True, stages=None):
+        """on: instrument every stage (stages None) or only the named stages."""
+        if not on:
+            mask = 0
+        elif stages is None:
+            mask = -1
+        else:
+            names = [self.L.gsr_profile_stage_name(i).decode() for i in range(NUM_STAGES)]
+            mask = 0
+            for s in stages:
+                mask |= 1 << names.index(s)
+        self.L.gsr_profile_enable(mask)
 
     def reset(self):
         self.L.gsr_profile_reset()
