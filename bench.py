@@ -214,10 +214,17 @@ def main():
         try:
             with open(args.pmc_file) as fh:
                 pmc = json.load(fh)
-            v = pmc.get("kernels", {}).get(dom, {}).get("valu_active_per_wave_cycle")
+            pk = pmc.get("kernels", {}).get(dom, {})
+            v = pk.get("valu_active_per_wave_cycle")
             if v is not None and pmc.get("workload") == args.workload:
                 # SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES: the blend kernels are VALU/latency-bound
                 roofline["valu_active_per_wave_cycle_pmc"] = v
+            n_valu = pk.get("counters", {}).get("SQ_INSTS_VALU")
+            if n_valu and pmc.get("workload") == args.workload:
+                # VALU issue roofline: a wave64 VALU instruction occupies a 16-lane SIMD for 4
+                # cycles; 256 CUs x 4 SIMDs at the 2.4 GHz peak engine clock
+                peak = 256 * 4 * 2.4e9 / 4.0
+                roofline["valu_issue_frac_pmc"] = round(n_valu / (kd["avg_ms"] * 1e-3) / peak, 4)
         except (OSError, ValueError):
             pass
 

@@ -461,56 +461,58 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
       const bool contrib = cv[u];
       if (__ballot(contrib) == 0ull) continue;  // wave-uniform skip
       const uint32_t j = (packed >> (8 * u)) & 0xffu;
-      const float G = Gv[u];
-      const float alpha = av[u];
+      // Branch-free: a lane whose pixel does not take this splat runs the same arithmetic with
+      // G = alpha = 0, which makes every gradient term exactly zero and T / (1 - 0) == T; its
+      // recurrence state is kept by selects.  Contributing lanes compute exactly the operations
+      // of the reference (backward.cu:486-555).
+      const float G = contrib ? Gv[u] : 0.0f;
+      const float alpha = contrib ? av[u] : 0.0f;
       const float4 r0 = s_r0[j];
       const float4 r1 = s_r1[j];
+      const float4 r2 = s_r2[j];
       const float dx = r0.x - pfx, dy = r0.y - pfy;
 
       float g[kAccFloats];
-#pragma unroll
-      for (int k = 0; k < kAccFloats; k++) g[k] = 0.0f;
-      if (contrib) {
-        const float4 r2 = s_r2[j];
-        T = T / (1.f - alpha);
-        const float dchannel_dcolor = alpha * T;
-        float col[NC];
-        col[0] = r1.w; col[1] = r2.x; col[2] = r2.y;
-        if (NC > 3) { col[3 % NC] = r1.z; col[4 % NC] = 1.0f; }
-        if (FEAT) {
-          const float f2 = s_f2[j];
-          col[5 % NC] = r2.z; col[6 % NC] = r2.w; col[7 % NC] = f2;
-        }
-        float cdot = 0.0f;
-#pragma unroll
-        for (int c = 0; c < NC; c++) cdot += col[c] * dpix[c];
-        acc_dot = last_alpha * last_cdot + (1.f - last_alpha) * acc_dot;
-        last_cdot = cdot;
-        float dL_dalpha = cdot - acc_dot;
-        g[kAccR] = dchannel_dcolor * dpix[0];
-        g[kAccG] = dchannel_dcolor * dpix[1];
-        g[kAccB] = dchannel_dcolor * dpix[2];
-        if (NC > 3) g[kAccDepth] = dchannel_dcolor * dpix[3 % NC];
-        if (FEAT) {
-          g[kAccF0] = dchannel_dcolor * dpix[5 % NC];
-          g[kAccF1] = dchannel_dcolor * dpix[6 % NC];
-          g[kAccF2] = dchannel_dcolor * dpix[7 % NC];
-        }
-        dL_dalpha *= T;
-        last_alpha = alpha;
-        if (has_bg) dL_dalpha += (-T_final / (1.f - alpha)) * bg_dot;
-        const float dL_dG = r1.y * dL_dalpha;
-        const float gdx = G * dx;
-        const float gdy = G * dy;
-        const float dG_ddelx = -gdx * r0.z - gdy * r0.w;
-        const float dG_ddely = -gdy * r1.x - gdx * r0.w;
-        g[kAccMx] = dL_dG * dG_ddelx * ddelx_dx;
-        g[kAccMy] = dL_dG * dG_ddely * ddely_dy;
-        g[kAccCa] = -0.5f * gdx * dx * dL_dG;
-        g[kAccCb] = -0.5f * gdx * dy * dL_dG;
-        g[kAccCc] = -0.5f * gdy * dy * dL_dG;
-        g[kAccOp] = G * dL_dalpha;
+      T = T / (1.f - alpha);
+      const float dchannel_dcolor = alpha * T;
+      float col[NC];
+      col[0] = r1.w; col[1] = r2.x; col[2] = r2.y;
+      if (NC > 3) { col[3 % NC] = r1.z; col[4 % NC] = 1.0f; }
+      if (FEAT) {
+        const float f2 = s_f2[j];
+        col[5 % NC] = r2.z; col[6 % NC] = r2.w; col[7 % NC] = f2;
       }
+      float cdot = 0.0f;
+#pragma unroll
+      for (int c = 0; c < NC; c++) cdot += col[c] * dpix[c];
+      const float acc_new = last_alpha * last_cdot + (1.f - last_alpha) * acc_dot;
+      float dL_dalpha = cdot - acc_new;
+      acc_dot = contrib ? acc_new : acc_dot;
+      last_cdot = contrib ? cdot : last_cdot;
+      last_alpha = contrib ? alpha : last_alpha;
+      g[kAccR] = dchannel_dcolor * dpix[0];
+      g[kAccG] = dchannel_dcolor * dpix[1];
+      g[kAccB] = dchannel_dcolor * dpix[2];
+      g[kAccDepth] = NC > 3 ? dchannel_dcolor * dpix[3 % NC] : 0.0f;
+      g[kAccF0] = FEAT ? dchannel_dcolor * dpix[5 % NC] : 0.0f;
+      g[kAccF1] = FEAT ? dchannel_dcolor * dpix[6 % NC] : 0.0f;
+      g[kAccF2] = FEAT ? dchannel_dcolor * dpix[7 % NC] : 0.0f;
+      dL_dalpha *= T;
+      if (has_bg) dL_dalpha += (-T_final / (1.f - alpha)) * bg_dot;
+      const float dL_dG = r1.y * dL_dalpha;
+      const float gdx = G * dx;
+      const float gdy = G * dy;
+      const float dG_ddelx = -gdx * r0.z - gdy * r0.w;
+      const float dG_ddely = -gdy * r1.x - gdx * r0.w;
+      g[kAccMx] = dL_dG * dG_ddelx * ddelx_dx;
+      g[kAccMy] = dL_dG * dG_ddely * ddely_dy;
+      g[kAccCa] = -0.5f * gdx * dx * dL_dG;
+      g[kAccCb] = -0.5f * gdx * dy * dL_dG;
+      g[kAccCc] = -0.5f * gdy * dy * dL_dG;
+      g[kAccOp] = G * dL_dalpha;
+      g[kAccUsed] = 0.0f;
+      g[14] = 0.0f;
+      g[15] = 0.0f;
       const float sum = wave_reduce16_dpp(g, lane);
       if ((lane & 3) == 0) {
         const int k = reduce16_slot(lane, swap_orient);
