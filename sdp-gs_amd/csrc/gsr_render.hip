@@ -6,9 +6,11 @@
 //
 // gfx950 design:
 //  * one 256-lane workgroup (4 waves of 64) per 16x16 tile; wave w owns pixel rows 4w..4w+3;
-//  * XCD-aware tile order: blocks are dealt round-robin over the 8 XCDs, so block b is remapped
-//    to a contiguous band of tiles per XCD and neighbouring tiles (which share most of their
-//    splats) hit the same 4 MiB L2;
+//  * tile schedule: workgroups take tiles heaviest first (tile_schedule_kernel, LPT order), so
+//    the centre-heavy tiles start early instead of forming the tail (GSR_TILE_ORDER=natural|xcd
+//    select the natural order or contiguous per-XCD bands, both measured slower);
+//  * per-wave culling: each wave compacts the batch to the splats that can reach alpha >= 1/255
+//    in its 4 pixel rows (same conservative test as the binning);
 //  * batches of 256 splat records (64 B each, packed by the preprocess) staged in LDS and read
 //    by all lanes as broadcasts;
 //  * backward: the tile is replayed back to front starting at the tile's largest n_contrib (no
