@@ -123,8 +123,11 @@ def main():
     stats = {"R": [], "Pv": []}
 
     def step(record=False):
-        for p in model.parameters():
-            p.grad = None
+        if reducer is not None:
+            reducer.attach_grads()  # grads accumulate straight into the all-reduce buckets
+        else:
+            for p in model.parameters():
+                p.grad = None
         for cam in my_cams:
             pkg = render(cam, model, pipe, bg, opt)
             torch.autograd.backward([pkg["render"], pkg["depth"], pkg["feature"]],

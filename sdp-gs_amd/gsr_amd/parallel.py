@@ -45,9 +45,24 @@ class GradAllReducer:
             self.offsets.append(off)
             off += p.numel()
 
+    def attach_grads(self):
+        """Zero the flat buffer and make every parameter's .grad a view into it (gradient as
+        bucket view): the backward then accumulates straight into the all-reduce buffer and
+        allreduce() needs no pack / unpack copies.  Call instead of zero_grad()."""
+        self.flat.zero_()
+        for p, off in zip(self.params, self.offsets):
+            p.grad = self.flat[off:off + p.numel()].view_as(p)
+
+    def _attached(self, p, off):
+        g = p.grad
+        return (g is not None and g.data_ptr() == self.flat[off:off + 1].data_ptr()
+                and g.is_contiguous())
+
     def _pack(self):
         for p, off in zip(self.params, self.offsets):
             n = p.numel()
+            if self._attached(p, off):
+                continue
             if p.grad is None:
                 self.flat[off:off + n].zero_()
             else:
@@ -56,6 +71,8 @@ class GradAllReducer:
     def _unpack(self):
         for p, off in zip(self.params, self.offsets):
             n = p.numel()
+            if self._attached(p, off):
+                continue
             v = self.flat[off:off + n].view_as(p)
             if p.grad is None:
                 p.grad = v.clone()
@@ -87,15 +104,20 @@ def allreduce_densification_stats(xyz_gradient_accum: torch.Tensor, denom: torch
 
 
 def init_from_env(backend: str = "nccl"):
-    """One process per GPU (torch.distributed.run env: RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*)."""
+    """One process per GPU (torch.distributed.run env: RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*).
+    Returns (rank, world, device index).  GSR_DIST_BACKEND overrides the backend (e.g. "gloo" to
+    rehearse several ranks on one GPU: the device index is LOCAL_RANK modulo the visible GPUs)."""
+    backend = os.environ.get("GSR_DIST_BACKEND", backend)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = torch.cuda.device_count()  # does not initialise the device
+    dev_index = local % ndev if ndev > 0 else local
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend == "nccl":
-            torch.cuda.set_device(local)
-            dist.init_process_group(backend, device_id=torch.device("cuda", local))
+            torch.cuda.set_device(dev_index)
+            dist.init_process_group(backend, device_id=torch.device("cuda", dev_index))
         else:
             dist.init_process_group(backend)
-    return rank, world, local
+    return rank, world, dev_index

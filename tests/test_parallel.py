@@ -37,14 +37,20 @@ def _view_loss(params, v):
             + torch.sigmoid(params[2] * (v + 1)).mean())
 
 
-def _worker(rank, world, port, n_views, bucket_bytes, q):
+def _worker(rank, world, port, n_views, bucket_bytes, attach, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     params = _params()
+    reducer = GradAllReducer(params, bucket_bytes=bucket_bytes)
+    if attach:  # .grad are views into the all-reduce buffer (bench.py's training step)
+        reducer.attach_grads()
     for v in shard_views(n_views, rank, world):
         _view_loss(params, v).backward()
-    GradAllReducer(params, bucket_bytes=bucket_bytes).allreduce()
+    if attach:
+        assert all(p.grad.data_ptr() == reducer.flat[o:o + 1].data_ptr()
+                   for p, o in zip(params, reducer.offsets))
+    reducer.allreduce()
     accum = torch.full((10,), float(rank + 1))
     denom = torch.ones(10)
     radii = torch.arange(10, dtype=torch.float32) * (rank + 1)
@@ -55,12 +61,13 @@ def _worker(rank, world, port, n_views, bucket_bytes, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n_views,bucket_bytes", [(6, 64 << 20), (7, 4096)])
-def test_sharded_allreduce_equals_single_process(n_views, bucket_bytes):
+@pytest.mark.parametrize("n_views,bucket_bytes,attach", [(6, 64 << 20, False), (7, 4096, False),
+                                                        (7, 4096, True)])
+def test_sharded_allreduce_equals_single_process(n_views, bucket_bytes, attach):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, n_views, bucket_bytes, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, n_views, bucket_bytes, attach, q)) for r in range(2)]
     for p in procs:
         p.start()
     grads, accum, denom, radii = q.get(timeout=120)
