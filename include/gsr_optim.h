@@ -1,0 +1,34 @@
+/*
+ * gsr_optim.h -- C ABI of libgsr's fused optimizer step.
+ *
+ * Replaces the torch.optim.Adam step that train.py runs after every backward
+ * (train.py:229-231) over GaussianModel's parameter groups (scene/gaussian_model.py:217-271:
+ * Adam(groups, lr=0.0, eps=1e-15), one tensor per group).  The optimizer state stays in the
+ * caller's tensors (PyTorch's Adam state dict: exp_avg, exp_avg_sq, step), so the reference's
+ * densification code that edits optimizer.state (gaussian_model.py:400-470) keeps working.
+ */
+#ifndef GSR_OPTIM_H
+#define GSR_OPTIM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GSR_ADAM_MAX_TENSORS 16
+
+/* One Adam step over n_tensors float32 tensors in ONE launch (non-amsgrad, L2 weight decay).
+ * params/grads/exp_avg/exp_avg_sq[t]: device pointers to numel[t] contiguous floats;
+ * lr[t], weight_decay[t]: the tensor's group hyper-parameters; step[t]: the step count AFTER
+ * increment (>= 1).  Arithmetic and host scalars follow torch.optim.adam._multi_tensor_adam.
+ * Returns 0 on success, 1 on invalid arguments, 2 on a launch error. */
+int gsr_adam_step(int n_tensors, float* const* params, const float* const* grads,
+                  float* const* exp_avg, float* const* exp_avg_sq, const int64_t* numel,
+                  const double* lr, const double* weight_decay, const double* step,
+                  double beta1, double beta2, double eps, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GSR_OPTIM_H */

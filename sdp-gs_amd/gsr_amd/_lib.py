@@ -100,6 +100,16 @@ def load():
             _p, _p, _p, _p, _p, _p, _p, _p,  # grads: means2D, means3D, dc, rest, op, scale, rot, lang
             _i,                          # accumulate
             _p, _i]                      # stream, debug
+        # include/gsr_optim.h
+        _pp = ctypes.POINTER(_p)
+        L.gsr_adam_step.restype = _i
+        L.gsr_adam_step.argtypes = [
+            _i, _pp, _pp, _pp, _pp,                      # n, params, grads, exp_avg, exp_avg_sq
+            ctypes.POINTER(ctypes.c_int64),              # numel
+            ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),  # lr, weight_decay
+            ctypes.POINTER(ctypes.c_double),             # step
+            ctypes.c_double, ctypes.c_double, ctypes.c_double,  # beta1, beta2, eps
+            _p]                                          # stream
         L.gsr_mark_visible.restype = _i
         L.gsr_mark_visible.argtypes = [_i, _p, _p, _p, _p, _p]
         for n in ("gsr_geom_buffer_bytes", "gsr_binning_buffer_bytes"):

@@ -1,0 +1,80 @@
+"""Fused Adam for the Gaussian parameters (include/gsr_optim.h).
+
+`FusedAdam` is a drop-in for the optimizer GaussianModel.training_setup creates
+(`torch.optim.Adam(param_groups, lr=0.0, eps=1e-15)`, scene/gaussian_model.py:217-271): it IS a
+torch.optim.Adam (same constructor, param groups, state dict with exp_avg / exp_avg_sq / step), so
+the reference's learning-rate schedule (`update_learning_rate`, :277) and its densification code,
+which edits `optimizer.state` and `group["params"]` directly (:400-470), work unchanged.  Only
+`step()` differs: every tensor of every group is updated by ONE HIP launch (one streaming pass,
+28 B per element) instead of PyTorch's per-group foreach passes.  There is no CPU path.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+
+MAX_TENSORS = 16  # GSR_ADAM_MAX_TENSORS
+
+
+class FusedAdam(torch.optim.Adam):
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0,
+                 amsgrad=False, *, maximize=False):
+        if amsgrad or maximize:
+            raise ValueError("FusedAdam implements Adam without amsgrad / maximize")
+        super().__init__(params, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay,
+                         amsgrad=False, foreach=False)
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        batches = {}
+        for group in self.param_groups:
+            beta1, beta2 = group["betas"]
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                g = p.grad
+                if g.is_sparse:
+                    raise RuntimeError("FusedAdam does not support sparse gradients")
+                if not p.is_cuda:
+                    raise RuntimeError("FusedAdam updates HIP tensors only (no CPU path)")
+                if p.dtype != torch.float32 or g.dtype != torch.float32:
+                    raise RuntimeError("FusedAdam expects float32 parameters and gradients")
+                state = self.state[p]
+                if len(state) == 0:  # torch.optim.Adam._init_group layout
+                    state["step"] = torch.tensor(0.0, dtype=torch.float32)
+                    state["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    state["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                state["step"] += 1
+                m, v = state["exp_avg"], state["exp_avg_sq"]
+                for t, name in ((p, "param"), (g, "grad"), (m, "exp_avg"), (v, "exp_avg_sq")):
+                    if not t.is_contiguous() or t.numel() != p.numel() or t.device != p.device:
+                        raise RuntimeError(f"FusedAdam: {name} must be contiguous, on the "
+                                           "parameter's device, with the parameter's size")
+                key = (p.device, float(beta1), float(beta2), float(group["eps"]))
+                batches.setdefault(key, []).append(
+                    (p, g, m, v, float(group["lr"]), float(group["weight_decay"]),
+                     float(state["step"])))
+        L = _lib.load()
+        for (dev, beta1, beta2, eps), items in batches.items():
+            stream = torch.cuda.current_stream(dev).cuda_stream
+            for c in range(0, len(items), MAX_TENSORS):
+                chunk = items[c:c + MAX_TENSORS]
+                n = len(chunk)
+                ptrs = [(ctypes.c_void_p * n)(*[it[k].data_ptr() for it in chunk]) for k in range(4)]
+                numel = (ctypes.c_int64 * n)(*[it[0].numel() for it in chunk])
+                lr = (ctypes.c_double * n)(*[it[4] for it in chunk])
+                wd = (ctypes.c_double * n)(*[it[5] for it in chunk])
+                steps = (ctypes.c_double * n)(*[it[6] for it in chunk])
+                with torch.cuda.device(dev):
+                    rc = L.gsr_adam_step(n, ptrs[0], ptrs[1], ptrs[2], ptrs[3], numel, lr, wd,
+                                         steps, beta1, beta2, eps, stream)
+                if rc != 0:
+                    raise RuntimeError(f"gsr_adam_step failed with status {rc}")
+        return loss

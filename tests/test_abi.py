@@ -6,7 +6,8 @@ import re
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADERS = [os.path.join(ROOT, "include", h) for h in ("gsr.h", "gsr_testing.h")]
+HEADERS = sorted(os.path.join(ROOT, "include", h) for h in os.listdir(os.path.join(ROOT, "include"))
+                 if h.endswith(".h"))
 
 
 def declared_symbols():
