@@ -302,8 +302,10 @@ __global__ __launch_bounds__(kThreads) void radix_onesweep_kernel(
   for (uint32_t i = (uint32_t)t; i < nvalid; i += kThreads) {
     const uint32_t k = s_k[i];
     const uint32_t o = s_gofs[(k >> shift) & mask] + i;
-    kout[o] = k;
-    vout[o] = s_v[i];
+    if (o < n) {  // only a timed-out look-back (error word raised) can produce o >= n
+      kout[o] = k;
+      vout[o] = s_v[i];
+    }
   }
 }
 
