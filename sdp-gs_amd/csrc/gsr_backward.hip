@@ -13,7 +13,10 @@
 namespace gsr {
 namespace {
 
-constexpr int kThreads = 256;
+#ifndef GSR_BWD_THREADS
+#define GSR_BWD_THREADS 256
+#endif
+constexpr int kThreads = GSR_BWD_THREADS;  // Gaussians per workgroup (LDS staging: 192 B each)
 
 __device__ __forceinline__ void put3(float* p, size_t i, V3 v) {
   p[3 * i] = v.x; p[3 * i + 1] = v.y; p[3 * i + 2] = v.z;
