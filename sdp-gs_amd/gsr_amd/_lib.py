@@ -110,6 +110,20 @@ def load():
             ctypes.POINTER(ctypes.c_double),             # step
             ctypes.c_double, ctypes.c_double, ctypes.c_double,  # beta1, beta2, eps
             _p]                                          # stream
+        # include/gsr_densify.h
+        _i64 = ctypes.c_int64
+        _u32 = ctypes.c_uint32
+        L.gsr_densify_stats.restype = _i
+        L.gsr_densify_stats.argtypes = [_i64, _p, _i64, _p, _p, _p, _p, _p, _p]
+        L.gsr_densify_classify.restype = _i
+        L.gsr_densify_classify.argtypes = [_i64, _p, _p, _p, _p, _f, _f, _f, _i, _f, _p, _p, _p]
+        L.gsr_select_scratch_bytes.restype = _sz
+        L.gsr_select_scratch_bytes.argtypes = [_i64]
+        L.gsr_select_rows.restype = _i
+        L.gsr_select_rows.argtypes = [_i64, _p, _u32, _u32, _p, _p, _p, _p]
+        L.gsr_compact_rows.restype = _i
+        L.gsr_compact_rows.argtypes = [_i, _pp, _pp, _pp, ctypes.POINTER(_i64),
+                                       ctypes.POINTER(_u32), _i64, _p, _i64, _p]
         L.gsr_mark_visible.restype = _i
         L.gsr_mark_visible.argtypes = [_i, _p, _p, _p, _p, _p]
         for n in ("gsr_geom_buffer_bytes", "gsr_binning_buffer_bytes"):

@@ -46,6 +46,7 @@ class SplatModel:
     scaling_activation = staticmethod(torch.exp)
     opacity_activation = staticmethod(torch.sigmoid)
     rotation_activation = staticmethod(torch.nn.functional.normalize)
+    scaling_inverse_activation = staticmethod(torch.log)
 
     def __init__(self, params: GaussianParams, device="cuda", active_sh_degree=None):
         p = params.to(device)
@@ -61,8 +62,8 @@ class SplatModel:
         self.confidence = p.confidence.clone()
 
     def parameters(self):
-        return [self._xyz, self._features_dc, self._features_rest, self._scaling, self._rotation,
-                self._opacity, self._language_feature]
+        return [p for p in (self._xyz, self._features_dc, self._features_rest, self._scaling,
+                            self._rotation, self._opacity, self._language_feature) if p is not None]
 
     @property
     def get_xyz(self):
@@ -92,3 +93,46 @@ class SplatModel:
         # the reference passes the raw _rotation here (scene/gaussian_model.py:185-186)
         return build_covariance_from_scaling_rotation(self.get_scaling, scaling_modifier,
                                                       self._rotation)
+
+    def training_setup(self, training_args, spatial_lr_scale=1.0, prune_from_iter=500):
+        """scene/gaussian_model.py:217-271: densification statistics, parameters as nn.Parameter,
+        the named param groups (language group first when include_feature) and
+        Adam(lr=0.0, eps=1e-15) -- here the one-launch FusedAdam.  `args.prune_from_iter`
+        (arguments/__init__.py:92) is what prune_points consults."""
+        from types import SimpleNamespace
+
+        from .optim import FusedAdam
+        ta = training_args
+        P = self._xyz.shape[0]
+        dev = self._xyz.device
+        self.percent_dense = ta.percent_dense
+        self.spatial_lr_scale = spatial_lr_scale
+        self.args = SimpleNamespace(prune_from_iter=prune_from_iter)
+        self.xyz_gradient_accum = torch.zeros((P, 1), device=dev)
+        self.denom = torch.zeros((P, 1), device=dev)
+        self.max_radii2D = torch.zeros((P,), device=dev)
+        for name in ("_xyz", "_features_dc", "_features_rest", "_scaling", "_rotation",
+                     "_opacity", "_language_feature"):
+            setattr(self, name, torch.nn.Parameter(getattr(self, name).detach()
+                                                   .requires_grad_(True)))
+        groups = [
+            {"params": [self._xyz], "lr": ta.position_lr_init * spatial_lr_scale, "name": "xyz"},
+            {"params": [self._features_dc], "lr": ta.feature_lr, "name": "f_dc"},
+            {"params": [self._features_rest], "lr": ta.feature_lr / 20.0, "name": "f_rest"},
+            {"params": [self._opacity], "lr": ta.opacity_lr, "name": "opacity"},
+            {"params": [self._scaling], "lr": ta.scaling_lr, "name": "scaling"},
+            {"params": [self._rotation], "lr": ta.rotation_lr, "name": "rotation"},
+        ]
+        if getattr(ta, "include_feature", True):
+            groups = [{"params": [self._language_feature], "lr": ta.language_feature_lr,
+                       "name": "language_feature"}] + groups[1:3] + groups[:1] + groups[3:]
+        else:
+            self._language_feature = None
+        self.optimizer = FusedAdam(groups, lr=0.0, eps=1e-15)
+        return self.optimizer
+
+
+# the reference's densification methods (scene/gaussian_model.py:400-612) on libgsr
+from . import densify as _densify  # noqa: E402
+
+_densify.install(SplatModel)
