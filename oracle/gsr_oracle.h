@@ -27,6 +27,8 @@
 #ifndef GSR_ORACLE_H
 #define GSR_ORACLE_H
 
+#include <stdint.h>
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -101,6 +103,10 @@ int oracle_get_depths(const oracle_state* st, float* out);          /* [P] */
 int oracle_get_rgb(const oracle_state* st, float* out);             /* [P*3] */
 int oracle_get_tiles_touched(const oracle_state* st, unsigned* out);/* [P] */
 int oracle_get_cov3D(const oracle_state* st, float* out);           /* [P*6] */
+
+/* distCUDA2 (simple_knn, un-vendored; scene/gaussian_model.py:20,198,514) by brute force:
+ * gsr_oracle_knn.c.  pts [P,3]; mean [P]; idx [P,3] or NULL. */
+void oracle_dist_knn3(int64_t P, const float* pts, float* mean, int32_t* idx);
 
 #ifdef __cplusplus
 }

@@ -46,6 +46,8 @@ def lib():
         L.oracle_free.argtypes = [_p]
         L.oracle_mark_visible.restype = _i
         L.oracle_mark_visible.argtypes = [_i, _p, _p, _p, _p]
+        L.oracle_dist_knn3.restype = None
+        L.oracle_dist_knn3.argtypes = [ctypes.c_int64, _p, _p, _p]
         for name in ("point_list", "ranges", "final_T", "n_contrib", "means2D", "conic_opacity",
                      "depths", "rgb", "tiles_touched", "cov3D"):
             fn = getattr(L, "oracle_get_" + name)
@@ -195,3 +197,13 @@ def mark_visible(means3D, viewmatrix, projmatrix):
     out = np.zeros((m.shape[0],), np.uint8)
     lib().oracle_mark_visible(m.shape[0], _ptr(m), _ptr(v), _ptr(p), _ptr(out))
     return out.astype(bool)
+
+
+def dist_knn3(points):
+    """distCUDA2 restated (oracle/gsr_oracle_knn.c): (mean sq. dist [P] f32, indices [P,3] i32)."""
+    pts = _arr(points).reshape(-1, 3)
+    P = pts.shape[0]
+    mean = np.zeros(P, np.float32)
+    idx = np.zeros((P, 3), np.int32)
+    lib().oracle_dist_knn3(P, _ptr(pts), _ptr(mean), _ptr(idx))
+    return mean, idx

@@ -124,6 +124,11 @@ def load():
         L.gsr_compact_rows.restype = _i
         L.gsr_compact_rows.argtypes = [_i, _pp, _pp, _pp, ctypes.POINTER(_i64),
                                        ctypes.POINTER(_u32), _i64, _p, _i64, _p]
+        # include/gsr_knn.h
+        L.gsr_knn_scratch_bytes.restype = _sz
+        L.gsr_knn_scratch_bytes.argtypes = [_i64]
+        L.gsr_dist_knn3.restype = _i
+        L.gsr_dist_knn3.argtypes = [_i64, _p, _p, _p, _p, _p]
         L.gsr_mark_visible.restype = _i
         L.gsr_mark_visible.argtypes = [_i, _p, _p, _p, _p, _p]
         for n in ("gsr_geom_buffer_bytes", "gsr_binning_buffer_bytes"):

@@ -378,10 +378,31 @@ def densify_and_prune(self, max_grad, min_opacity, extent, max_screen_size, iter
 
 
 def proximity(self, scene_extent, include_feature, N=3):
-    """scene/gaussian_model.py:513-532 -- needs the 3-NN search of distCUDA2 (SURVEY.md 8(f)
-    rank 3), not built yet."""
-    raise NotImplementedError("proximity densification needs the KNN (distCUDA2) row; "
-                              "call densify_and_prune with iteration >= 2000")
+    """scene/gaussian_model.py:513-532: Gaussians far from their neighbours (mean squared 3-NN
+    distance > 5 extent) and large (max scale > extent) get N new Gaussians at midpoints towards
+    their neighbours (the reference's pairing: sources tiled, neighbour lists interleaved), with
+    the neighbour's scale / opacity / language feature, identity rotation and zero colour.
+    The 3-NN search is gsr_dist_knn3 (gsr_amd.knn.distCUDA2); the append is one rebuild."""
+    from .knn import distCUDA2
+    with torch.no_grad():
+        dist, nearest = distCUDA2(self._xyz)
+        sel = torch.logical_and(dist > (5.0 * scene_extent),
+                                self.get_scaling.max(dim=1).values > scene_extent)
+        flags = sel.to(torch.uint8)
+        n_sel = int(flags.sum())
+        idx = _selected(flags, 1, n_sel)
+        new_indices = nearest[idx].reshape(-1).long()
+        source_xyz = self._xyz[idx].repeat(1, N, 1).reshape(-1, 3)
+        new_xyz = (source_xyz + self._xyz[new_indices]) / 2
+        new_rotation = torch.zeros_like(self._rotation[new_indices])
+        new_rotation[:, 0] = 1
+        lang = self._language_feature
+        ext = _extras_dict(new_xyz, torch.zeros_like(self._features_dc[new_indices]),
+                           torch.zeros_like(self._features_rest[new_indices]),
+                           None if lang is None or not _has_group(self, "language_feature")
+                           else lang[new_indices],
+                           self._opacity[new_indices], self._scaling[new_indices], new_rotation)
+        _rebuild(self, None, _rows(self._xyz) + new_xyz.shape[0], ext, fresh_stats=True)
 
 
 METHODS = ("add_densification_stats", "update_densification_stats", "prune_points",

@@ -136,12 +136,32 @@ class RefDensify:
         drop = torch.cat((sel, torch.zeros(N * int(sel.sum()), device=sel.device, dtype=bool)))
         self.prune_points(drop, iteration)
 
+    def proximity(self, extent, N=3):
+        """:513-532, with distCUDA2 from the CPU oracle (oracle/gsr_oracle_knn.c)."""
+        from oracle.oracle import dist_knn3
+        d, nn = dist_knn3(self._xyz.detach().cpu().numpy())
+        dev = self._xyz.device
+        dist, nearest = torch.from_numpy(d).to(dev), torch.from_numpy(nn).to(dev)
+        sel = torch.logical_and(dist > (5. * extent), self.get_scaling.max(dim=1).values > extent)
+        idx = nearest[sel].reshape(-1).long()
+        new = {"xyz": (self._xyz[sel].repeat(1, N, 1).reshape(-1, 3) + self._xyz[idx]) / 2,
+               "scaling": self._scaling[idx], "opacity": self._opacity[idx],
+               "f_dc": torch.zeros_like(self._features_dc[idx]),
+               "f_rest": torch.zeros_like(self._features_rest[idx])}
+        rot = torch.zeros_like(self._rotation[idx])
+        rot[:, 0] = 1
+        new["rotation"] = rot
+        if self._language_feature is not None:
+            new["language_feature"] = self._language_feature[idx]
+        self.postfix(new)
+
     def densify_and_prune(self, max_grad, min_opacity, extent, max_screen_size, iteration):
         grads = self.xyz_gradient_accum / self.denom
         grads[grads.isnan()] = 0.0
         self.clone(grads, max_grad, extent)
         self.split(grads, max_grad, extent, iteration)
-        assert iteration >= 2000, "proximity is not restated here"
+        if iteration < 2000:
+            self.proximity(extent)
         prune = (self.get_opacity < min_opacity).squeeze()
         if max_screen_size:
             big_vs = self.max_radii2D > max_screen_size

@@ -225,6 +225,21 @@ def test_densify_and_prune_matches_reference(include_feature, iteration, max_scr
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("include_feature", [True, False])
+def test_densify_and_prune_with_proximity_matches_reference(include_feature):
+    """iteration < 2000: clone + split, then proximity densification (3-NN: gsr_dist_knn3 here,
+    the CPU oracle's distCUDA2 in the restatement), then the prune."""
+    P = 20_000
+    m, ref = _pair(P, seed=6, include_feature=include_feature)
+    extent = 1e-4  # proximity picks points whose mean squared 3-NN distance exceeds 5e-4
+    torch.manual_seed(8)
+    m.densify_and_prune(THR, MIN_OP, extent, None, 1500, include_feature)
+    torch.manual_seed(8)
+    ref.densify_and_prune(THR, MIN_OP, extent, None, 1500)
+    _assert_same(m, ref)
+
+
+@pytest.mark.gpu
 def test_densify_edge_cases():
     # nothing selected, nothing pruned
     m, ref = _pair(4096, state=False)
