@@ -254,15 +254,16 @@ def _clone_rows(self, idx):
                         self._opacity[idx], self._scaling[idx], self._rotation[idx])
 
 
-def _split_rows(self, idx, N):
+def _split_rows(self, idx, N, generator=None):
     """densify_and_split's children (:544-555): N samples from N(0, scale) rotated into place,
     scales shrunk by 0.8 N, everything else repeated (torch.normal draws the reference's
-    samples from the same generator)."""
+    samples from the same generator; data-parallel replicas pass one identically seeded
+    `generator` so that every rank draws the same samples)."""
     from .model import build_rotation
     sel_scaling = self.scaling_activation(self._scaling[idx])   # get_scaling[selected]
     stds = sel_scaling.repeat(N, 1)
     means = torch.zeros((stds.size(0), 3), device=stds.device)
-    samples = torch.normal(mean=means, std=stds)
+    samples = torch.normal(mean=means, std=stds, generator=generator)
     rots = build_rotation(self._rotation[idx]).repeat(N, 1, 1)
     new_xyz = torch.bmm(rots, samples.unsqueeze(-1)).squeeze(-1) + self._xyz[idx].repeat(N, 1)
     new_scaling = self.scaling_inverse_activation(sel_scaling.repeat(N, 1) / (0.8 * N))
@@ -301,7 +302,7 @@ def densify_and_clone(self, grads, grad_threshold, scene_extent, include_feature
 
 
 def densify_and_split(self, grads, grad_threshold, scene_extent, iter, include_feature=False,
-                      N=2):
+                      N=2, generator=None):
     """scene/gaussian_model.py:534-564 (grads may cover only the first rows: zero padded)."""
     with torch.no_grad():
         P = _rows(self._xyz)
@@ -310,7 +311,7 @@ def densify_and_split(self, grads, grad_threshold, scene_extent, iter, include_f
         flags, (_, ns) = classify(self, g, None, grad_threshold,
                                   self.percent_dense * scene_extent)
         idx = _selected(flags, SPLIT, ns)
-        ext = _split_rows(self, idx, N)
+        ext = _split_rows(self, idx, N, generator)
         if _prune_active(self, iter):
             # append the children and drop the split parents in the same pass
             keep = torch.cat((flags & SPLIT, torch.zeros(N * ns, dtype=torch.uint8,
@@ -322,13 +323,17 @@ def densify_and_split(self, grads, grad_threshold, scene_extent, iter, include_f
 
 
 def densify_and_prune(self, max_grad, min_opacity, extent, max_screen_size, iteration,
-                      include_feature=False):
+                      include_feature=False, generator=None):
     """scene/gaussian_model.py:583-604: clone, split, (proximity before iteration 2000), prune.
 
     Without proximity the whole update is ONE rebuild: the final keep set is known from the
     classify flags (a clone / split child inherits its parent's opacity; split children get the
     world-space size test on their own shrunk scales), so the rows
-    [originals | clones | split children] are filtered and written in a single pass."""
+    [originals | clones | split children] are filtered and written in a single pass.
+
+    Data parallel (one replica per rank): all-reduce the statistics first
+    (gsr_amd.parallel.allreduce_densification_stats) and pass a generator seeded identically on
+    every rank; every other step is deterministic, so the replicas stay bit-identical."""
     with torch.no_grad():
         P = _rows(self._xyz)
         big_limit = 0.1 * extent if max_screen_size else None
@@ -337,7 +342,7 @@ def densify_and_prune(self, max_grad, min_opacity, extent, max_screen_size, iter
                                    self.percent_dense * extent, min_opacity, big_limit)
         cidx = _selected(flags, CLONE, nc)
         sidx = _selected(flags, SPLIT, ns)
-        ext = _cat_extras(_clone_rows(self, cidx), _split_rows(self, sidx, 2))
+        ext = _cat_extras(_clone_rows(self, cidx), _split_rows(self, sidx, 2, generator))
         active = _prune_active(self, iteration)
         if iteration < 2000:
             # proximity needs the clone/split result materialised (its KNN runs on it)

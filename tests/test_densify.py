@@ -269,3 +269,59 @@ def test_optimizer_steps_after_densify():
     assert not torch.equal(before, m._xyz.detach())
     for g in m.optimizer.param_groups:
         assert float(m.optimizer.state[g["params"][0]]["step"]) == 8.0
+
+
+def _dp_worker(rank, world, port, q):
+    import os
+    import torch.distributed as dist
+    from gsr_amd.parallel import allreduce_densification_stats
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    m = _model(30_000, seed=12)                 # same replica on every rank
+    gen = torch.Generator(device="cuda").manual_seed(100 + rank)
+    vs = torch.zeros((30_000, 3), device="cuda", requires_grad=True)
+    for _ in range(3):                           # each rank sees its own views
+        radii = torch.randint(0, 20, (30_000,), generator=gen, device="cuda", dtype=torch.int32)
+        vs.grad = torch.randn((30_000, 3), generator=gen, device="cuda") * 2e-3
+        m.update_densification_stats(vs, radii)
+    allreduce_densification_stats(m.xyz_gradient_accum, m.denom, m.max_radii2D)
+    # numpy: pickled by value (torch CPU tensors would go through fds of an exiting process)
+    stats = [t.cpu().numpy() for t in (m.xyz_gradient_accum, m.denom, m.max_radii2D)]
+    g = torch.Generator(device="cuda").manual_seed(7)
+    m.densify_and_prune(THR, MIN_OP, EXTENT, None, 3000, True, generator=g)
+    q.put((rank, stats, {k: v.cpu().numpy() for k, v in model_arrays(m).items()}))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_densify_data_parallel_replicas_stay_identical():
+    """Two ranks (gloo, both on cuda:0): statistics all-reduced (SUM / SUM / MAX), then
+    densify_and_prune with an identically seeded generator -> bit-identical replicas, equal to the
+    reference restatement run once on the reduced statistics."""
+    import torch.multiprocessing as mp
+    from test_parallel import _free_port
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in procs], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, s0, a0), (_, s1, a1) = res
+    assert list(a0) == list(a1)
+    for k in a0:
+        assert np.array_equal(a0[k], a1[k]), k
+    m = _model(30_000, seed=12)
+    m.xyz_gradient_accum, m.denom, m.max_radii2D = [torch.from_numpy(t).cuda() for t in s0]
+    ref = RefDensify(m)
+    # the restatement draws torch.normal from the default generator: seed it like the ranks'
+    torch.cuda.manual_seed(7)
+    ref.densify_and_prune(THR, MIN_OP, EXTENT, None, 3000)
+    b = ref.arrays()
+    for k in a0:
+        assert np.array_equal(a0[k], b[k].cpu().numpy()), k
