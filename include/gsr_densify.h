@@ -43,7 +43,8 @@ int gsr_densify_stats(int64_t P, const float* viewspace_grad, int64_t grad_strid
 /* One flag byte per Gaussian from the raw parameters (_scaling [P,3] log scales, _opacity [P]
  * logits) and the statistics (grad_accum, denom: [P]); NaN ratios count as 0 (:585-586).  With
  * denom NULL, grad_accum holds the caller's grads as they are (densify_and_clone / _split called
- * directly).  max scale = max_k exp(_scaling[i,k]).  counts (device, 2 x u32): [#clone, #split]. */
+ * directly).  max scale = max_k exp(_scaling[i,k]).  counts (device, 2 x u32, may be NULL):
+ * [#clone, #split]. */
 int gsr_densify_classify(int64_t P, const float* grad_accum, const float* denom,
                          const float* scaling, const float* opacity, float grad_threshold,
                          float scale_limit, float min_opacity, int big_enable, float big_limit,

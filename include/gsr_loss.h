@@ -1,0 +1,59 @@
+/*
+ * gsr_loss.h -- C ABI of libgsr's training losses.
+ *
+ * Replaces the loss code either side of the rasterizer in train.py:
+ *   gsr_photometric_loss[_backward]  <- Ll1 = l1_loss(image, gt) (utils/loss_utils.py:106-107) and
+ *                                       loss = (1 - lambda) Ll1 + lambda (1 - ssim(image, gt))
+ *                                       (train.py:99-100; ssim / _ssim :129-162: 11x11 Gaussian
+ *                                       window, sigma 1.5, zero padding, C1 = 1e-4, C2 = 9e-4)
+ *   gsr_pearson_loss[_backward]      <- 1 - pearson_corrcoef(x, y) (torchmetrics, train.py:126-129,
+ *                                       :149), optionally min over x and 1 / (offset - x)
+ * All pointers are device pointers, the stream a hipStream_t.  Returns 0 / 1 (invalid arguments)
+ * / 2 (launch error).
+ */
+#ifndef GSR_LOSS_H
+#define GSR_LOSS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Device scratch for one (image, gt) pair of shape [C,H,W]; the forward leaves the backward
+ * coefficients in it (12 B per pixel-channel), so forward and backward share one scratch. */
+size_t gsr_photometric_scratch_bytes(int C, int H, int W);
+
+/* image, gt: [C,H,W] float32 contiguous.  out (device, 3 floats): loss, L1 mean, SSIM mean.
+ * need_grad = 0 skips the backward coefficients. */
+int gsr_photometric_loss(int C, int H, int W, const float* image, const float* gt,
+                         float lambda_dssim, int need_grad, float* out, void* scratch,
+                         void* stream);
+
+/* grad_image = d(out . g)/d image for upstream device scalars g = (grad_loss, grad_l1,
+ * grad_ssim), each may be NULL (= 0).  Needs the scratch of a need_grad forward on the same
+ * inputs. */
+int gsr_photometric_loss_backward(int C, int H, int W, const float* image, const float* gt,
+                                  float lambda_dssim, const float* grad_loss,
+                                  const float* grad_l1, const float* grad_ssim, float* grad_image,
+                                  void* scratch, void* stream);
+
+/* Pearson correlation per column of x, y: [N, K] float32 (K <= 256).  variants = 1: r(x, y);
+ * variants = 2: also r(1 / (offset - x), y) (train.py:127-128 with offset 200).  out_r
+ * [variants*K] (may be NULL): the clamped r; out_loss [K] (may be NULL): min over variants of
+ * 1 - r (the first variant on ties, as Python's min).  Scratch: gsr_pearson_scratch_bytes; the
+ * backward reuses it. */
+size_t gsr_pearson_scratch_bytes(int K, int variants);
+int gsr_pearson_loss(int64_t N, int K, const float* x, const float* y, int variants, float offset,
+                     float* out_r, float* out_loss, void* scratch, void* stream);
+/* grad_y (and, variants = 1 only, grad_x) of sum_k grad_loss[k] * out_loss[k]; grad_loss device
+ * [K] (NULL = ones); grad_y / grad_x may be NULL. */
+int gsr_pearson_loss_backward(int64_t N, int K, const float* x, const float* y, int variants,
+                              float offset, const float* grad_loss, float* grad_y, float* grad_x,
+                              void* scratch, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GSR_LOSS_H */

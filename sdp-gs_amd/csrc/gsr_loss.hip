@@ -1,0 +1,552 @@
+// gsr_loss.hip -- the training losses either side of the rasterizer.
+//
+// Reference (utils/loss_utils.py, train.py:99-130):
+//   Ll1  = l1_loss(image, gt)                         mean |x - y|                     (:106-107)
+//   loss = (1 - lambda) Ll1 + lambda (1 - ssim(image, gt))                              (train.py:100)
+//   ssim: 11x11 Gaussian window (sigma 1.5), zero padding, five depthwise F.conv2d        (:119-162)
+//         (mu_x, mu_y, E[x^2], E[y^2], E[xy]), C1 = 0.01^2, C2 = 0.03^2, mean of the map
+//   depth: 1 - pearson_corrcoef(...) (torchmetrics), min over two variants      (train.py:126-129)
+//
+// SSIM here: one tiled kernel per pass instead of five convolutions + ~20 element-wise kernels +
+// autograd through all of them.  A workgroup owns a 32x16 output tile of one channel: both
+// images' (32+10)x(16+10) halo tiles go to LDS, a horizontal pass blurs the five moments with the
+// separable 1-D window, a vertical pass finishes them, and the map value, |x - y| and the three
+// per-pixel backward coefficients
+//     A = dm/dmu1 - 2 mu1 dm/dsigma1^2 - mu2 dm/dsigma12,  B = dm/dsigma1^2,  C = dm/dsigma12
+// are produced in registers.  The backward blurs A, B, C the same way (the window is symmetric)
+// and forms dm_total/dx(p) = blur(A) + 2 x(p) blur(B) + y(p) blur(C).  Partial sums per workgroup
+// are reduced in a fixed order (deterministic).  HBM: forward reads 8 B and writes 12 B per
+// pixel-channel, backward reads 20 B and writes 4 B.
+//
+// Pearson: per column of [N, K] inputs, torchmetrics' two-pass form (means, then centred sums
+// var_x, var_y, cov, each divided by N - 1; r = cov / sqrt(var_x var_y), clamped to [-1, 1]),
+// with the reductions in double.
+#include <math.h>
+
+#include "gsr_internal.h"
+#include "../../include/gsr_loss.h"
+
+namespace gsr {
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kR = 5;                 // window radius (window_size 11)
+constexpr int kW = 2 * kR + 1;
+constexpr int kTX = 32, kTY = 16;     // output tile
+constexpr int kIX = kTX + 2 * kR;     // 42
+constexpr int kIY = kTY + 2 * kR;     // 26
+
+struct Window {
+  float w[kW];
+};
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+  return v;
+}
+
+// workgroup sum of two floats -> out[0], out[1] (thread 0)
+__device__ __forceinline__ void block_sum2(float a, float b, float* out) {
+  __shared__ float s[2][kThreads / 64];
+  a = wave_sum(a);
+  b = wave_sum(b);
+  const int w = (int)(threadIdx.x >> 6);
+  if ((threadIdx.x & 63) == 0) {
+    s[0][w] = a;
+    s[1][w] = b;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    out[0] = (s[0][0] + s[0][1]) + (s[0][2] + s[0][3]);
+    out[1] = (s[1][0] + s[1][1]) + (s[1][2] + s[1][3]);
+  }
+}
+
+struct SsimArgs {
+  int C, H, W;
+  const float *x, *y;     // [C,H,W]
+  float *A, *B, *Cc;      // [C,H,W] backward coefficients (may be null: no grad needed)
+  float* parts;           // [blocks][2]: sum of the map, sum of |x - y|
+  Window win;
+  float c1, c2;
+};
+
+__global__ __launch_bounds__(kThreads) void ssim_fwd_kernel(SsimArgs a) {
+  __shared__ float sx[kIY][kIX], sy[kIY][kIX];
+  __shared__ float h[5][kIY][kTX];
+  const int c = blockIdx.z;
+  const int x0 = blockIdx.x * kTX, y0 = blockIdx.y * kTY;
+  const size_t plane = (size_t)c * a.H * a.W;
+  for (int e = threadIdx.x; e < kIX * kIY; e += kThreads) {
+    const int r = e / kIX, q = e - r * kIX;
+    const int gy = y0 + r - kR, gx = x0 + q - kR;
+    const bool in = gy >= 0 && gy < a.H && gx >= 0 && gx < a.W;
+    const size_t o = plane + (size_t)gy * a.W + gx;
+    sx[r][q] = in ? a.x[o] : 0.f;
+    sy[r][q] = in ? a.y[o] : 0.f;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < kIY * kTX; e += kThreads) {
+    const int r = e / kTX, q = e - r * kTX;
+    float m1 = 0.f, m2 = 0.f, e11 = 0.f, e22 = 0.f, e12 = 0.f;
+#pragma unroll
+    for (int k = 0; k < kW; k++) {
+      const float u = sx[r][q + k], v = sy[r][q + k], w = a.win.w[k];
+      m1 += w * u;
+      m2 += w * v;
+      e11 += w * (u * u);
+      e22 += w * (v * v);
+      e12 += w * (u * v);
+    }
+    h[0][r][q] = m1;
+    h[1][r][q] = m2;
+    h[2][r][q] = e11;
+    h[3][r][q] = e22;
+    h[4][r][q] = e12;
+  }
+  __syncthreads();
+  float msum = 0.f, l1sum = 0.f;
+  for (int e = threadIdx.x; e < kTY * kTX; e += kThreads) {
+    const int r = e / kTX, q = e - r * kTX;
+    const int gy = y0 + r, gx = x0 + q;
+    if (gy >= a.H || gx >= a.W) continue;
+    float mu1 = 0.f, mu2 = 0.f, e11 = 0.f, e22 = 0.f, e12 = 0.f;
+#pragma unroll
+    for (int k = 0; k < kW; k++) {
+      const float w = a.win.w[k];
+      mu1 += w * h[0][r + k][q];
+      mu2 += w * h[1][r + k][q];
+      e11 += w * h[2][r + k][q];
+      e22 += w * h[3][r + k][q];
+      e12 += w * h[4][r + k][q];
+    }
+    // _ssim (loss_utils.py:143-162), same expression order
+    const float mu1_sq = mu1 * mu1, mu2_sq = mu2 * mu2, mu1_mu2 = mu1 * mu2;
+    const float s1 = e11 - mu1_sq, s2 = e22 - mu2_sq, s12 = e12 - mu1_mu2;
+    const float a1 = 2.f * mu1_mu2 + a.c1, a2 = 2.f * s12 + a.c2;
+    const float b1 = (mu1_sq + mu2_sq) + a.c1, b2 = (s1 + s2) + a.c2;
+    const float den = b1 * b2;
+    const float m = (a1 * a2) / den;
+    msum += m;
+    const float xv = sx[r + kR][q + kR], yv = sy[r + kR][q + kR];
+    l1sum += fabsf(xv - yv);
+    if (a.A) {
+      const float dmu1 = (2.f * mu2 * a2) / den - m * (2.f * mu1) / b1;
+      const float ds1 = -m / b2;
+      const float ds12 = (2.f * a1) / den;
+      const size_t o = plane + (size_t)gy * a.W + gx;
+      a.A[o] = dmu1 - 2.f * mu1 * ds1 - mu2 * ds12;
+      a.B[o] = ds1;
+      a.Cc[o] = ds12;
+    }
+  }
+  const size_t b = ((size_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+  block_sum2(msum, l1sum, a.parts + 2 * b);
+}
+
+// parts [n][2] -> out: loss, l1 mean, ssim mean (double accumulation, fixed order)
+__global__ __launch_bounds__(kThreads) void ssim_reduce_kernel(const float* __restrict__ parts,
+                                                               int n, double inv_count,
+                                                               float lambda,
+                                                               float* __restrict__ out) {
+  __shared__ double s[2][kThreads];
+  double m = 0.0, l = 0.0;
+  for (int i = threadIdx.x; i < n; i += kThreads) {
+    m += (double)parts[2 * i];
+    l += (double)parts[2 * i + 1];
+  }
+  s[0][threadIdx.x] = m;
+  s[1][threadIdx.x] = l;
+  __syncthreads();
+  for (int d = kThreads / 2; d >= 1; d >>= 1) {
+    if ((int)threadIdx.x < d) {
+      s[0][threadIdx.x] += s[0][threadIdx.x + d];
+      s[1][threadIdx.x] += s[1][threadIdx.x + d];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float ssim = (float)(s[0][0] * inv_count), l1 = (float)(s[1][0] * inv_count);
+    out[0] = (1.0f - lambda) * l1 + lambda * (1.0f - ssim);
+    out[1] = l1;
+    out[2] = ssim;
+  }
+}
+
+struct SsimBwdArgs {
+  int C, H, W;
+  const float *x, *y, *A, *B, *Cc;
+  const float *g_loss, *g_l1, *g_ssim;  // device scalars (null = 0)
+  float lambda, inv_count;
+  float* dx;
+  Window win;
+};
+
+__global__ __launch_bounds__(kThreads) void ssim_bwd_kernel(SsimBwdArgs a) {
+  __shared__ float s[3][kIY][kIX];
+  __shared__ float h[3][kIY][kTX];
+  const int c = blockIdx.z;
+  const int x0 = blockIdx.x * kTX, y0 = blockIdx.y * kTY;
+  const size_t plane = (size_t)c * a.H * a.W;
+  // d loss / d ssim_mean and d loss / d l1_mean for the three outputs (loss, l1, ssim)
+  const float gl = a.g_loss ? *a.g_loss : 0.f;
+  const float k_ssim = (-a.lambda * gl + (a.g_ssim ? *a.g_ssim : 0.f)) * a.inv_count;
+  const float k_l1 = ((1.0f - a.lambda) * gl + (a.g_l1 ? *a.g_l1 : 0.f)) * a.inv_count;
+  for (int e = threadIdx.x; e < kIX * kIY; e += kThreads) {
+    const int r = e / kIX, q = e - r * kIX;
+    const int gy = y0 + r - kR, gx = x0 + q - kR;
+    const bool in = gy >= 0 && gy < a.H && gx >= 0 && gx < a.W;
+    const size_t o = plane + (size_t)gy * a.W + gx;
+    s[0][r][q] = in ? a.A[o] : 0.f;
+    s[1][r][q] = in ? a.B[o] : 0.f;
+    s[2][r][q] = in ? a.Cc[o] : 0.f;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < kIY * kTX; e += kThreads) {
+    const int r = e / kTX, q = e - r * kTX;
+    float u0 = 0.f, u1 = 0.f, u2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < kW; k++) {
+      const float w = a.win.w[k];
+      u0 += w * s[0][r][q + k];
+      u1 += w * s[1][r][q + k];
+      u2 += w * s[2][r][q + k];
+    }
+    h[0][r][q] = u0;
+    h[1][r][q] = u1;
+    h[2][r][q] = u2;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < kTY * kTX; e += kThreads) {
+    const int r = e / kTX, q = e - r * kTX;
+    const int gy = y0 + r, gx = x0 + q;
+    if (gy >= a.H || gx >= a.W) continue;
+    float u0 = 0.f, u1 = 0.f, u2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < kW; k++) {
+      const float w = a.win.w[k];
+      u0 += w * h[0][r + k][q];
+      u1 += w * h[1][r + k][q];
+      u2 += w * h[2][r + k][q];
+    }
+    const size_t o = plane + (size_t)gy * a.W + gx;
+    const float xv = a.x[o], yv = a.y[o];
+    const float dm = u0 + 2.f * xv * u1 + yv * u2;
+    const float d = xv - yv;
+    const float sgn = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);  // torch.abs backward: sign
+    a.dx[o] = k_ssim * dm + k_l1 * sgn;
+  }
+}
+
+// ---- Pearson -------------------------------------------------------------------------------------
+// Column k of x (and of the transformed variant xt = 1 / (offset - x) when `variants` = 2) against
+// column k of y; stats[k]: {sum x, sum y} then {Sxx, Syy, Sxy}; two passes.
+struct PearsonArgs {
+  int64_t N;
+  int K;
+  const float *x, *y;  // [N, K]
+  double* acc;         // [variants][K][8]: sx, sy, sxx, syy, sxy
+  double* parts;       // [variants][K][nblocks][3] per-workgroup partial sums
+  int nblocks;
+  int variants;
+  float offset;
+};
+
+__device__ __forceinline__ float variant_x(float x, int v, float offset) {
+  return v == 0 ? x : 1.0f / (-x + offset);  // train.py:128: 1 / (-depth_mono + 200)
+}
+
+__device__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+  return v;
+}
+
+// Partial sums per workgroup, written to their own slots: no same-address atomics (on MI355X
+// those serialise at device scope across the 8 XCDs' L2s), and a fixed reduction order.
+template <int PASS>
+__global__ __launch_bounds__(kThreads) void pearson_kernel(PearsonArgs a) {
+  __shared__ double s[3][kThreads / 64];
+  const int k = blockIdx.y, v = blockIdx.z;
+  const double* acc = a.acc + ((size_t)v * a.K + k) * 8;
+  double t0 = 0.0, t1 = 0.0, t2 = 0.0;
+  double mx = 0.0, my = 0.0;
+  if (PASS == 1) {
+    mx = acc[0] / (double)a.N;
+    my = acc[1] / (double)a.N;
+  }
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < a.N;
+       i += (int64_t)gridDim.x * kThreads) {
+    const double xv = (double)variant_x(a.x[i * a.K + k], v, a.offset);
+    const double yv = (double)a.y[i * a.K + k];
+    if (PASS == 0) {
+      t0 += xv;
+      t1 += yv;
+    } else {
+      const double dx = xv - mx, dy = yv - my;
+      t0 += dx * dx;
+      t1 += dy * dy;
+      t2 += dx * dy;
+    }
+  }
+  t0 = wave_sum_d(t0);
+  t1 = wave_sum_d(t1);
+  t2 = wave_sum_d(t2);
+  const int w = (int)(threadIdx.x >> 6);
+  if ((threadIdx.x & 63) == 0) {
+    s[0][w] = t0;
+    s[1][w] = t1;
+    s[2][w] = t2;
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    const int j = threadIdx.x;
+    double* p = a.parts + (((size_t)v * a.K + k) * a.nblocks + blockIdx.x) * 3;
+    p[j] = (s[j][0] + s[j][1]) + (s[j][2] + s[j][3]);
+  }
+}
+
+// acc[v][k][PASS ? 2..4 : 0..1] = sum over the workgroup partials (grid: K x variants)
+template <int PASS>
+__global__ __launch_bounds__(kThreads) void pearson_reduce_kernel(PearsonArgs a) {
+  __shared__ double s[3][kThreads];
+  const int k = blockIdx.x, v = blockIdx.y;
+  const double* p = a.parts + ((size_t)v * a.K + k) * a.nblocks * 3;
+  double t[3] = {0.0, 0.0, 0.0};
+  for (int b = threadIdx.x; b < a.nblocks; b += kThreads)
+#pragma unroll
+    for (int j = 0; j < 3; j++) t[j] += p[3 * b + j];
+#pragma unroll
+  for (int j = 0; j < 3; j++) s[j][threadIdx.x] = t[j];
+  __syncthreads();
+  for (int d = kThreads / 2; d >= 1; d >>= 1) {
+    if ((int)threadIdx.x < d)
+#pragma unroll
+      for (int j = 0; j < 3; j++) s[j][threadIdx.x] += s[j][threadIdx.x + d];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    double* acc = a.acc + ((size_t)v * a.K + k) * 8;
+    if (PASS == 0) {
+      acc[0] = s[0][0];
+      acc[1] = s[1][0];
+    } else {
+      acc[2] = s[0][0];
+      acc[3] = s[1][0];
+      acc[4] = s[2][0];
+    }
+  }
+}
+
+// r per (variant, column); out_r[v*K + k]; loss = min over variants of 1 - r (first wins ties),
+// out_sel[k] = chosen variant
+__global__ void pearson_finish_kernel(PearsonArgs a, float* __restrict__ out_r,
+                                      float* __restrict__ out_loss, int32_t* __restrict__ out_sel) {
+  const int k = threadIdx.x;
+  if (k >= a.K) return;
+  float best = 0.f;
+  int sel = 0;
+  for (int v = 0; v < a.variants; v++) {
+    const double* acc = a.acc + ((size_t)v * a.K + k) * 8;
+    const double nb = (double)(a.N - 1);
+    const double vx = acc[2] / nb, vy = acc[3] / nb, cxy = acc[4] / nb;
+    float r = (float)(cxy / sqrt(vx * vy));
+    if (r == r) r = fminf(fmaxf(r, -1.0f), 1.0f);  // torch.clamp keeps NaN
+    out_r[v * a.K + k] = r;
+    const float l = 1.0f - r;
+    if (v == 0 || l < best) {  // Python min(a, b): b only if b < a
+      best = l;
+      sel = v;
+    }
+  }
+  if (out_loss) out_loss[k] = best;
+  if (out_sel) out_sel[k] = sel;
+}
+
+// d(1 - r_sel)/dy_i * g: -g * [ (x_i - mx) / sqrt(Sxx Syy) - r (y_i - my) / Syy ] (0 when clamped)
+__global__ __launch_bounds__(kThreads) void pearson_bwd_kernel(PearsonArgs a,
+                                                               const int32_t* __restrict__ sel,
+                                                               const float* __restrict__ g,
+                                                               float* __restrict__ dy,
+                                                               float* __restrict__ dx) {
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= a.N) return;
+  for (int k = 0; k < a.K; k++) {
+    const int v = sel ? sel[k] : 0;
+    const double* acc = a.acc + ((size_t)v * a.K + k) * 8;
+    const double mx = acc[0] / (double)a.N, my = acc[1] / (double)a.N;
+    const double sxx = acc[2], syy = acc[3], sxy = acc[4];
+    const double rr = sxy / sqrt(sxx * syy);
+    const bool pass = rr >= -1.0 && rr <= 1.0;  // clamp backward
+    const double gk = pass ? -(double)(g ? g[k] : 1.0f) : 0.0;
+    const double xv = (double)variant_x(a.x[i * a.K + k], v, a.offset);
+    const double yv = (double)a.y[i * a.K + k];
+    const double inv = 1.0 / sqrt(sxx * syy);
+    if (dy) dy[i * a.K + k] = (float)(gk * ((xv - mx) * inv - rr * (yv - my) / syy));
+    if (dx && v == 0) dx[i * a.K + k] = (float)(gk * ((yv - my) * inv - rr * (xv - mx) / sxx));
+  }
+}
+
+}  // namespace
+}  // namespace gsr
+
+using namespace gsr;
+
+namespace {
+
+Window make_window() {
+  // loss_utils.py:119-121: exp(-(x - 5)^2 / (2 sigma^2)) in double, stored as float32, then
+  // normalised in float32
+  Window w;
+  float g[kW], sum = 0.f;
+  for (int x = 0; x < kW; x++) {
+    g[x] = (float)exp(-(double)((x - kR) * (x - kR)) / (2.0 * 1.5 * 1.5));
+    sum += g[x];
+  }
+  for (int x = 0; x < kW; x++) w.w[x] = g[x] / sum;
+  return w;
+}
+
+dim3 ssim_grid(int C, int H, int W) {
+  return dim3((unsigned)((W + kTX - 1) / kTX), (unsigned)((H + kTY - 1) / kTY), (unsigned)C);
+}
+
+size_t ssim_blocks(int C, int H, int W) {
+  const dim3 g = ssim_grid(C, H, W);
+  return (size_t)g.x * g.y * g.z;
+}
+
+}  // namespace
+
+extern "C" size_t gsr_photometric_scratch_bytes(int C, int H, int W) {
+  if (C <= 0 || H <= 0 || W <= 0) return 0;
+  Carver c(nullptr);
+  c.take<float>((size_t)C * H * W * 3);
+  c.take<float>(2 * ssim_blocks(C, H, W));
+  return c.size();
+}
+
+static void carve_photometric(void* scratch, int C, int H, int W, float** A, float** B, float** Cc,
+                              float** parts) {
+  Carver c((char*)scratch);
+  const size_t n = (size_t)C * H * W;
+  float* abc = c.take<float>(n * 3);
+  *A = abc;
+  *B = abc + n;
+  *Cc = abc + 2 * n;
+  *parts = c.take<float>(2 * ssim_blocks(C, H, W));
+}
+
+extern "C" int gsr_photometric_loss(int C, int H, int W, const float* image, const float* gt,
+                                    float lambda_dssim, int need_grad, float* out,
+                                    void* scratch, void* stream) {
+  if (C <= 0 || H <= 0 || W <= 0 || !image || !gt || !out || !scratch) return 1;
+  SsimArgs a{};
+  a.C = C; a.H = H; a.W = W;
+  a.x = image; a.y = gt;
+  float *A, *B, *Cc, *parts;
+  carve_photometric(scratch, C, H, W, &A, &B, &Cc, &parts);
+  a.A = need_grad ? A : nullptr;
+  a.B = need_grad ? B : nullptr;
+  a.Cc = need_grad ? Cc : nullptr;
+  a.parts = parts;
+  a.win = make_window();
+  a.c1 = (float)(0.01 * 0.01);
+  a.c2 = (float)(0.03 * 0.03);
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(ssim_fwd_kernel, ssim_grid(C, H, W), dim3(kThreads), 0, s, a);
+  const double inv = 1.0 / ((double)C * H * W);
+  hipLaunchKernelGGL(ssim_reduce_kernel, dim3(1), dim3(kThreads), 0, s, parts,
+                     (int)ssim_blocks(C, H, W), inv, lambda_dssim, out);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+extern "C" int gsr_photometric_loss_backward(int C, int H, int W, const float* image,
+                                             const float* gt, float lambda_dssim,
+                                             const float* grad_loss, const float* grad_l1,
+                                             const float* grad_ssim, float* grad_image,
+                                             void* scratch, void* stream) {
+  if (C <= 0 || H <= 0 || W <= 0 || !image || !gt || !grad_image || !scratch) return 1;
+  SsimBwdArgs a{};
+  a.C = C; a.H = H; a.W = W;
+  a.x = image; a.y = gt;
+  float *A, *B, *Cc, *parts;
+  carve_photometric(scratch, C, H, W, &A, &B, &Cc, &parts);
+  a.A = A; a.B = B; a.Cc = Cc;
+  a.g_loss = grad_loss; a.g_l1 = grad_l1; a.g_ssim = grad_ssim;
+  a.lambda = lambda_dssim;
+  a.inv_count = (float)(1.0 / ((double)C * H * W));
+  a.dx = grad_image;
+  a.win = make_window();
+  hipLaunchKernelGGL(ssim_bwd_kernel, ssim_grid(C, H, W), dim3(kThreads), 0, (hipStream_t)stream,
+                     a);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+static unsigned pearson_blocks(int64_t N) {
+  const int64_t b = (N + kThreads * 8 - 1) / (kThreads * 8);
+  return (unsigned)(b < 1 ? 1 : (b > 1024 ? 1024 : b));
+}
+
+extern "C" size_t gsr_pearson_scratch_bytes(int K, int variants) {
+  if (K <= 0 || variants < 1 || variants > 2) return 0;
+  Carver c(nullptr);
+  c.take<double>((size_t)variants * K * 8);
+  c.take<float>((size_t)variants * K);
+  c.take<int32_t>((size_t)K);
+  c.take<double>((size_t)variants * K * 1024 * 3);
+  return c.size();
+}
+
+static void carve_pearson(void* scratch, int K, int variants, double** acc, float** r,
+                          int32_t** sel, double** parts) {
+  Carver c((char*)scratch);
+  *acc = c.take<double>((size_t)variants * K * 8);
+  *r = c.take<float>((size_t)variants * K);
+  *sel = c.take<int32_t>((size_t)K);
+  *parts = c.take<double>((size_t)variants * K * 1024 * 3);
+}
+
+extern "C" int gsr_pearson_loss(int64_t N, int K, const float* x, const float* y, int variants,
+                                float offset, float* out_r, float* out_loss, void* scratch,
+                                void* stream) {
+  if (N < 2 || K < 1 || K > 256 || variants < 1 || variants > 2 || !x || !y || !scratch)
+    return 1;
+  hipStream_t s = (hipStream_t)stream;
+  PearsonArgs a{};
+  a.N = N; a.K = K; a.x = x; a.y = y; a.variants = variants; a.offset = offset;
+  a.nblocks = (int)pearson_blocks(N);
+  float* r;
+  int32_t* sel;
+  carve_pearson(scratch, K, variants, &a.acc, &r, &sel, &a.parts);
+  const dim3 grid((unsigned)a.nblocks, (unsigned)K, (unsigned)variants);
+  const dim3 rgrid((unsigned)K, (unsigned)variants);
+  hipLaunchKernelGGL(pearson_kernel<0>, grid, dim3(kThreads), 0, s, a);
+  hipLaunchKernelGGL(pearson_reduce_kernel<0>, rgrid, dim3(kThreads), 0, s, a);
+  hipLaunchKernelGGL(pearson_kernel<1>, grid, dim3(kThreads), 0, s, a);
+  hipLaunchKernelGGL(pearson_reduce_kernel<1>, rgrid, dim3(kThreads), 0, s, a);
+  hipLaunchKernelGGL(pearson_finish_kernel, dim3(1), dim3(256), 0, s, a, r, out_loss, sel);
+  if (out_r &&
+      hipMemcpyAsync(out_r, r, (size_t)variants * K * sizeof(float), hipMemcpyDeviceToDevice, s) !=
+          hipSuccess)
+    return 2;
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+extern "C" int gsr_pearson_loss_backward(int64_t N, int K, const float* x, const float* y,
+                                         int variants, float offset, const float* grad_loss,
+                                         float* grad_y, float* grad_x, void* scratch,
+                                         void* stream) {
+  if (N < 2 || K < 1 || K > 256 || variants < 1 || variants > 2 || !x || !y || !scratch ||
+      (grad_x && variants != 1))
+    return 1;
+  PearsonArgs a{};
+  a.N = N; a.K = K; a.x = x; a.y = y; a.variants = variants; a.offset = offset;
+  float* r;
+  int32_t* sel;
+  carve_pearson(scratch, K, variants, &a.acc, &r, &sel, &a.parts);
+  hipLaunchKernelGGL(pearson_bwd_kernel, dim3((unsigned)((N + kThreads - 1) / kThreads)),
+                     dim3(kThreads), 0, (hipStream_t)stream, a, sel, grad_loss, grad_y, grad_x);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}

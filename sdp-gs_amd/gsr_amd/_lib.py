@@ -124,6 +124,20 @@ def load():
         L.gsr_compact_rows.restype = _i
         L.gsr_compact_rows.argtypes = [_i, _pp, _pp, _pp, ctypes.POINTER(_i64),
                                        ctypes.POINTER(_u32), _i64, _p, _i64, _p]
+        # include/gsr_loss.h
+        L.gsr_photometric_scratch_bytes.restype = _sz
+        L.gsr_photometric_scratch_bytes.argtypes = [_i, _i, _i]
+        L.gsr_photometric_loss.restype = _i
+        L.gsr_photometric_loss.argtypes = [_i, _i, _i, _p, _p, _f, _i, _p, _p, _p]
+        L.gsr_photometric_loss_backward.restype = _i
+        L.gsr_photometric_loss_backward.argtypes = [_i, _i, _i, _p, _p, _f, _p, _p, _p, _p, _p,
+                                                    _p]
+        L.gsr_pearson_scratch_bytes.restype = _sz
+        L.gsr_pearson_scratch_bytes.argtypes = [_i, _i]
+        L.gsr_pearson_loss.restype = _i
+        L.gsr_pearson_loss.argtypes = [_i64, _i, _p, _p, _i, _f, _p, _p, _p, _p]
+        L.gsr_pearson_loss_backward.restype = _i
+        L.gsr_pearson_loss_backward.argtypes = [_i64, _i, _p, _p, _i, _f, _p, _p, _p, _p, _p]
         # include/gsr_knn.h
         L.gsr_knn_scratch_bytes.restype = _sz
         L.gsr_knn_scratch_bytes.argtypes = [_i64]

@@ -108,24 +108,27 @@ def compact_rows(arrays, n_old: int, index, n_out: int):
 
 def classify(self, grad_accum, denom, grad_threshold, scale_limit, min_opacity=float("-inf"),
              big_limit=None):
-    """gsr_densify_classify over self's raw _scaling / _opacity -> (flags u8 [P], [#clone, #split]
-    on the host).  denom None: grad_accum already holds the ratio."""
+    """gsr_densify_classify over self's raw _scaling / _opacity, then the clone and split index
+    lists -> (flags u8 [P], clone rows, split rows) (ascending int64; one host read for both
+    counts).  denom None: grad_accum already holds the ratio."""
     P = _rows(self._xyz)
     _cuda(grad_accum, denom, self._scaling, self._opacity)
     dev = self._xyz.device
     for t in (grad_accum, denom):
         assert t is None or (t.is_contiguous() and t.numel() == P and t.dtype == torch.float32)
     flags = torch.empty(P, dtype=torch.uint8, device=dev)
-    counts = torch.empty(2, dtype=torch.int32, device=dev)
     sc, op = self._scaling.detach(), self._opacity.detach()
     assert sc.is_contiguous() and op.is_contiguous() and sc.numel() == 3 * P and op.numel() == P
     with torch.cuda.device(dev):
         _check(_lib.load().gsr_densify_classify(
             P, _ptr(grad_accum), _ptr(denom), _ptr(sc), _ptr(op), float(grad_threshold),
             float(scale_limit), float(min_opacity), int(big_limit is not None),
-            float(big_limit if big_limit is not None else 0.0), _ptr(flags), _ptr(counts),
+            float(big_limit if big_limit is not None else 0.0), _ptr(flags), None,
             _stream(dev)), "gsr_densify_classify")
-    return flags, [int(x) for x in counts.tolist()]
+    ci, cc = select_rows(flags, CLONE, CLONE)
+    si, scount = select_rows(flags, SPLIT, SPLIT)
+    nc, ns = (int(x) for x in torch.cat((cc, scount)).tolist())
+    return flags, ci[:nc].long(), si[:ns].long()
 
 
 # ---- statistics (every step) ---------------------------------------------------------------------
@@ -284,21 +287,14 @@ def _cat_extras(a, b):
     return {k: torch.cat((a[k], b[k]), dim=0) for k in a}
 
 
-def _selected(flags, bit, n):
-    index, _ = select_rows(flags, bit, bit)
-    return index[:n].long()
-
-
 # ---- the reference's densification entry points ------------------------------------------------
 def densify_and_clone(self, grads, grad_threshold, scene_extent, include_feature):
     """scene/gaussian_model.py:566-589."""
     with torch.no_grad():
         g = grads.reshape(-1).contiguous()
-        flags, (nc, _) = classify(self, g, None, grad_threshold,
-                                  self.percent_dense * scene_extent)
-        idx = _selected(flags, CLONE, nc)
+        _, idx, _ = classify(self, g, None, grad_threshold, self.percent_dense * scene_extent)
         ext = _clone_rows(self, idx)
-        _rebuild(self, None, _rows(self._xyz) + nc, ext, fresh_stats=True)
+        _rebuild(self, None, _rows(self._xyz) + idx.numel(), ext, fresh_stats=True)
 
 
 def densify_and_split(self, grads, grad_threshold, scene_extent, iter, include_feature=False,
@@ -308,9 +304,8 @@ def densify_and_split(self, grads, grad_threshold, scene_extent, iter, include_f
         P = _rows(self._xyz)
         g = torch.zeros(P, device=self._xyz.device)
         g[:grads.shape[0]] = grads.squeeze()
-        flags, (_, ns) = classify(self, g, None, grad_threshold,
-                                  self.percent_dense * scene_extent)
-        idx = _selected(flags, SPLIT, ns)
+        flags, _, idx = classify(self, g, None, grad_threshold, self.percent_dense * scene_extent)
+        ns = idx.numel()
         ext = _split_rows(self, idx, N, generator)
         if _prune_active(self, iter):
             # append the children and drop the split parents in the same pass
@@ -337,11 +332,10 @@ def densify_and_prune(self, max_grad, min_opacity, extent, max_screen_size, iter
     with torch.no_grad():
         P = _rows(self._xyz)
         big_limit = 0.1 * extent if max_screen_size else None
-        flags, (nc, ns) = classify(self, self.xyz_gradient_accum.reshape(-1),
-                                   self.denom.reshape(-1), max_grad,
-                                   self.percent_dense * extent, min_opacity, big_limit)
-        cidx = _selected(flags, CLONE, nc)
-        sidx = _selected(flags, SPLIT, ns)
+        flags, cidx, sidx = classify(self, self.xyz_gradient_accum.reshape(-1),
+                                     self.denom.reshape(-1), max_grad,
+                                     self.percent_dense * extent, min_opacity, big_limit)
+        nc, ns = cidx.numel(), sidx.numel()
         ext = _cat_extras(_clone_rows(self, cidx), _split_rows(self, sidx, 2, generator))
         active = _prune_active(self, iteration)
         if iteration < 2000:
@@ -393,9 +387,8 @@ def proximity(self, scene_extent, include_feature, N=3):
         dist, nearest = distCUDA2(self._xyz)
         sel = torch.logical_and(dist > (5.0 * scene_extent),
                                 self.get_scaling.max(dim=1).values > scene_extent)
-        flags = sel.to(torch.uint8)
-        n_sel = int(flags.sum())
-        idx = _selected(flags, 1, n_sel)
+        index, count = select_rows(sel.to(torch.uint8), 1, 1)
+        idx = index[:int(count.item())].long()
         new_indices = nearest[idx].reshape(-1).long()
         source_xyz = self._xyz[idx].repeat(1, N, 1).reshape(-1, 3)
         new_xyz = (source_xyz + self._xyz[new_indices]) / 2

@@ -1,0 +1,159 @@
+"""Training losses on libgsr (include/gsr_loss.h).
+
+Mirrors the loss calls of train.py around the rasterizer:
+  photometric_loss(image, gt, lambda_dssim) -> (loss, Ll1)
+        = ((1 - lambda) * l1_loss(image, gt) + lambda * (1 - ssim(image, gt)), l1_loss(image, gt))
+        (train.py:99-100; utils/loss_utils.py:106-162) as ONE forward and ONE backward kernel
+  ssim(img1, img2, mask=None, window_size=11, size_average=True)     (loss_utils.py:129-162)
+  pearson_corrcoef(preds, target)                (torchmetrics.functional, train.py:22,126-149)
+  depth_pearson_loss(depth_mono, depth, offset=200.0)
+        = min(1 - pearson(depth_mono, depth), 1 - pearson(1 / (-depth_mono + offset), depth))
+        (train.py:126-129) without the host sync of Python's min() on tensors
+Gradients flow to the rendered image / depth (the first argument of ssim, either argument of
+pearson_corrcoef, `depth` of depth_pearson_loss).  No CPU path.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+
+def _stream(t):
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed with status {rc}")
+
+
+def _cuda(*ts):
+    for t in ts:
+        if not t.is_cuda:
+            raise RuntimeError("gsr losses run on HIP tensors only (no CPU path)")
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+class _Photometric(torch.autograd.Function):
+    """out[3] = (loss, l1 mean, ssim mean) of image vs gt, [C,H,W]."""
+
+    @staticmethod
+    def forward(ctx, image, gt, lambda_dssim):
+        _cuda(image, gt)
+        if image.shape != gt.shape or image.dim() != 3:
+            raise ValueError("photometric loss expects image and gt of the same [C,H,W] shape")
+        if gt.requires_grad:
+            raise ValueError("gradients flow to the rendered image only (gt must not require grad)")
+        x = image.detach().contiguous().float()
+        y = gt.detach().contiguous().float()
+        C, H, W = x.shape
+        L = _lib.load()
+        scratch = torch.empty(int(L.gsr_photometric_scratch_bytes(C, H, W)), dtype=torch.uint8,
+                              device=x.device)
+        out = torch.empty(3, dtype=torch.float32, device=x.device)
+        need = int(image.requires_grad)
+        with torch.cuda.device(x.device):
+            _check(L.gsr_photometric_loss(C, H, W, x.data_ptr(), y.data_ptr(),
+                                          float(lambda_dssim), need, out.data_ptr(),
+                                          scratch.data_ptr(), _stream(x)), "gsr_photometric_loss")
+        ctx.save_for_backward(x, y)
+        ctx.scratch = scratch
+        ctx.lam = float(lambda_dssim)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        x, y = ctx.saved_tensors
+        C, H, W = x.shape
+        g = g.contiguous()
+        dx = torch.empty_like(x)
+        with torch.cuda.device(x.device):
+            _check(_lib.load().gsr_photometric_loss_backward(
+                C, H, W, x.data_ptr(), y.data_ptr(), ctx.lam, g.data_ptr(), g.data_ptr() + 4,
+                g.data_ptr() + 8, dx.data_ptr(), ctx.scratch.data_ptr(), _stream(x)),
+                "gsr_photometric_loss_backward")
+        return dx, None, None
+
+
+def photometric_loss(image, gt, lambda_dssim=0.2):
+    """(loss, Ll1) of train.py:99-100 in one pass (lambda_dssim: arguments/__init__.py:87)."""
+    out = _Photometric.apply(image, gt, lambda_dssim)
+    return out[0], out[1]
+
+
+def ssim(img1, img2, mask=None, window_size=11, size_average=True):
+    """utils/loss_utils.py:129-162 (11x11 window only; gradient to img1)."""
+    if window_size != 11:
+        raise ValueError("gsr ssim implements the reference's window_size=11")
+    if mask is not None:
+        img1 = img1 * mask + (1 - mask)
+        img2 = img2 * mask + (1 - mask)
+    if img1.dim() == 3:
+        if not size_average:
+            raise ValueError("size_average=False needs batched [B,C,H,W] input (as the reference)")
+        return _Photometric.apply(img1, img2, 0.0)[2]
+    maps = [_Photometric.apply(a, b, 0.0)[2] for a, b in zip(img1, img2)]
+    per_image = torch.stack(maps)
+    return per_image.mean() if size_average else per_image
+
+
+class _Pearson(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, y, variants, offset):
+        _cuda(x, y)
+        if x.shape != y.shape or x.dim() not in (1, 2):
+            raise ValueError("pearson expects preds and target of the same [N] or [N, K] shape")
+        xs = x.detach().reshape(x.shape[0], -1).contiguous().float()
+        ys = y.detach().reshape(y.shape[0], -1).contiguous().float()
+        N, K = xs.shape
+        L = _lib.load()
+        scratch = torch.empty(int(L.gsr_pearson_scratch_bytes(K, variants)), dtype=torch.uint8,
+                              device=xs.device)
+        r = torch.empty(variants * K, dtype=torch.float32, device=xs.device)
+        loss = torch.empty(K, dtype=torch.float32, device=xs.device)
+        with torch.cuda.device(xs.device):
+            _check(L.gsr_pearson_loss(N, K, xs.data_ptr(), ys.data_ptr(), variants, float(offset),
+                                      r.data_ptr(), loss.data_ptr(), scratch.data_ptr(),
+                                      _stream(xs)), "gsr_pearson_loss")
+        ctx.save_for_backward(xs, ys)
+        ctx.scratch, ctx.variants, ctx.offset, ctx.shape = scratch, variants, offset, x.shape
+        return loss, r
+
+    @staticmethod
+    def backward(ctx, g_loss, g_r):
+        xs, ys = ctx.saved_tensors
+        N, K = xs.shape
+        need_x, need_y = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        # r-output grads are folded in as -g (loss = 1 - r) for the single-variant form
+        g = -g_r[:K] if ctx.variants == 1 else torch.zeros(K, device=xs.device)
+        if g_loss is not None:
+            g = g + g_loss
+        g = g.contiguous().float()
+        dx = torch.empty_like(xs) if need_x else None
+        dy = torch.empty_like(ys) if need_y else None
+        if need_x and ctx.variants != 1:
+            raise ValueError("depth_pearson_loss: gradients flow to the rendered depth only")
+        with torch.cuda.device(xs.device):
+            _check(_lib.load().gsr_pearson_loss_backward(
+                N, K, xs.data_ptr(), ys.data_ptr(), ctx.variants, float(ctx.offset), g.data_ptr(),
+                _ptr(dy), _ptr(dx), ctx.scratch.data_ptr(), _stream(xs)),
+                "gsr_pearson_loss_backward")
+        return (None if dx is None else dx.reshape(ctx.shape),
+                None if dy is None else dy.reshape(ctx.shape), None, None)
+
+
+def pearson_corrcoef(preds, target):
+    """torchmetrics.functional.pearson_corrcoef: r per column, squeezed ([N] -> scalar)."""
+    _, r = _Pearson.apply(preds, target, 1, 0.0)
+    return r.squeeze()
+
+
+def depth_pearson_loss(depth_mono, depth, offset=200.0):
+    """train.py:126-129: min(1 - r(mono, depth), 1 - r(1 / (-mono + offset), depth)); gradient to
+    depth (either [H,W]-like tensor, flattened to a column as the reference's reshape(-1, 1))."""
+    loss, _ = _Pearson.apply(depth_mono.reshape(-1, 1), depth.reshape(-1, 1), 2, offset)
+    return loss.squeeze()

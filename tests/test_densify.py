@@ -163,8 +163,19 @@ def test_classify_exact_on_thresholds():
     rows = [5, 77, 1234, 99_999]
     for k in rows:
         thr, lim, mo, big = g[k].item(), smax[k].item(), op[k].item(), smax[k + 1].item()
-        flags, (nc, ns) = densify.classify(m, m.xyz_gradient_accum.reshape(-1),
-                                           m.denom.reshape(-1), thr, lim, mo, big)
+        flags, cidx, sidx = densify.classify(m, m.xyz_gradient_accum.reshape(-1),
+                                             m.denom.reshape(-1), thr, lim, mo, big)
+        nc, ns = cidx.numel(), sidx.numel()
+        assert torch.equal(cidx, torch.nonzero(flags & densify.CLONE).flatten())
+        # the C-ABI's optional counters (one atomic per workgroup)
+        from gsr_amd import _lib
+        counts = torch.full((2,), 7, dtype=torch.int32, device="cuda")
+        flags2 = torch.empty_like(flags)
+        assert _lib.load().gsr_densify_classify(
+            P, m.xyz_gradient_accum.data_ptr(), m.denom.data_ptr(), m._scaling.data_ptr(),
+            m._opacity.data_ptr(), thr, lim, mo, 1, big, flags2.data_ptr(), counts.data_ptr(),
+            torch.cuda.current_stream().cuda_stream) == 0
+        assert torch.equal(flags, flags2) and counts.tolist() == [nc, ns]
         t32 = lambda x: torch.tensor(x, dtype=torch.float32, device="cuda")  # noqa: E731
         clone = (torch.norm(g[:, None], dim=-1) >= t32(thr)) & (smax <= t32(lim))
         split = (g >= t32(thr)) & (smax > t32(lim))
