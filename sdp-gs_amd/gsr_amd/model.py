@@ -94,6 +94,34 @@ class SplatModel:
         return build_covariance_from_scaling_rotation(self.get_scaling, scaling_modifier,
                                                       self._rotation)
 
+    @classmethod
+    def from_point_cloud(cls, points, colors, max_sh_degree=3, device="cuda"):
+        """create_from_pcd (scene/gaussian_model.py:189-214): SH DC from the colours (RGB2SH),
+        isotropic log-scales from the mean squared 3-NN distance (distCUDA2 = gsr_dist_knn3,
+        clamped at 1e-7), identity rotations, opacity logit(0.1), confidence 1; the language
+        feature starts at zero as training_setup creates it (:223-226)."""
+        from .knn import distCUDA2
+        pts =torch.tensor(points).float().to(device)
+        C0 = 0.28209479177387814  # utils/sh_utils.py RGB2SH
+        fused_color = (torch.tensor(colors).float().to(device) - 0.5) / C0
+        P = pts.shape[0]
+        features = torch.zeros((P, 3, (max_sh_degree + 1) ** 2), device=device)
+        features[:, :3, 0] = fused_color
+        dist2 = torch.clamp_min(distCUDA2(pts)[0], 0.0000001)
+        scales = torch.log(torch.sqrt(dist2))[..., None].repeat(1, 3)
+        rots = torch.zeros((P, 4), device=device)
+        rots[:, 0] = 1
+        x = 0.1 * torch.ones((P, 1), dtype=torch.float, device=device)
+        opacities = torch.log(x / (1 - x))  # inverse_sigmoid (utils/general_utils.py)
+        gp = GaussianParams(xyz=pts, features_dc=features[:, :, 0:1].transpose(1, 2).contiguous(),
+                            features_rest=features[:, :, 1:].transpose(1, 2).contiguous(),
+                            scaling=scales, rotation=rots, opacity=opacities,
+                            language_feature=torch.zeros((P, 3), device=device),
+                            confidence=torch.ones_like(opacities), max_sh_degree=max_sh_degree)
+        m = cls(gp, device=device, active_sh_degree=0)
+        m.max_radii2D = torch.zeros((P,), device=device)
+        return m
+
     def training_setup(self, training_args, spatial_lr_scale=1.0, prune_from_iter=500):
         """scene/gaussian_model.py:217-271: densification statistics, parameters as nn.Parameter,
         the named param groups (language group first when include_feature) and
@@ -136,3 +164,8 @@ class SplatModel:
 from . import densify as _densify  # noqa: E402
 
 _densify.install(SplatModel)
+
+# the reference's PLY methods (scene/gaussian_model.py:286-398)
+from . import ply as _ply  # noqa: E402
+
+_ply.install(SplatModel)
