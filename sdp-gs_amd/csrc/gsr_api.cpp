@@ -288,7 +288,12 @@ static int forward_impl(int P, int M, const float* background, const float* mean
   uint32_t* host = pinned_slot();
   hipEvent_t ready = readback_event();
   if (!host || !ready) return fail(GSR_ERR_HIP, "pinned host slot / event creation failed");
-  GSR_CHECK(hipMemcpyAsync(host, g.flags, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+  uint32_t* timeouts = sort_timeouts_word();
+  if (!timeouts) return fail(GSR_ERR_HIP, "sort timeout word unavailable");
+  GSR_CHECK(hipMemcpyAsync(host, g.flags, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+  // look-back timeouts of the sorts of EARLIER calls on this stream (the one-sweep sort's spin
+  // bound): reported here, one call late, instead of a sync after every sort
+  GSR_CHECK(hipMemcpyAsync(host + 3, timeouts, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
   GSR_CHECK(hipEventRecord(ready, stream));
 
   bool in_b = false;
@@ -302,6 +307,11 @@ static int forward_impl(int P, int M, const float* background, const float* mean
   PROF_END(SCAN);
 
   GSR_CHECK(hipEventSynchronize(ready));
+  if (host[3]) {
+    (void)hipMemsetAsync(timeouts, 0, sizeof(uint32_t), stream);
+    return fail(GSR_ERR_HIP, "a radix-sort look-back timed out in an earlier call on this device: "
+                "that call's outputs are invalid");
+  }
   const uint32_t R = host[1];
   if (host[0]) return fail(GSR_ERR_PREFILTERED,
                            "Point is filtered although prefiltered is set. This shouldn't happen!");

@@ -47,7 +47,13 @@ struct Carver {
 // ---- device-wide primitives (gsr_sort.hip) -----------------------------------------------------
 constexpr int kScanTile = 2048;       // elements per scan workgroup (256 threads x 8)
 constexpr int kScanMaxParts = 8192;   // partials scanned by the single-workgroup middle pass
-constexpr int kSortTile = 4096;       // keys per radix-sort workgroup (256 threads x 16)
+#ifndef GSR_SORT_KPT
+#define GSR_SORT_KPT 16
+#endif
+#ifndef GSR_SORT_TICKET
+#define GSR_SORT_TICKET 0  // one-sweep partitions by atomic ticket (1) or by blockIdx (0)
+#endif
+constexpr int kSortTile = 256 * GSR_SORT_KPT;  // keys per radix-sort workgroup (256 threads x KPT)
 
 inline size_t scan_parts(size_t n) { return (n + kScanTile - 1) / kScanTile; }
 inline size_t sort_blocks(size_t n) { return (n + kSortTile - 1) / kSortTile; }
@@ -83,6 +89,9 @@ hipError_t reduce_u32(const uint32_t* in, size_t n, uint32_t* parts, uint32_t* o
 // One-sweep passes: 1 memset + 1 digit-totals launch + 1 launch per 8-bit digit.
 hipError_t radix_sort_pairs(uint32_t* ka, uint32_t* va, uint32_t* kb, uint32_t* vb, size_t n,
                             int bits, SortScratch scratch, bool* result_in_b, hipStream_t s);
+// Device word counting look-back timeouts of any sort on the current device (sticky until the
+// host resets it); every forward reads it back with its instance count.
+uint32_t* sort_timeouts_word();
 
 // ---- layouts -------------------------------------------------------------------------------------
 struct GeomState {

@@ -145,10 +145,26 @@ __device__ __forceinline__ uint64_t match_digit(uint32_t d, bool valid, int bits
 // the error word (checked by the host at its next synchronisation) and proceeds, so no wave can
 // hang the device.
 constexpr uint64_t kStAgg = 1ull << 32, kStIncl = 2ull << 32, kStFlags = 3ull << 32;
+}  // namespace
+// count of timed-out look-backs since the last check (sort_timeouts_word)
+__device__ uint32_t g_lookback_timeouts;
+namespace {
 constexpr int kSpinLimit = 1 << 18;
 constexpr int kLookback = 16;
-constexpr int kKeysPerThread = kSortTile / kThreads;  // 16
-constexpr int kKeysPerWave = kKeysPerThread * 64;     // 1024
+constexpr int kKeysPerThread = kSortTile / kThreads;  // GSR_SORT_KPT (default 16)
+constexpr int kKeysPerWave = kKeysPerThread * 64;
+
+// Digit totals of every pass from the unsorted keys.  Its own tile (GSR_TOTALS_KPT keys per
+// thread) and a bounded grid striding over tiles: short per-workgroup chains for latency, and at
+// most GSR_TOTALS_GROUPS global atomics per counter at the end.
+#ifndef GSR_TOTALS_KPT
+#define GSR_TOTALS_KPT 16
+#endif
+#ifndef GSR_TOTALS_GROUPS
+#define GSR_TOTALS_GROUPS 1024
+#endif
+constexpr int kTotKPT = GSR_TOTALS_KPT;
+constexpr int kTotTile = kThreads * kTotKPT;
 
 __global__ __launch_bounds__(kThreads) void radix_totals_kernel(const uint32_t* __restrict__ keys,
                                                                 size_t n, int bits,
@@ -158,28 +174,30 @@ __global__ __launch_bounds__(kThreads) void radix_totals_kernel(const uint32_t* 
   for (int p = 0; p < kSortMaxPasses; p++) cnt[p][threadIdx.x] = 0;
   __syncthreads();
   const int passes = (bits + 7) / 8;
-  const size_t base = (size_t)blockIdx.x * kSortTile;
-  // all loads of the partition in flight before any is consumed
-  uint32_t key[kKeysPerThread];
+  for (size_t base = (size_t)blockIdx.x * kTotTile; base < n;
+       base += (size_t)gridDim.x * kTotTile) {
+    // all loads of the tile in flight before any is consumed
+    uint32_t key[kTotKPT];
 #pragma unroll
-  for (int r = 0; r < kKeysPerThread; r++) {
-    const size_t i = base + (size_t)r * kThreads + threadIdx.x;
-    key[r] = i < n ? keys[i] : 0u;
-  }
+    for (int r = 0; r < kTotKPT; r++) {
+      const size_t i = base + (size_t)r * kThreads + threadIdx.x;
+      key[r] = i < n ? keys[i] : 0u;
+    }
 #pragma unroll
-  for (int r = 0; r < kKeysPerThread; r++) {
-    const bool valid = base + (size_t)r * kThreads + threadIdx.x < n;
-    const uint64_t vmask = __ballot(valid);
-    if (vmask == 0ull) continue;
-    for (int p = 0; p < passes; p++) {
-      const uint32_t d = (key[r] >> (8 * p)) & 0xffu;
-      // typical depth keys share their top byte across a wave: one LDS add instead of 64
-      // serialised same-address atomics
-      const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
-      if (__ballot(valid && d != d0) == 0ull) {
-        if ((threadIdx.x & 63) == 0) atomicAdd(&cnt[p][d0], (uint32_t)__popcll(vmask));
-      } else if (valid) {
-        atomicAdd(&cnt[p][d], 1u);
+    for (int r = 0; r < kTotKPT; r++) {
+      const bool valid = base + (size_t)r * kThreads + threadIdx.x < n;
+      const uint64_t vmask = __ballot(valid);
+      if (vmask == 0ull) continue;
+      for (int p = 0; p < passes; p++) {
+        const uint32_t d = (key[r] >> (8 * p)) & 0xffu;
+        // typical depth keys share their top byte across a wave: one LDS add instead of 64
+        // serialised same-address atomics
+        const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
+        if (__ballot(valid && d != d0) == 0ull) {
+          if ((threadIdx.x & 63) == 0) atomicAdd(&cnt[p][d0], (uint32_t)__popcll(vmask));
+        } else if (valid) {
+          atomicAdd(&cnt[p][d], 1u);
+        }
       }
     }
   }
@@ -213,7 +231,13 @@ __global__ __launch_bounds__(kThreads) void radix_onesweep_kernel(
   // ticket, not blockIdx: a partition can only wait on partitions whose workgroups already run
   // (a per-XCD ticket variant timed out its look-back on gfx950 -- dispatch order across XCDs
   // gives no such guarantee)
+#if GSR_SORT_TICKET
   if (t == 0) s_part = atomicAdd(ticket, 1u);
+#else
+  // blockIdx order: every XCD dispatches its workgroups in index order, so the lowest unfinished
+  // partition is always resident and the look-back always progresses (bounded spin as backstop)
+  if (t == 0) s_part = blockIdx.x;
+#endif
 #pragma unroll
   for (int w = 0; w < kThreads / 64; w++) s_cnt[w][t] = 0;
   __syncthreads();
@@ -280,7 +304,11 @@ __global__ __launch_bounds__(kThreads) void radix_onesweep_kernel(
       if (done) break;
       q -= used;
       if (used < kLookback) {
-        if (++spins > kSpinLimit) { atomicOr(err, 1u); break; }
+        if (++spins > kSpinLimit) {
+          atomicOr(err, 1u);
+          atomicAdd(&g_lookback_timeouts, 1u);  // sticky, read back by every forward
+          break;
+        }
         __builtin_amdgcn_s_sleep(1);
       }
     }
@@ -352,6 +380,12 @@ hipError_t scan_u32(const uint32_t* in, const uint32_t* gather, uint32_t* out, s
   return hipGetLastError();
 }
 
+uint32_t* sort_timeouts_word() {
+  void* p = nullptr;
+  if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_lookback_timeouts)) != hipSuccess) return nullptr;
+  return (uint32_t*)p;
+}
+
 hipError_t radix_sort_pairs(uint32_t* ka, uint32_t* va, uint32_t* kb, uint32_t* vb, size_t n,
                             int bits, SortScratch scratch, bool* result_in_b, hipStream_t s) {
   *result_in_b = false;
@@ -363,8 +397,10 @@ hipError_t radix_sort_pairs(uint32_t* ka, uint32_t* va, uint32_t* kb, uint32_t* 
   const size_t clear = (size_t)((char*)(scratch.status + (size_t)passes * nb * 256) - (char*)scratch.aux);
   hipError_t e = hipMemsetAsync(scratch.aux, 0, clear, s);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(radix_totals_kernel, dim3(nb), dim3(kThreads), 0, s, ka, n, bits,
-                     scratch.aux + kSortAuxTotals);
+  const size_t tot_tiles = (n + kTotTile - 1) / kTotTile;
+  hipLaunchKernelGGL(radix_totals_kernel,
+                     dim3((unsigned)(tot_tiles < GSR_TOTALS_GROUPS ? tot_tiles : GSR_TOTALS_GROUPS)),
+                     dim3(kThreads), 0, s, ka, n, bits, scratch.aux + kSortAuxTotals);
   uint32_t *kin = ka, *vin = va, *kout = kb, *vout = vb;
   bool in_b = false;
   for (int p = 0; p < passes; p++) {
