@@ -80,6 +80,10 @@ __global__ __launch_bounds__(kSchedThreads) void tile_schedule_kernel(const uint
 #ifndef GSR_QUAD_WAVES
 #define GSR_QUAD_WAVES 1
 #endif
+// backward transmittance recovery T / (1 - alpha): 0 = IEEE division, 1 = rcp + Newton step
+#ifndef GSR_BWD_FAST_DIV
+#define GSR_BWD_FAST_DIV 1
+#endif
 __device__ __forceinline__ void pixel_of(uint32_t tx, uint32_t ty, uint32_t t, uint32_t& px,
                                          uint32_t& py) {
   const uint32_t w = t >> 6, l = t & 63u;
@@ -500,7 +504,20 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
       const float dx = r0.x - pfx, dy = r0.y - pfy;
 
       float g[kAccFloats];
+#if GSR_BWD_FAST_DIV
+      {
+        // T / (1 - alpha) by v_rcp_f32 + one Newton correction on the exact residual (4 VALU
+        // instead of the 10 of the scaled IEEE sequence): operands lie in [1e-4, 1] / [0.01, 1],
+        // so the result is the correctly rounded quotient up to rare last-ulp ties; alpha = 0
+        // (non-contributing lanes) gives T exactly
+        const float d = 1.f - alpha;
+        const float r = __builtin_amdgcn_rcpf(d);
+        const float q = T * r;
+        T = __builtin_fmaf(__builtin_fmaf(-q, d, T), r, q);
+      }
+#else
       T = T / (1.f - alpha);
+#endif
       const float dchannel_dcolor = alpha * T;
       float col[NC];
       col[0] = r1.w; col[1] = r2.x; col[2] = r2.y;

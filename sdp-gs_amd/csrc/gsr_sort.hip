@@ -150,7 +150,10 @@ constexpr uint64_t kStAgg = 1ull << 32, kStIncl = 2ull << 32, kStFlags = 3ull <<
 __device__ uint32_t g_lookback_timeouts;
 namespace {
 constexpr int kSpinLimit = 1 << 18;
-constexpr int kLookback = 16;
+#ifndef GSR_LOOKBACK
+#define GSR_LOOKBACK 16
+#endif
+constexpr int kLookback = GSR_LOOKBACK;  // predecessor status words loaded per look-back step
 constexpr int kKeysPerThread = kSortTile / kThreads;  // GSR_SORT_KPT (default 16)
 constexpr int kKeysPerWave = kKeysPerThread * 64;
 

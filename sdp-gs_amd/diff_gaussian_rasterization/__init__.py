@@ -351,8 +351,16 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
         dfeat = g(grad_feature) if mt["include_feature"] else None
         s_dc, s_rest, s_op, s_sc, s_rot = mt["shapes"]
         fopts = dict(dtype=torch.float32, device=dev)
-        accumulate = ctx.leaves is not None
-        if accumulate:
+        into_leaves = ctx.leaves is not None
+        accumulate = into_leaves
+        if into_leaves and all(t is None or t.grad is None for t in ctx.leaves):
+            # first view after zero_grad(set_to_none=True): the kernel's store mode writes every
+            # element of fresh .grad tensors (zeros for culled Gaussians) -- no memset, no read
+            accumulate = False
+            for t in ctx.leaves:
+                if t is not None:
+                    t.grad = torch.empty_like(t, memory_format=torch.contiguous_format)
+        if into_leaves:
             # add straight into the parameters' .grad (created as zeros when absent, as
             # AccumulateGrad would); culled Gaussians are not touched at all
             grads = []
@@ -363,7 +371,7 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
             if any(gr is not None and not gr.is_contiguous() for gr in grads):
                 raise RuntimeError("grad-into-leaves needs contiguous .grad tensors")
             d_means3D, d_dc, d_rest, d_op, d_sc, d_rot, d_lf = grads
-            d_means2D = torch.zeros((P, 3), **fopts)
+            d_means2D = (torch.zeros if accumulate else torch.empty)((P, 3), **fopts)
         else:
             d_means2D = torch.empty((P, 3), **fopts)
             d_means3D = torch.empty((P, 3), **fopts)
@@ -389,7 +397,7 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
         _lib.check(rc)
         # forward inputs: means3D, means2D, features_dc, features_rest, opacity_raw, scaling_raw,
         # rotation_raw, language_feature, raster_settings
-        if accumulate:
+        if into_leaves:
             return None, d_means2D, None, None, None, None, None, None, None
         return d_means3D, d_means2D, d_dc, d_rest, d_op, d_sc, d_rot, d_lf, None
 
