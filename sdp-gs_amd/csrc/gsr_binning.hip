@@ -40,23 +40,21 @@ __global__ __launch_bounds__(kThreads) void duplicate_kernel(int P,
   // Gaussian's 64-byte record line
   const float4 r0 = rec[4 * (size_t)gid];
   const float4 r1 = rec[4 * (size_t)gid + 1];
-  const int r = (int)rec[4 * (size_t)gid + 3].y;
-  const float qc = splat_q_cut(r0.z, r0.w, r1.x, r1.y);
+  const float4 r3 = rec[4 * (size_t)gid + 3];  // {f2, radius, q_cut, -}
+  const int r = (int)r3.y;
   uint32_t x0, y0, x1, y1;
   tile_rect(r0.x, r0.y, r, gx, gy, x0, y0, x1, y1);
-  // the same conservative tile test as the preprocess count (gsr_device.h), so exactly
-  // tiles_touched ids are written
-  for (uint32_t y = y0; y < y1 && off < end; y++)
-    for (uint32_t x = x0; x < x1 && off < end; x++) {
-      if (qc >= 0.0f &&
-          !splat_touches_rect(r0.x, r0.y, r0.z, r0.w, r1.x, qc, (float)(x * kTile),
-                              (float)(x * kTile + kTile - 1), (float)(y * kTile),
-                              (float)(y * kTile + kTile - 1)))
-        continue;
+  // exactly the per-row tile ranges the preprocess counted (cut_row_range, gsr_device.h)
+  const SplatCut cut = make_cut(r0.x, r0.y, r0.z, r0.w, r1.x, r3.z);
+  for (uint32_t y = y0; y < y1 && off < end; y++) {
+    uint32_t a, b;
+    cut_row_range(cut, y, x0, x1, a, b);
+    for (uint32_t x = a; x < b && off < end; x++) {
       tkey[off] = y * gx + x;
       tval[off] = gid;
       off++;
     }
+  }
 }
 
 __global__ __launch_bounds__(kThreads) void tile_ranges_kernel(size_t R,

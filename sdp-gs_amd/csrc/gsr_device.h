@@ -135,15 +135,31 @@ __device__ __forceinline__ float splat_q_cut(float ca, float cb, float cc, float
   return (float)(2.0 * log(255.0 * (double)op));
 }
 
+// Per-splat constants of the rectangle test: centre, conic, q_cut and the two ratios -cb/cc,
+// -cb/ca of the edge minimisers (computed once per splat, not per rectangle edge).
+struct SplatCut {
+  float mx, my, ca, cb, cc, qc, kx, ky;  // kx = -cb / cc (dy* per dx), ky = -cb / ca (dx* per dy)
+};
+__device__ __forceinline__ SplatCut make_cut(float mx, float my, float ca, float cb, float cc,
+                                             float qc) {
+  SplatCut s{mx, my, ca, cb, cc, qc, 0.0f, 0.0f};
+  if (qc >= 0.0f) {  // positive definite: ca, cc > 0
+    s.kx = -cb / cc;
+    s.ky = -cb / ca;
+  }
+  return s;
+}
+
 // True unless q > q_cut (plus a safety margin) on the whole rectangle of pixel centres
 // [x0, x1] x [y0, y1].  The minimum of the positive-definite form over a rectangle is 0 when the
-// centre is inside, else it lies on an edge; each edge is a clamped 1-D quadratic minimisation.
-__device__ __forceinline__ bool splat_touches_rect(float mx, float my, float ca, float cb, float cc,
-                                                   float q_cut, float x0, float x1, float y0,
-                                                   float y1) {
-  if (q_cut == -2.0f) return false;
-  if (q_cut < 0.0f) return true;
-  const float dx0 = x0 - mx, dx1 = x1 - mx, dy0 = y0 - my, dy1 = y1 - my;
+// centre is inside, else it lies on an edge; each edge is a clamped 1-D quadratic minimisation
+// (the minimiser's float rounding only moves the evaluated point along the edge, raising q by a
+// second-order amount far inside the margin).
+__device__ __forceinline__ bool cut_touches_rect(const SplatCut& s, float x0, float x1, float y0,
+                                                 float y1) {
+  if (s.qc == -2.0f) return false;
+  if (s.qc < 0.0f) return true;
+  const float dx0 = x0 - s.mx, dx1 = x1 - s.mx, dy0 = y0 - s.my, dy1 = y1 - s.my;
   if (dx0 <= 0.0f && dx1 >= 0.0f && dy0 <= 0.0f && dy1 >= 0.0f) return true;
   float qmin = 3.0e38f, tabs = 0.0f;
 #pragma unroll
@@ -151,18 +167,41 @@ __device__ __forceinline__ bool splat_touches_rect(float mx, float my, float ca,
     float dx, dy;
     if (e < 2) {
       dx = (e == 0) ? dx0 : dx1;
-      dy = fminf(fmaxf(-cb * dx / cc, dy0), dy1);
+      dy = fminf(fmaxf(s.kx * dx, dy0), dy1);
     } else {
       dy = (e == 2) ? dy0 : dy1;
-      dx = fminf(fmaxf(-cb * dy / ca, dx0), dx1);
+      dx = fminf(fmaxf(s.ky * dy, dx0), dx1);
     }
-    const float t1 = ca * dx * dx, t2 = cc * dy * dy, t3 = 2.0f * cb * dx * dy;
+    const float t1 = s.ca * dx * dx, t2 = s.cc * dy * dy, t3 = 2.0f * s.cb * dx * dy;
     const float q = t1 + t2 + t3;
     if (q < qmin) { qmin = q; tabs = t1 + t2 + fabsf(t3); }
   }
   // margin >> the float error of the blend's own evaluation: dx = mx - px carries up to
   // ulp(2048) = 2.4e-4 px, i.e. |dq| <= 2 sqrt(ca q) * 2.4e-4 < 3e-3 for q <= 11, ca <= 1/0.3
-  return qmin <= q_cut + 2e-2f + 1e-4f * tabs;
+  return qmin <= s.qc + 2e-2f + 1e-4f * tabs;
+}
+
+// Tiles of tile row ty, among [x0, x1), kept by the binning: the contiguous range [a, b) from the
+// first to the last tile passing cut_touches_rect.  In exact arithmetic the passing tiles of a
+// row ARE contiguous (they meet the projection of the convex region q <= cut onto the row band),
+// so the range only adds tiles that rounding could have split off -- a conservative superset.
+// The preprocess counts and the duplication emits exactly these ranges.
+__device__ __forceinline__ void cut_row_range(const SplatCut& s, uint32_t ty, uint32_t x0,
+                                              uint32_t x1, uint32_t& a, uint32_t& b) {
+  if (s.qc < 0.0f) {
+    a = x0;
+    b = s.qc == -2.0f ? x0 : x1;
+    return;
+  }
+  const float y0 = (float)(ty * kTile), y1 = (float)(ty * kTile + kTile - 1);
+  a = x0;
+  while (a < x1 && !cut_touches_rect(s, (float)(a * kTile), (float)(a * kTile + kTile - 1), y0, y1))
+    a++;
+  b = x1;
+  while (b > a + 1 &&
+         !cut_touches_rect(s, (float)((b - 1) * kTile), (float)((b - 1) * kTile + kTile - 1), y0, y1))
+    b--;
+  if (a == x1) b = x1;
 }
 
 // auxiliary.h:58-77 (the 4x4 matrices are row-major tensors read as column-major)

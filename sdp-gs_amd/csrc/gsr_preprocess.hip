@@ -9,7 +9,8 @@
 //   rec[4g+0] = {x_px, y_px, conic.a, conic.b}
 //   rec[4g+1] = {conic.c, opacity*confidence, depth, r}
 //   rec[4g+2] = {g, b, f0, f1}
-//   rec[4g+3] = {f2, radius, 0, 0}   (radius as float: exact, read by the duplication)
+//   rec[4g+3] = {f2, radius, q_cut, 0}   (radius as float: exact; q_cut: the culling threshold of
+//                                        gsr_device.h, computed once here for the binning and blends)
 // so the blend reads one contiguous record per instance instead of five scattered arrays.
 #include "gsr_device.h"
 #include "gsr_internal.h"
@@ -148,11 +149,13 @@ __global__ __launch_bounds__(kThreads) void preprocess_kernel(PreArgs a) {
   if (qc == -1.0f) {
     count = (y1 - y0) * (x1 - x0);
   } else if (qc >= 0.0f) {
-    for (uint32_t ty = y0; ty < y1; ty++)
-      for (uint32_t tx = x0; tx < x1; tx++)
-        count += splat_touches_rect(px, py, con_a, con_b, con_c, qc, (float)(tx * kTile),
-                                    (float)(tx * kTile + kTile - 1), (float)(ty * kTile),
-                                    (float)(ty * kTile + kTile - 1));
+    // per tile row, the kept tiles form one range (cut_row_range): found from both ends
+    const SplatCut cut = make_cut(px, py, con_a, con_b, con_c, qc);
+    for (uint32_t ty = y0; ty < y1; ty++) {
+      uint32_t ra, rb;
+      cut_row_range(cut, ty, x0, x1, ra, rb);
+      count += rb - ra;
+    }
   }
   g.tiles_touched[idx] = count;
   g.dkey_a[idx] = __float_as_uint(depth);
@@ -160,7 +163,7 @@ __global__ __launch_bounds__(kThreads) void preprocess_kernel(PreArgs a) {
   rec[0] = make_float4(px, py, con_a, con_b);
   rec[1] = make_float4(con_c, op, depth, cr);
   rec[2] = make_float4(cg, cb, f0, f1);
-  rec[3] = make_float4(f2, (float)r, 0.f, 0.f);
+  rec[3] = make_float4(f2, (float)r, qc, 0.f);
 }
 
 __global__ __launch_bounds__(kThreads) void mark_visible_kernel(int P, const float* __restrict__ m,

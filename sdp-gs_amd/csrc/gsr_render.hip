@@ -98,10 +98,12 @@ __device__ __forceinline__ void pixel_of(uint32_t tx, uint32_t ty, uint32_t t, u
 
 // Which of the 4 waves a splat can reach: bit w set unless the conservative test of
 // gsr_device.h proves alpha < 1/255 on all 64 pixels of wave w.
-__device__ __forceinline__ uint32_t wave_mask(float4 r0, float4 r1, uint32_t tx, uint32_t ty) {
-  const float qc = splat_q_cut(r0.z, r0.w, r1.x, r1.y);
+__device__ __forceinline__ uint32_t wave_mask(float4 r0, float4 r1, float qc, uint32_t tx,
+                                              uint32_t ty) {
+  // qc: the record's q_cut (rec[3].z, computed once by the preprocess)
   if (qc == -1.0f) return 0xfu;
   if (qc == -2.0f) return 0u;
+  const SplatCut cut = make_cut(r0.x, r0.y, r0.z, r0.w, r1.x, qc);
   uint32_t m = 0;
 #pragma unroll
   for (int w = 0; w < 4; w++) {
@@ -113,7 +115,7 @@ __device__ __forceinline__ uint32_t wave_mask(float4 r0, float4 r1, uint32_t tx,
       x0 = (float)(tx * kTile); x1 = (float)(tx * kTile + kTile - 1);
       y0 = (float)(ty * kTile + 4 * w); y1 = y0 + 3.0f;
     }
-    m |= splat_touches_rect(r0.x, r0.y, r0.z, r0.w, r1.x, qc, x0, x1, y0, y1) ? (1u << w) : 0u;
+    m |= cut_touches_rect(cut, x0, x1, y0, y1) ? (1u << w) : 0u;
   }
   return m;
 }
@@ -172,12 +174,12 @@ __global__ __launch_bounds__(kThreads) void render_fwd_kernel(RenderArgs a) {
     if (i < range.y) {
       const uint32_t gid = a.point_list[i];
       const float4* rec = a.rec + 4 * (size_t)gid;
-      const float4 q0 = rec[0], q1 = rec[1];
+      const float4 q0 = rec[0], q1 = rec[1], q3 = rec[3];
       s_r0[threadIdx.x] = q0;
       s_r1[threadIdx.x] = q1;
       s_r2[threadIdx.x] = rec[2];
-      if (FEAT) s_f2[threadIdx.x] = rec[3].x;
-      s_mask[threadIdx.x] = (uint8_t)wave_mask(q0, q1, tx, ty);
+      if (FEAT) s_f2[threadIdx.x] = q3.x;
+      s_mask[threadIdx.x] = (uint8_t)wave_mask(q0, q1, q3.z, tx, ty);
     }
     __syncthreads();
     const uint32_t cnt = min((uint32_t)kThreads, range.y - base);
@@ -451,12 +453,12 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
       const uint32_t gid = a.point_list[range.x + rel];
       s_gid[threadIdx.x] = gid;
       const float4* rec = a.rec + 4 * (size_t)gid;
-      const float4 q0 = rec[0], q1 = rec[1];
+      const float4 q0 = rec[0], q1 = rec[1], q3 = rec[3];
       s_r0[threadIdx.x] = q0;
       s_r1[threadIdx.x] = q1;
-      s_mask[threadIdx.x] = (uint8_t)wave_mask(q0, q1, tx, ty);
+      s_mask[threadIdx.x] = (uint8_t)wave_mask(q0, q1, q3.z, tx, ty);
       s_r2[threadIdx.x] = rec[2];
-      if (FEAT) s_f2[threadIdx.x] = rec[3].x;
+      if (FEAT) s_f2[threadIdx.x] = q3.x;
     }
     __syncthreads();
     const uint32_t nlist = build_wave_list(s_mask, s_list[wid], cnt, wid, lane);
