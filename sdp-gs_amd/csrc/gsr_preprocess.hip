@@ -19,6 +19,9 @@ namespace gsr {
 namespace {
 
 constexpr int kThreads = 256;
+#ifndef GSR_PRE_HOIST
+#define GSR_PRE_HOIST 0
+#endif
 
 // forward.cu:20-71 (float32, same evaluation order as the CPU restatement)
 // s0: coefficient 0 of this Gaussian, s1: its coefficients 1.. (contiguous); for the reference's
@@ -61,6 +64,18 @@ __global__ __launch_bounds__(kThreads) void preprocess_kernel(PreArgs a) {
   // slower here: its 48 KB of LDS cut occupancy below what this latency-bound kernel needs)
   const int idx = (int)(blockIdx.x * kThreads + threadIdx.x);
   if (idx >= a.P) return;
+#if GSR_PRE_HOIST
+  // the small per-Gaussian inputs are all put in flight before the first dependent computation
+  // (the compiler cannot hoist loads above the cull branches itself)
+  float4 q_in = make_float4(0.f, 0.f, 0.f, 0.f);
+  float s_in0 = 0.f, s_in1 = 0.f, s_in2 = 0.f;
+  if (!a.cov3D_precomp) {  // kernel-argument (uniform) test
+    q_in = reinterpret_cast<const float4*>(a.rotations)[idx];
+    s_in0 = a.scales[3 * idx]; s_in1 = a.scales[3 * idx + 1]; s_in2 = a.scales[3 * idx + 2];
+  }
+  const float op_in = a.opacities[idx];
+  const float conf_in = a.confidence ? a.confidence[idx] : 1.0f;
+#endif
   const V3 p_orig = v3(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
   const V3 p_view = xform_point43(p_orig, a.view);
   // in_frustum: near-plane test only (auxiliary.h:154)
@@ -84,8 +99,13 @@ __global__ __launch_bounds__(kThreads) void preprocess_kernel(PreArgs a) {
 #pragma unroll
     for (int k = 0; k < 6; k++) c3buf[k] = a.cov3D_precomp[6 * (size_t)idx + k];
   } else {
+#if GSR_PRE_HOIST
+    float4 q = q_in;
+    float sx = s_in0, sy = s_in1, sz = s_in2;
+#else
     float4 q = reinterpret_cast<const float4*>(a.rotations)[idx];
     float sx = a.scales[3 * idx], sy = a.scales[3 * idx + 1], sz = a.scales[3 * idx + 2];
+#endif
     if (a.fused) {  // GaussianModel activations: exp(_scaling), normalize(_rotation)
       sx = expf(sx); sy = expf(sy); sz = expf(sz);
       q = normalize_quat(q);
@@ -124,9 +144,15 @@ __global__ __launch_bounds__(kThreads) void preprocess_kernel(PreArgs a) {
     cg = a.colors_precomp[3 * idx + 1];
     cb = a.colors_precomp[3 * idx + 2];
   }
+#if GSR_PRE_HOIST
+  float op = op_in;
+  if (a.fused) op = sigmoid_f(op);  // GaussianModel.get_opacity
+  if (a.confidence) op = op * conf_in;
+#else
   float op = a.opacities[idx];
   if (a.fused) op = sigmoid_f(op);  // GaussianModel.get_opacity
   if (a.confidence) op = op * a.confidence[idx];
+#endif
   float f0 = 0.f, f1 = 0.f, f2 = 0.f;
   if (a.include_feature) {
     if (a.lang_precomp) {
