@@ -84,6 +84,11 @@ __global__ __launch_bounds__(kSchedThreads) void tile_schedule_kernel(const uint
 #ifndef GSR_BWD_FAST_DIV
 #define GSR_BWD_FAST_DIV 1
 #endif
+// backward per-splat gradient sum: waves with at most this many contributing lanes add lane
+// values into LDS directly instead of the wave butterfly (0 = always the butterfly)
+#ifndef GSR_BWD_SPARSE_K
+#define GSR_BWD_SPARSE_K 0
+#endif
 __device__ __forceinline__ void pixel_of(uint32_t tx, uint32_t ty, uint32_t t, uint32_t& px,
                                          uint32_t& py) {
   const uint32_t w = t >> 6, l = t & 63u;
@@ -492,7 +497,8 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
 #pragma unroll
     for (int u = 0; u < GROUP; u++) {
       const bool contrib = cv[u];
-      if (__ballot(contrib) == 0ull) continue;  // wave-uniform skip
+      const uint64_t cmask = __ballot(contrib);
+      if (cmask == 0ull) continue;  // wave-uniform skip
       const uint32_t j = (packed >> (8 * u)) & 0xffu;
       // Branch-free: a lane whose pixel does not take this splat runs the same arithmetic with
       // G = alpha = 0, which makes every gradient term exactly zero and T / (1 - 0) == T; its
@@ -559,6 +565,17 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
       g[kAccUsed] = 0.0f;
       g[14] = 0.0f;
       g[15] = 0.0f;
+#if GSR_BWD_SPARSE_K > 0
+      if (__popcll(cmask) <= GSR_BWD_SPARSE_K) {
+        // few contributing lanes: they add their values into the LDS row directly (LDS atomic
+        // pipe) instead of the ~45-instruction VALU butterfly of the whole wave
+        if (contrib) {
+#pragma unroll
+          for (int k = 0; k < kAccUsed; k++) atomicAdd(&s_acc[j][k], g[k]);
+        }
+        continue;
+      }
+#endif
       const float sum = wave_reduce16_dpp(g, lane);
       if ((lane & 3) == 0) {
         const int k = reduce16_slot(lane, swap_orient);
