@@ -89,6 +89,10 @@ __global__ __launch_bounds__(kSchedThreads) void tile_schedule_kernel(const uint
 #ifndef GSR_BWD_SPARSE_K
 #define GSR_BWD_SPARSE_K 0
 #endif
+// forward: 1 = blend weight alpha * T formed once per pair, 0 = col * alpha * T per channel
+#ifndef GSR_FWD_WEIGHT
+#define GSR_FWD_WEIGHT 1
+#endif
 __device__ __forceinline__ void pixel_of(uint32_t tx, uint32_t ty, uint32_t t, uint32_t& px,
                                          uint32_t& py) {
   const uint32_t w = t >> 6, l = t & 63u;
@@ -224,6 +228,21 @@ __global__ __launch_bounds__(kThreads) void render_fwd_kernel(RenderArgs a) {
           done = true;
           continue;
         }
+#if GSR_FWD_WEIGHT
+        // blend weight alpha * T formed once (the reference forms col * alpha * T per channel,
+        // forward.cu:341-343: same value up to the rounding of one product)
+        const float wgt = alpha * T;
+        C[0] += r1v[u].w * wgt;
+        C[1] += r2v[u].x * wgt;
+        C[2] += r2v[u].y * wgt;
+        C[3] += r1v[u].z * wgt;
+        C[4] += wgt;
+        if (FEAT) {
+          C[5 % NC] += r2v[u].z * wgt;
+          C[6 % NC] += r2v[u].w * wgt;
+          C[7 % NC] += f2v[u] * wgt;
+        }
+#else
         C[0] += r1v[u].w * alpha * T;
         C[1] += r2v[u].x * alpha * T;
         C[2] += r2v[u].y * alpha * T;
@@ -234,6 +253,7 @@ __global__ __launch_bounds__(kThreads) void render_fwd_kernel(RenderArgs a) {
           C[6 % NC] += r2v[u].w * alpha * T;
           C[7 % NC] += f2v[u] * alpha * T;
         }
+#endif
         T = test_T;
         // the reference counts every list position (forward.cu:328); skipped entries cannot blend
         last_contributor = rel0 + jj[u] + 1;
