@@ -128,7 +128,8 @@ int gsr_rasterize_gaussians_fused(
  * accumulate = 0: every element written (zeros for culled Gaussians), as the plain backward.
  * accumulate = 1: visible Gaussians' grads are ADDED into the buffers and culled ones are left
  *   untouched, so the buffers may be the leaves' .grad tensors across views of one step.
- * dL_dmeans2D[P,3] is the screen-space gradient (the reference's means2D.grad). */
+ * dL_dmeans2D[P,3] is the screen-space gradient (the reference's means2D.grad): a per-call
+ * output, always stored (zeros for culled Gaussians), also when accumulate = 1. */
 int gsr_rasterize_gaussians_fused_backward(
     int P, int M, int R,
     const float* background, const float* means3D, const int* radii,

@@ -164,7 +164,7 @@ __device__ __forceinline__ void gaussian_bwd(const BwdPreArgs& a, size_t i, floa
   // slots: q0 = {mx, my, ca, cb}, q1 = {cc, op, r, g}, q2 = {b, depth, f0, f1}, q3 = {f2, used, -, -}
   const float gmx = q0.x, gmy = q0.y;
   const float dcx = q0.z, dcy = q0.w, dcz = q1.x;
-  st3<ACC>(a.dL_dmeans2D, i, v3(gmx, gmy, 0.0f));
+  put3(a.dL_dmeans2D, i, v3(gmx, gmy, 0.0f));  // per-call output, stored in both modes
   const V3 dL_dcolor = v3(q1.z, q1.w, q2.x);
   if (a.dL_dcolors) st3<ACC>(a.dL_dcolors, i, dL_dcolor);
   {
@@ -403,6 +403,7 @@ __global__ __launch_bounds__(kThreads) void preprocess_bwd_kernel(BwdPreArgs a) 
     }
   } else {
     if (!ACC && t < n) zero_outputs(a, i);
+    if (ACC && t < n) put3(a.dL_dmeans2D, i, v3(0, 0, 0));  // stored output: zeros when culled
     if (has_sh && t < n) {  // culled: zero rows (written in store mode, skipped or +0 in ACC)
       for (int k = 0; k < 3; k++) r0[k] = 0.0f;
       for (int k = 3; k < a.M * 3; k++) r1[k - 3] = 0.0f;

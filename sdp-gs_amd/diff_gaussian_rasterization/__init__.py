@@ -371,7 +371,7 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
             if any(gr is not None and not gr.is_contiguous() for gr in grads):
                 raise RuntimeError("grad-into-leaves needs contiguous .grad tensors")
             d_means3D, d_dc, d_rest, d_op, d_sc, d_rot, d_lf = grads
-            d_means2D = (torch.zeros if accumulate else torch.empty)((P, 3), **fopts)
+            d_means2D = torch.empty((P, 3), **fopts)  # always stored by the kernel
         else:
             d_means2D = torch.empty((P, 3), **fopts)
             d_means3D = torch.empty((P, 3), **fopts)
