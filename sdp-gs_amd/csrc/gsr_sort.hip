@@ -148,14 +148,30 @@ constexpr uint64_t kStAgg = 1ull << 32, kStIncl = 2ull << 32, kStFlags = 3ull <<
 }  // namespace
 // count of timed-out look-backs since the last check (sort_timeouts_word)
 __device__ uint32_t g_lookback_timeouts;
+#ifndef GSR_SORT_TRACE
+#define GSR_SORT_TRACE 0
+#endif
+#if GSR_SORT_TRACE
+// per-partition phase timestamps (100 MHz wall clock) of the last one-sweep pass:
+// [part][0..5] = start, ranked, scanned, looked back, reordered, stored; [part][6] = hw id
+__device__ uint64_t g_sort_trace[16384][8];
+#endif
 namespace {
 constexpr int kSpinLimit = 1 << 18;
 #ifndef GSR_LOOKBACK
 #define GSR_LOOKBACK 16
 #endif
 constexpr int kLookback = GSR_LOOKBACK;  // predecessor status words loaded per look-back step
-constexpr int kKeysPerThread = kSortTile / kThreads;  // GSR_SORT_KPT (default 16)
-constexpr int kKeysPerWave = kKeysPerThread * 64;
+// One-sweep workgroup size: NT lanes share a partition of kSortTile keys.  More lanes keep the
+// ranking chain short (kSortTile / NT keys per lane) and hide its LDS latency with other waves
+// (256 lanes = one wave per SIMD, every latency exposed: 7.5 us of ranking per pass); but 1024-lane
+// workgroups (48 KB LDS, 16 waves) fit only 2 per CU, so with more than 2 x 256 partitions the
+// late ones wait for a slot.  GSR_SORT_THREADS = 0 picks 1024 when every partition is resident
+// at once and 512 otherwise; 256 / 512 / 1024 force one shape.
+#ifndef GSR_SORT_THREADS
+#define GSR_SORT_THREADS 0
+#endif
+constexpr uint32_t kResident1024 = 2 * 256;  // 1024-lane partitions resident at once (256 CUs)
 
 // Digit totals of every pass from the unsorted keys.  Its own tile (GSR_TOTALS_KPT keys per
 // thread) and a bounded grid striding over tiles: short per-workgroup chains for latency, and at
@@ -218,19 +234,31 @@ __device__ __forceinline__ void status_store(uint64_t* p, uint64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__global__ __launch_bounds__(kThreads) void radix_onesweep_kernel(
+template <int NT>
+__global__ __launch_bounds__(NT) void radix_onesweep_kernel(
     const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin, size_t n, int shift,
     int bits, const uint32_t* __restrict__ totals, uint32_t* __restrict__ ticket,
     uint64_t* __restrict__ status, uint32_t* __restrict__ err, uint32_t* __restrict__ kout,
     uint32_t* __restrict__ vout) {
+  constexpr int kSortWaves = NT / 64, kSortThreads = NT;
+  constexpr int kKeysPerThread = kSortTile / NT, kKeysPerWave = kKeysPerThread * 64;
+  static_assert(NT >= 256 && kSortTile % NT == 0, "one-sweep tile shape");
   __shared__ uint32_t s_k[kSortTile];
   __shared__ uint32_t s_v[kSortTile];
-  __shared__ uint32_t s_cnt[kThreads / 64][256];
+  __shared__ uint32_t s_cnt[kSortWaves][256];
   __shared__ uint32_t s_gofs[256];
-  __shared__ uint32_t s_scan[kThreads / 64];
+  __shared__ uint32_t s_scan[kSortWaves];
   __shared__ uint32_t s_part;
   const int t = (int)threadIdx.x, lane = t & 63, wid = t >> 6;
   const uint32_t mask = (1u << bits) - 1u;
+#if GSR_SORT_TRACE
+  uint64_t tr[6];
+#define SORT_TRACE(k) \
+  if (t == 0) tr[k] = wall_clock64();
+#else
+#define SORT_TRACE(k)
+#endif
+  SORT_TRACE(0)
   // ticket, not blockIdx: a partition can only wait on partitions whose workgroups already run
   // (a per-XCD ticket variant timed out its look-back on gfx950 -- dispatch order across XCDs
   // gives no such guarantee)
@@ -241,8 +269,7 @@ __global__ __launch_bounds__(kThreads) void radix_onesweep_kernel(
   // partition is always resident and the look-back always progresses (bounded spin as backstop)
   if (t == 0) s_part = blockIdx.x;
 #endif
-#pragma unroll
-  for (int w = 0; w < kThreads / 64; w++) s_cnt[w][t] = 0;
+  for (int e = t; e < kSortWaves * 256; e += kSortThreads) (&s_cnt[0][0])[e] = 0;
   __syncthreads();
   const uint32_t part = s_part;
   const size_t base = (size_t)part * kSortTile;
@@ -268,20 +295,31 @@ __global__ __launch_bounds__(kThreads) void radix_onesweep_kernel(
     if (valid && (__ffsll((long long)peers) - 1) == lane) s_cnt[wid][d] = before + (uint32_t)__popcll(peers);
   }
   __syncthreads();
-  // thread t <-> digit t
-  const uint32_t c0 = s_cnt[0][t], c1 = s_cnt[1][t], c2 = s_cnt[2][t], c3 = s_cnt[3][t];
-  const uint32_t h = c0 + c1 + c2 + c3;
-  uint64_t* my = status + (size_t)part * 256 + t;
-  status_store(my, (part == 0 ? kStIncl : kStAgg) | (uint64_t)h);
+  SORT_TRACE(1)
+  // thread t < 256 <-> digit t (the other lanes join the workgroup scans with zeros)
+  const bool dig = t < 256;
+  const int dt = dig ? t : 0;
+  uint32_t h = 0;
+  if (dig)
+#pragma unroll
+    for (int w = 0; w < kSortWaves; w++) h += s_cnt[w][t];
+  uint64_t* my = status + (size_t)part * 256 + dt;
+  if (dig) status_store(my, (part == 0 ? kStIncl : kStAgg) | (uint64_t)h);
   uint32_t total_n;
-  const uint32_t lstart = block_excl_scan<kThreads / 64>(h, s_scan, total_n);
-  const uint32_t dbase = block_excl_scan<kThreads / 64>(totals[t], s_scan, total_n);
-  s_cnt[0][t] = lstart;
-  s_cnt[1][t] = lstart + c0;
-  s_cnt[2][t] = lstart + c0 + c1;
-  s_cnt[3][t] = lstart + c0 + c1 + c2;
+  const uint32_t lstart = block_excl_scan<kSortWaves>(dig ? h : 0u, s_scan, total_n);
+  const uint32_t dbase = block_excl_scan<kSortWaves>(dig ? totals[t] : 0u, s_scan, total_n);
+  if (dig) {
+    uint32_t run = lstart;
+#pragma unroll
+    for (int w = 0; w < kSortWaves; w++) {
+      const uint32_t c = s_cnt[w][t];
+      s_cnt[w][t] = run;
+      run += c;
+    }
+  }
+  SORT_TRACE(2)
   uint32_t excl = 0;
-  if (part > 0) {
+  if (dig && part > 0) {
     // windowed look-back: kLookback predecessors' words are loaded together (independent
     // loads in flight) and consumed in order up to the first INCLUSIVE one or the first word not
     // yet published (then re-polled from there); partition 0 is always INCLUSIVE, so the walk
@@ -292,7 +330,7 @@ __global__ __launch_bounds__(kThreads) void radix_onesweep_kernel(
       uint64_t w[kLookback];
 #pragma unroll
       for (int j = 0; j < kLookback; j++)
-        w[j] = (q - j >= 0) ? status_load(status + (size_t)(q - j) * 256 + t) : kStIncl;
+        w[j] = (q - j >= 0) ? status_load(status + (size_t)(q - j) * 256 + dt) : kStIncl;
       int used = 0;
       bool done = false, stop = false;
 #pragma unroll
@@ -317,8 +355,9 @@ __global__ __launch_bounds__(kThreads) void radix_onesweep_kernel(
     }
     status_store(my, kStIncl | (uint64_t)(excl + h));
   }
-  s_gofs[t] = dbase + excl - lstart;
+  if (dig) s_gofs[t] = dbase + excl - lstart;
   __syncthreads();
+  SORT_TRACE(3)
 #pragma unroll
   for (int r = 0; r < kKeysPerThread; r++) {
     if (wbase + (size_t)r * 64 + lane < n) {
@@ -329,8 +368,9 @@ __global__ __launch_bounds__(kThreads) void radix_onesweep_kernel(
     }
   }
   __syncthreads();
+  SORT_TRACE(4)
   const uint32_t nvalid = (uint32_t)min((size_t)kSortTile, n - base);
-  for (uint32_t i = (uint32_t)t; i < nvalid; i += kThreads) {
+  for (uint32_t i = (uint32_t)t; i < nvalid; i += kSortThreads) {
     const uint32_t k = s_k[i];
     const uint32_t o = s_gofs[(k >> shift) & mask] + i;
     if (o < n) {  // only a timed-out look-back (error word raised) can produce o >= n
@@ -338,6 +378,16 @@ __global__ __launch_bounds__(kThreads) void radix_onesweep_kernel(
       vout[o] = s_v[i];
     }
   }
+#if GSR_SORT_TRACE
+  SORT_TRACE(5)
+  if (t == 0 && part < 16384) {
+    for (int k = 0; k < 6; k++) g_sort_trace[part][k] = tr[k];
+    uint32_t hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(hw));
+    g_sort_trace[part][6] = hw;
+  }
+#endif
+#undef SORT_TRACE
 }
 
 // One workgroup: *out = sum of the n partials (n <= kScanMaxParts).
@@ -383,6 +433,14 @@ hipError_t scan_u32(const uint32_t* in, const uint32_t* gather, uint32_t* out, s
   return hipGetLastError();
 }
 
+#if GSR_SORT_TRACE
+extern "C" int gsr_test_sort_trace(uint64_t* out, int parts) {
+  if (parts > 16384) parts = 16384;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sort_trace), (size_t)parts * 8 * sizeof(uint64_t))
+             == hipSuccess ? 0 : 2;
+}
+#endif
+
 uint32_t* sort_timeouts_word() {
   void* p = nullptr;
   if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_lookback_timeouts)) != hipSuccess) return nullptr;
@@ -409,10 +467,16 @@ hipError_t radix_sort_pairs(uint32_t* ka, uint32_t* va, uint32_t* kb, uint32_t* 
   for (int p = 0; p < passes; p++) {
     const int shift = 8 * p;
     const int dbits = (bits - shift) < 8 ? (bits - shift) : 8;
-    hipLaunchKernelGGL(radix_onesweep_kernel, dim3(nb), dim3(kThreads), 0, s, kin, vin, n, shift,
-                       dbits, scratch.aux + kSortAuxTotals + 256 * p,
-                       scratch.aux + kSortAuxTickets + 8 * p, scratch.status + (size_t)p * nb * 256,
-                       scratch.aux + kSortAuxErr, kout, vout);
+    const int nt = GSR_SORT_THREADS ? GSR_SORT_THREADS : (nb <= kResident1024 ? 1024 : 512);
+#define GSR_ONESWEEP(NT)                                                                          \
+  hipLaunchKernelGGL(radix_onesweep_kernel<NT>, dim3(nb), dim3(NT), 0, s, kin, vin, n, shift,    \
+                     dbits, scratch.aux + kSortAuxTotals + 256 * p,                              \
+                     scratch.aux + kSortAuxTickets + 8 * p, scratch.status + (size_t)p * nb * 256, \
+                     scratch.aux + kSortAuxErr, kout, vout)
+    if (nt == 1024) GSR_ONESWEEP(1024);
+    else if (nt == 512) GSR_ONESWEEP(512);
+    else GSR_ONESWEEP(256);
+#undef GSR_ONESWEEP
     uint32_t* t;
     t = kin; kin = kout; kout = t;
     t = vin; vin = vout; vout = t;
