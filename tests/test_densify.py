@@ -282,13 +282,10 @@ def test_optimizer_steps_after_densify():
         assert float(m.optimizer.state[g["params"][0]]["step"]) == 8.0
 
 
-def _dp_worker(rank, world, port, q):
-    import os
+def _dp_worker(rank, world, init, q):
     import torch.distributed as dist
     from gsr_amd.parallel import allreduce_densification_stats
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=init, rank=rank, world_size=world)
     m = _model(30_000, seed=12)                 # same replica on every rank
     gen = torch.Generator(device="cuda").manual_seed(100 + rank)
     vs = torch.zeros((30_000, 3), device="cuda", requires_grad=True)
@@ -312,11 +309,11 @@ def test_densify_data_parallel_replicas_stay_identical():
     densify_and_prune with an identically seeded generator -> bit-identical replicas, equal to the
     reference restatement run once on the reduced statistics."""
     import torch.multiprocessing as mp
-    from test_parallel import _free_port
+    from test_parallel import _init_method
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, q)) for r in range(2)]
+    init = _init_method()
+    procs = [ctx.Process(target=_dp_worker, args=(r, 2, init, q)) for r in range(2)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=300) for _ in procs], key=lambda x: x[0])

@@ -5,7 +5,7 @@ a differentiable CPU stand-in so the sharding + bucketed all-reduce logic is exe
 device: the summed gradients of the sharded run must equal the single-process gradients over all
 views."""
 import os
-import socket
+import tempfile
 
 import pytest
 import torch
@@ -15,12 +15,12 @@ import torch.multiprocessing as mp
 from gsr_amd.parallel import GradAllReducer, allreduce_densification_stats, shard_views
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+def _init_method():
+    """File rendezvous: no TCP port to race for between picking it and binding it."""
+    fd, path = tempfile.mkstemp(prefix="gsr_pg_")
+    os.close(fd)
+    os.unlink(path)
+    return "file://" + path
 
 
 def _params(seed=0):
@@ -37,10 +37,8 @@ def _view_loss(params, v):
             + torch.sigmoid(params[2] * (v + 1)).mean())
 
 
-def _worker(rank, world, port, n_views, bucket_bytes, attach, q):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+def _worker(rank, world, init, n_views, bucket_bytes, attach, q):
+    dist.init_process_group("gloo", init_method=init, rank=rank, world_size=world)
     params = _params()
     reducer = GradAllReducer(params, bucket_bytes=bucket_bytes)
     if attach:  # .grad are views into the all-reduce buffer (bench.py's training step)
@@ -66,8 +64,8 @@ def _worker(rank, world, port, n_views, bucket_bytes, attach, q):
 def test_sharded_allreduce_equals_single_process(n_views, bucket_bytes, attach):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, n_views, bucket_bytes, attach, q)) for r in range(2)]
+    init = _init_method()
+    procs = [ctx.Process(target=_worker, args=(r, 2, init, n_views, bucket_bytes, attach, q)) for r in range(2)]
     for p in procs:
         p.start()
     grads, accum, denom, radii = q.get(timeout=120)
