@@ -20,6 +20,10 @@ size_t gsr_test_sort_scratch_bytes(size_t n);
 /* Stable LSD radix sort of (keys, vals) over key bits [0, bits), in place (device pointers). */
 int gsr_test_radix_sort_pairs(uint32_t* keys, uint32_t* vals, size_t n, int bits, void* scratch,
                               void* stream);
+/* Same, as the depth sort runs it: keys equal to 0xffffffff (culled Gaussians) may end up at any
+ * position; every other key is in stable sorted order. */
+int gsr_test_radix_sort_pairs_sentinel(uint32_t* keys, uint32_t* vals, size_t n, int bits,
+                                       void* scratch, void* stream);
 /* Scratch bytes needed by gsr_test_scan for n elements. */
 size_t gsr_test_scan_scratch_bytes(size_t n);
 /* out = inclusive (or exclusive) prefix sum of in (device pointers). */

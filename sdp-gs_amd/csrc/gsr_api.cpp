@@ -68,6 +68,33 @@ ImgState carve_img(char* base, size_t W, size_t H) {
   return s;
 }
 
+// Geometry buffers whose gradient accumulator rows were zeroed by their forward's preprocess
+// and not yet used by a backward: the backward skips its memset exactly once per forward (a
+// second backward through the same graph, retain_graph=True, clears them itself).
+namespace {
+std::mutex g_acc_mu;
+std::vector<const void*> g_acc_clean;
+}  // namespace
+void acc_mark_clean(const void* geom) {
+  std::lock_guard<std::mutex> l(g_acc_mu);
+  for (const void* p : g_acc_clean)
+    if (p == geom) return;
+  // forwards without a backward (inference) leave entries behind: keep the newest few (a
+  // dropped entry only costs its backward a memset)
+  if (g_acc_clean.size() >= 64) g_acc_clean.erase(g_acc_clean.begin());
+  g_acc_clean.push_back(geom);
+}
+bool acc_take_clean(const void* geom) {
+  std::lock_guard<std::mutex> l(g_acc_mu);
+  for (size_t i = 0; i < g_acc_clean.size(); i++)
+    if (g_acc_clean[i] == geom) {
+      g_acc_clean[i] = g_acc_clean.back();
+      g_acc_clean.pop_back();
+      return true;
+    }
+  return false;
+}
+
 int tile_schedule_mode() {
   static const int mode = [] {
     const char* e = getenv("GSR_TILE_ORDER");
@@ -264,7 +291,8 @@ static int forward_impl(int P, int M, const float* background, const float* mean
   ImgState im = carve_img(ibase, (size_t)W, (size_t)H);
   int32_t* radii_ptr = radii ? radii : g.radii;
 
-  GSR_CHECK(hipMemsetAsync(g.flags, 0, 4 * sizeof(uint32_t), stream));
+  // flags[0] (prefiltered violation) is only written -- and only read back -- when prefiltered
+  if (prefiltered) GSR_CHECK(hipMemsetAsync(g.flags, 0, 4 * sizeof(uint32_t), stream));
   PreArgs pa{};
   pa.P = P; pa.D = degree; pa.M = M; pa.W = W; pa.H = H; pa.gx = gx; pa.gy = gy;
   pa.means3D = means3D; pa.scales = scales; pa.rotations = rotations; pa.opacities = opacities;
@@ -278,28 +306,33 @@ static int forward_impl(int P, int M, const float* background, const float* mean
   pa.prefiltered = prefiltered; pa.include_feature = include_feature;
   pa.radii = radii_ptr; pa.g = g;
   pa.fused = fused; pa.sh_dc = sh_dc; pa.sh_rest = sh_rest;
+  // the preprocess grid also zeroes the depth sort's scratch and the backward's accumulators
+  pa.clear = SideClear{g.sort.aux, sort_clear_bytes(g.sort, (size_t)P, 32)};
+  pa.acc_zero = 1;
   PROF_BEGIN(PREPROCESS);
   GSR_CHECK(launch_preprocess(pa, stream));
   // R = total tile count (order-independent): reduced right after the preprocess and read back
   // while the depth sort and the scan are already queued behind it, so the host's wait and the
   // binning-buffer allocation overlap GPU work instead of draining the stream
-  GSR_CHECK(reduce_u32(g.tiles_touched, (size_t)P, g.scan_parts, g.flags + 1, stream));
+  // flags[1] = R, flags[2] = the sticky look-back timeout counter of earlier sorts (P > 0 here)
+  GSR_CHECK(reduce_u32(g.tiles_touched, (size_t)P, g.scan_parts, g.flags + 1, stream, true));
   PROF_END(PREPROCESS);
   uint32_t* host = pinned_slot();
   hipEvent_t ready = readback_event();
   if (!host || !ready) return fail(GSR_ERR_HIP, "pinned host slot / event creation failed");
   uint32_t* timeouts = sort_timeouts_word();
   if (!timeouts) return fail(GSR_ERR_HIP, "sort timeout word unavailable");
-  GSR_CHECK(hipMemcpyAsync(host, g.flags, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
-  // look-back timeouts of the sorts of EARLIER calls on this stream (the one-sweep sort's spin
-  // bound): reported here, one call late, instead of a sync after every sort
-  GSR_CHECK(hipMemcpyAsync(host + 3, timeouts, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+  // one read-back: flags[0] (prefiltered violation), R, and the look-back timeouts of the sorts
+  // of EARLIER calls on this stream (the one-sweep sort's spin bound) -- reported here, one call
+  // late, instead of a sync after every sort
+  GSR_CHECK(hipMemcpyAsync(host, g.flags, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
   GSR_CHECK(hipEventRecord(ready, stream));
 
   bool in_b = false;
   PROF_BEGIN(DEPTH_SORT);
   GSR_CHECK(radix_sort_pairs(g.dkey_a, g.dval_a, g.dkey_b, g.dval_b, (size_t)P, 32,
-                             g.sort, &in_b, stream));
+                             g.sort, &in_b, stream, /*sentinel_anywhere=*/true,
+                             /*precleared=*/true));
   PROF_END(DEPTH_SORT);
   const uint32_t* order = in_b ? g.dval_b : g.dval_a;
   PROF_BEGIN(SCAN);
@@ -307,13 +340,13 @@ static int forward_impl(int P, int M, const float* background, const float* mean
   PROF_END(SCAN);
 
   GSR_CHECK(hipEventSynchronize(ready));
-  if (host[3]) {
+  if (host[2]) {
     (void)hipMemsetAsync(timeouts, 0, sizeof(uint32_t), stream);
     return fail(GSR_ERR_HIP, "a radix-sort look-back timed out in an earlier call on this device: "
                 "that call's outputs are invalid");
   }
   const uint32_t R = host[1];
-  if (host[0]) return fail(GSR_ERR_PREFILTERED,
+  if (prefiltered && host[0]) return fail(GSR_ERR_PREFILTERED,
                            "Point is filtered although prefiltered is set. This shouldn't happen!");
   if (R > 0x7fffffffu)
     return fail(GSR_ERR_TOO_LARGE, "num_rendered = %u exceeds the sort capacity", R);
@@ -329,12 +362,16 @@ static int forward_impl(int P, int M, const float* background, const float* mean
   BinState b = carve_bin(bbase, R);
 
   PROF_BEGIN(DUPLICATE);
-  GSR_CHECK(launch_duplicate(P, order, g.offsets, radii_ptr, g.rec, gx, gy, b.tkey_a, b.tval_a, stream));
+  // the duplicate grid also zeroes the tile sort's scratch and the tile ranges
+  const int tbits = tile_bits(ntiles);
+  GSR_CHECK(launch_duplicate(P, order, g.offsets, radii_ptr, g.rec, gx, gy, b.tkey_a, b.tval_a,
+                             SideClear{b.sort.aux, sort_clear_bytes(b.sort, R, tbits)},
+                             SideClear{im.ranges, sizeof(uint2) * ntiles}, stream));
   PROF_END(DUPLICATE);
   bool t_in_b = false;
   PROF_BEGIN(TILE_SORT);
-  GSR_CHECK(radix_sort_pairs(b.tkey_a, b.tval_a, b.tkey_b, b.tval_b, R, tile_bits(ntiles),
-                             b.sort, &t_in_b, stream));
+  GSR_CHECK(radix_sort_pairs(b.tkey_a, b.tval_a, b.tkey_b, b.tval_b, R, tbits, b.sort, &t_in_b,
+                             stream, false, /*precleared=*/true));
   PROF_END(TILE_SORT);
   if (debug) {
     GSR_CHECK(hipMemcpyAsync(host + 2, b.sort.aux + kSortAuxErr, 4, hipMemcpyDeviceToHost, stream));
@@ -344,7 +381,7 @@ static int forward_impl(int P, int M, const float* background, const float* mean
   const uint32_t* tiles_sorted = t_in_b ? b.tkey_b : b.tkey_a;
   const uint32_t* point_list = t_in_b ? b.tval_b : b.tval_a;
   PROF_BEGIN(RANGES);
-  GSR_CHECK(launch_tile_ranges(R, tiles_sorted, im.ranges, ntiles, stream));
+  GSR_CHECK(launch_tile_ranges(R, tiles_sorted, im.ranges, ntiles, stream, /*ranges_cleared=*/true));
   PROF_END(RANGES);
 
   RenderArgs ra{};
@@ -358,6 +395,7 @@ static int forward_impl(int P, int M, const float* background, const float* mean
   GSR_CHECK(launch_render_forward(ra, stream));
   PROF_END(RENDER_FWD);
   *num_rendered = (int)R;
+  acc_mark_clean(gbase);
   return GSR_OK;
 }
 
@@ -448,9 +486,11 @@ static int backward_impl(
   const uint32_t* point_list = (passes & 1) ? b.tval_b : b.tval_a;
   const int32_t* radii_ptr = radii ? radii : g.radii;
 
-  PROF_BEGIN(ACC_ZERO);
-  GSR_CHECK(hipMemsetAsync(g.acc, 0, sizeof(float) * kAccFloats * (size_t)P, stream));
-  PROF_END(ACC_ZERO);
+  if (!acc_take_clean(geom_buffer)) {  // not freshly zeroed by this buffer's forward
+    PROF_BEGIN(ACC_ZERO);
+    GSR_CHECK(hipMemsetAsync(g.acc, 0, sizeof(float) * kAccFloats * (size_t)P, stream));
+    PROF_END(ACC_ZERO);
+  }
   if (R > 0) {
     RenderBwdArgs rb{};
     rb.W = W; rb.H = H; rb.gx = gx; rb.gy = gy;
@@ -549,8 +589,21 @@ size_t gsr_test_sort_scratch_bytes(size_t n) {
   return sort_scratch_layout(nullptr, n, nullptr, nullptr, nullptr);
 }
 
+static int test_radix_sort(uint32_t* keys, uint32_t* vals, size_t n, int bits, void* scratch,
+                           void* stream_ptr, bool sentinel_anywhere);
+
 int gsr_test_radix_sort_pairs(uint32_t* keys, uint32_t* vals, size_t n, int bits, void* scratch,
                               void* stream_ptr) {
+  return test_radix_sort(keys, vals, n, bits, scratch, stream_ptr, false);
+}
+
+int gsr_test_radix_sort_pairs_sentinel(uint32_t* keys, uint32_t* vals, size_t n, int bits,
+                                       void* scratch, void* stream_ptr) {
+  return test_radix_sort(keys, vals, n, bits, scratch, stream_ptr, true);
+}
+
+static int test_radix_sort(uint32_t* keys, uint32_t* vals, size_t n, int bits, void* scratch,
+                           void* stream_ptr, bool sentinel_anywhere) {
   g_err.clear();
   hipStream_t stream = (hipStream_t)stream_ptr;
   const int debug = 0;
@@ -561,7 +614,7 @@ int gsr_test_radix_sort_pairs(uint32_t* keys, uint32_t* vals, size_t n, int bits
   SortScratch sc;
   sort_scratch_layout((char*)scratch, n, &kb, &vb, &sc);
   bool in_b = false;
-  GSR_CHECK(radix_sort_pairs(keys, vals, kb, vb, n, bits, sc, &in_b, stream));
+  GSR_CHECK(radix_sort_pairs(keys, vals, kb, vb, n, bits, sc, &in_b, stream, sentinel_anywhere));
   uint32_t* host = pinned_slot();
   if (!host) return fail(GSR_ERR_HIP, "pinned host allocation failed");
   GSR_CHECK(hipMemcpyAsync(host + 2, sc.aux + kSortAuxErr, 4, hipMemcpyDeviceToHost, stream));

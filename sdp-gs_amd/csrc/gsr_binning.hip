@@ -28,8 +28,12 @@ __global__ __launch_bounds__(kThreads) void duplicate_kernel(int P,
                                                              const float4* __restrict__ rec,
                                                              uint32_t gx, uint32_t gy,
                                                              uint32_t* __restrict__ tkey,
-                                                             uint32_t* __restrict__ tval) {
+                                                             uint32_t* __restrict__ tval,
+                                                             SideClear clear0, SideClear clear1) {
   const int s = (int)(blockIdx.x * kThreads + threadIdx.x);
+  const size_t nth = (size_t)gridDim.x * kThreads;
+  side_clear(clear0.p, clear0.bytes, (size_t)s, nth);
+  side_clear(clear1.p, clear1.bytes, (size_t)s, nth);
   if (s >= P) return;
   // coalesced reads first: culled / tile-less Gaussians (count 0) never touch the random gather
   uint32_t off = (s == 0) ? 0u : offsets[s - 1];
@@ -79,17 +83,21 @@ __global__ __launch_bounds__(kThreads) void tile_ranges_kernel(size_t R,
 
 hipError_t launch_duplicate(int P, const uint32_t* order, const uint32_t* offsets,
                             const int32_t* radii, const float4* rec, uint32_t gx, uint32_t gy,
-                            uint32_t* tkey, uint32_t* tval, hipStream_t s) {
+                            uint32_t* tkey, uint32_t* tval, SideClear clear0, SideClear clear1,
+                            hipStream_t s) {
   if (P == 0) return hipSuccess;
   hipLaunchKernelGGL(duplicate_kernel, dim3((P + kThreads - 1) / kThreads), dim3(kThreads), 0, s,
-                     P, order, offsets, radii, rec, gx, gy, tkey, tval);
+                     P, order, offsets, radii, rec, gx, gy, tkey, tval, clear0, clear1);
   return hipGetLastError();
 }
 
 hipError_t launch_tile_ranges(size_t R, const uint32_t* sorted_tiles, uint2* ranges,
-                              uint32_t ntiles, hipStream_t s) {
-  hipError_t e = hipMemsetAsync(ranges, 0, sizeof(uint2) * ntiles, s);
-  if (e != hipSuccess || R == 0) return e;
+                              uint32_t ntiles, hipStream_t s, bool ranges_cleared) {
+  if (!ranges_cleared) {
+    hipError_t e = hipMemsetAsync(ranges, 0, sizeof(uint2) * ntiles, s);
+    if (e != hipSuccess) return e;
+  }
+  if (R == 0) return hipSuccess;
   hipLaunchKernelGGL(tile_ranges_kernel, dim3((unsigned)((R + kThreads - 1) / kThreads)),
                      dim3(kThreads), 0, s, R, sorted_tiles, ranges);
   return hipGetLastError();

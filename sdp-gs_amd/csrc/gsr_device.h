@@ -31,6 +31,17 @@ __device__ constexpr float SH_C3_4 = -0.4570457994644658f;
 __device__ constexpr float SH_C3_5 = 1.445305721320277f;
 __device__ constexpr float SH_C3_6 = -0.5900435899266435f;
 
+// Grid-stride share of a SideClear (gsr_internal.h) for thread `tid` of `nthreads`.
+__device__ __forceinline__ void side_clear(void* p, size_t bytes, size_t tid, size_t nthreads) {
+  if (!p) return;
+  uint4* q = reinterpret_cast<uint4*>(p);
+  const size_t n16 = bytes >> 4;
+  for (size_t i = tid; i < n16; i += nthreads) q[i] = make_uint4(0u, 0u, 0u, 0u);
+  uint32_t* w = reinterpret_cast<uint32_t*>(p);
+  const size_t tail = (bytes & 15u) >> 2;
+  if (tid < tail) w[4 * n16 + tid] = 0u;
+}
+
 struct V3 { float x, y, z; };
 struct M3 { float m[3][3]; };  // m[col][row], glm::mat3 convention
 

@@ -62,13 +62,31 @@ constexpr int kSortMaxPasses = 4;
 // u64 look-back status words: one per (pass, partition, digit)
 inline size_t sort_status_len(size_t n) { return (size_t)kSortMaxPasses * sort_blocks(n) * 256; }
 // u32 aux words: digit totals [kSortMaxPasses][256], partition tickets [kSortMaxPasses][8],
+// digit-presence masks [kSortMaxPasses][8] (256 bits per pass over the keys != kSortSentinel),
 // error flag
 constexpr size_t kSortAuxTotals = 0, kSortAuxTickets = kSortMaxPasses * 256,
-                 kSortAuxErr = kSortAuxTickets + 8 * kSortMaxPasses, kSortAuxLen = kSortAuxErr + 4;
+                 kSortAuxMask = kSortAuxTickets + 8 * kSortMaxPasses,
+                 kSortAuxErr = kSortAuxMask + 8 * kSortMaxPasses, kSortAuxLen = kSortAuxErr + 4;
+// Key whose position in the sorted output does not matter (culled Gaussians: no tiles): it is
+// left out of the digit-presence masks, so a pass whose digit is constant over every other key
+// is a plain copy (see radix_onesweep_kernel).
+constexpr uint32_t kSortSentinel = 0xffffffffu;
 
 struct SortScratch {
   uint64_t* status;  // [sort_status_len(n)]
   uint32_t* aux;     // [kSortAuxLen]; aux[kSortAuxErr] != 0 after a sort = look-back timeout
+};
+// Bytes from scratch.aux that must be zero before a sort of n keys over `bits` bits (aux words
+// and the status words of the passes used); a multiple of 16 (status is 256-B aligned).
+inline size_t sort_clear_bytes(const SortScratch& sc, size_t n, int bits) {
+  return (size_t)((char*)(sc.status + (size_t)sort_passes(bits) * sort_blocks(n) * 256) -
+                  (char*)sc.aux);
+}
+// A zero-fill piggy-backed on a kernel that runs anyway (no separate memset launch): every
+// thread of the grid clears its grid-stride share.  bytes: multiple of 4, p 16-B aligned.
+struct SideClear {
+  void* p;
+  size_t bytes;
 };
 inline SortScratch take_sort_scratch(Carver& c, size_t n) {
   SortScratch s;
@@ -83,12 +101,18 @@ hipError_t scan_u32(const uint32_t* in, const uint32_t* gather, uint32_t* out, s
                     bool inclusive, uint32_t* parts, hipStream_t s);
 // *out = sum of n u32 values (two launches); parts: scratch of scan_parts(n) u32.
 hipError_t reduce_u32(const uint32_t* in, size_t n, uint32_t* parts, uint32_t* out,
-                      hipStream_t s);
+                      hipStream_t s, bool with_timeouts = false);
 // Stable LSD radix sort of (key, value) u32 pairs over key bits [0, bits).  Ping-pongs between
 // (ka, va) and (kb, vb); returns through *result_in_b whether the sorted data ended in (kb, vb).
-// One-sweep passes: 1 memset + 1 digit-totals launch + 1 launch per 8-bit digit.
+// One-sweep passes: 1 memset + 1 digit-totals launch + 1 launch per 8-bit digit; a pass whose
+// digit is the same for every key is a plain copy.  sentinel_anywhere: keys equal to
+// kSortSentinel may end up at any position (the depth sort's culled Gaussians), so they do not
+// count when deciding whether a digit is constant.
+// precleared: sort_clear_bytes(scratch, n, bits) from scratch.aux are already zero (cleared by
+// an earlier kernel on the stream through a SideClear): the memset launch is skipped.
 hipError_t radix_sort_pairs(uint32_t* ka, uint32_t* va, uint32_t* kb, uint32_t* vb, size_t n,
-                            int bits, SortScratch scratch, bool* result_in_b, hipStream_t s);
+                            int bits, SortScratch scratch, bool* result_in_b, hipStream_t s,
+                            bool sentinel_anywhere = false, bool precleared = false);
 // Device word counting look-back timeouts of any sort on the current device (sticky until the
 // host resets it); every forward reads it back with its instance count.
 uint32_t* sort_timeouts_word();
@@ -151,6 +175,10 @@ struct PreArgs {
   // and the SH coefficients come split as sh_dc [P,1,3] + sh_rest [P,M-1,3]
   int fused;
   const float *sh_dc, *sh_rest;
+  // zero-fills done by the preprocess grid: the depth sort's scratch, and (acc_zero != 0) the
+  // backward's per-Gaussian gradient accumulator rows g.acc
+  SideClear clear;
+  int acc_zero;
 };
 hipError_t launch_preprocess(const PreArgs& a, hipStream_t s);
 hipError_t launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present,
@@ -180,11 +208,14 @@ struct BwdPreArgs {
 hipError_t launch_preprocess_backward(const BwdPreArgs& a, hipStream_t s);
 
 // ---- binning (gsr_binning.hip) -------------------------------------------------------------------
+// The duplicate grid also zero-fills clear0 / clear1 (the tile sort's scratch, the ranges).
 hipError_t launch_duplicate(int P, const uint32_t* order, const uint32_t* offsets,
                             const int32_t* radii, const float4* rec, uint32_t gx, uint32_t gy,
-                            uint32_t* tkey, uint32_t* tval, hipStream_t s);
+                            uint32_t* tkey, uint32_t* tval, SideClear clear0, SideClear clear1,
+                            hipStream_t s);
+// ranges_cleared: the ranges are already zero (duplicate's side clear): no memset launch.
 hipError_t launch_tile_ranges(size_t R, const uint32_t* sorted_tiles, uint2* ranges,
-                              uint32_t ntiles, hipStream_t s);
+                              uint32_t ntiles, hipStream_t s, bool ranges_cleared = false);
 
 // ---- blend (gsr_render.hip) ----------------------------------------------------------------------
 struct RenderArgs {

@@ -63,7 +63,13 @@ __global__ __launch_bounds__(kThreads) void preprocess_kernel(PreArgs a) {
   // one lane per Gaussian; SH rows are read directly (an LDS-staged variant, gsr_stage.h, measured
   // slower here: its 48 KB of LDS cut occupancy below what this latency-bound kernel needs)
   const int idx = (int)(blockIdx.x * kThreads + threadIdx.x);
+  side_clear(a.clear.p, a.clear.bytes, (size_t)idx, (size_t)gridDim.x * kThreads);
   if (idx >= a.P) return;
+  if (a.acc_zero) {  // this Gaussian's 64-B gradient accumulator row (zeroed before the backward)
+    float4* row = reinterpret_cast<float4*>(a.g.acc + (size_t)idx * kAccFloats);
+#pragma unroll
+    for (int k = 0; k < kAccFloats / 4; k++) row[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
 #if GSR_PRE_HOIST
   // the small per-Gaussian inputs are all put in flight before the first dependent computation
   // (the compiler cannot hoist loads above the cull branches itself)
@@ -83,7 +89,7 @@ __global__ __launch_bounds__(kThreads) void preprocess_kernel(PreArgs a) {
   const GeomState& g = a.g;
   a.radii[idx] = 0;
   g.tiles_touched[idx] = 0;
-  g.dkey_a[idx] = 0xffffffffu;
+  g.dkey_a[idx] = kSortSentinel;  // culled: no tiles, any sorted position is fine
   g.dval_a[idx] = (uint32_t)idx;
   if (!near_ok) {
     if (a.prefiltered) atomicOr(&g.flags[0], 1u);  // reference __trap()s (auxiliary.h:156-160)

@@ -187,10 +187,14 @@ constexpr int kTotTile = kThreads * kTotKPT;
 
 __global__ __launch_bounds__(kThreads) void radix_totals_kernel(const uint32_t* __restrict__ keys,
                                                                 size_t n, int bits,
-                                                                uint32_t* __restrict__ totals) {
+                                                                uint32_t* __restrict__ totals,
+                                                                uint32_t* __restrict__ present,
+                                                                int skip_sentinel) {
   __shared__ uint32_t cnt[kSortMaxPasses][256];
+  __shared__ uint32_t nsent;  // sentinel keys of this workgroup (all digits 0xff)
 #pragma unroll
   for (int p = 0; p < kSortMaxPasses; p++) cnt[p][threadIdx.x] = 0;
+  if (threadIdx.x == 0) nsent = 0;
   __syncthreads();
   const int passes = (bits + 7) / 8;
   for (size_t base = (size_t)blockIdx.x * kTotTile; base < n;
@@ -207,6 +211,10 @@ __global__ __launch_bounds__(kThreads) void radix_totals_kernel(const uint32_t* 
       const bool valid = base + (size_t)r * kThreads + threadIdx.x < n;
       const uint64_t vmask = __ballot(valid);
       if (vmask == 0ull) continue;
+      if (skip_sentinel) {
+        const uint64_t sm = __ballot(valid && key[r] == kSortSentinel);
+        if (sm && (threadIdx.x & 63) == 0) atomicAdd(&nsent, (uint32_t)__popcll(sm));
+      }
       for (int p = 0; p < passes; p++) {
         const uint32_t d = (key[r] >> (8 * p)) & 0xffu;
         // typical depth keys share their top byte across a wave: one LDS add instead of 64
@@ -221,9 +229,18 @@ __global__ __launch_bounds__(kThreads) void radix_totals_kernel(const uint32_t* 
     }
   }
   __syncthreads();
+  const uint32_t ns = nsent;
+  const int lane = (int)(threadIdx.x & 63);
   for (int p = 0; p < passes; p++) {
     const uint32_t c = cnt[p][threadIdx.x];
     if (c) atomicAdd(&totals[p * 256 + threadIdx.x], c);
+    // digit presence over the non-sentinel keys (a sentinel has digit 0xff in every pass)
+    const uint32_t real = c - (threadIdx.x == 255u ? ns : 0u);
+    const uint64_t m = __ballot(real != 0u);
+    if (m && lane < 2) {
+      const uint32_t word = (uint32_t)(lane ? (m >> 32) : m);
+      if (word) atomicOr(&present[p * 8 + 2 * (threadIdx.x >> 6) + lane], word);
+    }
   }
 }
 
@@ -237,9 +254,9 @@ __device__ __forceinline__ void status_store(uint64_t* p, uint64_t v) {
 template <int NT>
 __global__ __launch_bounds__(NT) void radix_onesweep_kernel(
     const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin, size_t n, int shift,
-    int bits, const uint32_t* __restrict__ totals, uint32_t* __restrict__ ticket,
-    uint64_t* __restrict__ status, uint32_t* __restrict__ err, uint32_t* __restrict__ kout,
-    uint32_t* __restrict__ vout) {
+    int bits, const uint32_t* __restrict__ totals, const uint32_t* __restrict__ present,
+    uint32_t* __restrict__ ticket, uint64_t* __restrict__ status, uint32_t* __restrict__ err,
+    uint32_t* __restrict__ kout, uint32_t* __restrict__ vout) {
   constexpr int kSortWaves = NT / 64, kSortThreads = NT;
   constexpr int kKeysPerThread = kSortTile / NT, kKeysPerWave = kKeysPerThread * 64;
   static_assert(NT >= 256 && kSortTile % NT == 0, "one-sweep tile shape");
@@ -259,6 +276,23 @@ __global__ __launch_bounds__(NT) void radix_onesweep_kernel(
 #define SORT_TRACE(k)
 #endif
   SORT_TRACE(0)
+  {
+    // Every non-sentinel key has the same digit in this pass: the stable sort by it is the
+    // identity on those keys, and sentinel keys may land anywhere -- the pass is a copy (no
+    // ranking, no look-back).  Workgroup-uniform (the masks are final before the launch).
+    uint32_t ndig = 0;
+#pragma unroll
+    for (int w = 0; w < 8; w++) ndig += (uint32_t)__popc(present[w]);
+    if (ndig <= 1u) {
+      const size_t b0 = (size_t)blockIdx.x * kSortTile;
+      const size_t e0 = min(n, b0 + (size_t)kSortTile);
+      for (size_t i = b0 + (size_t)t; i < e0; i += NT) {
+        kout[i] = kin[i];
+        vout[i] = vin[i];
+      }
+      return;
+    }
+  }
   // ticket, not blockIdx: a partition can only wait on partitions whose workgroups already run
   // (a per-XCD ticket variant timed out its look-back on gfx950 -- dispatch order across XCDs
   // gives no such guarantee)
@@ -391,26 +425,33 @@ __global__ __launch_bounds__(NT) void radix_onesweep_kernel(
 }
 
 // One workgroup: *out = sum of the n partials (n <= kScanMaxParts).
+// with_timeouts: out[1] = the sticky look-back timeout counter (same read-back as the total).
 __global__ __launch_bounds__(1024) void sum_parts_kernel(const uint32_t* __restrict__ parts, int n,
-                                                         uint32_t* __restrict__ out) {
+                                                         uint32_t* __restrict__ out,
+                                                         int with_timeouts) {
   __shared__ uint32_t lds[16];
   uint32_t s = 0;
   for (int i = (int)threadIdx.x; i < n; i += 1024) s += parts[i];
   uint32_t total;
   block_excl_scan<16>(s, lds, total);
-  if (threadIdx.x == 0) *out = total;
+  if (threadIdx.x == 0) {
+    out[0] = total;
+    if (with_timeouts)
+      out[1] = __hip_atomic_load(&g_lookback_timeouts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 }  // namespace
 
 hipError_t reduce_u32(const uint32_t* in, size_t n, uint32_t* parts, uint32_t* out,
-                      hipStream_t s) {
+                      hipStream_t s, bool with_timeouts) {
   if (n == 0) return hipMemsetAsync(out, 0, sizeof(uint32_t), s);
   const size_t np = scan_parts(n);
   if (np > (size_t)kScanMaxParts) return hipErrorInvalidValue;
   hipLaunchKernelGGL(scan_reduce_kernel<false>, dim3((unsigned)np), dim3(kThreads), 0, s, in,
                      (const uint32_t*)nullptr, n, parts);
-  hipLaunchKernelGGL(sum_parts_kernel, dim3(1), dim3(1024), 0, s, parts, (int)np, out);
+  hipLaunchKernelGGL(sum_parts_kernel, dim3(1), dim3(1024), 0, s, parts, (int)np, out,
+                     with_timeouts ? 1 : 0);
   return hipGetLastError();
 }
 
@@ -448,20 +489,23 @@ uint32_t* sort_timeouts_word() {
 }
 
 hipError_t radix_sort_pairs(uint32_t* ka, uint32_t* va, uint32_t* kb, uint32_t* vb, size_t n,
-                            int bits, SortScratch scratch, bool* result_in_b, hipStream_t s) {
+                            int bits, SortScratch scratch, bool* result_in_b, hipStream_t s,
+                            bool sentinel_anywhere, bool precleared) {
   *result_in_b = false;
   if (n == 0 || bits <= 0) return hipSuccess;
   if (bits > 32 || n > 0xffffffffull) return hipErrorInvalidValue;
   const int passes = sort_passes(bits);
   const uint32_t nb = (uint32_t)sort_blocks(n);
   // aux (totals, tickets, error word) and the status words of the passes used: one memset
-  const size_t clear = (size_t)((char*)(scratch.status + (size_t)passes * nb * 256) - (char*)scratch.aux);
-  hipError_t e = hipMemsetAsync(scratch.aux, 0, clear, s);
-  if (e != hipSuccess) return e;
+  if (!precleared) {
+    hipError_t e = hipMemsetAsync(scratch.aux, 0, sort_clear_bytes(scratch, n, bits), s);
+    if (e != hipSuccess) return e;
+  }
   const size_t tot_tiles = (n + kTotTile - 1) / kTotTile;
   hipLaunchKernelGGL(radix_totals_kernel,
                      dim3((unsigned)(tot_tiles < GSR_TOTALS_GROUPS ? tot_tiles : GSR_TOTALS_GROUPS)),
-                     dim3(kThreads), 0, s, ka, n, bits, scratch.aux + kSortAuxTotals);
+                     dim3(kThreads), 0, s, ka, n, bits, scratch.aux + kSortAuxTotals,
+                     scratch.aux + kSortAuxMask, sentinel_anywhere ? 1 : 0);
   uint32_t *kin = ka, *vin = va, *kout = kb, *vout = vb;
   bool in_b = false;
   for (int p = 0; p < passes; p++) {
@@ -471,7 +515,8 @@ hipError_t radix_sort_pairs(uint32_t* ka, uint32_t* va, uint32_t* kb, uint32_t* 
 #define GSR_ONESWEEP(NT)                                                                          \
   hipLaunchKernelGGL(radix_onesweep_kernel<NT>, dim3(nb), dim3(NT), 0, s, kin, vin, n, shift,    \
                      dbits, scratch.aux + kSortAuxTotals + 256 * p,                              \
-                     scratch.aux + kSortAuxTickets + 8 * p, scratch.status + (size_t)p * nb * 256, \
+                     scratch.aux + kSortAuxMask + 8 * p, scratch.aux + kSortAuxTickets + 8 * p,  \
+                     scratch.status + (size_t)p * nb * 256, \
                      scratch.aux + kSortAuxErr, kout, vout)
     if (nt == 1024) GSR_ONESWEEP(1024);
     else if (nt == 512) GSR_ONESWEEP(512);

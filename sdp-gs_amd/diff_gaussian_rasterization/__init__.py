@@ -164,6 +164,9 @@ class _RasterizeGaussians(torch.autograd.Function):
                               conf if conf is not None else empty, bg, view, proj, campos,
                               geom, binning, image)
         ctx.mark_non_differentiable(radii)
+        # outputs the loss does not use arrive as None (the kernels take NULL as zero) instead of
+        # autograd materialising zero images and an int zero radii tensor per view
+        ctx.set_materialize_grads(False)
         return color, depth, alpha, feature, radii
 
     @staticmethod
@@ -327,6 +330,9 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
                               conf if conf is not None else empty, bg, view, proj, campos,
                               geom, binning, image)
         ctx.mark_non_differentiable(radii)
+        # outputs the loss does not use arrive as None (the kernels take NULL as zero) instead of
+        # autograd materialising zero images and an int zero radii tensor per view
+        ctx.set_materialize_grads(False)
         return color, depth, alpha, feature, radii
 
     @staticmethod

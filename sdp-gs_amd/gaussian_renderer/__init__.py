@@ -47,19 +47,79 @@ def _fused_eligible(pc, pipe, opt, override_color, override_language) -> bool:
             and getattr(pc, "rotation_activation", None) is torch.nn.functional.normalize)
 
 
+class _RenderPkg(dict):
+    """render()'s result dict with entries computed on first access (train.py never reads
+    "opacity", so the fused path does not launch its sigmoid per view).  Behaves as the plain
+    dict the reference returns: keys, iteration, `in`, get() and copies see every entry.  A lazy
+    entry is evaluated from the model as it is at first access."""
+
+    def __init__(self, items, lazy):
+        super().__init__(items)
+        self._lazy = dict(lazy)
+
+    def _fill(self):
+        for k in list(self._lazy):
+            self[k]
+        return self
+
+    def __missing__(self, key):
+        if key in self._lazy:
+            value = self._lazy.pop(key)()
+            self[key] = value
+            return value
+        raise KeyError(key)
+
+    def __contains__(self, key):
+        return super().__contains__(key) or key in self._lazy
+
+    def get(self, key, default=None):
+        return self[key] if key in self else default
+
+    def __iter__(self):
+        return dict.__iter__(self._fill())
+
+    def __len__(self):
+        return super().__len__() + len(self._lazy)
+
+    def keys(self):
+        return dict.keys(self._fill())
+
+    def values(self):
+        return dict.values(self._fill())
+
+    def items(self):
+        return dict.items(self._fill())
+
+    def copy(self):
+        return dict(dict.items(self._fill()))
+
+
 def render(viewpoint_camera, pc, pipe, bg_color: torch.Tensor, opt, scaling_modifier=1.0,
            override_color=None, override_language=None):
     xyz = pc.get_xyz
-    screenspace_points = torch.zeros_like(xyz, dtype=xyz.dtype, requires_grad=True,
-                                          device=xyz.device) + 0
-    try:
-        screenspace_points.retain_grad()
-    except Exception:
-        pass
+    fused = _fused_eligible(pc, pipe, opt, override_color, override_language)
+    if fused:
+        # the kernel never reads means2D's values, only returns its gradient: a zero leaf (one
+        # fill) stands in for the reference's zeros_like(...) + 0 non-leaf (fill + add); its
+        # .grad is the same per-view screen-space gradient
+        screenspace_points = torch.zeros_like(xyz, dtype=xyz.dtype, requires_grad=True,
+                                              device=xyz.device)
+    else:
+        screenspace_points = torch.zeros_like(xyz, dtype=xyz.dtype, requires_grad=True,
+                                              device=xyz.device) + 0
+        try:
+            screenspace_points.retain_grad()
+        except Exception:
+            pass
 
     tanfovx = math.tan(viewpoint_camera.FoVx * 0.5)
     tanfovy = math.tan(viewpoint_camera.FoVy * 0.5)
-    confidence = pc.confidence if pipe.use_confidence else torch.ones_like(pc.confidence)
+    if pipe.use_confidence:
+        confidence = pc.confidence
+    elif fused:
+        confidence = None  # the kernels treat a missing confidence as ones (no fill per view)
+    else:
+        confidence = torch.ones_like(pc.confidence)
     raster_settings = GaussianRasterizationSettings(
         image_height=int(viewpoint_camera.image_height),
         image_width=int(viewpoint_camera.image_width),
@@ -77,7 +137,7 @@ def render(viewpoint_camera, pc, pipe, bg_color: torch.Tensor, opt, scaling_modi
         debug=pipe.debug)
     rasterizer = GaussianRasterizer(raster_settings=raster_settings)
 
-    if _fused_eligible(pc, pipe, opt, override_color, override_language):
+    if fused:
         # Default configuration: the activations / cat of GaussianModel's getters run inside the
         # preprocess kernel and the backward writes the raw leaves' grads (identical outputs).
         lang = pc._language_feature if opt.include_feature else None
@@ -85,15 +145,15 @@ def render(viewpoint_camera, pc, pipe, bg_color: torch.Tensor, opt, scaling_modi
             rasterize_gaussians_fused(xyz, screenspace_points, pc._features_dc,
                                       pc._features_rest, pc._opacity, pc._scaling, pc._rotation,
                                       lang, raster_settings)
-        return {"render": rendered_image,
-                "depth": rendered_depth,
-                "alpha": rendered_alpha,
-                "opacity": pc.get_opacity,
-                "feature": language_feature_image,
-                "viewspace_points": screenspace_points,
-                "visibility_filter": radii > 0,
-                "radii": radii,
-                "color": None}
+        return _RenderPkg({"render": rendered_image,
+                           "depth": rendered_depth,
+                           "alpha": rendered_alpha,
+                           "feature": language_feature_image,
+                           "viewspace_points": screenspace_points,
+                           "visibility_filter": radii > 0,
+                           "radii": radii,
+                           "color": None},
+                          {"opacity": lambda: pc.get_opacity})
 
     means3D = xyz
     means2D = screenspace_points

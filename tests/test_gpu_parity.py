@@ -175,6 +175,7 @@ def test_forward_is_deterministic():
 @pytest.mark.parametrize("n,bits,kind", [(1, 8, "int"), (4095, 13, "int"), (4097, 32, "int"),
                                          (1_000_003, 32, "int"), (3_000_000, 13, "int"),
                                          (8191, 4, "int"), (1_000_000, 32, "depth"),
+                                         (1_000_000, 32, "depth_narrow"),
                                          (2_500_000, 12, "tiles")])
 def test_radix_sort_sorted_and_stable(n, bits, kind):
     """One-sweep radix sort (gsr_sort.hip) == numpy's stable argsort, bit for bit: full 32-bit
@@ -184,6 +185,8 @@ def test_radix_sort_sorted_and_stable(n, bits, kind):
     rng = np.random.default_rng(n)
     if kind == "depth":
         keys = rng.lognormal(1.0, 0.5, size=n).astype(np.float32).view(np.uint32) + 0
+    elif kind == "depth_narrow":  # constant top byte: that pass is a copy
+        keys = rng.uniform(3.0, 5.0, size=n).astype(np.float32).view(np.uint32) + 0
     elif kind == "tiles":
         keys = np.minimum(rng.exponential(300.0, size=n), (1 << bits) - 1).astype(np.uint32)
     else:
@@ -198,6 +201,35 @@ def test_radix_sort_sorted_and_stable(n, bits, kind):
     order = np.argsort(keys, kind="stable")
     np.testing.assert_array_equal(k.cpu().numpy().view(np.uint32), keys[order])
     np.testing.assert_array_equal(v.cpu().numpy().view(np.uint32), vals[order])
+
+
+@pytest.mark.parametrize("n,frac_culled", [(1_000_000, 0.0), (1_000_000, 0.2), (70_001, 0.5),
+                                           (4097, 1.0)])
+def test_radix_sort_sentinel_copy_pass(n, frac_culled):
+    """Depth-sort mode: culled keys (0xffffffff) may land anywhere; every other key must be in
+    stable sorted order.  Depths in [3, 5) share their top byte, so that pass is a plain copy."""
+    from gsr_amd import _lib
+    L = _lib.load()
+    rng = np.random.default_rng(n)
+    keys = rng.uniform(3.0, 5.0, size=n).astype(np.float32).view(np.uint32) + 0
+    keys[: n // 4] = keys[0]  # ties
+    culled = rng.random(n) < frac_culled
+    keys[culled] = 0xFFFFFFFF
+    vals = np.arange(n, dtype=np.uint32)
+    k = torch.tensor(keys.view(np.int32), device="cuda")
+    v = torch.tensor(vals.view(np.int32), device="cuda")
+    scratch = torch.empty(int(L.gsr_test_sort_scratch_bytes(n)), dtype=torch.uint8, device="cuda")
+    _lib.check(L.gsr_test_radix_sort_pairs_sentinel(k.data_ptr(), v.data_ptr(), n, 32,
+                                                    scratch.data_ptr(),
+                                                    torch.cuda.current_stream().cuda_stream))
+    gk = k.cpu().numpy().view(np.uint32)
+    gv = v.cpu().numpy().view(np.uint32)
+    np.testing.assert_array_equal(np.sort(gv), vals)          # a permutation
+    np.testing.assert_array_equal(gk, keys[gv])                # pairs travel together
+    keep = ~culled[gv]
+    order = np.argsort(keys, kind="stable")
+    order = order[~culled[order]]
+    np.testing.assert_array_equal(gv[keep], order)
 
 
 @pytest.mark.parametrize("n", [1, 2047, 2049, 5_000_001])
@@ -226,3 +258,22 @@ def test_config3_full_size_forward_parity():
     """BASELINE config 3 scale (1M Gaussians, 1008x756): forward parity vs the oracle."""
     kw = scene(P=1_000_000, W=1008, H=756, seed=0, cam=1, mode="sh", feature="sh")
     compare(kw, with_bwd=False)
+
+
+def test_backward_twice_through_one_forward():
+    """retain_graph: a second backward through the same forward gives the same gradients (the
+    accumulators zeroed by the forward's preprocess are used once; the second backward clears
+    them itself)."""
+    from diff_gaussian_rasterization import GaussianRasterizer
+    kw = scene(P=3000, W=97, H=61, seed=4)
+    settings, inp = to_torch_call(kw)
+    color, depth, _, _, _ = GaussianRasterizer(settings)(
+        means3D=inp["means3D"], means2D=inp["means2D"], opacities=inp["opacities"],
+        shs=inp.get("shs"), colors_precomp=inp.get("colors_precomp"), scales=inp.get("scales"),
+        rotations=inp.get("rotations"), cov3D_precomp=inp.get("cov3D_precomp"))
+    g = torch.randn(color.shape, device="cuda", generator=torch.Generator("cuda").manual_seed(0))
+    loss = (color * g).sum() + depth.sum()
+    first = torch.autograd.grad(loss, [inp["means3D"], inp["opacities"]], retain_graph=True)
+    second = torch.autograd.grad(loss, [inp["means3D"], inp["opacities"]])
+    for a, b in zip(first, second):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-7)

@@ -70,3 +70,19 @@ def test_cpu_tensors_are_rejected_not_rasterized_on_cpu():
         GaussianRasterizer(s)(means3D=torch.zeros((1, 3)), means2D=torch.zeros((1, 3)),
                               opacities=torch.ones((1, 1)), colors_precomp=torch.ones((1, 3)),
                               scales=torch.ones((1, 3)), rotations=torch.tensor([[1., 0, 0, 0]]))
+
+
+def test_render_pkg_lazy_entries_behave_like_dict_items():
+    """render()'s fused-path result dict: "opacity" is computed on first access only, and the
+    dict still reports every key of the reference's dict."""
+    from gaussian_renderer import _RenderPkg
+    calls = []
+    pkg = _RenderPkg({"render": 1, "radii": 2}, {"opacity": lambda: calls.append(1) or 3})
+    assert "opacity" in pkg and len(pkg) == 3 and calls == []
+    assert pkg.get("render") == 1 and pkg.get("missing", 7) == 7
+    assert pkg["opacity"] == 3 and pkg["opacity"] == 3 and calls == [1]
+    pkg2 = _RenderPkg({"a": 0}, {"b": lambda: 5})
+    assert set(pkg2) == {"a", "b"} and dict(pkg2.items()) == {"a": 0, "b": 5}
+    import pytest
+    with pytest.raises(KeyError):
+        pkg2["nope"]
