@@ -95,12 +95,16 @@ def main():
     ap.add_argument("--no-stage-timing", action="store_true")
     ap.add_argument("--autograd-grads", action="store_true",
                     help="return per-view raw grads to autograd instead of adding them into .grad")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="views of a step issued round-robin on this many HIP streams "
+                         "(gsr_amd.pipeline.ViewPipeline; 1 = strictly sequential)")
     ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_r01.json"))
     args = ap.parse_args()
 
     from gsr_amd import _lib
     from gsr_amd.model import SplatModel
     from gsr_amd.parallel import GradAllReducer, init_from_env, shard_views
+    from gsr_amd.pipeline import ViewPipeline
     from gsr_amd.synthetic import make_cameras, make_gaussians, upstream_grads
     import diff_gaussian_rasterization as dgr
     from gaussian_renderer import render
@@ -121,6 +125,15 @@ def main():
     reducer = GradAllReducer(model.parameters()) if world > 1 else None
     pipe, opt = Pipe(), Opt()
     stats = {"R": [], "Pv": []}
+    views = ViewPipeline(dev, depth=max(1, args.streams))
+
+    def one_view(cam, record):
+        pkg = render(cam, model, pipe, bg, opt)
+        torch.autograd.backward([pkg["render"], pkg["depth"], pkg["feature"]],
+                                [dimg, ddep, dfeat])
+        if record:
+            stats["R"].append(dgr.LAST_STATS["num_rendered"])
+            stats["Pv"].append(int(pkg["visibility_filter"].sum()))
 
     def step(record=False):
         if reducer is not None:
@@ -128,13 +141,7 @@ def main():
         else:
             for p in model.parameters():
                 p.grad = None
-        for cam in my_cams:
-            pkg = render(cam, model, pipe, bg, opt)
-            torch.autograd.backward([pkg["render"], pkg["depth"], pkg["feature"]],
-                                    [dimg, ddep, dfeat])
-            if record:
-                stats["R"].append(dgr.LAST_STATS["num_rendered"])
-                stats["Pv"].append(int(pkg["visibility_filter"].sum()))
+        views.run(my_cams, lambda cam: one_view(cam, record))
         if reducer is not None:
             reducer.allreduce()
 
@@ -256,6 +263,7 @@ def main():
                        "raster_path": ("fused" if os.environ.get("GSR_FUSED", "1") != "0"
                                        else "unfused"),
                        "grad_mode": "autograd" if args.autograd_grads else "into_leaves",
+                       "view_streams": views.depth,
                        "num_rendered_mean": int(R), "visible_mean": int(Pv), "tiles": T},
             "roofline": roofline,
             "cpu_baseline": cpu,

@@ -388,7 +388,10 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
             d_rot = torch.empty(s_rot, **fopts)
             d_lf = torch.empty((P, 3), **fopts) if lf is not None else None
         L = _lib.load()
-        stream = torch.cuda.current_stream(dev).cuda_stream
+        cur = torch.cuda.current_stream(dev)
+        stream = cur.cuda_stream
+        if into_leaves:
+            _order_leaf_grads(dev, cur)
         with torch.cuda.device(dev):
             rc = L.gsr_rasterize_gaussians_fused_backward(
                 P, M, ctx.num_rendered, _ptr(bg), _ptr(m3), _ptr(radii), _ptr(dc), _ptr(rest),
@@ -401,6 +404,10 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
                 _ptr(d_sc), _ptr(d_rot), _ptr(d_lf), int(accumulate), stream,
                 int(bool(rs.debug)))
         _lib.check(rc)
+        if into_leaves:
+            ev = torch.cuda.Event()
+            ev.record(cur)
+            _LEAF_GRAD_EVENT[dev.index] = (ev, cur.stream_id)
         # forward inputs: means3D, means2D, features_dc, features_rest, opacity_raw, scaling_raw,
         # rotation_raw, language_feature, raster_settings
         if into_leaves:
@@ -409,6 +416,17 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
 
 
 _GRAD_INTO_LEAVES = None
+# device index -> (event after the last grad-into-leaves backward, id of the stream it ran on)
+_LEAF_GRAD_EVENT = {}
+
+
+def _order_leaf_grads(dev, stream):
+    """grad-into-leaves backwards read-modify-write the leaves' .grad without atomics, so two
+    of them issued on different streams (gsr_amd.pipeline.ViewPipeline) must not overlap: the
+    stream of this backward waits for the previous one when that ran on another stream."""
+    prev = _LEAF_GRAD_EVENT.get(dev.index)
+    if prev is not None and prev[1] != stream.stream_id:
+        stream.wait_event(prev[0])
 
 
 def grad_into_leaves(enable: Optional[bool] = None) -> bool:

@@ -1,0 +1,52 @@
+"""Multi-view step on several HIP streams (several views per GPU per
+optimizer step, gradients summed over the views).
+
+Within one step the views only read the Gaussians and add into the same .grad tensors, so view
+k+1's forward (preprocess, depth sort, scan, the instance-count read-back, binning and tile sort --
+mostly latency-bound launches that leave most CUs idle) can run while view k's backward blend (a
+full-chip, VALU-bound launch) is still executing.  ViewPipeline issues view i on stream i mod depth;
+the only cross-view dependency, the read-modify-write of the leaves' .grad by the fused backward's
+grad-into-leaves mode, is ordered by diff_gaussian_rasterization itself (one event per device,
+see ``_order_leaf_grads``), so any multi-stream caller gets correct accumulation, not only this
+helper.  The reference renders one view per step on the legacy default stream
+(train.py:64-236); with depth = 1 this helper is exactly that sequential loop.
+"""
+from __future__ import annotations
+
+from typing import Callable, Iterable, List, Optional, TypeVar
+
+import torch
+
+T = TypeVar("T")
+R = TypeVar("R")
+
+
+class ViewPipeline:
+    """Round-robin per-view work over ``depth`` streams: the caller's current stream plus
+    ``depth - 1`` side streams, joined back into the current stream at the end of run()."""
+
+    def __init__(self, device: Optional[torch.device] = None, depth: int = 2):
+        if depth < 1:
+            raise ValueError("depth must be >= 1")
+        self.device = torch.device(device) if device is not None else torch.device(
+            "cuda", torch.cuda.current_device())
+        self.depth = depth
+        self.side = [torch.cuda.Stream(device=self.device) for _ in range(depth - 1)]
+
+    def run(self, items: Iterable[T], fn: Callable[[T], R]) -> List[R]:
+        """Call fn(item) for every item, item i issued on stream i mod depth.  fn should do a
+        view's render + backward and return host values (or tensors it no longer needs on the
+        device): tensors created on a side stream and used after run() on the main stream need
+        Tensor.record_stream to be safe under the caching allocator."""
+        main = torch.cuda.current_stream(self.device)
+        streams = [main] + self.side
+        for s in self.side:
+            s.wait_stream(main)  # inputs prepared on the main stream (zeroed grads, cameras)
+        out = []
+        for i, it in enumerate(items):
+            s = streams[i % self.depth]
+            with torch.cuda.stream(s):
+                out.append(fn(it))
+        for s in self.side:
+            main.wait_stream(s)
+        return out
