@@ -84,11 +84,6 @@ __global__ __launch_bounds__(kSchedThreads) void tile_schedule_kernel(const uint
 #ifndef GSR_BWD_FAST_DIV
 #define GSR_BWD_FAST_DIV 1
 #endif
-// backward per-splat gradient sum: waves with at most this many contributing lanes add lane
-// values into LDS directly instead of the wave butterfly (0 = always the butterfly)
-#ifndef GSR_BWD_SPARSE_K
-#define GSR_BWD_SPARSE_K 0
-#endif
 // forward: 1 = blend weight alpha * T formed once per pair, 0 = col * alpha * T per channel
 #ifndef GSR_FWD_WEIGHT
 #define GSR_FWD_WEIGHT 1
@@ -288,9 +283,17 @@ __global__ __launch_bounds__(kThreads) void render_fwd_kernel(RenderArgs a) {
   }
 }
 
+// Two floats in one 64-bit register pair: gfx950's packed FP32 VALU (v_pk_mul_f32, v_pk_add_f32,
+// v_pk_fma_f32) does both halves in one issue slot.
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2 mk2(float x, float y) { return f2{x, y}; }
+__device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+
+// DPP move with bound_ctrl and full masks (every source lane of the patterns used here exists), in
+// the form the backend folds into the consuming v_add_f32 as a DPP operand
 template <int CTRL>
 __device__ __forceinline__ float dpp(float x) {
-  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), CTRL, 0xf, 0xf, false));
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xf, 0xf, true));
 }
 
 // Orientation of gfx950's v_permlane32_swap / v_permlane16_swap (which half of the pair keeps
@@ -309,40 +312,44 @@ __device__ __forceinline__ SwapOrient probe_swaps(int lane) {
   return o;
 }
 
-// Halving butterfly on VALU only: on entry every lane holds 16 partial values; on exit every
-// lane holds the full wave sum of ONE value, index k = 8*b5' + 4*b4' + 2*b3 + b2 (b = lane bits,
-// b5'/b4' corrected by the probed swap orientation), 4 lanes per value.  Steps: permlane32_swap
-// (pairs lane l with l^32, 8 values -> 8 adds), permlane16_swap (l^16, 4 adds), DPP row_mirror
-// (l^15 within a row), DPP row_half_mirror (l^7), quad_perm xor 2, xor 1.  The partner maps
-// {^15, ^7, ^2, ^1} are linearly independent over the low 4 lane bits, so every lane of the
-// 16-lane row is summed exactly once; no LDS traffic (the previous form used 17 ds_bpermute).
-__device__ __forceinline__ float wave_reduce16_dpp(float (&v)[16], int lane) {
+__device__ __forceinline__ f2 swap32_add(f2 p, f2 q) {
+  const auto rx = __builtin_amdgcn_permlane32_swap(__float_as_uint(p.x), __float_as_uint(q.x), false, false);
+  const auto ry = __builtin_amdgcn_permlane32_swap(__float_as_uint(p.y), __float_as_uint(q.y), false, false);
+  return mk2(__uint_as_float(rx[0]), __uint_as_float(ry[0])) +
+         mk2(__uint_as_float(rx[1]), __uint_as_float(ry[1]));
+}
+__device__ __forceinline__ f2 swap16_add(f2 p, f2 q) {
+  const auto rx = __builtin_amdgcn_permlane16_swap(__float_as_uint(p.x), __float_as_uint(q.x), false, false);
+  const auto ry = __builtin_amdgcn_permlane16_swap(__float_as_uint(p.y), __float_as_uint(q.y), false, false);
+  return mk2(__uint_as_float(rx[0]), __uint_as_float(ry[0])) +
+         mk2(__uint_as_float(rx[1]), __uint_as_float(ry[1]));
+}
+
+// Halving butterfly on VALU only: on entry every lane holds 16 partial values as 8 pairs
+// (v[i] = values 2i, 2i+1); on exit every lane holds the full wave sum of ONE value, index
+// k = 8*b5' + 4*b4' + 2*b3 + b2 (b = lane bits, b5'/b4' corrected by the probed swap
+// orientation), 4 lanes per value.  Steps: permlane32_swap (pairs lane l with l^32: values k and
+// k+8, 4 packed adds), permlane16_swap (l^16: k and k+4, 2 packed adds), DPP row_mirror (l^15
+// within a row: k and k+2, one packed add), DPP row_half_mirror (l^7), quad_perm xor 2, xor 1.
+// The partner maps {^15, ^7, ^2, ^1} are linearly independent over the low 4 lane bits, so every
+// lane of the 16-lane row is summed exactly once; no LDS traffic.
+__device__ __forceinline__ float wave_reduce16_dpp(f2 (&v)[8], int lane) {
 #pragma unroll
-  for (int i = 0; i < 8; i++) {
-    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[i]), __float_as_uint(v[i + 8]),
-                                                    false, false);
-    v[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
-  }
+  for (int i = 0; i < 4; i++) v[i] = swap32_add(v[i], v[i + 4]);
 #pragma unroll
-  for (int i = 0; i < 4; i++) {
-    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[i]), __float_as_uint(v[i + 4]),
-                                                    false, false);
-    v[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
-  }
+  for (int i = 0; i < 2; i++) v[i] = swap16_add(v[i], v[i + 2]);
+  f2 w;
   {
     const bool hi = lane & 8;
-#pragma unroll
-    for (int i = 0; i < 2; i++) {
-      const float send = hi ? v[i] : v[i + 2];
-      const float keep = hi ? v[i + 2] : v[i];
-      v[i] = keep + dpp<0x140>(send);  // row_mirror
-    }
+    const f2 send = hi ? v[0] : v[1];
+    const f2 keep = hi ? v[1] : v[0];
+    w = keep + mk2(dpp<0x140>(send.x), dpp<0x140>(send.y));  // row_mirror
   }
   float x;
   {
     const bool hi = lane & 4;
-    const float send = hi ? v[0] : v[1];
-    const float keep = hi ? v[1] : v[0];
+    const float send = hi ? w.x : w.y;
+    const float keep = hi ? w.y : w.x;
     x = keep + dpp<0x141>(send);  // row_half_mirror
   }
   x += dpp<0x4E>(x);  // quad_perm [2,3,0,1]
@@ -354,48 +361,6 @@ __device__ __forceinline__ int reduce16_slot(int lane, SwapOrient o) {
   const int b5 = ((lane >> 5) & 1) ^ (int)o.flip32;
   const int b4 = ((lane >> 4) & 1) ^ (int)o.flip16;
   return b5 * 8 + b4 * 4 + ((lane >> 3) & 1) * 2 + ((lane >> 2) & 1);
-}
-
-// Halving butterfly: on entry every lane holds 16 partial values; on exit lane l holds the wave
-// sum of value index ((l>>5)&1)*8 + ((l>>4)&1)*4 + ((l>>3)&1)*2 + ((l>>2)&1) (4 lanes each).
-__device__ __forceinline__ float wave_reduce16(float (&v)[16], int lane) {
-  {
-    const bool hi = lane & 32;
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-      const float send = hi ? v[i] : v[i + 8];
-      const float keep = hi ? v[i + 8] : v[i];
-      v[i] = keep + __shfl_xor(send, 32, 64);
-    }
-  }
-  {
-    const bool hi = lane & 16;
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-      const float send = hi ? v[i] : v[i + 4];
-      const float keep = hi ? v[i + 4] : v[i];
-      v[i] = keep + __shfl_xor(send, 16, 64);
-    }
-  }
-  {
-    const bool hi = lane & 8;
-#pragma unroll
-    for (int i = 0; i < 2; i++) {
-      const float send = hi ? v[i] : v[i + 2];
-      const float keep = hi ? v[i + 2] : v[i];
-      v[i] = keep + __shfl_xor(send, 8, 64);
-    }
-  }
-  float x;
-  {
-    const bool hi = lane & 4;
-    const float send = hi ? v[0] : v[1];
-    const float keep = hi ? v[1] : v[0];
-    x = keep + __shfl_xor(send, 4, 64);
-  }
-  x += __shfl_xor(x, 2, 64);
-  x += __shfl_xor(x, 1, 64);
-  return x;
 }
 
 template <bool EXTRA, bool FEAT, int GROUP>
@@ -461,6 +426,15 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
   //   acc_dot' = last_alpha * last_cdot + (1 - last_alpha) * acc_dot,  cdot = sum_c col_c dpix_c,
   //   dL_dalpha = cdot - acc_dot'
   // (the same recurrence on one scalar instead of NC channels; equal up to float rounding)
+  // upstream gradients as the pairs the packed math uses: A = (r, g), B = (b, depth),
+  // C = (f0, f1), D = (f2, alpha) -- absent channels are zero
+  const f2 dpA = mk2(dpix[0], dpix[1]);
+  const f2 dpB = mk2(dpix[2], NC > 3 ? dpix[3 % NC] : 0.f);
+  const f2 dpC = mk2(FEAT ? dpix[5 % NC] : 0.f, FEAT ? dpix[6 % NC] : 0.f);
+  const f2 dpD = mk2(FEAT ? dpix[7 % NC] : 0.f, NC > 3 ? dpix[4 % NC] : 0.f);
+  static_assert(kAccMx == 0 && kAccMy == 1 && kAccCa == 2 && kAccCb == 3 && kAccCc == 4 &&
+                kAccOp == 5 && kAccR == 6 && kAccG == 7 && kAccB == 8 && kAccDepth == 9 &&
+                kAccF0 == 10 && kAccF1 == 11 && kAccF2 == 12, "pair layout of the gradient row");
   float acc_dot = 0.0f, last_cdot = 0.0f;
   float last_alpha = 0.0f;
   const float ddelx_dx = (float)(0.5 * a.W);
@@ -529,9 +503,8 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
       const float4 r0 = s_r0[j];
       const float4 r1 = s_r1[j];
       const float4 r2 = s_r2[j];
-      const float dx = r0.x - pfx, dy = r0.y - pfy;
+      const f2 dxy = mk2(r0.x - pfx, r0.y - pfy);
 
-      float g[kAccFloats];
 #if GSR_BWD_FAST_DIV
       {
         // T / (1 - alpha) by v_rcp_f32 + one Newton correction on the exact residual (4 VALU
@@ -547,61 +520,56 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
       T = T / (1.f - alpha);
 #endif
       const float dchannel_dcolor = alpha * T;
-      float col[NC];
-      col[0] = r1.w; col[1] = r2.x; col[2] = r2.y;
-      if (NC > 3) { col[3 % NC] = r1.z; col[4 % NC] = 1.0f; }
-      if (FEAT) {
-        const float f2 = s_f2[j];
-        col[5 % NC] = r2.z; col[6 % NC] = r2.w; col[7 % NC] = f2;
-      }
-      float cdot = 0.0f;
-#pragma unroll
-      for (int c = 0; c < NC; c++) cdot += col[c] * dpix[c];
+      // cdot = sum_c col_c * dpix_c as packed FMAs over the record's natural pairs (gradient-only
+      // arithmetic: the forward-consistent quantities G, alpha, T above are computed unfused)
+      f2 c2 = mk2(r1.w, r2.x) * dpA;
+      if (NC > 3) c2 = fma2(mk2(r2.y, r1.z), dpB, c2);
+      else c2 = fma2(mk2(r2.y, 0.f), dpB, c2);
+      if (FEAT) c2 = fma2(mk2(r2.z, r2.w), dpC, c2);
+      if (NC > 3) c2 = fma2(mk2(FEAT ? s_f2[j] : 0.f, 1.0f), dpD, c2);
+      const float cdot = c2.x + c2.y;
       const float acc_new = last_alpha * last_cdot + (1.f - last_alpha) * acc_dot;
       float dL_dalpha = cdot - acc_new;
       acc_dot = contrib ? acc_new : acc_dot;
       last_cdot = contrib ? cdot : last_cdot;
       last_alpha = contrib ? alpha : last_alpha;
-      g[kAccR] = dchannel_dcolor * dpix[0];
-      g[kAccG] = dchannel_dcolor * dpix[1];
-      g[kAccB] = dchannel_dcolor * dpix[2];
-      g[kAccDepth] = NC > 3 ? dchannel_dcolor * dpix[3 % NC] : 0.0f;
-      g[kAccF0] = FEAT ? dchannel_dcolor * dpix[5 % NC] : 0.0f;
-      g[kAccF1] = FEAT ? dchannel_dcolor * dpix[6 % NC] : 0.0f;
-      g[kAccF2] = FEAT ? dchannel_dcolor * dpix[7 % NC] : 0.0f;
       dL_dalpha *= T;
       if (has_bg) dL_dalpha += (-T_final / (1.f - alpha)) * bg_dot;
-      const float dL_dG = r1.y * dL_dalpha;
-      const float gdx = G * dx;
-      const float gdy = G * dy;
-      const float dG_ddelx = -gdx * r0.z - gdy * r0.w;
-      const float dG_ddely = -gdy * r1.x - gdx * r0.w;
-      g[kAccMx] = dL_dG * dG_ddelx * ddelx_dx;
-      g[kAccMy] = dL_dG * dG_ddely * ddely_dy;
-      g[kAccCa] = -0.5f * gdx * dx * dL_dG;
-      g[kAccCb] = -0.5f * gdx * dy * dL_dG;
-      g[kAccCc] = -0.5f * gdy * dy * dL_dG;
-      g[kAccOp] = G * dL_dalpha;
-      g[kAccUsed] = 0.0f;
-      g[14] = 0.0f;
-      g[15] = 0.0f;
-#if GSR_BWD_SPARSE_K > 0
-      if (__popcll(cmask) <= GSR_BWD_SPARSE_K) {
-        // few contributing lanes: they add their values into the LDS row directly (LDS atomic
-        // pipe) instead of the ~45-instruction VALU butterfly of the whole wave
-        if (contrib) {
-#pragma unroll
-          for (int k = 0; k < kAccUsed; k++) atomicAdd(&s_acc[j][k], g[k]);
-        }
-        continue;
-      }
-#endif
+      // Per-pixel moments instead of the reference's per-pixel conic / mean2D terms: with
+      // u = G * dL/dalpha, dL/dG = opacity * dL/dalpha, and d = (dx, dy) (backward.cu:536-554)
+      //   dL/dmean2D.x = -(W/2) o (a sum u dx + b sum u dy),  dL/dmean2D.y = -(H/2) o (c sum u dy + b sum u dx)
+      //   dL/dconic.{x,y,w} = -1/2 o sum u {dx dx, dx dy, dy dy},   dL/dopacity = sum u
+      // The per-splat constants (a, b, c, o) are applied once per (splat, tile) at the flush.
+      const float uu = G * dL_dalpha;
+      f2 g[8];
+      g[0] = uu * dxy;                               // kAccMx, kAccMy   <- sum u dx, sum u dy
+      g[1] = (uu * dxy.x) * dxy;                     // kAccCa, kAccCb   <- sum u dx dx, sum u dx dy
+      g[2] = mk2((uu * dxy.y) * dxy.y, uu);          // kAccCc, kAccOp   <- sum u dy dy, sum u
+      g[3] = dchannel_dcolor * dpA;                  // kAccR, kAccG
+      g[4] = dchannel_dcolor * dpB;                  // kAccB, kAccDepth
+      g[5] = FEAT ? dchannel_dcolor * dpC : mk2(0.f, 0.f);          // kAccF0, kAccF1
+      g[6] = mk2(FEAT ? dchannel_dcolor * dpD.x : 0.f, 0.f);       // kAccF2, (13)
+      g[7] = mk2(0.f, 0.f);                                         // (14, 15)
       const float sum = wave_reduce16_dpp(g, lane);
       if ((lane & 3) == 0) {
         const int k = reduce16_slot(lane, swap_orient);
         if (sum != 0.0f) atomicAdd(&s_acc[j][k], sum);
       }
     }
+    }
+    __syncthreads();
+    // moments -> the reference's dL/dmean2D (NDC-scaled) and dL/dconic, once per (splat, tile)
+    if (threadIdx.x < cnt) {
+      const float4 r0 = s_r0[threadIdx.x];
+      const float4 r1 = s_r1[threadIdx.x];
+      float* row = s_acc[threadIdx.x];
+      const float sx = row[kAccMx], sy = row[kAccMy];
+      const float o = r1.y;
+      row[kAccMx] = -(o * (r0.z * sx + r0.w * sy)) * ddelx_dx;
+      row[kAccMy] = -(o * (r1.x * sy + r0.w * sx)) * ddely_dy;
+      row[kAccCa] = (-0.5f * o) * row[kAccCa];
+      row[kAccCb] = (-0.5f * o) * row[kAccCb];
+      row[kAccCc] = (-0.5f * o) * row[kAccCc];
     }
     __syncthreads();
     // flush: lane l of wave-instruction `it` handles splat (it*16 + tid/16), slot tid%16
