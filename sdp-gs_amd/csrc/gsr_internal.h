@@ -61,14 +61,17 @@ inline int sort_passes(int bits) { return (bits + 7) / 8; }
 constexpr int kSortMaxPasses = 4;
 // u64 look-back status words: one per (pass, partition, digit)
 inline size_t sort_status_len(size_t n) { return (size_t)kSortMaxPasses * sort_blocks(n) * 256; }
-// u32 aux words: digit totals [kSortMaxPasses][256], partition tickets [kSortMaxPasses][8],
-// digit-presence masks [kSortMaxPasses][8] (256 bits per pass over the keys != kSortSentinel),
-// error flag
-constexpr size_t kSortAuxTotals = 0, kSortAuxTickets = kSortMaxPasses * 256,
-                 kSortAuxMask = kSortAuxTickets + 8 * kSortMaxPasses,
-                 kSortAuxErr = kSortAuxMask + 8 * kSortMaxPasses, kSortAuxLen = kSortAuxErr + 4;
+// u32 aux words: digit totals as kSortTotShards partial copies [shard][kSortMaxPasses][256] (the
+// totals kernel's workgroups add into shard blockIdx % kSortTotShards: same-line device-scope
+// atomics serialise at the memory side, so one shared copy made ~250-720 workgroups queue on the
+// same 8 lines), sentinel-key counts [shard], partition tickets [kSortMaxPasses][8], error flag
+constexpr int kSortTotShards = 16;
+constexpr size_t kSortAuxTotals = 0,
+                 kSortAuxSent = kSortAuxTotals + (size_t)kSortTotShards * kSortMaxPasses * 256,
+                 kSortAuxTickets = kSortAuxSent + kSortTotShards,
+                 kSortAuxErr = kSortAuxTickets + 8 * kSortMaxPasses, kSortAuxLen = kSortAuxErr + 4;
 // Key whose position in the sorted output does not matter (culled Gaussians: no tiles): it is
-// left out of the digit-presence masks, so a pass whose digit is constant over every other key
+// left out of the count of digits present, so a pass whose digit is constant over every other key
 // is a plain copy (see radix_onesweep_kernel).
 constexpr uint32_t kSortSentinel = 0xffffffffu;
 

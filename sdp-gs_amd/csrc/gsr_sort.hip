@@ -188,7 +188,7 @@ constexpr int kTotTile = kThreads * kTotKPT;
 __global__ __launch_bounds__(kThreads) void radix_totals_kernel(const uint32_t* __restrict__ keys,
                                                                 size_t n, int bits,
                                                                 uint32_t* __restrict__ totals,
-                                                                uint32_t* __restrict__ present,
+                                                                uint32_t* __restrict__ nsent_out,
                                                                 int skip_sentinel) {
   __shared__ uint32_t cnt[kSortMaxPasses][256];
   __shared__ uint32_t nsent;  // sentinel keys of this workgroup (all digits 0xff)
@@ -229,19 +229,14 @@ __global__ __launch_bounds__(kThreads) void radix_totals_kernel(const uint32_t* 
     }
   }
   __syncthreads();
-  const uint32_t ns = nsent;
-  const int lane = (int)(threadIdx.x & 63);
+  // this workgroup's partial copy of the totals (see kSortTotShards)
+  const uint32_t shard = blockIdx.x % (uint32_t)kSortTotShards;
+  uint32_t* tot = totals + (size_t)shard * kSortMaxPasses * 256;
   for (int p = 0; p < passes; p++) {
     const uint32_t c = cnt[p][threadIdx.x];
-    if (c) atomicAdd(&totals[p * 256 + threadIdx.x], c);
-    // digit presence over the non-sentinel keys (a sentinel has digit 0xff in every pass)
-    const uint32_t real = c - (threadIdx.x == 255u ? ns : 0u);
-    const uint64_t m = __ballot(real != 0u);
-    if (m && lane < 2) {
-      const uint32_t word = (uint32_t)(lane ? (m >> 32) : m);
-      if (word) atomicOr(&present[p * 8 + 2 * (threadIdx.x >> 6) + lane], word);
-    }
+    if (c) atomicAdd(&tot[p * 256 + threadIdx.x], c);
   }
+  if (threadIdx.x == 0 && nsent) atomicAdd(&nsent_out[shard], nsent);
 }
 
 __device__ __forceinline__ uint64_t status_load(const uint64_t* p) {
@@ -254,7 +249,7 @@ __device__ __forceinline__ void status_store(uint64_t* p, uint64_t v) {
 template <int NT>
 __global__ __launch_bounds__(NT) void radix_onesweep_kernel(
     const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin, size_t n, int shift,
-    int bits, const uint32_t* __restrict__ totals, const uint32_t* __restrict__ present,
+    int bits, const uint32_t* __restrict__ totals, const uint32_t* __restrict__ nsent_sh,
     uint32_t* __restrict__ ticket, uint64_t* __restrict__ status, uint32_t* __restrict__ err,
     uint32_t* __restrict__ kout, uint32_t* __restrict__ vout) {
   constexpr int kSortWaves = NT / 64, kSortThreads = NT;
@@ -276,13 +271,27 @@ __global__ __launch_bounds__(NT) void radix_onesweep_kernel(
 #define SORT_TRACE(k)
 #endif
   SORT_TRACE(0)
+  // thread t < 256 <-> digit t: this pass's digit total, summed over the partial copies
+  const bool dig = t < 256;
+  const int dt = dig ? t : 0;
+  uint32_t dtotal = 0;
+  if (dig) {
+#pragma unroll
+    for (int sh = 0; sh < kSortTotShards; sh++) dtotal += totals[(size_t)sh * kSortMaxPasses * 256 + t];
+  }
   {
     // Every non-sentinel key has the same digit in this pass: the stable sort by it is the
     // identity on those keys, and sentinel keys may land anywhere -- the pass is a copy (no
-    // ranking, no look-back).  Workgroup-uniform (the masks are final before the launch).
-    uint32_t ndig = 0;
+    // ranking, no look-back).  Workgroup-uniform (the totals are final before the launch).
+    uint32_t real = dtotal;
+    if (t == 255 && nsent_sh) {
 #pragma unroll
-    for (int w = 0; w < 8; w++) ndig += (uint32_t)__popc(present[w]);
+      for (int sh = 0; sh < kSortTotShards; sh++) real -= nsent_sh[sh];
+    }
+    const uint64_t b = __ballot(dig && real != 0u);
+    if (lane == 0 && wid < 4) s_scan[wid] = (uint32_t)__popcll(b);
+    __syncthreads();
+    const uint32_t ndig = s_scan[0] + s_scan[1] + s_scan[2] + s_scan[3];
     if (ndig <= 1u) {
       const size_t b0 = (size_t)blockIdx.x * kSortTile;
       const size_t e0 = min(n, b0 + (size_t)kSortTile);
@@ -330,9 +339,7 @@ __global__ __launch_bounds__(NT) void radix_onesweep_kernel(
   }
   __syncthreads();
   SORT_TRACE(1)
-  // thread t < 256 <-> digit t (the other lanes join the workgroup scans with zeros)
-  const bool dig = t < 256;
-  const int dt = dig ? t : 0;
+  // (the lanes t >= 256 join the workgroup scans with zeros)
   uint32_t h = 0;
   if (dig)
 #pragma unroll
@@ -341,7 +348,7 @@ __global__ __launch_bounds__(NT) void radix_onesweep_kernel(
   if (dig) status_store(my, (part == 0 ? kStIncl : kStAgg) | (uint64_t)h);
   uint32_t total_n;
   const uint32_t lstart = block_excl_scan<kSortWaves>(dig ? h : 0u, s_scan, total_n);
-  const uint32_t dbase = block_excl_scan<kSortWaves>(dig ? totals[t] : 0u, s_scan, total_n);
+  const uint32_t dbase = block_excl_scan<kSortWaves>(dig ? dtotal : 0u, s_scan, total_n);
   if (dig) {
     uint32_t run = lstart;
 #pragma unroll
@@ -505,7 +512,7 @@ hipError_t radix_sort_pairs(uint32_t* ka, uint32_t* va, uint32_t* kb, uint32_t* 
   hipLaunchKernelGGL(radix_totals_kernel,
                      dim3((unsigned)(tot_tiles < GSR_TOTALS_GROUPS ? tot_tiles : GSR_TOTALS_GROUPS)),
                      dim3(kThreads), 0, s, ka, n, bits, scratch.aux + kSortAuxTotals,
-                     scratch.aux + kSortAuxMask, sentinel_anywhere ? 1 : 0);
+                     scratch.aux + kSortAuxSent, sentinel_anywhere ? 1 : 0);
   uint32_t *kin = ka, *vin = va, *kout = kb, *vout = vb;
   bool in_b = false;
   for (int p = 0; p < passes; p++) {
@@ -515,7 +522,8 @@ hipError_t radix_sort_pairs(uint32_t* ka, uint32_t* va, uint32_t* kb, uint32_t* 
 #define GSR_ONESWEEP(NT)                                                                          \
   hipLaunchKernelGGL(radix_onesweep_kernel<NT>, dim3(nb), dim3(NT), 0, s, kin, vin, n, shift,    \
                      dbits, scratch.aux + kSortAuxTotals + 256 * p,                              \
-                     scratch.aux + kSortAuxMask + 8 * p, scratch.aux + kSortAuxTickets + 8 * p,  \
+                     sentinel_anywhere ? scratch.aux + kSortAuxSent : nullptr,                   \
+                     scratch.aux + kSortAuxTickets + 8 * p,                                      \
                      scratch.status + (size_t)p * nb * 256, \
                      scratch.aux + kSortAuxErr, kout, vout)
     if (nt == 1024) GSR_ONESWEEP(1024);
