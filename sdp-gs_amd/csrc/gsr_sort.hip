@@ -247,7 +247,7 @@ __device__ __forceinline__ void status_store(uint64_t* p, uint64_t v) {
 }
 
 template <int NT>
-__global__ __launch_bounds__(NT) void radix_onesweep_kernel(
+__global__ __launch_bounds__(NT, NT == 1024 ? 8 : (NT == 512 ? 6 : 1)) void radix_onesweep_kernel(
     const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin, size_t n, int shift,
     int bits, const uint32_t* __restrict__ totals, const uint32_t* __restrict__ nsent_sh,
     uint32_t* __restrict__ ticket, uint64_t* __restrict__ status, uint32_t* __restrict__ err,
@@ -358,6 +358,19 @@ __global__ __launch_bounds__(NT) void radix_onesweep_kernel(
       run += c;
     }
   }
+  __syncthreads();
+  // keys to their digit-ordered slots in LDS now, before the look-back: the local order does not
+  // depend on the global offsets, and the look-back then runs with the keys out of registers
+  // (75 VGPRs at 512 lanes: 3 workgroups per CU, so 768 partitions are resident at once)
+#pragma unroll
+  for (int r = 0; r < kKeysPerThread; r++) {
+    if (wbase + (size_t)r * 64 + lane < n) {
+      const uint32_t d = (key[r] >> shift) & mask;
+      const uint32_t pos = s_cnt[wid][d] + rk[r];
+      s_k[pos] = key[r];
+      s_v[pos] = val[r];
+    }
+  }
   SORT_TRACE(2)
   uint32_t excl = 0;
   if (dig && part > 0) {
@@ -397,17 +410,7 @@ __global__ __launch_bounds__(NT) void radix_onesweep_kernel(
     status_store(my, kStIncl | (uint64_t)(excl + h));
   }
   if (dig) s_gofs[t] = dbase + excl - lstart;
-  __syncthreads();
   SORT_TRACE(3)
-#pragma unroll
-  for (int r = 0; r < kKeysPerThread; r++) {
-    if (wbase + (size_t)r * 64 + lane < n) {
-      const uint32_t d = (key[r] >> shift) & mask;
-      const uint32_t pos = s_cnt[wid][d] + rk[r];
-      s_k[pos] = key[r];
-      s_v[pos] = val[r];
-    }
-  }
   __syncthreads();
   SORT_TRACE(4)
   const uint32_t nvalid = (uint32_t)min((size_t)kSortTile, n - base);
