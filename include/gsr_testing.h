@@ -30,6 +30,9 @@ size_t gsr_test_scan_scratch_bytes(size_t n);
 int gsr_test_scan(const uint32_t* in, uint32_t* out, size_t n, int inclusive, void* scratch,
                   void* stream);
 
+/* ref[i] = expf(x[i]) (OCML), fast[i] = the blends' range-check-free exp (device pointers). */
+int gsr_test_expf_pair(const float* x, float* ref, float* fast, size_t n, void* stream);
+
 /* Stage timing with hipEvents recorded on the caller's stream around the kernels of the forward
  * and backward (used by bench.py for the per-kernel roofline).  Off by default; each enabled
  * stage launch is bracketed by two events (a few microseconds per stage and view, so bench.py

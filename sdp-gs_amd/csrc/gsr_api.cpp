@@ -640,6 +640,15 @@ int gsr_test_scan(const uint32_t* in, uint32_t* out, size_t n, int inclusive, vo
   return GSR_OK;
 }
 
+int gsr_test_expf_pair(const float* x, float* ref, float* fast, size_t n, void* stream_ptr) {
+  g_err.clear();
+  hipStream_t stream = (hipStream_t)stream_ptr;
+  const int debug = 0;
+  if (n && (!x || !ref || !fast)) return fail(GSR_ERR_ARGUMENT, "null pointer");
+  GSR_CHECK(launch_expf_pair(x, ref, fast, n, stream));
+  return GSR_OK;
+}
+
 void gsr_profile_enable(int stage_mask) { prof().mask.store((uint32_t)stage_mask); }
 
 int gsr_profile_collect(double* ms, long long* calls) {

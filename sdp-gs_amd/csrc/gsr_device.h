@@ -131,6 +131,25 @@ __device__ __forceinline__ float4 normalize_quat_backward(float4 r, float4 go) {
                      go.w / d - k * r.w);
 }
 // torch.sigmoid on float: 1 / (1 + exp(-x)); backward: go * (1 - y) * y
+// expf for the blends' Gaussian weight G = exp(power): OCML's expf sequence (x*log2(e) split into
+// a rounded product and its error term, round-to-nearest-even exponent, v_exp_f32 of the
+// fraction, ldexp) with one range select (x < -104 -> 0; NaN passes through) instead of its two.
+// For every x >= -103.2 it returns OCML's value bit for bit (tested on the GPU,
+// tests/test_gpu_parity.py); in [-104, -103.2) it may give the smallest denormal where OCML gives
+// 0.  Above 88.7 it still returns inf for the range the product stays exact in; the blends skip
+// power > 0 and use G only through alpha = min(0.99, o * G) >= 1/255, so no decision and no
+// output changes.  (Without the select, |x| > 2^23 / log2(e) can leave a positive fraction and
+// return inf.)
+__device__ __forceinline__ float blend_expf(float x) {
+  const float kLog2e = 0x1.715476p+0f, kLog2eLo = 0x1.4ae0bep-26f;
+  const float ph = x * kLog2e;
+  float pl = __builtin_fmaf(x, kLog2e, -ph);
+  pl = __builtin_fmaf(x, kLog2eLo, pl);
+  const float n = __builtin_rintf(ph);
+  const float f = (ph - n) + pl;
+  const float r = __builtin_amdgcn_ldexpf(__builtin_amdgcn_exp2f(f), (int)n);
+  return x < -104.0f ? 0.0f : r;
+}
 __device__ __forceinline__ float sigmoid_f(float x) { return 1.0f / (1.0f + expf(-x)); }
 
 // ---- conservative splat / pixel-rectangle culling ----------------------------------------------

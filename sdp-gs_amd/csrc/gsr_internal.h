@@ -184,6 +184,8 @@ struct PreArgs {
   int acc_zero;
 };
 hipError_t launch_preprocess(const PreArgs& a, hipStream_t s);
+// test hook: ref = OCML expf(x), fast = blend_expf(x) (gsr_device.h)
+hipError_t launch_expf_pair(const float* x, float* ref, float* fast, size_t n, hipStream_t s);
 hipError_t launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present,
                                hipStream_t s);
 

@@ -210,7 +210,7 @@ __global__ __launch_bounds__(kThreads) void render_fwd_kernel(RenderArgs a) {
         const float power = -0.5f * (r0.z * dx * dx + r1v[u].x * dy * dy) - r0.w * dx * dy;
         // entries past the list end get power = +1 and are skipped like any power > 0 pair
         pw[u] = (k + u < nlist) ? power : 1.0f;
-        al[u] = fminf(0.99f, r1v[u].y * expf(pw[u]));
+        al[u] = fminf(0.99f, r1v[u].y * blend_expf(pw[u]));
       }
 #pragma unroll
       for (int u = 0; u < 4; u++) {
@@ -483,7 +483,7 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
       const float4 r1 = s_r1[j];
       const float dx = r0.x - pfx, dy = r0.y - pfy;
       const float power = -0.5f * (r0.z * dx * dx + r1.x * dy * dy) - r0.w * dx * dy;
-      Gv[u] = expf(power);
+      Gv[u] = blend_expf(power);
       av[u] = fminf(0.99f, r1.y * Gv[u]);
       cv[u] = (k0 + u < nlist) && rel < last_contributor && !(power > 0.0f) &&
               !(av[u] < 1.0f / 255.0f);
@@ -588,7 +588,23 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
   }
 }
 
+__global__ void expf_pair_kernel(const float* __restrict__ x, float* __restrict__ ref,
+                                 float* __restrict__ fast, size_t n) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    ref[i] = expf(x[i]);
+    fast[i] = blend_expf(x[i]);
+  }
+}
+
 }  // namespace
+
+hipError_t launch_expf_pair(const float* x, float* ref, float* fast, size_t n, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(expf_pair_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, ref,
+                     fast, n);
+  return hipGetLastError();
+}
 
 hipError_t launch_render_forward(const RenderArgs& a, hipStream_t s) {
   const uint32_t ntiles = a.gx * a.gy;

@@ -17,7 +17,10 @@ namespace gsr {
 // same way (ACC: read-add-write).  A vector spans at most two rows (w >= 3); vectors whose rows
 // are all culled are skipped in ACC mode.
 constexpr int kShMaxFloats = 48;  // 16 coefficients x 3 per Gaussian (M <= 16, checked by the API)
-constexpr int kStageBatch = 4;
+#ifndef GSR_STAGE_BATCH
+#define GSR_STAGE_BATCH 4
+#endif
+constexpr int kStageBatch = GSR_STAGE_BATCH;
 
 struct ShPlane {
   const float* src;  // global input plane (row-major [P, w])

@@ -161,6 +161,8 @@ def load():
         L.gsr_test_scan_scratch_bytes.argtypes = [_sz]
         L.gsr_test_scan.restype = _i
         L.gsr_test_scan.argtypes = [_p, _p, _sz, _i, _p, _p]
+        L.gsr_test_expf_pair.restype = _i
+        L.gsr_test_expf_pair.argtypes = [_p, _p, _p, _sz, _p]
         L.gsr_profile_enable.restype = None
         L.gsr_profile_enable.argtypes = [_i]
         L.gsr_profile_collect.restype = _i

@@ -248,6 +248,44 @@ def test_scan(n):
         np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), ref)
 
 
+def test_blend_expf_matches_ocml_expf():
+    """The blends' exp with one range select instead of OCML's two (gsr_device.h blend_expf) equals
+    expf on [-103.2, 88.7] (the alpha-relevant range [-6, 0] by a dense sweep of bit patterns,
+    every float around the alpha cut, the rest by a 2^24-point sweep) and underflows to at most
+    a denormal below it (never an alpha >= 1/255)."""
+    from gsr_amd import _lib
+    L = _lib.load()
+    lo = np.float32(-6.0)
+    # [-6, -2^-20] by bit pattern (every 5th float: 38M points) plus every float around the
+    # alpha cut ln(1/255) = -5.54 ([-5.6, -5.5])
+    a = np.arange(np.float32(-2.0 ** -20).view(np.uint32), lo.view(np.uint32) + 1, 5, dtype=np.uint32)
+    c = np.arange(np.float32(-5.5).view(np.uint32), np.float32(-5.6).view(np.uint32) + 1,
+                  dtype=np.uint32)
+    dense = np.concatenate([a, c]).view(np.float32)
+    sweep = np.linspace(-103.2, 88.7, 1 << 24, dtype=np.float64).astype(np.float32)
+    tiny = np.arange(0, np.float32(2.0 ** -20).view(np.uint32), 97, dtype=np.uint32).view(np.float32)
+    xs = np.concatenate([dense, sweep, tiny, -tiny]).astype(np.float32)
+    x = torch.tensor(xs, device="cuda")
+    ref, fast = torch.empty_like(x), torch.empty_like(x)
+    _lib.check(L.gsr_test_expf_pair(x.data_ptr(), ref.data_ptr(), fast.data_ptr(), x.numel(),
+                                    torch.cuda.current_stream().cuda_stream))
+    r = ref.cpu().numpy().view(np.uint32)
+    f = fast.cpu().numpy().view(np.uint32)
+    bad = np.nonzero(r != f)[0]
+    assert bad.size == 0, (xs[bad[:5]], r[bad[:5]], f[bad[:5]])
+    # below: at most the smallest denormals in [-104, -103.2), exactly 0 further down (also for
+    # -inf and |x| beyond 2^23 / log2(e)), NaN stays NaN
+    low = np.concatenate([np.linspace(-104.5, -103.2, 4096, dtype=np.float32),
+                          -np.logspace(2.1, 38, 4096, dtype=np.float64).astype(np.float32),
+                          np.array([-np.inf, np.nan], np.float32)])
+    xl = torch.tensor(low, device="cuda")
+    _lib.check(L.gsr_test_expf_pair(xl.data_ptr(), ref.data_ptr(), fast.data_ptr(), xl.numel(),
+                                    torch.cuda.current_stream().cuda_stream))
+    fl = fast[:xl.numel()].cpu().numpy()
+    assert np.all(fl[:-1] <= np.float32(2.0 ** -148)) and np.all(fl[:-1] >= 0)
+    assert np.all(fl[(low < -104.0)] == 0) and np.isnan(fl[-1])
+
+
 @pytest.mark.parametrize("P,W,H", [(100_000, 800, 800)])
 def test_config2_full_size_parity(P, W, H):
     """BASELINE config 2 at full size (100k Gaussians, 800x800, SH degree 3), fwd + bwd."""
