@@ -55,12 +55,13 @@ class Opt:
     include_feature = True
 
 
-def algorithmic_bytes(stage, P, Pv, R, T, HW, D=3, C=8, tile_passes=2, acc=True):
+def algorithmic_bytes(stage, P, Pv, R, T, HW, D=3, C=8, tile_passes=2, acc=True, defer_sh=False):
     """Bytes each stage must move per launch.
     P Gaussians, Pv visible, R instances, T tiles, HW pixels, C blended channels (rgb, depth,
-    alpha, feature x3), acc: the backward adds into existing gradients (read + write)."""
+    alpha, feature x3), acc: the backward adds into existing gradients (read + write),
+    defer_sh: the SH gradients are replaced by a stored 12-B dL/dRGB (flushed once per step)."""
     sh = 12 * (D + 1) ** 2
-    grads = 12 + 12 + 4 + 12 + 16 + 12 + sh  # means2D, means3D, opacity, scale, rot, lang, SH
+    grads = 12 + 12 + 4 + 12 + 16 + 12 + (0 if defer_sh else sh)  # means2D/3D, op, scale, rot, lang, SH
     return {
         # means (all); scale, rot, opacity, SH, language (visible); radii/tiles/key/value (all);
         # 64-B splat record + clamp bits (visible)
@@ -79,7 +80,7 @@ def algorithmic_bytes(stage, P, Pv, R, T, HW, D=3, C=8, tile_passes=2, acc=True)
         "render_bwd": R * (4 + 64) + T * 12 + HW * (4 * C + 8) + Pv * 64,
         # accumulator row + per-Gaussian inputs (visible), radii (all), gradients (RMW when acc)
         "preprocess_bwd": Pv * (64 + 12 + 12 + 16 + 4 + sh + 12 + 1) + P * 4
-                          + ((2 * Pv) if acc else P) * grads,
+                          + ((2 * Pv) if acc else P) * grads + (P * 12 if defer_sh else 0),
     }[stage]
 
 
@@ -95,9 +96,12 @@ def main():
     ap.add_argument("--no-stage-timing", action="store_true")
     ap.add_argument("--autograd-grads", action="store_true",
                     help="return per-view raw grads to autograd instead of adding them into .grad")
-    ap.add_argument("--streams", type=int, default=2,
+    ap.add_argument("--streams", type=int, default=3,
                     help="views of a step issued round-robin on this many HIP streams "
                          "(gsr_amd.pipeline.ViewPipeline; 1 = strictly sequential)")
+    ap.add_argument("--no-defer-sh", action="store_true",
+                    help="write the SH gradients in every view's backward instead of one flush "
+                         "per step (diff_gaussian_rasterization.ShGradDeferral)")
     ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_r01.json"))
     args = ap.parse_args()
 
@@ -125,7 +129,8 @@ def main():
     reducer = GradAllReducer(model.parameters()) if world > 1 else None
     pipe, opt = Pipe(), Opt()
     stats = {"R": [], "Pv": []}
-    views = ViewPipeline(dev, depth=max(1, args.streams))
+    defer_sh = not args.no_defer_sh and not args.autograd_grads
+    views = ViewPipeline(dev, depth=max(1, args.streams), defer_sh=defer_sh)
 
     def one_view(cam, record):
         pkg = render(cam, model, pipe, bg, opt)
@@ -150,7 +155,10 @@ def main():
     step(record=True)  # one recorded step for the per-view statistics (not timed)
     timer = _lib.StageTimer()
     # Per-stage table from one fully instrumented, untimed step (events around every stage cost
-    # ~7% of a view); inside the timed region only the dominant stage is bracketed by events.
+    # ~7% of a view).  The headline value comes from a clean timed region (no events: with the
+    # views on several streams even the dominant kernel's two events per view perturb the
+    # overlap); the dominant kernel's launch duration then comes from a second timed region of the
+    # same K steps with only that stage bracketed by events.
     all_stages = {}
     dom_stage = None
     if not args.no_stage_timing:
@@ -162,27 +170,32 @@ def main():
         busy = {n: ms for n, (ms, c) in all_stages.items() if c}
         dom_stage = max(busy, key=busy.get) if busy else None
         timer.reset()
-        if dom_stage is not None:
-            timer.enable(True, stages=[dom_stage])
 
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    timer.enable(False)
+    def timed_region():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el
+
+    elapsed = timed_region()
     stages = dict(all_stages)
+    dom_elapsed = None
     if dom_stage is not None:
-        stages[dom_stage] = timer.collect()[dom_stage]  # measured over the timed region
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        timer.enable(True, stages=[dom_stage])
+        dom_elapsed = timed_region()
+        timer.enable(False)
+        stages[dom_stage] = timer.collect()[dom_stage]  # measured over the second timed region
 
     total_views = args.steps * n_views
     value = total_views / elapsed
@@ -197,7 +210,8 @@ def main():
         if calls == 0:
             continue
         avg_ms = ms / calls
-        b = algorithmic_bytes(name, P, Pv, R, T, HW, D=deg, acc=not args.autograd_grads)
+        b = algorithmic_bytes(name, P, Pv, R, T, HW, D=deg, acc=not args.autograd_grads,
+                              defer_sh=defer_sh)
         k = {"avg_ms": round(avg_ms, 4), "calls": int(calls), "bytes": int(b),
              "gbs": round(b / (avg_ms * 1e-3) / 1e9, 1)}
         if name in ("render_fwd", "render_bwd"):
@@ -220,7 +234,8 @@ def main():
             pass
         roofline = {"kernel": dom, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                    "algorithmic_bytes": kd["bytes"], "avg_ms": kd["avg_ms"]}
+                    "algorithmic_bytes": kd["bytes"], "avg_ms": kd["avg_ms"],
+                    "timed_region_views_per_s": round(args.steps * n_views / dom_elapsed, 3)}
         try:
             with open(args.pmc_file) as fh:
                 pmc = json.load(fh)
@@ -264,6 +279,7 @@ def main():
                                        else "unfused"),
                        "grad_mode": "autograd" if args.autograd_grads else "into_leaves",
                        "view_streams": views.depth,
+                       "sh_grads": "deferred (one flush per step)" if defer_sh else "per view",
                        "num_rendered_mean": int(R), "visible_mean": int(Pv), "tiles": T},
             "roofline": roofline,
             "cpu_baseline": cpu,

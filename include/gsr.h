@@ -147,6 +147,38 @@ int gsr_rasterize_gaussians_fused_backward(
     float* dL_dlanguage_feature, int accumulate,
     void* stream, int debug);
 
+/* Deferred SH gradients for multi-view steps (gsr_amd/pipeline.py; no reference counterpart: the
+ * reference steps after every view).  Same as gsr_rasterize_gaussians_fused_backward, but when
+ * dL_dcolor_sh != NULL the SH gradients are NOT written (dL_dfeatures_dc / _rest may be NULL);
+ * instead the clamp-masked colour gradient dL/dRGB of every Gaussian ([P,3], zeros when culled)
+ * is stored there.  The SH gradient is basis(dir) x dL/dRGB (backward.cu:20-139), so
+ * gsr_sh_grad_flush forms it for all deferred views of a step in one pass over the SH rows. */
+int gsr_rasterize_gaussians_fused_backward_deferred(
+    int P, int M, int R,
+    const float* background, const float* means3D, const int* radii,
+    const float* features_dc, const float* features_rest, const float* opacity_raw,
+    const float* scaling_raw, const float* rotation_raw, float scale_modifier,
+    const float* viewmatrix, const float* projmatrix, float tan_fovx, float tan_fovy,
+    int image_height, int image_width,
+    const float* dL_dout_color, const float* dL_dout_depth, const float* dL_dout_alpha,
+    const float* dL_dout_feature,
+    int degree, const float* campos,
+    const float* language_feature, const float* confidence, int include_feature,
+    void* geom_buffer, void* binning_buffer, void* image_buffer,
+    float* dL_dmeans2D, float* dL_dmeans3D, float* dL_dfeatures_dc, float* dL_dfeatures_rest,
+    float* dL_dopacity_raw, float* dL_dscaling_raw, float* dL_drotation_raw,
+    float* dL_dlanguage_feature, float* dL_dcolor_sh, int accumulate,
+    void* stream, int debug);
+
+/* dL/dfeatures_dc [P,1,3] and dL/dfeatures_rest [P,M-1,3] of nviews deferred views:
+ * sum_v basis(normalize(means3D - campos[v])) x dL_dcolor_sh[v], coefficients above `degree`
+ * zero; stored (accumulate = 0) or added (accumulate = 1).  campos / dL_dcolor_sh: HOST arrays
+ * of nviews DEVICE pointers ([3] and [P,3]).  Views are summed in order in registers. */
+int gsr_sh_grad_flush(int P, int M, int degree, const float* means3D, int nviews,
+                      const float* const* campos, const float* const* dL_dcolor_sh,
+                      float* dL_dfeatures_dc, float* dL_dfeatures_rest, int accumulate,
+                      void* stream);
+
 /* Replaces _C.mark_visible -> markVisible (rasterize_points.cu:198-217) -> checkFrustum
  * (rasterizer_impl.cu:54-66): present[i] = view-space z > 0.2 (bool as uint8). */
 int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,

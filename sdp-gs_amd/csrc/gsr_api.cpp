@@ -450,12 +450,15 @@ static int backward_impl(
     float* dL_dcolors, float* dL_dopacity, float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh,
     float* dL_dscales, float* dL_drotations, float* dL_dsh_language, float* dL_dlanguage_feature,
     void* stream_ptr, int debug, int fused, const float* sh_dc, const float* sh_rest,
-    const float* opacity_raw, float* dL_dsh_rest, int accumulate) {
+    const float* opacity_raw, float* dL_dsh_rest, int accumulate, float* dRGB_sh = nullptr) {
   g_err.clear();
   if (fused) {
-    if (!sh_dc || (M > 1 && (!sh_rest || !dL_dsh_rest)) || !scales || !rotations || !opacity_raw)
+    if (!sh_dc || (M > 1 && !sh_rest) || (M > 1 && !dL_dsh_rest && !dRGB_sh) || !scales ||
+        !rotations || !opacity_raw)
       return fail(GSR_ERR_ARGUMENT, "fused backward needs the raw parameters and their grads");
     sh = sh_dc;
+  } else if (dRGB_sh) {
+    return fail(GSR_ERR_ARGUMENT, "deferred SH gradients are a fused-path mode");
   }
   hipStream_t stream = (hipStream_t)stream_ptr;
   const int W = image_width, H = image_height;
@@ -465,7 +468,7 @@ static int backward_impl(
     return fail(GSR_ERR_ARGUMENT, "forward scratch buffers missing");
   if (!dL_dout_color || !dL_dmeans2D || !dL_dopacity || !dL_dmeans3D)
     return fail(GSR_ERR_ARGUMENT, "required gradient buffers missing");
-  if (sh && !dL_dsh) return fail(GSR_ERR_ARGUMENT, "dL_dsh required when sh is given");
+  if (sh && !dL_dsh && !dRGB_sh) return fail(GSR_ERR_ARGUMENT, "dL_dsh required when sh is given");
   if (scales && (!dL_dscales || !dL_drotations || !rotations))
     return fail(GSR_ERR_ARGUMENT, "dL_dscales / dL_drotations required when scales are given");
   if ((rotations && !aligned16(rotations)) || (dL_drotations && !aligned16(dL_drotations)))
@@ -521,6 +524,8 @@ static int backward_impl(
   ba.dL_dsh_language = dL_dsh_language; ba.dL_dlanguage_feature = dL_dlanguage_feature;
   ba.fused = fused; ba.accumulate = accumulate; ba.sh_dc = sh_dc; ba.sh_rest = sh_rest;
   ba.opacities_raw = opacity_raw; ba.dL_dsh_rest = dL_dsh_rest;
+  ba.dRGB_out = dRGB_sh;
+  if (dRGB_sh) ba.dL_dsh = ba.dL_dsh_rest = nullptr;
   PROF_BEGIN(PREPROCESS_BWD);
   GSR_CHECK(launch_preprocess_backward(ba, stream));
   PROF_END(PREPROCESS_BWD);
@@ -561,6 +566,28 @@ int gsr_rasterize_gaussians_fused_backward(
     float* dL_dmeans3D, float* dL_dfeatures_dc, float* dL_dfeatures_rest, float* dL_dopacity_raw,
     float* dL_dscaling_raw, float* dL_drotation_raw, float* dL_dlanguage_feature, int accumulate,
     void* stream_ptr, int debug) {
+  return gsr_rasterize_gaussians_fused_backward_deferred(
+      P, M, R, background, means3D, radii, features_dc, features_rest, opacity_raw, scaling_raw,
+      rotation_raw, scale_modifier, viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height,
+      image_width, dL_dout_color, dL_dout_depth, dL_dout_alpha, dL_dout_feature, degree, campos,
+      language_feature, confidence, include_feature, geom_buffer, binning_buffer, image_buffer,
+      dL_dmeans2D, dL_dmeans3D, dL_dfeatures_dc, dL_dfeatures_rest, dL_dopacity_raw,
+      dL_dscaling_raw, dL_drotation_raw, dL_dlanguage_feature, nullptr, accumulate, stream_ptr,
+      debug);
+}
+
+int gsr_rasterize_gaussians_fused_backward_deferred(
+    int P, int M, int R, const float* background, const float* means3D, const int* radii,
+    const float* features_dc, const float* features_rest, const float* opacity_raw,
+    const float* scaling_raw, const float* rotation_raw, float scale_modifier,
+    const float* viewmatrix, const float* projmatrix, float tan_fovx, float tan_fovy,
+    int image_height, int image_width, const float* dL_dout_color, const float* dL_dout_depth,
+    const float* dL_dout_alpha, const float* dL_dout_feature, int degree, const float* campos,
+    const float* language_feature, const float* confidence, int include_feature,
+    void* geom_buffer, void* binning_buffer, void* image_buffer, float* dL_dmeans2D,
+    float* dL_dmeans3D, float* dL_dfeatures_dc, float* dL_dfeatures_rest, float* dL_dopacity_raw,
+    float* dL_dscaling_raw, float* dL_drotation_raw, float* dL_dlanguage_feature,
+    float* dL_dcolor_sh, int accumulate, void* stream_ptr, int debug) {
   return backward_impl(P, M, R, background, means3D, radii, nullptr, scaling_raw, rotation_raw,
                        scale_modifier, nullptr, viewmatrix, projmatrix, tan_fovx, tan_fovy,
                        image_height, image_width, dL_dout_color, dL_dout_depth, dL_dout_alpha,
@@ -569,7 +596,36 @@ int gsr_rasterize_gaussians_fused_backward(
                        dL_dmeans2D, nullptr, dL_dopacity_raw, dL_dmeans3D, nullptr,
                        dL_dfeatures_dc, dL_dscaling_raw, dL_drotation_raw, dL_dlanguage_feature,
                        nullptr, stream_ptr, debug, 1, features_dc, features_rest, opacity_raw,
-                       dL_dfeatures_rest, accumulate);
+                       dL_dfeatures_rest, accumulate, dL_dcolor_sh);
+}
+
+int gsr_sh_grad_flush(int P, int M, int degree, const float* means3D, int nviews,
+                      const float* const* campos, const float* const* dL_dcolor_sh,
+                      float* dL_dfeatures_dc, float* dL_dfeatures_rest, int accumulate,
+                      void* stream_ptr) {
+  g_err.clear();
+  hipStream_t stream = (hipStream_t)stream_ptr;
+  const int debug = 0;
+  if (P < 0 || nviews < 0) return fail(GSR_ERR_ARGUMENT, "invalid sizes");
+  if (P == 0 || nviews == 0) return GSR_OK;
+  if (M < 1 || M > 16 || degree < 0 || degree > 3 || (degree + 1) * (degree + 1) > M)
+    return fail(GSR_ERR_ARGUMENT, "invalid sh degree %d for M = %d", degree, M);
+  if (!means3D || !campos || !dL_dcolor_sh || !dL_dfeatures_dc || (M > 1 && !dL_dfeatures_rest))
+    return fail(GSR_ERR_ARGUMENT, "null pointer");
+  for (int v0 = 0; v0 < nviews; v0 += kShFlushMaxViews) {
+    ShFlushArgs a{};
+    a.P = P; a.M = M; a.D = degree; a.means3D = means3D;
+    a.nviews = nviews - v0 < kShFlushMaxViews ? nviews - v0 : kShFlushMaxViews;
+    a.accumulate = (v0 > 0 || accumulate) ? 1 : 0;
+    for (int v = 0; v < a.nviews; v++) {
+      if (!campos[v0 + v] || !dL_dcolor_sh[v0 + v]) return fail(GSR_ERR_ARGUMENT, "null view pointer");
+      a.campos[v] = campos[v0 + v];
+      a.dRGB[v] = dL_dcolor_sh[v0 + v];
+    }
+    a.dL_dsh_dc = dL_dfeatures_dc; a.dL_dsh_rest = dL_dfeatures_rest;
+    GSR_CHECK(launch_sh_grad_flush(a, stream));
+  }
+  return GSR_OK;
 }
 
 // ---- test hooks (include/gsr_testing.h) -----------------------------------------------------------

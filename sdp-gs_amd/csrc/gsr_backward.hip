@@ -35,6 +35,7 @@ __device__ __forceinline__ void st3(float* p, size_t i, V3 v) {
 // s0: coefficient 0 of this Gaussian, s1: its coefficients 1.. (rows of the LDS staging planes);
 // the gradients go to the same places.  The used coefficients are read into registers first, so
 // the computation is in place.
+template <bool WRITE = true>
 __device__ __forceinline__ V3 sh_backward(float* s0, float* s1, int deg, V3 dir_orig,
                                           V3 dL_dRGB) {
   V3 c[16];
@@ -46,9 +47,11 @@ __device__ __forceinline__ V3 sh_backward(float* s0, float* s1, int deg, V3 dir_
 #define SH(k) c[k]
 #define PUT(k, v)                                                   \
   do {                                                              \
-    V3 _t = (v);                                                    \
-    float* _d = (k) == 0 ? s0 : s1 + 3 * (k) - 3;                   \
-    _d[0] = _t.x; _d[1] = _t.y; _d[2] = _t.z;                       \
+    if (WRITE) {                                                    \
+      V3 _t = (v);                                                  \
+      float* _d = (k) == 0 ? s0 : s1 + 3 * (k) - 3;                 \
+      _d[0] = _t.x; _d[1] = _t.y; _d[2] = _t.z;                     \
+    }                                                               \
   } while (0)
   const float len = sqrtf(dot3(dir_orig, dir_orig));
   const V3 dir = v3(dir_orig.x / len, dir_orig.y / len, dir_orig.z / len);
@@ -274,7 +277,12 @@ __device__ __forceinline__ void gaussian_bwd(const BwdPreArgs& a, size_t i, floa
     dRGB.y *= (cl & 2) ? 0 : 1;
     dRGB.z *= (cl & 4) ? 0 : 1;
     const V3 dir_orig = mean - v3(a.campos[0], a.campos[1], a.campos[2]);
-    dmean = dmean + sh_backward(sh0, sh1, a.D, dir_orig, dRGB);
+    if (a.dRGB_out) {  // deferred: dL/dsh = basis(dir) x dRGB is formed by the step's flush
+      put3(a.dRGB_out, i, dRGB);
+      dmean = dmean + sh_backward<false>(sh0, sh1, a.D, dir_orig, dRGB);
+    } else {
+      dmean = dmean + sh_backward<true>(sh0, sh1, a.D, dir_orig, dRGB);
+    }
   }
 
   // ---- cov3D -> scale / rotation (backward.cu:278-341, 393-395) ----
@@ -395,28 +403,115 @@ __global__ __launch_bounds__(kThreads) void preprocess_bwd_kernel(BwdPreArgs a) 
   // this Gaussian's rows: coefficient 0 and coefficients 1..
   float* r0 = s_sh + p0.lds + t * p0.w;
   float* r1 = a.fused ? s_sh + p1.lds + t * p1.w : r0 + 3;
+  const bool defer = a.dRGB_out != nullptr;
   if (live) {
     gaussian_bwd<ACC>(a, i, r0, r1);
-    if (has_sh) {  // coefficients above the active degree: zero gradient
+    if (has_sh && !defer) {  // coefficients above the active degree: zero gradient
       const int used = (a.D + 1) * (a.D + 1) * 3;
       for (int k = used; k < a.M * 3; k++) r1[k - 3] = 0.0f;
     }
   } else {
     if (!ACC && t < n) zero_outputs(a, i);
     if (ACC && t < n) put3(a.dL_dmeans2D, i, v3(0, 0, 0));  // stored output: zeros when culled
-    if (has_sh && t < n) {  // culled: zero rows (written in store mode, skipped or +0 in ACC)
+    if (defer && t < n) put3(a.dRGB_out, i, v3(0, 0, 0));
+    if (has_sh && !defer && t < n) {  // culled: zero rows (written in store mode, skipped or +0 in ACC)
       for (int k = 0; k < 3; k++) r0[k] = 0.0f;
       for (int k = 3; k < a.M * 3; k++) r1[k - 3] = 0.0f;
     }
   }
-  if (has_sh) {
+  if (has_sh && !defer) {
     __syncthreads();
     stage<kThreads, false, ACC>(p0, base, n, s_live, s_sh);
     stage<kThreads, false, ACC>(p1, base, n, s_live, s_sh);
   }
 }
 
+// Deferred SH gradients of a multi-view step: per Gaussian, for each view v in order,
+//   dL/dsh_k += basis_k(normalize(mean - campos_v)) * dL/dRGB_v      (backward.cu:20-139 PUTs)
+// with the same basis arithmetic as sh_backward, summed in registers, written once (store) or
+// added once (ACC) through the LDS staging planes -- instead of one 192-byte read-modify-write of
+// the SH gradient rows per view.
+__device__ __forceinline__ void sh_basis(V3 dir_orig, int deg, float (&b)[16]) {
+  const float len = sqrtf(dot3(dir_orig, dir_orig));
+  const V3 dir = v3(dir_orig.x / len, dir_orig.y / len, dir_orig.z / len);
+  const float x = dir.x, y = dir.y, z = dir.z;
+#pragma unroll
+  for (int k = 0; k < 16; k++) b[k] = 0.0f;
+  b[0] = SH_C0;
+  if (deg > 0) {
+    b[1] = -SH_C1 * y;
+    b[2] = SH_C1 * z;
+    b[3] = -SH_C1 * x;
+    if (deg > 1) {
+      const float xx = x * x, yy = y * y, zz = z * z;
+      const float xy = x * y, yz = y * z, xz = x * z;
+      b[4] = SH_C2_0 * xy;
+      b[5] = SH_C2_1 * yz;
+      b[6] = SH_C2_2 * (2.f * zz - xx - yy);
+      b[7] = SH_C2_3 * xz;
+      b[8] = SH_C2_4 * (xx - yy);
+      if (deg > 2) {
+        b[9] = SH_C3_0 * y * (3.f * xx - yy);
+        b[10] = SH_C3_1 * xy * z;
+        b[11] = SH_C3_2 * y * (4.f * zz - xx - yy);
+        b[12] = SH_C3_3 * z * (2.f * zz - 3.f * xx - 3.f * yy);
+        b[13] = SH_C3_4 * x * (4.f * zz - xx - yy);
+        b[14] = SH_C3_5 * z * (xx - yy);
+        b[15] = SH_C3_6 * x * (xx - 3.f * yy);
+      }
+    }
+  }
+}
+
+template <bool ACC>
+__global__ __launch_bounds__(kThreads) void sh_flush_kernel(ShFlushArgs a) {
+  __shared__ float4 s_sh4[kThreads * kShMaxFloats / 4];
+  __shared__ uint8_t s_live[kThreads];
+  float* s_sh = reinterpret_cast<float*>(s_sh4);
+  const int base = (int)(blockIdx.x * kThreads);
+  const int n = min(kThreads, a.P - base);
+  const int t = (int)threadIdx.x;
+  const size_t i = (size_t)base + t;
+  s_live[t] = t < n;
+  const ShPlane p0{nullptr, a.dL_dsh_dc, 3, 0};
+  const ShPlane p1{nullptr, a.dL_dsh_rest, (a.M - 1) * 3, kThreads * 3};
+  if (t < n) {
+    const V3 mean = v3(a.means3D[3 * i], a.means3D[3 * i + 1], a.means3D[3 * i + 2]);
+    V3 g[16];
+    const int used = (a.D + 1) * (a.D + 1);
+    for (int v = 0; v < a.nviews; v++) {
+      const float* cp = a.campos[v];
+      float b[16];
+      sh_basis(mean - v3(cp[0], cp[1], cp[2]), a.D, b);
+      const float* d = a.dRGB[v] + 3 * i;
+      const V3 dRGB = v3(d[0], d[1], d[2]);
+#pragma unroll
+      for (int k = 0; k < 16; k++) g[k] = v == 0 ? b[k] * dRGB : g[k] + b[k] * dRGB;
+    }
+    float* r0 = s_sh + p0.lds + t * p0.w;
+    float* r1 = s_sh + p1.lds + t * p1.w;
+    r0[0] = g[0].x; r0[1] = g[0].y; r0[2] = g[0].z;
+    for (int k = 1; k < a.M; k++) {
+      const V3 v = k < used ? g[k] : v3(0, 0, 0);
+      r1[3 * k - 3] = v.x; r1[3 * k - 2] = v.y; r1[3 * k - 1] = v.z;
+    }
+  }
+  __syncthreads();
+  stage<kThreads, false, ACC>(p0, base, n, s_live, s_sh);
+  stage<kThreads, false, ACC>(p1, base, n, s_live, s_sh);
+}
+
 }  // namespace
+
+hipError_t launch_sh_grad_flush(const ShFlushArgs& a, hipStream_t s) {
+  if (a.P == 0 || a.nviews <= 0) return hipSuccess;
+  const dim3 grid((a.P + kThreads - 1) / kThreads);
+  if (a.accumulate)
+    hipLaunchKernelGGL(sh_flush_kernel<true>, grid, dim3(kThreads), 0, s, a);
+  else
+    hipLaunchKernelGGL(sh_flush_kernel<false>, grid, dim3(kThreads), 0, s, a);
+  return hipGetLastError();
+}
 
 hipError_t launch_preprocess_backward(const BwdPreArgs& a, hipStream_t s) {
   if (a.P == 0) return hipSuccess;

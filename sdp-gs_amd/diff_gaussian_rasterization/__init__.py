@@ -359,18 +359,25 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
         fopts = dict(dtype=torch.float32, device=dev)
         into_leaves = ctx.leaves is not None
         accumulate = into_leaves
-        if into_leaves and all(t is None or t.grad is None for t in ctx.leaves):
+        # deferred SH gradients (gsr_amd.pipeline.ViewPipeline): this view stores dL/dRGB [P,3]
+        # and the step's flush writes features_dc / features_rest .grad once for all its views
+        defer = _SH_DEFER.get(dev.index) if into_leaves else None
+        direct = ctx.leaves
+        if defer is not None:
+            direct = tuple(None if k in (1, 2) else t for k, t in enumerate(ctx.leaves))
+        if into_leaves and all(t is None or t.grad is None for t in direct):
             # first view after zero_grad(set_to_none=True): the kernel's store mode writes every
             # element of fresh .grad tensors (zeros for culled Gaussians) -- no memset, no read
             accumulate = False
-            for t in ctx.leaves:
+            for t in direct:
                 if t is not None:
                     t.grad = torch.empty_like(t, memory_format=torch.contiguous_format)
+        d_rgb = None
         if into_leaves:
             # add straight into the parameters' .grad (created as zeros when absent, as
             # AccumulateGrad would); culled Gaussians are not touched at all
             grads = []
-            for t in ctx.leaves:
+            for t in direct:
                 if t is not None and t.grad is None:
                     t.grad = torch.zeros_like(t, memory_format=torch.contiguous_format)
                 grads.append(None if t is None else t.grad)
@@ -378,6 +385,9 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
                 raise RuntimeError("grad-into-leaves needs contiguous .grad tensors")
             d_means3D, d_dc, d_rest, d_op, d_sc, d_rot, d_lf = grads
             d_means2D = torch.empty((P, 3), **fopts)  # always stored by the kernel
+            if defer is not None:
+                d_rgb = torch.empty((P, 3), **fopts)
+                defer.add(ctx.leaves, d_rgb, campos, m3, int(rs.sh_degree), M)
         else:
             d_means2D = torch.empty((P, 3), **fopts)
             d_means3D = torch.empty((P, 3), **fopts)
@@ -393,7 +403,7 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
         if into_leaves:
             _order_leaf_grads(dev, cur)
         with torch.cuda.device(dev):
-            rc = L.gsr_rasterize_gaussians_fused_backward(
+            rc = L.gsr_rasterize_gaussians_fused_backward_deferred(
                 P, M, ctx.num_rendered, _ptr(bg), _ptr(m3), _ptr(radii), _ptr(dc), _ptr(rest),
                 _ptr(op), _ptr(sc), _ptr(rot), float(rs.scale_modifier), _ptr(view), _ptr(proj),
                 float(rs.tanfovx), float(rs.tanfovy), H, W, _ptr(dcol), _ptr(ddep), _ptr(dalp),
@@ -401,7 +411,7 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
                 int(mt["include_feature"]), _ptr(geom) if geom.numel() else None,
                 _ptr(binning) if binning.numel() else None, _ptr(image) if image.numel() else None,
                 _ptr(d_means2D), _ptr(d_means3D), _ptr(d_dc), _ptr(d_rest), _ptr(d_op),
-                _ptr(d_sc), _ptr(d_rot), _ptr(d_lf), int(accumulate), stream,
+                _ptr(d_sc), _ptr(d_rot), _ptr(d_lf), _ptr(d_rgb), int(accumulate), stream,
                 int(bool(rs.debug)))
         _lib.check(rc)
         if into_leaves:
@@ -416,6 +426,72 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
 
 
 _GRAD_INTO_LEAVES = None
+# device index -> ShGradDeferral collecting the views of the current multi-view step
+_SH_DEFER = {}
+
+
+class ShGradDeferral:
+    """Deferred SH gradients of one multi-view step on one device (include/gsr.h
+    gsr_rasterize_gaussians_fused_backward_deferred / gsr_sh_grad_flush).  While installed
+    (``with ShGradDeferral(dev):``), grad-into-leaves backwards store each view's clamp-masked
+    dL/dRGB [P,3] instead of read-modify-writing the 192-byte SH gradient rows, and flush()
+    writes features_dc / features_rest .grad once: sum over the views of basis(dir_v) x dRGB_v,
+    the reference's own per-view SH backward (backward.cu:20-139) summed in view order.  The
+    .grad of the SH leaves is only complete after flush() (the context's exit flushes)."""
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self.views = []
+        self.leaves = None
+
+    def __enter__(self):
+        if self.device.index in _SH_DEFER:
+            raise RuntimeError("an SH-gradient deferral is already active on this device")
+        _SH_DEFER[self.device.index] = self
+        return self
+
+    def __exit__(self, *exc):
+        _SH_DEFER.pop(self.device.index, None)
+        if exc[0] is None:
+            self.flush()
+        self.views = []
+        return False
+
+    def add(self, leaves, d_rgb, campos, means3D, degree, M):
+        if self.leaves is not None and any(a is not b for a, b in zip(self.leaves, leaves)):
+            raise RuntimeError("deferred SH gradients: views of one step must share the leaves")
+        if self.views and (self.views[0][3], self.views[0][4]) != (degree, M):
+            raise RuntimeError("deferred SH gradients: views of one step must share the SH degree")
+        self.leaves = leaves
+        self.views.append((d_rgb, campos, torch.cuda.current_stream(self.device), degree, M,
+                           means3D))
+
+    def flush(self):
+        """Write the SH leaves' .grad for the collected views on the current stream (which must
+        be ordered after every view's backward, e.g. joined by ViewPipeline.run)."""
+        if not self.views:
+            return
+        _, dc, rest = self.leaves[0], self.leaves[1], self.leaves[2]
+        d_rgb0, _, _, degree, M, m3 = self.views[0]
+        P = int(m3.shape[0])
+        cur = torch.cuda.current_stream(self.device)
+        accumulate = dc.grad is not None
+        for t in (dc, rest):
+            if t is not None and t.grad is None:
+                t.grad = torch.empty_like(t, memory_format=torch.contiguous_format)
+        n = len(self.views)
+        camp = (_lib.ctypes.c_void_p * n)(*[v[1].data_ptr() for v in self.views])
+        rgbs = (_lib.ctypes.c_void_p * n)(*[v[0].data_ptr() for v in self.views])
+        with torch.cuda.device(self.device):
+            rc = _lib.load().gsr_sh_grad_flush(P, M, degree, _ptr(m3), n, camp, rgbs,
+                                               _ptr(dc.grad),
+                                               _ptr(rest.grad) if rest is not None else None,
+                                               int(accumulate), cur.cuda_stream)
+        _lib.check(rc)
+        for v in self.views:  # buffers made on the views' streams, read here on this one
+            v[0].record_stream(cur)
+            v[1].record_stream(cur)
+        self.views = []
 # device index -> (event after the last grad-into-leaves backward, id of the stream it ran on)
 _LEAF_GRAD_EVENT = {}
 

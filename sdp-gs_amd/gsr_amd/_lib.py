@@ -100,6 +100,12 @@ def load():
             _p, _p, _p, _p, _p, _p, _p, _p,  # grads: means2D, means3D, dc, rest, op, scale, rot, lang
             _i,                          # accumulate
             _p, _i]                      # stream, debug
+        L.gsr_rasterize_gaussians_fused_backward_deferred.restype = _i
+        L.gsr_rasterize_gaussians_fused_backward_deferred.argtypes = (
+            L.gsr_rasterize_gaussians_fused_backward.argtypes[:-3] + [_p, _i, _p, _i])
+        L.gsr_sh_grad_flush.restype = _i
+        L.gsr_sh_grad_flush.argtypes = [_i, _i, _i, _p, _i, ctypes.POINTER(_p),
+                                        ctypes.POINTER(_p), _p, _p, _i, _p]
         # include/gsr_optim.h
         _pp = ctypes.POINTER(_p)
         L.gsr_adam_step.restype = _i

@@ -10,9 +10,16 @@ grad-into-leaves mode, is ordered by diff_gaussian_rasterization itself (one eve
 see ``_order_leaf_grads``), so any multi-stream caller gets correct accumulation, not only this
 helper.  The reference renders one view per step on the legacy default stream
 (train.py:64-236); with depth = 1 this helper is exactly that sequential loop.
+
+With defer_sh (default), the grad-into-leaves backwards of the step store each view's
+clamp-masked colour gradient dL/dRGB [P,3] instead of read-modify-writing the 192-byte SH
+gradient rows, and run() writes features_dc / features_rest .grad once at the end
+(diff_gaussian_rasterization.ShGradDeferral): the SH gradient of a view is basis(dir) x dL/dRGB,
+so the per-view SH traffic drops from 384 to 12 bytes per Gaussian.
 """
 from __future__ import annotations
 
+import contextlib
 from typing import Callable, Iterable, List, Optional, TypeVar
 
 import torch
@@ -25,28 +32,34 @@ class ViewPipeline:
     """Round-robin per-view work over ``depth`` streams: the caller's current stream plus
     ``depth - 1`` side streams, joined back into the current stream at the end of run()."""
 
-    def __init__(self, device: Optional[torch.device] = None, depth: int = 2):
+    def __init__(self, device: Optional[torch.device] = None, depth: int = 2,
+                 defer_sh: bool = True):
         if depth < 1:
             raise ValueError("depth must be >= 1")
         self.device = torch.device(device) if device is not None else torch.device(
             "cuda", torch.cuda.current_device())
         self.depth = depth
+        self.defer_sh = defer_sh
         self.side = [torch.cuda.Stream(device=self.device) for _ in range(depth - 1)]
 
     def run(self, items: Iterable[T], fn: Callable[[T], R]) -> List[R]:
         """Call fn(item) for every item, item i issued on stream i mod depth.  fn should do a
         view's render + backward and return host values (or tensors it no longer needs on the
         device): tensors created on a side stream and used after run() on the main stream need
-        Tensor.record_stream to be safe under the caching allocator."""
+        Tensor.record_stream to be safe under the caching allocator.  With defer_sh the SH
+        leaves' .grad is complete when run() returns, not after each view."""
+        import diff_gaussian_rasterization as dgr
         main = torch.cuda.current_stream(self.device)
         streams = [main] + self.side
         for s in self.side:
             s.wait_stream(main)  # inputs prepared on the main stream (zeroed grads, cameras)
         out = []
-        for i, it in enumerate(items):
-            s = streams[i % self.depth]
-            with torch.cuda.stream(s):
-                out.append(fn(it))
-        for s in self.side:
-            main.wait_stream(s)
+        defer = dgr.ShGradDeferral(self.device) if self.defer_sh else contextlib.nullcontext()
+        with defer:  # exit: the SH gradients of all views, on the main stream after the join
+            for i, it in enumerate(items):
+                s = streams[i % self.depth]
+                with torch.cuda.stream(s):
+                    out.append(fn(it))
+            for s in self.side:
+                main.wait_stream(s)
         return out

@@ -148,8 +148,9 @@ def test_grad_into_leaves_equals_autograd_accumulation():
 def test_view_pipeline_two_streams_equals_sequential(into_leaves):
     """gsr_amd.pipeline.ViewPipeline: six views issued round-robin on two HIP streams (view k+1's
     forward overlapping view k's backward; grad-into-leaves read-modify-writes ordered by the
-    library's per-device event) give the same accumulated gradients and per-view screen-space
-    gradients as the strictly sequential loop (to float-atomic ordering)."""
+    library's per-device event) and, by default, SH gradients deferred to one flush per step
+    (diff_gaussian_rasterization.ShGradDeferral) give the same accumulated gradients and per-view
+    screen-space gradients as the strictly sequential loop (to float-atomic ordering)."""
     import diff_gaussian_rasterization as dgr
     from gsr_amd.pipeline import ViewPipeline
     render, m, _ = _setup()
@@ -158,21 +159,49 @@ def test_view_pipeline_two_streams_equals_sequential(into_leaves):
     res = []
     try:
         dgr.grad_into_leaves(into_leaves)
-        for depth in (1, 2):
+        for depth, defer in ((1, False), (2, True), (1, True), (2, False)):
             _zero(m)
-            pipe = ViewPipeline(torch.device("cuda"), depth=depth)
+            pipe = ViewPipeline(torch.device("cuda"), depth=depth, defer_sh=defer)
 
             def one(c):
                 pkg = render(c, m, Pipe(sh_py=True), bg, Opt())
                 (pkg["render"].sum() + pkg["feature"].sum() + pkg["depth"].mean()).backward()
-                v = pkg["viewspace_points"].grad.clone()
-                return v
+                return pkg["viewspace_points"].grad.clone()
 
             vs = pipe.run(cams, one)
             torch.cuda.synchronize()
             res.append((_leaf_grads(m), vs))
     finally:
         dgr.grad_into_leaves(False)
-    (ga, va), (gb, vb) = res
-    for x, y in zip(ga + va, gb + vb):
+    ga, va = res[0]
+    for gb, vb in res[1:]:
+        for x, y in zip(ga + va, gb + vb):
+            torch.testing.assert_close(x, y, rtol=1e-4, atol=1e-5 * y.abs().max().item())
+
+
+def test_sh_grad_deferral_accumulates_into_existing_grads():
+    """A deferred step adds into SH .grad tensors that already hold values (the all-reduce
+    bucket views of GradAllReducer.attach_grads): flush(accumulate = 1) == sequential sum."""
+    import diff_gaussian_rasterization as dgr
+    from gsr_amd.pipeline import ViewPipeline
+    render, m, _ = _setup()
+    cams = [c.to("cuda") for c in make_cameras(3, 200, 150, seed=4)]
+    bg = torch.zeros(3, device="cuda")
+    res = []
+    try:
+        dgr.grad_into_leaves(True)
+        for defer in (False, True):
+            for p in m.parameters():
+                p.grad = torch.full_like(p, 0.25)
+
+            def one(c):
+                pkg = render(c, m, Pipe(sh_py=False), bg, Opt())
+                (pkg["render"] * 2.0).sum().backward()
+
+            ViewPipeline(torch.device("cuda"), depth=2, defer_sh=defer).run(cams, one)
+            torch.cuda.synchronize()
+            res.append(_leaf_grads(m))
+    finally:
+        dgr.grad_into_leaves(False)
+    for x, y in zip(*res):
         torch.testing.assert_close(x, y, rtol=1e-4, atol=1e-5 * y.abs().max().item())
