@@ -102,6 +102,8 @@ def main():
     ap.add_argument("--no-defer-sh", action="store_true",
                     help="write the SH gradients in every view's backward instead of one flush "
                          "per step (diff_gaussian_rasterization.ShGradDeferral)")
+    ap.add_argument("--no-precolor", action="store_true",
+                    help="each view evaluates its SH colour itself instead of the step's pre-pass")
     ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_r01.json"))
     args = ap.parse_args()
 
@@ -130,7 +132,8 @@ def main():
     pipe, opt = Pipe(), Opt()
     stats = {"R": [], "Pv": []}
     defer_sh = not args.no_defer_sh and not args.autograd_grads
-    views = ViewPipeline(dev, depth=max(1, args.streams), defer_sh=defer_sh)
+    views = ViewPipeline(dev, depth=max(1, args.streams), defer_sh=defer_sh,
+                         precolor=not args.no_precolor)
 
     def one_view(cam, record):
         pkg = render(cam, model, pipe, bg, opt)
@@ -146,7 +149,7 @@ def main():
         else:
             for p in model.parameters():
                 p.grad = None
-        views.run(my_cams, lambda cam: one_view(cam, record))
+        views.run(my_cams, lambda cam: one_view(cam, record), model=model)
         if reducer is not None:
             reducer.allreduce()
 
@@ -280,6 +283,7 @@ def main():
                        "grad_mode": "autograd" if args.autograd_grads else "into_leaves",
                        "view_streams": views.depth,
                        "sh_grads": "deferred (one flush per step)" if defer_sh else "per view",
+                       "sh_colour": "per view" if args.no_precolor else "multi-view pre-pass",
                        "num_rendered_mean": int(R), "visible_mean": int(Pv), "tiles": T},
             "roofline": roofline,
             "cpu_baseline": cpu,

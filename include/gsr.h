@@ -152,7 +152,9 @@ int gsr_rasterize_gaussians_fused_backward(
  * dL_dcolor_sh != NULL the SH gradients are NOT written (dL_dfeatures_dc / _rest may be NULL);
  * instead the clamp-masked colour gradient dL/dRGB of every Gaussian ([P,3], zeros when culled)
  * is stored there.  The SH gradient is basis(dir) x dL/dRGB (backward.cu:20-139), so
- * gsr_sh_grad_flush forms it for all deferred views of a step in one pass over the SH rows. */
+ * gsr_sh_grad_flush forms it for all deferred views of a step in one pass over the SH rows.
+ * pre_jac (optional, needs dL_dcolor_sh): this view's colour Jacobian from gsr_sh_precolor; the
+ * SH rows are then not read. */
 int gsr_rasterize_gaussians_fused_backward_deferred(
     int P, int M, int R,
     const float* background, const float* means3D, const int* radii,
@@ -167,7 +169,28 @@ int gsr_rasterize_gaussians_fused_backward_deferred(
     void* geom_buffer, void* binning_buffer, void* image_buffer,
     float* dL_dmeans2D, float* dL_dmeans3D, float* dL_dfeatures_dc, float* dL_dfeatures_rest,
     float* dL_dopacity_raw, float* dL_dscaling_raw, float* dL_drotation_raw,
-    float* dL_dlanguage_feature, float* dL_dcolor_sh, int accumulate,
+    float* dL_dlanguage_feature, float* dL_dcolor_sh, const float* pre_jac, int accumulate,
+    void* stream, int debug);
+
+/* Multi-view colour pre-pass (gsr_amd/pipeline.py): for nviews cameras, one pass over the SH
+ * rows writes per view the fused forward's colour clamp(SH(dir) + 0.5) [P,3] (forward.cu:20-71),
+ * its clamp bits [P] (u8) and the colour's direction Jacobian dRGB/d(dir_x, dir_y, dir_z) [P,9]
+ * (backward.cu:56-131).  campos / color / clamped / jac: HOST arrays of nviews DEVICE pointers. */
+int gsr_sh_precolor(int P, int M, int degree, const float* means3D, const float* features_dc,
+                    const float* features_rest, int nviews, const float* const* campos,
+                    float* const* color, uint8_t* const* clamped, float* const* jac, void* stream);
+
+/* gsr_rasterize_gaussians_fused with the SH colour and clamp bits of this view taken from
+ * gsr_sh_precolor (identical outputs; the SH rows are not read). */
+int gsr_rasterize_gaussians_fused_precolor(
+    int P, int M, const float* background, const float* means3D, const float* features_dc,
+    const float* features_rest, const float* opacity_raw, const float* scaling_raw,
+    const float* rotation_raw, float scale_modifier, const float* viewmatrix,
+    const float* projmatrix, float tan_fovx, float tan_fovy, int image_height, int image_width,
+    int degree, const float* campos, int prefiltered, const float* language_feature,
+    const float* confidence, int include_feature, const float* pre_color,
+    const uint8_t* pre_clamp, float* out_color, float* out_depth, float* out_alpha,
+    float* out_feature, int* radii, int* num_rendered, gsr_alloc_fn alloc, void* alloc_ctx,
     void* stream, int debug);
 
 /* dL/dfeatures_dc [P,1,3] and dL/dfeatures_rest [P,M-1,3] of nviews deferred views:

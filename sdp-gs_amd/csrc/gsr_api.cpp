@@ -237,8 +237,11 @@ static int forward_impl(int P, int M, const float* background, const float* mean
                         int include_feature, float* out_color, float* out_depth, float* out_alpha,
                         float* out_feature, int* radii, int* num_rendered, gsr_alloc_fn alloc,
                         void* alloc_ctx, void* stream_ptr, int debug, int fused,
-                        const float* sh_dc, const float* sh_rest) {
+                        const float* sh_dc, const float* sh_rest,
+                        const float* pre_color = nullptr, const uint8_t* pre_clamp = nullptr) {
   g_err.clear();
+  if ((pre_color == nullptr) != (pre_clamp == nullptr) || (pre_color && !fused))
+    return fail(GSR_ERR_ARGUMENT, "pre_color / pre_clamp: both or neither, fused path only");
   if (fused) {
     if (!sh_dc || (M > 1 && !sh_rest) || !scales || !rotations)
       return fail(GSR_ERR_ARGUMENT, "fused path needs features_dc/_rest, _scaling, _rotation");
@@ -306,6 +309,7 @@ static int forward_impl(int P, int M, const float* background, const float* mean
   pa.prefiltered = prefiltered; pa.include_feature = include_feature;
   pa.radii = radii_ptr; pa.g = g;
   pa.fused = fused; pa.sh_dc = sh_dc; pa.sh_rest = sh_rest;
+  pa.pre_color = pre_color; pa.pre_clamp = pre_clamp;
   // the preprocess grid also zeroes the depth sort's scratch and the backward's accumulators
   pa.clear = SideClear{g.sort.aux, sort_clear_bytes(g.sort, (size_t)P, 32)};
   pa.acc_zero = 1;
@@ -438,6 +442,24 @@ int gsr_rasterize_gaussians_fused(int P, int M, const float* background, const f
                       debug, 1, features_dc, features_rest);
 }
 
+int gsr_rasterize_gaussians_fused_precolor(
+    int P, int M, const float* background, const float* means3D, const float* features_dc,
+    const float* features_rest, const float* opacity_raw, const float* scaling_raw,
+    const float* rotation_raw, float scale_modifier, const float* viewmatrix,
+    const float* projmatrix, float tan_fovx, float tan_fovy, int image_height, int image_width,
+    int degree, const float* campos, int prefiltered, const float* language_feature,
+    const float* confidence, int include_feature, const float* pre_color,
+    const uint8_t* pre_clamp, float* out_color, float* out_depth, float* out_alpha,
+    float* out_feature, int* radii, int* num_rendered, gsr_alloc_fn alloc, void* alloc_ctx,
+    void* stream_ptr, int debug) {
+  return forward_impl(P, M, background, means3D, nullptr, opacity_raw, scaling_raw, rotation_raw,
+                      scale_modifier, nullptr, viewmatrix, projmatrix, tan_fovx, tan_fovy,
+                      image_height, image_width, nullptr, degree, campos, prefiltered,
+                      language_feature, nullptr, confidence, include_feature, out_color, out_depth,
+                      out_alpha, out_feature, radii, num_rendered, alloc, alloc_ctx, stream_ptr,
+                      debug, 1, features_dc, features_rest, pre_color, pre_clamp);
+}
+
 static int backward_impl(
     int P, int M, int R, const float* background, const float* means3D, const int* radii,
     const float* colors_precomp, const float* scales, const float* rotations, float scale_modifier,
@@ -450,7 +472,8 @@ static int backward_impl(
     float* dL_dcolors, float* dL_dopacity, float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh,
     float* dL_dscales, float* dL_drotations, float* dL_dsh_language, float* dL_dlanguage_feature,
     void* stream_ptr, int debug, int fused, const float* sh_dc, const float* sh_rest,
-    const float* opacity_raw, float* dL_dsh_rest, int accumulate, float* dRGB_sh = nullptr) {
+    const float* opacity_raw, float* dL_dsh_rest, int accumulate, float* dRGB_sh = nullptr,
+    const float* pre_jac = nullptr) {
   g_err.clear();
   if (fused) {
     if (!sh_dc || (M > 1 && !sh_rest) || (M > 1 && !dL_dsh_rest && !dRGB_sh) || !scales ||
@@ -460,6 +483,8 @@ static int backward_impl(
   } else if (dRGB_sh) {
     return fail(GSR_ERR_ARGUMENT, "deferred SH gradients are a fused-path mode");
   }
+  if (pre_jac && !dRGB_sh)
+    return fail(GSR_ERR_ARGUMENT, "pre_jac needs the deferred SH gradients (dL_dcolor_sh)");
   hipStream_t stream = (hipStream_t)stream_ptr;
   const int W = image_width, H = image_height;
   if (P < 0 || R < 0 || W <= 0 || H <= 0) return fail(GSR_ERR_ARGUMENT, "invalid sizes");
@@ -525,6 +550,7 @@ static int backward_impl(
   ba.fused = fused; ba.accumulate = accumulate; ba.sh_dc = sh_dc; ba.sh_rest = sh_rest;
   ba.opacities_raw = opacity_raw; ba.dL_dsh_rest = dL_dsh_rest;
   ba.dRGB_out = dRGB_sh;
+  ba.pre_jac = pre_jac;
   if (dRGB_sh) ba.dL_dsh = ba.dL_dsh_rest = nullptr;
   PROF_BEGIN(PREPROCESS_BWD);
   GSR_CHECK(launch_preprocess_backward(ba, stream));
@@ -572,8 +598,8 @@ int gsr_rasterize_gaussians_fused_backward(
       image_width, dL_dout_color, dL_dout_depth, dL_dout_alpha, dL_dout_feature, degree, campos,
       language_feature, confidence, include_feature, geom_buffer, binning_buffer, image_buffer,
       dL_dmeans2D, dL_dmeans3D, dL_dfeatures_dc, dL_dfeatures_rest, dL_dopacity_raw,
-      dL_dscaling_raw, dL_drotation_raw, dL_dlanguage_feature, nullptr, accumulate, stream_ptr,
-      debug);
+      dL_dscaling_raw, dL_drotation_raw, dL_dlanguage_feature, nullptr, nullptr, accumulate,
+      stream_ptr, debug);
 }
 
 int gsr_rasterize_gaussians_fused_backward_deferred(
@@ -587,7 +613,7 @@ int gsr_rasterize_gaussians_fused_backward_deferred(
     void* geom_buffer, void* binning_buffer, void* image_buffer, float* dL_dmeans2D,
     float* dL_dmeans3D, float* dL_dfeatures_dc, float* dL_dfeatures_rest, float* dL_dopacity_raw,
     float* dL_dscaling_raw, float* dL_drotation_raw, float* dL_dlanguage_feature,
-    float* dL_dcolor_sh, int accumulate, void* stream_ptr, int debug) {
+    float* dL_dcolor_sh, const float* pre_jac, int accumulate, void* stream_ptr, int debug) {
   return backward_impl(P, M, R, background, means3D, radii, nullptr, scaling_raw, rotation_raw,
                        scale_modifier, nullptr, viewmatrix, projmatrix, tan_fovx, tan_fovy,
                        image_height, image_width, dL_dout_color, dL_dout_depth, dL_dout_alpha,
@@ -596,7 +622,36 @@ int gsr_rasterize_gaussians_fused_backward_deferred(
                        dL_dmeans2D, nullptr, dL_dopacity_raw, dL_dmeans3D, nullptr,
                        dL_dfeatures_dc, dL_dscaling_raw, dL_drotation_raw, dL_dlanguage_feature,
                        nullptr, stream_ptr, debug, 1, features_dc, features_rest, opacity_raw,
-                       dL_dfeatures_rest, accumulate, dL_dcolor_sh);
+                       dL_dfeatures_rest, accumulate, dL_dcolor_sh, pre_jac);
+}
+
+int gsr_sh_precolor(int P, int M, int degree, const float* means3D, const float* features_dc,
+                    const float* features_rest, int nviews, const float* const* campos,
+                    float* const* color, uint8_t* const* clamped, float* const* jac,
+                    void* stream_ptr) {
+  g_err.clear();
+  hipStream_t stream = (hipStream_t)stream_ptr;
+  const int debug = 0;
+  if (P < 0 || nviews < 0) return fail(GSR_ERR_ARGUMENT, "invalid sizes");
+  if (P == 0 || nviews == 0) return GSR_OK;
+  if (M < 1 || M > 16 || degree < 0 || degree > 3 || (degree + 1) * (degree + 1) > M)
+    return fail(GSR_ERR_ARGUMENT, "invalid sh degree %d for M = %d", degree, M);
+  if (!means3D || !features_dc || (M > 1 && !features_rest) || !campos || !color || !clamped || !jac)
+    return fail(GSR_ERR_ARGUMENT, "null pointer");
+  for (int v0 = 0; v0 < nviews; v0 += kShFlushMaxViewsFwd) {
+    PrecolorArgs a{};
+    a.P = P; a.M = M; a.D = degree; a.means3D = means3D; a.sh_dc = features_dc;
+    a.sh_rest = features_rest;
+    a.nviews = nviews - v0 < kShFlushMaxViewsFwd ? nviews - v0 : kShFlushMaxViewsFwd;
+    for (int v = 0; v < a.nviews; v++) {
+      if (!campos[v0 + v] || !color[v0 + v] || !clamped[v0 + v] || !jac[v0 + v])
+        return fail(GSR_ERR_ARGUMENT, "null view pointer");
+      a.campos[v] = campos[v0 + v]; a.color[v] = color[v0 + v];
+      a.clamp[v] = clamped[v0 + v]; a.jac[v] = jac[v0 + v];
+    }
+    GSR_CHECK(launch_sh_precolor(a, stream));
+  }
+  return GSR_OK;
 }
 
 int gsr_sh_grad_flush(int P, int M, int degree, const float* means3D, int nviews,

@@ -8,6 +8,7 @@
 // Inputs come from the 64-byte accumulator row the backward blend filled (gsr_internal.h AccSlot).
 #include "gsr_device.h"
 #include "gsr_internal.h"
+#include "gsr_sh.h"
 #include "gsr_stage.h"
 
 namespace gsr {
@@ -44,103 +45,26 @@ __device__ __forceinline__ V3 sh_backward(float* s0, float* s1, int deg, V3 dir_
 #pragma unroll
   for (int k = 1; k < 16; k++)
     c[k] = k < ncoef_used ? v3(s1[3 * k - 3], s1[3 * k - 2], s1[3 * k - 1]) : v3(0, 0, 0);
-#define SH(k) c[k]
-#define PUT(k, v)                                                   \
-  do {                                                              \
-    if (WRITE) {                                                    \
-      V3 _t = (v);                                                  \
-      float* _d = (k) == 0 ? s0 : s1 + 3 * (k) - 3;                 \
-      _d[0] = _t.x; _d[1] = _t.y; _d[2] = _t.z;                     \
-    }                                                               \
-  } while (0)
   const float len = sqrtf(dot3(dir_orig, dir_orig));
   const V3 dir = v3(dir_orig.x / len, dir_orig.y / len, dir_orig.z / len);
-  V3 dRGBdx = v3(0, 0, 0), dRGBdy = v3(0, 0, 0), dRGBdz = v3(0, 0, 0);
-  const float x = dir.x, y = dir.y, z = dir.z;
-  const float dRGBdsh0 = SH_C0;
-  PUT(0, dRGBdsh0 * dL_dRGB);
-  if (deg > 0) {
-    const float dRGBdsh1 = -SH_C1 * y;
-    const float dRGBdsh2 = SH_C1 * z;
-    const float dRGBdsh3 = -SH_C1 * x;
-    PUT(1, dRGBdsh1 * dL_dRGB);
-    PUT(2, dRGBdsh2 * dL_dRGB);
-    PUT(3, dRGBdsh3 * dL_dRGB);
-    dRGBdx = -SH_C1 * SH(3);
-    dRGBdy = -SH_C1 * SH(1);
-    dRGBdz = SH_C1 * SH(2);
-    if (deg > 1) {
-      const float xx = x * x, yy = y * y, zz = z * z;
-      const float xy = x * y, yz = y * z, xz = x * z;
-      const float dRGBdsh4 = SH_C2_0 * xy;
-      const float dRGBdsh5 = SH_C2_1 * yz;
-      const float dRGBdsh6 = SH_C2_2 * (2.f * zz - xx - yy);
-      const float dRGBdsh7 = SH_C2_3 * xz;
-      const float dRGBdsh8 = SH_C2_4 * (xx - yy);
-      PUT(4, dRGBdsh4 * dL_dRGB);
-      PUT(5, dRGBdsh5 * dL_dRGB);
-      PUT(6, dRGBdsh6 * dL_dRGB);
-      PUT(7, dRGBdsh7 * dL_dRGB);
-      PUT(8, dRGBdsh8 * dL_dRGB);
-      const V3 tx = (((SH_C2_0 * y) * SH(4) + (SH_C2_2 * 2.f * -x) * SH(6)) + (SH_C2_3 * z) * SH(7)) +
-                    (SH_C2_4 * 2.f * x) * SH(8);
-      const V3 ty = (((SH_C2_0 * x) * SH(4) + (SH_C2_1 * z) * SH(5)) + (SH_C2_2 * 2.f * -y) * SH(6)) +
-                    (SH_C2_4 * 2.f * -y) * SH(8);
-      const V3 tz = ((SH_C2_1 * y) * SH(5) + (SH_C2_2 * 2.f * 2.f * z) * SH(6)) + (SH_C2_3 * x) * SH(7);
-      dRGBdx = dRGBdx + tx;
-      dRGBdy = dRGBdy + ty;
-      dRGBdz = dRGBdz + tz;
-      if (deg > 2) {
-        const float dRGBdsh9 = SH_C3_0 * y * (3.f * xx - yy);
-        const float dRGBdsh10 = SH_C3_1 * xy * z;
-        const float dRGBdsh11 = SH_C3_2 * y * (4.f * zz - xx - yy);
-        const float dRGBdsh12 = SH_C3_3 * z * (2.f * zz - 3.f * xx - 3.f * yy);
-        const float dRGBdsh13 = SH_C3_4 * x * (4.f * zz - xx - yy);
-        const float dRGBdsh14 = SH_C3_5 * z * (xx - yy);
-        const float dRGBdsh15 = SH_C3_6 * x * (xx - 3.f * yy);
-        PUT(9, dRGBdsh9 * dL_dRGB);
-        PUT(10, dRGBdsh10 * dL_dRGB);
-        PUT(11, dRGBdsh11 * dL_dRGB);
-        PUT(12, dRGBdsh12 * dL_dRGB);
-        PUT(13, dRGBdsh13 * dL_dRGB);
-        PUT(14, dRGBdsh14 * dL_dRGB);
-        PUT(15, dRGBdsh15 * dL_dRGB);
-        // backward.cu:99-122: (scalar * vec3) followed by vec3 * scalar products, summed left to right
-        V3 ax = (((SH_C3_0 * SH(9)) * 3.f) * 2.f) * xy;
-        ax = ax + (SH_C3_1 * SH(10)) * yz;
-        ax = ax + ((SH_C3_2 * SH(11)) * -2.f) * xy;
-        ax = ax + (((SH_C3_3 * SH(12)) * -3.f) * 2.f) * xz;
-        ax = ax + (SH_C3_4 * SH(13)) * (-3.f * xx + 4.f * zz - yy);
-        ax = ax + ((SH_C3_5 * SH(14)) * 2.f) * xz;
-        ax = ax + ((SH_C3_6 * SH(15)) * 3.f) * (xx - yy);
-        V3 ay = ((SH_C3_0 * SH(9)) * 3.f) * (xx - yy);
-        ay = ay + (SH_C3_1 * SH(10)) * xz;
-        ay = ay + (SH_C3_2 * SH(11)) * (-3.f * yy + 4.f * zz - xx);
-        ay = ay + (((SH_C3_3 * SH(12)) * -3.f) * 2.f) * yz;
-        ay = ay + ((SH_C3_4 * SH(13)) * -2.f) * xy;
-        ay = ay + ((SH_C3_5 * SH(14)) * -2.f) * yz;
-        ay = ay + (((SH_C3_6 * SH(15)) * -3.f) * 2.f) * xy;
-        V3 az = (SH_C3_1 * SH(10)) * xy;
-        az = az + (((SH_C3_2 * SH(11)) * 4.f) * 2.f) * yz;
-        az = az + ((SH_C3_3 * SH(12)) * 3.f) * (2.f * zz - xx - yy);
-        az = az + (((SH_C3_4 * SH(13)) * 4.f) * 2.f) * xz;
-        az = az + (SH_C3_5 * SH(14)) * (xx - yy);
-        dRGBdx = dRGBdx + ax;
-        dRGBdy = dRGBdy + ay;
-        dRGBdz = dRGBdz + az;
+  if (WRITE) {
+    float b[16];
+    sh_basis_dir(dir, deg, b);
+    float* d = s0;
+    d[0] = b[0] * dL_dRGB.x; d[1] = b[0] * dL_dRGB.y; d[2] = b[0] * dL_dRGB.z;
+#pragma unroll
+    for (int k = 1; k < 16; k++) {
+      if (k < ncoef_used) {
+        d = s1 + 3 * k - 3;
+        const V3 t = b[k] * dL_dRGB;
+        d[0] = t.x; d[1] = t.y; d[2] = t.z;
       }
     }
   }
-#undef PUT
-#undef SH
+  V3 dRGBdx, dRGBdy, dRGBdz;
+  sh_dir_jacobian(c, deg, dir, dRGBdx, dRGBdy, dRGBdz);
   const V3 dL_ddir = v3(dot3(dRGBdx, dL_dRGB), dot3(dRGBdy, dL_dRGB), dot3(dRGBdz, dL_dRGB));
-  // auxiliary.h:107-117 dnormvdv
-  const V3 v = dir_orig, dv = dL_ddir;
-  const float sum2 = v.x * v.x + v.y * v.y + v.z * v.z;
-  const float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
-  return v3(((+sum2 - v.x * v.x) * dv.x - v.y * v.x * dv.y - v.z * v.x * dv.z) * invsum32,
-            (-v.x * v.y * dv.x + (sum2 - v.y * v.y) * dv.y - v.z * v.y * dv.z) * invsum32,
-            (-v.x * v.z * dv.x - v.y * v.z * dv.y + (sum2 - v.z * v.z) * dv.z) * invsum32);
+  return dnormvdv(dir_orig, dL_ddir);
 }
 
 // Culled Gaussian, store mode: zero every per-Gaussian output except the SH grads (those are
@@ -277,7 +201,13 @@ __device__ __forceinline__ void gaussian_bwd(const BwdPreArgs& a, size_t i, floa
     dRGB.y *= (cl & 2) ? 0 : 1;
     dRGB.z *= (cl & 4) ? 0 : 1;
     const V3 dir_orig = mean - v3(a.campos[0], a.campos[1], a.campos[2]);
-    if (a.dRGB_out) {  // deferred: dL/dsh = basis(dir) x dRGB is formed by the step's flush
+    if (a.dRGB_out && a.pre_jac) {  // deferred, Jacobian from the multi-view pre-pass
+      put3(a.dRGB_out, i, dRGB);
+      const float* j = a.pre_jac + 9 * i;
+      const V3 jx = v3(j[0], j[1], j[2]), jy = v3(j[3], j[4], j[5]), jz = v3(j[6], j[7], j[8]);
+      const V3 dL_ddir = v3(dot3(jx, dRGB), dot3(jy, dRGB), dot3(jz, dRGB));
+      dmean = dmean + dnormvdv(dir_orig, dL_ddir);
+    } else if (a.dRGB_out) {  // deferred: dL/dsh = basis(dir) x dRGB is formed by the step's flush
       put3(a.dRGB_out, i, dRGB);
       dmean = dmean + sh_backward<false>(sh0, sh1, a.D, dir_orig, dRGB);
     } else {
@@ -385,7 +315,8 @@ __global__ __launch_bounds__(kThreads) void preprocess_bwd_kernel(BwdPreArgs a) 
   const size_t i = (size_t)base + t;
   const bool live = t < n && a.radii[i] > 0;
   s_live[t] = live;
-  const bool has_sh = a.shs || a.fused;
+  // the SH rows are staged unless the colour Jacobian comes from the multi-view pre-pass
+  const bool has_sh = (a.shs || a.fused) && !a.pre_jac;
   ShPlane p0{}, p1{};
   if (has_sh) {
     const int ncoef = a.M * 3;
@@ -431,38 +362,6 @@ __global__ __launch_bounds__(kThreads) void preprocess_bwd_kernel(BwdPreArgs a) 
 // with the same basis arithmetic as sh_backward, summed in registers, written once (store) or
 // added once (ACC) through the LDS staging planes -- instead of one 192-byte read-modify-write of
 // the SH gradient rows per view.
-__device__ __forceinline__ void sh_basis(V3 dir_orig, int deg, float (&b)[16]) {
-  const float len = sqrtf(dot3(dir_orig, dir_orig));
-  const V3 dir = v3(dir_orig.x / len, dir_orig.y / len, dir_orig.z / len);
-  const float x = dir.x, y = dir.y, z = dir.z;
-#pragma unroll
-  for (int k = 0; k < 16; k++) b[k] = 0.0f;
-  b[0] = SH_C0;
-  if (deg > 0) {
-    b[1] = -SH_C1 * y;
-    b[2] = SH_C1 * z;
-    b[3] = -SH_C1 * x;
-    if (deg > 1) {
-      const float xx = x * x, yy = y * y, zz = z * z;
-      const float xy = x * y, yz = y * z, xz = x * z;
-      b[4] = SH_C2_0 * xy;
-      b[5] = SH_C2_1 * yz;
-      b[6] = SH_C2_2 * (2.f * zz - xx - yy);
-      b[7] = SH_C2_3 * xz;
-      b[8] = SH_C2_4 * (xx - yy);
-      if (deg > 2) {
-        b[9] = SH_C3_0 * y * (3.f * xx - yy);
-        b[10] = SH_C3_1 * xy * z;
-        b[11] = SH_C3_2 * y * (4.f * zz - xx - yy);
-        b[12] = SH_C3_3 * z * (2.f * zz - 3.f * xx - 3.f * yy);
-        b[13] = SH_C3_4 * x * (4.f * zz - xx - yy);
-        b[14] = SH_C3_5 * z * (xx - yy);
-        b[15] = SH_C3_6 * x * (xx - 3.f * yy);
-      }
-    }
-  }
-}
-
 template <bool ACC>
 __global__ __launch_bounds__(kThreads) void sh_flush_kernel(ShFlushArgs a) {
   __shared__ float4 s_sh4[kThreads * kShMaxFloats / 4];
@@ -482,7 +381,7 @@ __global__ __launch_bounds__(kThreads) void sh_flush_kernel(ShFlushArgs a) {
     for (int v = 0; v < a.nviews; v++) {
       const float* cp = a.campos[v];
       float b[16];
-      sh_basis(mean - v3(cp[0], cp[1], cp[2]), a.D, b);
+      sh_basis(mean - v3(cp[0], cp[1], cp[2]), a.D, b);  // gsr_sh.h
       const float* d = a.dRGB[v] + 3 * i;
       const V3 dRGB = v3(d[0], d[1], d[2]);
 #pragma unroll

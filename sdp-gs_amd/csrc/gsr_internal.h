@@ -163,6 +163,7 @@ ImgState carve_img(char* base, size_t W, size_t H);
 int tile_schedule_mode();
 
 // ---- per-Gaussian kernels (gsr_preprocess.hip, gsr_backward.hip) ----------------------------------
+constexpr int kShFlushMaxViewsFwd = 8;
 struct PreArgs {
   int P, D, M, W, H;
   uint32_t gx, gy;
@@ -182,8 +183,21 @@ struct PreArgs {
   // backward's per-Gaussian gradient accumulator rows g.acc
   SideClear clear;
   int acc_zero;
+  // multi-view colour pre-pass (fused only): when non-null, the SH colour of this view and its
+  // clamp bits come precomputed (gsr_sh_precolor) instead of being evaluated from the SH rows
+  const float* pre_color;
+  const uint8_t* pre_clamp;
 };
 hipError_t launch_preprocess(const PreArgs& a, hipStream_t s);
+struct PrecolorArgs {
+  int P, M, D, nviews;
+  const float *means3D, *sh_dc, *sh_rest;
+  const float* campos[kShFlushMaxViewsFwd];
+  float* color[kShFlushMaxViewsFwd];     // [P,3]
+  uint8_t* clamp[kShFlushMaxViewsFwd];   // [P]
+  float* jac[kShFlushMaxViewsFwd];       // [P,9]: dRGB/ddir_x, _y, _z (vec3 over the channels)
+};
+hipError_t launch_sh_precolor(const PrecolorArgs& a, hipStream_t s);
 // test hook: ref = OCML expf(x), fast = blend_expf(x) (gsr_device.h)
 hipError_t launch_expf_pair(const float* x, float* ref, float* fast, size_t n, hipStream_t s);
 hipError_t launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present,
@@ -213,6 +227,9 @@ struct BwdPreArgs {
   // clamp-masked colour gradient dL/dRGB [P,3] (zeros when culled) is stored here for
   // launch_sh_grad_flush, which forms dL/dsh = basis(dir) x dL/dRGB for all views of a step
   float* dRGB_out;
+  // with dRGB_out: the SH colour's direction Jacobian of this view from the pre-pass ([P,9]); the
+  // SH rows are then not read at all
+  const float* pre_jac;
 };
 hipError_t launch_preprocess_backward(const BwdPreArgs& a, hipStream_t s);
 constexpr int kShFlushMaxViews = 8;

@@ -14,6 +14,8 @@
 // so the blend reads one contiguous record per instance instead of five scattered arrays.
 #include "gsr_device.h"
 #include "gsr_internal.h"
+#include "gsr_sh.h"
+#include "gsr_stage.h"
 
 namespace gsr {
 namespace {
@@ -22,42 +24,6 @@ constexpr int kThreads = 256;
 #ifndef GSR_PRE_HOIST
 #define GSR_PRE_HOIST 0
 #endif
-
-// forward.cu:20-71 (float32, same evaluation order as the CPU restatement)
-// s0: coefficient 0 of this Gaussian, s1: its coefficients 1.. (contiguous); for the reference's
-// [P,M,3] layout s1 = s0 + 3, for the fused split layout s0 = features_dc, s1 = features_rest.
-__device__ __forceinline__ V3 sh_to_rgb(const float* __restrict__ s0, const float* __restrict__ s1,
-                                        int deg, V3 dir, uint8_t& clamped) {
-#define SH(k) ((k) == 0 ? v3(s0[0], s0[1], s0[2]) \
-                        : v3(s1[3 * ((k) - 1)], s1[3 * ((k) - 1) + 1], s1[3 * ((k) - 1) + 2]))
-  V3 result = SH_C0 * SH(0);
-  if (deg > 0) {
-    const float x = dir.x, y = dir.y, z = dir.z;
-    result = ((result - (SH_C1 * y) * SH(1)) + (SH_C1 * z) * SH(2)) - (SH_C1 * x) * SH(3);
-    if (deg > 1) {
-      const float xx = x * x, yy = y * y, zz = z * z;
-      const float xy = x * y, yz = y * z, xz = x * z;
-      result = result + (SH_C2_0 * xy) * SH(4);
-      result = result + (SH_C2_1 * yz) * SH(5);
-      result = result + (SH_C2_2 * (2.0f * zz - xx - yy)) * SH(6);
-      result = result + (SH_C2_3 * xz) * SH(7);
-      result = result + (SH_C2_4 * (xx - yy)) * SH(8);
-      if (deg > 2) {
-        result = result + (SH_C3_0 * y * (3.0f * xx - yy)) * SH(9);
-        result = result + (SH_C3_1 * xy * z) * SH(10);
-        result = result + (SH_C3_2 * y * (4.0f * zz - xx - yy)) * SH(11);
-        result = result + (SH_C3_3 * z * (2.0f * zz - 3.0f * xx - 3.0f * yy)) * SH(12);
-        result = result + (SH_C3_4 * x * (4.0f * zz - xx - yy)) * SH(13);
-        result = result + (SH_C3_5 * z * (xx - yy)) * SH(14);
-        result = result + (SH_C3_6 * x * (xx - 3.0f * yy)) * SH(15);
-      }
-    }
-  }
-#undef SH
-  result = v3(result.x + 0.5f, result.y + 0.5f, result.z + 0.5f);
-  clamped = (uint8_t)((result.x < 0) | ((result.y < 0) << 1) | ((result.z < 0) << 2));
-  return v3(fmaxf(result.x, 0.0f), fmaxf(result.y, 0.0f), fmaxf(result.z, 0.0f));
-}
 
 __global__ __launch_bounds__(kThreads) void preprocess_kernel(PreArgs a) {
   // one lane per Gaussian; SH rows are read directly (an LDS-staged variant, gsr_stage.h, measured
@@ -135,7 +101,10 @@ __global__ __launch_bounds__(kThreads) void preprocess_kernel(PreArgs a) {
   if ((x1 - x0) * (y1 - y0) == 0) return;
 
   float cr, cg, cb;
-  if (a.colors_precomp == nullptr) {
+  if (a.pre_color) {  // multi-view pre-pass: the same sh_to_rgb, evaluated for all views at once
+    cr = a.pre_color[3 * idx]; cg = a.pre_color[3 * idx + 1]; cb = a.pre_color[3 * idx + 2];
+    g.clamped[idx] = a.pre_clamp[idx];
+  } else if (a.colors_precomp == nullptr) {
     V3 dir = p_orig - v3(a.campos[0], a.campos[1], a.campos[2]);
     const float len = sqrtf(dot3(dir, dir));
     dir = v3(dir.x / len, dir.y / len, dir.z / len);
@@ -198,6 +167,58 @@ __global__ __launch_bounds__(kThreads) void preprocess_kernel(PreArgs a) {
   rec[3] = make_float4(f2, (float)r, qc, 0.f);
 }
 
+// Multi-view colour pre-pass (gsr_amd/pipeline.py): one pass over the SH rows serves the
+// forward colour and the backward's colour Jacobian of every view of a step, instead of every
+// view's preprocess and backward preprocess reading the 192-byte rows again.  Per Gaussian and
+// view: sh_to_rgb (forward.cu:20-71, the forward's own function) -> colour [P,3] + clamp bits,
+// and sh_dir_jacobian (backward.cu:56-131) -> dRGB/ddir [P,9].  The rows go through LDS
+// (gsr_stage.h) so the global reads are coalesced 16-byte vectors.
+__global__ __launch_bounds__(kThreads) void sh_precolor_kernel(PrecolorArgs a) {
+  __shared__ float4 s_sh4[kThreads * kShMaxFloats / 4];
+  __shared__ uint8_t s_live[kThreads];
+  float* s_sh = reinterpret_cast<float*>(s_sh4);
+  const int base = (int)(blockIdx.x * kThreads);
+  const int n = min(kThreads, a.P - base);
+  const int t = (int)threadIdx.x;
+  const size_t i = (size_t)base + t;
+  s_live[t] = t < n;
+  const ShPlane p0{a.sh_dc, nullptr, 3, 0};
+  const ShPlane p1{a.sh_rest, nullptr, (a.M - 1) * 3, kThreads * 3};
+  __syncthreads();
+  stage<kThreads, true, false>(p0, base, n, s_live, s_sh);
+  stage<kThreads, true, false>(p1, base, n, s_live, s_sh);
+  __syncthreads();
+  if (t >= n) return;
+  const float* r0 = s_sh + p0.lds + t * p0.w;
+  const float* r1 = s_sh + p1.lds + t * p1.w;
+  const int used = (a.D + 1) * (a.D + 1);
+  V3 c[16];
+  c[0] = v3(r0[0], r0[1], r0[2]);
+#pragma unroll
+  for (int k = 1; k < 16; k++)
+    c[k] = (k < used && k < a.M) ? v3(r1[3 * k - 3], r1[3 * k - 2], r1[3 * k - 1]) : v3(0, 0, 0);
+  const V3 p_orig = v3(a.means3D[3 * i], a.means3D[3 * i + 1], a.means3D[3 * i + 2]);
+  for (int v = 0; v < a.nviews; v++) {
+    const float* cp = a.campos[v];
+    const V3 dir_orig = p_orig - v3(cp[0], cp[1], cp[2]);
+    // forward: gsr_preprocess_kernel's direction and colour
+    const float len = sqrtf(dot3(dir_orig, dir_orig));
+    const V3 dir = v3(dir_orig.x / len, dir_orig.y / len, dir_orig.z / len);
+    uint8_t cl;
+    const V3 col = sh_to_rgb(r0, r1, a.D, dir, cl);
+    float* co = a.color[v] + 3 * i;
+    co[0] = col.x; co[1] = col.y; co[2] = col.z;
+    a.clamp[v][i] = cl;
+    // backward: sh_backward's Jacobian at the same normalised direction
+    V3 jx, jy, jz;
+    sh_dir_jacobian(c, a.D, dir, jx, jy, jz);
+    float* jo = a.jac[v] + 9 * i;
+    jo[0] = jx.x; jo[1] = jx.y; jo[2] = jx.z;
+    jo[3] = jy.x; jo[4] = jy.y; jo[5] = jy.z;
+    jo[6] = jz.x; jo[7] = jz.y; jo[8] = jz.z;
+  }
+}
+
 __global__ __launch_bounds__(kThreads) void mark_visible_kernel(int P, const float* __restrict__ m,
                                                                 const float* __restrict__ view,
                                                                 uint8_t* __restrict__ present) {
@@ -212,6 +233,13 @@ __global__ __launch_bounds__(kThreads) void mark_visible_kernel(int P, const flo
 hipError_t launch_preprocess(const PreArgs& a, hipStream_t s) {
   if (a.P == 0) return hipSuccess;
   hipLaunchKernelGGL(preprocess_kernel, dim3((a.P + kThreads - 1) / kThreads), dim3(kThreads), 0,
+                     s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_sh_precolor(const PrecolorArgs& a, hipStream_t s) {
+  if (a.P == 0 || a.nviews <= 0) return hipSuccess;
+  hipLaunchKernelGGL(sh_precolor_kernel, dim3((a.P + kThreads - 1) / kThreads), dim3(kThreads), 0,
                      s, a);
   return hipGetLastError();
 }

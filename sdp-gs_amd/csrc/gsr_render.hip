@@ -84,6 +84,20 @@ __global__ __launch_bounds__(kSchedThreads) void tile_schedule_kernel(const uint
 #ifndef GSR_BWD_FAST_DIV
 #define GSR_BWD_FAST_DIV 1
 #endif
+// instrumentation build (-DGSR_BLEND_STATS=1): per-wave work counters of both blends, read with
+// gsr_test_blend_stats (scripts/blend_stats.py); off in the product build
+#ifndef GSR_BLEND_STATS
+#define GSR_BLEND_STATS 0
+#endif
+#if GSR_BLEND_STATS
+// [0] fwd list entries, [1] fwd entries evaluated, [2] fwd entries with a contributing lane,
+// [3] fwd contributing (lane, entry) pairs, [4] bwd list entries, [5] bwd groups evaluated,
+// [6] bwd entries with a contributing lane, [7] bwd contributing pairs, [8] waves
+__device__ unsigned long long g_blend_stats[16];
+#define BLEND_STAT(k, v) do { if ((threadIdx.x & 63) == 0) atomicAdd(&g_blend_stats[k], (unsigned long long)(v)); } while (0)
+#else
+#define BLEND_STAT(k, v) do { } while (0)
+#endif
 // forward: 1 = blend weight alpha * T formed once per pair, 0 = col * alpha * T per channel
 #ifndef GSR_FWD_WEIGHT
 #define GSR_FWD_WEIGHT 1
@@ -188,12 +202,14 @@ __global__ __launch_bounds__(kThreads) void render_fwd_kernel(RenderArgs a) {
     __syncthreads();
     const uint32_t cnt = min((uint32_t)kThreads, range.y - base);
     const uint32_t nlist = build_wave_list(s_mask, s_list[wid], cnt, wid, lane);
+    BLEND_STAT(0, nlist);
     const uint32_t rel0 = base - range.x;
     // Four list entries per iteration: their (independent) Gaussian weights are evaluated
     // together, then composited in list order exactly as the reference's per-splat loop
     // (forward.cu:325-362) -- same operations, same order, per pixel.
     for (uint32_t k = 0; k < nlist; k += 4) {
       if (__ballot(!done) == 0ull) break;  // wave-uniform
+      BLEND_STAT(1, min(4u, nlist - k));
       const uint32_t packed = *reinterpret_cast<const uint32_t*>(&s_list[wid][k]);
       uint32_t jj[4];
       float pw[4], al[4];
@@ -212,6 +228,13 @@ __global__ __launch_bounds__(kThreads) void render_fwd_kernel(RenderArgs a) {
         pw[u] = (k + u < nlist) ? power : 1.0f;
         al[u] = fminf(0.99f, r1v[u].y * blend_expf(pw[u]));
       }
+#if GSR_BLEND_STATS
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const uint64_t cb = __ballot(!done && !(pw[u] > 0.0f) && !(al[u] < 1.0f / 255.0f));
+        if (cb) { BLEND_STAT(2, 1); BLEND_STAT(3, __popcll(cb)); }
+      }
+#endif
 #pragma unroll
       for (int u = 0; u < 4; u++) {
         if (done) continue;
@@ -389,6 +412,7 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
 
   const uint2 range = a.ranges[tile];
   const uint32_t tile_last = a.tile_last[tile];
+  BLEND_STAT(8, 1);
   const float T_final = inside ? a.final_T[pix] : 0.0f;
   float T = T_final;
   const uint32_t last_contributor = inside ? a.n_contrib[pix] : 0u;
@@ -461,6 +485,7 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
     }
     __syncthreads();
     const uint32_t nlist = build_wave_list(s_mask, s_list[wid], cnt, wid, lane);
+    BLEND_STAT(4, nlist);
     // Four list entries per group: the cheap per-pair test (power, G, alpha) of all four is
     // evaluated first (independent work), then the entries are replayed in list order.
     for (uint32_t k0 = 0; k0 < nlist; k0 += GROUP) {
@@ -473,6 +498,7 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
       const uint32_t jl = (packed >> (8 * ulast)) & 0xffu;
       if (tile_last - 1 - done_cnt - jl >= wave_last) continue;  // wave-uniform
     }
+    BLEND_STAT(5, 1);
     float Gv[GROUP], av[GROUP];
     bool cv[GROUP];
 #pragma unroll
@@ -493,6 +519,8 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
       const bool contrib = cv[u];
       const uint64_t cmask = __ballot(contrib);
       if (cmask == 0ull) continue;  // wave-uniform skip
+      BLEND_STAT(6, 1);
+      BLEND_STAT(7, __popcll(cmask));
       const uint32_t j = (packed >> (8 * u)) & 0xffu;
       // Branch-free: a lane whose pixel does not take this splat runs the same arithmetic with
       // G = alpha = 0, which makes every gradient term exactly zero and T / (1 - 0) == T; its
@@ -598,6 +626,17 @@ __global__ void expf_pair_kernel(const float* __restrict__ x, float* __restrict_
 }
 
 }  // namespace
+
+#if GSR_BLEND_STATS
+extern "C" int gsr_test_blend_stats(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_blend_stats), sizeof(g_blend_stats)) != hipSuccess) return 2;
+  if (reset) {
+    unsigned long long z[16] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_blend_stats), z, sizeof(z)) != hipSuccess) return 2;
+  }
+  return 0;
+}
+#endif
 
 hipError_t launch_expf_pair(const float* x, float* ref, float* fast, size_t n, hipStream_t s) {
   if (n == 0) return hipSuccess;

@@ -286,16 +286,22 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
         L = _lib.load()
         nr = _lib.ctypes.c_int(0)
         stream = torch.cuda.current_stream(dev).cuda_stream
+        pre = _precolor_lookup(dev, campos, m3, dc, rest, int(rs.sh_degree), M)
         try:
             with torch.cuda.device(dev):
-                rc = L.gsr_rasterize_gaussians_fused(
-                    P, M, _ptr(bg), _ptr(m3), _ptr(dc), _ptr(rest), _ptr(op), _ptr(sc), _ptr(rot),
-                    float(rs.scale_modifier), _ptr(view), _ptr(proj), float(rs.tanfovx),
-                    float(rs.tanfovy), H, W, int(rs.sh_degree), _ptr(campos),
-                    int(bool(rs.prefiltered)), _ptr(lf), _ptr(conf), int(include_feature),
-                    _ptr(color), _ptr(depth), _ptr(alpha), _ptr(feature), _ptr(radii),
-                    _lib.ctypes.byref(nr), _lib.alloc_callback(), holder.key, stream,
-                    int(bool(rs.debug)))
+                head = (P, M, _ptr(bg), _ptr(m3), _ptr(dc), _ptr(rest), _ptr(op), _ptr(sc),
+                        _ptr(rot), float(rs.scale_modifier), _ptr(view), _ptr(proj),
+                        float(rs.tanfovx), float(rs.tanfovy), H, W, int(rs.sh_degree),
+                        _ptr(campos), int(bool(rs.prefiltered)), _ptr(lf), _ptr(conf),
+                        int(include_feature))
+                tail = (_ptr(color), _ptr(depth), _ptr(alpha), _ptr(feature), _ptr(radii),
+                        _lib.ctypes.byref(nr), _lib.alloc_callback(), holder.key, stream,
+                        int(bool(rs.debug)))
+                if pre is not None:  # colour + clamp bits from the multi-view pre-pass
+                    rc = L.gsr_rasterize_gaussians_fused_precolor(
+                        *head, _ptr(pre[0]), _ptr(pre[1]), *tail)
+                else:
+                    rc = L.gsr_rasterize_gaussians_fused(*head, *tail)
             _lib.check(rc)
         finally:
             holder.release()
@@ -305,6 +311,7 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
 
         ctx.raster_settings = rs
         ctx.num_rendered = num_rendered
+        ctx.pre_jac = None if pre is None else pre[2]
         # grad-into-leaves mode: only when every differentiable input is itself the float32
         # contiguous leaf (then the kernel's pointer IS the parameter's storage)
         leaves = (means3D, features_dc, features_rest, opacity_raw, scaling_raw, rotation_raw,
@@ -411,7 +418,8 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
                 int(mt["include_feature"]), _ptr(geom) if geom.numel() else None,
                 _ptr(binning) if binning.numel() else None, _ptr(image) if image.numel() else None,
                 _ptr(d_means2D), _ptr(d_means3D), _ptr(d_dc), _ptr(d_rest), _ptr(d_op),
-                _ptr(d_sc), _ptr(d_rot), _ptr(d_lf), _ptr(d_rgb), int(accumulate), stream,
+                _ptr(d_sc), _ptr(d_rot), _ptr(d_lf), _ptr(d_rgb),
+                _ptr(ctx.pre_jac) if d_rgb is not None else None, int(accumulate), stream,
                 int(bool(rs.debug)))
         _lib.check(rc)
         if into_leaves:
@@ -428,6 +436,66 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
 _GRAD_INTO_LEAVES = None
 # device index -> ShGradDeferral collecting the views of the current multi-view step
 _SH_DEFER = {}
+# device index -> ShPrecolor of the current multi-view step
+_PRECOLOR = {}
+
+
+def _precolor_lookup(dev, campos, m3, dc, rest, degree, M):
+    pc = _PRECOLOR.get(dev.index)
+    if pc is None:
+        return None
+    return pc.lookup(campos, m3, dc, rest, degree, M)
+
+
+class ShPrecolor:
+    """Multi-view colour pre-pass of one step on one device (include/gsr.h gsr_sh_precolor).
+    One pass over the SH rows computes, for every camera of the step, the fused forward's colour
+    and clamp bits and the backward's colour Jacobian; while installed (``with``), fused
+    forwards whose camera centre (same tensor), leaves and SH degree match use them instead of
+    reading the 192-byte SH rows again, and -- under ShGradDeferral -- so do their backwards.
+    Outputs are identical (the same device functions, gsr_sh.h)."""
+
+    def __init__(self, means3D, features_dc, features_rest, degree, campos_list):
+        self.device = means3D.device
+        self.keys = (means3D.data_ptr(), features_dc.data_ptr(),
+                     features_rest.data_ptr() if features_rest is not None else 0, int(degree))
+        P = int(means3D.shape[0])
+        self.M = 1 + (features_rest.numel() // (3 * P) if features_rest is not None and P else 0)
+        fopts = dict(dtype=torch.float32, device=self.device)
+        self.views = {}
+        cams = [_dev_f32(c, "campos", self.device) for c in campos_list]
+        bufs = [(torch.empty((P, 3), **fopts), torch.empty((P,), dtype=torch.uint8, device=self.device),
+                 torch.empty((P, 9), **fopts)) for _ in cams]
+        n = len(cams)
+        if n and P:
+            arr = lambda xs: (_lib.ctypes.c_void_p * n)(*[x.data_ptr() for x in xs])  # noqa: E731
+            with torch.cuda.device(self.device):
+                rc = _lib.load().gsr_sh_precolor(
+                    P, self.M, int(degree), _ptr(means3D.contiguous()), _ptr(features_dc),
+                    _ptr(features_rest), n, arr(cams), arr([b[0] for b in bufs]),
+                    arr([b[1] for b in bufs]), arr([b[2] for b in bufs]),
+                    torch.cuda.current_stream(self.device).cuda_stream)
+            _lib.check(rc)
+        for c, b in zip(cams, bufs):
+            self.views[c.data_ptr()] = b
+        self._campos = cams  # keep the keyed tensors alive
+
+    def lookup(self, campos, m3, dc, rest, degree, M):
+        keys = (m3.data_ptr(), dc.data_ptr(), rest.data_ptr() if rest is not None else 0,
+                int(degree))
+        if keys != self.keys or M != self.M:
+            return None
+        return self.views.get(campos.data_ptr())
+
+    def __enter__(self):
+        if self.device.index in _PRECOLOR:
+            raise RuntimeError("a colour pre-pass is already active on this device")
+        _PRECOLOR[self.device.index] = self
+        return self
+
+    def __exit__(self, *exc):
+        _PRECOLOR.pop(self.device.index, None)
+        return False
 
 
 class ShGradDeferral:

@@ -86,6 +86,9 @@ def load():
             ctypes.POINTER(_i),          # num_rendered
             ALLOC_FN, _p,                # alloc, alloc_ctx
             _p, _i]                      # stream, debug
+        L.gsr_rasterize_gaussians_fused_precolor.restype = _i
+        fa = L.gsr_rasterize_gaussians_fused.argtypes
+        L.gsr_rasterize_gaussians_fused_precolor.argtypes = fa[:22] + [_p, _p] + fa[22:]
         L.gsr_rasterize_gaussians_fused_backward.restype = _i
         L.gsr_rasterize_gaussians_fused_backward.argtypes = [
             _i, _i, _i,                  # P, M, R
@@ -102,7 +105,10 @@ def load():
             _p, _i]                      # stream, debug
         L.gsr_rasterize_gaussians_fused_backward_deferred.restype = _i
         L.gsr_rasterize_gaussians_fused_backward_deferred.argtypes = (
-            L.gsr_rasterize_gaussians_fused_backward.argtypes[:-3] + [_p, _i, _p, _i])
+            L.gsr_rasterize_gaussians_fused_backward.argtypes[:-3] + [_p, _p, _i, _p, _i])
+        L.gsr_sh_precolor.restype = _i
+        L.gsr_sh_precolor.argtypes = [_i, _i, _i, _p, _p, _p, _i, ctypes.POINTER(_p),
+                                      ctypes.POINTER(_p), ctypes.POINTER(_p), ctypes.POINTER(_p), _p]
         L.gsr_sh_grad_flush.restype = _i
         L.gsr_sh_grad_flush.argtypes = [_i, _i, _i, _p, _i, ctypes.POINTER(_p),
                                         ctypes.POINTER(_p), _p, _p, _i, _p]

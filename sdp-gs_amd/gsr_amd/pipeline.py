@@ -16,6 +16,11 @@ clamp-masked colour gradient dL/dRGB [P,3] instead of read-modify-writing the 19
 gradient rows, and run() writes features_dc / features_rest .grad once at the end
 (diff_gaussian_rasterization.ShGradDeferral): the SH gradient of a view is basis(dir) x dL/dRGB,
 so the per-view SH traffic drops from 384 to 12 bytes per Gaussian.
+
+With precolor (default) and the model passed to run(), one pre-pass over the SH rows computes
+every view's colour, clamp bits and colour Jacobian up front (diff_gaussian_rasterization.
+ShPrecolor, gsr_sh_precolor); the views' forward and backward preprocesses then read 12 + 1 and
+36 bytes per Gaussian instead of the 192-byte SH rows each.
 """
 from __future__ import annotations
 
@@ -33,29 +38,38 @@ class ViewPipeline:
     ``depth - 1`` side streams, joined back into the current stream at the end of run()."""
 
     def __init__(self, device: Optional[torch.device] = None, depth: int = 2,
-                 defer_sh: bool = True):
+                 defer_sh: bool = True, precolor: bool = True):
         if depth < 1:
             raise ValueError("depth must be >= 1")
         self.device = torch.device(device) if device is not None else torch.device(
             "cuda", torch.cuda.current_device())
         self.depth = depth
         self.defer_sh = defer_sh
+        self.precolor = precolor
         self.side = [torch.cuda.Stream(device=self.device) for _ in range(depth - 1)]
 
-    def run(self, items: Iterable[T], fn: Callable[[T], R]) -> List[R]:
+    def run(self, items: Iterable[T], fn: Callable[[T], R], model=None,
+            campos_of: Callable[[T], torch.Tensor] = lambda cam: cam.camera_center) -> List[R]:
         """Call fn(item) for every item, item i issued on stream i mod depth.  fn should do a
         view's render + backward and return host values (or tensors it no longer needs on the
         device): tensors created on a side stream and used after run() on the main stream need
         Tensor.record_stream to be safe under the caching allocator.  With defer_sh the SH
-        leaves' .grad is complete when run() returns, not after each view."""
+        leaves' .grad is complete when run() returns, not after each view.  model (a
+        GaussianModel: _xyz, _features_dc, _features_rest, active_sh_degree) enables the colour
+        pre-pass for the cameras campos_of(item)."""
         import diff_gaussian_rasterization as dgr
+        items = list(items)
         main = torch.cuda.current_stream(self.device)
         streams = [main] + self.side
+        pre = contextlib.nullcontext()
+        if self.precolor and model is not None and items:
+            pre = dgr.ShPrecolor(model._xyz, model._features_dc, model._features_rest,
+                                 model.active_sh_degree, [campos_of(it) for it in items])
         for s in self.side:
-            s.wait_stream(main)  # inputs prepared on the main stream (zeroed grads, cameras)
+            s.wait_stream(main)  # inputs prepared on the main stream (zeroed grads, pre-pass)
         out = []
         defer = dgr.ShGradDeferral(self.device) if self.defer_sh else contextlib.nullcontext()
-        with defer:  # exit: the SH gradients of all views, on the main stream after the join
+        with pre, defer:  # defer's exit: the SH gradients of all views, after the join
             for i, it in enumerate(items):
                 s = streams[i % self.depth]
                 with torch.cuda.stream(s):

@@ -148,9 +148,10 @@ def test_grad_into_leaves_equals_autograd_accumulation():
 def test_view_pipeline_two_streams_equals_sequential(into_leaves):
     """gsr_amd.pipeline.ViewPipeline: six views issued round-robin on two HIP streams (view k+1's
     forward overlapping view k's backward; grad-into-leaves read-modify-writes ordered by the
-    library's per-device event) and, by default, SH gradients deferred to one flush per step
-    (diff_gaussian_rasterization.ShGradDeferral) give the same accumulated gradients and per-view
-    screen-space gradients as the strictly sequential loop (to float-atomic ordering)."""
+    library's per-device event), SH gradients deferred to one flush per step
+    (diff_gaussian_rasterization.ShGradDeferral) and the multi-view colour pre-pass (ShPrecolor),
+    in every combination, give the same accumulated gradients and per-view screen-space gradients
+    as the strictly sequential loop (to float-atomic ordering)."""
     import diff_gaussian_rasterization as dgr
     from gsr_amd.pipeline import ViewPipeline
     render, m, _ = _setup()
@@ -159,16 +160,17 @@ def test_view_pipeline_two_streams_equals_sequential(into_leaves):
     res = []
     try:
         dgr.grad_into_leaves(into_leaves)
-        for depth, defer in ((1, False), (2, True), (1, True), (2, False)):
+        for depth, defer, pre in ((1, False, False), (2, True, True), (1, True, False),
+                                  (2, False, True), (3, True, True)):
             _zero(m)
-            pipe = ViewPipeline(torch.device("cuda"), depth=depth, defer_sh=defer)
+            pipe = ViewPipeline(torch.device("cuda"), depth=depth, defer_sh=defer, precolor=pre)
 
             def one(c):
                 pkg = render(c, m, Pipe(sh_py=True), bg, Opt())
                 (pkg["render"].sum() + pkg["feature"].sum() + pkg["depth"].mean()).backward()
                 return pkg["viewspace_points"].grad.clone()
 
-            vs = pipe.run(cams, one)
+            vs = pipe.run(cams, one, model=m)
             torch.cuda.synchronize()
             res.append((_leaf_grads(m), vs))
     finally:
@@ -205,3 +207,21 @@ def test_sh_grad_deferral_accumulates_into_existing_grads():
         dgr.grad_into_leaves(False)
     for x, y in zip(*res):
         torch.testing.assert_close(x, y, rtol=1e-4, atol=1e-5 * y.abs().max().item())
+
+
+def test_precolor_forward_is_bit_identical():
+    """The multi-view colour pre-pass (gsr_sh_precolor, sh_to_rgb of gsr_sh.h) feeds the fused
+    forward exactly the colours and clamp bits its own preprocess computes: every output is
+    bitwise equal, and so is the backward through the precomputed Jacobian up to atomic order."""
+    import diff_gaussian_rasterization as dgr
+    render, m, _ = _setup()
+    cams = [c.to("cuda") for c in make_cameras(2, 200, 150, seed=6)]
+    bg = torch.tensor([0.1, 0.2, 0.3], device="cuda")
+    with torch.no_grad():
+        ref = [render(c, m, Pipe(sh_py=True), bg, Opt()) for c in cams]
+        with dgr.ShPrecolor(m._xyz, m._features_dc, m._features_rest, m.active_sh_degree,
+                            [c.camera_center for c in cams]):
+            got = [render(c, m, Pipe(sh_py=True), bg, Opt()) for c in cams]
+    for a, b in zip(ref, got):
+        for k in ("render", "depth", "alpha", "feature", "radii"):
+            assert torch.equal(a[k], b[k]), k
