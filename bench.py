@@ -55,17 +55,22 @@ class Opt:
     include_feature = True
 
 
-def algorithmic_bytes(stage, P, Pv, R, T, HW, D=3, C=8, tile_passes=2, acc=True, defer_sh=False):
+def algorithmic_bytes(stage, P, Pv, R, T, HW, D=3, C=8, tile_passes=2, acc=True, defer_sh=False,
+                      precolor=False):
     """Bytes each stage must move per launch.
     P Gaussians, Pv visible, R instances, T tiles, HW pixels, C blended channels (rgb, depth,
     alpha, feature x3), acc: the backward adds into existing gradients (read + write),
-    defer_sh: the SH gradients are replaced by a stored 12-B dL/dRGB (flushed once per step)."""
+    defer_sh: the SH gradients are replaced by a stored 12-B dL/dRGB (flushed once per step),
+    precolor: the SH rows are replaced by the pre-pass's colour + clamp (13 B, forward) and
+    colour Jacobian (36 B, backward)."""
     sh = 12 * (D + 1) ** 2
+    sh_fwd = 13 if precolor else sh
+    sh_bwd = 36 if (precolor and defer_sh) else sh
     grads = 12 + 12 + 4 + 12 + 16 + 12 + (0 if defer_sh else sh)  # means2D/3D, op, scale, rot, lang, SH
     return {
         # means (all); scale, rot, opacity, SH, language (visible); radii/tiles/key/value (all);
         # 64-B splat record + clamp bits (visible)
-        "preprocess": P * 12 + Pv * (12 + 16 + 4 + sh + 12) + P * 16 + Pv * (64 + 1),
+        "preprocess": P * 12 + Pv * (12 + 16 + 4 + sh_fwd + 12) + P * 16 + Pv * (64 + 1),
         # one-sweep: digit totals read the keys once, each 8-bit pass reads and writes key+value
         "depth_sort": P * 4 + 4 * P * 16,
         "scan": P * 12,
@@ -79,7 +84,7 @@ def algorithmic_bytes(stage, P, Pv, R, T, HW, D=3, C=8, tile_passes=2, acc=True,
         # same gathers, C upstream grads + final_T + n_contrib, one 64-B accumulator row per Gaussian
         "render_bwd": R * (4 + 64) + T * 12 + HW * (4 * C + 8) + Pv * 64,
         # accumulator row + per-Gaussian inputs (visible), radii (all), gradients (RMW when acc)
-        "preprocess_bwd": Pv * (64 + 12 + 12 + 16 + 4 + sh + 12 + 1) + P * 4
+        "preprocess_bwd": Pv * (64 + 12 + 12 + 16 + 4 + sh_bwd + 12 + 1) + P * 4
                           + ((2 * Pv) if acc else P) * grads + (P * 12 if defer_sh else 0),
     }[stage]
 
@@ -214,7 +219,7 @@ def main():
             continue
         avg_ms = ms / calls
         b = algorithmic_bytes(name, P, Pv, R, T, HW, D=deg, acc=not args.autograd_grads,
-                              defer_sh=defer_sh)
+                              defer_sh=defer_sh, precolor=not args.no_precolor)
         k = {"avg_ms": round(avg_ms, 4), "calls": int(calls), "bytes": int(b),
              "gbs": round(b / (avg_ms * 1e-3) / 1e9, 1)}
         if name in ("render_fwd", "render_bwd"):

@@ -304,9 +304,10 @@ __device__ __forceinline__ void gaussian_bwd(const BwdPreArgs& a, size_t i, floa
 // One workgroup = kThreads consecutive Gaussians.  The SH coefficients (48 of the ~60 floats a
 // Gaussian reads, and 48 of the grads it writes) go through LDS so that global traffic is
 // coalesced 16-byte vectors instead of lane-strided by 180-192 bytes.
-template <bool ACC>
+template <bool ACC, bool STAGE>
 __global__ __launch_bounds__(kThreads) void preprocess_bwd_kernel(BwdPreArgs a) {
-  __shared__ float4 s_sh4[kThreads * kShMaxFloats / 4];
+  // STAGE = false (colour Jacobian from the multi-view pre-pass): no SH rows, no 48 KB of LDS
+  __shared__ float4 s_sh4[STAGE ? kThreads * kShMaxFloats / 4 : 4];
   __shared__ uint8_t s_live[kThreads];
   float* s_sh = reinterpret_cast<float*>(s_sh4);
   const int base = (int)(blockIdx.x * kThreads);
@@ -316,7 +317,7 @@ __global__ __launch_bounds__(kThreads) void preprocess_bwd_kernel(BwdPreArgs a) 
   const bool live = t < n && a.radii[i] > 0;
   s_live[t] = live;
   // the SH rows are staged unless the colour Jacobian comes from the multi-view pre-pass
-  const bool has_sh = (a.shs || a.fused) && !a.pre_jac;
+  const bool has_sh = STAGE && (a.shs || a.fused) && !a.pre_jac;
   ShPlane p0{}, p1{};
   if (has_sh) {
     const int ncoef = a.M * 3;
@@ -390,9 +391,12 @@ __global__ __launch_bounds__(kThreads) void sh_flush_kernel(ShFlushArgs a) {
     float* r0 = s_sh + p0.lds + t * p0.w;
     float* r1 = s_sh + p1.lds + t * p1.w;
     r0[0] = g[0].x; r0[1] = g[0].y; r0[2] = g[0].z;
-    for (int k = 1; k < a.M; k++) {
-      const V3 v = k < used ? g[k] : v3(0, 0, 0);
-      r1[3 * k - 3] = v.x; r1[3 * k - 2] = v.y; r1[3 * k - 1] = v.z;
+#pragma unroll
+    for (int k = 1; k < 16; k++) {  // static indices: g stays in registers
+      if (k < a.M) {
+        const V3 v = k < used ? g[k] : v3(0, 0, 0);
+        r1[3 * k - 3] = v.x; r1[3 * k - 2] = v.y; r1[3 * k - 1] = v.z;
+      }
     }
   }
   __syncthreads();
@@ -415,10 +419,14 @@ hipError_t launch_sh_grad_flush(const ShFlushArgs& a, hipStream_t s) {
 hipError_t launch_preprocess_backward(const BwdPreArgs& a, hipStream_t s) {
   if (a.P == 0) return hipSuccess;
   const dim3 grid((a.P + kThreads - 1) / kThreads);
-  if (a.accumulate)
-    hipLaunchKernelGGL(preprocess_bwd_kernel<true>, grid, dim3(kThreads), 0, s, a);
-  else
-    hipLaunchKernelGGL(preprocess_bwd_kernel<false>, grid, dim3(kThreads), 0, s, a);
+  const bool stage = (a.shs || a.fused) && !a.pre_jac;
+  if (a.accumulate) {
+    if (stage) hipLaunchKernelGGL((preprocess_bwd_kernel<true, true>), grid, dim3(kThreads), 0, s, a);
+    else hipLaunchKernelGGL((preprocess_bwd_kernel<true, false>), grid, dim3(kThreads), 0, s, a);
+  } else {
+    if (stage) hipLaunchKernelGGL((preprocess_bwd_kernel<false, true>), grid, dim3(kThreads), 0, s, a);
+    else hipLaunchKernelGGL((preprocess_bwd_kernel<false, false>), grid, dim3(kThreads), 0, s, a);
+  }
   return hipGetLastError();
 }
 
