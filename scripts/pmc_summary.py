@@ -19,7 +19,8 @@ STAGE = {"preprocess_kernel": "preprocess", "duplicate_kernel": "duplicate",
          "render_bwd_kernel": "render_bwd", "preprocess_bwd_kernel": "preprocess_bwd",
          "radix_totals_kernel": "radix_totals", "radix_onesweep_kernel": "radix_onesweep",
          "scan_reduce_kernel": "scan_reduce", "scan_final_kernel": "scan_final",
-         "scan_parts_kernel": "scan_parts"}
+         "scan_parts_kernel": "scan_parts", "sh_precolor_kernel": "sh_precolor",
+         "sh_flush_kernel": "sh_flush"}
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
 meta = {}
 for f in sorted(glob.glob(f"{src}/*/*counter_collection.csv")):
