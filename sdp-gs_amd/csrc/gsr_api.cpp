@@ -242,7 +242,7 @@ static int forward_impl(int P, int M, const float* background, const float* mean
   g_err.clear();
   if ((pre_color == nullptr) != (pre_clamp == nullptr) || (pre_color && !fused))
     return fail(GSR_ERR_ARGUMENT, "pre_color / pre_clamp: both or neither, fused path only");
-  if (fused) {
+  if (fused && P != 0) {  // P = 0: empty tensors have null data (rasterize_points.cu:81)
     if (!sh_dc || (M > 1 && !sh_rest) || !scales || !rotations)
       return fail(GSR_ERR_ARGUMENT, "fused path needs features_dc/_rest, _scaling, _rotation");
     sh = sh_dc;  // "SH present" for the checks below; the kernels read sh_dc / sh_rest
@@ -475,7 +475,7 @@ static int backward_impl(
     const float* opacity_raw, float* dL_dsh_rest, int accumulate, float* dRGB_sh = nullptr,
     const float* pre_jac = nullptr) {
   g_err.clear();
-  if (fused) {
+  if (fused && P != 0) {
     if (!sh_dc || (M > 1 && !sh_rest) || (M > 1 && !dL_dsh_rest && !dRGB_sh) || !scales ||
         !rotations || !opacity_raw)
       return fail(GSR_ERR_ARGUMENT, "fused backward needs the raw parameters and their grads");

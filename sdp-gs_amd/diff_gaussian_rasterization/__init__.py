@@ -423,7 +423,10 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
                 int(bool(rs.debug)))
         _lib.check(rc)
         if into_leaves:
-            ev = torch.cuda.Event()
+            # one event per device, re-recorded: a later wait_event has already captured the
+            # previous record (hipStreamWaitEvent waits for the record current at the call)
+            prev = _LEAF_GRAD_EVENT.get(dev.index)
+            ev = prev[0] if prev is not None else torch.cuda.Event()
             ev.record(cur)
             _LEAF_GRAD_EVENT[dev.index] = (ev, cur.stream_id)
         # forward inputs: means3D, means2D, features_dc, features_rest, opacity_raw, scaling_raw,

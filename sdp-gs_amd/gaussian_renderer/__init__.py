@@ -150,10 +150,10 @@ def render(viewpoint_camera, pc, pipe, bg_color: torch.Tensor, opt, scaling_modi
                            "alpha": rendered_alpha,
                            "feature": language_feature_image,
                            "viewspace_points": screenspace_points,
-                           "visibility_filter": radii > 0,
                            "radii": radii,
                            "color": None},
-                          {"opacity": lambda: pc.get_opacity})
+                          {"opacity": lambda: pc.get_opacity,
+                           "visibility_filter": lambda: radii > 0})
 
     means3D = xyz
     means2D = screenspace_points

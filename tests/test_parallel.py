@@ -54,7 +54,9 @@ def _worker(rank, world, init, n_views, bucket_bytes, attach, q):
     radii = torch.arange(10, dtype=torch.float32) * (rank + 1)
     allreduce_densification_stats(accum, denom, radii)
     if rank == 0:
-        q.put(([p.grad.clone() for p in params], accum, denom, radii))
+        # numpy copies travel by value (torch tensors go through fd sharing, which races with
+        # this process's exit)
+        q.put(([p.grad.numpy().copy() for p in params], accum.numpy(), denom.numpy(), radii.numpy()))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -69,6 +71,8 @@ def test_sharded_allreduce_equals_single_process(n_views, bucket_bytes, attach):
     for p in procs:
         p.start()
     grads, accum, denom, radii = q.get(timeout=120)
+    grads = [torch.from_numpy(g) for g in grads]
+    accum, denom, radii = torch.from_numpy(accum), torch.from_numpy(denom), torch.from_numpy(radii)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0

@@ -225,3 +225,24 @@ def test_precolor_forward_is_bit_identical():
     for a, b in zip(ref, got):
         for k in ("render", "depth", "alpha", "feature", "radii"):
             assert torch.equal(a[k], b[k]), k
+
+
+def test_fused_render_of_empty_model():
+    """render() on a GaussianModel with no Gaussians (the reference rasterizer returns zero images
+    for P = 0, rasterize_points.cu:81): the fused path accepts the empty leaves (null data
+    pointers) in the forward and the backward, in both grad modes."""
+    import diff_gaussian_rasterization as dgr
+    render, m, cam = _setup(P=10)
+    for n in ("_xyz", "_features_dc", "_features_rest", "_opacity", "_scaling", "_rotation",
+              "_language_feature"):
+        setattr(m, n, getattr(m, n)[:0].detach().clone().requires_grad_(True))
+    bg = torch.tensor([0.1, 0.2, 0.3], device="cuda")
+    try:
+        for into in (False, True):
+            dgr.grad_into_leaves(into)
+            pkg = render(cam, m, Pipe(sh_py=True), bg, Opt())
+            assert torch.all(pkg["render"] == 0) and pkg["radii"].shape == (0,)
+            (pkg["render"].sum() + pkg["depth"].sum()).backward()
+            torch.cuda.synchronize()
+    finally:
+        dgr.grad_into_leaves(False)
