@@ -39,6 +39,7 @@ GeomState carve_geom(char* base, size_t P) {
   g.acc = c.take<float>((size_t)kAccFloats * P);
   g.sort = take_sort_scratch(c, P);
   g.scan_parts = c.take<uint32_t>(scan_parts(P) + 1);
+  g.pre_parts = c.take<uint32_t>((P + 255) / 256 + 1);
   g.bytes = c.size();
   return g;
 }
@@ -313,13 +314,14 @@ static int forward_impl(int P, int M, const float* background, const float* mean
   // the preprocess grid also zeroes the depth sort's scratch and the backward's accumulators
   pa.clear = SideClear{g.sort.aux, sort_clear_bytes(g.sort, (size_t)P, 32)};
   pa.acc_zero = 1;
+  pa.parts = g.pre_parts;
   PROF_BEGIN(PREPROCESS);
   GSR_CHECK(launch_preprocess(pa, stream));
   // R = total tile count (order-independent): reduced right after the preprocess and read back
   // while the depth sort and the scan are already queued behind it, so the host's wait and the
   // binning-buffer allocation overlap GPU work instead of draining the stream
   // flags[1] = R, flags[2] = the sticky look-back timeout counter of earlier sorts (P > 0 here)
-  GSR_CHECK(reduce_u32(g.tiles_touched, (size_t)P, g.scan_parts, g.flags + 1, stream, true));
+  GSR_CHECK(sum_u32_parts(g.pre_parts, ((size_t)P + 255) / 256, g.flags + 1, stream, true));
   PROF_END(PREPROCESS);
   uint32_t* host = pinned_slot();
   hipEvent_t ready = readback_event();

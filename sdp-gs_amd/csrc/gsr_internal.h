@@ -102,6 +102,10 @@ inline SortScratch take_sort_scratch(Carver& c, size_t n) {
 // input element i is in[gather[i]].  parts: scratch of scan_parts(n) u32.
 hipError_t scan_u32(const uint32_t* in, const uint32_t* gather, uint32_t* out, size_t n,
                     bool inclusive, uint32_t* parts, hipStream_t s);
+// *out = sum of n u32 partial sums (one launch; with_timeouts: out[1] = the sticky sort timeout
+// counter, read back with it).
+hipError_t sum_u32_parts(const uint32_t* parts, size_t n, uint32_t* out, hipStream_t s,
+                         bool with_timeouts);
 // *out = sum of n u32 values (two launches); parts: scratch of scan_parts(n) u32.
 hipError_t reduce_u32(const uint32_t* in, size_t n, uint32_t* parts, uint32_t* out,
                       hipStream_t s, bool with_timeouts = false);
@@ -135,6 +139,7 @@ struct GeomState {
   uint32_t* flags;          // [4]  [0]: prefiltered violation
   SortScratch sort;         // depth-sort scratch
   uint32_t* scan_parts;
+  uint32_t* pre_parts;      // [ceil(P/256)] tile-count sum of each preprocess workgroup
   size_t bytes;
 };
 GeomState carve_geom(char* base, size_t P);
@@ -183,6 +188,7 @@ struct PreArgs {
   // backward's per-Gaussian gradient accumulator rows g.acc
   SideClear clear;
   int acc_zero;
+  uint32_t* parts;  // [gridDim.x] sum of the workgroup's tile counts
   // multi-view colour pre-pass (fused only): when non-null, the SH colour of this view and its
   // clamp bits come precomputed (gsr_sh_precolor) instead of being evaluated from the SH rows
   const float* pre_color;

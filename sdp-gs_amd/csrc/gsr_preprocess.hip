@@ -25,12 +25,8 @@ constexpr int kThreads = 256;
 #define GSR_PRE_HOIST 0
 #endif
 
-__global__ __launch_bounds__(kThreads) void preprocess_kernel(PreArgs a) {
-  // one lane per Gaussian; SH rows are read directly (an LDS-staged variant, gsr_stage.h, measured
-  // slower here: its 48 KB of LDS cut occupancy below what this latency-bound kernel needs)
-  const int idx = (int)(blockIdx.x * kThreads + threadIdx.x);
-  side_clear(a.clear.p, a.clear.bytes, (size_t)idx, (size_t)gridDim.x * kThreads);
-  if (idx >= a.P) return;
+// One Gaussian; returns its tile count (0 when culled).
+__device__ __forceinline__ uint32_t preprocess_gaussian(const PreArgs& a, int idx) {
   if (a.acc_zero) {  // this Gaussian's 64-B gradient accumulator row (zeroed before the backward)
     float4* row = reinterpret_cast<float4*>(a.g.acc + (size_t)idx * kAccFloats);
 #pragma unroll
@@ -59,7 +55,7 @@ __global__ __launch_bounds__(kThreads) void preprocess_kernel(PreArgs a) {
   g.dval_a[idx] = (uint32_t)idx;
   if (!near_ok) {
     if (a.prefiltered) atomicOr(&g.flags[0], 1u);  // reference __trap()s (auxiliary.h:156-160)
-    return;
+    return 0;
   }
   const V3 ph = xform_point43(p_orig, a.proj);
   const float pw = 1.0f / (xform_w(p_orig, a.proj) + 0.0000001f);
@@ -87,7 +83,7 @@ __global__ __launch_bounds__(kThreads) void preprocess_kernel(PreArgs a) {
   }
   const Ewa e = ewa_project(p_orig, a.fx, a.fy, a.tanx, a.tany, c3, a.view);
   const float det = (e.a * e.c - e.b * e.b);
-  if (det == 0.0f) return;
+  if (det == 0.0f) return 0;
   const float det_inv = 1.f / det;
   const float con_a = e.c * det_inv, con_b = -e.b * det_inv, con_c = e.a * det_inv;
   const float mid = 0.5f * (e.a + e.c);
@@ -98,7 +94,7 @@ __global__ __launch_bounds__(kThreads) void preprocess_kernel(PreArgs a) {
   const int r = f2i_sat(my_radius);
   uint32_t x0, y0, x1, y1;
   tile_rect(px, py, r, a.gx, a.gy, x0, y0, x1, y1);
-  if ((x1 - x0) * (y1 - y0) == 0) return;
+  if ((x1 - x0) * (y1 - y0) == 0) return 0;
 
   float cr, cg, cb;
   if (a.pre_color) {  // multi-view pre-pass: the same sh_to_rgb, evaluated for all views at once
@@ -165,6 +161,28 @@ __global__ __launch_bounds__(kThreads) void preprocess_kernel(PreArgs a) {
   rec[1] = make_float4(con_c, op, depth, cr);
   rec[2] = make_float4(cg, cb, f0, f1);
   rec[3] = make_float4(f2, (float)r, qc, 0.f);
+  return count;
+}
+
+// one lane per Gaussian; SH rows are read directly (an LDS-staged variant, gsr_stage.h, measured
+// slower here: its 48 KB of LDS cut occupancy below what this latency-bound kernel needs).  Each
+// workgroup also writes the sum of its tile counts (a.parts), so R = sum of the partials needs one
+// more small launch instead of a separate pass over tiles_touched.
+__global__ __launch_bounds__(kThreads) void preprocess_kernel(PreArgs a) {
+  const int idx = (int)(blockIdx.x * kThreads + threadIdx.x);
+  side_clear(a.clear.p, a.clear.bytes, (size_t)idx, (size_t)gridDim.x * kThreads);
+  uint32_t count = idx < a.P ? preprocess_gaussian(a, idx) : 0u;
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) count += (uint32_t)__shfl_xor((int)count, d, 64);
+  __shared__ uint32_t s_sum[kThreads / 64];
+  if ((threadIdx.x & 63) == 0) s_sum[threadIdx.x >> 6] = count;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+#pragma unroll
+    for (int w = 0; w < kThreads / 64; w++) t += s_sum[w];
+    a.parts[blockIdx.x] = t;
+  }
 }
 
 // Multi-view colour pre-pass (gsr_amd/pipeline.py): one pass over the SH rows serves the

@@ -453,6 +453,14 @@ __global__ __launch_bounds__(1024) void sum_parts_kernel(const uint32_t* __restr
 
 }  // namespace
 
+hipError_t sum_u32_parts(const uint32_t* parts, size_t n, uint32_t* out, hipStream_t s,
+                         bool with_timeouts) {
+  if (n > 0x7fffffffull) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(sum_parts_kernel, dim3(1), dim3(1024), 0, s, parts, (int)n, out,
+                     with_timeouts ? 1 : 0);
+  return hipGetLastError();
+}
+
 hipError_t reduce_u32(const uint32_t* in, size_t n, uint32_t* parts, uint32_t* out,
                       hipStream_t s, bool with_timeouts) {
   if (n == 0) return hipMemsetAsync(out, 0, sizeof(uint32_t), s);

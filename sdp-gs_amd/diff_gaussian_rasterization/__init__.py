@@ -458,7 +458,9 @@ class ShPrecolor:
     reading the 192-byte SH rows again, and -- under ShGradDeferral -- so do their backwards.
     Outputs are identical (the same device functions, gsr_sh.h)."""
 
-    def __init__(self, means3D, features_dc, features_rest, degree, campos_list):
+    def __init__(self, means3D, features_dc, features_rest, degree, campos_list, buffers=None):
+        """buffers: optional list of (colour [P,3], clamp [P] u8, Jacobian [P,9]) per camera to
+        reuse (written on the current stream, so every earlier reader must be ordered before it)."""
         self.device = means3D.device
         self.keys = (means3D.data_ptr(), features_dc.data_ptr(),
                      features_rest.data_ptr() if features_rest is not None else 0, int(degree))
@@ -467,8 +469,14 @@ class ShPrecolor:
         fopts = dict(dtype=torch.float32, device=self.device)
         self.views = {}
         cams = [_dev_f32(c, "campos", self.device) for c in campos_list]
-        bufs = [(torch.empty((P, 3), **fopts), torch.empty((P,), dtype=torch.uint8, device=self.device),
-                 torch.empty((P, 9), **fopts)) for _ in cams]
+        if buffers is not None and len(buffers) == len(cams) and all(
+                b[0].shape == (P, 3) and b[2].shape == (P, 9) for b in buffers):
+            bufs = list(buffers)
+        else:
+            bufs = [(torch.empty((P, 3), **fopts),
+                     torch.empty((P,), dtype=torch.uint8, device=self.device),
+                     torch.empty((P, 9), **fopts)) for _ in cams]
+        self.buffers = bufs
         n = len(cams)
         if n and P:
             arr = lambda xs: (_lib.ctypes.c_void_p * n)(*[x.data_ptr() for x in xs])  # noqa: E731

@@ -46,6 +46,7 @@ class ViewPipeline:
         self.depth = depth
         self.defer_sh = defer_sh
         self.precolor = precolor
+        self._pre_bufs = None  # the pre-pass's per-view buffers, reused step after step
         self.side = [torch.cuda.Stream(device=self.device) for _ in range(depth - 1)]
 
     def run(self, items: Iterable[T], fn: Callable[[T], R], model=None,
@@ -64,7 +65,10 @@ class ViewPipeline:
         pre = contextlib.nullcontext()
         if self.precolor and model is not None and items:
             pre = dgr.ShPrecolor(model._xyz, model._features_dc, model._features_rest,
-                                 model.active_sh_degree, [campos_of(it) for it in items])
+                                 model.active_sh_degree, [campos_of(it) for it in items],
+                                 buffers=self._pre_bufs)
+            # reuse next step: its pre-pass is issued on this stream after this step's join
+            self._pre_bufs = pre.buffers
         for s in self.side:
             s.wait_stream(main)  # inputs prepared on the main stream (zeroed grads, pre-pass)
         out = []
