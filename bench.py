@@ -56,7 +56,7 @@ class Opt:
 
 
 def algorithmic_bytes(stage, P, Pv, R, T, HW, D=3, C=8, tile_passes=2, acc=True, defer_sh=False,
-                      precolor=False):
+                      precolor=False, views=6):
     """Bytes each stage must move per launch.
     P Gaussians, Pv visible, R instances, T tiles, HW pixels, C blended channels (rgb, depth,
     alpha, feature x3), acc: the backward adds into existing gradients (read + write),
@@ -86,6 +86,10 @@ def algorithmic_bytes(stage, P, Pv, R, T, HW, D=3, C=8, tile_passes=2, acc=True,
         # accumulator row + per-Gaussian inputs (visible), radii (all), gradients (RMW when acc)
         "preprocess_bwd": Pv * (64 + 12 + 12 + 16 + 4 + sh_bwd + 12 + 1) + P * 4
                           + ((2 * Pv) if acc else P) * grads + (P * 12 if defer_sh else 0),
+        # once per step for V views (reported per launch): SH rows + means in, 49 B per view out
+        "sh_precolor": P * (12 + sh) + P * 49 * views,
+        # means + V stored dL/dRGB in, SH gradients out (store mode)
+        "sh_flush": P * (12 + 12 * views) + P * sh,
     }[stage]
 
 
@@ -219,7 +223,8 @@ def main():
             continue
         avg_ms = ms / calls
         b = algorithmic_bytes(name, P, Pv, R, T, HW, D=deg, acc=not args.autograd_grads,
-                              defer_sh=defer_sh, precolor=not args.no_precolor)
+                              defer_sh=defer_sh, precolor=not args.no_precolor,
+                              views=len(my_cams))
         k = {"avg_ms": round(avg_ms, 4), "calls": int(calls), "bytes": int(b),
              "gbs": round(b / (avg_ms * 1e-3) / 1e9, 1)}
         if name in ("render_fwd", "render_bwd"):

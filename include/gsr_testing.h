@@ -40,7 +40,8 @@ int gsr_test_expf_pair(const float* x, float* ref, float* fast, size_t n, void* 
 enum {
   GSR_STAGE_PREPROCESS = 0, GSR_STAGE_DEPTH_SORT, GSR_STAGE_SCAN, GSR_STAGE_DUPLICATE,
   GSR_STAGE_TILE_SORT, GSR_STAGE_RANGES, GSR_STAGE_RENDER_FWD, GSR_STAGE_ACC_ZERO,
-  GSR_STAGE_RENDER_BWD, GSR_STAGE_PREPROCESS_BWD, GSR_NUM_STAGES
+  GSR_STAGE_RENDER_BWD, GSR_STAGE_PREPROCESS_BWD, GSR_STAGE_SH_PRECOLOR, GSR_STAGE_SH_FLUSH,
+  GSR_NUM_STAGES
 };
 /* stage_mask: bit GSR_STAGE_x enables that stage; 0 disables; -1 (all bits) enables all. */
 void gsr_profile_enable(int stage_mask);

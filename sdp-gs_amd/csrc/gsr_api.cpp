@@ -211,7 +211,8 @@ void prof_end(int stage, hipEvent_t a, hipStream_t s) {
 
 const char* kStageNames[GSR_NUM_STAGES] = {"preprocess", "depth_sort", "scan", "duplicate",
                                           "tile_sort", "ranges", "render_fwd", "acc_zero",
-                                          "render_bwd", "preprocess_bwd"};
+                                          "render_bwd", "preprocess_bwd", "sh_precolor",
+                                          "sh_flush"};
 
 }  // namespace
 
@@ -651,7 +652,9 @@ int gsr_sh_precolor(int P, int M, int degree, const float* means3D, const float*
       a.campos[v] = campos[v0 + v]; a.color[v] = color[v0 + v];
       a.clamp[v] = clamped[v0 + v]; a.jac[v] = jac[v0 + v];
     }
+    PROF_BEGIN(SH_PRECOLOR);
     GSR_CHECK(launch_sh_precolor(a, stream));
+    PROF_END(SH_PRECOLOR);
   }
   return GSR_OK;
 }
@@ -680,7 +683,9 @@ int gsr_sh_grad_flush(int P, int M, int degree, const float* means3D, int nviews
       a.dRGB[v] = dL_dcolor_sh[v0 + v];
     }
     a.dL_dsh_dc = dL_dfeatures_dc; a.dL_dsh_rest = dL_dfeatures_rest;
+    PROF_BEGIN(SH_FLUSH);
     GSR_CHECK(launch_sh_grad_flush(a, stream));
+    PROF_END(SH_FLUSH);
   }
   return GSR_OK;
 }

@@ -240,7 +240,7 @@ def alloc_callback():
     return _ALLOC_CB
 
 
-NUM_STAGES = 10
+NUM_STAGES = 12
 
 
 class StageTimer:
