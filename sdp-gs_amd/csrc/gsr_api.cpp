@@ -372,7 +372,7 @@ static int forward_impl(int P, int M, const float* background, const float* mean
   // the duplicate grid also zeroes the tile sort's scratch and the tile ranges
   const int tbits = tile_bits(ntiles);
   GSR_CHECK(launch_duplicate(P, order, g.offsets, radii_ptr, g.rec, gx, gy, b.tkey_a, b.tval_a,
-                             SideClear{b.sort.aux, sort_clear_bytes(b.sort, R, tbits)},
+                             (uint32_t)R, SideClear{b.sort.aux, sort_clear_bytes(b.sort, R, tbits)},
                              SideClear{im.ranges, sizeof(uint2) * ntiles}, stream));
   PROF_END(DUPLICATE);
   bool t_in_b = false;
@@ -393,7 +393,7 @@ static int forward_impl(int P, int M, const float* background, const float* mean
 
   RenderArgs ra{};
   ra.W = W; ra.H = H; ra.gx = gx; ra.gy = gy;
-  ra.ranges = im.ranges; ra.point_list = point_list; ra.rec = g.rec; ra.bg = background;
+  ra.ranges = im.ranges; ra.point_list = point_list; ra.rec = g.rec; ra.P = (uint32_t)P; ra.bg = background;
   ra.final_T = im.final_T; ra.n_contrib = im.n_contrib; ra.tile_last = im.tile_last;
   ra.out_color = out_color; ra.out_depth = out_depth; ra.out_alpha = out_alpha;
   ra.out_feature = out_feature; ra.include_feature = include_feature;
@@ -525,7 +525,7 @@ static int backward_impl(
   if (R > 0) {
     RenderBwdArgs rb{};
     rb.W = W; rb.H = H; rb.gx = gx; rb.gy = gy;
-    rb.ranges = im.ranges; rb.point_list = point_list; rb.rec = g.rec; rb.bg = background;
+    rb.ranges = im.ranges; rb.point_list = point_list; rb.rec = g.rec; rb.P = (uint32_t)P; rb.bg = background;
     rb.final_T = im.final_T; rb.n_contrib = im.n_contrib; rb.tile_last = im.tile_last;
     rb.dL_dcolor = dL_dout_color; rb.dL_ddepth = dL_dout_depth; rb.dL_dalpha = dL_dout_alpha;
     rb.dL_dfeature = dL_dout_feature; rb.acc = g.acc; rb.include_feature = include_feature;

@@ -29,7 +29,8 @@ __global__ __launch_bounds__(kThreads) void duplicate_kernel(int P,
                                                              uint32_t gx, uint32_t gy,
                                                              uint32_t* __restrict__ tkey,
                                                              uint32_t* __restrict__ tval,
-                                                             SideClear clear0, SideClear clear1) {
+                                                             uint32_t R, SideClear clear0,
+                                                             SideClear clear1) {
   const int s = (int)(blockIdx.x * kThreads + threadIdx.x);
   const size_t nth = (size_t)gridDim.x * kThreads;
   side_clear(clear0.p, clear0.bytes, (size_t)s, nth);
@@ -37,9 +38,9 @@ __global__ __launch_bounds__(kThreads) void duplicate_kernel(int P,
   if (s >= P) return;
   // coalesced reads first: culled / tile-less Gaussians (count 0) never touch the random gather
   uint32_t off = (s == 0) ? 0u : offsets[s - 1];
-  const uint32_t end = offsets[s];
+  const uint32_t end = min(offsets[s], R);
   if (off == end) return;
-  const uint32_t gid = order[s];
+  const uint32_t gid = min(order[s], (uint32_t)P - 1u);  // in range unless a sort gave up (reported)
   // the radius travels in the record (rec[3].y, exact as float): the gather stays inside the
   // Gaussian's 64-byte record line
   const float4 r0 = rec[4 * (size_t)gid];
@@ -63,31 +64,35 @@ __global__ __launch_bounds__(kThreads) void duplicate_kernel(int P,
 
 __global__ __launch_bounds__(kThreads) void tile_ranges_kernel(size_t R,
                                                                const uint32_t* __restrict__ tiles,
-                                                               uint2* __restrict__ ranges) {
+                                                               uint2* __restrict__ ranges,
+                                                               uint32_t ntiles) {
   const size_t idx = (size_t)blockIdx.x * kThreads + threadIdx.x;
   if (idx >= R) return;
+  // tile ids are < ntiles by construction; the bounds tests only keep the output of a sort whose
+  // look-back gave up (reported by the next read-back) from writing outside the table
   const uint32_t cur = tiles[idx];
+  const bool cur_ok = cur < ntiles;
   if (idx == 0) {
-    ranges[cur].x = 0;
+    if (cur_ok) ranges[cur].x = 0;
   } else {
     const uint32_t prev = tiles[idx - 1];
     if (cur != prev) {
-      ranges[prev].y = (uint32_t)idx;
-      ranges[cur].x = (uint32_t)idx;
+      if (prev < ntiles) ranges[prev].y = (uint32_t)idx;
+      if (cur_ok) ranges[cur].x = (uint32_t)idx;
     }
   }
-  if (idx == R - 1) ranges[cur].y = (uint32_t)R;
+  if (idx == R - 1 && cur_ok) ranges[cur].y = (uint32_t)R;
 }
 
 }  // namespace
 
 hipError_t launch_duplicate(int P, const uint32_t* order, const uint32_t* offsets,
                             const int32_t* radii, const float4* rec, uint32_t gx, uint32_t gy,
-                            uint32_t* tkey, uint32_t* tval, SideClear clear0, SideClear clear1,
-                            hipStream_t s) {
+                            uint32_t* tkey, uint32_t* tval, uint32_t R, SideClear clear0,
+                            SideClear clear1, hipStream_t s) {
   if (P == 0) return hipSuccess;
   hipLaunchKernelGGL(duplicate_kernel, dim3((P + kThreads - 1) / kThreads), dim3(kThreads), 0, s,
-                     P, order, offsets, radii, rec, gx, gy, tkey, tval, clear0, clear1);
+                     P, order, offsets, radii, rec, gx, gy, tkey, tval, R, clear0, clear1);
   return hipGetLastError();
 }
 
@@ -99,7 +104,7 @@ hipError_t launch_tile_ranges(size_t R, const uint32_t* sorted_tiles, uint2* ran
   }
   if (R == 0) return hipSuccess;
   hipLaunchKernelGGL(tile_ranges_kernel, dim3((unsigned)((R + kThreads - 1) / kThreads)),
-                     dim3(kThreads), 0, s, R, sorted_tiles, ranges);
+                     dim3(kThreads), 0, s, R, sorted_tiles, ranges, ntiles);
   return hipGetLastError();
 }
 

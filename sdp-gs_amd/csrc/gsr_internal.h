@@ -51,7 +51,7 @@ constexpr int kScanMaxParts = 8192;   // partials scanned by the single-workgrou
 #define GSR_SORT_KPT 16
 #endif
 #ifndef GSR_SORT_TICKET
-#define GSR_SORT_TICKET 0  // one-sweep partitions by atomic ticket (1) or by blockIdx (0)
+#define GSR_SORT_TICKET 1  // one-sweep partitions by atomic ticket (1) or by blockIdx (0)
 #endif
 constexpr int kSortTile = 256 * GSR_SORT_KPT;  // keys per radix-sort workgroup (256 threads x KPT)
 
@@ -250,10 +250,11 @@ hipError_t launch_sh_grad_flush(const ShFlushArgs& a, hipStream_t s);
 
 // ---- binning (gsr_binning.hip) -------------------------------------------------------------------
 // The duplicate grid also zero-fills clear0 / clear1 (the tile sort's scratch, the ranges).
+// R bounds the writes (offsets of a complete depth order never exceed it).
 hipError_t launch_duplicate(int P, const uint32_t* order, const uint32_t* offsets,
                             const int32_t* radii, const float4* rec, uint32_t gx, uint32_t gy,
-                            uint32_t* tkey, uint32_t* tval, SideClear clear0, SideClear clear1,
-                            hipStream_t s);
+                            uint32_t* tkey, uint32_t* tval, uint32_t R, SideClear clear0,
+                            SideClear clear1, hipStream_t s);
 // ranges_cleared: the ranges are already zero (duplicate's side clear): no memset launch.
 hipError_t launch_tile_ranges(size_t R, const uint32_t* sorted_tiles, uint2* ranges,
                               uint32_t ntiles, hipStream_t s, bool ranges_cleared = false);
@@ -265,6 +266,7 @@ struct RenderArgs {
   const uint2* ranges;
   const uint32_t* point_list;
   const float4* rec;
+  uint32_t P;  // rows of rec: point_list entries are clamped to it (a failed sort cannot fault)
   const float* bg;
   float* final_T;
   uint32_t* n_contrib;
@@ -282,6 +284,7 @@ struct RenderBwdArgs {
   const uint2* ranges;
   const uint32_t* point_list;
   const float4* rec;
+  uint32_t P;  // rows of rec: point_list entries are clamped to it (a failed sort cannot fault)
   const float* bg;
   const float* final_T;
   const uint32_t* n_contrib;

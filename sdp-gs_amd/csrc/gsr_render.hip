@@ -190,7 +190,7 @@ __global__ __launch_bounds__(kThreads) void render_fwd_kernel(RenderArgs a) {
     if (__syncthreads_count(done) == kThreads) break;
     const uint32_t i = base + threadIdx.x;
     if (i < range.y) {
-      const uint32_t gid = a.point_list[i];
+      const uint32_t gid = min(a.point_list[i], a.P - 1u);
       const float4* rec = a.rec + 4 * (size_t)gid;
       const float4 q0 = rec[0], q1 = rec[1], q3 = rec[3];
       s_r0[threadIdx.x] = q0;
@@ -473,7 +473,7 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
     const uint32_t cnt = min((uint32_t)kThreads, tile_last - done_cnt);
     if (threadIdx.x < cnt) {
       const uint32_t rel = tile_last - 1 - done_cnt - threadIdx.x;
-      const uint32_t gid = a.point_list[range.x + rel];
+      const uint32_t gid = min(a.point_list[range.x + rel], a.P - 1u);
       s_gid[threadIdx.x] = gid;
       const float4* rec = a.rec + 4 * (size_t)gid;
       const float4 q0 = rec[0], q1 = rec[1], q3 = rec[3];

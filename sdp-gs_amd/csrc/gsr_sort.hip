@@ -62,7 +62,7 @@ __global__ __launch_bounds__(kThreads) void scan_reduce_kernel(const uint32_t* _
 #pragma unroll
   for (int k = 0; k < kScanItems; k++) {
     size_t i = base + (size_t)k * kThreads + threadIdx.x;
-    if (i < n) s += GATHER ? in[gather[i]] : in[i];
+    if (i < n) s += GATHER ? in[min(gather[i], (uint32_t)n - 1u)] : in[i];
   }
   uint32_t total;
   block_excl_scan<kThreads / 64>(s, lds, total);
@@ -103,7 +103,7 @@ __global__ __launch_bounds__(kThreads) void scan_final_kernel(const uint32_t* __
 #pragma unroll
   for (int k = 0; k < kScanItems; k++) {
     size_t i = base + k;
-    v[k] = (i < n) ? (GATHER ? in[gather[i]] : in[i]) : 0u;
+    v[k] = (i < n) ? (GATHER ? in[min(gather[i], (uint32_t)n - 1u)] : in[i]) : 0u;
     s += v[k];
   }
   uint32_t total;
