@@ -203,6 +203,58 @@ def test_radix_sort_sorted_and_stable(n, bits, kind):
     np.testing.assert_array_equal(v.cpu().numpy().view(np.uint32), vals[order])
 
 
+@pytest.mark.gpu
+def test_radix_sort_concurrent_streams():
+    """Several one-sweep sorts in flight at once on separate streams (as the view streams and two
+    processes on one GPU produce): the look-back must never wait on a partition that cannot be
+    dispatched (ticketed partitions, gsr_sort.hip), so every sort completes without the look-back
+    timeout and matches numpy's stable argsort.  (Correctness under overlap only: the blockIdx
+    variant, GSR_SORT_TICKET=0, also passes this in one process; its failure was seen with two
+    processes sharing the GPU, scripts/dist_rehearsal.sh.)"""
+    import threading
+    from gsr_amd import _lib
+    L = _lib.load()
+    n, nthreads, reps = 3_000_000, 4, 6
+    rng = np.random.default_rng(7)
+    keys = [rng.lognormal(1.0, 0.5, size=n).astype(np.float32).view(np.uint32) + 0
+            for _ in range(nthreads)]
+    orders = [np.argsort(k, kind="stable") for k in keys]
+    dev = [(torch.tensor(k.view(np.int32), device="cuda"),
+            torch.empty(n, dtype=torch.int32, device="cuda"),
+            torch.empty(int(L.gsr_test_sort_scratch_bytes(n)), dtype=torch.uint8, device="cuda"),
+            torch.cuda.Stream()) for k in keys]
+    torch.cuda.synchronize()
+    errors = []
+
+    def worker(i):
+        k0, v, scratch, s = dev[i]
+        try:
+            for _ in range(reps):
+                k = k0.clone()
+                v.copy_(torch.arange(n, dtype=torch.int32, device="cuda"))
+                torch.cuda.synchronize()
+                rc = L.gsr_test_radix_sort_pairs(k.data_ptr(), v.data_ptr(), n, 32,
+                                                 scratch.data_ptr(), s.cuda_stream)
+                if rc != 0:
+                    errors.append((i, rc, L.gsr_last_error()))
+                    return
+                s.synchronize()
+                got = v.cpu().numpy().view(np.uint32)
+                if not np.array_equal(got, orders[i].astype(np.uint32)):
+                    errors.append((i, "order mismatch"))
+                    return
+        except Exception as e:  # surfaced below
+            errors.append((i, repr(e)))
+
+    threads = [threading.Thread(target=worker, args=(i,)) for i in range(nthreads)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=100)
+    assert not any(t.is_alive() for t in threads), "a sort thread did not finish"
+    assert not errors, errors
+
+
 @pytest.mark.parametrize("n,frac_culled", [(1_000_000, 0.0), (1_000_000, 0.2), (70_001, 0.5),
                                            (4097, 1.0)])
 def test_radix_sort_sentinel_copy_pass(n, frac_culled):
