@@ -30,8 +30,18 @@ size_t gsr_test_scan_scratch_bytes(size_t n);
 int gsr_test_scan(const uint32_t* in, uint32_t* out, size_t n, int inclusive, void* scratch,
                   void* stream);
 
-/* ref[i] = expf(x[i]) (OCML), fast[i] = the blends' range-check-free exp (device pointers). */
+/* ref[i] = expf(x[i]) (OCML), fast[i] = splat_exp(x[i]), the blends' deterministic exp
+ * (gsr_device.h; the oracle evaluates the same sequence) (device pointers). */
 int gsr_test_expf_pair(const float* x, float* ref, float* fast, size_t n, void* stream);
+
+/* The fused path's GaussianModel activations as its kernels evaluate them (device pointers):
+ * opacity = sigmoid(opacity_raw) [P], scaling = exp(scaling_raw) [P,3],
+ * rotation = normalize(rotation_raw) [P,4] (16-byte aligned).  Lets the tests feed the CPU oracle
+ * the exact activated values the kernels used and compare them with torch's getters
+ * (scene/gaussian_model.py:33-41). */
+int gsr_test_activations(const float* opacity_raw, const float* scaling_raw,
+                         const float* rotation_raw, size_t P, float* opacity, float* scaling,
+                         float* rotation, void* stream);
 
 /* Stage timing with hipEvents recorded on the caller's stream around the kernels of the forward
  * and backward (used by bench.py for the per-kernel roofline).  Off by default; each enabled

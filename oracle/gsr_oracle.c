@@ -9,11 +9,13 @@
  * here (no nvcc, un-vendored glm: SURVEY.md 8(c)), so this restatement is pinned by (a) golden
  * vectors generated from the importable reference Python maths (eval_sh, getProjectionMatrix,
  * getWorld2View2) in tests/golden/, (b) analytic known-answer cases, and (c) a float64 autograd
- * cross-check of the backward (tests/test_oracle_autograd.py).
+ * cross-check of the backward (tests/test_oracle.py).  Host threads (oracle_set_threads) only
+ * split loops into fixed chunks; see the comment above par_for.
  */
 #include "gsr_oracle.h"
 
 #include <math.h>
+#include <pthread.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -90,6 +92,30 @@ static int f2i_sat(float f) {
 static float fminf_cuda(float a, float b) { return fminf(a, b); }
 static float fmaxf_cuda(float a, float b) { return fmaxf(a, b); }
 
+/* The blend's Gaussian weight exp(power) (forward.cu:343, backward.cu:498 call expf): the same
+ * deterministic single-precision exp the HIP kernels evaluate (sdp-gs_amd/csrc/gsr_device.h
+ * splat_exp), every step a correctly rounded IEEE operation (fmaf, rintf, ldexpf).  <= 1.01 ulp of
+ * exp over [-87, 0]; the reference's CUDA expf is specified to 2 ulp.  Sharing it makes the
+ * alpha >= 1/255 and T < 1e-4 decisions of GPU and oracle identical pixel for pixel. */
+static float splat_exp(float x) {
+    const float k = rintf(x * 1.44269504088896341f);
+    float r = fmaf(-k, 0.693359375f, x);
+    r = fmaf(-k, -2.12194440e-4f, r);
+    float p = 1.9875691500e-4f;
+    p = fmaf(p, r, 1.3981999507e-3f);
+    p = fmaf(p, r, 8.3334519073e-3f);
+    p = fmaf(p, r, 4.1665795894e-2f);
+    p = fmaf(p, r, 1.6666665459e-1f);
+    p = fmaf(p, r, 5.0000001201e-1f);
+    const float r2 = r * r;
+    const float y = fmaf(p, r2, r) + 1.0f;
+    const float res = ldexpf(y, (int)k);
+    return x < -104.0f ? 0.0f : res;
+}
+void oracle_splat_exp(long n, const float* x, float* out) {
+    for (long i = 0; i < n; i++) out[i] = splat_exp(x[i]);
+}
+
 /* auxiliary.h:41-44: promoted to double */
 static float ndc2Pix(float v, int S) { return (float)((((double)v + 1.0) * S - 1.0) * 0.5); }
 
@@ -164,6 +190,7 @@ struct oracle_state {
     /* image */
     float* final_T;
     unsigned* n_contrib;
+    float* margin; /* [H*W] test-side diagnostic, see oracle_get_margin */
 };
 
 /* forward.cu:20-71 computeColorFromSH */
@@ -279,6 +306,234 @@ static int inst_cmp(const void* a, const void* b) {
 
 static void* xcalloc(size_t n, size_t s) { return calloc(n ? n : 1, s); }
 
+/* ------------------------------------------------------------------------------------------ */
+/* Host threads, for the full-size parity tests and the CPU baseline (oracle_set_threads).    */
+/* With 1 thread (the default) every loop runs in the reference's sequential order.  With n:  */
+/* the per-Gaussian and per-pixel-row loops run as n contiguous static chunks (each element is */
+/* computed by the same code, so the forward is bit-identical); the instance sort sorts n runs */
+/* and merges them (the comparator is a total order, so the order is identical); the backward */
+/* blend sums each chunk's contributions into private accumulators, added in chunk order      */
+/* afterwards (deterministic for a given n; the sums differ from the sequential ones only by   */
+/* float association, as the reference's own atomics do).                                     */
+/* ------------------------------------------------------------------------------------------ */
+#define ORACLE_MAX_THREADS 256
+static int g_threads = 1;
+void oracle_set_threads(int n) {
+    g_threads = n < 1 ? 1 : (n > ORACLE_MAX_THREADS ? ORACLE_MAX_THREADS : n);
+}
+int oracle_get_threads(void) { return g_threads; }
+
+typedef void (*range_fn)(void* ctx, long lo, long hi, int chunk);
+typedef struct { range_fn fn; void* ctx; long lo, hi; int chunk; } par_job;
+static void* par_entry(void* p) {
+    par_job* j = (par_job*)p;
+    j->fn(j->ctx, j->lo, j->hi, j->chunk);
+    return NULL;
+}
+/* Chunk count par_for(n, ...) uses. */
+static int par_chunks(long n) {
+    int nt = g_threads;
+    if ((long)nt > n) nt = n > 0 ? (int)n : 1;
+    return nt;
+}
+/* fn over [0, n) in par_chunks(n) contiguous chunks, chunk c on its own thread. */
+static void par_for(long n, range_fn fn, void* ctx) {
+    const int nt = par_chunks(n);
+    if (nt <= 1) { fn(ctx, 0, n, 0); return; }
+    pthread_t th[ORACLE_MAX_THREADS];
+    par_job job[ORACLE_MAX_THREADS];
+    int started[ORACLE_MAX_THREADS];
+    const long base = n / nt, rem = n % nt;
+    for (int c = 0; c < nt; c++) {
+        job[c].fn = fn; job[c].ctx = ctx; job[c].chunk = c;
+        job[c].lo = c * base + (c < rem ? c : rem);
+        job[c].hi = job[c].lo + base + (c < rem ? 1 : 0);
+    }
+    for (int c = 1; c < nt; c++) started[c] = pthread_create(&th[c], NULL, par_entry, &job[c]) == 0;
+    par_entry(&job[0]);
+    for (int c = 1; c < nt; c++) {
+        if (started[c]) pthread_join(th[c], NULL);
+        else par_entry(&job[c]); /* could not start a thread: run the chunk here */
+    }
+}
+
+/* ---- preprocessCUDA, forward.cu:155-256 (one Gaussian) ---- */
+static void preprocess_one(oracle_state* st, int idx) {
+    const float* means3D = st->means3D;
+    const int W = st->W, H = st->H;
+    st->radii[idx] = 0;
+    st->tiles_touched[idx] = 0;
+    v3 p_view;
+    if (!in_frustum(idx, means3D, st->view, &p_view)) return;
+    v3 p_orig = v3_mk(means3D[3 * idx], means3D[3 * idx + 1], means3D[3 * idx + 2]);
+    float p_hom[4];
+    transformPoint4x4(p_orig, st->proj, p_hom);
+    float p_w = 1.0f / (p_hom[3] + 0.0000001f);
+    float p_proj_x = p_hom[0] * p_w, p_proj_y = p_hom[1] * p_w;
+    const float* c3;
+    if (st->cov3D_precomp) {
+        c3 = st->cov3D_precomp + (size_t)idx * 6;
+    } else {
+        cov3d(st->scales + 3 * (size_t)idx, st->scale_modifier, st->rotations + 4 * (size_t)idx,
+              st->cov3D + (size_t)idx * 6);
+        c3 = st->cov3D + (size_t)idx * 6;
+    }
+    float cov[3];
+    cov2d(p_orig, st->focal_x, st->focal_y, st->tan_fovx, st->tan_fovy, c3, st->view, cov);
+    float det = (cov[0] * cov[2] - cov[1] * cov[1]);
+    if (det == 0.0f) return;
+    float det_inv = 1.f / det;
+    float conic[3] = {cov[2] * det_inv, -cov[1] * det_inv, cov[0] * det_inv};
+    float mid = 0.5f * (cov[0] + cov[2]);
+    float lambda1 = mid + sqrtf(fmaxf_cuda(0.1f, mid * mid - det));
+    float lambda2 = mid - sqrtf(fmaxf_cuda(0.1f, mid * mid - det));
+    float my_radius = ceilf(3.f * sqrtf(fmaxf_cuda(lambda1, lambda2)));
+    float pix_x = ndc2Pix(p_proj_x, W), pix_y = ndc2Pix(p_proj_y, H);
+    u2 rmin, rmax;
+    getRect(pix_x, pix_y, f2i_sat(my_radius), &rmin, &rmax, st->gx, st->gy);
+    if ((rmax.x - rmin.x) * (rmax.y - rmin.y) == 0) return;
+    if (!st->colors_precomp) {
+        v3 c = color_from_sh(idx, st->D, st->M, means3D, st->campos, st->sh, st->clamped);
+        st->rgb[3 * idx + 0] = c.x;
+        st->rgb[3 * idx + 1] = c.y;
+        st->rgb[3 * idx + 2] = c.z;
+    }
+    st->depths[idx] = p_view.z;
+    st->radii[idx] = f2i_sat(my_radius);
+    st->means2D[2 * idx] = pix_x;
+    st->means2D[2 * idx + 1] = pix_y;
+    float op = st->opacities[idx];
+    if (st->confidence) op = op * st->confidence[idx]; /* confidence = opacity multiplier */
+    st->conic_opacity[4 * idx + 0] = conic[0];
+    st->conic_opacity[4 * idx + 1] = conic[1];
+    st->conic_opacity[4 * idx + 2] = conic[2];
+    st->conic_opacity[4 * idx + 3] = op;
+    st->tiles_touched[idx] = (rmax.y - rmin.y) * (rmax.x - rmin.x);
+    if (st->include_feature) { /* language feature channels */
+        if (st->lang_precomp) {
+            for (int k = 0; k < 3; k++) st->feat[3 * idx + k] = st->lang_precomp[3 * idx + k];
+        } else if (st->sh_language) {
+            const float* l = st->sh_language;
+            float u0 = SH_C0 * l[3 * idx], u1 = SH_C0 * l[3 * idx + 1], u2v = SH_C0 * l[3 * idx + 2];
+            float n = sqrtf(u0 * u0 + u1 * u1 + u2v * u2v);
+            float den = n + 1e-9f;
+            st->feat[3 * idx + 0] = u0 / den;
+            st->feat[3 * idx + 1] = u1 / den;
+            st->feat[3 * idx + 2] = u2v / den;
+        }
+    }
+}
+static void preprocess_range(void* ctx, long lo, long hi, int chunk) {
+    (void)chunk;
+    for (long i = lo; i < hi; i++) preprocess_one((oracle_state*)ctx, (int)i);
+}
+
+/* ---- stable sort of the instances: per-chunk qsort + pairwise merges (same total order) ---- */
+typedef struct { inst_t* a; const long* b; } sort_ctx;
+static void sort_runs(void* ctx, long lo, long hi, int chunk) {
+    (void)chunk;
+    sort_ctx* c = (sort_ctx*)ctx;
+    for (long r = lo; r < hi; r++)
+        qsort(c->a + c->b[r], (size_t)(c->b[r + 1] - c->b[r]), sizeof(inst_t), inst_cmp);
+}
+typedef struct { const inst_t* src; inst_t* dst; const long* b; int nruns; } merge_ctx;
+static void merge_runs(void* ctx, long lo, long hi, int chunk) {
+    (void)chunk;
+    merge_ctx* m = (merge_ctx*)ctx;
+    for (long k = lo; k < hi; k++) {
+        const long r = 2 * k;
+        const long s0 = m->b[r], e0 = m->b[r + 1];
+        const long e1 = (r + 2 <= m->nruns) ? m->b[r + 2] : e0;
+        long i = s0, j = e0, o = s0;
+        while (i < e0 && j < e1) m->dst[o++] = inst_cmp(&m->src[j], &m->src[i]) < 0 ? m->src[j++] : m->src[i++];
+        while (i < e0) m->dst[o++] = m->src[i++];
+        while (j < e1) m->dst[o++] = m->src[j++];
+    }
+}
+static void sort_instances(inst_t* a, long n) {
+    int nruns = par_chunks(n);
+    inst_t* tmp = (nruns > 1 && n >= 4096) ? (inst_t*)malloc(sizeof(inst_t) * (size_t)n) : NULL;
+    if (!tmp) {
+        qsort(a, (size_t)n, sizeof(inst_t), inst_cmp);
+        return;
+    }
+    long b[ORACLE_MAX_THREADS + 1];
+    const long base = n / nruns, rem = n % nruns;
+    for (int r = 0; r <= nruns; r++) b[r] = r * base + (r < rem ? r : rem);
+    sort_ctx sc = {a, b};
+    par_for(nruns, sort_runs, &sc);
+    inst_t *src = a, *dst = tmp;
+    while (nruns > 1) {
+        const long npairs = (nruns + 1) / 2;
+        merge_ctx mc = {src, dst, b, nruns};
+        par_for(npairs, merge_runs, &mc);
+        for (long k = 0; k < npairs; k++) b[k] = b[2 * k];
+        b[npairs] = n;
+        nruns = (int)npairs;
+        inst_t* t = src; src = dst; dst = t;
+    }
+    if (src != a) memcpy(a, src, sizeof(inst_t) * (size_t)n);
+    free(tmp);
+}
+
+/* ---- renderCUDA (fwd), forward.cu:261-374, extended to NCH channels; rows [lo, hi) ---- */
+typedef struct {
+    oracle_state* st;
+    const float* background;
+    float *out_color, *out_depth, *out_alpha, *out_feature;
+} blend_fwd_ctx;
+static void blend_fwd_rows(void* ctx, long lo, long hi, int chunk) {
+    (void)chunk;
+    const blend_fwd_ctx* c = (const blend_fwd_ctx*)ctx;
+    oracle_state* st = c->st;
+    const int W = st->W, H = st->H;
+    const unsigned gx = st->gx;
+    const float* feat_ptr = st->colors_precomp ? st->colors_precomp : st->rgb;
+    const int nch = st->include_feature ? NCH : 5;
+    for (long py = lo; py < hi; py++)
+        for (int px = 0; px < W; px++) {
+            const unsigned tile = (unsigned)(py / BLOCK_Y) * gx + (unsigned)(px / BLOCK_X);
+            const unsigned rs = st->ranges[2 * tile], re = st->ranges[2 * tile + 1];
+            const float pfx = (float)px, pfy = (float)py;
+            float T = 1.0f;
+            unsigned contributor = 0, last_contributor = 0;
+            float C[NCH] = {0};
+            float margin = 1.0f;
+            for (unsigned k = rs; k < re; k++) {
+                contributor++;
+                const unsigned g = st->point_list[k];
+                const float dx = st->means2D[2 * g] - pfx, dy = st->means2D[2 * g + 1] - pfy;
+                const float* co = st->conic_opacity + 4 * (size_t)g;
+                float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
+                if (fabsf(power) < 1e-6f) margin = 0.0f;
+                if (power > 0.0f) continue;
+                float alpha = fminf_cuda(0.99f, co[3] * splat_exp(power));
+                margin = fminf(margin, fabsf(alpha * 255.0f - 1.0f));
+                if (alpha < 1.0f / 255.0f) continue;
+                float test_T = T * (1 - alpha);
+                margin = fminf(margin, fabsf(test_T * 1e4f - 1.0f));
+                if (test_T < 0.0001f) break; /* done: nothing later changes this pixel */
+                float v[NCH];
+                v[0] = feat_ptr[3 * g]; v[1] = feat_ptr[3 * g + 1]; v[2] = feat_ptr[3 * g + 2];
+                v[3] = st->depths[g]; v[4] = 1.0f;
+                v[5] = st->feat[3 * g]; v[6] = st->feat[3 * g + 1]; v[7] = st->feat[3 * g + 2];
+                for (int ch = 0; ch < nch; ch++) C[ch] += v[ch] * alpha * T;
+                T = test_T;
+                last_contributor = contributor;
+            }
+            const size_t pix = (size_t)py * W + px, HW = (size_t)W * H;
+            st->final_T[pix] = T;
+            st->n_contrib[pix] = last_contributor;
+            st->margin[pix] = margin;
+            for (int ch = 0; ch < 3; ch++) c->out_color[ch * HW + pix] = C[ch] + T * c->background[ch];
+            if (c->out_depth) c->out_depth[pix] = C[3];
+            if (c->out_alpha) c->out_alpha[pix] = C[4];
+            if (c->out_feature)
+                for (int ch = 0; ch < 3; ch++)
+                    c->out_feature[ch * HW + pix] = st->include_feature ? C[5 + ch] : 0.0f;
+        }
+}
+
 oracle_state* oracle_forward(int P, int M, const float* background, const float* means3D,
                              const float* colors_precomp, const float* opacities,
                              const float* scales, const float* rotations, float scale_modifier,
@@ -325,69 +580,7 @@ oracle_state* oracle_forward(int P, int M, const float* background, const float*
     st->tiles_touched = (unsigned*)xcalloc(P, sizeof(unsigned));
 
     /* ---- preprocessCUDA, forward.cu:155-256 ---- */
-    for (int idx = 0; idx < P; idx++) {
-        st->radii[idx] = 0;
-        st->tiles_touched[idx] = 0;
-        v3 p_view;
-        if (!in_frustum(idx, means3D, viewmatrix, &p_view)) continue;
-        v3 p_orig = v3_mk(means3D[3 * idx], means3D[3 * idx + 1], means3D[3 * idx + 2]);
-        float p_hom[4];
-        transformPoint4x4(p_orig, projmatrix, p_hom);
-        float p_w = 1.0f / (p_hom[3] + 0.0000001f);
-        float p_proj_x = p_hom[0] * p_w, p_proj_y = p_hom[1] * p_w;
-        const float* c3;
-        if (cov3D_precomp) {
-            c3 = cov3D_precomp + (size_t)idx * 6;
-        } else {
-            cov3d(scales + 3 * (size_t)idx, scale_modifier, rotations + 4 * (size_t)idx,
-                  st->cov3D + (size_t)idx * 6);
-            c3 = st->cov3D + (size_t)idx * 6;
-        }
-        float cov[3];
-        cov2d(p_orig, st->focal_x, st->focal_y, tan_fovx, tan_fovy, c3, viewmatrix, cov);
-        float det = (cov[0] * cov[2] - cov[1] * cov[1]);
-        if (det == 0.0f) continue;
-        float det_inv = 1.f / det;
-        float conic[3] = {cov[2] * det_inv, -cov[1] * det_inv, cov[0] * det_inv};
-        float mid = 0.5f * (cov[0] + cov[2]);
-        float lambda1 = mid + sqrtf(fmaxf_cuda(0.1f, mid * mid - det));
-        float lambda2 = mid - sqrtf(fmaxf_cuda(0.1f, mid * mid - det));
-        float my_radius = ceilf(3.f * sqrtf(fmaxf_cuda(lambda1, lambda2)));
-        float pix_x = ndc2Pix(p_proj_x, W), pix_y = ndc2Pix(p_proj_y, H);
-        u2 rmin, rmax;
-        getRect(pix_x, pix_y, f2i_sat(my_radius), &rmin, &rmax, gx, gy);
-        if ((rmax.x - rmin.x) * (rmax.y - rmin.y) == 0) continue;
-        if (!colors_precomp) {
-            v3 c = color_from_sh(idx, degree, M, means3D, campos, sh, st->clamped);
-            st->rgb[3 * idx + 0] = c.x;
-            st->rgb[3 * idx + 1] = c.y;
-            st->rgb[3 * idx + 2] = c.z;
-        }
-        st->depths[idx] = p_view.z;
-        st->radii[idx] = f2i_sat(my_radius);
-        st->means2D[2 * idx] = pix_x;
-        st->means2D[2 * idx + 1] = pix_y;
-        float op = opacities[idx];
-        if (confidence) op = op * confidence[idx]; /* confidence = opacity multiplier */
-        st->conic_opacity[4 * idx + 0] = conic[0];
-        st->conic_opacity[4 * idx + 1] = conic[1];
-        st->conic_opacity[4 * idx + 2] = conic[2];
-        st->conic_opacity[4 * idx + 3] = op;
-        st->tiles_touched[idx] = (rmax.y - rmin.y) * (rmax.x - rmin.x);
-        if (include_feature) { /* language feature channels */
-            if (language_feature_precomp) {
-                for (int k = 0; k < 3; k++) st->feat[3 * idx + k] = language_feature_precomp[3 * idx + k];
-            } else if (sh_language) {
-                float u0 = SH_C0 * sh_language[3 * idx], u1 = SH_C0 * sh_language[3 * idx + 1],
-                      u2v = SH_C0 * sh_language[3 * idx + 2];
-                float n = sqrtf(u0 * u0 + u1 * u1 + u2v * u2v);
-                float den = n + 1e-9f;
-                st->feat[3 * idx + 0] = u0 / den;
-                st->feat[3 * idx + 1] = u1 / den;
-                st->feat[3 * idx + 2] = u2v / den;
-            }
-        }
-    }
+    par_for(P, preprocess_range, st);
     if (radii_out) memcpy(radii_out, st->radii, sizeof(int) * (size_t)P);
 
     /* ---- scan + duplicateWithKeys + stable SortPairs, rasterizer_impl.cu:70-111, 277-308 ---- */
@@ -416,7 +609,7 @@ oracle_state* oracle_forward(int P, int M, const float* background, const float*
                 }
         }
     }
-    qsort(inst, (size_t)R, sizeof(inst_t), inst_cmp);
+    sort_instances(inst, R);
     st->point_list = (unsigned*)xcalloc((size_t)R, sizeof(unsigned));
     for (int i = 0; i < R; i++) st->point_list[i] = inst[i].val;
     /* identifyTileRanges, rasterizer_impl.cu:116-138 (ranges zeroed first, :310) */
@@ -440,44 +633,9 @@ oracle_state* oracle_forward(int P, int M, const float* background, const float*
     /* ---- renderCUDA (fwd), forward.cu:261-374, extended to NCH channels ---- */
     st->final_T = (float*)xcalloc((size_t)W * H, sizeof(float));
     st->n_contrib = (unsigned*)xcalloc((size_t)W * H, sizeof(unsigned));
-    const float* feat_ptr = colors_precomp ? colors_precomp : st->rgb;
-    const int nch = include_feature ? NCH : 5;
-    for (int py = 0; py < H; py++)
-        for (int px = 0; px < W; px++) {
-            const unsigned tile = (unsigned)(py / BLOCK_Y) * gx + (unsigned)(px / BLOCK_X);
-            const unsigned rs = st->ranges[2 * tile], re = st->ranges[2 * tile + 1];
-            const float pfx = (float)px, pfy = (float)py;
-            float T = 1.0f;
-            unsigned contributor = 0, last_contributor = 0;
-            float C[NCH] = {0};
-            for (unsigned k = rs; k < re; k++) {
-                contributor++;
-                const unsigned g = st->point_list[k];
-                const float dx = st->means2D[2 * g] - pfx, dy = st->means2D[2 * g + 1] - pfy;
-                const float* co = st->conic_opacity + 4 * (size_t)g;
-                float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
-                if (power > 0.0f) continue;
-                float alpha = fminf_cuda(0.99f, co[3] * expf(power));
-                if (alpha < 1.0f / 255.0f) continue;
-                float test_T = T * (1 - alpha);
-                if (test_T < 0.0001f) break; /* done: nothing later changes this pixel */
-                float v[NCH];
-                v[0] = feat_ptr[3 * g]; v[1] = feat_ptr[3 * g + 1]; v[2] = feat_ptr[3 * g + 2];
-                v[3] = st->depths[g]; v[4] = 1.0f;
-                v[5] = st->feat[3 * g]; v[6] = st->feat[3 * g + 1]; v[7] = st->feat[3 * g + 2];
-                for (int ch = 0; ch < nch; ch++) C[ch] += v[ch] * alpha * T;
-                T = test_T;
-                last_contributor = contributor;
-            }
-            const size_t pix = (size_t)py * W + px, HW = (size_t)W * H;
-            st->final_T[pix] = T;
-            st->n_contrib[pix] = last_contributor;
-            for (int ch = 0; ch < 3; ch++) out_color[ch * HW + pix] = C[ch] + T * background[ch];
-            if (out_depth) out_depth[pix] = C[3];
-            if (out_alpha) out_alpha[pix] = C[4];
-            if (out_feature)
-                for (int ch = 0; ch < 3; ch++) out_feature[ch * HW + pix] = include_feature ? C[5 + ch] : 0.0f;
-        }
+    st->margin = (float*)xcalloc((size_t)W * H, sizeof(float));
+    blend_fwd_ctx bc = {st, background, out_color, out_depth, out_alpha, out_feature};
+    par_for(H, blend_fwd_rows, &bc);
     return st;
 }
 
@@ -704,36 +862,37 @@ static void cov3d_backward(int idx, const float* scale, float mod, const float* 
 #undef D
 }
 
-int oracle_backward(oracle_state* st, const float* dL_dout_color, const float* dL_dout_depth,
-                    const float* dL_dout_alpha, const float* dL_dout_feature, float* dL_dmeans2D,
-                    float* dL_dcolors, float* dL_dopacity, float* dL_dmeans3D, float* dL_dcov3D,
-                    float* dL_dsh, float* dL_dscales, float* dL_drotations,
-                    float* dL_dsh_language, float* dL_dlanguage_feature) {
-    if (!st) return 1;
-    const int P = st->P, M = st->M, W = st->W, H = st->H;
+/* ---- renderCUDA (bwd), backward.cu:399-557, per pixel, extended to NCH channels ---- */
+/* Gradient accumulators of one chunk of pixel rows: the caller's arrays (one chunk) or the     */
+/* chunk's private block [colors 3P | depth P | feat 3P | means2D 3P | conic 4P | opacity P].     */
+enum { ACC_COL = 0, ACC_DEP = 3, ACC_FEAT = 4, ACC_M2D = 7, ACC_CON = 10, ACC_OP = 14, ACC_ROW = 15 };
+typedef struct {
+    oracle_state* st;
+    const float *dc, *dd, *da, *df;
+    float* priv;                                        /* private blocks, or NULL */
+    float *dcolors, *ddepth, *dfeat, *dmeans2D, *dconic, *dopacity; /* shared targets */
+} blend_bwd_ctx;
+static void blend_bwd_rows(void* ctx, long lo, long hi, int chunk) {
+    const blend_bwd_ctx* c = (const blend_bwd_ctx*)ctx;
+    oracle_state* st = c->st;
+    const size_t P = (size_t)st->P;
+    float *dL_dcolors, *ddepth, *dfeat, *dL_dmeans2D, *dconic, *dL_dopacity;
+    if (c->priv) {
+        float* b = c->priv + (size_t)chunk * ACC_ROW * P;
+        dL_dcolors = b + ACC_COL * P; ddepth = b + ACC_DEP * P; dfeat = b + ACC_FEAT * P;
+        dL_dmeans2D = b + ACC_M2D * P; dconic = b + ACC_CON * P; dL_dopacity = b + ACC_OP * P;
+    } else {
+        dL_dcolors = c->dcolors; ddepth = c->ddepth; dfeat = c->dfeat;
+        dL_dmeans2D = c->dmeans2D; dconic = c->dconic; dL_dopacity = c->dopacity;
+    }
+    const int W = st->W, H = st->H;
     const size_t HW = (size_t)W * H;
     const unsigned gx = st->gx;
-    /* rasterize_points.cu:151-159 zero-initialised grads */
-    memset(dL_dmeans2D, 0, sizeof(float) * 3 * (size_t)P);
-    memset(dL_dcolors, 0, sizeof(float) * 3 * (size_t)P);
-    memset(dL_dopacity, 0, sizeof(float) * (size_t)P);
-    memset(dL_dmeans3D, 0, sizeof(float) * 3 * (size_t)P);
-    memset(dL_dcov3D, 0, sizeof(float) * 6 * (size_t)P);
-    if (dL_dsh) memset(dL_dsh, 0, sizeof(float) * 3 * (size_t)P * M);
-    if (dL_dscales) memset(dL_dscales, 0, sizeof(float) * 3 * (size_t)P);
-    if (dL_drotations) memset(dL_drotations, 0, sizeof(float) * 4 * (size_t)P);
-    if (dL_dsh_language) memset(dL_dsh_language, 0, sizeof(float) * 3 * (size_t)P);
-    if (dL_dlanguage_feature) memset(dL_dlanguage_feature, 0, sizeof(float) * 3 * (size_t)P);
-    float* dconic = (float*)xcalloc((size_t)P * 4, sizeof(float));
-    float* ddepth = (float*)xcalloc((size_t)P, sizeof(float));
-    float* dfeat = (float*)xcalloc((size_t)P * 3, sizeof(float));
     const float* color_ptr = st->colors_precomp ? st->colors_precomp : st->rgb;
     const int nch = st->include_feature ? NCH : 5;
-
-    /* ---- renderCUDA (bwd), backward.cu:399-557, per pixel, extended to NCH channels ---- */
     const float ddelx_dx = (float)(0.5 * W);
     const float ddely_dy = (float)(0.5 * H);
-    for (int py = 0; py < H; py++)
+    for (long py = lo; py < hi; py++)
         for (int px = 0; px < W; px++) {
             const unsigned tile = (unsigned)(py / BLOCK_Y) * gx + (unsigned)(px / BLOCK_X);
             const unsigned rs = st->ranges[2 * tile], re = st->ranges[2 * tile + 1];
@@ -744,10 +903,10 @@ int oracle_backward(oracle_state* st, const float* dL_dout_color, const float* d
             unsigned contributor = re - rs;
             const unsigned last_contributor = st->n_contrib[pix];
             float accum_rec[NCH] = {0}, last_color[NCH] = {0}, dL_dpixel[NCH] = {0};
-            for (int i = 0; i < 3; i++) dL_dpixel[i] = dL_dout_color[i * HW + pix];
-            dL_dpixel[3] = dL_dout_depth ? dL_dout_depth[pix] : 0.0f;
-            dL_dpixel[4] = dL_dout_alpha ? dL_dout_alpha[pix] : 0.0f;
-            for (int i = 0; i < 3; i++) dL_dpixel[5 + i] = dL_dout_feature ? dL_dout_feature[i * HW + pix] : 0.0f;
+            for (int i = 0; i < 3; i++) dL_dpixel[i] = c->dc[i * HW + pix];
+            dL_dpixel[3] = c->dd ? c->dd[pix] : 0.0f;
+            dL_dpixel[4] = c->da ? c->da[pix] : 0.0f;
+            for (int i = 0; i < 3; i++) dL_dpixel[5 + i] = c->df ? c->df[i * HW + pix] : 0.0f;
             float last_alpha = 0;
             for (unsigned k = re; k-- > rs;) {
                 contributor--;
@@ -757,7 +916,7 @@ int oracle_backward(oracle_state* st, const float* dL_dout_color, const float* d
                 const float* co = st->conic_opacity + 4 * (size_t)g;
                 const float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
                 if (power > 0.0f) continue;
-                const float G = expf(power);
+                const float G = splat_exp(power);
                 const float alpha = fminf_cuda(0.99f, co[3] * G);
                 if (alpha < 1.0f / 255.0f) continue;
                 T = T / (1.f - alpha);
@@ -768,11 +927,11 @@ int oracle_backward(oracle_state* st, const float* dL_dout_color, const float* d
                 v[3] = st->depths[g]; v[4] = 1.0f;
                 v[5] = st->feat[3 * g]; v[6] = st->feat[3 * g + 1]; v[7] = st->feat[3 * g + 2];
                 for (int ch = 0; ch < nch; ch++) {
-                    const float c = v[ch];
+                    const float cv = v[ch];
                     accum_rec[ch] = last_alpha * last_color[ch] + (1.f - last_alpha) * accum_rec[ch];
-                    last_color[ch] = c;
+                    last_color[ch] = cv;
                     const float dL_dchannel = dL_dpixel[ch];
-                    dL_dalpha += (c - accum_rec[ch]) * dL_dchannel;
+                    dL_dalpha += (cv - accum_rec[ch]) * dL_dchannel;
                     const float gv = dchannel_dcolor * dL_dchannel;
                     if (ch < 3) dL_dcolors[3 * (size_t)g + ch] += gv;
                     else if (ch == 3) ddepth[g] += gv;
@@ -796,16 +955,44 @@ int oracle_backward(oracle_state* st, const float* dL_dout_color, const float* d
                 dL_dopacity[g] += G * dL_dalpha;
             }
         }
-
-    /* ---- BACKWARD::preprocess, backward.cu:559-622 ---- */
-    const float* cov3D_ptr = st->cov3D_precomp ? st->cov3D_precomp : st->cov3D;
-    for (int idx = 0; idx < P; idx++) {
-        if (!(st->radii[idx] > 0)) continue;
-        cov2d_backward(idx, st->means3D, cov3D_ptr, st->focal_x, st->focal_y, st->tan_fovx,
-                       st->tan_fovy, st->view, dconic, dL_dmeans3D, dL_dcov3D);
+}
+/* target[i] = sum over chunks (in chunk order) of private slot `slot0`+.. element i */
+typedef struct { const float* priv; int nchunks; size_t P; size_t slot; float* dst; } reduce_ctx;
+static void reduce_range(void* ctx, long lo, long hi, int chunk) {
+    (void)chunk;
+    const reduce_ctx* r = (const reduce_ctx*)ctx;
+    for (long i = lo; i < hi; i++) {
+        float s = 0.0f;
+        for (int c = 0; c < r->nchunks; c++) s += r->priv[(size_t)c * ACC_ROW * r->P + r->slot * r->P + i];
+        r->dst[i] = s;
     }
+}
+
+/* ---- BACKWARD::preprocess, backward.cu:559-622, per Gaussian ---- */
+typedef struct {
+    oracle_state* st;
+    const float* cov3D_ptr;
+    float *dL_dmeans2D, *dL_dcolors, *dL_dopacity, *dL_dmeans3D, *dL_dcov3D, *dL_dsh, *dL_dscales,
+        *dL_drotations, *dL_dsh_language, *dL_dlanguage_feature, *dconic, *ddepth, *dfeat;
+} pre_bwd_ctx;
+static void cov2d_bwd_range(void* ctx, long lo, long hi, int chunk) {
+    (void)chunk;
+    const pre_bwd_ctx* c = (const pre_bwd_ctx*)ctx;
+    oracle_state* st = c->st;
+    for (long i = lo; i < hi; i++) {
+        const int idx = (int)i;
+        if (!(st->radii[idx] > 0)) continue;
+        cov2d_backward(idx, st->means3D, c->cov3D_ptr, st->focal_x, st->focal_y, st->tan_fovx,
+                       st->tan_fovy, st->view, c->dconic, c->dL_dmeans3D, c->dL_dcov3D);
+    }
+}
+static void pre_bwd_range(void* ctx, long lo, long hi, int chunk) {
+    (void)chunk;
+    const pre_bwd_ctx* c = (const pre_bwd_ctx*)ctx;
+    oracle_state* st = c->st;
     const float* proj = st->proj;
-    for (int idx = 0; idx < P; idx++) {
+    for (long i = lo; i < hi; i++) {
+        const int idx = (int)i;
         if (!(st->radii[idx] > 0)) continue;
         /* backward.cu:370-387 */
         v3 m = v3_mk(st->means3D[3 * idx], st->means3D[3 * idx + 1], st->means3D[3 * idx + 2]);
@@ -814,33 +1001,34 @@ int oracle_backward(oracle_state* st, const float* dL_dout_color, const float* d
         float m_w = 1.0f / (m_hom[3] + 0.0000001f);
         float mul1 = (proj[0] * m.x + proj[4] * m.y + proj[8] * m.z + proj[12]) * m_w * m_w;
         float mul2 = (proj[1] * m.x + proj[5] * m.y + proj[9] * m.z + proj[13]) * m_w * m_w;
-        const float gx2 = dL_dmeans2D[3 * idx], gy2 = dL_dmeans2D[3 * idx + 1];
+        const float gx2 = c->dL_dmeans2D[3 * idx], gy2 = c->dL_dmeans2D[3 * idx + 1];
         v3 dm;
         dm.x = (proj[0] * m_w - proj[3] * mul1) * gx2 + (proj[1] * m_w - proj[3] * mul2) * gy2;
         dm.y = (proj[4] * m_w - proj[7] * mul1) * gx2 + (proj[5] * m_w - proj[7] * mul2) * gy2;
         dm.z = (proj[8] * m_w - proj[11] * mul1) * gx2 + (proj[9] * m_w - proj[11] * mul2) * gy2;
-        dL_dmeans3D[3 * idx + 0] += dm.x;
-        dL_dmeans3D[3 * idx + 1] += dm.y;
-        dL_dmeans3D[3 * idx + 2] += dm.z;
-        if (st->sh && dL_dsh)
-            sh_backward(idx, st->D, M, st->means3D, st->campos, st->sh, st->clamped, dL_dcolors,
-                        dL_dmeans3D, dL_dsh);
-        if (st->scales && dL_dscales && dL_drotations)
+        c->dL_dmeans3D[3 * idx + 0] += dm.x;
+        c->dL_dmeans3D[3 * idx + 1] += dm.y;
+        c->dL_dmeans3D[3 * idx + 2] += dm.z;
+        if (st->sh && c->dL_dsh)
+            sh_backward(idx, st->D, st->M, st->means3D, st->campos, st->sh, st->clamped,
+                        c->dL_dcolors, c->dL_dmeans3D, c->dL_dsh);
+        if (st->scales && c->dL_dscales && c->dL_drotations)
             cov3d_backward(idx, st->scales + 3 * (size_t)idx, st->scale_modifier,
-                           st->rotations + 4 * (size_t)idx, dL_dcov3D, dL_dscales, dL_drotations);
+                           st->rotations + 4 * (size_t)idx, c->dL_dcov3D, c->dL_dscales,
+                           c->dL_drotations);
         /* depth channel -> view-space z = view[2]x + view[6]y + view[10]z + view[14] */
-        const float dz = ddepth[idx];
-        dL_dmeans3D[3 * idx + 0] += dz * st->view[2];
-        dL_dmeans3D[3 * idx + 1] += dz * st->view[6];
-        dL_dmeans3D[3 * idx + 2] += dz * st->view[10];
+        const float dz = c->ddepth[idx];
+        c->dL_dmeans3D[3 * idx + 0] += dz * st->view[2];
+        c->dL_dmeans3D[3 * idx + 1] += dz * st->view[6];
+        c->dL_dmeans3D[3 * idx + 2] += dz * st->view[10];
         /* confidence is an opacity multiplier */
-        if (st->confidence) dL_dopacity[idx] = dL_dopacity[idx] * st->confidence[idx];
+        if (st->confidence) c->dL_dopacity[idx] = c->dL_dopacity[idx] * st->confidence[idx];
         if (st->include_feature) {
-            const float* gf = dfeat + 3 * (size_t)idx;
+            const float* gf = c->dfeat + 3 * (size_t)idx;
             if (st->lang_precomp) {
-                if (dL_dlanguage_feature)
-                    for (int k = 0; k < 3; k++) dL_dlanguage_feature[3 * idx + k] = gf[k];
-            } else if (st->sh_language && dL_dsh_language) {
+                if (c->dL_dlanguage_feature)
+                    for (int k = 0; k < 3; k++) c->dL_dlanguage_feature[3 * idx + k] = gf[k];
+            } else if (st->sh_language && c->dL_dsh_language) {
                 /* f = u / (|u| + 1e-9), u = SH_C0 * l */
                 const float* l = st->sh_language + 3 * (size_t)idx;
                 float u0 = SH_C0 * l[0], u1 = SH_C0 * l[1], u2v = SH_C0 * l[2];
@@ -848,12 +1036,61 @@ int oracle_backward(oracle_state* st, const float* dL_dout_color, const float* d
                 float den = n + 1e-9f;
                 float ug = u0 * gf[0] + u1 * gf[1] + u2v * gf[2];
                 float k2 = n > 0.0f ? ug / (den * den * n) : 0.0f;
-                dL_dsh_language[3 * idx + 0] = SH_C0 * (gf[0] / den - u0 * k2);
-                dL_dsh_language[3 * idx + 1] = SH_C0 * (gf[1] / den - u1 * k2);
-                dL_dsh_language[3 * idx + 2] = SH_C0 * (gf[2] / den - u2v * k2);
+                c->dL_dsh_language[3 * idx + 0] = SH_C0 * (gf[0] / den - u0 * k2);
+                c->dL_dsh_language[3 * idx + 1] = SH_C0 * (gf[1] / den - u1 * k2);
+                c->dL_dsh_language[3 * idx + 2] = SH_C0 * (gf[2] / den - u2v * k2);
             }
         }
     }
+}
+
+int oracle_backward(oracle_state* st, const float* dL_dout_color, const float* dL_dout_depth,
+                    const float* dL_dout_alpha, const float* dL_dout_feature, float* dL_dmeans2D,
+                    float* dL_dcolors, float* dL_dopacity, float* dL_dmeans3D, float* dL_dcov3D,
+                    float* dL_dsh, float* dL_dscales, float* dL_drotations,
+                    float* dL_dsh_language, float* dL_dlanguage_feature) {
+    if (!st) return 1;
+    const int P = st->P, M = st->M, H = st->H;
+    /* rasterize_points.cu:151-159 zero-initialised grads */
+    memset(dL_dmeans2D, 0, sizeof(float) * 3 * (size_t)P);
+    memset(dL_dcolors, 0, sizeof(float) * 3 * (size_t)P);
+    memset(dL_dopacity, 0, sizeof(float) * (size_t)P);
+    memset(dL_dmeans3D, 0, sizeof(float) * 3 * (size_t)P);
+    memset(dL_dcov3D, 0, sizeof(float) * 6 * (size_t)P);
+    if (dL_dsh) memset(dL_dsh, 0, sizeof(float) * 3 * (size_t)P * M);
+    if (dL_dscales) memset(dL_dscales, 0, sizeof(float) * 3 * (size_t)P);
+    if (dL_drotations) memset(dL_drotations, 0, sizeof(float) * 4 * (size_t)P);
+    if (dL_dsh_language) memset(dL_dsh_language, 0, sizeof(float) * 3 * (size_t)P);
+    if (dL_dlanguage_feature) memset(dL_dlanguage_feature, 0, sizeof(float) * 3 * (size_t)P);
+    float* dconic = (float*)xcalloc((size_t)P * 4, sizeof(float));
+    float* ddepth = (float*)xcalloc((size_t)P, sizeof(float));
+    float* dfeat = (float*)xcalloc((size_t)P * 3, sizeof(float));
+
+    /* ---- renderCUDA (bwd), backward.cu:399-557 ---- */
+    blend_bwd_ctx bc = {st, dL_dout_color, dL_dout_depth, dL_dout_alpha, dL_dout_feature, NULL,
+                        dL_dcolors, ddepth, dfeat, dL_dmeans2D, dconic, dL_dopacity};
+    const int nchunks = par_chunks(H);
+    if (nchunks > 1) bc.priv = (float*)calloc((size_t)nchunks * ACC_ROW * (size_t)P, sizeof(float));
+    if (bc.priv) par_for(H, blend_bwd_rows, &bc);
+    else blend_bwd_rows(&bc, 0, H, 0); /* one chunk straight into the outputs */
+    if (bc.priv) {
+        float* dst[6] = {dL_dcolors, ddepth, dfeat, dL_dmeans2D, dconic, dL_dopacity};
+        const size_t slot[6] = {ACC_COL, ACC_DEP, ACC_FEAT, ACC_M2D, ACC_CON, ACC_OP};
+        const size_t len[6] = {3, 1, 3, 3, 4, 1};
+        for (int a = 0; a < 6; a++)
+            for (size_t s = 0; s < len[a]; s++) {
+                reduce_ctx rc = {bc.priv, nchunks, (size_t)P, slot[a] + s, dst[a] + s * (size_t)P};
+                par_for(P, reduce_range, &rc);
+            }
+        free(bc.priv);
+    }
+
+    /* ---- BACKWARD::preprocess, backward.cu:559-622 ---- */
+    pre_bwd_ctx pc = {st, st->cov3D_precomp ? st->cov3D_precomp : st->cov3D, dL_dmeans2D,
+                      dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales,
+                      dL_drotations, dL_dsh_language, dL_dlanguage_feature, dconic, ddepth, dfeat};
+    par_for(P, cov2d_bwd_range, &pc);
+    par_for(P, pre_bwd_range, &pc);
     /* invisible Gaussians: the grads of the colour channels etc. are already zero. */
     free(dconic);
     free(ddepth);
@@ -865,7 +1102,7 @@ void oracle_free(oracle_state* st) {
     if (!st) return;
     free(st->depths); free(st->clamped); free(st->radii); free(st->means2D); free(st->cov3D);
     free(st->conic_opacity); free(st->rgb); free(st->feat); free(st->tiles_touched);
-    free(st->point_list); free(st->ranges); free(st->final_T); free(st->n_contrib);
+    free(st->point_list); free(st->ranges); free(st->final_T); free(st->n_contrib); free(st->margin);
     free(st);
 }
 
@@ -873,6 +1110,7 @@ int oracle_get_point_list(const oracle_state* st, unsigned* out) { memcpy(out, s
 int oracle_get_ranges(const oracle_state* st, unsigned* out) { memcpy(out, st->ranges, sizeof(unsigned) * 2 * (size_t)st->gx * st->gy); return 0; }
 int oracle_get_final_T(const oracle_state* st, float* out) { memcpy(out, st->final_T, sizeof(float) * (size_t)st->W * st->H); return 0; }
 int oracle_get_n_contrib(const oracle_state* st, unsigned* out) { memcpy(out, st->n_contrib, sizeof(unsigned) * (size_t)st->W * st->H); return 0; }
+int oracle_get_margin(const oracle_state* st, float* out) { memcpy(out, st->margin, sizeof(float) * (size_t)st->W * st->H); return 0; }
 int oracle_get_means2D(const oracle_state* st, float* out) { memcpy(out, st->means2D, sizeof(float) * 2 * (size_t)st->P); return 0; }
 int oracle_get_conic_opacity(const oracle_state* st, float* out) { memcpy(out, st->conic_opacity, sizeof(float) * 4 * (size_t)st->P); return 0; }
 int oracle_get_depths(const oracle_state* st, float* out) { memcpy(out, st->depths, sizeof(float) * (size_t)st->P); return 0; }

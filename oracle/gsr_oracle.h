@@ -21,8 +21,11 @@
  * here as extra blend channels on the reference's blend arithmetic.
  *
  * Arithmetic: float32, reference expression order, glm column-major conventions, compiled
- * with -ffp-contract=off (no silent FMA contraction); ndc2Pix in double as auxiliary.h:41-44.
- * Single-threaded and deterministic (fixed accumulation order).
+ * with -ffp-contract=off (no silent FMA contraction); ndc2Pix in double as auxiliary.h:41-44;
+ * the blend's exp(power) is splat_exp, the deterministic float exp the HIP kernels also use.
+ * Deterministic: single-threaded by default (the reference's sequential order);
+ * oracle_set_threads(n) splits the loops into n fixed chunks (forward bit-identical; backward
+ * sums per chunk, added in chunk order) for the full-size tests and the CPU baseline.
  */
 #ifndef GSR_ORACLE_H
 #define GSR_ORACLE_H
@@ -34,6 +37,10 @@ extern "C" {
 #endif
 
 typedef struct oracle_state oracle_state;
+
+/* Host threads used by oracle_forward / oracle_backward (1 = sequential, the default). */
+void oracle_set_threads(int n);
+int oracle_get_threads(void);
 
 /* Forward.  Argument order mirrors _C.rasterize_gaussians (rasterize_points.cu:35-55) plus the
  * extended-API inputs.  NULL means "empty tensor" exactly like the reference's nullptr
@@ -97,12 +104,18 @@ int oracle_get_point_list(const oracle_state* st, unsigned* out);   /* [num_rend
 int oracle_get_ranges(const oracle_state* st, unsigned* out);       /* [tiles*2] */
 int oracle_get_final_T(const oracle_state* st, float* out);         /* [H*W] */
 int oracle_get_n_contrib(const oracle_state* st, unsigned* out);    /* [H*W] */
+/* [H*W] min relative distance of the pixel's blend decisions from alpha = 1/255 and
+ * T = 1e-4 (test diagnostic: where two correct float evaluations may decide differently) */
+int oracle_get_margin(const oracle_state* st, float* out);
 int oracle_get_means2D(const oracle_state* st, float* out);         /* [P*2] */
 int oracle_get_conic_opacity(const oracle_state* st, float* out);   /* [P*4] */
 int oracle_get_depths(const oracle_state* st, float* out);          /* [P] */
 int oracle_get_rgb(const oracle_state* st, float* out);             /* [P*3] */
 int oracle_get_tiles_touched(const oracle_state* st, unsigned* out);/* [P] */
 int oracle_get_cov3D(const oracle_state* st, float* out);           /* [P*6] */
+
+/* The blend's exp(power): the deterministic single-precision exp shared with the HIP kernels. */
+void oracle_splat_exp(long n, const float* x, float* out);
 
 /* distCUDA2 (simple_knn, un-vendored; scene/gaussian_model.py:20,198,514) by brute force:
  * gsr_oracle_knn.c.  pts [P,3]; mean [P]; idx [P,3] or NULL. */

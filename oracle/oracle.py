@@ -46,15 +46,27 @@ def lib():
         L.oracle_free.argtypes = [_p]
         L.oracle_mark_visible.restype = _i
         L.oracle_mark_visible.argtypes = [_i, _p, _p, _p, _p]
+        L.oracle_splat_exp.restype = None
+        L.oracle_splat_exp.argtypes = [ctypes.c_long, _p, _p]
+        L.oracle_set_threads.restype = None
+        L.oracle_set_threads.argtypes = [_i]
+        L.oracle_get_threads.restype = _i
+        L.oracle_get_threads.argtypes = []
         L.oracle_dist_knn3.restype = None
         L.oracle_dist_knn3.argtypes = [ctypes.c_int64, _p, _p, _p]
-        for name in ("point_list", "ranges", "final_T", "n_contrib", "means2D", "conic_opacity",
+        for name in ("point_list", "ranges", "final_T", "n_contrib", "margin", "means2D", "conic_opacity",
                      "depths", "rgb", "tiles_touched", "cov3D"):
             fn = getattr(L, "oracle_get_" + name)
             fn.restype = _i
             fn.argtypes = [_p, _p]
         _lib = L
     return _lib
+
+
+def set_threads(n: int) -> int:
+    """Host threads of the oracle's loops (1 = the sequential restatement); returns the value set."""
+    lib().oracle_set_threads(int(n))
+    return int(lib().oracle_get_threads())
 
 
 def _arr(x, dtype=np.float32):
@@ -141,6 +153,13 @@ class OracleRaster:
     def n_contrib(self):
         return self._get("n_contrib", (self.H, self.W), np.uint32)
 
+    def margin(self):
+        """Per pixel: the smallest relative distance of any blend decision from its threshold
+        (|255 alpha - 1|, |1e4 test_T - 1|, 0 for |power| < 1e-6).  Test-side diagnostic: a
+        pixel whose margin is a few ulps can legitimately flip between two correct float
+        implementations (the reference's own expf is specified to 2 ulp)."""
+        return self._get("margin", (self.H, self.W), np.float32)
+
     def means2D(self):
         return self._get("means2D", (self.P, 2), np.float32)
 
@@ -188,6 +207,14 @@ class OracleRaster:
         if rc != 0:
             raise RuntimeError("oracle_backward failed")
         return g
+
+
+def splat_exp(x):
+    """The blend's exp (oracle/gsr_oracle.c splat_exp) of a float32 array."""
+    xs = _arr(x).reshape(-1)
+    out = np.empty_like(xs)
+    lib().oracle_splat_exp(xs.size, _ptr(xs), _ptr(out))
+    return out
 
 
 def mark_visible(means3D, viewmatrix, projmatrix):

@@ -767,6 +767,21 @@ int gsr_test_expf_pair(const float* x, float* ref, float* fast, size_t n, void* 
   return GSR_OK;
 }
 
+int gsr_test_activations(const float* opacity_raw, const float* scaling_raw,
+                         const float* rotation_raw, size_t P, float* opacity, float* scaling,
+                         float* rotation, void* stream_ptr) {
+  g_err.clear();
+  hipStream_t stream = (hipStream_t)stream_ptr;
+  const int debug = 0;
+  if (P && (!opacity_raw || !scaling_raw || !rotation_raw || !opacity || !scaling || !rotation))
+    return fail(GSR_ERR_ARGUMENT, "null pointer");
+  if (!aligned16(rotation_raw) || !aligned16(rotation))
+    return fail(GSR_ERR_ARGUMENT, "rotations must be 16-byte aligned");
+  GSR_CHECK(launch_activations(opacity_raw, scaling_raw, rotation_raw, P, opacity, scaling,
+                               rotation, stream));
+  return GSR_OK;
+}
+
 void gsr_profile_enable(int stage_mask) { prof().mask.store((uint32_t)stage_mask); }
 
 int gsr_profile_collect(double* ms, long long* calls) {

@@ -113,9 +113,14 @@ __device__ __forceinline__ void tile_rect(float px, float py, int r, uint32_t gx
 }
 
 // ---- GaussianModel activations (scene/gaussian_model.py:33-41), for the fused-activation path ----
-// torch.nn.functional.normalize(r, dim=1): r / max(||r||_2, 1e-12)
+// torch.nn.functional.normalize(r, dim=1): r / max(||r||_2, 1e-12).  torch's row norm of 4 floats
+// sums the squares pairwise, (x^2 + y^2) + (z^2 + w^2) (its vectorised reduction's two
+// accumulators); this order reproduces F.normalize bit for bit (scripts/probe_activations.py on
+// MI355X: 0 of 4M rows differ; the sequential sum differed in 12 %)
 __device__ __forceinline__ float quat_norm(float4 r) {
-  return sqrtf(r.x * r.x + r.y * r.y + r.z * r.z + r.w * r.w);
+  const float a = r.x * r.x + r.y * r.y;
+  const float b = r.z * r.z + r.w * r.w;
+  return sqrtf(a + b);
 }
 __device__ __forceinline__ float4 normalize_quat(float4 r) {
   const float d = fmaxf(quat_norm(r), 1e-12f);
@@ -131,24 +136,29 @@ __device__ __forceinline__ float4 normalize_quat_backward(float4 r, float4 go) {
                      go.w / d - k * r.w);
 }
 // torch.sigmoid on float: 1 / (1 + exp(-x)); backward: go * (1 - y) * y
-// expf for the blends' Gaussian weight G = exp(power): OCML's expf sequence (x*log2(e) split into
-// a rounded product and its error term, round-to-nearest-even exponent, v_exp_f32 of the
-// fraction, ldexp) with one range select (x < -104 -> 0; NaN passes through) instead of its two.
-// For every x >= -103.2 it returns OCML's value bit for bit (tested on the GPU,
-// tests/test_gpu_parity.py); in [-104, -103.2) it may give the smallest denormal where OCML gives
-// 0.  Above 88.7 it still returns inf for the range the product stays exact in; the blends skip
-// power > 0 and use G only through alpha = min(0.99, o * G) >= 1/255, so no decision and no
-// output changes.  (Without the select, |x| > 2^23 / log2(e) can leave a positive fraction and
-// return inf.)
-__device__ __forceinline__ float blend_expf(float x) {
-  const float kLog2e = 0x1.715476p+0f, kLog2eLo = 0x1.4ae0bep-26f;
-  const float ph = x * kLog2e;
-  float pl = __builtin_fmaf(x, kLog2e, -ph);
-  pl = __builtin_fmaf(x, kLog2eLo, pl);
-  const float n = __builtin_rintf(ph);
-  const float f = (ph - n) + pl;
-  const float r = __builtin_amdgcn_ldexpf(__builtin_amdgcn_exp2f(f), (int)n);
-  return x < -104.0f ? 0.0f : r;
+// exp for the blends' Gaussian weight G = exp(power) (forward.cu:343, backward.cu:498 call expf).
+// A deterministic single-precision exp: Cody-Waite reduction by ln 2 and a degree-5 polynomial
+// (Cephes expf coefficients), every step a correctly rounded IEEE operation (explicit fma, no
+// hardware exp approximation).  Its error is <= 1.01 ulp of exp over [-87, 0] (~90 % correctly
+// rounded; the reference's CUDA expf is specified to 2 ulp), and the oracle evaluates the SAME
+// sequence (the CPU restatement's splat_exp), so GPU and oracle take identical alpha >= 1/255 and
+// T < 1e-4 decisions on every pixel -- with a libm / OCML expf pair a 1-ulp disagreement at a
+// threshold flips a pixel at 5M Gaussians x 1080p.  Below -104 it returns 0 (alpha < 1/255 there
+// for any opacity); the blends never use power > 0.
+__device__ __forceinline__ float splat_exp(float x) {
+  const float k = __builtin_rintf(x * 1.44269504088896341f);
+  float r = __builtin_fmaf(-k, 0.693359375f, x);
+  r = __builtin_fmaf(-k, -2.12194440e-4f, r);
+  float p = 1.9875691500e-4f;
+  p = __builtin_fmaf(p, r, 1.3981999507e-3f);
+  p = __builtin_fmaf(p, r, 8.3334519073e-3f);
+  p = __builtin_fmaf(p, r, 4.1665795894e-2f);
+  p = __builtin_fmaf(p, r, 1.6666665459e-1f);
+  p = __builtin_fmaf(p, r, 5.0000001201e-1f);
+  const float r2 = r * r;
+  const float y = __builtin_fmaf(p, r2, r) + 1.0f;
+  const float res = __builtin_amdgcn_ldexpf(y, (int)k);
+  return x < -104.0f ? 0.0f : res;
 }
 __device__ __forceinline__ float sigmoid_f(float x) { return 1.0f / (1.0f + expf(-x)); }
 

@@ -204,8 +204,11 @@ struct PrecolorArgs {
   float* jac[kShFlushMaxViewsFwd];       // [P,9]: dRGB/ddir_x, _y, _z (vec3 over the channels)
 };
 hipError_t launch_sh_precolor(const PrecolorArgs& a, hipStream_t s);
-// test hook: ref = OCML expf(x), fast = blend_expf(x) (gsr_device.h)
+// test hook: ref = OCML expf(x), fast = splat_exp(x) (gsr_device.h), the blends' exp
 hipError_t launch_expf_pair(const float* x, float* ref, float* fast, size_t n, hipStream_t s);
+// test hook: the fused path's in-kernel activations (sigmoid / exp / normalize of gsr_device.h)
+hipError_t launch_activations(const float* op_raw, const float* sc_raw, const float* rot_raw,
+                              size_t P, float* op, float* sc, float* rot, hipStream_t s);
 hipError_t launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present,
                                hipStream_t s);
 

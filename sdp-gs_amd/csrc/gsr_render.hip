@@ -27,6 +27,7 @@ namespace gsr {
 namespace {
 
 constexpr int kThreads = kTilePix;  // 256
+constexpr int kAccPad = kAccFloats + 1;  // LDS accumulator row stride (odd: conflict-free columns)
 
 __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t ntiles) {
   const uint32_t q = ntiles >> 3, r = ntiles & 7u;
@@ -226,7 +227,7 @@ __global__ __launch_bounds__(kThreads) void render_fwd_kernel(RenderArgs a) {
         const float power = -0.5f * (r0.z * dx * dx + r1v[u].x * dy * dy) - r0.w * dx * dy;
         // entries past the list end get power = +1 and are skipped like any power > 0 pair
         pw[u] = (k + u < nlist) ? power : 1.0f;
-        al[u] = fminf(0.99f, r1v[u].y * blend_expf(pw[u]));
+        al[u] = fminf(0.99f, r1v[u].y * splat_exp(pw[u]));
       }
 #if GSR_BLEND_STATS
 #pragma unroll
@@ -393,7 +394,10 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
   __shared__ float4 s_r2[kThreads];
   __shared__ float s_f2[FEAT ? kThreads : 1];  // rec[3].x (feature 2) only
   __shared__ uint32_t s_gid[kThreads];
-  __shared__ float s_acc[kThreads][kAccFloats];
+  // accumulator rows padded to an odd stride (17 floats): the per-splat moments pass (lane t ->
+  // row t) and the zero-fill are bank-conflict-free; the butterfly's adds (16 lanes -> 16 slots of
+  // one row) and the flush (4 rows x 16 slots per wave) stay conflict-free as well
+  __shared__ float s_acc[kThreads * kAccPad];
   __shared__ uint8_t s_mask[kThreads];
   __shared__ uint8_t s_list[kThreads / 64][kThreads];
 
@@ -464,8 +468,7 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
   const float ddelx_dx = (float)(0.5 * a.W);
   const float ddely_dy = (float)(0.5 * a.H);
 
-#pragma unroll
-  for (int k = 0; k < kAccFloats; k++) s_acc[threadIdx.x][k] = 0.0f;
+  for (int k = (int)threadIdx.x; k < kThreads * kAccPad; k += kThreads) s_acc[k] = 0.0f;
 
   // rel = position inside the tile's list; every pixel only uses rel < its n_contrib <= tile_last
   for (uint32_t done_cnt = 0; done_cnt < tile_last; done_cnt += kThreads) {
@@ -509,7 +512,7 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
       const float4 r1 = s_r1[j];
       const float dx = r0.x - pfx, dy = r0.y - pfy;
       const float power = -0.5f * (r0.z * dx * dx + r1.x * dy * dy) - r0.w * dx * dy;
-      Gv[u] = blend_expf(power);
+      Gv[u] = splat_exp(power);
       av[u] = fminf(0.99f, r1.y * Gv[u]);
       cv[u] = (k0 + u < nlist) && rel < last_contributor && !(power > 0.0f) &&
               !(av[u] < 1.0f / 255.0f);
@@ -581,7 +584,7 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
       const float sum = wave_reduce16_dpp(g, lane);
       if ((lane & 3) == 0) {
         const int k = reduce16_slot(lane, swap_orient);
-        if (sum != 0.0f) atomicAdd(&s_acc[j][k], sum);
+        if (sum != 0.0f) atomicAdd(&s_acc[j * kAccPad + k], sum);
       }
     }
     }
@@ -590,7 +593,7 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
     if (threadIdx.x < cnt) {
       const float4 r0 = s_r0[threadIdx.x];
       const float4 r1 = s_r1[threadIdx.x];
-      float* row = s_acc[threadIdx.x];
+      float* row = s_acc + threadIdx.x * kAccPad;
       const float sx = row[kAccMx], sy = row[kAccMy];
       const float o = r1.y;
       row[kAccMx] = -(o * (r0.z * sx + r0.w * sy)) * ddelx_dx;
@@ -606,10 +609,10 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
       const uint32_t jj = (uint32_t)it * (kThreads / kAccFloats) + (threadIdx.x >> 4);
       const int k = (int)(threadIdx.x & 15);
       if (jj < cnt) {
-        const float v = s_acc[jj][k];
+        const float v = s_acc[jj * kAccPad + k];
         if (v != 0.0f) {
           atomicAdd(&a.acc[(size_t)s_gid[jj] * kAccFloats + k], v);
-          s_acc[jj][k] = 0.0f;
+          s_acc[jj * kAccPad + k] = 0.0f;
         }
       }
     }
@@ -621,11 +624,35 @@ __global__ void expf_pair_kernel(const float* __restrict__ x, float* __restrict_
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) {
     ref[i] = expf(x[i]);
-    fast[i] = blend_expf(x[i]);
+    fast[i] = splat_exp(x[i]);
   }
 }
 
+// The fused path's GaussianModel activations, exactly as the preprocess / backward kernels evaluate
+// them (gsr_device.h): sigmoid(_opacity), exp(_scaling), normalize(_rotation).
+__global__ void activations_kernel(const float* __restrict__ op_raw, const float* __restrict__ sc_raw,
+                                   const float4* __restrict__ rot_raw, size_t P,
+                                   float* __restrict__ op, float* __restrict__ sc,
+                                   float4* __restrict__ rot) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= P) return;
+  op[i] = sigmoid_f(op_raw[i]);
+  sc[3 * i] = expf(sc_raw[3 * i]);
+  sc[3 * i + 1] = expf(sc_raw[3 * i + 1]);
+  sc[3 * i + 2] = expf(sc_raw[3 * i + 2]);
+  rot[i] = normalize_quat(rot_raw[i]);
+}
+
 }  // namespace
+
+hipError_t launch_activations(const float* op_raw, const float* sc_raw, const float* rot_raw,
+                              size_t P, float* op, float* sc, float* rot, hipStream_t s) {
+  if (P == 0) return hipSuccess;
+  hipLaunchKernelGGL(activations_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s,
+                     op_raw, sc_raw, reinterpret_cast<const float4*>(rot_raw), P, op, sc,
+                     reinterpret_cast<float4*>(rot));
+  return hipGetLastError();
+}
 
 #if GSR_BLEND_STATS
 extern "C" int gsr_test_blend_stats(unsigned long long* out, int reset) {

@@ -175,6 +175,8 @@ def load():
         L.gsr_test_scan.argtypes = [_p, _p, _sz, _i, _p, _p]
         L.gsr_test_expf_pair.restype = _i
         L.gsr_test_expf_pair.argtypes = [_p, _p, _p, _sz, _p]
+        L.gsr_test_activations.restype = _i
+        L.gsr_test_activations.argtypes = [_p, _p, _p, _sz, _p, _p, _p, _p]
         L.gsr_profile_enable.restype = None
         L.gsr_profile_enable.argtypes = [_i]
         L.gsr_profile_collect.restype = _i

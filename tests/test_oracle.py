@@ -309,3 +309,46 @@ def test_oracle_backward_matches_float64_autograd(case):
         assert err < 1e-5, f"{gname}: max err {err:.3e} (scale {scale:.3e})"
         checked += 1
     assert checked >= 5
+
+
+@pytest.mark.parametrize("mode", ["sh", "colors"])
+def test_oracle_threads_match_sequential(mode):
+    """oracle_set_threads only splits loops into fixed chunks: the forward is bit-identical to the
+    sequential restatement, the backward differs only by the association of its per-chunk sums."""
+    from oracle.oracle import set_threads
+    kw = scene(P=3000, W=97, H=61, seed=11, mode=mode, feature="sh")
+    rng = np.random.default_rng(0)
+    g = [rng.standard_normal(s).astype(np.float32) for s in ((3, 61, 97), (1, 61, 97), (1, 61, 97),
+                                                             (3, 61, 97))]
+    res = []
+    try:
+        for n in (1, 5):
+            assert set_threads(n) == n
+            o = OracleRaster(**kw)
+            res.append((o.color.copy(), o.depth.copy(), o.feature.copy(), o.radii.copy(),
+                        o.point_list(), o.backward(*g)))
+    finally:
+        set_threads(1)
+    (c1, d1, f1, r1, p1, g1), (c5, d5, f5, r5, p5, g5) = res
+    for a, b in ((c1, c5), (d1, d5), (f1, f5), (r1, r5), (p1, p5)):
+        np.testing.assert_array_equal(a, b)
+    for k, v in g1.items():
+        if v is None:
+            continue
+        scale = max(float(np.abs(v).max()), 1e-12)
+        assert float(np.abs(v - g5[k]).max()) / scale <= 1e-6, k
+
+
+def test_splat_exp_accuracy():
+    """The blend's deterministic exp (oracle/gsr_oracle.c splat_exp, shared with the kernels):
+    within 1.01 ulp of exp on [-87, 0] (CUDA's expf, which the reference calls, is specified to
+    2 ulp) and 0 below -104."""
+    from oracle.oracle import splat_exp
+    xs = np.concatenate([np.linspace(-87.0, 0.0, 1 << 22, dtype=np.float64).astype(np.float32),
+                         np.float32(-5.54) + np.arange(-2000, 2000, dtype=np.float32) * 1e-6])
+    f = splat_exp(xs)
+    e = np.exp(xs.astype(np.float64))
+    ulp = np.spacing(e.astype(np.float32)).astype(np.float64)
+    assert float(np.max(np.abs(f - e) / ulp)) <= 1.02
+    assert np.mean(f == e.astype(np.float32)) > 0.9  # ~90.6 % correctly rounded
+    assert np.all(splat_exp(np.array([-104.5, -1e30, -np.inf], np.float32)) == 0.0)
