@@ -39,7 +39,10 @@ typedef enum gsr_status {
   GSR_ERR_HIP = 2,          /* a HIP runtime call or kernel launch failed */
   GSR_ERR_ALLOC = 3,        /* the allocator callback returned NULL */
   GSR_ERR_PREFILTERED = 4,  /* a Gaussian was culled although prefiltered was set (auxiliary.h:156-160) */
-  GSR_ERR_TOO_LARGE = 5     /* problem exceeds the scan/sort capacity */
+  GSR_ERR_TOO_LARGE = 5,    /* problem exceeds the scan/sort capacity */
+  GSR_ERR_SORT = 6          /* a sort of this call gave up (bounded look-back) or an id was out of
+                             * range: the call's outputs / gradients are NaN-poisoned (the
+                             * reference traps instead, auxiliary.h:156-160) */
 } gsr_status;
 
 enum { GSR_BUF_GEOM = 0, GSR_BUF_BINNING = 1, GSR_BUF_IMAGE = 2 };
@@ -49,6 +52,17 @@ typedef void* (*gsr_alloc_fn)(void* ctx, size_t bytes, int which);
 
 int gsr_abi_version(void);
 const char* gsr_last_error(void);
+
+/* Status of the forward that used `image_buffer` (GSR_OK or GSR_ERR_SORT with gsr_last_error()).
+ * The reference __trap()s on an invalid state inside the call (auxiliary.h:156-160); here the
+ * one-sweep sorts bound their look-back spin, and a call whose sort gave up -- or whose blend had
+ * to clamp an out-of-range id -- is failed: its outputs and gradients are NaN on the device, its
+ * backward returns GSR_ERR_SORT once the status is published (checked on entry without a wait),
+ * and these checks report it.  wait != 0 blocks until that forward has finished. */
+int gsr_forward_status(const void* image_buffer, int wait);
+/* The same over every forward not yet checked (on any stream of this process), plus failures of
+ * forwards whose mailbox was recycled unchecked.  wait != 0 blocks until they have finished. */
+int gsr_check_forwards(int wait);
 
 /* Forward.  Replaces _C.rasterize_gaussians -> RasterizeGaussiansCUDA (rasterize_points.cu:35-115)
  * -> CudaRasterizer::Rasterizer::forward (rasterizer_impl.cu:198-336); argument order follows the

@@ -22,6 +22,10 @@ int gsr_test_radix_sort_pairs(uint32_t* keys, uint32_t* vals, size_t n, int bits
                               void* stream);
 /* Same, as the depth sort runs it: keys equal to 0xffffffff (culled Gaussians) may end up at any
  * position; every other key is in stable sorted order. */
+/* Test hook: on != 0 makes every one-sweep look-back take its bounded-spin give-up path (the
+ * sort's error word is raised and its output is garbage), to test the same-call backstop. */
+int gsr_test_force_sort_timeout(int on);
+
 int gsr_test_radix_sort_pairs_sentinel(uint32_t* keys, uint32_t* vals, size_t n, int bits,
                                        void* scratch, void* stream);
 /* Scratch bytes needed by gsr_test_scan for n elements. */

@@ -65,6 +65,7 @@ ImgState carve_img(char* base, size_t W, size_t H) {
   s.ranges = c.take<uint2>(gx * gy);
   s.tile_last = c.take<uint32_t>(gx * gy);
   s.order = c.take<uint32_t>(gx * gy);
+  s.status = c.take<uint32_t>(4);
   s.bytes = c.size();
   return s;
 }
@@ -166,6 +167,119 @@ hipEvent_t readback_event() {
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
+// ---- per-call forward status (the same-call backstop of the sorts' bounded look-back) -----------
+// Each forward gets a mailbox: a pinned, device-mapped word the tile-ranges kernel writes the
+// call's status into (kStatus* bits; the forward blend or-s in kStatusClamp), and an event
+// recorded after the forward blend.  No copy and no host wait is added to the forward.  The
+// backward of the same call checks it on entry without blocking (a status already published fails
+// that backward); gsr_forward_status / gsr_check_forwards check with or without waiting.  The
+// device side poisons the outputs (NaN) and the gradients of a failed call in any case.
+constexpr int kMailSlots = 256;
+constexpr uint32_t kMailPending = 0xffffffffu;
+struct Mailbox {
+  const void* key = nullptr;  // the call's image buffer
+  hipEvent_t ev = nullptr;
+  int dev = -1;
+  bool armed = false;
+};
+std::mutex g_mail_mu;
+Mailbox g_mail[kMailSlots];
+volatile uint32_t* g_mail_host = nullptr;
+int g_mail_next = 0;
+std::string g_mail_lost;  // a failed status found when its slot was recycled unchecked
+
+std::string status_message(uint32_t v) {
+  std::string m = "forward status 0x" + std::to_string(v) + ":";
+  if (v & kStatusDepthSort) m += " depth-sort look-back timed out;";
+  if (v & kStatusTileSort) m += " tile-sort look-back timed out;";
+  if (v & kStatusClamp) m += " an out-of-range Gaussian id was clamped;";
+  return m + " the call's outputs and gradients are invalid (NaN-poisoned)";
+}
+
+// caller holds g_mail_mu; returns the final status if known (0 = fine), kMailPending otherwise
+uint32_t mail_read(int i, bool wait) {
+  Mailbox& m = g_mail[i];
+  if (!m.armed) return 0;
+  bool complete = false;
+  if (wait) complete = hipEventSynchronize(m.ev) == hipSuccess;
+  else complete = hipEventQuery(m.ev) == hipSuccess;
+  const uint32_t v = g_mail_host[i];
+  if (v != 0 && v != kMailPending) {  // a failure is final as soon as it is published
+    m.armed = false;
+    return v;
+  }
+  if (complete) {
+    m.armed = false;
+    return v == kMailPending ? 0u : v;  // an event that completed always saw the kernel write
+  }
+  return kMailPending;
+}
+
+// Arm a mailbox for the forward on image buffer `key`; returns the device-visible status word
+// (null if pinned memory is unavailable: the device-side poison still applies).
+uint32_t* mail_post(const void* key, int* slot) {
+  std::lock_guard<std::mutex> l(g_mail_mu);
+  *slot = -1;
+  if (!g_mail_host) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, sizeof(uint32_t) * kMailSlots, hipHostMallocCoherent) != hipSuccess)
+      return nullptr;
+    g_mail_host = (volatile uint32_t*)p;
+    for (int i = 0; i < kMailSlots; i++) g_mail_host[i] = 0;
+  }
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  // retire an older forward on the same buffer and the slot's previous owner without waiting: a
+  // failure they already published is kept for gsr_check_forwards (their outputs and gradients
+  // were poisoned on the device either way)
+  auto retire = [](int j) {
+    const uint32_t v = mail_read(j, false);
+    if (v && v != kMailPending && g_mail_lost.empty()) g_mail_lost = status_message(v);
+    g_mail[j].armed = false;
+  };
+  for (int j = 0; j < kMailSlots; j++)
+    if (g_mail[j].armed && g_mail[j].key == key) retire(j);
+  const int i = g_mail_next;
+  g_mail_next = (g_mail_next + 1) % kMailSlots;
+  Mailbox& m = g_mail[i];
+  if (m.armed) retire(i);
+  if (m.ev && m.dev != dev) {
+    (void)hipEventDestroy(m.ev);
+    m.ev = nullptr;
+  }
+  if (!m.ev && hipEventCreateWithFlags(&m.ev, hipEventDisableTiming) != hipSuccess) {
+    m.ev = nullptr;
+    return nullptr;
+  }
+  m.dev = dev;
+  m.key = key;
+  g_mail_host[i] = kMailPending;
+  *slot = i;
+  void* dptr = nullptr;
+  if (hipHostGetDevicePointer(&dptr, (void*)(g_mail_host + i), 0) != hipSuccess) return nullptr;
+  return (uint32_t*)dptr;
+}
+
+hipError_t mail_arm(int slot, hipStream_t s) {
+  if (slot < 0) return hipSuccess;
+  std::lock_guard<std::mutex> l(g_mail_mu);
+  hipError_t e = hipEventRecord(g_mail[slot].ev, s);
+  g_mail[slot].armed = e == hipSuccess;
+  return e;
+}
+
+// 0 = fine or not yet known (wait = 0); else the failing status
+uint32_t mail_check(const void* key, bool wait) {
+  std::lock_guard<std::mutex> l(g_mail_mu);
+  if (!g_mail_host) return 0;
+  for (int i = 0; i < kMailSlots; i++)
+    if (g_mail[i].armed && g_mail[i].key == key) {
+      const uint32_t v = mail_read(i, wait);
+      return v == kMailPending ? 0u : v;
+    }
+  return 0;
+}
+
 // ---- optional per-stage hipEvent timing (include/gsr_testing.h) ----------------------------------
 struct Profiler {
   std::mutex mu;
@@ -219,6 +333,31 @@ const char* kStageNames[GSR_NUM_STAGES] = {"preprocess", "depth_sort", "scan", "
 extern "C" {
 
 int gsr_abi_version(void) { return GSR_ABI_VERSION; }
+
+int gsr_forward_status(const void* image_buffer, int wait) {
+  g_err.clear();
+  if (const uint32_t v = mail_check(image_buffer, wait != 0))
+    return fail(GSR_ERR_SORT, "%s", status_message(v).c_str());
+  return GSR_OK;
+}
+
+int gsr_check_forwards(int wait) {
+  g_err.clear();
+  std::lock_guard<std::mutex> l(g_mail_mu);
+  if (!g_mail_lost.empty()) {
+    g_err = g_mail_lost;
+    g_mail_lost.clear();
+    return GSR_ERR_SORT;
+  }
+  if (!g_mail_host) return GSR_OK;
+  uint32_t bad = 0;
+  for (int i = 0; i < kMailSlots; i++) {
+    const uint32_t v = mail_read(i, wait != 0);
+    if (v && v != kMailPending && !bad) bad = v;
+  }
+  if (bad) return fail(GSR_ERR_SORT, "%s", status_message(bad).c_str());
+  return GSR_OK;
+}
 const char* gsr_last_error(void) { return g_err.c_str(); }
 
 size_t gsr_geom_buffer_bytes(int P) { return carve_geom(nullptr, (size_t)(P > 0 ? P : 0)).bytes; }
@@ -321,18 +460,15 @@ static int forward_impl(int P, int M, const float* background, const float* mean
   // R = total tile count (order-independent): reduced right after the preprocess and read back
   // while the depth sort and the scan are already queued behind it, so the host's wait and the
   // binning-buffer allocation overlap GPU work instead of draining the stream
-  // flags[1] = R, flags[2] = the sticky look-back timeout counter of earlier sorts (P > 0 here)
-  GSR_CHECK(sum_u32_parts(g.pre_parts, ((size_t)P + 255) / 256, g.flags + 1, stream, true));
+  // flags[1] = R
+  GSR_CHECK(sum_u32_parts(g.pre_parts, ((size_t)P + 255) / 256, g.flags + 1, stream, false));
   PROF_END(PREPROCESS);
   uint32_t* host = pinned_slot();
   hipEvent_t ready = readback_event();
   if (!host || !ready) return fail(GSR_ERR_HIP, "pinned host slot / event creation failed");
-  uint32_t* timeouts = sort_timeouts_word();
-  if (!timeouts) return fail(GSR_ERR_HIP, "sort timeout word unavailable");
-  // one read-back: flags[0] (prefiltered violation), R, and the look-back timeouts of the sorts
-  // of EARLIER calls on this stream (the one-sweep sort's spin bound) -- reported here, one call
-  // late, instead of a sync after every sort
-  GSR_CHECK(hipMemcpyAsync(host, g.flags, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+  // one read-back: flags[0] (prefiltered violation) and R.  The sorts' look-back timeouts are
+  // this call's status (mailbox below), not part of this wait.
+  GSR_CHECK(hipMemcpyAsync(host, g.flags, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
   GSR_CHECK(hipEventRecord(ready, stream));
 
   bool in_b = false;
@@ -347,11 +483,6 @@ static int forward_impl(int P, int M, const float* background, const float* mean
   PROF_END(SCAN);
 
   GSR_CHECK(hipEventSynchronize(ready));
-  if (host[2]) {
-    (void)hipMemsetAsync(timeouts, 0, sizeof(uint32_t), stream);
-    return fail(GSR_ERR_HIP, "a radix-sort look-back timed out in an earlier call on this device: "
-                "that call's outputs are invalid");
-  }
   const uint32_t R = host[1];
   if (prefiltered && host[0]) return fail(GSR_ERR_PREFILTERED,
                            "Point is filtered although prefiltered is set. This shouldn't happen!");
@@ -387,8 +518,12 @@ static int forward_impl(int P, int M, const float* background, const float* mean
   }
   const uint32_t* tiles_sorted = t_in_b ? b.tkey_b : b.tkey_a;
   const uint32_t* point_list = t_in_b ? b.tval_b : b.tval_a;
+  int mail_slot = -1;
+  uint32_t* host_status = mail_post(ibase, &mail_slot);
   PROF_BEGIN(RANGES);
-  GSR_CHECK(launch_tile_ranges(R, tiles_sorted, im.ranges, ntiles, stream, /*ranges_cleared=*/true));
+  GSR_CHECK(launch_tile_ranges(R, tiles_sorted, im.ranges, ntiles, g.sort.aux + kSortAuxErr,
+                               b.sort.aux + kSortAuxErr, im.status, host_status, stream,
+                               /*ranges_cleared=*/true));
   PROF_END(RANGES);
 
   RenderArgs ra{};
@@ -398,9 +533,15 @@ static int forward_impl(int P, int M, const float* background, const float* mean
   ra.out_color = out_color; ra.out_depth = out_depth; ra.out_alpha = out_alpha;
   ra.out_feature = out_feature; ra.include_feature = include_feature;
   ra.order = im.order; ra.sched = tile_schedule_mode();
+  ra.status = im.status; ra.host_status = host_status;
   PROF_BEGIN(RENDER_FWD);
   GSR_CHECK(launch_render_forward(ra, stream));
   PROF_END(RENDER_FWD);
+  GSR_CHECK(mail_arm(mail_slot, stream));
+  if (debug) {
+    const uint32_t v = mail_check(ibase, true);
+    if (v) return fail(GSR_ERR_SORT, "%s", status_message(v).c_str());
+  }
   *num_rendered = (int)R;
   acc_mark_clean(gbase);
   return GSR_OK;
@@ -494,6 +635,10 @@ static int backward_impl(
   if (P == 0) return GSR_OK;
   if (!geom_buffer || !image_buffer || (R > 0 && !binning_buffer))
     return fail(GSR_ERR_ARGUMENT, "forward scratch buffers missing");
+  // the forward of these buffers failed and has already said so (no wait; the device side
+  // poisons the gradients whether or not the host has seen the status yet)
+  if (const uint32_t v = mail_check(image_buffer, debug != 0))
+    return fail(GSR_ERR_SORT, "%s", status_message(v).c_str());
   if (!dL_dout_color || !dL_dmeans2D || !dL_dopacity || !dL_dmeans3D)
     return fail(GSR_ERR_ARGUMENT, "required gradient buffers missing");
   if (sh && !dL_dsh && !dRGB_sh) return fail(GSR_ERR_ARGUMENT, "dL_dsh required when sh is given");
@@ -554,6 +699,7 @@ static int backward_impl(
   ba.opacities_raw = opacity_raw; ba.dL_dsh_rest = dL_dsh_rest;
   ba.dRGB_out = dRGB_sh;
   ba.pre_jac = pre_jac;
+  ba.status = im.status;
   if (dRGB_sh) ba.dL_dsh = ba.dL_dsh_rest = nullptr;
   PROF_BEGIN(PREPROCESS_BWD);
   GSR_CHECK(launch_preprocess_backward(ba, stream));

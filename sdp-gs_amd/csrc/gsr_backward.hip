@@ -314,6 +314,15 @@ __global__ __launch_bounds__(kThreads) void preprocess_bwd_kernel(BwdPreArgs a) 
   const int n = min(kThreads, a.P - base);
   const int t = (int)threadIdx.x;
   const size_t i = (size_t)base + t;
+  if (a.status && *a.status) {  // the forward's sort gave up (grid-uniform): NaN gradients
+    if (t < n) {
+      const float nan = __builtin_nanf("");
+      put3(a.dL_dmeans2D, i, v3(nan, nan, nan));
+      st3<ACC>(a.dL_dmeans3D, i, v3(nan, nan, nan));
+      if (a.dRGB_out) put3(a.dRGB_out, i, v3(nan, nan, nan));
+    }
+    return;
+  }
   const bool live = t < n && a.radii[i] > 0;
   s_live[t] = live;
   // the SH rows are staged unless the colour Jacobian comes from the multi-view pre-pass

@@ -65,9 +65,22 @@ __global__ __launch_bounds__(kThreads) void duplicate_kernel(int P,
 __global__ __launch_bounds__(kThreads) void tile_ranges_kernel(size_t R,
                                                                const uint32_t* __restrict__ tiles,
                                                                uint2* __restrict__ ranges,
-                                                               uint32_t ntiles) {
+                                                               uint32_t ntiles,
+                                                               const uint32_t* __restrict__ derr,
+                                                               const uint32_t* __restrict__ terr,
+                                                               uint32_t* __restrict__ status,
+                                                               uint32_t* host_status) {
   const size_t idx = (size_t)blockIdx.x * kThreads + threadIdx.x;
-  if (idx >= R) return;
+  if (idx >= (R ? R : 1)) return;
+  // the call's status: both sorts have finished (stream order); a timed-out look-back of either
+  // fails this call (render_fwd poisons the outputs, the backward the gradients)
+  if (idx == 0) {
+    const uint32_t st =
+        ((derr && *derr) ? kStatusDepthSort : 0u) | ((terr && *terr) ? kStatusTileSort : 0u);
+    *status = st;
+    if (host_status) *host_status = st;  // pinned mailbox the host checks (gsr_api.cpp)
+  }
+  if (R == 0) return;
   // tile ids are < ntiles by construction; the bounds tests only keep the output of a sort whose
   // look-back gave up (reported by the next read-back) from writing outside the table
   const uint32_t cur = tiles[idx];
@@ -97,14 +110,18 @@ hipError_t launch_duplicate(int P, const uint32_t* order, const uint32_t* offset
 }
 
 hipError_t launch_tile_ranges(size_t R, const uint32_t* sorted_tiles, uint2* ranges,
-                              uint32_t ntiles, hipStream_t s, bool ranges_cleared) {
+                              uint32_t ntiles, const uint32_t* depth_err, const uint32_t* tile_err,
+                              uint32_t* status, uint32_t* host_status, hipStream_t s,
+                              bool ranges_cleared) {
   if (!ranges_cleared) {
     hipError_t e = hipMemsetAsync(ranges, 0, sizeof(uint2) * ntiles, s);
     if (e != hipSuccess) return e;
   }
-  if (R == 0) return hipSuccess;
-  hipLaunchKernelGGL(tile_ranges_kernel, dim3((unsigned)((R + kThreads - 1) / kThreads)),
-                     dim3(kThreads), 0, s, R, sorted_tiles, ranges, ntiles);
+  // R == 0: no instances, nothing tile-sorted; one lane still publishes the depth sort's word
+  const size_t n = R ? R : 1;
+  hipLaunchKernelGGL(tile_ranges_kernel, dim3((unsigned)((n + kThreads - 1) / kThreads)),
+                     dim3(kThreads), 0, s, R, sorted_tiles, ranges, ntiles, depth_err,
+                     R ? tile_err : nullptr, status, host_status);
   return hipGetLastError();
 }
 

@@ -160,9 +160,14 @@ struct ImgState {
   uint2* ranges;        // [tiles]
   uint32_t* tile_last;  // [tiles] max n_contrib over the tile's pixels
   uint32_t* order;      // [tiles] workgroup -> tile schedule (heaviest first)
+  // [4] per-call status of this forward (kStatus* bits): written by the tile-ranges kernel from
+  // the two sorts' error words, or-ed by the forward blend when it clamps an out-of-range id; a
+  // non-zero word poisons this call's outputs and gradients and fails its backward / status check
+  uint32_t* status;
   size_t bytes;
 };
 ImgState carve_img(char* base, size_t W, size_t H);
+constexpr uint32_t kStatusDepthSort = 1u, kStatusTileSort = 2u, kStatusClamp = 4u;
 
 // workgroup -> tile schedule of the blend kernels (env GSR_TILE_ORDER: natural | xcd | lpt)
 int tile_schedule_mode();
@@ -239,6 +244,8 @@ struct BwdPreArgs {
   // with dRGB_out: the SH colour's direction Jacobian of this view from the pre-pass ([P,9]); the
   // SH rows are then not read at all
   const float* pre_jac;
+  // the forward's status word (ImgState::status): non-zero -> NaN gradients (same-call poison)
+  const uint32_t* status;
 };
 hipError_t launch_preprocess_backward(const BwdPreArgs& a, hipStream_t s);
 constexpr int kShFlushMaxViews = 8;
@@ -259,8 +266,11 @@ hipError_t launch_duplicate(int P, const uint32_t* order, const uint32_t* offset
                             uint32_t* tkey, uint32_t* tval, uint32_t R, SideClear clear0,
                             SideClear clear1, hipStream_t s);
 // ranges_cleared: the ranges are already zero (duplicate's side clear): no memset launch.
+// Also writes the call's status word from the depth / tile sorts' error words (either may be null).
 hipError_t launch_tile_ranges(size_t R, const uint32_t* sorted_tiles, uint2* ranges,
-                              uint32_t ntiles, hipStream_t s, bool ranges_cleared = false);
+                              uint32_t ntiles, const uint32_t* depth_err, const uint32_t* tile_err,
+                              uint32_t* status, uint32_t* host_status, hipStream_t s,
+                              bool ranges_cleared = false);
 
 // ---- blend (gsr_render.hip) ----------------------------------------------------------------------
 struct RenderArgs {
@@ -278,6 +288,8 @@ struct RenderArgs {
   int include_feature;
   uint32_t* order;
   int sched;
+  uint32_t* status;  // ImgState::status: non-zero -> NaN outputs; kStatusClamp or-ed on a clamp
+  uint32_t* host_status;  // pinned, device-mapped mirror of the clamp bit (may be null)
 };
 hipError_t launch_render_forward(const RenderArgs& a, hipStream_t s);
 

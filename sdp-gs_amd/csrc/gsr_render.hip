@@ -178,6 +178,24 @@ __global__ __launch_bounds__(kThreads) void render_fwd_kernel(RenderArgs a) {
   bool done = !inside;
   if (threadIdx.x == 0) s_max = 0;
 
+  // a sort of this call gave up (look-back timeout): the lists are not the reference's, so the
+  // call's outputs are NaN and its backward fails (gsr_api.cpp) instead of training on them
+  if (*a.status & (kStatusDepthSort | kStatusTileSort)) {
+    if (threadIdx.x == 0) a.tile_last[tile] = 0;
+    if (inside) {
+      const size_t pix = (size_t)py * a.W + px, HW = (size_t)a.W * a.H;
+      const float nan = __builtin_nanf("");
+      a.final_T[pix] = nan;
+      a.n_contrib[pix] = 0;
+      for (int c = 0; c < 3; c++) a.out_color[c * HW + pix] = nan;
+      if (a.out_depth) a.out_depth[pix] = nan;
+      if (a.out_alpha) a.out_alpha[pix] = nan;
+      if (a.out_feature)
+        for (int c = 0; c < 3; c++) a.out_feature[c * HW + pix] = nan;
+    }
+    return;
+  }
+
   const uint2 range = a.ranges[tile];
   float T = 1.0f;
   uint32_t last_contributor = 0;
@@ -191,7 +209,12 @@ __global__ __launch_bounds__(kThreads) void render_fwd_kernel(RenderArgs a) {
     if (__syncthreads_count(done) == kThreads) break;
     const uint32_t i = base + threadIdx.x;
     if (i < range.y) {
-      const uint32_t gid = min(a.point_list[i], a.P - 1u);
+      const uint32_t pid = a.point_list[i];
+      if (pid >= a.P) {  // memory-safe clamp, reported to this call's status check
+        atomicOr(a.status, kStatusClamp);
+        if (a.host_status) *a.host_status = kStatusClamp;  // sort bits are 0 on this path
+      }
+      const uint32_t gid = min(pid, a.P - 1u);
       const float4* rec = a.rec + 4 * (size_t)gid;
       const float4 q0 = rec[0], q1 = rec[1], q3 = rec[3];
       s_r0[threadIdx.x] = q0;

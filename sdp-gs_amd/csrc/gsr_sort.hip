@@ -148,6 +148,8 @@ constexpr uint64_t kStAgg = 1ull << 32, kStIncl = 2ull << 32, kStFlags = 3ull <<
 }  // namespace
 // count of timed-out look-backs since the last check (sort_timeouts_word)
 __device__ uint32_t g_lookback_timeouts;
+// test hook (gsr_test_force_sort_timeout): every look-back behaves as if its spin bound ran out
+__device__ uint32_t g_force_lookback_timeout;
 #ifndef GSR_SORT_TRACE
 #define GSR_SORT_TRACE 0
 #endif
@@ -380,6 +382,10 @@ __global__ __launch_bounds__(NT, NT == 1024 ? 8 : (NT == 512 ? 6 : 1)) void radi
     // ends there at the latest
     int spins = 0;
     int64_t q = (int64_t)part - 1;
+    if (g_force_lookback_timeout) {  // test hook only: the bounded spin's give-up path
+      atomicOr(err, 1u);
+      atomicAdd(&g_lookback_timeouts, 1u);
+    } else
     for (;;) {
       uint64_t w[kLookback];
 #pragma unroll
@@ -499,6 +505,11 @@ extern "C" int gsr_test_sort_trace(uint64_t* out, int parts) {
              == hipSuccess ? 0 : 2;
 }
 #endif
+
+extern "C" int gsr_test_force_sort_timeout(int on) {
+  const uint32_t v = on ? 1u : 0u;
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_force_lookback_timeout), &v, sizeof(v)) == hipSuccess ? 0 : 2;
+}
 
 uint32_t* sort_timeouts_word() {
   void* p = nullptr;

@@ -554,10 +554,13 @@ class ShGradDeferral:
         d_rgb0, _, _, degree, M, m3 = self.views[0]
         P = int(m3.shape[0])
         cur = torch.cuda.current_stream(self.device)
-        accumulate = dc.grad is not None
+        # one flag for both planes: add when either already holds a gradient (a missing one is
+        # then created as zeros), store when neither does
+        accumulate = any(t is not None and t.grad is not None for t in (dc, rest))
         for t in (dc, rest):
             if t is not None and t.grad is None:
-                t.grad = torch.empty_like(t, memory_format=torch.contiguous_format)
+                t.grad = (torch.zeros_like if accumulate else torch.empty_like)(
+                    t, memory_format=torch.contiguous_format)
         n = len(self.views)
         camp = (_lib.ctypes.c_void_p * n)(*[v[1].data_ptr() for v in self.views])
         rgbs = (_lib.ctypes.c_void_p * n)(*[v[0].data_ptr() for v in self.views])
@@ -644,6 +647,14 @@ class GaussianRasterizer(nn.Module):
         return rasterize_gaussians_extended(means3D, means2D, shs, shs_language, colors_precomp,
                                             language_feature_precomp, opacities, scales, rotations,
                                             cov3D_precomp, rs)
+
+
+def check_forwards(wait: bool = True):
+    """Raise if a forward since the last check failed (a one-sweep sort gave up its bounded
+    look-back, or an out-of-range id had to be clamped).  Such a call's outputs and gradients are
+    NaN on the device and its backward raises once the failure is published; this check is the
+    blocking form (wait=True) for the end of a training step (include/gsr.h gsr_check_forwards)."""
+    _lib.check_forwards(wait)
 
 
 def mark_visible(positions, viewmatrix, projmatrix):

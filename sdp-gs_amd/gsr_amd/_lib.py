@@ -157,6 +157,10 @@ def load():
         L.gsr_dist_knn3.argtypes = [_i64, _p, _p, _p, _p, _p]
         L.gsr_mark_visible.restype = _i
         L.gsr_mark_visible.argtypes = [_i, _p, _p, _p, _p, _p]
+        L.gsr_forward_status.restype = _i
+        L.gsr_forward_status.argtypes = [_p, _i]
+        L.gsr_check_forwards.restype = _i
+        L.gsr_check_forwards.argtypes = [_i]
         for n in ("gsr_geom_buffer_bytes", "gsr_binning_buffer_bytes"):
             getattr(L, n).restype = _sz
             getattr(L, n).argtypes = [_i]
@@ -175,6 +179,8 @@ def load():
         L.gsr_test_scan.argtypes = [_p, _p, _sz, _i, _p, _p]
         L.gsr_test_expf_pair.restype = _i
         L.gsr_test_expf_pair.argtypes = [_p, _p, _p, _sz, _p]
+        L.gsr_test_force_sort_timeout.restype = _i
+        L.gsr_test_force_sort_timeout.argtypes = [_i]
         L.gsr_test_activations.restype = _i
         L.gsr_test_activations.argtypes = [_p, _p, _p, _sz, _p, _p, _p, _p]
         L.gsr_profile_enable.restype = None
@@ -194,6 +200,13 @@ def check(rc: int):
     if rc != 0:
         msg = load().gsr_last_error().decode(errors="replace")
         raise GsrError(f"libgsr error {rc}: {msg}")
+
+
+def check_forwards(wait: bool = True):
+    """Raise GsrError if any forward not yet checked failed (a sort gave up its bounded
+    look-back or an id had to be clamped; that call's outputs and gradients are NaN).  wait
+    blocks until those forwards have finished (include/gsr.h gsr_check_forwards)."""
+    check(load().gsr_check_forwards(1 if wait else 0))
 
 
 # --- allocator callback: the library asks for its three scratch buffers through it ---------------
