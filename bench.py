@@ -113,7 +113,11 @@ def main():
                          "per step (diff_gaussian_rasterization.ShGradDeferral)")
     ap.add_argument("--no-precolor", action="store_true",
                     help="each view evaluates its SH colour itself instead of the step's pre-pass")
-    ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_r01.json"))
+    ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_r02.json"))
+    ap.add_argument("--no-extra-legs", action="store_true",
+                    help="skip the train-step, reference-cadence and reference-API legs")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="host threads of the CPU baseline (0: OMP_NUM_THREADS or all cores)")
     args = ap.parse_args()
 
     from gsr_amd import _lib
@@ -137,7 +141,8 @@ def main():
     my_cams = [cams_all[i].to(dev) for i in shard_views(n_views, rank, world)]
     dimg, ddep, dfeat = upstream_grads(H, W, seed=1, device=dev)
     bg = torch.zeros(3, device=dev)
-    reducer = GradAllReducer(model.parameters()) if world > 1 else None
+    # re-reads the model's parameters every step (densification replaces them)
+    reducer = GradAllReducer(model) if world > 1 else None
     pipe, opt = Pipe(), Opt()
     stats = {"R": [], "Pv": []}
     defer_sh = not args.no_defer_sh and not args.autograd_grads
@@ -158,9 +163,9 @@ def main():
         else:
             for p in model.parameters():
                 p.grad = None
-        views.run(my_cams, lambda cam: one_view(cam, record), model=model)
-        if reducer is not None:
-            reducer.allreduce()
+        # with a reducer the all-reduce overlaps the step's tail (non-SH grads while the SH
+        # gradients are flushed in row slices, each slice reduced as soon as it is written)
+        views.run(my_cams, lambda cam: one_view(cam, record), model=model, reducer=reducer)
 
     for _ in range(args.warmup):
         step()
@@ -183,13 +188,15 @@ def main():
         dom_stage = max(busy, key=busy.get) if busy else None
         timer.reset()
 
-    def timed_region():
+    def timed_region(fn=None, steps=None):
+        fn = fn or step
+        steps = args.steps if steps is None else steps
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(args.steps):
-            step()
+        for i in range(steps):
+            fn(i)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -200,12 +207,12 @@ def main():
             el = float(t.item())
         return el
 
-    elapsed = timed_region()
+    elapsed = timed_region(lambda i: step())
     stages = dict(all_stages)
     dom_elapsed = None
     if dom_stage is not None:
         timer.enable(True, stages=[dom_stage])
-        dom_elapsed = timed_region()
+        dom_elapsed = timed_region(lambda i: step())
         timer.enable(False)
         stages[dom_stage] = timer.collect()[dom_stage]  # measured over the second timed region
 
@@ -267,9 +274,15 @@ def main():
         except (OSError, ValueError):
             pass
 
+    legs = {}
+    if not args.no_extra_legs:
+        legs = extra_legs(args, model, my_cams, cams_all, views, reducer, timed_region, rank,
+                          world, dev, (P, W, H, deg), (dimg, ddep, dfeat), bg)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_baseline_views > 0:
-        cpu = cpu_baseline(model, cams_all[: args.cpu_baseline_views], dimg, ddep, dfeat, deg)
+        cpu = cpu_baseline(model, cams_all[: args.cpu_baseline_views], dimg, ddep, dfeat, deg,
+                           args.cpu_threads)
 
     if rank == 0:
         line = {
@@ -300,43 +313,210 @@ def main():
             "cpu_baseline": cpu,
             "kernels": kernels,
         }
+        line.update(legs)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
-def cpu_baseline(model, cams, dimg, ddep, dfeat, deg):
-    """The CPU restatement (oracle/, single-threaded C) on a bounded sample of the same workload:
-    `len(cams)` full views (forward + backward).  Rank 0 at N = 1 only."""
+def extra_legs(args, model, my_cams, cams_all, views, reducer, timed_region, rank, world, dev,
+               wl, grads, bg):
+    """The other ways the reference's users run this path, timed like the headline (same
+    barrier / synchronize / max-over-ranks region, K steps after W warm-up steps):
+
+    * reference_api: render() through the reference's own operator API -- GSR_FUSED=0, so
+      GaussianModel's getters and the Python SH pre-pass run as torch ops and
+      GaussianRasterizer gets the activated tensors, autograd returns the gradients, one view
+      at a time on one stream (gaussian_renderer/__init__.py:209-338 as written);
+    * train_step: the training iteration of train.py (render -> L1 + SSIM + Pearson depth loss ->
+      backward -> densification statistics -> FusedAdam step), batched over this rank's views
+      on the HIP streams, gradients all-reduced across ranks (gsr_amd.trainer.train_step_views);
+      plus one densify_and_prune (train.py:223-225) timed on its own, and the step rate with it
+      amortised over its 100-iteration interval;
+    * reference_cadence: train.py's cadence exactly -- one view per iteration, one stream, Adam
+      after every view (gsr_amd.trainer.train_iteration), rank 0 at N = 1.
+    These legs train the model (the headline is measured before them)."""
+    import diff_gaussian_rasterization as dgr
+    from gaussian_renderer import render
+    from gsr_amd import trainer
+    from gsr_amd.synthetic import training_targets
+    P, W, H, deg = wl
+    dimg, ddep, dfeat = grads
+    out = {}
+    n_views = len(my_cams) * world
+
+    # ---- reference operator API (no fused entry, no grad-into-leaves, one stream) ----------
+    prev_fused = os.environ.get("GSR_FUSED")
+    prev_leaves = dgr.grad_into_leaves(False)
+    os.environ["GSR_FUSED"] = "0"
     try:
-        from oracle.oracle import OracleRaster, build
+        def ref_api_step():
+            for p in model.parameters():
+                p.grad = None
+            for cam in my_cams:
+                pkg = render(cam, model, Pipe(), bg, Opt())
+                torch.autograd.backward([pkg["render"], pkg["depth"], pkg["feature"]],
+                                        [dimg, ddep, dfeat])
+            if reducer is not None:
+                reducer.allreduce()
+        for _ in range(args.warmup):
+            ref_api_step()
+        el = timed_region(lambda i: ref_api_step())
+        out["reference_api"] = {
+            "value": round(args.steps * n_views / el, 3), "unit": "views/s",
+            "ms_per_step": round(1000.0 * el / args.steps, 3),
+            "path": "render() -> GaussianRasterizer (GSR_FUSED=0): torch getters + Python SH, "
+                    "autograd grads, 1 stream, views_per_gpu views per step"}
+    finally:
+        if prev_fused is None:
+            os.environ.pop("GSR_FUSED", None)
+        else:
+            os.environ["GSR_FUSED"] = prev_fused
+        dgr.grad_into_leaves(prev_leaves)
+
+    # ---- training: batched step, densify_and_prune, train.py cadence -----------------------------
+    targs = trainer.OptArgs()
+    trainer.make_trainable(model, targs)
+    if reducer is not None:
+        reducer.attach_grads()  # the parameters are now the trainer's nn.Parameters
+    gts, monos = training_targets(len(my_cams), H, W, seed=2 + rank, device=dev)
+    extent = 2.78  # ~ the scene extent of make_gaussians (tests/test_densify.py EXTENT)
+    dgr.grad_into_leaves(True)
+    it = [1]  # iteration counter below densify_from_iter: no densification inside the steps
+
+    def train_step():
+        trainer.train_step_views(model, my_cams, gts, monos, bg, targs, it[0], extent, views,
+                                 reducer=reducer)
+        it[0] += 1
+    for _ in range(args.warmup):
+        train_step()
+    el = timed_region(lambda i: train_step())
+    step_ms = 1000.0 * el / args.steps
+    leg = {"value": round(args.steps * n_views / el, 3), "unit": "views/s",
+           "ms_per_step": round(step_ms, 3),
+           "step": "per view: render + L1/SSIM + Pearson depth loss + backward + densification "
+                   "statistics; per step: gradient all-reduce (N>1) + FusedAdam",
+           "views_per_step": n_views}
+    # one densify_and_prune on the statistics of these steps (iteration 1000: clone + split +
+    # prune, no proximity), timed alone, then amortised over densification_interval steps
+    gen = torch.Generator(device=dev).manual_seed(0)
+    P0 = int(model._xyz.shape[0])
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    from gsr_amd.parallel import allreduce_densification_stats
+    allreduce_densification_stats(model.xyz_gradient_accum, model.denom, model.max_radii2D)
+    trainer.densify_step(model, targs, 1000, extent, generator=gen)
+    torch.cuda.synchronize()
+    d_ms = 1000.0 * (time.perf_counter() - t0)
+    leg["densify_and_prune_ms"] = round(d_ms, 3)
+    leg["densify_rows"] = [P0, int(model._xyz.shape[0])]
+    amort = step_ms + d_ms / targs.densification_interval
+    leg["value_with_densify"] = round(1000.0 * n_views / amort, 3)
+    out["train_step"] = leg
+
+    if world == 1:
+        for p in model.parameters():
+            p.grad = None
+        cams1 = list(my_cams)
+
+        def ref_iter(i):
+            k = i % len(cams1)
+            trainer.train_iteration(model, cams1[k], gts[k], monos[k], bg, targs, 1 + i, extent)
+        n_it = args.steps * len(cams1)
+        for i in range(args.warmup):
+            ref_iter(i)
+        el = timed_region(ref_iter, steps=n_it)
+        out["reference_cadence"] = {
+            "value": round(n_it / el, 3), "unit": "views/s",
+            "ms_per_view": round(1000.0 * el / n_it, 3),
+            "step": "train.py: one view per iteration, one stream, FusedAdam after every view"}
+    return out
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or platform.machine()
+
+
+def cpu_baseline(model, cams, dimg, ddep, dfeat, deg, threads=0):
+    """The CPU restatement (oracle/: C, float32, the reference's arithmetic) on the host cores,
+    timed in this run (rank 0 at N = 1), 2 warm-ups then the median of 5 (BASELINE.md CPU plan):
+      * config 1: 10k synthetic Gaussians, one 400x400 camera, forward only (SH degree 0 as
+        render()'s default Python SH at active degree 0);
+      * the headline workload: one full view of it, forward + backward.
+    Threads: OMP_NUM_THREADS (the box's CPU share) or all cores; the oracle splits its loops into
+    fixed chunks, one per thread (oracle/gsr_oracle.c)."""
+    try:
+        from oracle.oracle import OracleRaster, build, set_threads
         build()
     except Exception as exc:  # pragma: no cover - reported, not fatal
         return {"value": None, "error": repr(exc)[:200]}
+    from gsr_amd.synthetic import make_cameras, make_gaussians
+    n = threads or int(os.environ.get("OMP_NUM_THREADS") or 0) or (os.cpu_count() or 1)
+    n = set_threads(n)
+
+    def kw_of(m_xyz, m_op, m_sh, m_sc, m_rot, m_lang, degree):
+        return dict(means3D=m_xyz, opacities=m_op, shs=m_sh, sh_degree=degree, scales=m_sc,
+                    rotations=m_rot, shs_language=m_lang, include_feature=True,
+                    bg=np.zeros(3, np.float32))
+
+    def cam_kw(cam):
+        return dict(viewmatrix=cam.world_view_transform.cpu().numpy(),
+                    projmatrix=cam.full_proj_transform.cpu().numpy(),
+                    campos=cam.camera_center.cpu().numpy(),
+                    tanfovx=math.tan(cam.FoVx * 0.5), tanfovy=math.tan(cam.FoVy * 0.5),
+                    image_height=cam.image_height, image_width=cam.image_width)
+
+    def median_time(fn, warm=2, reps=5):
+        for _ in range(warm):
+            fn()
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        return float(np.median(ts))
+
+    # config 1
+    g1 = make_gaussians(10_000, sh_degree=3, seed=0)
+    c1 = make_cameras(1, 400, 400, seed=0)[0]
+    kw1 = kw_of(g1.xyz.numpy(), g1.get_opacity().numpy(), g1.get_features().numpy(),
+                g1.get_scaling().numpy(), g1.get_rotation().numpy(), g1.language_feature.numpy(),
+                0)
+    kw1.update(cam_kw(c1))
+    t1 = median_time(lambda: OracleRaster(**kw1))
+
+    # one headline view, forward + backward
     with torch.no_grad():
-        xyz = model.get_xyz.detach().cpu().numpy()
-        kw_common = dict(
-            means3D=xyz, opacities=model.get_opacity.detach().cpu().numpy(),
-            shs=model.get_features.detach().cpu().numpy(), sh_degree=deg,
-            scales=model.get_scaling.detach().cpu().numpy(),
-            rotations=model.get_rotation.detach().cpu().numpy(),
-            shs_language=model.get_language_feature.detach().cpu().numpy(), include_feature=True,
-            bg=np.zeros(3, np.float32))
+        kwh = kw_of(model.get_xyz.detach().cpu().numpy(),
+                    model.get_opacity.detach().cpu().numpy(),
+                    model.get_features.detach().cpu().numpy(),
+                    model.get_scaling.detach().cpu().numpy(),
+                    model.get_rotation.detach().cpu().numpy(),
+                    model.get_language_feature.detach().cpu().numpy(), deg)
         dimg_n, ddep_n, dfeat_n = (t.detach().cpu().numpy() for t in (dimg, ddep, dfeat))
-    t0 = time.perf_counter()
-    for cam in cams:
-        orc = OracleRaster(viewmatrix=cam.world_view_transform.cpu().numpy(),
-                           projmatrix=cam.full_proj_transform.cpu().numpy(),
-                           campos=cam.camera_center.cpu().numpy(),
-                           tanfovx=math.tan(cam.FoVx * 0.5), tanfovy=math.tan(cam.FoVy * 0.5),
-                           image_height=cam.image_height, image_width=cam.image_width, **kw_common)
-        orc.backward(dimg_n, ddep_n, None, dfeat_n)
-        del orc
-    dt = time.perf_counter() - t0
-    return {"value": round(len(cams) / dt, 4), "unit": "views/s", "cores": 1, "kind": "port",
-            "sample": f"{len(cams)} full views (fwd+bwd) of the same workload on the oracle "
-                      f"(single-threaded C restatement), {dt:.1f} s",
-            "cpu": platform.processor() or platform.machine()}
+    kwh.update(cam_kw(cams[0]))
+
+    def fwd_bwd():
+        OracleRaster(**kwh).backward(dimg_n, ddep_n, None, dfeat_n)
+    th = median_time(fwd_bwd)
+    return {"value": round(1.0 / th, 4), "unit": "views/s", "cores": n, "kind": "port",
+            "sample": (f"one headline view ({cams[0].image_width}x{cams[0].image_height}, "
+                       f"{kwh['means3D'].shape[0]} Gaussians, SH degree {deg}, fwd+bwd) on the C "
+                       f"restatement with {n} threads: median of 5 after 2 warm-ups, "
+                       f"{1000 * th:.0f} ms"),
+            "config1_fwd_views_per_s": round(1.0 / t1, 3),
+            "config1": (f"10k Gaussians, 400x400, forward only, SH degree 0: median "
+                        f"{1000 * t1:.1f} ms"),
+            "cpu": _cpu_model(), "os_cpu_count": os.cpu_count(),
+            "threads": n}
 
 
 if __name__ == "__main__":

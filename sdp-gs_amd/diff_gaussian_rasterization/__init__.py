@@ -518,10 +518,16 @@ class ShGradDeferral:
     the reference's own per-view SH backward (backward.cu:20-139) summed in view order.  The
     .grad of the SH leaves is only complete after flush() (the context's exit flushes)."""
 
-    def __init__(self, device):
+    def __init__(self, device, on_rows=None, chunk_rows: int = 0):
+        """on_rows(a, b): called after the flush of Gaussian rows [a, b) has been issued on the
+        current stream (gsr_amd.parallel.GradAllReducer starts that slice's all-reduce there);
+        chunk_rows > 0 splits the flush into row ranges of that size (multiple of 256)."""
         self.device = torch.device(device)
         self.views = []
         self.leaves = None
+        self.on_rows = on_rows
+        self.chunk_rows = int(chunk_rows)
+        self.views_flushed = False  # a flush wrote SH gradients (the on_rows hooks ran)
 
     def __enter__(self):
         if self.device.index in _SH_DEFER:
@@ -550,6 +556,7 @@ class ShGradDeferral:
         be ordered after every view's backward, e.g. joined by ViewPipeline.run)."""
         if not self.views:
             return
+        self.views_flushed = True
         _, dc, rest = self.leaves[0], self.leaves[1], self.leaves[2]
         d_rgb0, _, _, degree, M, m3 = self.views[0]
         P = int(m3.shape[0])
@@ -563,13 +570,21 @@ class ShGradDeferral:
                     t, memory_format=torch.contiguous_format)
         n = len(self.views)
         camp = (_lib.ctypes.c_void_p * n)(*[v[1].data_ptr() for v in self.views])
-        rgbs = (_lib.ctypes.c_void_p * n)(*[v[0].data_ptr() for v in self.views])
-        with torch.cuda.device(self.device):
-            rc = _lib.load().gsr_sh_grad_flush(P, M, degree, _ptr(m3), n, camp, rgbs,
-                                               _ptr(dc.grad),
-                                               _ptr(rest.grad) if rest is not None else None,
-                                               int(accumulate), cur.cuda_stream)
-        _lib.check(rc)
+        step = P if self.chunk_rows <= 0 else max(256, (self.chunk_rows // 256) * 256)
+        rest_w = 3 * (M - 1)
+        L = _lib.load()
+        for a in range(0, P, step):  # row slices: the kernel is per Gaussian, pointers offset
+            b = min(P, a + step)
+            rgbs = (_lib.ctypes.c_void_p * n)(*[v[0].data_ptr() + 12 * a for v in self.views])
+            with torch.cuda.device(self.device):
+                rc = L.gsr_sh_grad_flush(b - a, M, degree, _ptr(m3) + 12 * a, n, camp, rgbs,
+                                         _ptr(dc.grad) + 12 * a,
+                                         (_ptr(rest.grad) + 4 * rest_w * a)
+                                         if rest is not None else None,
+                                         int(accumulate), cur.cuda_stream)
+            _lib.check(rc)
+            if self.on_rows is not None:
+                self.on_rows(a, b)
         for v in self.views:  # buffers made on the views' streams, read here on this one
             v[0].record_stream(cur)
             v[1].record_stream(cur)

@@ -132,6 +132,9 @@ def classify(self, grad_accum, denom, grad_threshold, scale_limit, min_opacity=f
 
 
 # ---- statistics (every step) ---------------------------------------------------------------------
+_STATS_EVENT = {}  # device index -> (event after the last statistics update, its stream id)
+
+
 def _stats(self, grad, radii, filt, with_radii, with_grad):
     P = _rows(self.xyz_gradient_accum)
     _cuda(grad, radii, filt)
@@ -144,12 +147,21 @@ def _stats(self, grad, radii, filt, with_radii, with_grad):
     for t in (self.xyz_gradient_accum, self.denom, self.max_radii2D):
         assert t.is_contiguous() and t.numel() == P
     dev = self.xyz_gradient_accum.device
+    stream = torch.cuda.current_stream(dev)
+    prev = _STATS_EVENT.get(dev.index)
+    if prev is not None and prev[1] != stream.stream_id:
+        # the statistics are read-modify-written without atomics: views on other streams
+        # (gsr_amd.pipeline.ViewPipeline) add theirs in issue order, as train.py does per view
+        stream.wait_event(prev[0])
     with torch.cuda.device(dev):
         _check(_lib.load().gsr_densify_stats(
             P, _ptr(grad) if with_grad else None, grad.stride(0) if with_grad else 0,
             _ptr(radii), _ptr(filt), _ptr(self.max_radii2D) if with_radii else None,
             _ptr(self.xyz_gradient_accum) if with_grad else None,
             _ptr(self.denom) if with_grad else None, _stream(dev)), "gsr_densify_stats")
+    ev = torch.cuda.Event()
+    ev.record(stream)
+    _STATS_EVENT[dev.index] = (ev, stream.stream_id)
 
 
 def add_densification_stats(self, viewspace_point_tensor, update_filter):

@@ -12,7 +12,7 @@ all-reduced asynchronously while the next one is packed, instead of one collecti
 from __future__ import annotations
 
 import os
-from typing import Iterable, List, Sequence
+from typing import Iterable, List
 
 import torch
 import torch.distributed as dist
@@ -26,70 +26,174 @@ def shard_views(n_views: int, rank: int, world: int) -> List[int]:
 
 
 class GradAllReducer:
-    """Bucketed SUM all-reduce of .grad over a fixed list of parameters."""
+    """Bucketed SUM all-reduce of .grad over the model's parameters.
 
-    def __init__(self, params: Sequence[torch.Tensor], bucket_bytes: int = 64 << 20,
-                 group=None, average: bool = False):
-        self.params = list(params)
+    ``params`` is the model (anything with ``.parameters()``), a callable returning the current
+    parameter list, or a fixed sequence.  With a model or a callable the parameter list is re-read
+    at every attach_grads() / allreduce() / begin(): densification (gsr_amd.densify) replaces every
+    parameter with a new tensor of another row count, and the flat buffer, its offsets and buckets
+    are rebuilt whenever the list (identity or size) changes -- a fixed sequence cannot see that.
+
+    Two ways to use it per step:
+      * ``allreduce()`` after the step's backward: one bucketed all-reduce of everything;
+      * overlapped (ViewPipeline.run(..., reducer=...)): ``begin()``, then ``reduce_async(params)``
+        as soon as those gradients are final (the non-SH leaves, right after the last view's
+        backward) and ``reduce_rows_async(param, a, b)`` for row slices finished later (the SH
+        gradients, flushed in bucket-sized row ranges), then ``wait()``.  RCCL runs the
+        collectives on its own stream, ordered after the work already issued on the current
+        stream, so they overlap the flush of the next slice.
+    """
+
+    def __init__(self, params, bucket_bytes: int = 64 << 20, group=None, average: bool = False):
+        self._source = params
         self.group = group
         self.average = average
-        dev = self.params[0].device
-        self.numel = sum(p.numel() for p in self.params)
+        self.bucket_bytes = int(bucket_bytes)
+        self._sig = None
+        self._works = []
+        self._sync_layout()
+
+    # -- layout -----------------------------------------------------------------------------------
+    def current_params(self) -> List[torch.Tensor]:
+        src = self._source
+        if hasattr(src, "parameters"):
+            ps = src.parameters()
+        elif callable(src):
+            ps = src()
+        else:
+            ps = src
+        return [p for p in ps if p is not None]
+
+    def _sync_layout(self):
+        params = self.current_params()
+        sig = tuple((id(p), p.numel(), str(p.device)) for p in params)
+        if sig == self._sig:
+            return False
+        if self._works:
+            raise RuntimeError("GradAllReducer: parameters changed while collectives are in flight")
+        self._sig = sig
+        self.params = params
+        dev = params[0].device
+        self.numel = sum(p.numel() for p in params)
         self.flat = torch.zeros(self.numel, dtype=torch.float32, device=dev)
-        # bucket boundaries on whole tensors where possible, split big tensors by elements
-        per = max(1, bucket_bytes // 4)
+        per = max(1, self.bucket_bytes // 4)
         self.buckets = [(s, min(s + per, self.numel)) for s in range(0, self.numel, per)]
         self.offsets = []
         off = 0
-        for p in self.params:
+        for p in params:
             self.offsets.append(off)
             off += p.numel()
+        self._index = {id(p): i for i, p in enumerate(params)}
+        return True
+
+    def _active(self):
+        return dist.is_available() and dist.is_initialized() and \
+            dist.get_world_size(self.group) > 1
 
     def attach_grads(self):
         """Zero the flat buffer and make every parameter's .grad a view into it (gradient as
-        bucket view): the backward then accumulates straight into the all-reduce buffer and
-        allreduce() needs no pack / unpack copies.  Call instead of zero_grad()."""
+        bucket view): the backward then accumulates straight into the all-reduce buffer and the
+        reduction needs no pack / unpack copies.  Call instead of zero_grad()."""
+        self._sync_layout()
         self.flat.zero_()
         for p, off in zip(self.params, self.offsets):
             p.grad = self.flat[off:off + p.numel()].view_as(p)
 
     def _attached(self, p, off):
         g = p.grad
-        return (g is not None and g.data_ptr() == self.flat[off:off + 1].data_ptr()
-                and g.is_contiguous())
+        return (g is not None and g.is_contiguous() and g.numel() == p.numel()
+                and g.data_ptr() == self.flat[off:off + 1].data_ptr())
 
-    def _pack(self):
-        for p, off in zip(self.params, self.offsets):
-            n = p.numel()
-            if self._attached(p, off):
-                continue
-            if p.grad is None:
-                self.flat[off:off + n].zero_()
+    def _range(self, p, a=None, b=None):
+        """Flat [lo, hi) of rows [a, b) of parameter p (all rows when a is None)."""
+        i = self._index.get(id(p))
+        if i is None:
+            raise KeyError("GradAllReducer: not one of the current parameters")
+        off, n = self.offsets[i], p.numel()
+        if a is None:
+            return i, off, off + n
+        row = n // max(1, p.shape[0])
+        return i, off + a * row, off + min(b, p.shape[0]) * row
+
+    def _pack(self, i, lo, hi):
+        p, off = self.params[i], self.offsets[i]
+        if self._attached(p, off):
+            return
+        dst = self.flat[lo:hi]
+        if p.grad is None:
+            dst.zero_()
+        else:
+            dst.copy_(p.grad.reshape(-1)[lo - off:hi - off])
+
+    def _issue(self, lo, hi):
+        per = max(1, self.bucket_bytes // 4)
+        for a in range(lo, hi, per):
+            self._works.append(dist.all_reduce(self.flat[a:min(a + per, hi)],
+                                               op=dist.ReduceOp.SUM, group=self.group,
+                                               async_op=True))
+
+    # -- overlapped use -----------------------------------------------------------------------------
+    def begin(self):
+        """Start of a step's reduction: re-read the parameters (after a densification)."""
+        self._sync_layout()
+        self._works = []
+        self._done = set()
+
+    def reduce_async(self, params: Iterable[torch.Tensor]):
+        """Start the all-reduce of these parameters' whole gradients (no-op at world size 1)."""
+        if not self._active():
+            return
+        spans = []
+        for p in params:
+            i, lo, hi = self._range(p)
+            self._pack(i, lo, hi)
+            spans.append((lo, hi))
+            self._done.add(i)
+        spans.sort()
+        merged = []
+        for lo, hi in spans:  # adjacent tensors of the flat buffer go out as one collective
+            if merged and merged[-1][1] == lo:
+                merged[-1] = (merged[-1][0], hi)
             else:
-                self.flat[off:off + n].copy_(p.grad.reshape(-1))
+                merged.append((lo, hi))
+        for lo, hi in merged:
+            self._issue(lo, hi)
 
-    def _unpack(self):
-        for p, off in zip(self.params, self.offsets):
-            n = p.numel()
-            if self._attached(p, off):
+    def reduce_rows_async(self, p: torch.Tensor, a: int, b: int):
+        """Start the all-reduce of rows [a, b) of p's gradient."""
+        if not self._active():
+            return
+        i, lo, hi = self._range(p, a, b)
+        self._pack(i, lo, hi)
+        self._issue(lo, hi)
+        self._done.add(i)
+
+    def wait(self):
+        """Finish the step's reduction: wait for the collectives (their results are ordered
+        before later work on the current stream), average if asked, unpack non-view grads."""
+        if not self._active():
+            return
+        for w in self._works:
+            w.wait()
+        self._works = []
+        if self.average:
+            self.flat.div_(dist.get_world_size(self.group))
+        for i, (p, off) in enumerate(zip(self.params, self.offsets)):
+            if i not in self._done or self._attached(p, off):
                 continue
-            v = self.flat[off:off + n].view_as(p)
+            v = self.flat[off:off + p.numel()].view_as(p)
             if p.grad is None:
                 p.grad = v.clone()
             else:
                 p.grad.copy_(v)
 
+    # -- one-shot ------------------------------------------------------------------------------------
     def allreduce(self):
-        if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(self.group) == 1:
+        if not self._active():
             return
-        self._pack()
-        works = [dist.all_reduce(self.flat[a:b], op=dist.ReduceOp.SUM, group=self.group,
-                                 async_op=True) for a, b in self.buckets]
-        for w in works:
-            w.wait()
-        if self.average:
-            self.flat.div_(dist.get_world_size(self.group))
-        self._unpack()
+        self.begin()
+        self.reduce_async(self.params)
+        self.wait()
 
 
 def allreduce_densification_stats(xyz_gradient_accum: torch.Tensor, denom: torch.Tensor,

@@ -50,14 +50,21 @@ class ViewPipeline:
         self.side = [torch.cuda.Stream(device=self.device) for _ in range(depth - 1)]
 
     def run(self, items: Iterable[T], fn: Callable[[T], R], model=None,
-            campos_of: Callable[[T], torch.Tensor] = lambda cam: cam.camera_center) -> List[R]:
+            campos_of: Callable[[T], torch.Tensor] = lambda cam: cam.camera_center,
+            reducer=None) -> List[R]:
         """Call fn(item) for every item, item i issued on stream i mod depth.  fn should do a
         view's render + backward and return host values (or tensors it no longer needs on the
         device): tensors created on a side stream and used after run() on the main stream need
         Tensor.record_stream to be safe under the caching allocator.  With defer_sh the SH
         leaves' .grad is complete when run() returns, not after each view.  model (a
         GaussianModel: _xyz, _features_dc, _features_rest, active_sh_degree) enables the colour
-        pre-pass for the cameras campos_of(item)."""
+        pre-pass for the cameras campos_of(item).
+
+        reducer (gsr_amd.parallel.GradAllReducer over model's parameters, multi-GPU): the
+        step's gradient all-reduce is overlapped with the end of the step -- the non-SH
+        gradients (final once the last view's backward is done) are reduced while the deferred
+        SH gradients are flushed in bucket-sized row slices, each slice reduced as soon as it is
+        flushed.  The reduction is complete (on the current stream) when run() returns."""
         import diff_gaussian_rasterization as dgr
         items = list(items)
         main = torch.cuda.current_stream(self.device)
@@ -72,7 +79,21 @@ class ViewPipeline:
         for s in self.side:
             s.wait_stream(main)  # inputs prepared on the main stream (zeroed grads, pre-pass)
         out = []
-        defer = dgr.ShGradDeferral(self.device) if self.defer_sh else contextlib.nullcontext()
+        sh_leaves = ()
+        on_rows, chunk = None, 0
+        if reducer is not None:
+            reducer.begin()
+            if self.defer_sh and model is not None:
+                dc, rest = model._features_dc, model._features_rest
+                sh_leaves = tuple(t for t in (dc, rest) if t is not None)
+                row_bytes = sum(t[0].numel() * 4 for t in sh_leaves)
+                chunk = max(256, reducer.bucket_bytes // max(1, row_bytes))
+
+                def on_rows(a, b):
+                    for t in sh_leaves:
+                        reducer.reduce_rows_async(t, a, b)
+        defer = (dgr.ShGradDeferral(self.device, on_rows=on_rows, chunk_rows=chunk)
+                 if self.defer_sh else contextlib.nullcontext())
         with pre, defer:  # defer's exit: the SH gradients of all views, after the join
             for i, it in enumerate(items):
                 s = streams[i % self.depth]
@@ -80,4 +101,11 @@ class ViewPipeline:
                     out.append(fn(it))
             for s in self.side:
                 main.wait_stream(s)
+            if reducer is not None:  # every view's backward is done: the non-SH grads are final
+                ids = {id(t) for t in sh_leaves}
+                reducer.reduce_async([p for p in reducer.current_params() if id(p) not in ids])
+        if reducer is not None:
+            if sh_leaves and not defer.views_flushed:
+                reducer.reduce_async(sh_leaves)  # no view produced deferred SH gradients
+            reducer.wait()
         return out

@@ -110,3 +110,13 @@ def upstream_grads(H: int, W: int, seed: int = 1, device="cpu"):
     ddepth = torch.randn((1, H, W), generator=g)
     dfeat = torch.randn((3, H, W), generator=g)
     return dimg.to(device), ddepth.to(device), dfeat.to(device)
+
+
+def training_targets(n: int, H: int, W: int, seed: int = 2, device="cpu"):
+    """Synthetic per-camera training targets for the train-step benchmark: a ground-truth image
+    [3,H,W] in [0,1] and a monocular depth map [1,H,W] in [1,3] (the shape train.py reads from
+    viewpoint_cam.original_image / depth_mono, train.py:97,117)."""
+    g = torch.Generator().manual_seed(seed)
+    gts = [torch.rand((3, H, W), generator=g).to(device) for _ in range(n)]
+    monos = [(1.0 + 2.0 * torch.rand((1, H, W), generator=g)).to(device) for _ in range(n)]
+    return gts, monos

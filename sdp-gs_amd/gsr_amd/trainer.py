@@ -1,0 +1,136 @@
+"""The training iteration around the rasterizer (train.py:63-236), on libgsr.
+
+`train_iteration` is the reference's per-iteration body for one camera with the depth branch:
+
+    render(cam) -> loss = (1 - lambda_dssim) * L1 + lambda_dssim * (1 - SSIM)      (train.py:93-100)
+                        + depth_weight * min(1 - pearson(d_mono, d), 1 - pearson(1/(200 - d_mono), d))
+                                                                                     (train.py:117-131)
+    loss.backward()                                                                  (train.py:194)
+    max_radii2D / add_densification_stats; densify_and_prune every
+    densification_interval iterations inside [densify_from_iter, densify_until_iter) (:218-225)
+    optimizer.step(); optimizer.zero_grad(set_to_none=True)                          (:229-231)
+
+The language-feature loss (loss_feature_metric) and the pseudo-view branch (:101-193) need the
+scene's CLIP features / MiDaS depth, which a synthetic benchmark does not have; the feature image is
+still rendered (include_feature) and the pseudo-view interval is past end_sample_pseudo at the
+reference's defaults for most of training.  `train_step_views` is the batched multi-view form of the
+same iteration (ViewPipeline over HIP streams, gradients summed over the views, one optimizer step;
+with a GradAllReducer the per-view gradients of all ranks are summed first).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+import torch
+
+
+@dataclass
+class OptArgs:
+    """OptimizationParams fields the iteration reads (arguments/__init__.py:73-120)."""
+    percent_dense: float = 0.01
+    position_lr_init: float = 0.016
+    feature_lr: float = 0.0025
+    opacity_lr: float = 0.05
+    scaling_lr: float = 0.003
+    rotation_lr: float = 0.001
+    language_feature_lr: float = 0.013
+    lambda_dssim: float = 0.2
+    densification_interval: int = 100
+    densify_from_iter: int = 500
+    densify_until_iter: int = 6000
+    densify_grad_threshold: float = 0.0013
+    prune_threshold: float = 0.01
+    depth_weight: float = 0.05
+    include_feature: bool = True
+
+
+class _Pipe:  # PipelineParams defaults (arguments/__init__.py:66-72)
+    convert_SHs_python = True
+    compute_cov3D_python = False
+    debug = False
+    use_confidence = False
+
+
+def make_trainable(model, args: OptArgs, spatial_lr_scale: float = 1.0):
+    """GaussianModel.training_setup (scene/gaussian_model.py:217-271) with FusedAdam."""
+    model.training_setup(args, spatial_lr_scale=spatial_lr_scale)
+    return model
+
+
+def _view_loss(pkg, gt_image, depth_mono, args: OptArgs):
+    from .losses import depth_pearson_loss, photometric_loss
+    loss, _ = photometric_loss(pkg["render"], gt_image, args.lambda_dssim)
+    if depth_mono is not None:
+        loss = loss + args.depth_weight * depth_pearson_loss(depth_mono, pkg["depth"])
+    return loss
+
+
+def _densify_due(iteration: int, args: OptArgs) -> bool:
+    return (iteration < args.densify_until_iter and iteration > args.densify_from_iter
+            and iteration % args.densification_interval == 0)
+
+
+def densify_step(model, args: OptArgs, iteration: int, extent: float, generator=None):
+    """train.py:223-225 (size_threshold None)."""
+    model.densify_and_prune(args.densify_grad_threshold, args.prune_threshold, extent, None,
+                            iteration, args.include_feature, generator=generator)
+
+
+def train_iteration(model, cam, gt_image, depth_mono, bg, args: OptArgs, iteration: int,
+                    extent: float, pipe=None):
+    """One reference iteration on one camera.  Returns the loss tensor (not synchronised)."""
+    from gaussian_renderer import render
+    pipe = pipe or _Pipe()
+    pkg = render(cam, model, pipe, bg, args)
+    loss = _view_loss(pkg, gt_image, depth_mono, args)
+    loss.backward()
+    with torch.no_grad():
+        if iteration < args.densify_until_iter:
+            model.update_densification_stats(pkg["viewspace_points"], pkg["radii"],
+                                             pkg["visibility_filter"])
+            if _densify_due(iteration, args):
+                densify_step(model, args, iteration, extent)
+        model.optimizer.step()
+        model.optimizer.zero_grad(set_to_none=True)
+    return loss.detach()
+
+
+def train_step_views(model, cams: Sequence, gt_images: Sequence[torch.Tensor],
+                     depth_monos: Sequence[Optional[torch.Tensor]], bg, args: OptArgs,
+                     iteration: int, extent: float, pipeline, reducer=None, pipe=None,
+                     generator=None) -> List[torch.Tensor]:
+    """The batched iteration: every camera's render + loss + backward + statistics on the
+    pipeline's streams (gradients summed over the views), the gradient all-reduce across ranks
+    (reducer, overlapped with the step's tail), densification when due (statistics summed / maxed
+    across ranks first, identical generator on every rank), one optimizer step."""
+    from gaussian_renderer import render
+    from .parallel import allreduce_densification_stats
+    pipe = pipe or _Pipe()
+    if reducer is not None:
+        reducer.attach_grads()
+    else:
+        model.optimizer.zero_grad(set_to_none=True)
+    gts = {id(c): (g, d) for c, g, d in zip(cams, gt_images, depth_monos)}
+
+    def one(cam):
+        pkg = render(cam, model, pipe, bg, args)
+        gt, dm = gts[id(cam)]
+        loss = _view_loss(pkg, gt, dm, args)
+        loss.backward()
+        with torch.no_grad():
+            if iteration < args.densify_until_iter:
+                model.update_densification_stats(pkg["viewspace_points"], pkg["radii"],
+                                                 pkg["visibility_filter"])
+        return loss.detach()
+
+    losses = pipeline.run(cams, one, model=model, reducer=reducer)
+    with torch.no_grad():
+        if _densify_due(iteration, args):
+            allreduce_densification_stats(model.xyz_gradient_accum, model.denom,
+                                           model.max_radii2D)
+            densify_step(model, args, iteration, extent, generator=generator)
+        # after a densification the new parameters have no .grad: Adam skips them, as in the
+        # reference (train.py:223-231)
+        model.optimizer.step()
+    return losses

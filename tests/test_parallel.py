@@ -85,6 +85,79 @@ def test_sharded_allreduce_equals_single_process(n_views, bucket_bytes, attach):
     torch.testing.assert_close(radii, torch.arange(10, dtype=torch.float32) * 2)
 
 
+class _Model:
+    """Stand-in for a GaussianModel: densify() replaces every parameter with a new, longer one
+    (gsr_amd.densify._rebuild does the same with nn.Parameters)."""
+
+    def __init__(self):
+        self.params = _params()
+
+    def parameters(self):
+        return list(self.params)
+
+    def densify(self, extra=300):
+        g = torch.Generator().manual_seed(99)
+        self.params = [torch.cat([p.detach(), torch.randn((extra,) + tuple(p.shape[1:]),
+                                                          generator=g)]).requires_grad_(True)
+                       for p in self.params]
+
+
+def _overlapped_worker(rank, world, init, n_views, q):
+    """Two steps with a densification between them; the reducer is built once on the model.
+    Step order as ViewPipeline.run(reducer=...): non-SH gradients reduced first, then the 'SH'
+    parameter (params[1]) in row slices as they are 'flushed'."""
+    dist.init_process_group("gloo", init_method=init, rank=rank, world_size=world)
+    model = _Model()
+    reducer = GradAllReducer(model, bucket_bytes=4096)
+    out = []
+    for step in range(2):
+        if step == 1:
+            model.densify()
+        reducer.attach_grads()  # re-reads the (new) parameters
+        ps = model.parameters()
+        assert reducer.numel == sum(p.numel() for p in ps)
+        for v in shard_views(n_views, rank, world):
+            _view_loss(ps, v + step).backward()
+        reducer.begin()
+        reducer.reduce_async([ps[0], ps[2]])
+        rows = ps[1].shape[0]
+        for a in range(0, rows, 256):
+            reducer.reduce_rows_async(ps[1], a, min(rows, a + 256))
+        reducer.wait()
+        out.append([p.grad.numpy().copy() for p in ps])
+    if rank == 0:
+        q.put(out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_overlapped_allreduce_follows_densification():
+    """after densification replaces the parameters, the reducer rebuilds its flat
+    buffer and the new .grad are the ones reduced; the sliced (overlapped) ordering gives the
+    single-process gradients."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    init = _init_method()
+    procs = [ctx.Process(target=_overlapped_worker, args=(r, 2, init, 5, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref = _Model()
+    for step in range(2):
+        if step == 1:
+            ref.densify()
+        ps = ref.parameters()
+        for p in ps:
+            p.grad = None
+        for v in range(5):
+            _view_loss(ps, v + step).backward()
+        for g, p in zip(out[step], ps):
+            torch.testing.assert_close(torch.from_numpy(g), p.grad, rtol=1e-5, atol=1e-6)
+
+
 def test_shard_views_partition():
     for n in range(0, 20):
         for world in (1, 2, 3, 8):
