@@ -397,21 +397,37 @@ def extra_legs(args, model, my_cams, cams_all, views, reducer, timed_region, ran
            "step": "per view: render + L1/SSIM + Pearson depth loss + backward + densification "
                    "statistics; per step: gradient all-reduce (N>1) + FusedAdam",
            "views_per_step": n_views}
-    # one densify_and_prune on the statistics of these steps (iteration 1000: clone + split +
-    # prune, no proximity), timed alone, then amortised over densification_interval steps
+    # densify_and_prune on the statistics of these steps at iteration 2500 (clone + split + prune,
+    # past the proximity window of gaussian_model.py:591-604), with the gradient threshold set to
+    # the 90th percentile of this scene's accumulated view-space gradients so that about 10 % of
+    # the Gaussians clone or split (synthetic targets give gradients far below the reference's
+    # 0.0013); one untimed call first (first-use allocations), then K more training steps, then
+    # the timed call.  Amortised over densification_interval steps for value_with_densify.
+    from gsr_amd.parallel import allreduce_densification_stats
     gen = torch.Generator(device=dev).manual_seed(0)
+    dargs = trainer.OptArgs(**{**targs.__dict__})
+
+    def densify_once():
+        allreduce_densification_stats(model.xyz_gradient_accum, model.denom, model.max_radii2D)
+        g = (model.xyz_gradient_accum / model.denom).nan_to_num_(0.0).reshape(-1)
+        dargs.densify_grad_threshold = float(torch.quantile(g[g > 0][: 1 << 24], 0.9)) \
+            if bool((g > 0).any()) else targs.densify_grad_threshold
+        trainer.densify_step(model, dargs, 2500, extent, generator=gen)
+
+    densify_once()
+    for _ in range(args.steps):
+        train_step()
     P0 = int(model._xyz.shape[0])
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    from gsr_amd.parallel import allreduce_densification_stats
-    allreduce_densification_stats(model.xyz_gradient_accum, model.denom, model.max_radii2D)
-    trainer.densify_step(model, targs, 1000, extent, generator=gen)
+    densify_once()
     torch.cuda.synchronize()
     d_ms = 1000.0 * (time.perf_counter() - t0)
     leg["densify_and_prune_ms"] = round(d_ms, 3)
     leg["densify_rows"] = [P0, int(model._xyz.shape[0])]
+    leg["densify_grad_threshold"] = dargs.densify_grad_threshold
     amort = step_ms + d_ms / targs.densification_interval
     leg["value_with_densify"] = round(1000.0 * n_views / amort, 3)
     out["train_step"] = leg

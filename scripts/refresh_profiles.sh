@@ -4,5 +4,5 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 bash scripts/gpu_pmc.sh || exit $?
-python3 scripts/pmc_summary.py gpurun_out/pmc profiles/pmc_r01.json && cp profiles/pmc_r01.json gpurun_out/pmc_r01.json || exit $?
+python3 scripts/pmc_summary.py gpurun_out/pmc profiles/pmc_r02.json && cp profiles/pmc_r02.json gpurun_out/pmc_r02.json || exit $?
 bash scripts/gpu_check.sh

@@ -10,6 +10,9 @@ L = _lib.load()
 rng = np.random.default_rng(0)
 cases = [("depth1M", rng.lognormal(1.0, 0.5, 1_000_000).astype(np.float32).view(np.uint32), 32),
          ("tiles3M", np.minimum(rng.exponential(300.0, 2_960_000), 3023).astype(np.uint32), 12)]
+if os.environ.get("SORT_LARGE", "0") == "1":  # config 5: 5M Gaussians, 16.3M instances, 8160 tiles
+    cases += [("depth5M", rng.lognormal(1.0, 0.5, 5_000_000).astype(np.float32).view(np.uint32), 32),
+              ("tiles16M", np.minimum(rng.exponential(800.0, 16_250_000), 8159).astype(np.uint32), 13)]
 for name, keys, bits in cases:
     n = keys.size
     k0 = torch.tensor(keys.view(np.int32), device="cuda")

@@ -473,13 +473,15 @@ static int forward_impl(int P, int M, const float* background, const float* mean
 
   bool in_b = false;
   PROF_BEGIN(DEPTH_SORT);
+  // the last pass writes each Gaussian's tile count in place of its sorted key
   GSR_CHECK(radix_sort_pairs(g.dkey_a, g.dval_a, g.dkey_b, g.dval_b, (size_t)P, 32,
                              g.sort, &in_b, stream, /*sentinel_anywhere=*/true,
-                             /*precleared=*/true));
+                             /*precleared=*/true, /*key_payload=*/g.tiles_touched));
   PROF_END(DEPTH_SORT);
   const uint32_t* order = in_b ? g.dval_b : g.dval_a;
+  const uint32_t* counts_sorted = in_b ? g.dkey_b : g.dkey_a;
   PROF_BEGIN(SCAN);
-  GSR_CHECK(scan_u32(g.tiles_touched, order, g.offsets, (size_t)P, true, g.scan_parts, stream));
+  GSR_CHECK(scan_u32(counts_sorted, nullptr, g.offsets, (size_t)P, true, g.scan_parts, stream));
   PROF_END(SCAN);
 
   GSR_CHECK(hipEventSynchronize(ready));

@@ -117,9 +117,13 @@ hipError_t reduce_u32(const uint32_t* in, size_t n, uint32_t* parts, uint32_t* o
 // count when deciding whether a digit is constant.
 // precleared: sort_clear_bytes(scratch, n, bits) from scratch.aux are already zero (cleared by
 // an earlier kernel on the stream through a SideClear): the memset launch is skipped.
+// key_payload: when set, the LAST pass writes key_payload[value] instead of the sorted key (the
+// keys themselves are not needed afterwards): the depth sort hands the scan its tile counts
+// already in depth order, one gather inside the sort instead of two in the scan.
 hipError_t radix_sort_pairs(uint32_t* ka, uint32_t* va, uint32_t* kb, uint32_t* vb, size_t n,
                             int bits, SortScratch scratch, bool* result_in_b, hipStream_t s,
-                            bool sentinel_anywhere = false, bool precleared = false);
+                            bool sentinel_anywhere = false, bool precleared = false,
+                            const uint32_t* key_payload = nullptr);
 // Device word counting look-back timeouts of any sort on the current device (sticky until the
 // host resets it); every forward reads it back with its instance count.
 uint32_t* sort_timeouts_word();

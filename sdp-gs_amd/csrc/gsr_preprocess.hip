@@ -25,13 +25,11 @@ constexpr int kThreads = 256;
 #define GSR_PRE_HOIST 0
 #endif
 
-// One Gaussian; returns its tile count (0 when culled).
-__device__ __forceinline__ uint32_t preprocess_gaussian(const PreArgs& a, int idx) {
-  if (a.acc_zero) {  // this Gaussian's 64-B gradient accumulator row (zeroed before the backward)
-    float4* row = reinterpret_cast<float4*>(a.g.acc + (size_t)idx * kAccFloats);
+// One Gaussian; returns its tile count (0 when culled) and writes its splat record to rec[0..3]
+// (the workgroup's LDS staging row; all zero when culled: such a record is never read).
+__device__ __forceinline__ uint32_t preprocess_gaussian(const PreArgs& a, int idx, float4* rec) {
 #pragma unroll
-    for (int k = 0; k < kAccFloats / 4; k++) row[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-  }
+  for (int k = 0; k < 4; k++) rec[k] = make_float4(0.f, 0.f, 0.f, 0.f);
 #if GSR_PRE_HOIST
   // the small per-Gaussian inputs are all put in flight before the first dependent computation
   // (the compiler cannot hoist loads above the cull branches itself)
@@ -156,7 +154,6 @@ __device__ __forceinline__ uint32_t preprocess_gaussian(const PreArgs& a, int id
   }
   g.tiles_touched[idx] = count;
   g.dkey_a[idx] = __float_as_uint(depth);
-  float4* rec = g.rec + 4 * (size_t)idx;
   rec[0] = make_float4(px, py, con_a, con_b);
   rec[1] = make_float4(con_c, op, depth, cr);
   rec[2] = make_float4(cg, cb, f0, f1);
@@ -165,18 +162,36 @@ __device__ __forceinline__ uint32_t preprocess_gaussian(const PreArgs& a, int id
 }
 
 // one lane per Gaussian; SH rows are read directly (an LDS-staged variant, gsr_stage.h, measured
-// slower here: its 48 KB of LDS cut occupancy below what this latency-bound kernel needs).  Each
-// workgroup also writes the sum of its tile counts (a.parts), so R = sum of the partials needs one
-// more small launch instead of a separate pass over tiles_touched.
+// slower here: its 48 KB of LDS cut occupancy below what this latency-bound kernel needs).  The
+// 64-byte records and accumulator rows (128 of the 145 bytes a Gaussian writes) leave as the
+// workgroup's contiguous 16-KB segments: lane t stores 16-byte chunk t, t + 256, ... (records
+// transposed through LDS at an 80-byte row stride) instead of 16-byte pieces at a 64-byte lane
+// stride.  Each workgroup also writes the sum of its tile counts (a.parts), so R = sum of the
+// partials needs one more small launch instead of a separate pass over tiles_touched.
+constexpr int kRecStride = 5;  // float4s per LDS record row (4 + 1 pad)
+// (__launch_bounds__(256, 6), 80 VGPRs with a 12-byte spill, measured equal to the unbounded 82)
 __global__ __launch_bounds__(kThreads) void preprocess_kernel(PreArgs a) {
-  const int idx = (int)(blockIdx.x * kThreads + threadIdx.x);
+  __shared__ float4 s_rec[kThreads * kRecStride];
+  const int base = (int)(blockIdx.x * kThreads);
+  const int idx = base + (int)threadIdx.x;
+  const int n = min(kThreads, a.P - base);
   side_clear(a.clear.p, a.clear.bytes, (size_t)idx, (size_t)gridDim.x * kThreads);
-  uint32_t count = idx < a.P ? preprocess_gaussian(a, idx) : 0u;
+  uint32_t count = idx < a.P ? preprocess_gaussian(a, idx, s_rec + threadIdx.x * kRecStride) : 0u;
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) count += (uint32_t)__shfl_xor((int)count, d, 64);
   __shared__ uint32_t s_sum[kThreads / 64];
   if ((threadIdx.x & 63) == 0) s_sum[threadIdx.x >> 6] = count;
   __syncthreads();
+  {
+    float4* out = a.g.rec + 4 * (size_t)base;
+    for (int q = (int)threadIdx.x; q < 4 * n; q += kThreads)
+      out[q] = s_rec[(q >> 2) * kRecStride + (q & 3)];
+  }
+  if (a.acc_zero) {  // the workgroup's 64-B gradient accumulator rows (zeroed before the backward)
+    float4* z = reinterpret_cast<float4*>(a.g.acc + (size_t)base * kAccFloats);
+    for (int q = (int)threadIdx.x; q < n * (kAccFloats / 4); q += kThreads)
+      z[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
   if (threadIdx.x == 0) {
     uint32_t t = 0;
 #pragma unroll

@@ -253,7 +253,7 @@ __global__ __launch_bounds__(NT, NT == 1024 ? 8 : (NT == 512 ? 6 : 1)) void radi
     const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin, size_t n, int shift,
     int bits, const uint32_t* __restrict__ totals, const uint32_t* __restrict__ nsent_sh,
     uint32_t* __restrict__ ticket, uint64_t* __restrict__ status, uint32_t* __restrict__ err,
-    uint32_t* __restrict__ kout, uint32_t* __restrict__ vout) {
+    uint32_t* __restrict__ kout, uint32_t* __restrict__ vout, const uint32_t* __restrict__ kpay) {
   constexpr int kSortWaves = NT / 64, kSortThreads = NT;
   constexpr int kKeysPerThread = kSortTile / NT, kKeysPerWave = kKeysPerThread * 64;
   static_assert(NT >= 256 && kSortTile % NT == 0, "one-sweep tile shape");
@@ -298,8 +298,9 @@ __global__ __launch_bounds__(NT, NT == 1024 ? 8 : (NT == 512 ? 6 : 1)) void radi
       const size_t b0 = (size_t)blockIdx.x * kSortTile;
       const size_t e0 = min(n, b0 + (size_t)kSortTile);
       for (size_t i = b0 + (size_t)t; i < e0; i += NT) {
-        kout[i] = kin[i];
-        vout[i] = vin[i];
+        const uint32_t v = vin[i];
+        kout[i] = kpay ? kpay[min(v, (uint32_t)n - 1u)] : kin[i];
+        vout[i] = v;
       }
       return;
     }
@@ -424,8 +425,9 @@ __global__ __launch_bounds__(NT, NT == 1024 ? 8 : (NT == 512 ? 6 : 1)) void radi
     const uint32_t k = s_k[i];
     const uint32_t o = s_gofs[(k >> shift) & mask] + i;
     if (o < n) {  // only a timed-out look-back (error word raised) can produce o >= n
-      kout[o] = k;
-      vout[o] = s_v[i];
+      const uint32_t v = s_v[i];
+      kout[o] = kpay ? kpay[min(v, (uint32_t)n - 1u)] : k;
+      vout[o] = v;
     }
   }
 #if GSR_SORT_TRACE
@@ -519,7 +521,8 @@ uint32_t* sort_timeouts_word() {
 
 hipError_t radix_sort_pairs(uint32_t* ka, uint32_t* va, uint32_t* kb, uint32_t* vb, size_t n,
                             int bits, SortScratch scratch, bool* result_in_b, hipStream_t s,
-                            bool sentinel_anywhere, bool precleared) {
+                            bool sentinel_anywhere, bool precleared,
+                            const uint32_t* key_payload) {
   *result_in_b = false;
   if (n == 0 || bits <= 0) return hipSuccess;
   if (bits > 32 || n > 0xffffffffull) return hipErrorInvalidValue;
@@ -547,7 +550,8 @@ hipError_t radix_sort_pairs(uint32_t* ka, uint32_t* va, uint32_t* kb, uint32_t* 
                      sentinel_anywhere ? scratch.aux + kSortAuxSent : nullptr,                   \
                      scratch.aux + kSortAuxTickets + 8 * p,                                      \
                      scratch.status + (size_t)p * nb * 256, \
-                     scratch.aux + kSortAuxErr, kout, vout)
+                     scratch.aux + kSortAuxErr, kout, vout,                                      \
+                     p == passes - 1 ? key_payload : nullptr)
     if (nt == 1024) GSR_ONESWEEP(1024);
     else if (nt == 512) GSR_ONESWEEP(512);
     else GSR_ONESWEEP(256);
