@@ -19,6 +19,9 @@ L.gsr_test_sort_trace.argtypes = [ctypes.c_void_p, ctypes.c_int]
 rng = np.random.default_rng(0)
 cases = [("depth1M", rng.lognormal(1.0, 0.5, 1_000_000).astype(np.float32).view(np.uint32), 32),
          ("tiles3M", np.minimum(rng.exponential(300.0, 2_960_000), 3023).astype(np.uint32), 12)]
+if os.environ.get("SORT_LARGE", "0") == "1":  # config 5 sizes
+    cases += [("depth5M", rng.lognormal(1.0, 0.5, 5_000_000).astype(np.float32).view(np.uint32), 32),
+              ("tiles16M", np.minimum(rng.exponential(800.0, 16_250_000), 8159).astype(np.uint32), 13)]
 out = {}
 for name, keys, bits in cases:
     n = keys.size
@@ -31,7 +34,7 @@ for name, keys, bits in cases:
         _lib.check(L.gsr_test_radix_sort_pairs(k.data_ptr(), v.data_ptr(), n, bits,
                                                scratch.data_ptr(), s))
     torch.cuda.synchronize()
-    parts = (n + 4095) // 4096
+    parts = min((n + 4095) // 4096, 16384)
     tr = np.zeros((parts, 8), np.uint64)
     assert L.gsr_test_sort_trace(tr.ctypes.data, parts) == 0
     t = tr[:, :6].astype(np.int64)

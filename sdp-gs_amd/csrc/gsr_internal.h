@@ -59,8 +59,14 @@ inline size_t scan_parts(size_t n) { return (n + kScanTile - 1) / kScanTile; }
 inline size_t sort_blocks(size_t n) { return (n + kSortTile - 1) / kSortTile; }
 inline int sort_passes(int bits) { return (bits + 7) / 8; }
 constexpr int kSortMaxPasses = 4;
-// u64 look-back status words: one per (pass, partition, digit)
-inline size_t sort_status_len(size_t n) { return (size_t)kSortMaxPasses * sort_blocks(n) * 256; }
+// Partitions per look-back super-partition: besides its own status word, every partition adds its
+// digit counts into its super-partition's word, so a look-back crosses 16 partitions per word.
+constexpr int kSortSuper = 16;
+inline size_t sort_supers(size_t n) { return (sort_blocks(n) + kSortSuper - 1) / kSortSuper; }
+// u64 look-back words of one pass: [partition][256] status words, then [super-partition][256]
+// super words (count | contributors << 32)
+inline size_t sort_pass_words(size_t n) { return (sort_blocks(n) + sort_supers(n)) * 256; }
+inline size_t sort_status_len(size_t n) { return (size_t)kSortMaxPasses * sort_pass_words(n); }
 // u32 aux words: digit totals as kSortTotShards partial copies [shard][kSortMaxPasses][256] (the
 // totals kernel's workgroups add into shard blockIdx % kSortTotShards: same-line device-scope
 // atomics serialise at the memory side, so one shared copy made ~250-720 workgroups queue on the
@@ -82,7 +88,7 @@ struct SortScratch {
 // Bytes from scratch.aux that must be zero before a sort of n keys over `bits` bits (aux words
 // and the status words of the passes used); a multiple of 16 (status is 256-B aligned).
 inline size_t sort_clear_bytes(const SortScratch& sc, size_t n, int bits) {
-  return (size_t)((char*)(sc.status + (size_t)sort_passes(bits) * sort_blocks(n) * 256) -
+  return (size_t)((char*)(sc.status + (size_t)sort_passes(bits) * sort_pass_words(n)) -
                   (char*)sc.aux);
 }
 // A zero-fill piggy-backed on a kernel that runs anyway (no separate memset launch): every

@@ -81,6 +81,10 @@ __global__ __launch_bounds__(kSchedThreads) void tile_schedule_kernel(const uint
 #ifndef GSR_QUAD_WAVES
 #define GSR_QUAD_WAVES 1
 #endif
+// diagnostic builds (wrong gradients, timing only): 1 = no wave reduction of the pair terms
+#ifndef GSR_BWD_DIAG
+#define GSR_BWD_DIAG 0
+#endif
 // backward transmittance recovery T / (1 - alpha): 0 = IEEE division, 1 = rcp + Newton step
 #ifndef GSR_BWD_FAST_DIV
 #define GSR_BWD_FAST_DIV 1
@@ -604,11 +608,19 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
       g[5] = FEAT ? dchannel_dcolor * dpC : mk2(0.f, 0.f);          // kAccF0, kAccF1
       g[6] = mk2(FEAT ? dchannel_dcolor * dpD.x : 0.f, 0.f);       // kAccF2, (13)
       g[7] = mk2(0.f, 0.f);                                         // (14, 15)
+#if GSR_BWD_DIAG == 1
+      // diagnostic build only (wrong gradients): no wave reduction, one lane-local LDS add
+      {
+        f2 t = g[0] + g[1] + g[2] + g[3] + g[4] + g[5] + g[6];
+        if (lane == 0 && t.x + t.y != 0.0f) atomicAdd(&s_acc[j * kAccPad], t.x + t.y);
+      }
+#else
       const float sum = wave_reduce16_dpp(g, lane);
       if ((lane & 3) == 0) {
         const int k = reduce16_slot(lane, swap_orient);
         if (sum != 0.0f) atomicAdd(&s_acc[j * kAccPad + k], sum);
       }
+#endif
     }
     }
     __syncthreads();

@@ -145,6 +145,7 @@ __device__ __forceinline__ uint64_t match_digit(uint32_t d, bool valid, int bits
 // the error word (checked by the host at its next synchronisation) and proceeds, so no wave can
 // hang the device.
 constexpr uint64_t kStAgg = 1ull << 32, kStIncl = 2ull << 32, kStFlags = 3ull << 32;
+constexpr uint64_t kStOne = 1ull << 32;  // one contributor in a super-partition word
 }  // namespace
 // count of timed-out look-backs since the last check (sort_timeouts_word)
 __device__ uint32_t g_lookback_timeouts;
@@ -160,10 +161,6 @@ __device__ uint64_t g_sort_trace[16384][8];
 #endif
 namespace {
 constexpr int kSpinLimit = 1 << 18;
-#ifndef GSR_LOOKBACK
-#define GSR_LOOKBACK 16
-#endif
-constexpr int kLookback = GSR_LOOKBACK;  // predecessor status words loaded per look-back step
 // One-sweep workgroup size: NT lanes share a partition of kSortTile keys.  More lanes keep the
 // ranking chain short (kSortTile / NT keys per lane) and hide its LDS latency with other waves
 // (256 lanes = one wave per SIMD, every latency exposed: 7.5 us of ranking per pass); but 1024-lane
@@ -348,7 +345,15 @@ __global__ __launch_bounds__(NT, NT == 1024 ? 8 : (NT == 512 ? 6 : 1)) void radi
 #pragma unroll
     for (int w = 0; w < kSortWaves; w++) h += s_cnt[w][t];
   uint64_t* my = status + (size_t)part * 256 + dt;
-  if (dig) status_store(my, (part == 0 ? kStIncl : kStAgg) | (uint64_t)h);
+  // super-partition words follow the partition words of this pass (sort_pass_words)
+  uint64_t* super = status + (size_t)gridDim.x * 256;
+  if (dig) {
+    status_store(my, (part == 0 ? kStIncl : kStAgg) | (uint64_t)h);
+    // one contributor and its count into the super-partition's word: self-describing (complete
+    // when the contributor count reaches kSortSuper), so no fence orders it against other words
+    __hip_atomic_fetch_add(super + (size_t)(part / kSortSuper) * 256 + dt, kStOne | (uint64_t)h,
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   uint32_t total_n;
   const uint32_t lstart = block_excl_scan<kSortWaves>(dig ? h : 0u, s_scan, total_n);
   const uint32_t dbase = block_excl_scan<kSortWaves>(dig ? dtotal : 0u, s_scan, total_n);
@@ -377,42 +382,79 @@ __global__ __launch_bounds__(NT, NT == 1024 ? 8 : (NT == 512 ? 6 : 1)) void radi
   SORT_TRACE(2)
   uint32_t excl = 0;
   if (dig && part > 0) {
-    // windowed look-back: kLookback predecessors' words are loaded together (independent
-    // loads in flight) and consumed in order up to the first INCLUSIVE one or the first word not
-    // yet published (then re-polled from there); partition 0 is always INCLUSIVE, so the walk
-    // ends there at the latest
+    // Two-level windowed look-back.  (A) the predecessors inside this partition's own
+    // super-partition (at most kSortSuper - 1 words, 8 per round), consumed in order up to the
+    // first INCLUSIVE word or the first word not yet published (re-polled from there).  (B) then
+    // whole super-partitions, newest first, 4 at a time: the inclusive word of a
+    // super-partition's last partition ends the walk, else its super word once complete (all
+    // kSortSuper contributors) adds its 16 partitions at once.  Partition 0 is always INCLUSIVE,
+    // so the walk ends at super-partition 0 at the latest.  A look-back crosses 16x fewer
+    // unpublished-prefix words than a partition-by-partition walk (the frontier of inclusive
+    // prefixes advances 256 partitions per round instead of 16).
     int spins = 0;
-    int64_t q = (int64_t)part - 1;
+    bool done = false;
+    auto spin = [&]() {
+      if (++spins > kSpinLimit) {
+        atomicOr(err, 1u);
+        atomicAdd(&g_lookback_timeouts, 1u);  // sticky, read back by every forward
+        done = true;
+        return;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    };
     if (g_force_lookback_timeout) {  // test hook only: the bounded spin's give-up path
       atomicOr(err, 1u);
       atomicAdd(&g_lookback_timeouts, 1u);
-    } else
-    for (;;) {
-      uint64_t w[kLookback];
+      done = true;
+    }
+    const int64_t qlo = (int64_t)(part / kSortSuper) * kSortSuper;
+    int64_t q = (int64_t)part - 1;
+    constexpr int kAW = 8;  // partition words per round inside the super-partition (no spill)
+    while (!done && q >= qlo) {
+      uint64_t w[kAW];
 #pragma unroll
-      for (int j = 0; j < kLookback; j++)
-        w[j] = (q - j >= 0) ? status_load(status + (size_t)(q - j) * 256 + dt) : kStIncl;
+      for (int j = 0; j < kAW; j++)
+        w[j] = (q - j >= qlo) ? status_load(status + (size_t)(q - j) * 256 + dt) : 0ull;
       int used = 0;
-      bool done = false, stop = false;
+      bool stop = false;
 #pragma unroll
-      for (int j = 0; j < kLookback; j++) {  // branch-free so that w[] stays in registers
+      for (int j = 0; j < kAW; j++) {  // branch-free so that w[] stays in registers
         const uint64_t f = w[j] & kStFlags;
-        const bool take = !stop && f != 0;
+        const bool take = !stop && q - j >= qlo && f != 0;
         excl += take ? (uint32_t)w[j] : 0u;
         used = take ? j + 1 : used;
         done = done || (take && f == kStIncl);
         stop = stop || !take || f == kStIncl;
       }
-      if (done) break;
       q -= used;
-      if (used < kLookback) {
-        if (++spins > kSpinLimit) {
-          atomicOr(err, 1u);
-          atomicAdd(&g_lookback_timeouts, 1u);  // sticky, read back by every forward
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
+      if (!done && q >= qlo && used < kAW) spin();  // stopped at a word not yet published
+    }
+    int64_t S = (int64_t)(part / kSortSuper) - 1;
+    constexpr int kSW = 4;  // super-partitions per round (8 loads in flight per digit: no spill)
+    while (!done && S >= 0) {
+      uint64_t lw[kSW], sw[kSW];
+#pragma unroll
+      for (int j = 0; j < kSW; j++) {
+        const bool in = S - j >= 0;
+        lw[j] = in ? status_load(status + (size_t)((S - j) * kSortSuper + kSortSuper - 1) * 256 + dt)
+                   : 0ull;
+        sw[j] = in ? status_load(super + (size_t)(S - j) * 256 + dt) : 0ull;
       }
+      int used = 0;
+      bool stop = false;
+#pragma unroll
+      for (int j = 0; j < kSW; j++) {
+        const bool in = S - j >= 0;
+        const bool incl = in && (lw[j] & kStFlags) == kStIncl;
+        const bool full = in && (uint32_t)(sw[j] >> 32) == (uint32_t)kSortSuper;
+        const bool take = !stop && (incl || full);
+        excl += take ? (uint32_t)(incl ? lw[j] : sw[j]) : 0u;
+        used = take ? j + 1 : used;
+        done = done || (take && incl);
+        stop = stop || !take || incl;
+      }
+      S -= used;
+      if (!done && S >= 0 && used < kSW) spin();  // stopped at an incomplete super-partition
     }
     status_store(my, kStIncl | (uint64_t)(excl + h));
   }
@@ -549,7 +591,7 @@ hipError_t radix_sort_pairs(uint32_t* ka, uint32_t* va, uint32_t* kb, uint32_t* 
                      dbits, scratch.aux + kSortAuxTotals + 256 * p,                              \
                      sentinel_anywhere ? scratch.aux + kSortAuxSent : nullptr,                   \
                      scratch.aux + kSortAuxTickets + 8 * p,                                      \
-                     scratch.status + (size_t)p * nb * 256, \
+                     scratch.status + (size_t)p * sort_pass_words(n), \
                      scratch.aux + kSortAuxErr, kout, vout,                                      \
                      p == passes - 1 ? key_payload : nullptr)
     if (nt == 1024) GSR_ONESWEEP(1024);
