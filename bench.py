@@ -274,15 +274,16 @@ def main():
         except (OSError, ValueError):
             pass
 
-    legs = {}
-    if not args.no_extra_legs:
-        legs = extra_legs(args, model, my_cams, cams_all, views, reducer, timed_region, rank,
-                          world, dev, (P, W, H, deg), (dimg, ddep, dfeat), bg)
-
+    # the CPU baseline samples the headline model before the training legs change it
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_baseline_views > 0:
         cpu = cpu_baseline(model, cams_all[: args.cpu_baseline_views], dimg, ddep, dfeat, deg,
                            args.cpu_threads)
+
+    legs = {}
+    if not args.no_extra_legs:
+        legs = extra_legs(args, model, my_cams, cams_all, views, reducer, timed_region, rank,
+                          world, dev, (P, W, H, deg), (dimg, ddep, dfeat), bg)
 
     if rank == 0:
         line = {
