@@ -9,6 +9,9 @@ Mirrors the loss calls of train.py around the rasterizer:
   depth_pearson_loss(depth_mono, depth, offset=200.0)
         = min(1 - pearson(depth_mono, depth), 1 - pearson(1 / (-depth_mono + offset), depth))
         (train.py:126-129) without the host sync of Python's min() on tensors
+  train_view_loss(image, depth, gt, depth_mono, lambda_dssim, depth_weight)
+        = photometric_loss + depth_weight * depth_pearson_loss as one autograd node with pooled
+        scratch (the per-view loss of train.py:99-131; what gsr_amd.trainer uses)
 Gradients flow to the rendered image / depth (the first argument of ssim, either argument of
 pearson_corrcoef, `depth` of depth_pearson_loss).  No CPU path.
 """
@@ -157,3 +160,100 @@ def depth_pearson_loss(depth_mono, depth, offset=200.0):
     depth (either [H,W]-like tensor, flattened to a column as the reference's reshape(-1, 1))."""
     loss, _ = _Pearson.apply(depth_mono.reshape(-1, 1), depth.reshape(-1, 1), 2, offset)
     return loss.squeeze()
+
+
+# ---- one autograd node for train.py's per-view loss ----------------------------------------------
+# Scratch buffers keyed by (kind, shape, device, stream): a buffer is taken by a forward and given
+# back once its backward has been issued (or at once without autograd), so the next forward on the
+# same stream -- ordered after that backward -- reuses it; another stream gets its own.
+_POOL = {}
+
+
+def _take(key, nbytes, device):
+    free = _POOL.setdefault(key, [])
+    return free.pop() if free else torch.empty(nbytes, dtype=torch.uint8, device=device)
+
+
+def _give(key, buf):
+    _POOL.setdefault(key, []).append(buf)
+
+
+class _TrainViewLoss(torch.autograd.Function):
+    """loss = (1 - lambda) L1 + lambda (1 - SSIM) of (image, gt) + depth_weight * the Pearson depth
+    term of (depth_mono, depth) (train.py:99-100,117-131), as ONE autograd node: two kernel
+    pairs, no intermediate autograd nodes or allocations on the steady state."""
+
+    @staticmethod
+    def forward(ctx, image, depth, gt, depth_mono, lambda_dssim, depth_weight, offset):
+        _cuda(image, depth, gt, depth_mono)
+        if image.shape != gt.shape or image.dim() != 3:
+            raise ValueError("photometric loss expects image and gt of the same [C,H,W] shape")
+        if depth.numel() != depth_mono.numel():
+            raise ValueError("depth and depth_mono must have the same number of pixels")
+        x = image.detach().contiguous().float()
+        y = gt.detach().contiguous().float()
+        d = depth.detach().reshape(-1).contiguous().float()
+        m = depth_mono.detach().reshape(-1).contiguous().float()
+        C, H, W = x.shape
+        N = d.numel()
+        L = _lib.load()
+        dev = x.device
+        s = _stream(x)
+        kp = ("photo", C, H, W, dev.index, s)
+        kq = ("pearson", dev.index, s)
+        sp = _take(kp, int(L.gsr_photometric_scratch_bytes(C, H, W)), dev)
+        sq = _take(kq, int(L.gsr_pearson_scratch_bytes(1, 2)), dev)
+        out = torch.empty(5, dtype=torch.float32, device=dev)  # loss, l1, ssim, depth term, total
+        need = int(image.requires_grad or depth.requires_grad)
+        with torch.cuda.device(dev):
+            _check(L.gsr_photometric_loss(C, H, W, x.data_ptr(), y.data_ptr(),
+                                          float(lambda_dssim), need, out.data_ptr(),
+                                          sp.data_ptr(), s), "gsr_photometric_loss")
+            _check(L.gsr_pearson_loss(N, 1, m.data_ptr(), d.data_ptr(), 2, float(offset), None,
+                                      out.data_ptr() + 12, sq.data_ptr(), s), "gsr_pearson_loss")
+        total = torch.add(out[0], out[3], alpha=float(depth_weight))
+        if need:
+            ctx.save_for_backward(x, y, d, m)
+            ctx.bufs = (kp, sp, kq, sq)
+            ctx.args = (float(lambda_dssim), float(depth_weight), float(offset))
+            ctx.dshape = depth.shape
+        else:
+            _give(kp, sp)
+            _give(kq, sq)
+        ctx.mark_non_differentiable(out)
+        return total, out
+
+    @staticmethod
+    def backward(ctx, g_total, g_out):
+        x, y, d, m = ctx.saved_tensors
+        kp, sp, kq, sq = ctx.bufs
+        lam, w, offset = ctx.args
+        C, H, W = x.shape
+        L = _lib.load()
+        g = g_total.reshape(1).contiguous().float()
+        gq = g * w
+        dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
+        dd = torch.empty_like(d) if ctx.needs_input_grad[1] else None
+        s = _stream(x)
+        with torch.cuda.device(x.device):
+            if dx is not None:
+                _check(L.gsr_photometric_loss_backward(C, H, W, x.data_ptr(), y.data_ptr(), lam,
+                                                       g.data_ptr(), None, None, dx.data_ptr(),
+                                                       sp.data_ptr(), s),
+                       "gsr_photometric_loss_backward")
+            if dd is not None:
+                _check(L.gsr_pearson_loss_backward(d.numel(), 1, m.data_ptr(), d.data_ptr(), 2,
+                                                   offset, gq.data_ptr(), dd.data_ptr(), None,
+                                                   sq.data_ptr(), s), "gsr_pearson_loss_backward")
+        _give(kp, sp)
+        _give(kq, sq)
+        return (dx, None if dd is None else dd.view(ctx.dshape), None, None, None, None, None)
+
+
+def train_view_loss(image, depth, gt_image, depth_mono, lambda_dssim=0.2, depth_weight=0.05,
+                    offset=200.0):
+    """train.py:99-131 for one view with the depth branch: (total loss, Ll1).  Gradients flow to
+    the rendered image and depth."""
+    total, out = _TrainViewLoss.apply(image, depth, gt_image, depth_mono, lambda_dssim,
+                                      depth_weight, offset)
+    return total, out[1]

@@ -59,10 +59,12 @@ def make_trainable(model, args: OptArgs, spatial_lr_scale: float = 1.0):
 
 
 def _view_loss(pkg, gt_image, depth_mono, args: OptArgs):
-    from .losses import depth_pearson_loss, photometric_loss
+    from .losses import photometric_loss, train_view_loss
+    if depth_mono is not None:  # one autograd node for both terms (losses.train_view_loss)
+        loss, _ = train_view_loss(pkg["render"], pkg["depth"], gt_image, depth_mono,
+                                  args.lambda_dssim, args.depth_weight)
+        return loss
     loss, _ = photometric_loss(pkg["render"], gt_image, args.lambda_dssim)
-    if depth_mono is not None:
-        loss = loss + args.depth_weight * depth_pearson_loss(depth_mono, pkg["depth"])
     return loss
 
 

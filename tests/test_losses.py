@@ -111,3 +111,30 @@ def test_depth_pearson_loss_matches_reference(flip):
     torch.testing.assert_close(loss.double(), ref, atol=2e-6, rtol=0)
     torch.testing.assert_close(d.grad.double(), d64.grad,
                                atol=1e-5 * float(d64.grad.abs().max()), rtol=0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("flip", [False, True])
+def test_train_view_loss_equals_the_two_terms(flip):
+    """train.py:99-131's per-view loss as one autograd node (losses.train_view_loss, what
+    gsr_amd.trainer uses) equals photometric_loss + depth_weight * depth_pearson_loss -- the two
+    functions pinned above -- in value and in both gradients, and its pooled scratch is reused
+    across calls without cross-talk (three calls in a row, all checked)."""
+    g = torch.Generator(device="cuda").manual_seed(11)
+    for it in range(3):
+        img, gt = _images(3, 61, 97, seed=20 + it)
+        mono = torch.rand((1, 61, 97), generator=g, device="cuda") * 50 + 1
+        base = (1 / (-mono + 200)) if flip else mono
+        depth = base * 3 + 0.05 * base.std() * torch.randn(mono.shape, generator=g, device="cuda")
+        a_img, a_dep = img.clone().requires_grad_(True), depth.clone().requires_grad_(True)
+        b_img, b_dep = img.clone().requires_grad_(True), depth.clone().requires_grad_(True)
+        tot, l1 = losses.train_view_loss(a_img, a_dep, gt, mono, 0.2, 0.05)
+        tot.backward()
+        ref_photo, ref_l1 = losses.photometric_loss(b_img, gt, 0.2)
+        ref = ref_photo + 0.05 * losses.depth_pearson_loss(mono, b_dep)
+        ref.backward()
+        torch.testing.assert_close(tot, ref, atol=1e-6, rtol=0)
+        torch.testing.assert_close(l1, ref_l1, atol=0, rtol=0)
+        torch.testing.assert_close(a_img.grad, b_img.grad, atol=0, rtol=0)
+        torch.testing.assert_close(a_dep.grad, b_dep.grad,
+                                   atol=1e-6 * float(b_dep.grad.abs().max()), rtol=0)
