@@ -85,6 +85,11 @@ __global__ __launch_bounds__(kSchedThreads) void tile_schedule_kernel(const uint
 #ifndef GSR_BWD_DIAG
 #define GSR_BWD_DIAG 0
 #endif
+// backward Gaussian weight: 1 = hardware exp2 with an exact splat_exp at the alpha >= 1/255
+// threshold (see render_bwd_kernel), 0 = splat_exp everywhere (the forward's sequence)
+#ifndef GSR_BWD_FAST_EXP
+#define GSR_BWD_FAST_EXP 1
+#endif
 // backward transmittance recovery T / (1 - alpha): 0 = IEEE division, 1 = rcp + Newton step
 #ifndef GSR_BWD_FAST_DIV
 #define GSR_BWD_FAST_DIV 1
@@ -539,7 +544,20 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
       const float4 r1 = s_r1[j];
       const float dx = r0.x - pfx, dy = r0.y - pfy;
       const float power = -0.5f * (r0.z * dx * dx + r1.x * dy * dy) - r0.w * dx * dy;
+#if GSR_BWD_FAST_EXP
+      // The backward needs the forward's alpha >= 1/255 DECISION exactly, its G only to gradient
+      // precision: G by the hardware exp2 (v_exp_f32, ~1 ulp; 3 instructions instead of the 17 of
+      // splat_exp), and splat_exp -- the forward's and the oracle's sequence -- wherever op * G
+      // lies within 2e-6 (relative) of 1/255, so the decision is the forward's at every pixel.
+      {
+        float G = __builtin_amdgcn_exp2f(power * 1.44269504088896341f);
+        const float t = r1.y * G;
+        if (fabsf(t - (1.0f / 255.0f)) <= 2e-6f * (1.0f / 255.0f)) G = splat_exp(power);
+        Gv[u] = G;
+      }
+#else
       Gv[u] = splat_exp(power);
+#endif
       av[u] = fminf(0.99f, r1.y * Gv[u]);
       cv[u] = (k0 + u < nlist) && rel < last_contributor && !(power > 0.0f) &&
               !(av[u] < 1.0f / 255.0f);
