@@ -31,10 +31,14 @@ torch.autograd.backward([pkg["render"], pkg["depth"], pkg["feature"]], [dimg, dd
 torch.cuda.synchronize()
 assert L.gsr_test_blend_stats(buf, 1) == 0
 v = list(buf)
-waves = v[8] * 4
+waves = v[8]  # BLEND_STAT(8) counts each wave once
 R = dgr.LAST_STATS["num_rendered"]
 print(f"R={R} waves={waves}")
 print(f"fwd: list/wave={v[0]/waves:.1f} evaluated/wave={v[1]/waves:.1f} contrib-entries/wave={v[2]/waves:.1f} "
       f"lanes/contrib-entry={v[3]/max(v[2],1):.1f}")
 print(f"bwd: list/wave={v[4]/waves:.1f} evaluated/wave={4*v[5]/waves:.1f} contrib-entries/wave={v[6]/waves:.1f} "
       f"lanes/contrib-entry={v[7]/max(v[6],1):.1f}")
+if os.environ.get("GSR_BLOCK_LISTS", "1") != "0":
+    # block-list forward: [0] sum of the wave's longest group list, [1] sum of its four group
+    # lists, [2] entries evaluated per group (the "fwd:" line above reads these slots)
+    print(f"blk fwd: max-list/wave={v[0]/waves:.1f} group-lists/wave={v[1]/waves:.1f} evaluated/wave-step-slot={v[2]/waves:.1f}")
