@@ -346,9 +346,37 @@ def extra_legs(args, model, my_cams, cams_all, views, reducer, timed_region, ran
     out = {}
     n_views = len(my_cams) * world
 
+    # ---- deterministic backward: the headline step with GSR_DEBUG_DETERMINISTIC --------------
+    prev_det = dgr.deterministic()
+    dgr.deterministic(True)
+    try:
+        def det_step():
+            if reducer is not None:
+                reducer.attach_grads()
+            else:
+                for p in model.parameters():
+                    p.grad = None
+
+            def one_view(cam):
+                pkg = render(cam, model, Pipe(), bg, Opt())
+                torch.autograd.backward([pkg["render"], pkg["depth"], pkg["feature"]],
+                                        [dimg, ddep, dfeat])
+            views.run(my_cams, one_view, model=model, reducer=reducer)
+        for _ in range(args.warmup):
+            det_step()
+        el = timed_region(lambda i: det_step())
+        out["deterministic"] = {
+            "value": round(args.steps * n_views / el, 3), "unit": "views/s",
+            "ms_per_step": round(1000.0 * el / args.steps, 3),
+            "path": "the headline step with the deterministic backward (per-instance rows + "
+                    "ordered per-Gaussian sums instead of float atomics; bitwise reproducible)"}
+    finally:
+        dgr.deterministic(prev_det)
+
     # ---- reference operator API (no fused entry, no grad-into-leaves, one stream) ----------
     prev_fused = os.environ.get("GSR_FUSED")
-    prev_leaves = dgr.grad_into_leaves(False)
+    prev_leaves = dgr.grad_into_leaves()
+    dgr.grad_into_leaves(False)
     os.environ["GSR_FUSED"] = "0"
     try:
         def ref_api_step():

@@ -47,6 +47,14 @@ typedef enum gsr_status {
 
 enum { GSR_BUF_GEOM = 0, GSR_BUF_BINNING = 1, GSR_BUF_IMAGE = 2 };
 
+/* `debug` argument of every rasterize entry point: bit 0 = the reference's debug flag (synchronous
+ * checks, rasterize_points.cu `debug`); bit 1 = deterministic backward -- the blend backward
+ * writes per-instance gradient rows and sums every Gaussian's rows in a fixed order instead of
+ * float atomics (the reference's backward.cu:523-554 atomics are run-to-run nondeterministic), so
+ * gradients are bitwise reproducible; slower, and its binning buffer holds two more arrays.  A
+ * backward must get the same bit 1 as its forward. */
+#define GSR_DEBUG_DETERMINISTIC 2
+
 /* Returns a device pointer to at least `bytes` bytes (16-byte aligned) or NULL. */
 typedef void* (*gsr_alloc_fn)(void* ctx, size_t bytes, int which);
 

@@ -44,7 +44,7 @@ GeomState carve_geom(char* base, size_t P) {
   return g;
 }
 
-BinState carve_bin(char* base, size_t R) {
+BinState carve_bin(char* base, size_t R, bool det) {
   Carver c(base);
   BinState b{};
   b.tkey_a = c.take<uint32_t>(R);
@@ -52,6 +52,10 @@ BinState carve_bin(char* base, size_t R) {
   b.tkey_b = c.take<uint32_t>(R);
   b.tval_b = c.take<uint32_t>(R);
   b.sort = take_sort_scratch(c, R);
+  if (det) {
+    b.egid = c.take<uint32_t>(R);
+    b.partial = c.take<float>(R * kAccFloats);
+  }
   b.bytes = c.size();
   return b;
 }
@@ -381,6 +385,8 @@ static int forward_impl(int P, int M, const float* background, const float* mean
                         const float* sh_dc, const float* sh_rest,
                         const float* pre_color = nullptr, const uint8_t* pre_clamp = nullptr) {
   g_err.clear();
+  const bool det = (debug & GSR_DEBUG_DETERMINISTIC) != 0;  // gsr.h: debug bit 1
+  debug &= 1;
   if ((pre_color == nullptr) != (pre_clamp == nullptr) || (pre_color && !fused))
     return fail(GSR_ERR_ARGUMENT, "pre_color / pre_clamp: both or neither, fused path only");
   if (fused && P != 0) {  // P = 0: empty tensors have null data (rasterize_points.cu:81)
@@ -496,17 +502,18 @@ static int forward_impl(int P, int M, const float* background, const float* mean
     if (host[2]) return fail(GSR_ERR_HIP, "depth sort look-back timed out");
   }
 
-  const size_t bbytes = carve_bin(nullptr, R).bytes;
+  const size_t bbytes = carve_bin(nullptr, R, det).bytes;
   char* bbase = (char*)alloc(alloc_ctx, bbytes, GSR_BUF_BINNING);
   if (!bbase) return fail(GSR_ERR_ALLOC, "binning buffer allocation of %zu bytes failed", bbytes);
-  BinState b = carve_bin(bbase, R);
+  BinState b = carve_bin(bbase, R, det);
 
   PROF_BEGIN(DUPLICATE);
   // the duplicate grid also zeroes the tile sort's scratch and the tile ranges
   const int tbits = tile_bits(ntiles);
   GSR_CHECK(launch_duplicate(P, order, g.offsets, radii_ptr, g.rec, gx, gy, b.tkey_a, b.tval_a,
                              (uint32_t)R, SideClear{b.sort.aux, sort_clear_bytes(b.sort, R, tbits)},
-                             SideClear{im.ranges, sizeof(uint2) * ntiles}, stream));
+                             SideClear{im.ranges, sizeof(uint2) * ntiles}, stream,
+                             det ? b.egid : nullptr));
   PROF_END(DUPLICATE);
   bool t_in_b = false;
   PROF_BEGIN(TILE_SORT);
@@ -520,6 +527,11 @@ static int forward_impl(int P, int M, const float* background, const float* mean
   }
   const uint32_t* tiles_sorted = t_in_b ? b.tkey_b : b.tkey_a;
   const uint32_t* point_list = t_in_b ? b.tval_b : b.tval_a;
+  if (det) {  // the sorted values are emission indices: Gaussian ids into the other value array
+    uint32_t* pl = t_in_b ? b.tval_a : b.tval_b;
+    GSR_CHECK(launch_det_gather(R, point_list, b.egid, pl, stream));
+    point_list = pl;
+  }
   int mail_slot = -1;
   uint32_t* host_status = mail_post(ibase, &mail_slot);
   PROF_BEGIN(RANGES);
@@ -621,6 +633,8 @@ static int backward_impl(
     const float* opacity_raw, float* dL_dsh_rest, int accumulate, float* dRGB_sh = nullptr,
     const float* pre_jac = nullptr) {
   g_err.clear();
+  const bool det = (debug & GSR_DEBUG_DETERMINISTIC) != 0;  // must match the forward's flags
+  debug &= 1;
   if (fused && P != 0) {
     if (!sh_dc || (M > 1 && !sh_rest) || (M > 1 && !dL_dsh_rest && !dRGB_sh) || !scales ||
         !rotations || !opacity_raw)
@@ -659,9 +673,14 @@ static int backward_impl(
   const uint32_t ntiles = gx * gy;
   GeomState g = carve_geom((char*)geom_buffer, (size_t)P);
   ImgState im = carve_img((char*)image_buffer, (size_t)W, (size_t)H);
-  BinState b = carve_bin((char*)binning_buffer, (size_t)R);
+  BinState b = carve_bin((char*)binning_buffer, (size_t)R, det);
   const int passes = sort_passes(tile_bits(ntiles));
   const uint32_t* point_list = (passes & 1) ? b.tval_b : b.tval_a;
+  const uint32_t* einst = nullptr;
+  if (det) {  // forward: emission indices sorted in place, Gaussian ids gathered into the other
+    einst = point_list;
+    point_list = (passes & 1) ? b.tval_a : b.tval_b;
+  }
   const int32_t* radii_ptr = radii ? radii : g.radii;
 
   if (!acc_take_clean(geom_buffer)) {  // not freshly zeroed by this buffer's forward
@@ -677,8 +696,14 @@ static int backward_impl(
     rb.dL_dcolor = dL_dout_color; rb.dL_ddepth = dL_dout_depth; rb.dL_dalpha = dL_dout_alpha;
     rb.dL_dfeature = dL_dout_feature; rb.acc = g.acc; rb.include_feature = include_feature;
     rb.order = im.order; rb.sched = tile_schedule_mode();
+    rb.einst = einst; rb.partial = det ? b.partial : nullptr;
     PROF_BEGIN(RENDER_BWD);
     GSR_CHECK(launch_render_backward(rb, stream));
+    if (det) {  // per-Gaussian sums of the instance rows in emission order (no atomics)
+      const bool in_b = (sort_passes(32) & 1) != 0;  // the depth sort's ping-pong, as the forward
+      GSR_CHECK(launch_det_reduce(P, in_b ? g.dval_b : g.dval_a, g.offsets, b.partial,
+                                  (uint32_t)R, g.acc, stream));
+    }
     PROF_END(RENDER_BWD);
   }
   BwdPreArgs ba{};

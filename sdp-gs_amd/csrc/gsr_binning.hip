@@ -30,7 +30,8 @@ __global__ __launch_bounds__(kThreads) void duplicate_kernel(int P,
                                                              uint32_t* __restrict__ tkey,
                                                              uint32_t* __restrict__ tval,
                                                              uint32_t R, SideClear clear0,
-                                                             SideClear clear1) {
+                                                             SideClear clear1,
+                                                             uint32_t* __restrict__ egid) {
   const int s = (int)(blockIdx.x * kThreads + threadIdx.x);
   const size_t nth = (size_t)gridDim.x * kThreads;
   side_clear(clear0.p, clear0.bytes, (size_t)s, nth);
@@ -56,7 +57,12 @@ __global__ __launch_bounds__(kThreads) void duplicate_kernel(int P,
     cut_row_range(cut, y, x0, x1, a, b);
     for (uint32_t x = a; x < b && off < end; x++) {
       tkey[off] = y * gx + x;
-      tval[off] = gid;
+      if (egid) {  // deterministic backward: sort the emission index, keep its Gaussian aside
+        tval[off] = off;
+        egid[off] = gid;
+      } else {
+        tval[off] = gid;
+      }
       off++;
     }
   }
@@ -97,15 +103,71 @@ __global__ __launch_bounds__(kThreads) void tile_ranges_kernel(size_t R,
   if (idx == R - 1 && cur_ok) ranges[cur].y = (uint32_t)R;
 }
 
+__global__ __launch_bounds__(kThreads) void det_gather_kernel(size_t R,
+                                                              const uint32_t* __restrict__ einst,
+                                                              const uint32_t* __restrict__ egid,
+                                                              uint32_t* __restrict__ point_list) {
+  const size_t q = (size_t)blockIdx.x * kThreads + threadIdx.x;
+  if (q < R) point_list[q] = egid[min(einst[q], (uint32_t)(R - 1))];
+}
+
+// Deterministic backward, second pass: one lane per depth-ordered Gaussian sums its instances'
+// rows (emission order = its tiles in row-major order, the same on every run) and stores the
+// total -- no float atomics anywhere, so the gradients are bitwise reproducible.
+__global__ __launch_bounds__(kThreads) void det_reduce_kernel(int P,
+                                                              const uint32_t* __restrict__ order,
+                                                              const uint32_t* __restrict__ offsets,
+                                                              const float4* __restrict__ partial,
+                                                              uint32_t R,
+                                                              float4* __restrict__ acc) {
+  const int s = (int)(blockIdx.x * kThreads + threadIdx.x);
+  if (s >= P) return;
+  const uint32_t beg = (s == 0) ? 0u : min(offsets[s - 1], R);
+  const uint32_t end = min(offsets[s], R);
+  if (beg == end) return;  // no instances: the row stays as zeroed
+  const uint32_t gid = min(order[s], (uint32_t)P - 1u);
+  constexpr int kV = kAccFloats / 4;
+  float4 t[kV];
+#pragma unroll
+  for (int v = 0; v < kV; v++) t[v] = partial[(size_t)beg * kV + v];
+  for (uint32_t e = beg + 1; e < end; e++) {
+#pragma unroll
+    for (int v = 0; v < kV; v++) {
+      const float4 x = partial[(size_t)e * kV + v];
+      t[v].x += x.x; t[v].y += x.y; t[v].z += x.z; t[v].w += x.w;
+    }
+  }
+#pragma unroll
+  for (int v = 0; v < kV; v++) acc[(size_t)gid * kV + v] = t[v];
+}
+
 }  // namespace
+
+hipError_t launch_det_gather(size_t R, const uint32_t* einst, const uint32_t* egid,
+                             uint32_t* point_list, hipStream_t s) {
+  if (R == 0) return hipSuccess;
+  hipLaunchKernelGGL(det_gather_kernel, dim3((unsigned)((R + kThreads - 1) / kThreads)),
+                     dim3(kThreads), 0, s, R, einst, egid, point_list);
+  return hipGetLastError();
+}
+
+hipError_t launch_det_reduce(int P, const uint32_t* order, const uint32_t* offsets,
+                             const float* partial, uint32_t R, float* acc, hipStream_t s) {
+  if (P == 0 || R == 0) return hipSuccess;
+  static_assert(kAccFloats % 4 == 0, "accumulator rows are float4 vectors");
+  hipLaunchKernelGGL(det_reduce_kernel, dim3((P + kThreads - 1) / kThreads), dim3(kThreads), 0, s,
+                     P, order, offsets, reinterpret_cast<const float4*>(partial), R,
+                     reinterpret_cast<float4*>(acc));
+  return hipGetLastError();
+}
 
 hipError_t launch_duplicate(int P, const uint32_t* order, const uint32_t* offsets,
                             const int32_t* radii, const float4* rec, uint32_t gx, uint32_t gy,
                             uint32_t* tkey, uint32_t* tval, uint32_t R, SideClear clear0,
-                            SideClear clear1, hipStream_t s) {
+                            SideClear clear1, hipStream_t s, uint32_t* egid) {
   if (P == 0) return hipSuccess;
   hipLaunchKernelGGL(duplicate_kernel, dim3((P + kThreads - 1) / kThreads), dim3(kThreads), 0, s,
-                     P, order, offsets, radii, rec, gx, gy, tkey, tval, R, clear0, clear1);
+                     P, order, offsets, radii, rec, gx, gy, tkey, tval, R, clear0, clear1, egid);
   return hipGetLastError();
 }
 

@@ -160,9 +160,13 @@ struct BinState {
   uint32_t* tkey_b;
   uint32_t* tval_b;
   SortScratch sort;  // tile-sort scratch
+  // deterministic backward only (gsr.h, debug bit 1): the tile sort carries each instance's
+  // emission index e (depth order, Gaussian-major) instead of its Gaussian id
+  uint32_t* egid;    // [R] Gaussian id of emission index e
+  float* partial;    // [R][kAccFloats] the blend backward's gradient row of each instance, by e
   size_t bytes;
 };
-BinState carve_bin(char* base, size_t R);
+BinState carve_bin(char* base, size_t R, bool det = false);
 
 struct ImgState {
   float* final_T;       // [H*W]
@@ -274,7 +278,7 @@ hipError_t launch_sh_grad_flush(const ShFlushArgs& a, hipStream_t s);
 hipError_t launch_duplicate(int P, const uint32_t* order, const uint32_t* offsets,
                             const int32_t* radii, const float4* rec, uint32_t gx, uint32_t gy,
                             uint32_t* tkey, uint32_t* tval, uint32_t R, SideClear clear0,
-                            SideClear clear1, hipStream_t s);
+                            SideClear clear1, hipStream_t s, uint32_t* egid = nullptr);
 // ranges_cleared: the ranges are already zero (duplicate's side clear): no memset launch.
 // Also writes the call's status word from the depth / tile sorts' error words (either may be null).
 hipError_t launch_tile_ranges(size_t R, const uint32_t* sorted_tiles, uint2* ranges,
@@ -319,7 +323,17 @@ struct RenderBwdArgs {
   int include_feature;
   uint32_t* order;
   int sched;
+  // deterministic backward: per-instance rows partial[einst[q]] instead of atomics into acc
+  const uint32_t* einst;  // [R] emission index of tile-sorted instance q
+  float* partial;         // [R][kAccFloats]
 };
 hipError_t launch_render_backward(const RenderBwdArgs& a, hipStream_t s);
+// deterministic backward: acc[order[s]] = sum over the instances e of depth-ordered Gaussian s
+// (e in [offsets[s-1], offsets[s]), increasing e) of partial[e]
+hipError_t launch_det_reduce(int P, const uint32_t* order, const uint32_t* offsets,
+                             const float* partial, uint32_t R, float* acc, hipStream_t s);
+// deterministic forward: point_list[q] = egid[einst[q]]
+hipError_t launch_det_gather(size_t R, const uint32_t* einst, const uint32_t* egid,
+                             uint32_t* point_list, hipStream_t s);
 
 }  // namespace gsr

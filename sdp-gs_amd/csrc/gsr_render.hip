@@ -419,7 +419,15 @@ __device__ __forceinline__ int reduce16_slot(int lane, SwapOrient o) {
   return b5 * 8 + b4 * 4 + ((lane >> 3) & 1) * 2 + ((lane >> 2) & 1);
 }
 
-template <bool EXTRA, bool FEAT, int GROUP>
+// Deterministic variant (DET, gsr.h debug bit 1): no float atomics.  Every wave stores its
+// butterfly sums into its OWN accumulator rows (each batch entry is in a wave's list at most
+// once), the four waves' rows are added in wave order, and each (splat, tile) row is stored to
+// partial[emission index of the instance]; det_reduce_kernel then sums every Gaussian's rows in
+// emission order.  13-float rows (the gradient values; slots 13-15 are always zero), 2
+// workgroups per CU.
+constexpr int kAccDet = 13;
+
+template <bool EXTRA, bool FEAT, int GROUP, bool DET>
 __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
   __shared__ float4 s_r0[kThreads];
   __shared__ float4 s_r1[kThreads];
@@ -429,7 +437,8 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
   // accumulator rows padded to an odd stride (17 floats): the per-splat moments pass (lane t ->
   // row t) and the zero-fill are bank-conflict-free; the butterfly's adds (16 lanes -> 16 slots of
   // one row) and the flush (4 rows x 16 slots per wave) stay conflict-free as well
-  __shared__ float s_acc[kThreads * kAccPad];
+  constexpr int kRow = DET ? kAccDet : kAccPad;
+  __shared__ float s_acc[(DET ? 4 : 1) * kThreads * kRow];
   __shared__ uint8_t s_mask[kThreads];
   __shared__ uint8_t s_list[kThreads / 64][kThreads];
 
@@ -500,7 +509,7 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
   const float ddelx_dx = (float)(0.5 * a.W);
   const float ddely_dy = (float)(0.5 * a.H);
 
-  for (int k = (int)threadIdx.x; k < kThreads * kAccPad; k += kThreads) s_acc[k] = 0.0f;
+  for (int k = (int)threadIdx.x; k < (DET ? 4 : 1) * kThreads * kRow; k += kThreads) s_acc[k] = 0.0f;
 
   // rel = position inside the tile's list; every pixel only uses rel < its n_contrib <= tile_last
   for (uint32_t done_cnt = 0; done_cnt < tile_last; done_cnt += kThreads) {
@@ -636,7 +645,11 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
       const float sum = wave_reduce16_dpp(g, lane);
       if ((lane & 3) == 0) {
         const int k = reduce16_slot(lane, swap_orient);
-        if (sum != 0.0f) atomicAdd(&s_acc[j * kAccPad + k], sum);
+        if (DET) {
+          if (k < kAccDet) s_acc[(wid * kThreads + j) * kRow + k] = sum;
+        } else if (sum != 0.0f) {
+          atomicAdd(&s_acc[j * kAccPad + k], sum);
+        }
       }
 #endif
     }
@@ -646,7 +659,13 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
     if (threadIdx.x < cnt) {
       const float4 r0 = s_r0[threadIdx.x];
       const float4 r1 = s_r1[threadIdx.x];
-      float* row = s_acc + threadIdx.x * kAccPad;
+      float* row = s_acc + threadIdx.x * kRow;
+      if (DET) {  // the four waves' rows, added in wave order, into wave 0's row
+#pragma unroll
+        for (int k = 0; k < kAccDet; k++)
+          row[k] = ((row[k] + row[kThreads * kRow + k]) + row[2 * kThreads * kRow + k]) +
+                   row[3 * kThreads * kRow + k];
+      }
       const float sx = row[kAccMx], sy = row[kAccMy];
       const float o = r1.y;
       row[kAccMx] = -(o * (r0.z * sx + r0.w * sy)) * ddelx_dx;
@@ -662,13 +681,28 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
       const uint32_t jj = (uint32_t)it * (kThreads / kAccFloats) + (threadIdx.x >> 4);
       const int k = (int)(threadIdx.x & 15);
       if (jj < cnt) {
-        const float v = s_acc[jj * kAccPad + k];
-        if (v != 0.0f) {
-          atomicAdd(&a.acc[(size_t)s_gid[jj] * kAccFloats + k], v);
-          s_acc[jj * kAccPad + k] = 0.0f;
+        if (DET) {  // every slot of the instance's row is stored (zeros too), then re-zeroed
+          const uint32_t q = range.x + tile_last - 1 - done_cnt - jj;
+          const float v = k < kAccDet ? s_acc[jj * kRow + k] : 0.0f;
+          a.partial[(size_t)a.einst[q] * kAccFloats + k] = v;
+          if (k < kAccDet)
+#pragma unroll
+            for (int w = 0; w < 4; w++) s_acc[(w * kThreads + jj) * kRow + k] = 0.0f;
+        } else {
+          const float v = s_acc[jj * kAccPad + k];
+          if (v != 0.0f) {
+            atomicAdd(&a.acc[(size_t)s_gid[jj] * kAccFloats + k], v);
+            s_acc[jj * kAccPad + k] = 0.0f;
+          }
         }
       }
     }
+  }
+  if (DET) {  // instances behind the tile's last contributor: zero rows
+    const uint32_t n = range.y - range.x - min(tile_last, range.y - range.x);
+    for (uint32_t idx = threadIdx.x; idx < n * kAccFloats; idx += kThreads)
+      a.partial[(size_t)a.einst[range.x + tile_last + idx / kAccFloats] * kAccFloats +
+                idx % kAccFloats] = 0.0f;
   }
 }
 
@@ -1003,10 +1037,12 @@ hipError_t launch_render_backward(const RenderBwdArgs& a, hipStream_t s) {
                        a.tile_last, ntiles, a.order);
 #define GSR_BWD(E, F)                                                                             \
   do {                                                                                           \
-    if (group == 1)                                                                              \
-      hipLaunchKernelGGL((render_bwd_kernel<E, F, 1>), dim3(ntiles), dim3(kThreads), 0, s, a);   \
+    if (a.partial)                                                                               \
+      hipLaunchKernelGGL((render_bwd_kernel<E, F, 4, true>), dim3(ntiles), dim3(kThreads), 0, s, a); \
+    else if (group == 1)                                                                         \
+      hipLaunchKernelGGL((render_bwd_kernel<E, F, 1, false>), dim3(ntiles), dim3(kThreads), 0, s, a); \
     else                                                                                         \
-      hipLaunchKernelGGL((render_bwd_kernel<E, F, 4>), dim3(ntiles), dim3(kThreads), 0, s, a);   \
+      hipLaunchKernelGGL((render_bwd_kernel<E, F, 4, false>), dim3(ntiles), dim3(kThreads), 0, s, a); \
   } while (0)
   if (feat) GSR_BWD(true, true);
   else if (extra) GSR_BWD(true, false);

@@ -126,7 +126,7 @@ class _RasterizeGaussians(torch.autograd.Function):
                 int(bool(rs.prefiltered)), _ptr(shl), _ptr(lfp), _ptr(conf), int(include_feature),
                 _ptr(color), _ptr(depth), _ptr(alpha), _ptr(feature), _ptr(radii),
                 _lib.ctypes.byref(nr), _lib.alloc_callback(), holder.key, stream,
-                int(bool(rs.debug)))
+                _debug_flags(rs.debug))
         try:
             with torch.cuda.device(dev):
                 rc = L.gsr_rasterize_gaussians(*args)
@@ -148,6 +148,7 @@ class _RasterizeGaussians(torch.autograd.Function):
         LAST_STATS["P"] = P
 
         ctx.raster_settings = rs
+        ctx.gsr_flags = _debug_flags(rs.debug)
         ctx.num_rendered = num_rendered
         ctx.meta = dict(P=P, M=M, H=H, W=W, include_feature=include_feature,
                         has_shs=shs is not None, has_shl=shl is not None,
@@ -213,7 +214,7 @@ class _RasterizeGaussians(torch.autograd.Function):
                 _ptr(binning) if binning.numel() else None, _ptr(image) if image.numel() else None,
                 _ptr(d_means2D), _ptr(d_colors), _ptr(d_opac), _ptr(d_means3D), _ptr(d_cov),
                 _ptr(d_sh), _ptr(d_sc), _ptr(d_rot), _ptr(d_shl), _ptr(d_lfp), stream,
-                int(bool(rs.debug)))
+                ctx.gsr_flags)
         try:
             with torch.cuda.device(dev):
                 rc = L.gsr_rasterize_gaussians_backward(*args)
@@ -296,7 +297,7 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
                         int(include_feature))
                 tail = (_ptr(color), _ptr(depth), _ptr(alpha), _ptr(feature), _ptr(radii),
                         _lib.ctypes.byref(nr), _lib.alloc_callback(), holder.key, stream,
-                        int(bool(rs.debug)))
+                        _debug_flags(rs.debug))
                 if pre is not None:  # colour + clamp bits from the multi-view pre-pass
                     rc = L.gsr_rasterize_gaussians_fused_precolor(
                         *head, _ptr(pre[0]), _ptr(pre[1]), *tail)
@@ -310,6 +311,7 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
         LAST_STATS["P"] = P
 
         ctx.raster_settings = rs
+        ctx.gsr_flags = _debug_flags(rs.debug)
         ctx.num_rendered = num_rendered
         ctx.pre_jac = None if pre is None else pre[2]
         # grad-into-leaves mode: only when every differentiable input is itself the float32
@@ -420,7 +422,7 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
                 _ptr(d_means2D), _ptr(d_means3D), _ptr(d_dc), _ptr(d_rest), _ptr(d_op),
                 _ptr(d_sc), _ptr(d_rot), _ptr(d_lf), _ptr(d_rgb),
                 _ptr(ctx.pre_jac) if d_rgb is not None else None, int(accumulate), stream,
-                int(bool(rs.debug)))
+                ctx.gsr_flags)
         _lib.check(rc)
         if into_leaves:
             # one event per device, re-recorded: a later wait_event has already captured the
@@ -437,6 +439,27 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
 
 
 _GRAD_INTO_LEAVES = None
+_DETERMINISTIC = None
+
+
+def deterministic(enable: Optional[bool] = None) -> bool:
+    """Query / set the deterministic backward (default: env GSR_DETERMINISTIC=1).  The reference's
+    backward adds gradients with unordered float atomics (backward.cu:523-554), so two runs differ
+    in the last bits; with this on, the blend backward stores per-instance gradient rows and sums
+    each Gaussian's rows in a fixed order (include/gsr.h GSR_DEBUG_DETERMINISTIC): bitwise
+    reproducible gradients, at some cost in speed and binning-buffer memory.  A forward's mode is
+    kept for its backward."""
+    global _DETERMINISTIC
+    if enable is not None:
+        _DETERMINISTIC = bool(enable)
+    if _DETERMINISTIC is None:
+        _DETERMINISTIC = os.environ.get("GSR_DETERMINISTIC", "0") == "1"
+    return _DETERMINISTIC
+
+
+def _debug_flags(debug) -> int:
+    """The C-ABI `debug` word: bit 0 the reference's debug flag, bit 1 deterministic backward."""
+    return int(bool(debug)) | (2 if deterministic() else 0)
 # device index -> ShGradDeferral collecting the views of the current multi-view step
 _SH_DEFER = {}
 # device index -> ShPrecolor of the current multi-view step

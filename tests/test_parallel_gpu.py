@@ -1,0 +1,97 @@
+"""The multi-GPU step's gradient plumbing on the HIP path, in one process (world size 1, gloo over
+the device tensors): gradient-as-bucket-view (the fused backward accumulates straight into the
+all-reduce buffer), the deferred SH flush written into the bucket in row slices, and the
+overlapped all-reduce of ViewPipeline.run(reducer=) give the gradients of the same step without a
+reducer (the collectives are issued at world size 1 too, so their stream ordering
+against the flush is checked).  tests/test_parallel.py covers the cross-rank sums (world size 2,
+CPU); this covers the rasterizer-side writes into the bucket, which have no CPU path.
+One process only: no GPU work is started in a child process."""
+import os
+
+import pytest
+import torch
+import torch.distributed as dist
+
+pytestmark = pytest.mark.gpu
+
+
+class _Pipe:
+    convert_SHs_python = True
+    compute_cov3D_python = False
+    debug = False
+    use_confidence = False
+
+
+class _Opt:
+    include_feature = True
+
+
+def _scene(dev):
+    from gsr_amd.model import SplatModel
+    from gsr_amd.synthetic import make_cameras, make_gaussians, upstream_grads
+    model = SplatModel(make_gaussians(20_000, sh_degree=3, seed=3), device=dev)
+    cams = [c.to(dev) for c in make_cameras(4, 320, 240, seed=5)]
+    grads = upstream_grads(240, 320, seed=7, device=dev)
+    return model, cams, grads
+
+
+def _step(model, cams, grads, views, reducer):
+    from gaussian_renderer import render
+    dimg, ddep, dfeat = grads
+    bg = torch.zeros(3, device=dimg.device)
+
+    def one_view(cam):
+        pkg = render(cam, model, _Pipe(), bg, _Opt())
+        torch.autograd.backward([pkg["render"], pkg["depth"], pkg["feature"]], [dimg, ddep, dfeat])
+
+    if reducer is not None:
+        reducer.attach_grads()
+    else:
+        for p in model.parameters():
+            p.grad = None
+    views.run(cams, one_view, model=model, reducer=reducer)
+    torch.cuda.synchronize()
+    return [p.grad.detach().clone() for p in model.parameters()]
+
+
+@pytest.fixture
+def gloo_world1(tmp_path):
+    init = "file://" + os.path.join(str(tmp_path), "pg")
+    dist.init_process_group("gloo", init_method=init, rank=0, world_size=1)
+    try:
+        yield
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("bucket_bytes", [64 << 20, 256 << 10])
+def test_bucket_view_grads_equal_plain_step(gloo_world1, bucket_bytes):
+    import diff_gaussian_rasterization as dgr
+    from gsr_amd.parallel import GradAllReducer
+    from gsr_amd.pipeline import ViewPipeline
+    dev = torch.device("cuda", 0)
+    prev = dgr.grad_into_leaves()
+    dgr.grad_into_leaves(True)
+    try:
+        model, cams, grads = _scene(dev)
+        views = ViewPipeline(dev, depth=2, defer_sh=True, precolor=True)
+        ref = _step(model, cams, grads, views, None)
+        reducer = GradAllReducer(model, bucket_bytes=bucket_bytes)
+        # issue the collectives at world size 1 as well: gloo copies each slice to the host and
+        # back, so a collective that ran before its slice was flushed would write stale zeros
+        reducer._active = lambda: True
+        for _ in range(2):  # the second step reuses the attached buffer (zeroed by attach_grads)
+            got = _step(model, cams, grads, views, reducer)
+            for p, g, r in zip(model.parameters(), got, ref):
+                assert g.shape == r.shape
+                # the backward's float atomics make two runs of a view differ in the last bits
+                # (as the reference's); a collective racing its slice would zero whole rows
+                err = float((g - r).abs().max())
+                assert err <= 1e-5 * float(r.abs().max()) + 1e-30, (tuple(p.shape), err)
+            # the .grad tensors are views into the flat all-reduce buffer
+            base = reducer.flat.data_ptr()
+            end = base + reducer.flat.numel() * 4
+            assert all(base <= p.grad.data_ptr() < end for p in model.parameters())
+        assert any(float(r.abs().max()) > 0 for r in ref)
+    finally:
+        dgr.grad_into_leaves(prev)
