@@ -793,8 +793,13 @@ __device__ __forceinline__ uint32_t build_group_lists(const uint16_t* s_mask, ui
   return grp == 0 ? n[0] : grp == 1 ? n[1] : grp == 2 ? n[2] : n[3];
 }
 
+// waves per SIMD the block-list forward is compiled for (VGPR budget 512 / n); 5 measured
+// slower (96 VGPRs with 16 spilled: 0.116 -> 0.122 ms), so the default lets it take 118
+#ifndef GSR_FWD_BLK_WAVES
+#define GSR_FWD_BLK_WAVES 1
+#endif
 template <bool FEAT>
-__global__ __launch_bounds__(kThreads) void render_fwd_blk_kernel(RenderArgs a) {
+__global__ __launch_bounds__(kThreads, GSR_FWD_BLK_WAVES) void render_fwd_blk_kernel(RenderArgs a) {
   __shared__ float4 s_r0[kThreads];
   __shared__ float4 s_r1[kThreads];
   __shared__ float4 s_r2[kThreads];
