@@ -16,6 +16,7 @@ out = sys.argv[2] if len(sys.argv) > 2 else "profiles/pmc_r01.json"
 workload = sys.argv[3] if len(sys.argv) > 3 else "llff_1m_1008x756"
 STAGE = {"preprocess_kernel": "preprocess", "duplicate_kernel": "duplicate",
          "tile_ranges_kernel": "ranges", "render_fwd_kernel": "render_fwd",
+         "render_fwd_blk_kernel": "render_fwd",
          "render_bwd_kernel": "render_bwd", "preprocess_bwd_kernel": "preprocess_bwd",
          "radix_totals_kernel": "radix_totals", "radix_onesweep_kernel": "radix_onesweep",
          "scan_reduce_kernel": "scan_reduce", "scan_final_kernel": "scan_final",

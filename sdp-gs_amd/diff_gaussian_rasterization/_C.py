@@ -31,6 +31,16 @@ def _p(t):
     return None if t is None else t.data_ptr()
 
 
+# deterministic-backward mode of each live forward, keyed by its binning buffer: the backward must
+# pass the forward's flags (include/gsr.h GSR_DEBUG_DETERMINISTIC), whatever the mode is by then
+_FWD_FLAGS = {}
+
+
+def _forward_flags(debug):
+    from . import _debug_flags
+    return _debug_flags(debug)
+
+
 def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations, scale_modifier,
                         cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height,
                         image_width, sh, degree, campos, prefiltered, debug):
@@ -49,6 +59,7 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
                                    _opt(rotations), _opt(cov3D_precomp), viewmatrix, projmatrix,
                                    campos)]
     bg, col, op, sc, rot, cov, view, proj, cp = keep
+    flags = _forward_flags(debug)
     try:
         with torch.cuda.device(dev):
             rc = _lib.load().gsr_rasterize_gaussians(
@@ -56,12 +67,16 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
                 _p(cov), _p(view), _p(proj), float(tan_fovx), float(tan_fovy), H, W, _p(shs),
                 int(degree), _p(cp), int(bool(prefiltered)), None, None, None, 0, _p(out_color),
                 None, None, None, _p(radii), ctypes.byref(nr), _lib.alloc_callback(), holder.key,
-                torch.cuda.current_stream(dev).cuda_stream, int(bool(debug)))
+                torch.cuda.current_stream(dev).cuda_stream, flags)
         _lib.check(rc)
     finally:
         holder.release()
     empty = torch.empty((0,), dtype=torch.uint8, device=dev)
     geom, binning, img = (b if b is not None else empty for b in holder.bufs)
+    if binning.numel():
+        if len(_FWD_FLAGS) > 4096:  # forwards whose backward never ran (inference)
+            _FWD_FLAGS.clear()
+        _FWD_FLAGS[binning.data_ptr()] = flags
     return int(nr.value), out_color, radii, geom, binning, img
 
 
@@ -92,6 +107,8 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     g = geomBuffer if geomBuffer.numel() else None
     b = binningBuffer if binningBuffer.numel() else None
     i = imageBuffer if imageBuffer.numel() else None
+    flags = (int(bool(debug)) | (_FWD_FLAGS.pop(b.data_ptr(), 0) & 2)) if b is not None \
+        else int(bool(debug))
     with torch.cuda.device(dev):
         rc = _lib.load().gsr_rasterize_gaussians_backward(
             P, M, int(R), _p(bg), _p(m3), _p(rad), _p(col), _p(sc), _p(rot), float(scale_modifier),
@@ -100,7 +117,7 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
             _p(d_means2D), _p(d_colors), _p(d_opacity), _p(d_means3D), _p(d_cov3D),
             _p(d_sh) if shs is not None else None, _p(d_scales) if sc is not None else None,
             _p(d_rot) if sc is not None else None, None, None,
-            torch.cuda.current_stream(dev).cuda_stream, int(bool(debug)))
+            torch.cuda.current_stream(dev).cuda_stream, flags)
     _lib.check(rc)
     return d_means2D, d_colors, d_opacity, d_means3D, d_cov3D, d_sh, d_scales, d_rot
 

@@ -114,19 +114,28 @@ def test_confidence_parity():
     compare(scene(P=P, W=80, H=64, seed=4, confidence=conf))
 
 
-def test_C_shim_matches_oracle_vanilla_api():
+@pytest.mark.parametrize("det", [False, True])
+def test_C_shim_matches_oracle_vanilla_api(det):
     """The `_C`-compatible shim with the reference's exact pybind signatures
-    (rasterize_points.cu:35-55, 117-140): forward tuple and the 8 backward grads."""
+    (rasterize_points.cu:35-55, 117-140): forward tuple and the 8 backward grads.  det: the
+    deterministic backward, switched off again between forward and backward (the shim keeps the
+    forward's mode for its backward)."""
+    import diff_gaussian_rasterization as dgr
     from diff_gaussian_rasterization import _C
     kw = scene(P=3000, W=97, H=61, seed=8, mode="sh", cov_mode="scale_rot", feature=None)
     d = lambda x: torch.tensor(np.asarray(x), device="cuda")  # noqa: E731
     E = torch.Tensor([]).cuda()
     P = kw["means3D"].shape[0]
-    num_rendered, color, radii, geom, binning, img = _C.rasterize_gaussians(
-        d(kw["bg"]), d(kw["means3D"]), E, d(kw["opacities"]).view(P, 1), d(kw["scales"]),
-        d(kw["rotations"]), 1.0, E, d(kw["viewmatrix"]), d(kw["projmatrix"]), kw["tanfovx"],
-        kw["tanfovy"], kw["image_height"], kw["image_width"], d(kw["shs"]), kw["sh_degree"],
-        d(kw["campos"]), False, False)
+    prev = dgr.deterministic()
+    dgr.deterministic(det)
+    try:
+        num_rendered, color, radii, geom, binning, img = _C.rasterize_gaussians(
+            d(kw["bg"]), d(kw["means3D"]), E, d(kw["opacities"]).view(P, 1), d(kw["scales"]),
+            d(kw["rotations"]), 1.0, E, d(kw["viewmatrix"]), d(kw["projmatrix"]), kw["tanfovx"],
+            kw["tanfovy"], kw["image_height"], kw["image_width"], d(kw["shs"]), kw["sh_degree"],
+            d(kw["campos"]), False, False)
+    finally:
+        dgr.deterministic(prev)
     orc = OracleRaster(**kw)
     assert num_rendered > 0
     np.testing.assert_array_equal(radii.cpu().numpy(), orc.radii)
