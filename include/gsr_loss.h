@@ -53,6 +53,26 @@ int gsr_pearson_loss_backward(int64_t N, int K, const float* x, const float* y, 
                               float offset, const float* grad_loss, float* grad_y, float* grad_x,
                               void* scratch, void* stream);
 
+/* One training view's loss (train.py:99-131 with the depth branch), forward in two launches and
+ * backward in one: total = (1 - lambda) L1 + lambda (1 - SSIM) of image vs gt, plus depth_weight *
+ * min over {mono, 1 / (offset - mono)} of 1 - pearson(., depth) (the depth term of
+ * gsr_pearson_loss with K = 1, variants = 2; single-pass shifted sums in double, same r to double
+ * rounding).  image, gt [C,H,W]; depth, depth_mono [N].  out (device, 5 floats): photometric
+ * loss, L1, SSIM, depth term, total; total (device, 1 float): the total again, a separate
+ * tensor for autograd.  Scratch: gsr_view_loss_scratch_bytes, shared by forward and backward. */
+size_t gsr_view_loss_scratch_bytes(int C, int H, int W);
+int gsr_view_loss(int C, int H, int W, const float* image, const float* gt, float lambda_dssim,
+                  int64_t N, const float* depth, const float* depth_mono, float offset,
+                  float depth_weight, int need_grad, float* out, float* total, void* scratch,
+                  void* stream);
+/* grad_image, grad_depth of grad_total * total (grad_total: device scalar); needs the scratch of a
+ * need_grad forward on the same inputs. */
+int gsr_view_loss_backward(int C, int H, int W, const float* image, const float* gt,
+                           float lambda_dssim, int64_t N, const float* depth,
+                           const float* depth_mono, float offset, float depth_weight,
+                           const float* grad_total, float* grad_image, float* grad_depth,
+                           void* scratch, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -72,11 +72,11 @@ struct SsimArgs {
   float c1, c2;
 };
 
-__global__ __launch_bounds__(kThreads) void ssim_fwd_kernel(SsimArgs a) {
+// one 32x16 output tile (bx, by) of channel c; its partial sums go to parts[2 * b]
+__device__ __forceinline__ void ssim_fwd_tile(const SsimArgs& a, int bx, int by, int c, size_t b) {
   __shared__ float sx[kIY][kIX], sy[kIY][kIX];
   __shared__ float h[5][kIY][kTX];
-  const int c = blockIdx.z;
-  const int x0 = blockIdx.x * kTX, y0 = blockIdx.y * kTY;
+  const int x0 = bx * kTX, y0 = by * kTY;
   const size_t plane = (size_t)c * a.H * a.W;
   for (int e = threadIdx.x; e < kIX * kIY; e += kThreads) {
     const int r = e / kIX, q = e - r * kIX;
@@ -141,8 +141,12 @@ __global__ __launch_bounds__(kThreads) void ssim_fwd_kernel(SsimArgs a) {
       a.Cc[o] = ds12;
     }
   }
-  const size_t b = ((size_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
   block_sum2(msum, l1sum, a.parts + 2 * b);
+}
+
+__global__ __launch_bounds__(kThreads) void ssim_fwd_kernel(SsimArgs a) {
+  ssim_fwd_tile(a, blockIdx.x, blockIdx.y, blockIdx.z,
+                ((size_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x);
 }
 
 // parts [n][2] -> out: loss, l1 mean, ssim mean (double accumulation, fixed order)
@@ -183,11 +187,10 @@ struct SsimBwdArgs {
   Window win;
 };
 
-__global__ __launch_bounds__(kThreads) void ssim_bwd_kernel(SsimBwdArgs a) {
+__device__ __forceinline__ void ssim_bwd_tile(const SsimBwdArgs& a, int bx, int by, int c) {
   __shared__ float s[3][kIY][kIX];
   __shared__ float h[3][kIY][kTX];
-  const int c = blockIdx.z;
-  const int x0 = blockIdx.x * kTX, y0 = blockIdx.y * kTY;
+  const int x0 = bx * kTX, y0 = by * kTY;
   const size_t plane = (size_t)c * a.H * a.W;
   // d loss / d ssim_mean and d loss / d l1_mean for the three outputs (loss, l1, ssim)
   const float gl = a.g_loss ? *a.g_loss : 0.f;
@@ -237,6 +240,10 @@ __global__ __launch_bounds__(kThreads) void ssim_bwd_kernel(SsimBwdArgs a) {
     const float sgn = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);  // torch.abs backward: sign
     a.dx[o] = k_ssim * dm + k_l1 * sgn;
   }
+}
+
+__global__ __launch_bounds__(kThreads) void ssim_bwd_kernel(SsimBwdArgs a) {
+  ssim_bwd_tile(a, blockIdx.x, blockIdx.y, blockIdx.z);
 }
 
 // ---- Pearson -------------------------------------------------------------------------------------
@@ -386,6 +393,177 @@ __global__ __launch_bounds__(kThreads) void pearson_bwd_kernel(PearsonArgs a,
     if (dy) dy[i * a.K + k] = (float)(gk * ((xv - mx) * inv - rr * (yv - my) / syy));
     if (dx && v == 0) dx[i * a.K + k] = (float)(gk * ((yv - my) * inv - rr * (xv - mx) / sxx));
   }
+}
+
+// ---- one training view's loss in three launches (train.py:99-131, losses.train_view_loss) -------
+// photometric (L1 + SSIM of image vs gt) + depth_weight * the Pearson depth term (depth_mono vs
+// the rendered depth, min over mono and 1 / (offset - mono)).  Forward: SSIM tiles and the Pearson
+// partial sums in ONE grid (the Pearson blocks follow the SSIM tiles), then one workgroup reduces
+// both and writes every output including the total; backward: SSIM tiles + Pearson elements in
+// one grid.  Pearson here is single-pass: sums of (x - x[0]), (y - y[0]) and their squares and
+// product in double (the shift keeps the centred sums free of cancellation), instead of the
+// two-pass means-then-centred form of gsr_pearson_loss; same r to double rounding.
+constexpr int kViewPearsonSums = 8;  // x0, x0^2, x0 y, x1, x1^2, x1 y, y, y^2 (shifted)
+constexpr int kViewPearsonMaxBlocks = 1024;
+
+struct ViewLossArgs {
+  SsimArgs ss;
+  int nssim;                 // SSIM tiles (grid x of ssim_grid, flattened)
+  int gx, gy;                // SSIM tile grid
+  int64_t N;                 // depth pixels
+  const float *mono, *depth;
+  float offset, depth_weight;
+  int npb;                   // Pearson partial blocks
+  double* pparts;            // [npb][8]
+  double* acc;               // [2][8]: the layout pearson_bwd_kernel reads (K = 1, variants = 2)
+  int32_t* sel;              // [1]
+  float* out;                // [5]: photometric loss, L1, SSIM, depth term, total (copy)
+  float* total;              // [1]
+  double inv_count;
+  float lambda;
+};
+
+__device__ double block_sum_d(double v, double* lds) {  // thread 0 gets the workgroup sum
+  v = wave_sum_d(v);
+  const int w = (int)(threadIdx.x >> 6);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) lds[w] = v;
+  __syncthreads();
+  return (lds[0] + lds[1]) + (lds[2] + lds[3]);
+}
+
+__device__ void view_pearson_partial(const ViewLossArgs& a, int b) {
+  __shared__ double lds[kThreads / 64];
+  const float x0s = a.mono[0], x1s = variant_x(a.mono[0], 1, a.offset), ys = a.depth[0];
+  double t[kViewPearsonSums] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int64_t i = (int64_t)b * kThreads + threadIdx.x; i < a.N; i += (int64_t)a.npb * kThreads) {
+    const float m = a.mono[i];
+    const double x0 = (double)m - (double)x0s;
+    const double x1 = (double)variant_x(m, 1, a.offset) - (double)x1s;
+    const double y = (double)a.depth[i] - (double)ys;
+    t[0] += x0; t[1] += x0 * x0; t[2] += x0 * y;
+    t[3] += x1; t[4] += x1 * x1; t[5] += x1 * y;
+    t[6] += y;  t[7] += y * y;
+  }
+#pragma unroll
+  for (int j = 0; j < kViewPearsonSums; j++) {
+    const double v = block_sum_d(t[j], lds);
+    if (threadIdx.x == 0) a.pparts[(size_t)b * kViewPearsonSums + j] = v;
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void view_loss_fwd_kernel(ViewLossArgs a) {
+  const int b = (int)blockIdx.x;
+  if (b < a.nssim) {
+    const int per = a.gx * a.gy;
+    const int c = b / per, r = b - c * per;
+    ssim_fwd_tile(a.ss, r % a.gx, r / a.gx, c, (size_t)b);
+  } else {
+    view_pearson_partial(a, b - a.nssim);
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void view_loss_finish_kernel(ViewLossArgs a) {
+  __shared__ double s[2][kThreads];
+  __shared__ double q[kViewPearsonSums][kThreads / 64];
+  // SSIM / L1 means exactly as ssim_reduce_kernel
+  double m = 0.0, l = 0.0;
+  for (int i = threadIdx.x; i < a.nssim; i += kThreads) {
+    m += (double)a.ss.parts[2 * i];
+    l += (double)a.ss.parts[2 * i + 1];
+  }
+  s[0][threadIdx.x] = m;
+  s[1][threadIdx.x] = l;
+  __syncthreads();
+  for (int d = kThreads / 2; d >= 1; d >>= 1) {
+    if ((int)threadIdx.x < d) {
+      s[0][threadIdx.x] += s[0][threadIdx.x + d];
+      s[1][threadIdx.x] += s[1][threadIdx.x + d];
+    }
+    __syncthreads();
+  }
+  // Pearson sums over the partial blocks, fixed order
+  double t[kViewPearsonSums] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int i = threadIdx.x; i < a.npb; i += kThreads)
+#pragma unroll
+    for (int j = 0; j < kViewPearsonSums; j++) t[j] += a.pparts[(size_t)i * kViewPearsonSums + j];
+  const int w = (int)(threadIdx.x >> 6);
+#pragma unroll
+  for (int j = 0; j < kViewPearsonSums; j++) {
+    const double v = wave_sum_d(t[j]);
+    if ((threadIdx.x & 63) == 0) q[j][w] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  const float ssim = (float)(s[0][0] * a.inv_count), l1 = (float)(s[1][0] * a.inv_count);
+  const float photo = (1.0f - a.lambda) * l1 + a.lambda * (1.0f - ssim);
+  double S[kViewPearsonSums];
+#pragma unroll
+  for (int j = 0; j < kViewPearsonSums; j++) S[j] = (q[j][0] + q[j][1]) + (q[j][2] + q[j][3]);
+  const double n = (double)a.N;
+  const float x0s = a.mono[0], x1s = variant_x(a.mono[0], 1, a.offset), ys = a.depth[0];
+  const double syy = S[7] - S[6] * S[6] / n;
+  float best = 0.f;
+  int sel = 0;
+  for (int v = 0; v < 2; v++) {
+    const double sx = S[3 * v], sxx = S[3 * v + 1] - sx * sx / n, sxy = S[3 * v + 2] - sx * S[6] / n;
+    double* acc = a.acc + (size_t)v * 8;  // pearson_bwd_kernel: mean = acc[0..1] / N, centred sums
+    acc[0] = ((double)(v == 0 ? x0s : x1s) + sx / n) * n;
+    acc[1] = ((double)ys + S[6] / n) * n;
+    acc[2] = sxx;
+    acc[3] = syy;
+    acc[4] = sxy;
+    float r = (float)(sxy / sqrt(sxx * syy));
+    if (r == r) r = fminf(fmaxf(r, -1.0f), 1.0f);  // torch.clamp keeps NaN
+    const float lv = 1.0f - r;
+    if (v == 0 || lv < best) {  // Python min(a, b): b only if b < a
+      best = lv;
+      sel = v;
+    }
+  }
+  *a.sel = sel;
+  const float total = photo + a.depth_weight * best;  // torch.add(photo, depth, alpha=w)
+  a.out[0] = photo;
+  a.out[1] = l1;
+  a.out[2] = ssim;
+  a.out[3] = best;
+  a.out[4] = total;
+  *a.total = total;
+}
+
+struct ViewLossBwdArgs {
+  SsimBwdArgs ss;
+  int nssim, gx, gy;
+  PearsonArgs pa;  // N, K = 1, x = mono, y = depth, variants = 2, acc
+  const int32_t* sel;
+  const float* g_total;
+  float depth_weight;
+  float* dd;
+};
+
+__global__ __launch_bounds__(kThreads) void view_loss_bwd_kernel(ViewLossBwdArgs a) {
+  const int b = (int)blockIdx.x;
+  if (b < a.nssim) {
+    const int per = a.gx * a.gy;
+    const int c = b / per, r = b - c * per;
+    ssim_bwd_tile(a.ss, r % a.gx, r / a.gx, c);
+    return;
+  }
+  // pearson_bwd_kernel's element work with grad_loss = g_total * depth_weight (as torch's g * w)
+  const int64_t i = (int64_t)(b - a.nssim) * kThreads + threadIdx.x;
+  if (i >= a.pa.N) return;
+  const int v = *a.sel;
+  const double* acc = a.pa.acc + (size_t)v * 8;
+  const double mx = acc[0] / (double)a.pa.N, my = acc[1] / (double)a.pa.N;
+  const double sxx = acc[2], syy = acc[3], sxy = acc[4];
+  const double rr = sxy / sqrt(sxx * syy);
+  const bool pass = rr >= -1.0 && rr <= 1.0;
+  const float gq = *a.g_total * a.depth_weight;
+  const double gk = pass ? -(double)gq : 0.0;
+  const double xv = (double)variant_x(a.pa.x[i], v, a.pa.offset);
+  const double yv = (double)a.pa.y[i];
+  const double inv = 1.0 / sqrt(sxx * syy);
+  a.dd[i] = (float)(gk * ((xv - mx) * inv - rr * (yv - my) / syy));
 }
 
 }  // namespace
@@ -548,5 +726,98 @@ extern "C" int gsr_pearson_loss_backward(int64_t N, int K, const float* x, const
   carve_pearson(scratch, K, variants, &a.acc, &r, &sel, &a.parts);
   hipLaunchKernelGGL(pearson_bwd_kernel, dim3((unsigned)((N + kThreads - 1) / kThreads)),
                      dim3(kThreads), 0, (hipStream_t)stream, a, sel, grad_loss, grad_y, grad_x);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+static size_t view_pearson_bytes() {
+  Carver c(nullptr);
+  c.take<double>(2 * 8);
+  c.take<int32_t>(4);
+  c.take<double>((size_t)kViewPearsonMaxBlocks * kViewPearsonSums);
+  return c.size();
+}
+
+extern "C" size_t gsr_view_loss_scratch_bytes(int C, int H, int W) {
+  const size_t p = gsr_photometric_scratch_bytes(C, H, W);
+  return p ? ((p + 255) & ~(size_t)255) + view_pearson_bytes() : 0;
+}
+
+static void carve_view(void* scratch, int C, int H, int W, float** A, float** B, float** Cc,
+                       float** parts, double** acc, int32_t** sel, double** pparts) {
+  carve_photometric(scratch, C, H, W, A, B, Cc, parts);
+  const size_t p = (gsr_photometric_scratch_bytes(C, H, W) + 255) & ~(size_t)255;
+  Carver c((char*)scratch + p);
+  *acc = c.take<double>(2 * 8);
+  *sel = c.take<int32_t>(4);
+  *pparts = c.take<double>((size_t)kViewPearsonMaxBlocks * kViewPearsonSums);
+}
+
+extern "C" int gsr_view_loss(int C, int H, int W, const float* image, const float* gt,
+                             float lambda_dssim, int64_t N, const float* depth,
+                             const float* depth_mono, float offset, float depth_weight,
+                             int need_grad, float* out, float* total, void* scratch,
+                             void* stream) {
+  if (C <= 0 || H <= 0 || W <= 0 || N < 2 || !image || !gt || !depth || !depth_mono || !out ||
+      !total || !scratch)
+    return 1;
+  ViewLossArgs a{};
+  a.ss.C = C; a.ss.H = H; a.ss.W = W;
+  a.ss.x = image; a.ss.y = gt;
+  float *A, *B, *Cc;
+  carve_view(scratch, C, H, W, &A, &B, &Cc, &a.ss.parts, &a.acc, &a.sel, &a.pparts);
+  a.ss.A = need_grad ? A : nullptr;
+  a.ss.B = need_grad ? B : nullptr;
+  a.ss.Cc = need_grad ? Cc : nullptr;
+  a.ss.win = make_window();
+  a.ss.c1 = (float)(0.01 * 0.01);
+  a.ss.c2 = (float)(0.03 * 0.03);
+  const dim3 g = ssim_grid(C, H, W);
+  a.gx = (int)g.x; a.gy = (int)g.y;
+  a.nssim = (int)ssim_blocks(C, H, W);
+  a.N = N; a.mono = depth_mono; a.depth = depth;
+  a.offset = offset; a.depth_weight = depth_weight;
+  a.npb = (int)pearson_blocks(N);
+  a.out = out; a.total = total;
+  a.inv_count = 1.0 / ((double)C * H * W);
+  a.lambda = lambda_dssim;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(view_loss_fwd_kernel, dim3((unsigned)(a.nssim + a.npb)), dim3(kThreads), 0, s,
+                     a);
+  hipLaunchKernelGGL(view_loss_finish_kernel, dim3(1), dim3(kThreads), 0, s, a);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+extern "C" int gsr_view_loss_backward(int C, int H, int W, const float* image, const float* gt,
+                                      float lambda_dssim, int64_t N, const float* depth,
+                                      const float* depth_mono, float offset, float depth_weight,
+                                      const float* grad_total, float* grad_image,
+                                      float* grad_depth, void* scratch, void* stream) {
+  if (C <= 0 || H <= 0 || W <= 0 || N < 2 || !image || !gt || !depth || !depth_mono ||
+      !grad_total || !grad_image || !grad_depth || !scratch)
+    return 1;
+  ViewLossBwdArgs a{};
+  a.ss.C = C; a.ss.H = H; a.ss.W = W;
+  a.ss.x = image; a.ss.y = gt;
+  float *A, *B, *Cc, *parts;
+  double *acc, *pparts;
+  int32_t* sel;
+  carve_view(scratch, C, H, W, &A, &B, &Cc, &parts, &acc, &sel, &pparts);
+  a.ss.A = A; a.ss.B = B; a.ss.Cc = Cc;
+  a.ss.g_loss = grad_total; a.ss.g_l1 = nullptr; a.ss.g_ssim = nullptr;
+  a.ss.lambda = lambda_dssim;
+  a.ss.inv_count = (float)(1.0 / ((double)C * H * W));
+  a.ss.dx = grad_image;
+  a.ss.win = make_window();
+  const dim3 g = ssim_grid(C, H, W);
+  a.gx = (int)g.x; a.gy = (int)g.y;
+  a.nssim = (int)ssim_blocks(C, H, W);
+  a.pa.N = N; a.pa.K = 1; a.pa.x = depth_mono; a.pa.y = depth; a.pa.variants = 2;
+  a.pa.offset = offset; a.pa.acc = acc;
+  a.sel = sel;
+  a.g_total = grad_total;
+  a.depth_weight = depth_weight;
+  a.dd = grad_depth;
+  const unsigned nb = (unsigned)(a.nssim + (N + kThreads - 1) / kThreads);
+  hipLaunchKernelGGL(view_loss_bwd_kernel, dim3(nb), dim3(kThreads), 0, (hipStream_t)stream, a);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }

@@ -150,6 +150,14 @@ def load():
         L.gsr_pearson_loss.argtypes = [_i64, _i, _p, _p, _i, _f, _p, _p, _p, _p]
         L.gsr_pearson_loss_backward.restype = _i
         L.gsr_pearson_loss_backward.argtypes = [_i64, _i, _p, _p, _i, _f, _p, _p, _p, _p, _p]
+        L.gsr_view_loss_scratch_bytes.restype = _sz
+        L.gsr_view_loss_scratch_bytes.argtypes = [_i, _i, _i]
+        L.gsr_view_loss.restype = _i
+        L.gsr_view_loss.argtypes = [_i, _i, _i, _p, _p, _f, _i64, _p, _p, _f, _f, _i, _p, _p, _p,
+                                    _p]
+        L.gsr_view_loss_backward.restype = _i
+        L.gsr_view_loss_backward.argtypes = [_i, _i, _i, _p, _p, _f, _i64, _p, _p, _f, _f, _p, _p,
+                                             _p, _p, _p]
         # include/gsr_knn.h
         L.gsr_knn_scratch_bytes.restype = _sz
         L.gsr_knn_scratch_bytes.argtypes = [_i64]

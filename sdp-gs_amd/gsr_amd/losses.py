@@ -180,8 +180,10 @@ def _give(key, buf):
 
 class _TrainViewLoss(torch.autograd.Function):
     """loss = (1 - lambda) L1 + lambda (1 - SSIM) of (image, gt) + depth_weight * the Pearson depth
-    term of (depth_mono, depth) (train.py:99-100,117-131), as ONE autograd node: two kernel
-    pairs, no intermediate autograd nodes or allocations on the steady state."""
+    term of (depth_mono, depth) (train.py:99-100,117-131), as ONE autograd node over
+    gsr_view_loss: the forward is two launches (SSIM tiles + Pearson partial sums in one grid,
+    then one reduction writing every output and the total), the backward one; no intermediate
+    autograd nodes, torch ops or allocations on the steady state."""
 
     @staticmethod
     def forward(ctx, image, depth, gt, depth_mono, lambda_dssim, depth_weight, offset):
@@ -199,55 +201,50 @@ class _TrainViewLoss(torch.autograd.Function):
         L = _lib.load()
         dev = x.device
         s = _stream(x)
-        kp = ("photo", C, H, W, dev.index, s)
-        kq = ("pearson", dev.index, s)
-        sp = _take(kp, int(L.gsr_photometric_scratch_bytes(C, H, W)), dev)
-        sq = _take(kq, int(L.gsr_pearson_scratch_bytes(1, 2)), dev)
+        kv = ("view", C, H, W, dev.index, s)
+        sv = _take(kv, int(L.gsr_view_loss_scratch_bytes(C, H, W)), dev)
         out = torch.empty(5, dtype=torch.float32, device=dev)  # loss, l1, ssim, depth term, total
+        total = torch.empty((), dtype=torch.float32, device=dev)
         need = int(image.requires_grad or depth.requires_grad)
         with torch.cuda.device(dev):
-            _check(L.gsr_photometric_loss(C, H, W, x.data_ptr(), y.data_ptr(),
-                                          float(lambda_dssim), need, out.data_ptr(),
-                                          sp.data_ptr(), s), "gsr_photometric_loss")
-            _check(L.gsr_pearson_loss(N, 1, m.data_ptr(), d.data_ptr(), 2, float(offset), None,
-                                      out.data_ptr() + 12, sq.data_ptr(), s), "gsr_pearson_loss")
-        total = torch.add(out[0], out[3], alpha=float(depth_weight))
+            _check(L.gsr_view_loss(C, H, W, x.data_ptr(), y.data_ptr(), float(lambda_dssim), N,
+                                   d.data_ptr(), m.data_ptr(), float(offset), float(depth_weight),
+                                   need, out.data_ptr(), total.data_ptr(), sv.data_ptr(), s),
+                   "gsr_view_loss")
         if need:
             ctx.save_for_backward(x, y, d, m)
-            ctx.bufs = (kp, sp, kq, sq)
+            ctx.bufs = (kv, sv)
             ctx.args = (float(lambda_dssim), float(depth_weight), float(offset))
             ctx.dshape = depth.shape
         else:
-            _give(kp, sp)
-            _give(kq, sq)
+            _give(kv, sv)
         ctx.mark_non_differentiable(out)
+        ctx.set_materialize_grads(False)  # `out` never gets a gradient: no zero-filled tensor
         return total, out
 
     @staticmethod
     def backward(ctx, g_total, g_out):
         x, y, d, m = ctx.saved_tensors
-        kp, sp, kq, sq = ctx.bufs
+        kv, sv = ctx.bufs
         lam, w, offset = ctx.args
         C, H, W = x.shape
+        if g_total is None:
+            _give(kv, sv)
+            return None, None, None, None, None, None, None
         L = _lib.load()
         g = g_total.reshape(1).contiguous().float()
-        gq = g * w
-        dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
-        dd = torch.empty_like(d) if ctx.needs_input_grad[1] else None
+        dx = torch.empty_like(x)
+        dd = torch.empty_like(d)
         s = _stream(x)
         with torch.cuda.device(x.device):
-            if dx is not None:
-                _check(L.gsr_photometric_loss_backward(C, H, W, x.data_ptr(), y.data_ptr(), lam,
-                                                       g.data_ptr(), None, None, dx.data_ptr(),
-                                                       sp.data_ptr(), s),
-                       "gsr_photometric_loss_backward")
-            if dd is not None:
-                _check(L.gsr_pearson_loss_backward(d.numel(), 1, m.data_ptr(), d.data_ptr(), 2,
-                                                   offset, gq.data_ptr(), dd.data_ptr(), None,
-                                                   sq.data_ptr(), s), "gsr_pearson_loss_backward")
-        _give(kp, sp)
-        _give(kq, sq)
-        return (dx, None if dd is None else dd.view(ctx.dshape), None, None, None, None, None)
+            _check(L.gsr_view_loss_backward(C, H, W, x.data_ptr(), y.data_ptr(), lam, d.numel(),
+                                            d.data_ptr(), m.data_ptr(), offset, w, g.data_ptr(),
+                                            dx.data_ptr(), dd.data_ptr(), sv.data_ptr(), s),
+                   "gsr_view_loss_backward")
+        _give(kv, sv)
+        return (dx if ctx.needs_input_grad[0] else None,
+                dd.view(ctx.dshape) if ctx.needs_input_grad[1] else None,
+                None, None, None, None, None)
 
 
 def train_view_loss(image, depth, gt_image, depth_mono, lambda_dssim=0.2, depth_weight=0.05,
