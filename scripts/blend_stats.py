@@ -36,6 +36,7 @@ R = dgr.LAST_STATS["num_rendered"]
 print(f"R={R} waves={waves}")
 print(f"fwd: list/wave={v[0]/waves:.1f} evaluated/wave={v[1]/waves:.1f} contrib-entries/wave={v[2]/waves:.1f} "
       f"lanes/contrib-entry={v[3]/max(v[2],1):.1f}")
+print(f"bwd imbalance: busiest-wave entries x4 / all entries = {v[10]/max(v[9],1):.3f}")
 print(f"bwd: list/wave={v[4]/waves:.1f} evaluated/wave={4*v[5]/waves:.1f} contrib-entries/wave={v[6]/waves:.1f} "
       f"lanes/contrib-entry={v[7]/max(v[6],1):.1f}")
 if os.environ.get("GSR_BLOCK_LISTS", "1") != "0":

@@ -530,6 +530,11 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
     __syncthreads();
     const uint32_t nlist = build_wave_list(s_mask, s_list[wid], cnt, wid, lane);
     BLEND_STAT(4, nlist);
+#if GSR_BLEND_STATS
+    uint32_t ncw = 0;  // this wave's contributing entries in the batch (imbalance statistic)
+    __shared__ uint32_t s_maxc;
+    if (threadIdx.x == 0) s_maxc = 0;
+#endif
     // Four list entries per group: the cheap per-pair test (power, G, alpha) of all four is
     // evaluated first (independent work), then the entries are replayed in list order.
     for (uint32_t k0 = 0; k0 < nlist; k0 += GROUP) {
@@ -578,6 +583,9 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
       if (cmask == 0ull) continue;  // wave-uniform skip
       BLEND_STAT(6, 1);
       BLEND_STAT(7, __popcll(cmask));
+#if GSR_BLEND_STATS
+      ncw++;
+#endif
       const uint32_t j = (packed >> (8 * u)) & 0xffu;
       // Branch-free: a lane whose pixel does not take this splat runs the same arithmetic with
       // G = alpha = 0, which makes every gradient term exactly zero and T / (1 - 0) == T; its
@@ -654,7 +662,15 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
 #endif
     }
     }
+#if GSR_BLEND_STATS
+    if ((threadIdx.x & 63) == 0) atomicMax(&s_maxc, ncw);
+#endif
     __syncthreads();
+#if GSR_BLEND_STATS
+    // [9] sum over waves of contributing entries, [10] 4 x the batch's busiest wave's
+    BLEND_STAT(9, ncw);
+    if (threadIdx.x == 0) atomicAdd(&g_blend_stats[10], 4ull * s_maxc);
+#endif
     // moments -> the reference's dL/dmean2D (NDC-scaled) and dL/dconic, once per (splat, tile)
     if (threadIdx.x < cnt) {
       const float4 r0 = s_r0[threadIdx.x];
