@@ -51,7 +51,7 @@ class ViewPipeline:
 
     def run(self, items: Iterable[T], fn: Callable[[T], R], model=None,
             campos_of: Callable[[T], torch.Tensor] = lambda cam: cam.camera_center,
-            reducer=None) -> List[R]:
+            reducer=None, bwd: Optional[Callable[[R], R]] = None, lag: int = 1) -> List[R]:
         """Call fn(item) for every item, item i issued on stream i mod depth.  fn should do a
         view's render + backward and return host values (or tensors it no longer needs on the
         device): tensors created on a side stream and used after run() on the main stream need
@@ -64,7 +64,12 @@ class ViewPipeline:
         step's gradient all-reduce is overlapped with the end of the step -- the non-SH
         gradients (final once the last view's backward is done) are reduced while the deferred
         SH gradients are flushed in bucket-sized row slices, each slice reduced as soon as it is
-        flushed.  The reduction is complete (on the current stream) when run() returns."""
+        flushed.  The reduction is complete (on the current stream) when run() returns.
+
+        bwd: split views -- fn(item) does a view's forward and returns what bwd needs, bwd(that)
+        its backward (same stream); view i's backward is issued after view i + lag's forward
+        (software-pipelined issue: the next view's latency-bound binning is queued before this
+        view's full-chip backward blend).  Returns bwd's results."""
         import diff_gaussian_rasterization as dgr
         items = list(items)
         main = torch.cuda.current_stream(self.device)
@@ -99,6 +104,14 @@ class ViewPipeline:
                 s = streams[i % self.depth]
                 with torch.cuda.stream(s):
                     out.append(fn(it))
+                j = i - lag
+                if bwd is not None and j >= 0:
+                    with torch.cuda.stream(streams[j % self.depth]):
+                        out[j] = bwd(out[j])
+            if bwd is not None:
+                for j in range(max(0, len(items) - lag), len(items)):
+                    with torch.cuda.stream(streams[j % self.depth]):
+                        out[j] = bwd(out[j])
             for s in self.side:
                 main.wait_stream(s)
             if reducer is not None:  # every view's backward is done: the non-SH grads are final

@@ -115,10 +115,13 @@ def train_step_views(model, cams: Sequence, gt_images: Sequence[torch.Tensor],
         model.optimizer.zero_grad(set_to_none=True)
     gts = {id(c): (g, d) for c, g, d in zip(cams, gt_images, depth_monos)}
 
-    def one(cam):
+    def forward(cam):
         pkg = render(cam, model, pipe, bg, args)
         gt, dm = gts[id(cam)]
-        loss = _view_loss(pkg, gt, dm, args)
+        return pkg, _view_loss(pkg, gt, dm, args)
+
+    def backward(fw):
+        pkg, loss = fw
         loss.backward()
         with torch.no_grad():
             if iteration < args.densify_until_iter:
@@ -126,7 +129,8 @@ def train_step_views(model, cams: Sequence, gt_images: Sequence[torch.Tensor],
                                                  pkg["visibility_filter"])
         return loss.detach()
 
-    losses = pipeline.run(cams, one, model=model, reducer=reducer)
+    # view i's backward is issued after view i + 1's forward (ViewPipeline.run(bwd=, lag=1))
+    losses = pipeline.run(cams, forward, model=model, reducer=reducer, bwd=backward, lag=1)
     with torch.no_grad():
         if _densify_due(iteration, args):
             allreduce_densification_stats(model.xyz_gradient_accum, model.denom,

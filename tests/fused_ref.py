@@ -59,9 +59,10 @@ def kernel_activations(m):
     return op, sc, rot
 
 
-def run_bench_path(m, cams, grads, streams=3, defer_sh=True, precolor=True):
+def run_bench_path(m, cams, grads, streams=3, defer_sh=True, precolor=True, lag=1):
     """bench.py's step on `cams`: per view render() + backward of the fixed upstream grads
-    (image, depth, feature), grad-into-leaves, ViewPipeline over `streams` HIP streams.  Returns
+    (image, depth, feature), grad-into-leaves, ViewPipeline over `streams` HIP streams, view i's
+    backward issued after view i + lag's forward (bench.py --lag, default 1; 0 = together).  Returns
     (per-view numpy dicts of the images, radii and screen-space gradient, leaf grads float64)."""
     import diff_gaussian_rasterization as dgr
     from gaussian_renderer import render
@@ -74,14 +75,19 @@ def run_bench_path(m, cams, grads, streams=3, defer_sh=True, precolor=True):
             getattr(m, n).grad = None
         vp = ViewPipeline(m._xyz.device, depth=streams, defer_sh=defer_sh, precolor=precolor)
 
-        def one(cam):
-            pkg = render(cam, m, Pipe(), bg, Opt())
+        def fwd(cam):
+            return render(cam, m, Pipe(), bg, Opt())
+
+        def bwd(pkg):
             torch.autograd.backward([pkg["render"], pkg["depth"], pkg["feature"]], list(grads))
             out = {k: pkg[k].detach().clone() for k in IMAGES + ("radii",)}
             out["means2D"] = pkg["viewspace_points"].grad.detach().clone()
             return out
 
-        outs = vp.run(cams, one, model=m)
+        if lag > 0:
+            outs = vp.run(cams, fwd, model=m, bwd=bwd, lag=lag)
+        else:
+            outs = vp.run(cams, lambda cam: bwd(fwd(cam)), model=m)
         torch.cuda.synchronize()
     finally:
         dgr.grad_into_leaves(prev)

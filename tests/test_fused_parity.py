@@ -37,6 +37,9 @@ STATS = os.path.join(ROOT, "gpurun_out", "parity_stats.jsonl")
 CASES = {
     "small_6views_3streams": dict(P=20_000, W=200, H=150, views=6, streams=3, seed=5, deg=3),
     "small_deg1_2streams": dict(P=20_000, W=200, H=150, views=4, streams=2, seed=6, deg=1),
+    # each view's forward and backward issued together (bench.py --lag 0); the others lag by 1
+    "small_6views_3streams_lag0": dict(P=20_000, W=200, H=150, views=6, streams=3, seed=7,
+                                       deg=3, lag=0),
     "cfg2_100k_800x800": dict(P=100_000, W=800, H=800, views=3, streams=3, seed=0, deg=3),
     "cfg3_1m_1008x756": dict(P=1_000_000, W=1008, H=756, views=3, streams=3, seed=0, deg=3),
     "cfg5_5m_1920x1080": dict(P=5_000_000, W=1920, H=1080, views=2, streams=2, seed=0, deg=3),
@@ -76,7 +79,7 @@ def test_benchmarked_path_matches_oracle(case):
     cams = [x.to("cuda") for x in make_cameras(c["views"], c["W"], c["H"], seed=c["seed"])]
     grads = upstream_grads(c["H"], c["W"], seed=1, device="cuda")
     act = kernel_activations(m)
-    vg, gg = run_bench_path(m, cams, grads, streams=c["streams"])
+    vg, gg = run_bench_path(m, cams, grads, streams=c["streams"], lag=c.get("lag", 1))
     _progress(f"[{case}] GPU path done")
     vo, go = run_oracle_path(m, cams, grads, act, progress=lambda s: _progress(f"[{case}] {s}"))
     st = compare(case, vg, vo, gg, go, STATS)
