@@ -2,7 +2,7 @@
 """Per-step wall times of the headline step (bench.py's workload: 1M Gaussians, 6 views at
 1008x756, 3 view streams, grad-into-leaves, deferred SH, colour pre-pass), each step bracketed by
 torch.cuda.synchronize(): the distribution shows whether a slow bench run is slow throughout or
-has a few stalled steps (host scheduling).  usage: step_times.py [steps] [lag]"""
+has a few stalled steps (host scheduling).  usage: step_times.py [steps] [lag] [streams]"""
 import os
 import statistics
 import sys
@@ -22,13 +22,14 @@ from gsr_amd.synthetic import make_cameras, make_gaussians, upstream_grads  # no
 
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 40
 lag = int(sys.argv[2]) if len(sys.argv) > 2 else 0
+depth = int(sys.argv[3]) if len(sys.argv) > 3 else 3
 dgr.grad_into_leaves(True)
 dev = torch.device("cuda", 0)
 model = SplatModel(make_gaussians(1_000_000, sh_degree=3, seed=0), device=dev)
 cams = [c.to(dev) for c in make_cameras(6, 1008, 756, seed=0)]
 dimg, ddep, dfeat = upstream_grads(756, 1008, seed=1, device=dev)
 bg = torch.zeros(3, device=dev)
-views = ViewPipeline(dev, depth=3)
+views = ViewPipeline(dev, depth=depth)
 
 
 def fwd(cam):
@@ -58,7 +59,7 @@ for _ in range(steps):
     torch.cuda.synchronize()
     ts.append(1000.0 * (time.perf_counter() - t0))
 ts_sorted = sorted(ts)
-print(f"lag {lag}: median {statistics.median(ts):.3f} ms  min {ts_sorted[0]:.3f}  "
+print(f"lag {lag} streams {depth}: median {statistics.median(ts):.3f} ms  min {ts_sorted[0]:.3f}  "
       f"p90 {ts_sorted[int(0.9 * len(ts)) - 1]:.3f}  max {ts_sorted[-1]:.3f}  "
       f"views/s at median {6000.0 / statistics.median(ts):.0f}")
 print("steps:", " ".join(f"{t:.2f}" for t in ts))
