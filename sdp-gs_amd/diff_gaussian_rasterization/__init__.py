@@ -119,7 +119,7 @@ class _RasterizeGaussians(torch.autograd.Function):
         holder = _lib.BufferHolder(dev)
         L = _lib.load()
         nr = _lib.ctypes.c_int(0)
-        stream = torch.cuda.current_stream(dev).cuda_stream
+        stream = _lib.raw_stream(dev)
         args = (P, M, _ptr(bg), _ptr(m3), _ptr(col), _ptr(op), _ptr(sc), _ptr(rot),
                 float(rs.scale_modifier), _ptr(cov), _ptr(view), _ptr(proj), float(rs.tanfovx),
                 float(rs.tanfovy), H, W, _ptr(shs), int(rs.sh_degree), _ptr(campos),
@@ -128,7 +128,7 @@ class _RasterizeGaussians(torch.autograd.Function):
                 _lib.ctypes.byref(nr), _lib.alloc_callback(), holder.key, stream,
                 _debug_flags(rs.debug))
         try:
-            with torch.cuda.device(dev):
+            with _lib.on_device(dev):
                 rc = L.gsr_rasterize_gaussians(*args)
             _lib.check(rc)
         except Exception:
@@ -205,7 +205,7 @@ class _RasterizeGaussians(torch.autograd.Function):
         d_lfp = torch.empty((P, 3), **fopts) if lfp is not None else None
 
         L = _lib.load()
-        stream = torch.cuda.current_stream(dev).cuda_stream
+        stream = _lib.raw_stream(dev)
         args = (P, M, ctx.num_rendered, _ptr(bg), _ptr(m3), _ptr(radii), _ptr(col), _ptr(sc),
                 _ptr(rot), float(rs.scale_modifier), _ptr(cov), _ptr(view), _ptr(proj),
                 float(rs.tanfovx), float(rs.tanfovy), H, W, _ptr(dcol), _ptr(ddep), _ptr(dalp),
@@ -216,7 +216,7 @@ class _RasterizeGaussians(torch.autograd.Function):
                 _ptr(d_sh), _ptr(d_sc), _ptr(d_rot), _ptr(d_shl), _ptr(d_lfp), stream,
                 ctx.gsr_flags)
         try:
-            with torch.cuda.device(dev):
+            with _lib.on_device(dev):
                 rc = L.gsr_rasterize_gaussians_backward(*args)
             _lib.check(rc)
         except Exception:
@@ -286,10 +286,10 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
         holder = _lib.BufferHolder(dev)
         L = _lib.load()
         nr = _lib.ctypes.c_int(0)
-        stream = torch.cuda.current_stream(dev).cuda_stream
+        stream = _lib.raw_stream(dev)
         pre = _precolor_lookup(dev, campos, m3, dc, rest, int(rs.sh_degree), M)
         try:
-            with torch.cuda.device(dev):
+            with _lib.on_device(dev):
                 head = (P, M, _ptr(bg), _ptr(m3), _ptr(dc), _ptr(rest), _ptr(op), _ptr(sc),
                         _ptr(rot), float(rs.scale_modifier), _ptr(view), _ptr(proj),
                         float(rs.tanfovx), float(rs.tanfovy), H, W, int(rs.sh_degree),
@@ -411,7 +411,7 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
         stream = cur.cuda_stream
         if into_leaves:
             _order_leaf_grads(dev, cur)
-        with torch.cuda.device(dev):
+        with _lib.on_device(dev):
             rc = L.gsr_rasterize_gaussians_fused_backward_deferred(
                 P, M, ctx.num_rendered, _ptr(bg), _ptr(m3), _ptr(radii), _ptr(dc), _ptr(rest),
                 _ptr(op), _ptr(sc), _ptr(rot), float(rs.scale_modifier), _ptr(view), _ptr(proj),
@@ -503,12 +503,12 @@ class ShPrecolor:
         n = len(cams)
         if n and P:
             arr = lambda xs: (_lib.ctypes.c_void_p * n)(*[x.data_ptr() for x in xs])  # noqa: E731
-            with torch.cuda.device(self.device):
+            with _lib.on_device(self.device):
                 rc = _lib.load().gsr_sh_precolor(
                     P, self.M, int(degree), _ptr(means3D.contiguous()), _ptr(features_dc),
                     _ptr(features_rest), n, arr(cams), arr([b[0] for b in bufs]),
                     arr([b[1] for b in bufs]), arr([b[2] for b in bufs]),
-                    torch.cuda.current_stream(self.device).cuda_stream)
+                    _lib.raw_stream(self.device))
             _lib.check(rc)
         for c, b in zip(cams, bufs):
             self.views[c.data_ptr()] = b
@@ -599,7 +599,7 @@ class ShGradDeferral:
         for a in range(0, P, step):  # row slices: the kernel is per Gaussian, pointers offset
             b = min(P, a + step)
             rgbs = (_lib.ctypes.c_void_p * n)(*[v[0].data_ptr() + 12 * a for v in self.views])
-            with torch.cuda.device(self.device):
+            with _lib.on_device(self.device):
                 rc = L.gsr_sh_grad_flush(b - a, M, degree, _ptr(m3) + 12 * a, n, camp, rgbs,
                                          _ptr(dc.grad) + 12 * a,
                                          (_ptr(rest.grad) + 4 * rest_w * a)
@@ -704,8 +704,8 @@ def mark_visible(positions, viewmatrix, projmatrix):
     P = int(m3.shape[0])
     present = torch.zeros((P,), dtype=torch.bool, device=dev)
     if P:
-        with torch.cuda.device(dev):
+        with _lib.on_device(dev):
             _lib.check(_lib.load().gsr_mark_visible(P, _ptr(m3), _ptr(view), _ptr(proj),
                                                    _ptr(present),
-                                                   torch.cuda.current_stream(dev).cuda_stream))
+                                                   _lib.raw_stream(dev)))
     return present

@@ -53,7 +53,7 @@ def _cuda(*ts):
 
 
 def _stream(dev):
-    return torch.cuda.current_stream(dev).cuda_stream
+    return _lib.raw_stream(dev)
 
 
 def _ptr(t):
@@ -76,7 +76,7 @@ def select_rows(flags: torch.Tensor, mask: int, want: int):
     count = torch.empty(1, dtype=torch.int32, device=flags.device)
     scratch = torch.empty(max(int(L.gsr_select_scratch_bytes(n)), 1), dtype=torch.uint8,
                           device=flags.device)
-    with torch.cuda.device(flags.device):
+    with _lib.on_device(flags.device):
         _check(L.gsr_select_rows(n, _ptr(flags), mask, want, _ptr(index), _ptr(count),
                                  _ptr(scratch), _stream(flags.device)), "gsr_select_rows")
     return index, count
@@ -101,7 +101,7 @@ def compact_rows(arrays, n_old: int, index, n_out: int):
             _cuda(s, e, d)
             for t in (s, e, d):
                 assert t is None or (t.is_contiguous() and t.device == dev)
-        with torch.cuda.device(dev):
+        with _lib.on_device(dev):
             _check(L.gsr_compact_rows(n, src, extra, dst, rb, fill, n_old, _ptr(index), n_out,
                                       _stream(dev)), "gsr_compact_rows")
 
@@ -119,7 +119,7 @@ def classify(self, grad_accum, denom, grad_threshold, scale_limit, min_opacity=f
     flags = torch.empty(P, dtype=torch.uint8, device=dev)
     sc, op = self._scaling.detach(), self._opacity.detach()
     assert sc.is_contiguous() and op.is_contiguous() and sc.numel() == 3 * P and op.numel() == P
-    with torch.cuda.device(dev):
+    with _lib.on_device(dev):
         _check(_lib.load().gsr_densify_classify(
             P, _ptr(grad_accum), _ptr(denom), _ptr(sc), _ptr(op), float(grad_threshold),
             float(scale_limit), float(min_opacity), int(big_limit is not None),
@@ -153,7 +153,7 @@ def _stats(self, grad, radii, filt, with_radii, with_grad):
         # the statistics are read-modify-written without atomics: views on other streams
         # (gsr_amd.pipeline.ViewPipeline) add theirs in issue order, as train.py does per view
         stream.wait_event(prev[0])
-    with torch.cuda.device(dev):
+    with _lib.on_device(dev):
         _check(_lib.load().gsr_densify_stats(
             P, _ptr(grad) if with_grad else None, grad.stride(0) if with_grad else 0,
             _ptr(radii), _ptr(filt), _ptr(self.max_radii2D) if with_radii else None,

@@ -23,7 +23,7 @@ from . import _lib
 
 
 def _stream(t):
-    return torch.cuda.current_stream(t.device).cuda_stream
+    return _lib.raw_stream(t.device)
 
 
 def _check(rc, what):
@@ -59,7 +59,7 @@ class _Photometric(torch.autograd.Function):
                               device=x.device)
         out = torch.empty(3, dtype=torch.float32, device=x.device)
         need = int(image.requires_grad)
-        with torch.cuda.device(x.device):
+        with _lib.on_device(x.device):
             _check(L.gsr_photometric_loss(C, H, W, x.data_ptr(), y.data_ptr(),
                                           float(lambda_dssim), need, out.data_ptr(),
                                           scratch.data_ptr(), _stream(x)), "gsr_photometric_loss")
@@ -74,7 +74,7 @@ class _Photometric(torch.autograd.Function):
         C, H, W = x.shape
         g = g.contiguous()
         dx = torch.empty_like(x)
-        with torch.cuda.device(x.device):
+        with _lib.on_device(x.device):
             _check(_lib.load().gsr_photometric_loss_backward(
                 C, H, W, x.data_ptr(), y.data_ptr(), ctx.lam, g.data_ptr(), g.data_ptr() + 4,
                 g.data_ptr() + 8, dx.data_ptr(), ctx.scratch.data_ptr(), _stream(x)),
@@ -118,7 +118,7 @@ class _Pearson(torch.autograd.Function):
                               device=xs.device)
         r = torch.empty(variants * K, dtype=torch.float32, device=xs.device)
         loss = torch.empty(K, dtype=torch.float32, device=xs.device)
-        with torch.cuda.device(xs.device):
+        with _lib.on_device(xs.device):
             _check(L.gsr_pearson_loss(N, K, xs.data_ptr(), ys.data_ptr(), variants, float(offset),
                                       r.data_ptr(), loss.data_ptr(), scratch.data_ptr(),
                                       _stream(xs)), "gsr_pearson_loss")
@@ -140,7 +140,7 @@ class _Pearson(torch.autograd.Function):
         dy = torch.empty_like(ys) if need_y else None
         if need_x and ctx.variants != 1:
             raise ValueError("depth_pearson_loss: gradients flow to the rendered depth only")
-        with torch.cuda.device(xs.device):
+        with _lib.on_device(xs.device):
             _check(_lib.load().gsr_pearson_loss_backward(
                 N, K, xs.data_ptr(), ys.data_ptr(), ctx.variants, float(ctx.offset), g.data_ptr(),
                 _ptr(dy), _ptr(dx), ctx.scratch.data_ptr(), _stream(xs)),
@@ -206,7 +206,7 @@ class _TrainViewLoss(torch.autograd.Function):
         out = torch.empty(5, dtype=torch.float32, device=dev)  # loss, l1, ssim, depth term, total
         total = torch.empty((), dtype=torch.float32, device=dev)
         need = int(image.requires_grad or depth.requires_grad)
-        with torch.cuda.device(dev):
+        with _lib.on_device(dev):
             _check(L.gsr_view_loss(C, H, W, x.data_ptr(), y.data_ptr(), float(lambda_dssim), N,
                                    d.data_ptr(), m.data_ptr(), float(offset), float(depth_weight),
                                    need, out.data_ptr(), total.data_ptr(), sv.data_ptr(), s),
@@ -236,7 +236,7 @@ class _TrainViewLoss(torch.autograd.Function):
         dx = torch.empty_like(x)
         dd = torch.empty_like(d)
         s = _stream(x)
-        with torch.cuda.device(x.device):
+        with _lib.on_device(x.device):
             _check(L.gsr_view_loss_backward(C, H, W, x.data_ptr(), y.data_ptr(), lam, d.numel(),
                                             d.data_ptr(), m.data_ptr(), offset, w, g.data_ptr(),
                                             dx.data_ptr(), dd.data_ptr(), sv.data_ptr(), s),

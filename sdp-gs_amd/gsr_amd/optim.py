@@ -63,7 +63,7 @@ class FusedAdam(torch.optim.Adam):
                      float(state["step"])))
         L = _lib.load()
         for (dev, beta1, beta2, eps), items in batches.items():
-            stream = torch.cuda.current_stream(dev).cuda_stream
+            stream = _lib.raw_stream(dev)
             for c in range(0, len(items), MAX_TENSORS):
                 chunk = items[c:c + MAX_TENSORS]
                 n = len(chunk)
@@ -72,7 +72,7 @@ class FusedAdam(torch.optim.Adam):
                 lr = (ctypes.c_double * n)(*[it[4] for it in chunk])
                 wd = (ctypes.c_double * n)(*[it[5] for it in chunk])
                 steps = (ctypes.c_double * n)(*[it[6] for it in chunk])
-                with torch.cuda.device(dev):
+                with _lib.on_device(dev):
                     rc = L.gsr_adam_step(n, ptrs[0], ptrs[1], ptrs[2], ptrs[3], numel, lr, wd,
                                          steps, beta1, beta2, eps, stream)
                 if rc != 0:

@@ -29,6 +29,8 @@ from typing import Callable, Iterable, List, Optional, TypeVar
 
 import torch
 
+from . import _lib
+
 T = TypeVar("T")
 R = TypeVar("R")
 
@@ -102,15 +104,15 @@ class ViewPipeline:
         with pre, defer:  # defer's exit: the SH gradients of all views, after the join
             for i, it in enumerate(items):
                 s = streams[i % self.depth]
-                with torch.cuda.stream(s):
+                with _lib.on_stream(s):
                     out.append(fn(it))
                 j = i - lag
                 if bwd is not None and j >= 0:
-                    with torch.cuda.stream(streams[j % self.depth]):
+                    with _lib.on_stream(streams[j % self.depth]):
                         out[j] = bwd(out[j])
             if bwd is not None:
                 for j in range(max(0, len(items) - lag), len(items)):
-                    with torch.cuda.stream(streams[j % self.depth]):
+                    with _lib.on_stream(streams[j % self.depth]):
                         out[j] = bwd(out[j])
             for s in self.side:
                 main.wait_stream(s)
