@@ -54,7 +54,14 @@ def main():
         min((1 - loss_ref.pearson_corrcoef(m, d)),
             (1 - loss_ref.pearson_corrcoef(1 / (-m + 200), d))).backward()
 
+    xd = depth.detach().clone().requires_grad_(True)
+
+    def ours_view():
+        tot, _ = losses.train_view_loss(x, xd, gt, mono, 0.2, 0.05)
+        tot.backward()
+
     out = {"bench": "losses", "shape": [3, H, W],
+           "train_view_loss_fwd_bwd_ms": round(_ms(ours_view), 4),
            "photometric_fwd_bwd_ms": round(_ms(ours_photo), 4),
            "photometric_ref_ms": round(_ms(ref_photo), 4),
            "depth_pearson_fwd_bwd_ms": round(_ms(ours_depth), 4),

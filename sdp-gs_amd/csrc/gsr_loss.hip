@@ -8,8 +8,8 @@
 //   depth: 1 - pearson_corrcoef(...) (torchmetrics), min over two variants      (train.py:126-129)
 //
 // SSIM here: one tiled kernel per pass instead of five convolutions + ~20 element-wise kernels +
-// autograd through all of them.  A workgroup owns a 32x16 output tile of one channel: both
-// images' (32+10)x(16+10) halo tiles go to LDS, a horizontal pass blurs the five moments with the
+// autograd through all of them.  A workgroup owns a 32x32 output tile of one channel: both
+// images' (32+10)x(32+10) halo tiles go to LDS, a horizontal pass blurs the five moments with the
 // separable 1-D window, a vertical pass finishes them, and the map value, |x - y| and the three
 // per-pixel backward coefficients
 //     A = dm/dmu1 - 2 mu1 dm/dsigma1^2 - mu2 dm/dsigma12,  B = dm/dsigma1^2,  C = dm/dsigma12
@@ -32,9 +32,62 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kR = 5;                 // window radius (window_size 11)
 constexpr int kW = 2 * kR + 1;
-constexpr int kTX = 32, kTY = 16;     // output tile
+#ifndef GSR_SSIM_TY
+#define GSR_SSIM_TY 32
+#endif
+constexpr int kTX = 32, kTY = GSR_SSIM_TY;  // output tile
 constexpr int kIX = kTX + 2 * kR;     // 42
-constexpr int kIY = kTY + 2 * kR;     // 26
+constexpr int kIY = kTY + 2 * kR;     // 42
+// Register blocking of the two blur passes: a thread of the horizontal pass produces kHS
+// consecutive outputs of one row from kHS + 10 inputs held in registers (one LDS read per input
+// instead of one per tap), a thread of the vertical pass kVS consecutive outputs of one column.
+// Every output still sums its 11 taps in tap order, so the blurred values are those of the
+// one-output-per-thread form.
+constexpr int kSX = 44;               // LDS row stride of the halo tiles (16-B aligned rows)
+constexpr int kHS = 8, kHN = kHS + 2 * kR;   // 18 inputs per horizontal task
+constexpr int kVS = kTY / 8, kVN = kVS + 2 * kR;  // 14 inputs per vertical task at kTY = 32
+static_assert(kIY * (kTX / kHS) <= kThreads, "one horizontal task per thread");
+static_assert(kTX * (kTY / kVS) == kThreads, "one vertical task per thread");
+
+// rows [0, kIY) x columns [0, kIX) of NP planes around (x0 - kR, y0 - kR), zero outside: every
+// load of the thread is issued before the first LDS store, so the tile's global reads overlap
+template <int NP>
+__device__ __forceinline__ void load_halo(const float* const (&src)[NP], size_t plane, int x0,
+                                          int y0, int H, int W, float (*dst)[kIY][kSX]) {
+  constexpr int kIt = (kIX * kIY + kThreads - 1) / kThreads;
+  float v[NP][kIt];
+#pragma unroll
+  for (int it = 0; it < kIt; it++) {
+    const int e = (int)threadIdx.x + it * kThreads;
+    const int r = e / kIX, q = e - r * kIX;
+    const int gy = y0 + r - kR, gx = x0 + q - kR;
+    const bool in = e < kIX * kIY && gy >= 0 && gy < H && gx >= 0 && gx < W;
+    const size_t o = in ? plane + (size_t)gy * W + gx : 0;
+#pragma unroll
+    for (int p = 0; p < NP; p++) v[p][it] = in ? src[p][o] : 0.f;
+  }
+#pragma unroll
+  for (int it = 0; it < kIt; it++) {
+    const int e = (int)threadIdx.x + it * kThreads;
+    const int r = e / kIX, q = e - r * kIX;
+    if (e < kIX * kIY)
+#pragma unroll
+      for (int p = 0; p < NP; p++) dst[p][r][q] = v[p][it];
+  }
+}
+
+// kHN consecutive floats of an LDS row starting at a multiple of 8 (16-B aligned)
+__device__ __forceinline__ void row_span(const float* row, float (&v)[kHN]) {
+  const float4* p = reinterpret_cast<const float4*>(row);
+#pragma unroll
+  for (int i = 0; i < kHN / 4; i++) {
+    const float4 t = p[i];
+    v[4 * i] = t.x; v[4 * i + 1] = t.y; v[4 * i + 2] = t.z; v[4 * i + 3] = t.w;
+  }
+  const float2 t = reinterpret_cast<const float2*>(row)[kHN / 2 - 1];
+  v[kHN - 2] = t.x;
+  v[kHN - 1] = t.y;
+}
 
 struct Window {
   float w[kW];
@@ -72,54 +125,68 @@ struct SsimArgs {
   float c1, c2;
 };
 
-// one 32x16 output tile (bx, by) of channel c; its partial sums go to parts[2 * b]
+// one 32x32 output tile (bx, by) of channel c; its partial sums go to parts[2 * b]
 __device__ __forceinline__ void ssim_fwd_tile(const SsimArgs& a, int bx, int by, int c, size_t b) {
-  __shared__ float sx[kIY][kIX], sy[kIY][kIX];
+  // the blurs and the map may contract to FMA (the reference's conv2d fixes no evaluation order;
+  // parity is against float64, tests/test_losses.py)
+#pragma clang fp contract(fast)
+  __shared__ __attribute__((aligned(16))) float sxy[2][kIY][kSX];
   __shared__ float h[5][kIY][kTX];
+  float (*sx)[kSX] = sxy[0];
+  float (*sy)[kSX] = sxy[1];
   const int x0 = bx * kTX, y0 = by * kTY;
   const size_t plane = (size_t)c * a.H * a.W;
-  for (int e = threadIdx.x; e < kIX * kIY; e += kThreads) {
-    const int r = e / kIX, q = e - r * kIX;
-    const int gy = y0 + r - kR, gx = x0 + q - kR;
-    const bool in = gy >= 0 && gy < a.H && gx >= 0 && gx < a.W;
-    const size_t o = plane + (size_t)gy * a.W + gx;
-    sx[r][q] = in ? a.x[o] : 0.f;
-    sy[r][q] = in ? a.y[o] : 0.f;
+  {
+    const float* const src[2] = {a.x, a.y};
+    load_halo<2>(src, plane, x0, y0, a.H, a.W, sxy);
   }
   __syncthreads();
-  for (int e = threadIdx.x; e < kIY * kTX; e += kThreads) {
-    const int r = e / kTX, q = e - r * kTX;
-    float m1 = 0.f, m2 = 0.f, e11 = 0.f, e22 = 0.f, e12 = 0.f;
+  if (threadIdx.x < kIY * (kTX / kHS)) {
+    const int r = (int)threadIdx.x / (kTX / kHS), q0 = ((int)threadIdx.x % (kTX / kHS)) * kHS;
+    float u[kHN], v[kHN];
+    row_span(&sx[r][q0], u);
+    row_span(&sy[r][q0], v);
 #pragma unroll
-    for (int k = 0; k < kW; k++) {
-      const float u = sx[r][q + k], v = sy[r][q + k], w = a.win.w[k];
-      m1 += w * u;
-      m2 += w * v;
-      e11 += w * (u * u);
-      e22 += w * (v * v);
-      e12 += w * (u * v);
+    for (int j = 0; j < kHS; j++) {
+      float m1 = 0.f, m2 = 0.f, e11 = 0.f, e22 = 0.f, e12 = 0.f;
+#pragma unroll
+      for (int k = 0; k < kW; k++) {
+        const float uk = u[j + k], vk = v[j + k], w = a.win.w[k];
+        m1 += w * uk;
+        m2 += w * vk;
+        e11 += w * (uk * uk);
+        e22 += w * (vk * vk);
+        e12 += w * (uk * vk);
+      }
+      h[0][r][q0 + j] = m1;
+      h[1][r][q0 + j] = m2;
+      h[2][r][q0 + j] = e11;
+      h[3][r][q0 + j] = e22;
+      h[4][r][q0 + j] = e12;
     }
-    h[0][r][q] = m1;
-    h[1][r][q] = m2;
-    h[2][r][q] = e11;
-    h[3][r][q] = e22;
-    h[4][r][q] = e12;
   }
   __syncthreads();
   float msum = 0.f, l1sum = 0.f;
-  for (int e = threadIdx.x; e < kTY * kTX; e += kThreads) {
-    const int r = e / kTX, q = e - r * kTX;
-    const int gy = y0 + r, gx = x0 + q;
+  const int q = (int)threadIdx.x % kTX, r0 = ((int)threadIdx.x / kTX) * kVS;
+  const int gx = x0 + q;
+  float col[5][kVN];
+#pragma unroll
+  for (int m = 0; m < 5; m++)
+#pragma unroll
+    for (int i = 0; i < kVN; i++) col[m][i] = h[m][r0 + i][q];
+#pragma unroll
+  for (int i = 0; i < kVS; i++) {
+    const int r = r0 + i, gy = y0 + r;
     if (gy >= a.H || gx >= a.W) continue;
     float mu1 = 0.f, mu2 = 0.f, e11 = 0.f, e22 = 0.f, e12 = 0.f;
 #pragma unroll
     for (int k = 0; k < kW; k++) {
       const float w = a.win.w[k];
-      mu1 += w * h[0][r + k][q];
-      mu2 += w * h[1][r + k][q];
-      e11 += w * h[2][r + k][q];
-      e22 += w * h[3][r + k][q];
-      e12 += w * h[4][r + k][q];
+      mu1 += w * col[0][i + k];
+      mu2 += w * col[1][i + k];
+      e11 += w * col[2][i + k];
+      e22 += w * col[3][i + k];
+      e12 += w * col[4][i + k];
     }
     // _ssim (loss_utils.py:143-162), same expression order
     const float mu1_sq = mu1 * mu1, mu2_sq = mu2 * mu2, mu1_mu2 = mu1 * mu2;
@@ -188,7 +255,8 @@ struct SsimBwdArgs {
 };
 
 __device__ __forceinline__ void ssim_bwd_tile(const SsimBwdArgs& a, int bx, int by, int c) {
-  __shared__ float s[3][kIY][kIX];
+#pragma clang fp contract(fast)
+  __shared__ __attribute__((aligned(16))) float s[3][kIY][kSX];
   __shared__ float h[3][kIY][kTX];
   const int x0 = bx * kTX, y0 = by * kTY;
   const size_t plane = (size_t)c * a.H * a.W;
@@ -196,42 +264,45 @@ __device__ __forceinline__ void ssim_bwd_tile(const SsimBwdArgs& a, int bx, int 
   const float gl = a.g_loss ? *a.g_loss : 0.f;
   const float k_ssim = (-a.lambda * gl + (a.g_ssim ? *a.g_ssim : 0.f)) * a.inv_count;
   const float k_l1 = ((1.0f - a.lambda) * gl + (a.g_l1 ? *a.g_l1 : 0.f)) * a.inv_count;
-  for (int e = threadIdx.x; e < kIX * kIY; e += kThreads) {
-    const int r = e / kIX, q = e - r * kIX;
-    const int gy = y0 + r - kR, gx = x0 + q - kR;
-    const bool in = gy >= 0 && gy < a.H && gx >= 0 && gx < a.W;
-    const size_t o = plane + (size_t)gy * a.W + gx;
-    s[0][r][q] = in ? a.A[o] : 0.f;
-    s[1][r][q] = in ? a.B[o] : 0.f;
-    s[2][r][q] = in ? a.Cc[o] : 0.f;
+  {
+    const float* const src[3] = {a.A, a.B, a.Cc};
+    load_halo<3>(src, plane, x0, y0, a.H, a.W, s);
   }
   __syncthreads();
-  for (int e = threadIdx.x; e < kIY * kTX; e += kThreads) {
-    const int r = e / kTX, q = e - r * kTX;
-    float u0 = 0.f, u1 = 0.f, u2 = 0.f;
+  if (threadIdx.x < kIY * (kTX / kHS)) {
+    const int r = (int)threadIdx.x / (kTX / kHS), q0 = ((int)threadIdx.x % (kTX / kHS)) * kHS;
 #pragma unroll
-    for (int k = 0; k < kW; k++) {
-      const float w = a.win.w[k];
-      u0 += w * s[0][r][q + k];
-      u1 += w * s[1][r][q + k];
-      u2 += w * s[2][r][q + k];
+    for (int m = 0; m < 3; m++) {
+      float v[kHN];
+      row_span(&s[m][r][q0], v);
+#pragma unroll
+      for (int j = 0; j < kHS; j++) {
+        float acc = 0.f;
+#pragma unroll
+        for (int k = 0; k < kW; k++) acc += a.win.w[k] * v[j + k];
+        h[m][r][q0 + j] = acc;
+      }
     }
-    h[0][r][q] = u0;
-    h[1][r][q] = u1;
-    h[2][r][q] = u2;
   }
   __syncthreads();
-  for (int e = threadIdx.x; e < kTY * kTX; e += kThreads) {
-    const int r = e / kTX, q = e - r * kTX;
-    const int gy = y0 + r, gx = x0 + q;
+  const int q = (int)threadIdx.x % kTX, r0 = ((int)threadIdx.x / kTX) * kVS;
+  const int gx = x0 + q;
+  float col[3][kVN];
+#pragma unroll
+  for (int m = 0; m < 3; m++)
+#pragma unroll
+    for (int i = 0; i < kVN; i++) col[m][i] = h[m][r0 + i][q];
+#pragma unroll
+  for (int i = 0; i < kVS; i++) {
+    const int gy = y0 + r0 + i;
     if (gy >= a.H || gx >= a.W) continue;
     float u0 = 0.f, u1 = 0.f, u2 = 0.f;
 #pragma unroll
     for (int k = 0; k < kW; k++) {
       const float w = a.win.w[k];
-      u0 += w * h[0][r + k][q];
-      u1 += w * h[1][r + k][q];
-      u2 += w * h[2][r + k][q];
+      u0 += w * col[0][i + k];
+      u1 += w * col[1][i + k];
+      u2 += w * col[2][i + k];
     }
     const size_t o = plane + (size_t)gy * a.W + gx;
     const float xv = a.x[o], yv = a.y[o];
@@ -453,13 +524,14 @@ __device__ void view_pearson_partial(const ViewLossArgs& a, int b) {
 }
 
 __global__ __launch_bounds__(kThreads) void view_loss_fwd_kernel(ViewLossArgs a) {
-  const int b = (int)blockIdx.x;
-  if (b < a.nssim) {
+  // the Pearson blocks come first in the grid, so they run beside the SSIM tiles, not after them
+  const int b = (int)blockIdx.x - a.npb;
+  if (b >= 0) {
     const int per = a.gx * a.gy;
     const int c = b / per, r = b - c * per;
     ssim_fwd_tile(a.ss, r % a.gx, r / a.gx, c, (size_t)b);
   } else {
-    view_pearson_partial(a, b - a.nssim);
+    view_pearson_partial(a, (int)blockIdx.x);
   }
 }
 
@@ -468,6 +540,7 @@ __global__ __launch_bounds__(kThreads) void view_loss_finish_kernel(ViewLossArgs
   __shared__ double q[kViewPearsonSums][kThreads / 64];
   // SSIM / L1 means exactly as ssim_reduce_kernel
   double m = 0.0, l = 0.0;
+#pragma unroll 8
   for (int i = threadIdx.x; i < a.nssim; i += kThreads) {
     m += (double)a.ss.parts[2 * i];
     l += (double)a.ss.parts[2 * i + 1];
@@ -484,6 +557,7 @@ __global__ __launch_bounds__(kThreads) void view_loss_finish_kernel(ViewLossArgs
   }
   // Pearson sums over the partial blocks, fixed order
   double t[kViewPearsonSums] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll 4
   for (int i = threadIdx.x; i < a.npb; i += kThreads)
 #pragma unroll
     for (int j = 0; j < kViewPearsonSums; j++) t[j] += a.pparts[(size_t)i * kViewPearsonSums + j];
@@ -534,6 +608,7 @@ __global__ __launch_bounds__(kThreads) void view_loss_finish_kernel(ViewLossArgs
 struct ViewLossBwdArgs {
   SsimBwdArgs ss;
   int nssim, gx, gy;
+  int npe;         // Pearson element blocks, first in the grid
   PearsonArgs pa;  // N, K = 1, x = mono, y = depth, variants = 2, acc
   const int32_t* sel;
   const float* g_total;
@@ -542,15 +617,15 @@ struct ViewLossBwdArgs {
 };
 
 __global__ __launch_bounds__(kThreads) void view_loss_bwd_kernel(ViewLossBwdArgs a) {
-  const int b = (int)blockIdx.x;
-  if (b < a.nssim) {
+  const int b = (int)blockIdx.x - a.npe;
+  if (b >= 0) {
     const int per = a.gx * a.gy;
     const int c = b / per, r = b - c * per;
     ssim_bwd_tile(a.ss, r % a.gx, r / a.gx, c);
     return;
   }
   // pearson_bwd_kernel's element work with grad_loss = g_total * depth_weight (as torch's g * w)
-  const int64_t i = (int64_t)(b - a.nssim) * kThreads + threadIdx.x;
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   if (i >= a.pa.N) return;
   const int v = *a.sel;
   const double* acc = a.pa.acc + (size_t)v * 8;
@@ -817,7 +892,8 @@ extern "C" int gsr_view_loss_backward(int C, int H, int W, const float* image, c
   a.g_total = grad_total;
   a.depth_weight = depth_weight;
   a.dd = grad_depth;
-  const unsigned nb = (unsigned)(a.nssim + (N + kThreads - 1) / kThreads);
+  a.npe = (int)((N + kThreads - 1) / kThreads);
+  const unsigned nb = (unsigned)(a.nssim + a.npe);
   hipLaunchKernelGGL(view_loss_bwd_kernel, dim3(nb), dim3(kThreads), 0, (hipStream_t)stream, a);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
