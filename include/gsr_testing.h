@@ -58,6 +58,10 @@ enum {
   GSR_NUM_STAGES
 };
 /* stage_mask: bit GSR_STAGE_x enables that stage; 0 disables; -1 (all bits) enables all. */
+// Host wall time (ms) the forward calls of this process spent waiting for their instance-count
+// read-back (hipEventSynchronize); reset != 0 zeroes the counter after reading it.
+double gsr_test_host_wait_ms(int reset);
+
 void gsr_profile_enable(int stage_mask);
 /* Waits for the recorded events, adds their durations into ms[GSR_NUM_STAGES] and
  * calls[GSR_NUM_STAGES] (accumulating since the last reset) and recycles the events. */

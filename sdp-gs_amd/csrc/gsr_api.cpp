@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <chrono>
 #include <cstdarg>
 #include <cstdlib>
 #include <cstdio>
@@ -147,6 +148,9 @@ int tile_bits(uint32_t ntiles) {
   if (ntiles <= 1) return 0;
   return 32 - __builtin_clz(ntiles - 1);
 }
+
+// host time spent waiting for forwards' instance-count read-backs (gsr_test_host_wait_ms)
+std::atomic<long long> g_wait_ns{0};
 
 // Pinned 16-byte landing zone for the one device->host read per forward.
 uint32_t* pinned_slot() {
@@ -490,7 +494,13 @@ static int forward_impl(int P, int M, const float* background, const float* mean
   GSR_CHECK(scan_u32(counts_sorted, nullptr, g.offsets, (size_t)P, true, g.scan_parts, stream));
   PROF_END(SCAN);
 
-  GSR_CHECK(hipEventSynchronize(ready));
+  {
+    const auto t0 = std::chrono::steady_clock::now();
+    GSR_CHECK(hipEventSynchronize(ready));
+    g_wait_ns.fetch_add((long long)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                            std::chrono::steady_clock::now() - t0).count(),
+                        std::memory_order_relaxed);
+  }
   const uint32_t R = host[1];
   if (prefiltered && host[0]) return fail(GSR_ERR_PREFILTERED,
                            "Point is filtered although prefiltered is set. This shouldn't happen!");
@@ -1007,3 +1017,8 @@ int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const
 }
 
 }  // extern "C"
+
+extern "C" double gsr_test_host_wait_ms(int reset) {
+  const long long ns = reset ? g_wait_ns.exchange(0) : g_wait_ns.load();
+  return (double)ns * 1e-6;
+}

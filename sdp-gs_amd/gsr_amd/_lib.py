@@ -250,6 +250,8 @@ def load():
         L.gsr_profile_reset.argtypes = []
         L.gsr_profile_stage_name.restype = ctypes.c_char_p
         L.gsr_profile_stage_name.argtypes = [_i]
+        L.gsr_test_host_wait_ms.restype = ctypes.c_double
+        L.gsr_test_host_wait_ms.argtypes = [_i]
         _lib = L
     return _lib
 
