@@ -39,6 +39,9 @@ print(f"fwd: list/wave={v[0]/waves:.1f} evaluated/wave={v[1]/waves:.1f} contrib-
 print(f"bwd imbalance: busiest-wave entries x4 / all entries = {v[10]/max(v[9],1):.3f}")
 print(f"bwd: list/wave={v[4]/waves:.1f} evaluated/wave={4*v[5]/waves:.1f} contrib-entries/wave={v[6]/waves:.1f} "
       f"lanes/contrib-entry={v[7]/max(v[6],1):.1f}")
+n6 = max(v[6], 1)
+print(f"bwd contributing lanes per entry: <=2 {v[11]/n6:.3f}  <=4 {v[12]/n6:.3f}  <=8 {v[13]/n6:.3f}  "
+      f"<=16 {v[14]/n6:.3f}")
 if os.environ.get("GSR_BLOCK_LISTS", "1") != "0":
     # block-list forward: [0] sum of the wave's longest group list, [1] sum of its four group
     # lists, [2] entries evaluated per group (the "fwd:" line above reads these slots)

@@ -583,6 +583,11 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
       if (cmask == 0ull) continue;  // wave-uniform skip
       BLEND_STAT(6, 1);
       BLEND_STAT(7, __popcll(cmask));
+      // contributing-lane histogram of the backward's entries: <= 2, <= 4, <= 8, <= 16 lanes
+      BLEND_STAT(11, __popcll(cmask) <= 2);
+      BLEND_STAT(12, __popcll(cmask) <= 4);
+      BLEND_STAT(13, __popcll(cmask) <= 8);
+      BLEND_STAT(14, __popcll(cmask) <= 16);
 #if GSR_BLEND_STATS
       ncw++;
 #endif
