@@ -203,8 +203,10 @@ __device__ __forceinline__ void gaussian_bwd(const BwdPreArgs& a, size_t i, floa
     const V3 dir_orig = mean - v3(a.campos[0], a.campos[1], a.campos[2]);
     if (a.dRGB_out && a.pre_jac) {  // deferred, Jacobian from the multi-view pre-pass
       put3(a.dRGB_out, i, dRGB);
-      const float* j = a.pre_jac + 9 * i;
-      const V3 jx = v3(j[0], j[1], j[2]), jy = v3(j[3], j[4], j[5]), jz = v3(j[6], j[7], j[8]);
+      const float* j = a.pre_jac + i;  // planar [9][P]
+      const size_t P = (size_t)a.P;
+      const V3 jx = v3(j[0], j[P], j[2 * P]), jy = v3(j[3 * P], j[4 * P], j[5 * P]),
+               jz = v3(j[6 * P], j[7 * P], j[8 * P]);
       const V3 dL_ddir = v3(dot3(jx, dRGB), dot3(jy, dRGB), dot3(jz, dRGB));
       dmean = dmean + dnormvdv(dir_orig, dL_ddir);
     } else if (a.dRGB_out) {  // deferred: dL/dsh = basis(dir) x dRGB is formed by the step's flush

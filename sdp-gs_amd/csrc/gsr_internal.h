@@ -218,7 +218,7 @@ struct PrecolorArgs {
   int P, M, D, nviews;
   const float *means3D, *sh_dc, *sh_rest;
   const float* campos[kShFlushMaxViewsFwd];
-  float* color[kShFlushMaxViewsFwd];     // [P,3]
+  float* color[kShFlushMaxViewsFwd];     // [3][P] (planar)
   uint8_t* clamp[kShFlushMaxViewsFwd];   // [P]
   float* jac[kShFlushMaxViewsFwd];       // [P,9]: dRGB/ddir_x, _y, _z (vec3 over the channels)
 };

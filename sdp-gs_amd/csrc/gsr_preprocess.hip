@@ -96,7 +96,8 @@ __device__ __forceinline__ uint32_t preprocess_gaussian(const PreArgs& a, int id
 
   float cr, cg, cb;
   if (a.pre_color) {  // multi-view pre-pass: the same sh_to_rgb, evaluated for all views at once
-    cr = a.pre_color[3 * idx]; cg = a.pre_color[3 * idx + 1]; cb = a.pre_color[3 * idx + 2];
+    cr = a.pre_color[idx]; cg = a.pre_color[(size_t)a.P + idx];  // planar [3][P]
+    cb = a.pre_color[2 * (size_t)a.P + idx];
     g.clamped[idx] = a.pre_clamp[idx];
   } else if (a.colors_precomp == nullptr) {
     V3 dir = p_orig - v3(a.campos[0], a.campos[1], a.campos[2]);
@@ -239,16 +240,19 @@ __global__ __launch_bounds__(kThreads) void sh_precolor_kernel(PrecolorArgs a) {
     const V3 dir = v3(dir_orig.x / len, dir_orig.y / len, dir_orig.z / len);
     uint8_t cl;
     const V3 col = sh_to_rgb(r0, r1, a.D, dir, cl);
-    float* co = a.color[v] + 3 * i;
-    co[0] = col.x; co[1] = col.y; co[2] = col.z;
+    // planar outputs ([3][P] colour, [9][P] Jacobian): every store instruction of the wave is
+    // one contiguous 256-byte run, and so is every load of the consuming preprocesses
+    const size_t P = (size_t)a.P;
+    float* co = a.color[v] + i;
+    co[0] = col.x; co[P] = col.y; co[2 * P] = col.z;
     a.clamp[v][i] = cl;
     // backward: sh_backward's Jacobian at the same normalised direction
     V3 jx, jy, jz;
     sh_dir_jacobian(c, a.D, dir, jx, jy, jz);
-    float* jo = a.jac[v] + 9 * i;
-    jo[0] = jx.x; jo[1] = jx.y; jo[2] = jx.z;
-    jo[3] = jy.x; jo[4] = jy.y; jo[5] = jy.z;
-    jo[6] = jz.x; jo[7] = jz.y; jo[8] = jz.z;
+    float* jo = a.jac[v] + i;
+    jo[0] = jx.x; jo[P] = jx.y; jo[2 * P] = jx.z;
+    jo[3 * P] = jy.x; jo[4 * P] = jy.y; jo[5 * P] = jy.z;
+    jo[6 * P] = jz.x; jo[7 * P] = jz.y; jo[8 * P] = jz.z;
   }
 }
 

@@ -482,8 +482,9 @@ class ShPrecolor:
     Outputs are identical (the same device functions, gsr_sh.h)."""
 
     def __init__(self, means3D, features_dc, features_rest, degree, campos_list, buffers=None):
-        """buffers: optional list of (colour [P,3], clamp [P] u8, Jacobian [P,9]) per camera to
-        reuse (written on the current stream, so every earlier reader must be ordered before it)."""
+        """buffers: optional list of (colour [3,P], clamp [P] u8, Jacobian [9,P]) per camera to
+        reuse (written on the current stream, so every earlier reader must be ordered before it).
+        Colour and Jacobian are planar (include/gsr.h gsr_sh_precolor)."""
         self.device = means3D.device
         self.keys = (means3D.data_ptr(), features_dc.data_ptr(),
                      features_rest.data_ptr() if features_rest is not None else 0, int(degree))
@@ -493,12 +494,12 @@ class ShPrecolor:
         self.views = {}
         cams = [_dev_f32(c, "campos", self.device) for c in campos_list]
         if buffers is not None and len(buffers) == len(cams) and all(
-                b[0].shape == (P, 3) and b[2].shape == (P, 9) for b in buffers):
+                b[0].shape == (3, P) and b[2].shape == (9, P) for b in buffers):
             bufs = list(buffers)
         else:
-            bufs = [(torch.empty((P, 3), **fopts),
+            bufs = [(torch.empty((3, P), **fopts),
                      torch.empty((P,), dtype=torch.uint8, device=self.device),
-                     torch.empty((P, 9), **fopts)) for _ in cams]
+                     torch.empty((9, P), **fopts)) for _ in cams]
         self.buffers = bufs
         n = len(cams)
         if n and P:
