@@ -220,7 +220,7 @@ struct PrecolorArgs {
   const float* campos[kShFlushMaxViewsFwd];
   float* color[kShFlushMaxViewsFwd];     // [3][P] (planar)
   uint8_t* clamp[kShFlushMaxViewsFwd];   // [P]
-  float* jac[kShFlushMaxViewsFwd];       // [P,9]: dRGB/ddir_x, _y, _z (vec3 over the channels)
+  float* jac[kShFlushMaxViewsFwd];       // [9][P] (planar): dRGB/ddir_x, _y, _z (vec3 over the channels)
 };
 hipError_t launch_sh_precolor(const PrecolorArgs& a, hipStream_t s);
 // test hook: ref = OCML expf(x), fast = splat_exp(x) (gsr_device.h), the blends' exp

@@ -204,8 +204,8 @@ __global__ __launch_bounds__(kThreads) void preprocess_kernel(PreArgs a) {
 // Multi-view colour pre-pass (gsr_amd/pipeline.py): one pass over the SH rows serves the
 // forward colour and the backward's colour Jacobian of every view of a step, instead of every
 // view's preprocess and backward preprocess reading the 192-byte rows again.  Per Gaussian and
-// view: sh_to_rgb (forward.cu:20-71, the forward's own function) -> colour [P,3] + clamp bits,
-// and sh_dir_jacobian (backward.cu:56-131) -> dRGB/ddir [P,9].  The rows go through LDS
+// view: sh_to_rgb (forward.cu:20-71, the forward's own function) -> colour [3][P] + clamp bits,
+// and sh_dir_jacobian (backward.cu:56-131) -> dRGB/ddir [9][P].  The rows go through LDS
 // (gsr_stage.h) so the global reads are coalesced 16-byte vectors.
 __global__ __launch_bounds__(kThreads) void sh_precolor_kernel(PrecolorArgs a) {
   __shared__ float4 s_sh4[kThreads * kShMaxFloats / 4];
