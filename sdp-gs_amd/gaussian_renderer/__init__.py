@@ -94,16 +94,30 @@ class _RenderPkg(dict):
         return dict(dict.items(self._fill()))
 
 
+_ZEROS = {}  # device -> zero buffer of the last shape asked for (render()'s means2D leaves)
+
+
+def _zero_leaf(xyz):
+    """A new leaf tensor (requires_grad, own .grad) whose values are zeros, like
+    torch.zeros_like(xyz, requires_grad=True), backed by a zero buffer shared by all views of the
+    same shape: the buffer is never written (the rasterizer only returns means2D's gradient)."""
+    z = _ZEROS.get(xyz.device)
+    if z is None or z.shape != xyz.shape or z.dtype != xyz.dtype:
+        z = torch.zeros_like(xyz, memory_format=torch.contiguous_format)
+        _ZEROS[xyz.device] = z
+    return z.detach().requires_grad_(True)
+
+
 def render(viewpoint_camera, pc, pipe, bg_color: torch.Tensor, opt, scaling_modifier=1.0,
            override_color=None, override_language=None):
     xyz = pc.get_xyz
     fused = _fused_eligible(pc, pipe, opt, override_color, override_language)
     if fused:
-        # the kernel never reads means2D's values, only returns its gradient: a zero leaf (one
-        # fill) stands in for the reference's zeros_like(...) + 0 non-leaf (fill + add); its
-        # .grad is the same per-view screen-space gradient
-        screenspace_points = torch.zeros_like(xyz, dtype=xyz.dtype, requires_grad=True,
-                                              device=xyz.device)
+        # the kernel never reads means2D's values, only returns its gradient: a fresh zero leaf
+        # stands in for the reference's zeros_like(...) + 0 non-leaf (fill + add); its .grad is
+        # the same per-view screen-space gradient.  The leaf is a new tensor over one cached
+        # zero buffer per device and shape, so a view costs no fill kernel.
+        screenspace_points = _zero_leaf(xyz)
     else:
         screenspace_points = torch.zeros_like(xyz, dtype=xyz.dtype, requires_grad=True,
                                               device=xyz.device) + 0
