@@ -43,6 +43,29 @@ def test_render_dict_and_grads():
     assert vs is not None and vs[:, :2].abs().sum() > 0 and torch.all(vs[:, 2] == 0)
 
 
+def test_viewspace_points_are_fresh_zero_leaves_per_view():
+    """The fused path's means2D leaves share one cached zero buffer (no fill per view): each view
+    still gets its own zero-valued leaf whose .grad holds only that view's screen-space gradient,
+    exactly what a fresh zeros_like(..., requires_grad=True) would give."""
+    render, m, cam = _setup()
+    cams = [cam] + [c.to("cuda") for c in make_cameras(2, 200, 150, seed=9)]
+    bg = torch.zeros(3, device="cuda")
+    pkgs = [render(c, m, Pipe(sh_py=False), bg, Opt()) for c in cams]
+    leaves = [p["viewspace_points"] for p in pkgs]
+    assert len({id(t) for t in leaves}) == len(leaves)
+    for t in leaves:
+        assert t.is_leaf and t.requires_grad and t.grad is None and not torch.any(t)
+    sum(p["render"].sum() for p in pkgs).backward()
+    for c, p in zip(cams, pkgs):  # each .grad equals the view rendered alone
+        m2 = SplatModel(make_gaussians(20000, seed=5), device="cuda")
+        q = render(c, m2, Pipe(sh_py=False), bg, Opt())
+        q["render"].sum().backward()
+        torch.testing.assert_close(p["viewspace_points"].grad, q["viewspace_points"].grad,
+                                   atol=1e-5 * float(q["viewspace_points"].grad.abs().max()),
+                                   rtol=0)
+    assert not torch.any(leaves[0])  # the shared buffer is never written
+
+
 def test_python_and_kernel_sh_paths_agree(monkeypatch):
     # both sides with torch's activations (the fused path's in-kernel sigmoid differs by ulps)
     monkeypatch.setenv("GSR_FUSED", "0")
