@@ -1058,7 +1058,15 @@ hipError_t launch_render_backward(const RenderBwdArgs& a, hipStream_t s) {
     const char* e = getenv("GSR_BWD_GROUP");
     return (e && atoi(e) == 1) ? 1 : 4;
   }();
-  if (a.sched == 2)  // backward work per tile ~ the replayed prefix (max n_contrib)
+  static const bool resched = [] {
+    const char* e = getenv("GSR_BWD_RESCHED");
+    return e && atoi(e) == 1;
+  }();
+  // The backward keeps the forward's heaviest-first order (by list length, still in a.order):
+  // re-ranking by the replayed prefix (max n_contrib, GSR_BWD_RESCHED=1) costs a launch and was
+  // measured slower, render_bwd 0.2361 vs 0.2324 ms at 1 stream, 3.408-3.427 vs 3.391-3.395 ms
+  // per 3-stream step
+  if (a.sched == 2 && resched)
     hipLaunchKernelGGL(tile_schedule_kernel, dim3(1), dim3(kSchedThreads), 0, s, a.ranges,
                        a.tile_last, ntiles, a.order);
 #define GSR_BWD(E, F)                                                                             \
