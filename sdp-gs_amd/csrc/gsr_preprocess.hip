@@ -27,7 +27,11 @@ constexpr int kThreads = 256;
 
 // One Gaussian; returns its tile count (0 when culled) and writes its splat record to rec[0..3]
 // (the workgroup's LDS staging row; all zero when culled: such a record is never read).
-__device__ __forceinline__ uint32_t preprocess_gaussian(const PreArgs& a, int idx, float4* rec) {
+// pm / ps / pl: this Gaussian's 3 floats of means3D / scales / sh_language (LDS-staged rows with
+// GSR_PRE_STAGE, else the global rows; ps / pl are only read when the arrays are in use)
+__device__ __forceinline__ uint32_t preprocess_gaussian(const PreArgs& a, int idx, float4* rec,
+                                                        const float* pm, const float* ps,
+                                                        const float* pl) {
 #pragma unroll
   for (int k = 0; k < 4; k++) rec[k] = make_float4(0.f, 0.f, 0.f, 0.f);
 #if GSR_PRE_HOIST
@@ -37,12 +41,12 @@ __device__ __forceinline__ uint32_t preprocess_gaussian(const PreArgs& a, int id
   float s_in0 = 0.f, s_in1 = 0.f, s_in2 = 0.f;
   if (!a.cov3D_precomp) {  // kernel-argument (uniform) test
     q_in = reinterpret_cast<const float4*>(a.rotations)[idx];
-    s_in0 = a.scales[3 * idx]; s_in1 = a.scales[3 * idx + 1]; s_in2 = a.scales[3 * idx + 2];
+    s_in0 = ps[0]; s_in1 = ps[1]; s_in2 = ps[2];
   }
   const float op_in = a.opacities[idx];
   const float conf_in = a.confidence ? a.confidence[idx] : 1.0f;
 #endif
-  const V3 p_orig = v3(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
+  const V3 p_orig = v3(pm[0], pm[1], pm[2]);
   const V3 p_view = xform_point43(p_orig, a.view);
   // in_frustum: near-plane test only (auxiliary.h:154)
   const bool near_ok = !(p_view.z <= 0.2f);
@@ -70,7 +74,7 @@ __device__ __forceinline__ uint32_t preprocess_gaussian(const PreArgs& a, int id
     float sx = s_in0, sy = s_in1, sz = s_in2;
 #else
     float4 q = reinterpret_cast<const float4*>(a.rotations)[idx];
-    float sx = a.scales[3 * idx], sy = a.scales[3 * idx + 1], sz = a.scales[3 * idx + 2];
+    float sx = ps[0], sy = ps[1], sz = ps[2];
 #endif
     if (a.fused) {  // GaussianModel activations: exp(_scaling), normalize(_rotation)
       sx = expf(sx); sy = expf(sy); sz = expf(sz);
@@ -128,9 +132,9 @@ __device__ __forceinline__ uint32_t preprocess_gaussian(const PreArgs& a, int id
     if (a.lang_precomp) {
       f0 = a.lang_precomp[3 * idx]; f1 = a.lang_precomp[3 * idx + 1]; f2 = a.lang_precomp[3 * idx + 2];
     } else if (a.sh_language) {
-      const float u0 = SH_C0 * a.sh_language[3 * idx];
-      const float u1 = SH_C0 * a.sh_language[3 * idx + 1];
-      const float u2 = SH_C0 * a.sh_language[3 * idx + 2];
+      const float u0 = SH_C0 * pl[0];
+      const float u1 = SH_C0 * pl[1];
+      const float u2 = SH_C0 * pl[2];
       const float n = sqrtf(u0 * u0 + u1 * u1 + u2 * u2);
       const float den = n + 1e-9f;
       f0 = u0 / den; f1 = u1 / den; f2 = u2 / den;
@@ -169,6 +173,21 @@ __device__ __forceinline__ uint32_t preprocess_gaussian(const PreArgs& a, int id
 // transposed through LDS at an 80-byte row stride) instead of 16-byte pieces at a 64-byte lane
 // stride.  Each workgroup also writes the sum of its tile counts (a.parts), so R = sum of the
 // partials needs one more small launch instead of a separate pass over tiles_touched.
+#ifndef GSR_PRE_STAGE
+#define GSR_PRE_STAGE 0
+#endif
+// n rows of 3 floats from g (row 0 at a 3-KB-aligned offset of the array) into LDS s
+__device__ __forceinline__ void stage_rows3(const float* __restrict__ g, int n, float* s) {
+  const int nf = 3 * n;
+  if ((reinterpret_cast<uintptr_t>(g) & 15u) == 0) {
+    const int n4 = nf >> 2;
+    const float4* g4 = reinterpret_cast<const float4*>(g);
+    for (int q = (int)threadIdx.x; q < n4; q += kThreads) reinterpret_cast<float4*>(s)[q] = g4[q];
+    for (int q = 4 * n4 + (int)threadIdx.x; q < nf; q += kThreads) s[q] = g[q];
+  } else {
+    for (int q = (int)threadIdx.x; q < nf; q += kThreads) s[q] = g[q];
+  }
+}
 constexpr int kRecStride = 5;  // float4s per LDS record row (4 + 1 pad)
 // (__launch_bounds__(256, 6), 80 VGPRs with a 12-byte spill, measured equal to the unbounded 82)
 __global__ __launch_bounds__(kThreads) void preprocess_kernel(PreArgs a) {
@@ -177,7 +196,25 @@ __global__ __launch_bounds__(kThreads) void preprocess_kernel(PreArgs a) {
   const int idx = base + (int)threadIdx.x;
   const int n = min(kThreads, a.P - base);
   side_clear(a.clear.p, a.clear.bytes, (size_t)idx, (size_t)gridDim.x * kThreads);
-  uint32_t count = idx < a.P ? preprocess_gaussian(a, idx, s_rec + threadIdx.x * kRecStride) : 0u;
+#if GSR_PRE_STAGE
+  // the [P,3] inputs (12-byte rows) enter as the workgroup's contiguous 3-KB segments in 16-byte
+  // loads instead of three 4-byte loads at a 12-byte lane stride; lane reads at a 3-dword LDS
+  // stride are bank-conflict free
+  __shared__ float s_m[3 * kThreads], s_s[3 * kThreads], s_l[3 * kThreads];
+  stage_rows3(a.means3D + 3 * (size_t)base, n, s_m);
+  const bool use_s = !a.cov3D_precomp, use_l = a.include_feature && !a.lang_precomp && a.sh_language;
+  if (use_s) stage_rows3(a.scales + 3 * (size_t)base, n, s_s);
+  if (use_l) stage_rows3(a.sh_language + 3 * (size_t)base, n, s_l);
+  __syncthreads();
+  const float* pm = s_m + 3 * threadIdx.x;
+  const float* ps = s_s + 3 * threadIdx.x;
+  const float* pl = s_l + 3 * threadIdx.x;
+#else
+  const float* pm = a.means3D + 3 * (size_t)idx;
+  const float* ps = a.scales + 3 * (size_t)idx;
+  const float* pl = a.sh_language + 3 * (size_t)idx;
+#endif
+  uint32_t count = idx < a.P ? preprocess_gaussian(a, idx, s_rec + threadIdx.x * kRecStride, pm, ps, pl) : 0u;
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) count += (uint32_t)__shfl_xor((int)count, d, 64);
   __shared__ uint32_t s_sum[kThreads / 64];
