@@ -11,7 +11,11 @@ N > 1, one bucketed SUM all-reduce of all gradients over RCCL.  Weak scaling: vi
 
     python bench.py --gpus N --steps K --warmup W
 
-Prints ONE JSON line on rank 0 (see DESIGN.md section 7 for the roofline byte model).
+Prints ONE JSON line on rank 0 (see DESIGN.md section 7 for the roofline byte model).  With
+--gpus N > 1 and no torch.distributed environment (WORLD_SIZE unset), this process starts
+`python -m torch.distributed.run --nproc-per-node N bench.py ...` as a CHILD (before anything
+touches the GPU), relays rank 0's JSON line and exits with the child's status; one rank per GPU
+over RCCL.  GSR_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs.
 """
 from __future__ import annotations
 
@@ -20,6 +24,8 @@ import json
 import math
 import os
 import platform
+import socket
+import subprocess
 import sys
 import time
 
@@ -40,6 +46,12 @@ WORKLOADS = {
     "cfg2_100k_800x800": (100_000, 800, 800, 3),
     "cfg5_5m_1920x1080": (5_000_000, 1920, 1080, 3),
 }
+
+
+# What bounds each stage (PMC in profiles/): the blends are latency / VALU
+# issue bound -- their HBM fraction (the contract's unit, still reported) is low by construction
+KERNEL_BOUND = {"render_fwd": "valu/latency", "render_bwd": "valu/latency",
+                "depth_sort": "latency", "tile_sort": "latency", "scan": "latency"}
 
 
 class Pipe:
@@ -93,6 +105,34 @@ def algorithmic_bytes(stage, P, Pv, R, T, HW, D=3, C=8, tile_passes=2, acc=True,
     }[stage]
 
 
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return int(sk.getsockname()[1])
+
+
+def launch_ranks(argv, nproc, script=None, env=None):
+    """Run `script argv` as nproc ranks of one node under torch.distributed.run, in a child
+    process (this process never initialises the GPU, so nothing is exec'ed over a HIP context).
+    Non-JSON stdout of the ranks goes to stderr; returns (exit status, rank 0's JSON line)."""
+    script = script or os.path.abspath(__file__)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={int(nproc)}", "--master-addr", "127.0.0.1", "--master-port",
+           str(_free_port()), script] + list(argv)
+    e = dict(os.environ if env is None else env)
+    e.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on these hosts
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=e, text=True)
+    line = None
+    for out in proc.stdout:
+        txt = out.strip()
+        if txt.startswith("{") and '"metric"' in txt:
+            line = txt
+        elif txt:
+            sys.stderr.write(out)
+            sys.stderr.flush()
+    return proc.wait(), line
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -105,9 +145,14 @@ def main():
     ap.add_argument("--no-stage-timing", action="store_true")
     ap.add_argument("--autograd-grads", action="store_true",
                     help="return per-view raw grads to autograd instead of adding them into .grad")
-    ap.add_argument("--streams", type=int, default=3,
+    ap.add_argument("--streams", type=int, default=0,
                     help="views of a step issued round-robin on this many HIP streams "
-                         "(gsr_amd.pipeline.ViewPipeline; 1 = strictly sequential)")
+                         "(gsr_amd.pipeline.ViewPipeline; 1 = strictly sequential).  0: 3 at one "
+                         "rank; 2 at N > 1, so that the view streams plus RCCL's stream fit the "
+                         "process's GPU_MAX_HW_QUEUES = 4 hardware queues")
+    ap.add_argument("--camera-pool", type=int, default=12,
+                    help="cameras of the scene (BASELINE config 3: a pool of 12 LLFF cameras); "
+                         "each step renders views_per_gpu x N of them, rotating through the pool")
     ap.add_argument("--no-defer-sh", action="store_true",
                     help="write the SH gradients in every view's backward instead of one flush "
                          "per step (diff_gaussian_rasterization.ShGradDeferral)")
@@ -124,6 +169,12 @@ def main():
                     help="host threads of the CPU baseline (0: OMP_NUM_THREADS or all cores)")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        rc, line = launch_ranks(sys.argv[1:], args.gpus)
+        if line is not None:
+            print(line, flush=True)
+        sys.exit(rc if rc != 0 else (0 if line is not None else 1))
+
     from gsr_amd import _lib
     from gsr_amd.model import SplatModel
     from gsr_amd.parallel import GradAllReducer, init_from_env, shard_views
@@ -137,12 +188,29 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     P, W, H, deg = WORKLOADS[args.workload]
+    # hardware-queue budget: view streams + RCCL's stream within GPU_MAX_HW_QUEUES (default 4), so
+    # a collective never shares a queue with a view's backward blend (it would serialise them)
+    hw_queues = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+    streams = args.streams or (3 if world == 1 else 2)
+    if world > 1:
+        streams = max(1, min(streams, hw_queues - 1))
 
     params = make_gaussians(P, sh_degree=deg, seed=0)
     model = SplatModel(params, device=dev)
     n_views = args.views_per_gpu * world
-    cams_all = make_cameras(n_views, W, H, seed=0)
-    my_cams = [cams_all[i].to(dev) for i in shard_views(n_views, rank, world)]
+    pool = max(args.camera_pool, n_views)
+    cams_all = make_cameras(pool, W, H, seed=0)
+    cams_dev = {}
+
+    def step_cams(k):
+        """This rank's cameras of step k: the step's n_views views rotate through the pool."""
+        ids = [(k * n_views + i) % pool for i in range(n_views)]
+        mine = [ids[i] for i in shard_views(n_views, rank, world)]
+        for c in mine:
+            if c not in cams_dev:
+                cams_dev[c] = cams_all[c].to(dev)
+        return [cams_dev[c] for c in mine]
+    my_cams = step_cams(0)
     dimg, ddep, dfeat = upstream_grads(H, W, seed=1, device=dev)
     bg = torch.zeros(3, device=dev)
     # re-reads the model's parameters every step (densification replaces them)
@@ -150,18 +218,22 @@ def main():
     pipe, opt = Pipe(), Opt()
     stats = {"R": [], "Pv": []}
     defer_sh = not args.no_defer_sh and not args.autograd_grads
-    views = ViewPipeline(dev, depth=max(1, args.streams), defer_sh=defer_sh,
-                         precolor=not args.no_precolor)
+    views = ViewPipeline(dev, depth=streams, defer_sh=defer_sh, precolor=not args.no_precolor)
+    stats["R_ref"] = []
+    step_no = [0]
 
     def one_view(cam, record):
         pkg = render(cam, model, pipe, bg, opt)
         torch.autograd.backward([pkg["render"], pkg["depth"], pkg["feature"]],
                                 [dimg, ddep, dfeat])
         if record:
-            stats["R"].append(dgr.LAST_STATS["num_rendered"])
+            stats["R"].append(dgr.LAST_STATS["num_instances"])
+            stats["R_ref"].append(dgr.LAST_STATS["num_rendered"])
             stats["Pv"].append(int(pkg["visibility_filter"].sum()))
 
     def step(record=False):
+        my_cams = step_cams(step_no[0])
+        step_no[0] += 1
         if reducer is not None:
             reducer.attach_grads()  # grads accumulate straight into the all-reduce buckets
         else:
@@ -177,19 +249,23 @@ def main():
 
     def view_forward(cam):
         pkg = render(cam, model, pipe, bg, opt)
-        pkg["num_rendered"] = dgr.LAST_STATS["num_rendered"]  # this view's, before the next
+        # this view's counts, before the next forward: instances binned / the reference's count
+        pkg["num_instances"] = dgr.LAST_STATS["num_instances"]
+        pkg["num_rendered"] = dgr.LAST_STATS["num_rendered"]
         return pkg
 
     def view_backward(pkg, record):
         torch.autograd.backward([pkg["render"], pkg["depth"], pkg["feature"]],
                                 [dimg, ddep, dfeat])
         if record:
-            stats["R"].append(pkg["num_rendered"])
+            stats["R"].append(pkg["num_instances"])
+            stats["R_ref"].append(pkg["num_rendered"])
             stats["Pv"].append(int(pkg["visibility_filter"].sum()))
 
     for _ in range(args.warmup):
         step()
-    step(record=True)  # one recorded step for the per-view statistics (not timed)
+    for _ in range(max(1, -(-pool // n_views))):  # recorded steps over the whole pool (untimed)
+        step(record=True)
     timer = _lib.StageTimer()
     # Per-stage table from one fully instrumented, untimed step (events around every stage cost
     # ~7% of a view).  The headline value comes from a clean timed region (no events: with the
@@ -241,6 +317,7 @@ def main():
     ms_per_step = 1000.0 * elapsed / args.steps
 
     R = float(np.mean(stats["R"]))
+    R_ref = float(np.mean(stats["R_ref"]))
     Pv = float(np.mean(stats["Pv"]))
     T = ((W + 15) // 16) * ((H + 15) // 16)
     HW = W * H
@@ -272,7 +349,8 @@ def main():
                 traffic = pmc["kernels"][dom].get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             pass
-        roofline = {"kernel": dom, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+        roofline = {"kernel": dom, "bound": KERNEL_BOUND.get(dom, "hbm"), "achieved": achieved,
+                    "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                     "algorithmic_bytes": kd["bytes"], "avg_ms": kd["avg_ms"],
                     "timed_region_views_per_s": round(args.steps * n_views / dom_elapsed, 3)}
@@ -302,8 +380,8 @@ def main():
 
     legs = {}
     if not args.no_extra_legs:
-        legs = extra_legs(args, model, my_cams, cams_all, views, reducer, timed_region, rank,
-                          world, dev, (P, W, H, deg), (dimg, ddep, dfeat), bg)
+        legs = extra_legs(args, model, step_cams, pool, n_views, views, reducer, timed_region,
+                          rank, world, dev, (P, W, H, deg), (dimg, ddep, dfeat), bg)
 
     if rank == 0:
         line = {
@@ -327,9 +405,16 @@ def main():
                                        else "unfused"),
                        "grad_mode": "autograd" if args.autograd_grads else "into_leaves",
                        "view_streams": views.depth,
+                       "hw_queue_budget": (f"{views.depth} view streams + 1 RCCL stream <= "
+                                           f"GPU_MAX_HW_QUEUES={hw_queues}") if world > 1 else
+                                          f"{views.depth} view streams (no collectives)",
+                       "camera_pool": pool,
                        "sh_grads": "deferred (one flush per step)" if defer_sh else "per view",
                        "sh_colour": "per view" if args.no_precolor else "multi-view pre-pass",
-                       "num_rendered_mean": int(R), "visible_mean": int(Pv), "tiles": T},
+                       # num_rendered: the reference's count (boundary return value, full
+                       # 3-sigma rectangles); instances: those binned after the exact tile cull
+                       "num_rendered_mean": int(R_ref), "instances_mean": int(R),
+                       "visible_mean": int(Pv), "tiles": T},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "kernels": kernels,
@@ -340,8 +425,8 @@ def main():
         dist.destroy_process_group()
 
 
-def extra_legs(args, model, my_cams, cams_all, views, reducer, timed_region, rank, world, dev,
-               wl, grads, bg):
+def extra_legs(args, model, step_cams, pool, n_views, views, reducer, timed_region, rank, world,
+               dev, wl, grads, bg):
     """The other ways the reference's users run this path, timed like the headline (same
     barrier / synchronize / max-over-ranks region, K steps after W warm-up steps):
 
@@ -364,7 +449,11 @@ def extra_legs(args, model, my_cams, cams_all, views, reducer, timed_region, ran
     P, W, H, deg = wl
     dimg, ddep, dfeat = grads
     out = {}
-    n_views = len(my_cams) * world
+    k_step = [0]
+
+    def next_cams():  # every leg rotates through the camera pool like the headline
+        k_step[0] += 1
+        return step_cams(k_step[0] - 1)
 
     # ---- deterministic backward: the headline step with GSR_DEBUG_DETERMINISTIC --------------
     prev_det = dgr.deterministic()
@@ -383,10 +472,11 @@ def extra_legs(args, model, my_cams, cams_all, views, reducer, timed_region, ran
             def bwd(pkg):
                 torch.autograd.backward([pkg["render"], pkg["depth"], pkg["feature"]],
                                         [dimg, ddep, dfeat])
+            cams = next_cams()
             if args.lag > 0:
-                views.run(my_cams, fwd, model=model, reducer=reducer, bwd=bwd, lag=args.lag)
+                views.run(cams, fwd, model=model, reducer=reducer, bwd=bwd, lag=args.lag)
             else:
-                views.run(my_cams, lambda cam: bwd(fwd(cam)), model=model, reducer=reducer)
+                views.run(cams, lambda cam: bwd(fwd(cam)), model=model, reducer=reducer)
         for _ in range(args.warmup):
             det_step()
         el = timed_region(lambda i: det_step())
@@ -407,7 +497,7 @@ def extra_legs(args, model, my_cams, cams_all, views, reducer, timed_region, ran
         def ref_api_step():
             for p in model.parameters():
                 p.grad = None
-            for cam in my_cams:
+            for cam in next_cams():
                 pkg = render(cam, model, Pipe(), bg, Opt())
                 torch.autograd.backward([pkg["render"], pkg["depth"], pkg["feature"]],
                                         [dimg, ddep, dfeat])
@@ -433,13 +523,16 @@ def extra_legs(args, model, my_cams, cams_all, views, reducer, timed_region, ran
     trainer.make_trainable(model, targs)
     if reducer is not None:
         reducer.attach_grads()  # the parameters are now the trainer's nn.Parameters
-    gts, monos = training_targets(len(my_cams), H, W, seed=2 + rank, device=dev)
+    # one synthetic target image + monocular depth per pool camera (Camera.uid = pool index)
+    gts, monos = training_targets(pool, H, W, seed=2, device=dev)
     extent = 2.78  # ~ the scene extent of make_gaussians (tests/test_densify.py EXTENT)
     dgr.grad_into_leaves(True)
     it = [1]  # iteration counter below densify_from_iter: no densification inside the steps
 
     def train_step():
-        trainer.train_step_views(model, my_cams, gts, monos, bg, targs, it[0], extent, views,
+        cams = next_cams()
+        trainer.train_step_views(model, cams, [gts[c.uid] for c in cams],
+                                 [monos[c.uid] for c in cams], bg, targs, it[0], extent, views,
                                  reducer=reducer)
         it[0] += 1
     for _ in range(args.warmup):
@@ -499,12 +592,12 @@ def extra_legs(args, model, my_cams, cams_all, views, reducer, timed_region, ran
     if world == 1:
         for p in model.parameters():
             p.grad = None
-        cams1 = list(my_cams)
+        cams1 = [c for k in range(max(1, -(-pool // n_views))) for c in step_cams(k)]
 
         def ref_iter(i):
-            k = i % len(cams1)
-            trainer.train_iteration(model, cams1[k], gts[k], monos[k], bg, targs, 1 + i, extent)
-        n_it = args.steps * len(cams1)
+            c = cams1[i % len(cams1)]
+            trainer.train_iteration(model, c, gts[c.uid], monos[c.uid], bg, targs, 1 + i, extent)
+        n_it = args.steps * n_views
         for i in range(args.warmup):
             ref_iter(i)
         el = timed_region(ref_iter, steps=n_it)

@@ -12,7 +12,7 @@
  *  - images are planar [C,H,W];  the 4x4 matrices are the reference's row-major tensors
  *    world_view_transform / full_proj_transform (scene/cameras.py:76-81);
  *  - all work is enqueued on `stream` (a hipStream_t, NULL = legacy default stream); the forward
- *    performs one 8-byte device->host read of the instance count (as rasterizer_impl.cu:281 does);
+ *    performs one 12-byte device->host read of the instance counts (as rasterizer_impl.cu:281 does);
  *  - scratch memory is owned by the caller: the library requests it through `alloc`, mirroring
  *    resizeFunctional (rasterize_points.cu:27-33); `which` is GSR_BUF_GEOM / _BINNING / _IMAGE.
  *    The three buffers must be handed back unchanged to the backward;
@@ -77,7 +77,11 @@ int gsr_check_forwards(int wait);
  * reference, the extended-API inputs/outputs are appended.  M = sh.size(1) (0 without SH).
  * Outputs: out_color[3,H,W] (= blend + T*bg), out_depth[1,H,W], out_alpha[1,H,W],
  * out_feature[3,H,W] (zeros unless include_feature), radii[P] (NULL -> internal),
- * *num_rendered (the reference's first return value).  With P == 0 nothing is written except
+ * *num_rendered (the reference's first return value, with its meaning: the sum over the Gaussians
+ * of the tiles in their full 3-sigma rectangles, forward.cu:255 + rasterizer_impl.cu:281; the
+ * binning buffer is sized for that many instances).  The library bins only the tiles of those
+ * rectangles where the splat can reach alpha >= 1/255 ("exact tile culling"; no
+ * output or gradient changes) -- gsr_last_forward_instances() gives that count.  With P == 0 nothing is written except
  * *num_rendered = 0 and out_* are zero-filled (the reference returns its zero-initialised tensors). */
 int gsr_rasterize_gaussians(
     int P, int M,
@@ -92,6 +96,18 @@ int gsr_rasterize_gaussians(
     int* num_rendered,
     gsr_alloc_fn alloc, void* alloc_ctx,
     void* stream, int debug);
+
+/* Tile instances binned by the last forward on this host thread (<= its num_rendered: the
+ * instances of the reference's list that can contribute).  0 before any forward. */
+int gsr_last_forward_instances(void);
+
+/* Sticky per-device fault word: the kStatus bits (1 depth sort, 2 tile sort, 4 clamped id) of
+ * every forward on the current device that failed since the last reset.  While it is non-zero,
+ * gsr_adam_step (gsr_optim.h) leaves parameters and moments unchanged, so the NaN gradients of a
+ * failed call cannot reach them (the reference __trap()s instead).  gsr_forward_faults() reads it
+ * (synchronously; -1 on a HIP error), gsr_reset_forward_faults() clears it (0 = ok). */
+int gsr_forward_faults(void);
+int gsr_reset_forward_faults(void);
 
 /* Backward.  Replaces _C.rasterize_gaussians_backward -> RasterizeGaussiansBackwardCUDA
  * (rasterize_points.cu:117-196) -> CudaRasterizer::Rasterizer::backward (rasterizer_impl.cu:340-434).
@@ -230,9 +246,12 @@ int gsr_sh_grad_flush(int P, int M, int degree, const float* means3D, int nviews
 int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
                      uint8_t* present, void* stream);
 
-/* Byte sizes of the three scratch buffers (for callers that pre-allocate). */
+/* Byte sizes of the three scratch buffers (for callers that pre-allocate).  R = num_rendered;
+ * gsr_binning_buffer_bytes_det: the same with the deterministic backward (GSR_DEBUG_DETERMINISTIC),
+ * whose binning buffer holds two more per-instance arrays. */
 size_t gsr_geom_buffer_bytes(int P);
 size_t gsr_binning_buffer_bytes(int R);
+size_t gsr_binning_buffer_bytes_det(int R);
 size_t gsr_image_buffer_bytes(int image_height, int image_width);
 
 #ifdef __cplusplus

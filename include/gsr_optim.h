@@ -22,6 +22,9 @@ extern "C" {
  * params/grads/exp_avg/exp_avg_sq[t]: device pointers to numel[t] contiguous floats;
  * lr[t], weight_decay[t]: the tensor's group hyper-parameters; step[t]: the step count AFTER
  * increment (>= 1).  Arithmetic and host scalars follow torch.optim.adam._multi_tensor_adam.
+ * Guard: while the device's forward fault word is set (gsr.h gsr_forward_faults: a rasterizer
+ * forward failed and its gradients are NaN), the kernel leaves every parameter and moment
+ * unchanged -- decided on the device, no host synchronisation.
  * Returns 0 on success, 1 on invalid arguments, 2 on a launch error. */
 int gsr_adam_step(int n_tensors, float* const* params, const float* const* grads,
                   float* const* exp_avg, float* const* exp_avg_sq, const int64_t* numel,

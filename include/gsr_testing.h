@@ -38,6 +38,16 @@ int gsr_test_scan(const uint32_t* in, uint32_t* out, size_t n, int inclusive, vo
  * (gsr_device.h; the oracle evaluates the same sequence) (device pointers). */
 int gsr_test_expf_pair(const float* x, float* ref, float* fast, size_t n, void* stream);
 
+/* The tile-sorted instance list a forward left in its buffers (device pointers; sizes as the
+ * forward was called): point_list_out[0 .. n_instances) -- the first gsr_last_forward_instances()
+ * entries the blends read -- and ranges_out[tiles * 2] (uint2 [start, end) per tile, (0, 0) when
+ * empty).  num_rendered is the forward's return value (it sizes the binning layout), debug its
+ * debug word (bit 1: deterministic layout).  Lets tests/ pin the binning (duplicateWithKeys +
+ * SortPairs + identifyTileRanges, rasterizer_impl.cu:70-138) to the oracle's lists. */
+int gsr_test_binning_lists(const void* binning_buffer, const void* image_buffer, int num_rendered,
+                           int image_height, int image_width, int debug, int n_instances,
+                           uint32_t* point_list_out, uint32_t* ranges_out, void* stream);
+
 /* The fused path's GaussianModel activations as its kernels evaluate them (device pointers):
  * opacity = sigmoid(opacity_raw) [P], scaling = exp(scaling_raw) [P,3],
  * rotation = normalize(rotation_raw) [P,4] (16-byte aligned).  Lets the tests feed the CPU oracle

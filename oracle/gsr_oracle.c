@@ -116,6 +116,97 @@ void oracle_splat_exp(long n, const float* x, float* out) {
     for (long i = 0; i < n; i++) out[i] = splat_exp(x[i]);
 }
 
+/* ------------------------------------------------------------------------------------------ */
+/* Exact tile culling of the HIP build (sdp-gs_amd/csrc/gsr_device.h).  Not in the  */
+/* reference: its duplicateWithKeys emits every tile of the 3-sigma rectangle                    */
+/* (rasterizer_impl.cu:94-109).  The build bins only the tiles of that rectangle where a splat   */
+/* can reach alpha >= 1/255 at some pixel centre; this restatement (same float operations, same */
+/* order, -ffp-contract=off) lets the tests pin the build's instance list to the reference's     */
+/* list filtered by that predicate (tests/test_index_parity.py).                                */
+/* ------------------------------------------------------------------------------------------ */
+static float splat_log(float x) { /* gsr_device.h splat_log: Cephes logf, explicit fmaf steps */
+    int e;
+    float m = frexpf(x, &e);
+    if (m < 0.707106781186547524f) {
+        e -= 1;
+        m = (m + m) - 1.0f;
+    } else {
+        m = m - 1.0f;
+    }
+    const float z = m * m;
+    float y = 7.0376836292e-2f;
+    y = fmaf(y, m, -1.1514610310e-1f);
+    y = fmaf(y, m, 1.1676998740e-1f);
+    y = fmaf(y, m, -1.2420140846e-1f);
+    y = fmaf(y, m, 1.4249322787e-1f);
+    y = fmaf(y, m, -1.6668057665e-1f);
+    y = fmaf(y, m, 2.0000714765e-1f);
+    y = fmaf(y, m, -2.4999993993e-1f);
+    y = fmaf(y, m, 3.3333331174e-1f);
+    y = (y * m) * z;
+    const float fe = (float)e;
+    y = fmaf(fe, -2.12194440e-4f, y);
+    y = fmaf(-0.5f, z, y);
+    const float r = m + y;
+    return fmaf(fe, 0.693359375f, r);
+}
+void oracle_splat_log(long n, const float* x, float* out) {
+    for (long i = 0; i < n; i++) out[i] = splat_log(x[i]);
+}
+typedef struct { float mx, my, ca, cb, cc, qc, kx, ky; } splat_cut;
+static float cut_q(float ca, float cb, float cc, float op) { /* gsr_device.h splat_q_cut */
+    if (!(op >= 1.0f / 255.0f)) return -2.0f;
+    if (!(ca > 0.0f && cc > 0.0f && ca * cc - cb * cb > 0.0f)) return -1.0f;
+    return 2.0f * splat_log(255.0f * op);
+}
+static splat_cut make_cut(float mx, float my, float ca, float cb, float cc, float qc) {
+    splat_cut s = {mx, my, ca, cb, cc, qc, 0.0f, 0.0f};
+    if (qc >= 0.0f) {
+        s.kx = -cb / cc;
+        s.ky = -cb / ca;
+    }
+    return s;
+}
+static int cut_touches_rect(const splat_cut* s, float x0, float x1, float y0, float y1) {
+    if (s->qc == -2.0f) return 0;
+    if (s->qc < 0.0f) return 1;
+    const float dx0 = x0 - s->mx, dx1 = x1 - s->mx, dy0 = y0 - s->my, dy1 = y1 - s->my;
+    if (dx0 <= 0.0f && dx1 >= 0.0f && dy0 <= 0.0f && dy1 >= 0.0f) return 1;
+    float qmin = 3.0e38f, tabs = 0.0f;
+    for (int e = 0; e < 4; e++) {
+        float dx, dy;
+        if (e < 2) {
+            dx = (e == 0) ? dx0 : dx1;
+            dy = fminf(fmaxf(s->kx * dx, dy0), dy1);
+        } else {
+            dy = (e == 2) ? dy0 : dy1;
+            dx = fminf(fmaxf(s->ky * dy, dx0), dx1);
+        }
+        const float t1 = s->ca * dx * dx, t2 = s->cc * dy * dy, t3 = 2.0f * s->cb * dx * dy;
+        const float q = t1 + t2 + t3;
+        if (q < qmin) { qmin = q; tabs = t1 + t2 + fabsf(t3); }
+    }
+    return qmin <= s->qc + 2e-2f + 1e-4f * tabs;
+}
+static void cut_row_range(const splat_cut* s, unsigned ty, unsigned x0, unsigned x1, unsigned* pa,
+                          unsigned* pb) {
+    if (s->qc < 0.0f) {
+        *pa = x0;
+        *pb = s->qc == -2.0f ? x0 : x1;
+        return;
+    }
+    const float y0 = (float)(ty * BLOCK_Y), y1 = (float)(ty * BLOCK_Y + BLOCK_Y - 1);
+    unsigned a = x0, b = x1;
+    while (a < x1 && !cut_touches_rect(s, (float)(a * BLOCK_X), (float)(a * BLOCK_X + BLOCK_X - 1), y0, y1))
+        a++;
+    while (b > a + 1 &&
+           !cut_touches_rect(s, (float)((b - 1) * BLOCK_X), (float)((b - 1) * BLOCK_X + BLOCK_X - 1), y0, y1))
+        b--;
+    if (a == x1) b = x1;
+    *pa = a;
+    *pb = b;
+}
+
 /* auxiliary.h:41-44: promoted to double */
 static float ndc2Pix(float v, int S) { return (float)((((double)v + 1.0) * S - 1.0) * 0.5); }
 
@@ -1104,6 +1195,32 @@ void oracle_free(oracle_state* st) {
     free(st->conic_opacity); free(st->rgb); free(st->feat); free(st->tiles_touched);
     free(st->point_list); free(st->ranges); free(st->final_T); free(st->n_contrib); free(st->margin);
     free(st);
+}
+
+/* The reference's instance list (point_list, ranges) with the instances the exact tile cull
+ * drops removed; order otherwise unchanged.  Returns the number of instances kept. */
+int oracle_cut_lists(const oracle_state* st, unsigned* point_list_out, unsigned* ranges_out) {
+    const unsigned ntiles = st->gx * st->gy;
+    unsigned n = 0;
+    for (unsigned t = 0; t < ntiles; t++) {
+        const unsigned rs = st->ranges[2 * t], re = st->ranges[2 * t + 1];
+        const unsigned tx = t % st->gx, ty = t / st->gx;
+        const unsigned start = n;
+        for (unsigned k = rs; k < re; k++) {
+            const unsigned g = st->point_list[k];
+            const float* co = st->conic_opacity + 4 * (size_t)g;
+            const float mx = st->means2D[2 * (size_t)g], my = st->means2D[2 * (size_t)g + 1];
+            u2 rmin, rmax;
+            getRect(mx, my, st->radii[g], &rmin, &rmax, st->gx, st->gy);
+            const splat_cut c = make_cut(mx, my, co[0], co[1], co[2], cut_q(co[0], co[1], co[2], co[3]));
+            unsigned a, b;
+            cut_row_range(&c, ty, rmin.x, rmax.x, &a, &b);
+            if (tx >= a && tx < b) point_list_out[n++] = g;
+        }
+        ranges_out[2 * t] = n > start ? start : 0;
+        ranges_out[2 * t + 1] = n > start ? n : 0;
+    }
+    return (int)n;
 }
 
 int oracle_get_point_list(const oracle_state* st, unsigned* out) { memcpy(out, st->point_list, sizeof(unsigned) * (size_t)st->R); return st->R; }

@@ -102,6 +102,10 @@ int oracle_mark_visible(int P, const float* means3D, const float* viewmatrix,
 /* Introspection for parity tests (copies internal state out). */
 int oracle_get_point_list(const oracle_state* st, unsigned* out);   /* [num_rendered] */
 int oracle_get_ranges(const oracle_state* st, unsigned* out);       /* [tiles*2] */
+/* point_list / ranges with the HIP build's exact tile cull applied (gsr_oracle.c); returns the
+ * instances kept.  point_list_out holds num_rendered entries, ranges_out tiles*2. */
+int oracle_cut_lists(const oracle_state* st, unsigned* point_list_out, unsigned* ranges_out);
+void oracle_splat_log(long n, const float* x, float* out);
 int oracle_get_final_T(const oracle_state* st, float* out);         /* [H*W] */
 int oracle_get_n_contrib(const oracle_state* st, unsigned* out);    /* [H*W] */
 /* [H*W] min relative distance of the pixel's blend decisions from alpha = 1/255 and

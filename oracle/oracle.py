@@ -48,6 +48,10 @@ def lib():
         L.oracle_mark_visible.argtypes = [_i, _p, _p, _p, _p]
         L.oracle_splat_exp.restype = None
         L.oracle_splat_exp.argtypes = [ctypes.c_long, _p, _p]
+        L.oracle_splat_log.restype = None
+        L.oracle_splat_log.argtypes = [ctypes.c_long, _p, _p]
+        L.oracle_cut_lists.restype = _i
+        L.oracle_cut_lists.argtypes = [_p, _p, _p]
         L.oracle_set_threads.restype = None
         L.oracle_set_threads.argtypes = [_i]
         L.oracle_get_threads.restype = _i
@@ -147,6 +151,15 @@ class OracleRaster:
     def ranges(self):
         return self._get("ranges", (self.gx * self.gy, 2), np.uint32)
 
+    def cut_lists(self):
+        """(point_list, ranges) of the reference's binning with the HIP build's exact tile cull
+        applied (oracle/gsr_oracle.c oracle_cut_lists): the instances that can contribute, in
+        the reference's order."""
+        pl = np.zeros((max(self.num_rendered, 1),), np.uint32)
+        rg = np.zeros((self.gx * self.gy, 2), np.uint32)
+        n = lib().oracle_cut_lists(self._st, _ptr(pl), _ptr(rg))
+        return pl[:n].copy(), rg
+
     def final_T(self):
         return self._get("final_T", (self.H, self.W), np.float32)
 
@@ -214,6 +227,14 @@ def splat_exp(x):
     xs = _arr(x).reshape(-1)
     out = np.empty_like(xs)
     lib().oracle_splat_exp(xs.size, _ptr(xs), _ptr(out))
+    return out
+
+
+def splat_log(x):
+    """The culling threshold's log (oracle/gsr_oracle.c splat_log) of a float32 array."""
+    xs = _arr(x).reshape(-1)
+    out = np.empty_like(xs)
+    lib().oracle_splat_log(xs.size, _ptr(xs), _ptr(out))
     return out
 
 

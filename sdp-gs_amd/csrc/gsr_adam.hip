@@ -20,6 +20,10 @@
 
 #include "../../include/gsr_optim.h"
 
+namespace gsr {
+uint32_t* forward_faults_word();  // gsr_sort.hip: sticky fault word of failed rasterizer forwards
+}
+
 namespace {
 
 constexpr int kThreads = 256;
@@ -39,6 +43,9 @@ struct AdamArgs {
   float wd[GSR_ADAM_MAX_TENSORS];
   uint32_t vec_ok;                           // bit t: all four arrays of tensor t 16-B aligned
   float w1, beta2, one_m_beta2, eps;
+  // the device's forward fault word: non-zero = a rasterizer forward failed (its gradients are
+  // NaN), so the step leaves parameters and moments untouched (include/gsr_optim.h)
+  const uint32_t* fault;
 };
 
 __device__ __forceinline__ float lerp_torch(float a, float b, float w) {
@@ -86,6 +93,7 @@ __device__ __forceinline__ void st4(float4* p, float4 v) {
 }
 
 __global__ __launch_bounds__(kThreads) void adam_kernel(AdamArgs a) {
+  if (a.fault && __hip_atomic_load(a.fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
   const uint32_t b = blockIdx.x;
   int t = 0;
   while (t + 1 < a.n && b >= a.block0[t + 1]) t++;  // workgroup-uniform, <= 16 tensors
@@ -169,6 +177,7 @@ extern "C" int gsr_adam_step(int n_tensors, float* const* params, const float* c
   a.beta2 = (float)beta2;
   a.one_m_beta2 = (float)(1.0 - beta2);
   a.eps = (float)eps;
+  a.fault = gsr::forward_faults_word();
   if (blocks == 0) return 0;
   hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(kThreads), 0, (hipStream_t)stream, a);
   return hipGetLastError() == hipSuccess ? 0 : 2;

@@ -38,14 +38,23 @@ GeomState carve_geom(char* base, size_t P) {
   g.tiles_touched = c.take<uint32_t>(P);
   g.offsets = c.take<uint32_t>(P);
   g.acc = c.take<float>((size_t)kAccFloats * P);
+  g.ebeg = c.take<uint32_t>(P);
   g.sort = take_sort_scratch(c, P);
   g.scan_parts = c.take<uint32_t>(scan_parts(P) + 1);
-  g.pre_parts = c.take<uint32_t>((P + 255) / 256 + 1);
+  g.pre_parts = c.take<uint32_t>(2 * ((P + 255) / 256) + 1);
   g.bytes = c.size();
   return g;
 }
 
-BinState carve_bin(char* base, size_t R, bool det) {
+bool bwd_rows_mode() {
+  static const bool rows = [] {
+    const char* e = getenv("GSR_BWD_ROWS");
+    return e ? atoi(e) != 0 : false;
+  }();
+  return rows;
+}
+
+BinState carve_bin(char* base, size_t R, bool rows) {
   Carver c(base);
   BinState b{};
   b.tkey_a = c.take<uint32_t>(R);
@@ -53,7 +62,7 @@ BinState carve_bin(char* base, size_t R, bool det) {
   b.tkey_b = c.take<uint32_t>(R);
   b.tval_b = c.take<uint32_t>(R);
   b.sort = take_sort_scratch(c, R);
-  if (det) {
+  if (rows) {
     b.egid = c.take<uint32_t>(R);
     b.partial = c.take<float>(R * kAccFloats);
   }
@@ -151,6 +160,8 @@ int tile_bits(uint32_t ntiles) {
 
 // host time spent waiting for forwards' instance-count read-backs (gsr_test_host_wait_ms)
 std::atomic<long long> g_wait_ns{0};
+// tile instances the last forward on this host thread actually binned (gsr_last_forward_instances)
+thread_local int g_last_instances = 0;
 
 // Pinned 16-byte landing zone for the one device->host read per forward.
 uint32_t* pinned_slot() {
@@ -342,6 +353,8 @@ extern "C" {
 
 int gsr_abi_version(void) { return GSR_ABI_VERSION; }
 
+int gsr_last_forward_instances(void) { return g_last_instances; }
+
 int gsr_forward_status(const void* image_buffer, int wait) {
   g_err.clear();
   if (const uint32_t v = mail_check(image_buffer, wait != 0))
@@ -369,7 +382,12 @@ int gsr_check_forwards(int wait) {
 const char* gsr_last_error(void) { return g_err.c_str(); }
 
 size_t gsr_geom_buffer_bytes(int P) { return carve_geom(nullptr, (size_t)(P > 0 ? P : 0)).bytes; }
-size_t gsr_binning_buffer_bytes(int R) { return carve_bin(nullptr, (size_t)(R > 0 ? R : 0)).bytes; }
+size_t gsr_binning_buffer_bytes(int R) {
+  return carve_bin(nullptr, (size_t)(R > 0 ? R : 0), bwd_rows_mode()).bytes;
+}
+size_t gsr_binning_buffer_bytes_det(int R) {
+  return carve_bin(nullptr, (size_t)(R > 0 ? R : 0), true).bytes;
+}
 size_t gsr_image_buffer_bytes(int H, int W) {
   return carve_img(nullptr, (size_t)(W > 0 ? W : 0), (size_t)(H > 0 ? H : 0)).bytes;
 }
@@ -390,6 +408,7 @@ static int forward_impl(int P, int M, const float* background, const float* mean
                         const float* pre_color = nullptr, const uint8_t* pre_clamp = nullptr) {
   g_err.clear();
   const bool det = (debug & GSR_DEBUG_DETERMINISTIC) != 0;  // gsr.h: debug bit 1
+  const bool rows = det || bwd_rows_mode();  // per-instance gradient rows (binning layout)
   debug &= 1;
   if ((pre_color == nullptr) != (pre_clamp == nullptr) || (pre_color && !fused))
     return fail(GSR_ERR_ARGUMENT, "pre_color / pre_clamp: both or neither, fused path only");
@@ -406,6 +425,7 @@ static int forward_impl(int P, int M, const float* background, const float* mean
   const size_t HW = (size_t)W * H;
   if (P == 0) {
     *num_rendered = 0;
+    g_last_instances = 0;
     GSR_CHECK(hipMemsetAsync(out_color, 0, 3 * HW * sizeof(float), stream));
     if (out_depth) GSR_CHECK(hipMemsetAsync(out_depth, 0, HW * sizeof(float), stream));
     if (out_alpha) GSR_CHECK(hipMemsetAsync(out_alpha, 0, HW * sizeof(float), stream));
@@ -463,7 +483,7 @@ static int forward_impl(int P, int M, const float* background, const float* mean
   pa.pre_color = pre_color; pa.pre_clamp = pre_clamp;
   // the preprocess grid also zeroes the depth sort's scratch and the backward's accumulators
   pa.clear = SideClear{g.sort.aux, sort_clear_bytes(g.sort, (size_t)P, 32)};
-  pa.acc_zero = 1;
+  pa.acc_zero = rows ? 0 : 1;  // the rows layout never reads the accumulator rows
   pa.parts = g.pre_parts;
   PROF_BEGIN(PREPROCESS);
   GSR_CHECK(launch_preprocess(pa, stream));
@@ -471,14 +491,19 @@ static int forward_impl(int P, int M, const float* background, const float* mean
   // while the depth sort and the scan are already queued behind it, so the host's wait and the
   // binning-buffer allocation overlap GPU work instead of draining the stream
   // flags[1] = R
-  GSR_CHECK(sum_u32_parts(g.pre_parts, ((size_t)P + 255) / 256, g.flags + 1, stream, false));
+  // flags[2] = the reference's num_rendered: the sum of the full 3-sigma tile rectangles
+  // (forward.cu:255, rasterizer_impl.cu:281), returned at the boundary; the binning buffer is
+  // carved for that many instances, so a backward handed the reference's count re-carves the
+  // same offsets
+  const size_t pre_blocks = ((size_t)P + 255) / 256;
+  GSR_CHECK(sum_u32_parts(g.pre_parts, pre_blocks, g.flags + 1, stream, g.pre_parts + pre_blocks));
   PROF_END(PREPROCESS);
   uint32_t* host = pinned_slot();
   hipEvent_t ready = readback_event();
   if (!host || !ready) return fail(GSR_ERR_HIP, "pinned host slot / event creation failed");
-  // one read-back: flags[0] (prefiltered violation) and R.  The sorts' look-back timeouts are
-  // this call's status (mailbox below), not part of this wait.
-  GSR_CHECK(hipMemcpyAsync(host, g.flags, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+  // one read-back: flags[0] (prefiltered violation), R and the reference's count.  The sorts'
+  // look-back timeouts are this call's status (mailbox below), not part of this wait.
+  GSR_CHECK(hipMemcpyAsync(host, g.flags, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
   GSR_CHECK(hipEventRecord(ready, stream));
 
   bool in_b = false;
@@ -501,21 +526,22 @@ static int forward_impl(int P, int M, const float* background, const float* mean
                             std::chrono::steady_clock::now() - t0).count(),
                         std::memory_order_relaxed);
   }
-  const uint32_t R = host[1];
+  const uint32_t R = host[1];       // instances binned: tiles that pass the exact cull
+  const uint32_t R_ref = host[2];   // the reference's num_rendered (full rectangles), R <= R_ref
   if (prefiltered && host[0]) return fail(GSR_ERR_PREFILTERED,
                            "Point is filtered although prefiltered is set. This shouldn't happen!");
-  if (R > 0x7fffffffu)
-    return fail(GSR_ERR_TOO_LARGE, "num_rendered = %u exceeds the sort capacity", R);
+  if (R_ref > 0x7fffffffu || R > R_ref)
+    return fail(GSR_ERR_TOO_LARGE, "num_rendered = %u exceeds the sort capacity", R_ref);
   if (debug) {
     GSR_CHECK(hipMemcpyAsync(host + 2, g.sort.aux + kSortAuxErr, 4, hipMemcpyDeviceToHost, stream));
     GSR_CHECK(hipStreamSynchronize(stream));
     if (host[2]) return fail(GSR_ERR_HIP, "depth sort look-back timed out");
   }
 
-  const size_t bbytes = carve_bin(nullptr, R, det).bytes;
+  const size_t bbytes = carve_bin(nullptr, R_ref, rows).bytes;
   char* bbase = (char*)alloc(alloc_ctx, bbytes, GSR_BUF_BINNING);
   if (!bbase) return fail(GSR_ERR_ALLOC, "binning buffer allocation of %zu bytes failed", bbytes);
-  BinState b = carve_bin(bbase, R, det);
+  BinState b = carve_bin(bbase, R_ref, rows);  // capacity R_ref, the first R entries used
 
   PROF_BEGIN(DUPLICATE);
   // the duplicate grid also zeroes the tile sort's scratch and the tile ranges
@@ -523,7 +549,7 @@ static int forward_impl(int P, int M, const float* background, const float* mean
   GSR_CHECK(launch_duplicate(P, order, g.offsets, radii_ptr, g.rec, gx, gy, b.tkey_a, b.tval_a,
                              (uint32_t)R, SideClear{b.sort.aux, sort_clear_bytes(b.sort, R, tbits)},
                              SideClear{im.ranges, sizeof(uint2) * ntiles}, stream,
-                             det ? b.egid : nullptr));
+                             rows ? b.egid : nullptr, rows ? g.ebeg : nullptr));
   PROF_END(DUPLICATE);
   bool t_in_b = false;
   PROF_BEGIN(TILE_SORT);
@@ -537,7 +563,7 @@ static int forward_impl(int P, int M, const float* background, const float* mean
   }
   const uint32_t* tiles_sorted = t_in_b ? b.tkey_b : b.tkey_a;
   const uint32_t* point_list = t_in_b ? b.tval_b : b.tval_a;
-  if (det) {  // the sorted values are emission indices: Gaussian ids into the other value array
+  if (rows) {  // the sorted values are emission indices: Gaussian ids into the other value array
     uint32_t* pl = t_in_b ? b.tval_a : b.tval_b;
     GSR_CHECK(launch_det_gather(R, point_list, b.egid, pl, stream));
     point_list = pl;
@@ -546,8 +572,8 @@ static int forward_impl(int P, int M, const float* background, const float* mean
   uint32_t* host_status = mail_post(ibase, &mail_slot);
   PROF_BEGIN(RANGES);
   GSR_CHECK(launch_tile_ranges(R, tiles_sorted, im.ranges, ntiles, g.sort.aux + kSortAuxErr,
-                               b.sort.aux + kSortAuxErr, im.status, host_status, stream,
-                               /*ranges_cleared=*/true));
+                               b.sort.aux + kSortAuxErr, im.status, host_status,
+                               forward_faults_word(), stream, /*ranges_cleared=*/true));
   PROF_END(RANGES);
 
   RenderArgs ra{};
@@ -557,7 +583,7 @@ static int forward_impl(int P, int M, const float* background, const float* mean
   ra.out_color = out_color; ra.out_depth = out_depth; ra.out_alpha = out_alpha;
   ra.out_feature = out_feature; ra.include_feature = include_feature;
   ra.order = im.order; ra.sched = tile_schedule_mode();
-  ra.status = im.status; ra.host_status = host_status;
+  ra.status = im.status; ra.host_status = host_status; ra.fault = forward_faults_word();
   PROF_BEGIN(RENDER_FWD);
   GSR_CHECK(launch_render_forward(ra, stream));
   PROF_END(RENDER_FWD);
@@ -566,8 +592,9 @@ static int forward_impl(int P, int M, const float* background, const float* mean
     const uint32_t v = mail_check(ibase, true);
     if (v) return fail(GSR_ERR_SORT, "%s", status_message(v).c_str());
   }
-  *num_rendered = (int)R;
-  acc_mark_clean(gbase);
+  *num_rendered = (int)R_ref;
+  g_last_instances = (int)R;
+  if (!rows) acc_mark_clean(gbase);
   return GSR_OK;
 }
 
@@ -644,6 +671,7 @@ static int backward_impl(
     const float* pre_jac = nullptr) {
   g_err.clear();
   const bool det = (debug & GSR_DEBUG_DETERMINISTIC) != 0;  // must match the forward's flags
+  const bool rows = det || bwd_rows_mode();
   debug &= 1;
   if (fused && P != 0) {
     if (!sh_dc || (M > 1 && !sh_rest) || (M > 1 && !dL_dsh_rest && !dRGB_sh) || !scales ||
@@ -683,17 +711,17 @@ static int backward_impl(
   const uint32_t ntiles = gx * gy;
   GeomState g = carve_geom((char*)geom_buffer, (size_t)P);
   ImgState im = carve_img((char*)image_buffer, (size_t)W, (size_t)H);
-  BinState b = carve_bin((char*)binning_buffer, (size_t)R, det);
+  BinState b = carve_bin((char*)binning_buffer, (size_t)R, rows);
   const int passes = sort_passes(tile_bits(ntiles));
   const uint32_t* point_list = (passes & 1) ? b.tval_b : b.tval_a;
   const uint32_t* einst = nullptr;
-  if (det) {  // forward: emission indices sorted in place, Gaussian ids gathered into the other
+  if (rows) {  // forward: emission indices sorted in place, Gaussian ids gathered into the other
     einst = point_list;
     point_list = (passes & 1) ? b.tval_a : b.tval_b;
   }
   const int32_t* radii_ptr = radii ? radii : g.radii;
 
-  if (!acc_take_clean(geom_buffer)) {  // not freshly zeroed by this buffer's forward
+  if (!rows && !acc_take_clean(geom_buffer)) {  // not freshly zeroed by this buffer's forward
     PROF_BEGIN(ACC_ZERO);
     GSR_CHECK(hipMemsetAsync(g.acc, 0, sizeof(float) * kAccFloats * (size_t)P, stream));
     PROF_END(ACC_ZERO);
@@ -706,14 +734,9 @@ static int backward_impl(
     rb.dL_dcolor = dL_dout_color; rb.dL_ddepth = dL_dout_depth; rb.dL_dalpha = dL_dout_alpha;
     rb.dL_dfeature = dL_dout_feature; rb.acc = g.acc; rb.include_feature = include_feature;
     rb.order = im.order; rb.sched = tile_schedule_mode();
-    rb.einst = einst; rb.partial = det ? b.partial : nullptr;
+    rb.einst = einst; rb.partial = rows ? b.partial : nullptr; rb.det = det ? 1 : 0;
     PROF_BEGIN(RENDER_BWD);
     GSR_CHECK(launch_render_backward(rb, stream));
-    if (det) {  // per-Gaussian sums of the instance rows in emission order (no atomics)
-      const bool in_b = (sort_passes(32) & 1) != 0;  // the depth sort's ping-pong, as the forward
-      GSR_CHECK(launch_det_reduce(P, in_b ? g.dval_b : g.dval_a, g.offsets, b.partial,
-                                  (uint32_t)R, g.acc, stream));
-    }
     PROF_END(RENDER_BWD);
   }
   BwdPreArgs ba{};
@@ -737,6 +760,10 @@ static int backward_impl(
   ba.dRGB_out = dRGB_sh;
   ba.pre_jac = pre_jac;
   ba.status = im.status;
+  // rows layout: each Gaussian sums its instances' rows (emission order, contiguous) itself
+  ba.use_rows = rows ? 1 : 0;
+  ba.rows = R > 0 && rows ? reinterpret_cast<const float4*>(b.partial) : nullptr;
+  ba.ebeg = g.ebeg; ba.count = g.tiles_touched;
   if (dRGB_sh) ba.dL_dsh = ba.dL_dsh_rest = nullptr;
   PROF_BEGIN(PREPROCESS_BWD);
   GSR_CHECK(launch_preprocess_backward(ba, stream));
@@ -962,6 +989,35 @@ int gsr_test_activations(const float* opacity_raw, const float* scaling_raw,
     return fail(GSR_ERR_ARGUMENT, "rotations must be 16-byte aligned");
   GSR_CHECK(launch_activations(opacity_raw, scaling_raw, rotation_raw, P, opacity, scaling,
                                rotation, stream));
+  return GSR_OK;
+}
+
+int gsr_test_binning_lists(const void* binning_buffer, const void* image_buffer, int num_rendered,
+                           int image_height, int image_width, int flags, int n_instances,
+                           uint32_t* point_list_out, uint32_t* ranges_out, void* stream_ptr) {
+  g_err.clear();
+  hipStream_t stream = (hipStream_t)stream_ptr;
+  const int debug = 0;
+  if (num_rendered < 0 || n_instances < 0 || n_instances > num_rendered || image_height <= 0 ||
+      image_width <= 0 || !image_buffer || !ranges_out ||
+      (n_instances && (!binning_buffer || !point_list_out)))
+    return fail(GSR_ERR_ARGUMENT, "invalid arguments");
+  const bool rows = (flags & GSR_DEBUG_DETERMINISTIC) != 0 || bwd_rows_mode();
+  const uint32_t gx = (uint32_t)((image_width + kTile - 1) / kTile);
+  const uint32_t gy = (uint32_t)((image_height + kTile - 1) / kTile);
+  const ImgState im = carve_img((char*)image_buffer, (size_t)image_width, (size_t)image_height);
+  GSR_CHECK(hipMemcpyAsync(ranges_out, im.ranges, sizeof(uint2) * gx * gy, hipMemcpyDeviceToHost,
+                           stream));
+  if (n_instances) {
+    // the backward's own carve (backward_impl): same layout, same ping-pong parity
+    const BinState b = carve_bin((char*)binning_buffer, (size_t)num_rendered, rows);
+    const int passes = sort_passes(tile_bits(gx * gy));
+    const uint32_t* pl = (passes & 1) ? b.tval_b : b.tval_a;
+    if (rows) pl = (passes & 1) ? b.tval_a : b.tval_b;
+    GSR_CHECK(hipMemcpyAsync(point_list_out, pl, sizeof(uint32_t) * (size_t)n_instances,
+                             hipMemcpyDeviceToHost, stream));
+  }
+  GSR_CHECK(hipStreamSynchronize(stream));
   return GSR_OK;
 }
 

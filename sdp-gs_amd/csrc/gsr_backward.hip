@@ -81,13 +81,67 @@ __device__ __forceinline__ void zero_outputs(const BwdPreArgs& a, size_t i) {
   if (a.dL_dlanguage_feature) put3(a.dL_dlanguage_feature, i, v3(0, 0, 0));
 }
 
+// Failed forward (its status word is set): every gradient element the normal path would write
+// for Gaussian i becomes NaN -- stored, or added (NaN + x = NaN) in accumulate mode -- so the
+// call's gradients are NaN-poisoned whatever the buffers held before (gsr.h GSR_ERR_SORT).
+template <bool ACC>
+__device__ __forceinline__ void poison_outputs(const BwdPreArgs& a, size_t i) {
+  const float nan = __builtin_nanf("");
+  const V3 n3 = v3(nan, nan, nan);
+  put3(a.dL_dmeans2D, i, n3);
+  st3<ACC>(a.dL_dmeans3D, i, n3);
+  if (a.dL_dcolors) st3<ACC>(a.dL_dcolors, i, n3);
+  st<ACC>(a.dL_dopacity + i, nan);
+  if (a.dL_dcov3D)
+    for (int k = 0; k < 6; k++) st<ACC>(a.dL_dcov3D + 6 * i + k, nan);
+  if (a.dL_dscales) st3<ACC>(a.dL_dscales, i, n3);
+  if (a.dL_drotations)
+    for (int k = 0; k < 4; k++) st<ACC>(a.dL_drotations + 4 * i + k, nan);
+  if (a.dL_dsh_language) st3<ACC>(a.dL_dsh_language, i, n3);
+  if (a.dL_dlanguage_feature) st3<ACC>(a.dL_dlanguage_feature, i, n3);
+  if (a.dRGB_out) {
+    put3(a.dRGB_out, i, n3);  // deferred: the step's SH flush spreads the NaN to the SH rows
+  } else if (a.fused) {
+    if (a.dL_dsh) st3<ACC>(a.dL_dsh, i, n3);  // features_dc [P,1,3]
+    if (a.dL_dsh_rest)
+      for (int k = 0; k < 3 * (a.M - 1); k++) st<ACC>(a.dL_dsh_rest + (size_t)3 * (a.M - 1) * i + k, nan);
+  } else if (a.dL_dsh) {
+    for (int k = 0; k < 3 * a.M; k++) st<ACC>(a.dL_dsh + (size_t)3 * a.M * i + k, nan);
+  }
+}
+
+__device__ __forceinline__ void add4(float4& t, float4 x) {
+  t.x += x.x; t.y += x.y; t.z += x.z; t.w += x.w;
+}
+// The Gaussian's 16-float gradient row (gsr_internal.h AccSlot): its accumulator row (atomic
+// mode), or the sum of its instances' rows in emission order (rows layout; zero without any).
+__device__ __forceinline__ void grad_row(const BwdPreArgs& a, size_t i, float4& q0, float4& q1,
+                                         float4& q2, float4& q3) {
+  if (!a.use_rows) {
+    const float4* accp = reinterpret_cast<const float4*>(a.acc + i * kAccFloats);
+    q0 = accp[0]; q1 = accp[1]; q2 = accp[2]; q3 = accp[3];
+    return;
+  }
+  const uint32_t n = a.count[i];
+  if (n == 0) {
+    q0 = q1 = q2 = q3 = make_float4(0.f, 0.f, 0.f, 0.f);
+    return;
+  }
+  const float4* r = a.rows + (size_t)a.ebeg[i] * (kAccFloats / 4);
+  q0 = r[0]; q1 = r[1]; q2 = r[2]; q3 = r[3];
+  for (uint32_t e = 1; e < n; e++) {
+    r += kAccFloats / 4;
+    add4(q0, r[0]); add4(q1, r[1]); add4(q2, r[2]); add4(q3, r[3]);
+  }
+}
+
 // Backward of one visible Gaussian.  sh0 / sh1: its rows (coefficient 0 / coefficients 1..) of
 // the LDS staging planes: SH coefficients in, SH gradients out; unused without SH.
 template <bool ACC>
 __device__ __forceinline__ void gaussian_bwd(const BwdPreArgs& a, size_t i, float* sh0,
                                              float* sh1) {
-  const float4* accp = reinterpret_cast<const float4*>(a.acc + i * kAccFloats);
-  const float4 q0 = accp[0], q1 = accp[1], q2 = accp[2], q3 = accp[3];
+  float4 q0, q1, q2, q3;
+  grad_row(a, i, q0, q1, q2, q3);
   // slots: q0 = {mx, my, ca, cb}, q1 = {cc, op, r, g}, q2 = {b, depth, f0, f1}, q3 = {f2, used, -, -}
   const float gmx = q0.x, gmy = q0.y;
   const float dcx = q0.z, dcy = q0.w, dcz = q1.x;
@@ -316,13 +370,8 @@ __global__ __launch_bounds__(kThreads) void preprocess_bwd_kernel(BwdPreArgs a) 
   const int n = min(kThreads, a.P - base);
   const int t = (int)threadIdx.x;
   const size_t i = (size_t)base + t;
-  if (a.status && *a.status) {  // the forward's sort gave up (grid-uniform): NaN gradients
-    if (t < n) {
-      const float nan = __builtin_nanf("");
-      put3(a.dL_dmeans2D, i, v3(nan, nan, nan));
-      st3<ACC>(a.dL_dmeans3D, i, v3(nan, nan, nan));
-      if (a.dRGB_out) put3(a.dRGB_out, i, v3(nan, nan, nan));
-    }
+  if (a.status && *a.status) {  // the forward failed (grid-uniform): NaN gradients
+    if (t < n) poison_outputs<ACC>(a, i);
     return;
   }
   const bool live = t < n && a.radii[i] > 0;

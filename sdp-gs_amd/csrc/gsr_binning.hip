@@ -31,7 +31,8 @@ __global__ __launch_bounds__(kThreads) void duplicate_kernel(int P,
                                                              uint32_t* __restrict__ tval,
                                                              uint32_t R, SideClear clear0,
                                                              SideClear clear1,
-                                                             uint32_t* __restrict__ egid) {
+                                                             uint32_t* __restrict__ egid,
+                                                             uint32_t* __restrict__ ebeg) {
   const int s = (int)(blockIdx.x * kThreads + threadIdx.x);
   const size_t nth = (size_t)gridDim.x * kThreads;
   side_clear(clear0.p, clear0.bytes, (size_t)s, nth);
@@ -48,6 +49,7 @@ __global__ __launch_bounds__(kThreads) void duplicate_kernel(int P,
   const float4 r1 = rec[4 * (size_t)gid + 1];
   const float4 r3 = rec[4 * (size_t)gid + 3];  // {f2, radius, q_cut, -}
   const int r = (int)r3.y;
+  if (egid) ebeg[gid] = off;  // rows layout: the Gaussian's rows start at its first instance
   uint32_t x0, y0, x1, y1;
   tile_rect(r0.x, r0.y, r, gx, gy, x0, y0, x1, y1);
   // exactly the per-row tile ranges the preprocess counted (cut_row_range, gsr_device.h)
@@ -57,7 +59,7 @@ __global__ __launch_bounds__(kThreads) void duplicate_kernel(int P,
     cut_row_range(cut, y, x0, x1, a, b);
     for (uint32_t x = a; x < b && off < end; x++) {
       tkey[off] = y * gx + x;
-      if (egid) {  // deterministic backward: sort the emission index, keep its Gaussian aside
+      if (egid) {  // rows layout: sort the emission index, keep its Gaussian aside
         tval[off] = off;
         egid[off] = gid;
       } else {
@@ -75,7 +77,8 @@ __global__ __launch_bounds__(kThreads) void tile_ranges_kernel(size_t R,
                                                                const uint32_t* __restrict__ derr,
                                                                const uint32_t* __restrict__ terr,
                                                                uint32_t* __restrict__ status,
-                                                               uint32_t* host_status) {
+                                                               uint32_t* host_status,
+                                                               uint32_t* fault) {
   const size_t idx = (size_t)blockIdx.x * kThreads + threadIdx.x;
   if (idx >= (R ? R : 1)) return;
   // the call's status: both sorts have finished (stream order); a timed-out look-back of either
@@ -85,6 +88,7 @@ __global__ __launch_bounds__(kThreads) void tile_ranges_kernel(size_t R,
         ((derr && *derr) ? kStatusDepthSort : 0u) | ((terr && *terr) ? kStatusTileSort : 0u);
     *status = st;
     if (host_status) *host_status = st;  // pinned mailbox the host checks (gsr_api.cpp)
+    if (st && fault) atomicOr(fault, st);  // sticky: the fused Adam step skips while set
   }
   if (R == 0) return;
   // tile ids are < ntiles by construction; the bounds tests only keep the output of a sort whose
@@ -111,36 +115,6 @@ __global__ __launch_bounds__(kThreads) void det_gather_kernel(size_t R,
   if (q < R) point_list[q] = egid[min(einst[q], (uint32_t)(R - 1))];
 }
 
-// Deterministic backward, second pass: one lane per depth-ordered Gaussian sums its instances'
-// rows (emission order = its tiles in row-major order, the same on every run) and stores the
-// total -- no float atomics anywhere, so the gradients are bitwise reproducible.
-__global__ __launch_bounds__(kThreads) void det_reduce_kernel(int P,
-                                                              const uint32_t* __restrict__ order,
-                                                              const uint32_t* __restrict__ offsets,
-                                                              const float4* __restrict__ partial,
-                                                              uint32_t R,
-                                                              float4* __restrict__ acc) {
-  const int s = (int)(blockIdx.x * kThreads + threadIdx.x);
-  if (s >= P) return;
-  const uint32_t beg = (s == 0) ? 0u : min(offsets[s - 1], R);
-  const uint32_t end = min(offsets[s], R);
-  if (beg == end) return;  // no instances: the row stays as zeroed
-  const uint32_t gid = min(order[s], (uint32_t)P - 1u);
-  constexpr int kV = kAccFloats / 4;
-  float4 t[kV];
-#pragma unroll
-  for (int v = 0; v < kV; v++) t[v] = partial[(size_t)beg * kV + v];
-  for (uint32_t e = beg + 1; e < end; e++) {
-#pragma unroll
-    for (int v = 0; v < kV; v++) {
-      const float4 x = partial[(size_t)e * kV + v];
-      t[v].x += x.x; t[v].y += x.y; t[v].z += x.z; t[v].w += x.w;
-    }
-  }
-#pragma unroll
-  for (int v = 0; v < kV; v++) acc[(size_t)gid * kV + v] = t[v];
-}
-
 }  // namespace
 
 hipError_t launch_det_gather(size_t R, const uint32_t* einst, const uint32_t* egid,
@@ -151,30 +125,21 @@ hipError_t launch_det_gather(size_t R, const uint32_t* einst, const uint32_t* eg
   return hipGetLastError();
 }
 
-hipError_t launch_det_reduce(int P, const uint32_t* order, const uint32_t* offsets,
-                             const float* partial, uint32_t R, float* acc, hipStream_t s) {
-  if (P == 0 || R == 0) return hipSuccess;
-  static_assert(kAccFloats % 4 == 0, "accumulator rows are float4 vectors");
-  hipLaunchKernelGGL(det_reduce_kernel, dim3((P + kThreads - 1) / kThreads), dim3(kThreads), 0, s,
-                     P, order, offsets, reinterpret_cast<const float4*>(partial), R,
-                     reinterpret_cast<float4*>(acc));
-  return hipGetLastError();
-}
-
 hipError_t launch_duplicate(int P, const uint32_t* order, const uint32_t* offsets,
                             const int32_t* radii, const float4* rec, uint32_t gx, uint32_t gy,
                             uint32_t* tkey, uint32_t* tval, uint32_t R, SideClear clear0,
-                            SideClear clear1, hipStream_t s, uint32_t* egid) {
+                            SideClear clear1, hipStream_t s, uint32_t* egid, uint32_t* ebeg) {
   if (P == 0) return hipSuccess;
   hipLaunchKernelGGL(duplicate_kernel, dim3((P + kThreads - 1) / kThreads), dim3(kThreads), 0, s,
-                     P, order, offsets, radii, rec, gx, gy, tkey, tval, R, clear0, clear1, egid);
+                     P, order, offsets, radii, rec, gx, gy, tkey, tval, R, clear0, clear1, egid,
+                     ebeg);
   return hipGetLastError();
 }
 
 hipError_t launch_tile_ranges(size_t R, const uint32_t* sorted_tiles, uint2* ranges,
                               uint32_t ntiles, const uint32_t* depth_err, const uint32_t* tile_err,
-                              uint32_t* status, uint32_t* host_status, hipStream_t s,
-                              bool ranges_cleared) {
+                              uint32_t* status, uint32_t* host_status, uint32_t* fault,
+                              hipStream_t s, bool ranges_cleared) {
   if (!ranges_cleared) {
     hipError_t e = hipMemsetAsync(ranges, 0, sizeof(uint2) * ntiles, s);
     if (e != hipSuccess) return e;
@@ -183,7 +148,7 @@ hipError_t launch_tile_ranges(size_t R, const uint32_t* sorted_tiles, uint2* ran
   const size_t n = R ? R : 1;
   hipLaunchKernelGGL(tile_ranges_kernel, dim3((unsigned)((n + kThreads - 1) / kThreads)),
                      dim3(kThreads), 0, s, R, sorted_tiles, ranges, ntiles, depth_err,
-                     R ? tile_err : nullptr, status, host_status);
+                     R ? tile_err : nullptr, status, host_status, fault);
   return hipGetLastError();
 }
 

@@ -162,6 +162,38 @@ __device__ __forceinline__ float splat_exp(float x) {
 }
 __device__ __forceinline__ float sigmoid_f(float x) { return 1.0f / (1.0f + expf(-x)); }
 
+// Natural log for the culling threshold q_cut (positive normal x only): Cephes logf -- frexp to
+// m in [sqrt(1/2), sqrt(2)), a degree-8 polynomial in m - 1 and the split ln 2 -- every step an
+// explicit IEEE operation, as splat_exp.  The CPU restatement evaluates the same sequence, so
+// the tests can pin the kept tile instances bit for bit;
+// its error (~1 ulp) is irrelevant next to the 2e-2 margin of cut_touches_rect.
+__device__ __forceinline__ float splat_log(float x) {
+  int e;
+  float m = __builtin_frexpf(x, &e);  // x = m 2^e, m in [0.5, 1)
+  if (m < 0.707106781186547524f) {
+    e -= 1;
+    m = (m + m) - 1.0f;
+  } else {
+    m = m - 1.0f;
+  }
+  const float z = m * m;
+  float y = 7.0376836292e-2f;
+  y = __builtin_fmaf(y, m, -1.1514610310e-1f);
+  y = __builtin_fmaf(y, m, 1.1676998740e-1f);
+  y = __builtin_fmaf(y, m, -1.2420140846e-1f);
+  y = __builtin_fmaf(y, m, 1.4249322787e-1f);
+  y = __builtin_fmaf(y, m, -1.6668057665e-1f);
+  y = __builtin_fmaf(y, m, 2.0000714765e-1f);
+  y = __builtin_fmaf(y, m, -2.4999993993e-1f);
+  y = __builtin_fmaf(y, m, 3.3333331174e-1f);
+  y = (y * m) * z;
+  const float fe = (float)e;
+  y = __builtin_fmaf(fe, -2.12194440e-4f, y);
+  y = __builtin_fmaf(-0.5f, z, y);
+  const float r = m + y;
+  return __builtin_fmaf(fe, 0.693359375f, r);
+}
+
 // ---- conservative splat / pixel-rectangle culling ----------------------------------------------
 // The blend skips a (splat, pixel) pair when alpha = min(0.99, op * exp(power)) < 1/255 with
 // power = -q/2, q = ca dx^2 + 2 cb dx dy + cc dy^2 (forward.cu:335-345).  A splat that fails that
@@ -172,8 +204,8 @@ __device__ __forceinline__ float sigmoid_f(float x) { return 1.0f / (1.0f + expf
 __device__ __forceinline__ float splat_q_cut(float ca, float cb, float cc, float op) {
   if (!(op >= 1.0f / 255.0f)) return -2.0f;
   if (!(ca > 0.0f && cc > 0.0f && ca * cc - cb * cb > 0.0f)) return -1.0f;
-  // float log: its error (~1e-7 relative) is far inside the 2e-2 margin of cut_touches_rect
-  return 2.0f * logf(255.0f * op);
+  // 255 op >= 1: a positive normal float
+  return 2.0f * splat_log(255.0f * op);
 }
 
 // Per-splat constants of the rectangle test: centre, conic, q_cut and the two ratios -cb/cc,

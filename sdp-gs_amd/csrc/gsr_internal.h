@@ -108,13 +108,12 @@ inline SortScratch take_sort_scratch(Carver& c, size_t n) {
 // input element i is in[gather[i]].  parts: scratch of scan_parts(n) u32.
 hipError_t scan_u32(const uint32_t* in, const uint32_t* gather, uint32_t* out, size_t n,
                     bool inclusive, uint32_t* parts, hipStream_t s);
-// *out = sum of n u32 partial sums (one launch; with_timeouts: out[1] = the sticky sort timeout
-// counter, read back with it).
+// out[0] = sum of n u32 partial sums (one launch); with parts2, out[1] = the sum of parts2[0..n).
 hipError_t sum_u32_parts(const uint32_t* parts, size_t n, uint32_t* out, hipStream_t s,
-                         bool with_timeouts);
+                         const uint32_t* parts2 = nullptr);
 // *out = sum of n u32 values (two launches); parts: scratch of scan_parts(n) u32.
 hipError_t reduce_u32(const uint32_t* in, size_t n, uint32_t* parts, uint32_t* out,
-                      hipStream_t s, bool with_timeouts = false);
+                      hipStream_t s);
 // Stable LSD radix sort of (key, value) u32 pairs over key bits [0, bits).  Ping-pongs between
 // (ka, va) and (kb, vb); returns through *result_in_b whether the sorted data ended in (kb, vb).
 // One-sweep passes: 1 memset + 1 digit-totals launch + 1 launch per 8-bit digit; a pass whose
@@ -133,6 +132,10 @@ hipError_t radix_sort_pairs(uint32_t* ka, uint32_t* va, uint32_t* kb, uint32_t* 
 // Device word counting look-back timeouts of any sort on the current device (sticky until the
 // host resets it); every forward reads it back with its instance count.
 uint32_t* sort_timeouts_word();
+// Device address of the sticky per-device forward fault word (kStatus* bits; gsr.h
+// gsr_forward_faults / gsr_reset_forward_faults): or-ed by the tile-ranges kernel and the forward
+// blend of a failed call, read by the fused Adam step (which then skips the update).
+uint32_t* forward_faults_word();
 
 // ---- layouts -------------------------------------------------------------------------------------
 struct GeomState {
@@ -145,11 +148,15 @@ struct GeomState {
   float4* rec;              // [P*4] splat record for the blend
   uint32_t* tiles_touched;  // [P]
   uint32_t* offsets;        // [P] inclusive scan of tiles_touched in depth order
-  float* acc;               // [P*16] backward accumulators
+  float* acc;               // [P*16] backward accumulators (atomic mode only, see bwd_rows_mode)
+  uint32_t* ebeg;           // [P] per Gaussian id: its first emission index (rows mode, DET)
   uint32_t* flags;          // [4]  [0]: prefiltered violation
   SortScratch sort;         // depth-sort scratch
   uint32_t* scan_parts;
-  uint32_t* pre_parts;      // [ceil(P/256)] tile-count sum of each preprocess workgroup
+  // [2 * ceil(P/256)] per preprocess workgroup: the sum of its exact tile counts, then (second
+  // half) the sum of its full 3-sigma tile rectangles -- the reference's tiles_touched
+  // (forward.cu:255), whose total is the num_rendered the boundary returns
+  uint32_t* pre_parts;
   size_t bytes;
 };
 GeomState carve_geom(char* base, size_t P);
@@ -160,13 +167,21 @@ struct BinState {
   uint32_t* tkey_b;
   uint32_t* tval_b;
   SortScratch sort;  // tile-sort scratch
-  // deterministic backward only (gsr.h, debug bit 1): the tile sort carries each instance's
-  // emission index e (depth order, Gaussian-major) instead of its Gaussian id
+  // rows layout (bwd_rows_mode() or the deterministic backward, gsr.h debug bit 1): the tile
+  // sort carries each instance's emission index e (depth order, Gaussian-major) instead of its
+  // Gaussian id, and the backward blend stores one gradient row per instance instead of float
+  // atomics
   uint32_t* egid;    // [R] Gaussian id of emission index e
   float* partial;    // [R][kAccFloats] the blend backward's gradient row of each instance, by e
   size_t bytes;
 };
-BinState carve_bin(char* base, size_t R, bool det = false);
+BinState carve_bin(char* base, size_t R, bool rows = false);
+// Backward gradient path (process-wide, env GSR_BWD_ROWS, default 1): true = the backward blend
+// stores one 64-B gradient row per (splat, tile) instance (plain coalesced stores, no global float
+// atomics) and the backward preprocess sums each Gaussian's rows (contiguous in emission order);
+// false = float atomics into one accumulator row per Gaussian.  The deterministic backward always
+// uses rows.  Fixed for the process, so a forward's layout is the one its backward expects.
+bool bwd_rows_mode();
 
 struct ImgState {
   float* final_T;       // [H*W]
@@ -207,7 +222,7 @@ struct PreArgs {
   // backward's per-Gaussian gradient accumulator rows g.acc
   SideClear clear;
   int acc_zero;
-  uint32_t* parts;  // [gridDim.x] sum of the workgroup's tile counts
+  uint32_t* parts;  // [2 * gridDim.x] sums of the workgroup's exact / full-rectangle tile counts
   // multi-view colour pre-pass (fused only): when non-null, the SH colour of this view and its
   // clamp bits come precomputed (gsr_sh_precolor) instead of being evaluated from the SH rows
   const float* pre_color;
@@ -260,6 +275,12 @@ struct BwdPreArgs {
   const float* pre_jac;
   // the forward's status word (ImgState::status): non-zero -> NaN gradients (same-call poison)
   const uint32_t* status;
+  // rows layout: Gaussian i's gradient row is the sum of rows[ebeg[i] .. ebeg[i] + count[i])
+  // (its instances' rows in emission order) instead of acc[i]
+  int use_rows;
+  const float4* rows;
+  const uint32_t* ebeg;
+  const uint32_t* count;
 };
 hipError_t launch_preprocess_backward(const BwdPreArgs& a, hipStream_t s);
 constexpr int kShFlushMaxViews = 8;
@@ -275,16 +296,20 @@ hipError_t launch_sh_grad_flush(const ShFlushArgs& a, hipStream_t s);
 // ---- binning (gsr_binning.hip) -------------------------------------------------------------------
 // The duplicate grid also zero-fills clear0 / clear1 (the tile sort's scratch, the ranges).
 // R bounds the writes (offsets of a complete depth order never exceed it).
+// egid != nullptr (rows layout): tval gets emission indices, egid[e] the Gaussian id and
+// ebeg[gid] the Gaussian's first emission index.
 hipError_t launch_duplicate(int P, const uint32_t* order, const uint32_t* offsets,
                             const int32_t* radii, const float4* rec, uint32_t gx, uint32_t gy,
                             uint32_t* tkey, uint32_t* tval, uint32_t R, SideClear clear0,
-                            SideClear clear1, hipStream_t s, uint32_t* egid = nullptr);
+                            SideClear clear1, hipStream_t s, uint32_t* egid = nullptr,
+                            uint32_t* ebeg = nullptr);
 // ranges_cleared: the ranges are already zero (duplicate's side clear): no memset launch.
 // Also writes the call's status word from the depth / tile sorts' error words (either may be null).
+// A failed call also or-s its status into `fault` (forward_faults_word(), may be null).
 hipError_t launch_tile_ranges(size_t R, const uint32_t* sorted_tiles, uint2* ranges,
                               uint32_t ntiles, const uint32_t* depth_err, const uint32_t* tile_err,
-                              uint32_t* status, uint32_t* host_status, hipStream_t s,
-                              bool ranges_cleared = false);
+                              uint32_t* status, uint32_t* host_status, uint32_t* fault,
+                              hipStream_t s, bool ranges_cleared = false);
 
 // ---- blend (gsr_render.hip) ----------------------------------------------------------------------
 struct RenderArgs {
@@ -304,6 +329,7 @@ struct RenderArgs {
   int sched;
   uint32_t* status;  // ImgState::status: non-zero -> NaN outputs; kStatusClamp or-ed on a clamp
   uint32_t* host_status;  // pinned, device-mapped mirror of the clamp bit (may be null)
+  uint32_t* fault;        // forward_faults_word() (may be null): kStatusClamp or-ed on a clamp
 };
 hipError_t launch_render_forward(const RenderArgs& a, hipStream_t s);
 
@@ -323,16 +349,14 @@ struct RenderBwdArgs {
   int include_feature;
   uint32_t* order;
   int sched;
-  // deterministic backward: per-instance rows partial[einst[q]] instead of atomics into acc
+  // rows layout: per-instance rows partial[einst[q]] instead of atomics into acc; det selects
+  // the deterministic summation order of the four waves' contributions (gsr.h debug bit 1)
   const uint32_t* einst;  // [R] emission index of tile-sorted instance q
   float* partial;         // [R][kAccFloats]
+  int det;
 };
 hipError_t launch_render_backward(const RenderBwdArgs& a, hipStream_t s);
-// deterministic backward: acc[order[s]] = sum over the instances e of depth-ordered Gaussian s
-// (e in [offsets[s-1], offsets[s]), increasing e) of partial[e]
-hipError_t launch_det_reduce(int P, const uint32_t* order, const uint32_t* offsets,
-                             const float* partial, uint32_t R, float* acc, hipStream_t s);
-// deterministic forward: point_list[q] = egid[einst[q]]
+// rows layout forward: point_list[q] = egid[einst[q]]
 hipError_t launch_det_gather(size_t R, const uint32_t* einst, const uint32_t* egid,
                              uint32_t* point_list, hipStream_t s);
 

@@ -25,15 +25,18 @@ constexpr int kThreads = 256;
 #define GSR_PRE_HOIST 0
 #endif
 
-// One Gaussian; returns its tile count (0 when culled) and writes its splat record to rec[0..3]
-// (the workgroup's LDS staging row; all zero when culled: such a record is never read).
+// One Gaussian; returns its exact tile count (0 when culled), sets rect_tiles to the tile count of
+// its full 3-sigma rectangle (the reference's tiles_touched, forward.cu:255; 0 when culled) and
+// writes its splat record to rec[0..3] (the workgroup's LDS staging row; all zero when culled:
+// such a record is never read).
 // pm / ps / pl: this Gaussian's 3 floats of means3D / scales / sh_language (LDS-staged rows with
 // GSR_PRE_STAGE, else the global rows; ps / pl are only read when the arrays are in use)
 __device__ __forceinline__ uint32_t preprocess_gaussian(const PreArgs& a, int idx, float4* rec,
                                                         const float* pm, const float* ps,
-                                                        const float* pl) {
+                                                        const float* pl, uint32_t& rect_tiles) {
 #pragma unroll
   for (int k = 0; k < 4; k++) rec[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+  rect_tiles = 0;
 #if GSR_PRE_HOIST
   // the small per-Gaussian inputs are all put in flight before the first dependent computation
   // (the compiler cannot hoist loads above the cull branches itself)
@@ -142,6 +145,7 @@ __device__ __forceinline__ uint32_t preprocess_gaussian(const PreArgs& a, int id
   }
   const float depth = p_view.z;
   a.radii[idx] = r;
+  rect_tiles = (y1 - y0) * (x1 - x0);
   // Exact tile list: the reference emits every tile of the 3-sigma square (forward.cu:255); tiles
   // in which no pixel can reach alpha >= 1/255 are dropped here (no output bit changes)
   const float qc = splat_q_cut(con_a, con_b, con_c, op);
@@ -214,11 +218,18 @@ __global__ __launch_bounds__(kThreads) void preprocess_kernel(PreArgs a) {
   const float* ps = a.scales + 3 * (size_t)idx;
   const float* pl = a.sh_language + 3 * (size_t)idx;
 #endif
-  uint32_t count = idx < a.P ? preprocess_gaussian(a, idx, s_rec + threadIdx.x * kRecStride, pm, ps, pl) : 0u;
+  uint32_t rect = 0;
+  uint32_t count = idx < a.P ? preprocess_gaussian(a, idx, s_rec + threadIdx.x * kRecStride, pm, ps, pl, rect) : 0u;
 #pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) count += (uint32_t)__shfl_xor((int)count, d, 64);
-  __shared__ uint32_t s_sum[kThreads / 64];
-  if ((threadIdx.x & 63) == 0) s_sum[threadIdx.x >> 6] = count;
+  for (int d = 32; d >= 1; d >>= 1) {
+    count += (uint32_t)__shfl_xor((int)count, d, 64);
+    rect += (uint32_t)__shfl_xor((int)rect, d, 64);
+  }
+  __shared__ uint32_t s_sum[kThreads / 64], s_rect[kThreads / 64];
+  if ((threadIdx.x & 63) == 0) {
+    s_sum[threadIdx.x >> 6] = count;
+    s_rect[threadIdx.x >> 6] = rect;
+  }
   __syncthreads();
   {
     float4* out = a.g.rec + 4 * (size_t)base;
@@ -231,10 +242,14 @@ __global__ __launch_bounds__(kThreads) void preprocess_kernel(PreArgs a) {
       z[q] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
   if (threadIdx.x == 0) {
-    uint32_t t = 0;
+    uint32_t t = 0, tr = 0;
 #pragma unroll
-    for (int w = 0; w < kThreads / 64; w++) t += s_sum[w];
+    for (int w = 0; w < kThreads / 64; w++) {
+      t += s_sum[w];
+      tr += s_rect[w];
+    }
     a.parts[blockIdx.x] = t;
+    a.parts[gridDim.x + blockIdx.x] = tr;
   }
 }
 

@@ -222,6 +222,7 @@ __global__ __launch_bounds__(kThreads) void render_fwd_kernel(RenderArgs a) {
       if (pid >= a.P) {  // memory-safe clamp, reported to this call's status check
         atomicOr(a.status, kStatusClamp);
         if (a.host_status) *a.host_status = kStatusClamp;  // sort bits are 0 on this path
+        if (a.fault) atomicOr(a.fault, kStatusClamp);
       }
       const uint32_t gid = min(pid, a.P - 1u);
       const float4* rec = a.rec + 4 * (size_t)gid;
@@ -427,8 +428,13 @@ __device__ __forceinline__ int reduce16_slot(int lane, SwapOrient o) {
 // workgroups per CU.
 constexpr int kAccDet = 13;
 
-template <bool EXTRA, bool FEAT, int GROUP, bool DET>
+// ROWS (rows layout, gsr_internal.h bwd_rows_mode): the flush STORES every (splat, tile) row to
+// partial[emission index] -- one coalesced 64-B row per instance, no global float atomics (they
+// execute at the memory side at ~1.3 TB/s chip-wide, MI355X_MICROARCH.md "Global float atomics")
+// -- and the backward preprocess sums each Gaussian's rows.  DET implies ROWS.
+template <bool EXTRA, bool FEAT, int GROUP, bool DET, bool ROWS>
 __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
+  static_assert(!DET || ROWS, "the deterministic backward stores per-instance rows");
   __shared__ float4 s_r0[kThreads];
   __shared__ float4 s_r1[kThreads];
   __shared__ float4 s_r2[kThreads];
@@ -709,17 +715,27 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
           if (k < kAccDet)
 #pragma unroll
             for (int w = 0; w < 4; w++) s_acc[(w * kThreads + jj) * kRow + k] = 0.0f;
+        } else if (ROWS) {  // every slot stored (16 lanes = one 64-B row), then re-zeroed
+          const uint32_t q = range.x + tile_last - 1 - done_cnt - jj;
+          const float v = s_acc[jj * kAccPad + k];
+          a.partial[(size_t)a.einst[q] * kAccFloats + k] = v;
+          s_acc[jj * kAccPad + k] = 0.0f;
         } else {
           const float v = s_acc[jj * kAccPad + k];
           if (v != 0.0f) {
+#if GSR_BWD_DIAG == 2
+            // diagnostic build only (wrong gradients): the flush's traffic as plain stores
+            a.acc[(size_t)s_gid[jj] * kAccFloats + k] = v;
+#else
             atomicAdd(&a.acc[(size_t)s_gid[jj] * kAccFloats + k], v);
+#endif
             s_acc[jj * kAccPad + k] = 0.0f;
           }
         }
       }
     }
   }
-  if (DET) {  // instances behind the tile's last contributor: zero rows
+  if (ROWS) {  // instances behind the tile's last contributor: zero rows
     const uint32_t n = range.y - range.x - min(tile_last, range.y - range.x);
     for (uint32_t idx = threadIdx.x; idx < n * kAccFloats; idx += kThreads)
       a.partial[(size_t)a.einst[range.x + tile_last + idx / kAccFloats] * kAccFloats +
@@ -876,6 +892,7 @@ __global__ __launch_bounds__(kThreads, GSR_FWD_BLK_WAVES) void render_fwd_blk_ke
       if (pid >= a.P) {  // memory-safe clamp, reported to this call's status check
         atomicOr(a.status, kStatusClamp);
         if (a.host_status) *a.host_status = kStatusClamp;
+        if (a.fault) atomicOr(a.fault, kStatusClamp);
       }
       const uint32_t gid = min(pid, a.P - 1u);
       const float4* rec = a.rec + 4 * (size_t)gid;
@@ -1071,12 +1088,14 @@ hipError_t launch_render_backward(const RenderBwdArgs& a, hipStream_t s) {
                        a.tile_last, ntiles, a.order);
 #define GSR_BWD(E, F)                                                                             \
   do {                                                                                           \
-    if (a.partial)                                                                               \
-      hipLaunchKernelGGL((render_bwd_kernel<E, F, 4, true>), dim3(ntiles), dim3(kThreads), 0, s, a); \
+    if (a.partial && a.det)                                                                      \
+      hipLaunchKernelGGL((render_bwd_kernel<E, F, 4, true, true>), dim3(ntiles), dim3(kThreads), 0, s, a); \
+    else if (a.partial)                                                                          \
+      hipLaunchKernelGGL((render_bwd_kernel<E, F, 4, false, true>), dim3(ntiles), dim3(kThreads), 0, s, a); \
     else if (group == 1)                                                                         \
-      hipLaunchKernelGGL((render_bwd_kernel<E, F, 1, false>), dim3(ntiles), dim3(kThreads), 0, s, a); \
+      hipLaunchKernelGGL((render_bwd_kernel<E, F, 1, false, false>), dim3(ntiles), dim3(kThreads), 0, s, a); \
     else                                                                                         \
-      hipLaunchKernelGGL((render_bwd_kernel<E, F, 4, false>), dim3(ntiles), dim3(kThreads), 0, s, a); \
+      hipLaunchKernelGGL((render_bwd_kernel<E, F, 4, false, false>), dim3(ntiles), dim3(kThreads), 0, s, a); \
   } while (0)
   if (feat) GSR_BWD(true, true);
   else if (extra) GSR_BWD(true, false);

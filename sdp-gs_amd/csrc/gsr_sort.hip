@@ -9,6 +9,8 @@
 // sort is one-sweep (one launch per 8-bit pass with a decoupled look-back over agent-scope status
 // words, see below), whose in-workgroup ranking uses wave64 ballots ("match" of the digit)
 // instead of shared-memory per-thread counters.
+#include <atomic>
+
 #include "gsr_internal.h"
 
 namespace gsr {
@@ -151,6 +153,11 @@ constexpr uint64_t kStOne = 1ull << 32;  // one contributor in a super-partition
 __device__ uint32_t g_lookback_timeouts;
 // test hook (gsr_test_force_sort_timeout): every look-back behaves as if its spin bound ran out
 __device__ uint32_t g_force_lookback_timeout;
+// Sticky per-device fault word (kStatus* bits of every failed forward since the last
+// gsr_reset_forward_faults): set by the tile-ranges kernel and the forward blend; the fused Adam
+// step reads it and leaves the parameters and moments untouched while it is non-zero, so NaN
+// gradients of a failed call never reach them (the reference __trap()s, auxiliary.h:156-160).
+__device__ uint32_t g_forward_faults;
 #ifndef GSR_SORT_TRACE
 #define GSR_SORT_TRACE 0
 #endif
@@ -485,41 +492,43 @@ __global__ __launch_bounds__(NT, NT == 1024 ? 8 : (NT == 512 ? 6 : 1)) void radi
 }
 
 // One workgroup: *out = sum of the n partials (n <= kScanMaxParts).
-// with_timeouts: out[1] = the sticky look-back timeout counter (same read-back as the total).
+// out[0] = sum of parts[0..n); with parts2: out[1] = sum of parts2[0..n) (the forward's exact
+// instance count and the reference's full-rectangle count, gsr_api.cpp, one read-back for both).
 __global__ __launch_bounds__(1024) void sum_parts_kernel(const uint32_t* __restrict__ parts, int n,
                                                          uint32_t* __restrict__ out,
-                                                         int with_timeouts) {
-  __shared__ uint32_t lds[16];
-  uint32_t s = 0;
-  for (int i = (int)threadIdx.x; i < n; i += 1024) s += parts[i];
-  uint32_t total;
+                                                         const uint32_t* __restrict__ parts2) {
+  __shared__ uint32_t lds[16], lds2[16];
+  uint32_t s = 0, s2 = 0;
+  for (int i = (int)threadIdx.x; i < n; i += 1024) {
+    s += parts[i];
+    if (parts2) s2 += parts2[i];
+  }
+  uint32_t total, total2 = 0;
   block_excl_scan<16>(s, lds, total);
+  if (parts2) block_excl_scan<16>(s2, lds2, total2);  // kernel-argument (uniform) branch
   if (threadIdx.x == 0) {
     out[0] = total;
-    if (with_timeouts)
-      out[1] = __hip_atomic_load(&g_lookback_timeouts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (parts2) out[1] = total2;
   }
 }
-
 }  // namespace
 
 hipError_t sum_u32_parts(const uint32_t* parts, size_t n, uint32_t* out, hipStream_t s,
-                         bool with_timeouts) {
+                         const uint32_t* parts2) {
   if (n > 0x7fffffffull) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(sum_parts_kernel, dim3(1), dim3(1024), 0, s, parts, (int)n, out,
-                     with_timeouts ? 1 : 0);
+  hipLaunchKernelGGL(sum_parts_kernel, dim3(1), dim3(1024), 0, s, parts, (int)n, out, parts2);
   return hipGetLastError();
 }
 
 hipError_t reduce_u32(const uint32_t* in, size_t n, uint32_t* parts, uint32_t* out,
-                      hipStream_t s, bool with_timeouts) {
+                      hipStream_t s) {
   if (n == 0) return hipMemsetAsync(out, 0, sizeof(uint32_t), s);
   const size_t np = scan_parts(n);
   if (np > (size_t)kScanMaxParts) return hipErrorInvalidValue;
   hipLaunchKernelGGL(scan_reduce_kernel<false>, dim3((unsigned)np), dim3(kThreads), 0, s, in,
                      (const uint32_t*)nullptr, n, parts);
   hipLaunchKernelGGL(sum_parts_kernel, dim3(1), dim3(1024), 0, s, parts, (int)np, out,
-                     with_timeouts ? 1 : 0);
+                     (const uint32_t*)nullptr);
   return hipGetLastError();
 }
 
@@ -553,6 +562,31 @@ extern "C" int gsr_test_sort_trace(uint64_t* out, int parts) {
 extern "C" int gsr_test_force_sort_timeout(int on) {
   const uint32_t v = on ? 1u : 0u;
   return hipMemcpyToSymbol(HIP_SYMBOL(g_force_lookback_timeout), &v, sizeof(v)) == hipSuccess ? 0 : 2;
+}
+
+uint32_t* forward_faults_word() {
+  // the symbol's address on the current device, looked up once per device
+  constexpr int kMaxDev = 64;
+  static std::atomic<uint32_t*> cache[kMaxDev];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return nullptr;
+  uint32_t* w = cache[dev].load(std::memory_order_relaxed);
+  if (w) return w;
+  void* p = nullptr;
+  if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_forward_faults)) != hipSuccess) return nullptr;
+  cache[dev].store((uint32_t*)p, std::memory_order_relaxed);
+  return (uint32_t*)p;
+}
+
+extern "C" int gsr_forward_faults(void) {
+  uint32_t v = 0;
+  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_forward_faults), sizeof(v)) != hipSuccess) return -1;
+  return (int)v;
+}
+
+extern "C" int gsr_reset_forward_faults(void) {
+  const uint32_t v = 0;
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_forward_faults), &v, sizeof(v)) == hipSuccess ? 0 : 2;
 }
 
 uint32_t* sort_timeouts_word() {

@@ -31,11 +31,6 @@ def _p(t):
     return None if t is None else t.data_ptr()
 
 
-# deterministic-backward mode of each live forward, keyed by its binning buffer: the backward must
-# pass the forward's flags (include/gsr.h GSR_DEBUG_DETERMINISTIC), whatever the mode is by then
-_FWD_FLAGS = {}
-
-
 def _forward_flags(debug):
     from . import _debug_flags
     return _debug_flags(debug)
@@ -73,11 +68,27 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
         holder.release()
     empty = torch.empty((0,), dtype=torch.uint8, device=dev)
     geom, binning, img = (b if b is not None else empty for b in holder.bufs)
-    if binning.numel():
-        if len(_FWD_FLAGS) > 4096:  # forwards whose backward never ran (inference)
-            _FWD_FLAGS.clear()
-        _FWD_FLAGS[binning.data_ptr()] = flags
     return int(nr.value), out_color, radii, geom, binning, img
+
+
+def _binning_is_deterministic(binning, R) -> bool:
+    """The forward's binning layout travels with its binning buffer, by size (include/gsr.h
+    gsr_binning_buffer_bytes / _det): no table of live forwards to keep or evict.  When the
+    default layout is the per-instance-rows one (GSR_BWD_ROWS=1) both sizes are equal and the
+    bit only selects the deterministic summation order, so the current mode is used; otherwise
+    the deterministic layout is recognised by its larger size (for every R > 0)."""
+    if binning is None or int(R) <= 0:
+        return False
+    L = _lib.load()
+    n = int(binning.numel())
+    det_n = int(L.gsr_binning_buffer_bytes_det(int(R)))
+    std_n = int(L.gsr_binning_buffer_bytes(int(R)))
+    if n not in (det_n, std_n):
+        raise RuntimeError("binningBuffer does not belong to a forward with this num_rendered")
+    if det_n == std_n:
+        from . import deterministic
+        return deterministic()
+    return n == det_n
 
 
 def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rotations,
@@ -107,8 +118,7 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     g = geomBuffer if geomBuffer.numel() else None
     b = binningBuffer if binningBuffer.numel() else None
     i = imageBuffer if imageBuffer.numel() else None
-    flags = (int(bool(debug)) | (_FWD_FLAGS.pop(b.data_ptr(), 0) & 2)) if b is not None \
-        else int(bool(debug))
+    flags = int(bool(debug)) | (2 if _binning_is_deterministic(b, R) else 0)
     with torch.cuda.device(dev):
         rc = _lib.load().gsr_rasterize_gaussians_backward(
             P, M, int(R), _p(bg), _p(m3), _p(rad), _p(col), _p(sc), _p(rot), float(scale_modifier),

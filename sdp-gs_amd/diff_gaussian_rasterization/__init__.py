@@ -25,9 +25,10 @@ from gsr_amd import _lib  # noqa: E402
 __all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians",
            "rasterize_gaussians_extended", "rasterize_gaussians_fused", "mark_visible"]
 
-# instance count of the most recent forward (the reference keeps it in ctx.num_rendered only);
-# read by bench.py to compute per-kernel algorithmic bytes
-LAST_STATS = {"num_rendered": 0, "P": 0}
+# counts of the most recent forward: num_rendered is the reference's value (the boundary's first
+# return value, kept in ctx.num_rendered), num_instances the tile instances actually binned after
+# the exact tile cull (include/gsr.h gsr_last_forward_instances; bench.py's algorithmic bytes)
+LAST_STATS = {"num_rendered": 0, "num_instances": 0, "P": 0}
 
 
 def cpu_deep_copy_tuple(input_tuple):
@@ -145,6 +146,7 @@ class _RasterizeGaussians(torch.autograd.Function):
             holder.release()
         num_rendered = int(nr.value)
         LAST_STATS["num_rendered"] = num_rendered
+        LAST_STATS["num_instances"] = int(L.gsr_last_forward_instances())
         LAST_STATS["P"] = P
 
         ctx.raster_settings = rs
@@ -308,6 +310,7 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
             holder.release()
         num_rendered = int(nr.value)
         LAST_STATS["num_rendered"] = num_rendered
+        LAST_STATS["num_instances"] = int(L.gsr_last_forward_instances())
         LAST_STATS["P"] = P
 
         ctx.raster_settings = rs

@@ -60,20 +60,26 @@ class on_device:
 
 
 class on_stream:
-    """`with torch.cuda.stream(s)` for a stream of the current device."""
-    __slots__ = ("stream", "prev")
+    """`with torch.cuda.stream(s)`: makes `s` the current stream of its device.  torch.cuda.
+    set_stream also makes that device current, so the previous current device is restored on
+    exit when it was another one (as torch.cuda.stream does)."""
+    __slots__ = ("stream", "prev", "prev_dev")
 
     def __init__(self, stream):
         self.stream = stream
         self.prev = None
+        self.prev_dev = -1
 
     def __enter__(self):
+        self.prev_dev = torch._C._cuda_getDevice()
         self.prev = torch.cuda.current_stream(self.stream.device)
         torch.cuda.set_stream(self.stream)
         return self.stream
 
     def __exit__(self, *exc):
         torch.cuda.set_stream(self.prev)
+        if torch._C._cuda_getDevice() != self.prev_dev:
+            torch._C._cuda_setDevice(self.prev_dev)
         return False
 
 
@@ -219,7 +225,11 @@ def load():
         L.gsr_forward_status.argtypes = [_p, _i]
         L.gsr_check_forwards.restype = _i
         L.gsr_check_forwards.argtypes = [_i]
-        for n in ("gsr_geom_buffer_bytes", "gsr_binning_buffer_bytes"):
+        for n in ("gsr_last_forward_instances", "gsr_forward_faults", "gsr_reset_forward_faults"):
+            getattr(L, n).restype = _i
+            getattr(L, n).argtypes = []
+        for n in ("gsr_geom_buffer_bytes", "gsr_binning_buffer_bytes",
+                  "gsr_binning_buffer_bytes_det"):
             getattr(L, n).restype = _sz
             getattr(L, n).argtypes = [_i]
         L.gsr_image_buffer_bytes.restype = _sz
@@ -239,6 +249,8 @@ def load():
         L.gsr_test_expf_pair.argtypes = [_p, _p, _p, _sz, _p]
         L.gsr_test_force_sort_timeout.restype = _i
         L.gsr_test_force_sort_timeout.argtypes = [_i]
+        L.gsr_test_binning_lists.restype = _i
+        L.gsr_test_binning_lists.argtypes = [_p, _p, _i, _i, _i, _i, _i, _p, _p, _p]
         L.gsr_test_activations.restype = _i
         L.gsr_test_activations.argtypes = [_p, _p, _p, _sz, _p, _p, _p, _p]
         L.gsr_profile_enable.restype = None
@@ -260,6 +272,17 @@ def check(rc: int):
     if rc != 0:
         msg = load().gsr_last_error().decode(errors="replace")
         raise GsrError(f"libgsr error {rc}: {msg}")
+
+
+def forward_faults() -> int:
+    """The device's sticky forward fault word (include/gsr.h gsr_forward_faults; synchronous)."""
+    return int(load().gsr_forward_faults())
+
+
+def reset_forward_faults():
+    """Clear the fault word (after a failure has been handled); FusedAdam steps again."""
+    if load().gsr_reset_forward_faults() != 0:
+        raise GsrError("gsr_reset_forward_faults failed")
 
 
 def check_forwards(wait: bool = True):

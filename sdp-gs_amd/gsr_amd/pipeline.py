@@ -73,6 +73,11 @@ class ViewPipeline:
         (software-pipelined issue: the next view's latency-bound binning is queued before this
         view's full-chip backward blend).  Returns bwd's results."""
         import diff_gaussian_rasterization as dgr
+        if reducer is not None and self.defer_sh and model is None:
+            # the early all-reduce must leave out the SH leaves, whose deferred gradients are only
+            # written by the flush at the end of the step; without the model they are unknown
+            raise ValueError("ViewPipeline.run: a reducer with defer_sh needs model= (the SH "
+                             "leaves are reduced after the deferred flush)")
         items = list(items)
         main = torch.cuda.current_stream(self.device)
         streams = [main] + self.side

@@ -79,6 +79,15 @@ def densify_step(model, args: OptArgs, iteration: int, extent: float, generator=
                             iteration, args.include_feature, generator=generator)
 
 
+def _guard_step():
+    """Before the optimizer step: raise if a forward of this step already reported a failure
+    (non-blocking, include/gsr.h gsr_check_forwards).  A failure not yet published by then is
+    caught on the device: FusedAdam leaves the parameters and moments untouched while the
+    device's forward fault word is set (include/gsr_optim.h), and the next check raises."""
+    import diff_gaussian_rasterization as dgr
+    dgr.check_forwards(wait=False)
+
+
 def train_iteration(model, cam, gt_image, depth_mono, bg, args: OptArgs, iteration: int,
                     extent: float, pipe=None):
     """One reference iteration on one camera.  Returns the loss tensor (not synchronised)."""
@@ -93,6 +102,7 @@ def train_iteration(model, cam, gt_image, depth_mono, bg, args: OptArgs, iterati
                                              pkg["visibility_filter"])
             if _densify_due(iteration, args):
                 densify_step(model, args, iteration, extent)
+        _guard_step()
         model.optimizer.step()
         model.optimizer.zero_grad(set_to_none=True)
     return loss.detach()
@@ -138,5 +148,6 @@ def train_step_views(model, cams: Sequence, gt_images: Sequence[torch.Tensor],
             densify_step(model, args, iteration, extent, generator=generator)
         # after a densification the new parameters have no .grad: Adam skips them, as in the
         # reference (train.py:223-231)
+        _guard_step()
         model.optimizer.step()
     return losses

@@ -57,12 +57,133 @@ def test_forced_sort_timeout_fails_the_same_call():
     with pytest.raises(_lib.GsrError, match="look-back timed out"):
         dgr.check_forwards(wait=True)
 
+    # both failures are in the device's sticky fault word (FusedAdam skips while it is set)
+    assert _lib.forward_faults() & 1
+    _lib.reset_forward_faults()
+    assert _lib.forward_faults() == 0
+
     # the hook cleared: a normal call is finite, its backward runs, and the checks are clean
     (color, depth, alpha, feature, radii), inp = _call()
     (color.sum() + depth.sum()).backward()
     torch.cuda.synchronize()
     assert torch.isfinite(color).all() and torch.isfinite(inp["means3D"].grad).all()
     dgr.check_forwards(wait=True)
+    assert _lib.forward_faults() == 0
+
+
+def _forced_failure(fn):
+    """Run fn() with every look-back forced to give up; returns its result."""
+    from gsr_amd import _lib
+    L = _lib.load()
+    _lib.check(L.gsr_test_force_sort_timeout(1))
+    try:
+        return fn()
+    finally:
+        _lib.check(L.gsr_test_force_sort_timeout(0))
+
+
+def test_backward_of_a_failed_forward_poisons_every_gradient():
+    """a backward that runs although its forward failed (here: the failure was already
+    reported by check_forwards, so the host-side check on entry passes) writes NaN to EVERY
+    gradient it returns -- store mode through the reference's `_C` signature (all 8 outputs), and
+    accumulate mode (grad-into-leaves into pre-filled .grad) through render()'s fused path."""
+    import numpy as np
+    from gsr_amd import _lib
+    import diff_gaussian_rasterization as dgr
+    from diff_gaussian_rasterization import _C
+    dgr.check_forwards(wait=True)
+    kw = scene(P=60_000, W=320, H=240, seed=3, mode="sh", feature=None)
+    d = lambda x: torch.tensor(np.asarray(x), device="cuda")  # noqa: E731
+    E = torch.Tensor([]).cuda()
+    P = kw["means3D"].shape[0]
+    nr, color, radii, geom, binning, img = _forced_failure(lambda: _C.rasterize_gaussians(
+        d(kw["bg"]), d(kw["means3D"]), E, d(kw["opacities"]).view(P, 1), d(kw["scales"]),
+        d(kw["rotations"]), 1.0, E, d(kw["viewmatrix"]), d(kw["projmatrix"]), kw["tanfovx"],
+        kw["tanfovy"], kw["image_height"], kw["image_width"], d(kw["shs"]), kw["sh_degree"],
+        d(kw["campos"]), False, False))
+    torch.cuda.synchronize()
+    with pytest.raises(_lib.GsrError):
+        dgr.check_forwards(wait=True)
+    dpix = torch.randn_like(color)
+    grads = _C.rasterize_gaussians_backward(
+        d(kw["bg"]), d(kw["means3D"]), radii, E, d(kw["scales"]), d(kw["rotations"]), 1.0, E,
+        d(kw["viewmatrix"]), d(kw["projmatrix"]), kw["tanfovx"], kw["tanfovy"], dpix,
+        d(kw["shs"]), kw["sh_degree"], d(kw["campos"]), geom, nr, binning, img, False)
+    torch.cuda.synchronize()
+    names = ["means2D", "colors", "opacity", "means3D", "cov3D", "sh", "scales", "rotations"]
+    for n, g in zip(names, grads):
+        assert torch.isnan(g).all(), n
+
+    # accumulate mode: the fused backward adds into the leaves' existing .grad
+    from gaussian_renderer import render
+    from gsr_amd.model import SplatModel
+    from gsr_amd.synthetic import make_cameras, make_gaussians
+    from fused_ref import LEAVES, Opt, Pipe
+    m = SplatModel(make_gaussians(60_000, sh_degree=3, seed=3), device="cuda")
+    cam = make_cameras(1, 320, 240, seed=3)[0].to("cuda")
+    for n in LEAVES:
+        getattr(m, n).grad = torch.ones_like(getattr(m, n))
+    prev = dgr.grad_into_leaves()
+    dgr.grad_into_leaves(True)
+    try:
+        pkg = _forced_failure(lambda: render(cam, m, Pipe(), torch.zeros(3, device="cuda"), Opt()))
+        torch.cuda.synchronize()
+        with pytest.raises(_lib.GsrError):
+            dgr.check_forwards(wait=True)
+        torch.autograd.backward([pkg["render"], pkg["depth"]],
+                                [torch.ones_like(pkg["render"]), torch.ones_like(pkg["depth"])])
+        torch.cuda.synchronize()
+    finally:
+        dgr.grad_into_leaves(prev)
+    for n in LEAVES:
+        assert torch.isnan(getattr(m, n).grad).all(), n
+    _lib.reset_forward_faults()
+
+
+def test_train_step_with_a_failed_forward_leaves_parameters_unchanged():
+    """NaN gradients of a failed forward never reach FusedAdam's parameters or
+    moments -- the trainer checks the published status before the step, and FusedAdam skips on
+    the device while the fault word is set (a failure not yet published by then)."""
+    from gsr_amd import _lib, trainer
+    from gsr_amd.model import SplatModel
+    from gsr_amd.synthetic import make_cameras, make_gaussians, training_targets
+    import diff_gaussian_rasterization as dgr
+    dgr.check_forwards(wait=True)
+    m = SplatModel(make_gaussians(60_000, sh_degree=3, seed=5), device="cuda")
+    args = trainer.OptArgs()
+    trainer.make_trainable(m, args)
+    cam = make_cameras(1, 320, 240, seed=5)[0].to("cuda")
+    gts, monos = training_targets(1, 240, 320, seed=2, device="cuda")
+    bg = torch.zeros(3, device="cuda")
+    before = [p.detach().clone() for p in m.parameters()]
+    raised = False
+    try:
+        _forced_failure(lambda: trainer.train_iteration(m, cam, gts[0], monos[0], bg, args, 1,
+                                                        2.78))
+        torch.cuda.synchronize()
+    except Exception:
+        raised = True
+    try:
+        dgr.check_forwards(wait=True)
+    except _lib.GsrError:
+        raised = True
+    assert raised
+    assert _lib.forward_faults() != 0
+    for p, b in zip(m.parameters(), before):
+        assert torch.equal(p.detach(), b)
+    # FusedAdam skips on the device as long as the fault word is set, even with a step issued
+    for p in m.parameters():
+        p.grad = torch.full_like(p, float("nan"))
+    m.optimizer.step()
+    torch.cuda.synchronize()
+    for p, b in zip(m.parameters(), before):
+        assert torch.equal(p.detach(), b)
+    _lib.reset_forward_faults()
+    m.optimizer.zero_grad(set_to_none=True)
+    trainer.train_iteration(m, cam, gts[0], monos[0], bg, args, 2, 2.78)
+    torch.cuda.synchronize()
+    assert any(not torch.equal(p.detach(), b) for p, b in zip(m.parameters(), before))
+    assert all(torch.isfinite(p).all() for p in m.parameters())
 
 
 def test_sh_deferral_flush_with_one_plane_grad_present():

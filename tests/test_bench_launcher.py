@@ -1,0 +1,60 @@
+"""bench.py --gpus N: the launcher path, on CPU.
+
+With --gpus N > 1 and no torch.distributed environment, bench.py starts
+`python -m torch.distributed.run --nproc-per-node N` as a child process (never an exec of a
+process that touched the GPU), relays rank 0's JSON line and exits non-zero when a rank fails.
+The ranks here are a stand-in script over gloo (the real ranks need the GPU)."""
+import json
+import os
+import subprocess
+import sys
+import textwrap
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+RANK_SCRIPT = textwrap.dedent("""
+    import json, os, sys
+    import torch, torch.distributed as dist
+    dist.init_process_group("gloo")
+    r, w = dist.get_rank(), dist.get_world_size()
+    t = torch.tensor([float(r + 1)])
+    dist.all_reduce(t)
+    if r == 0:
+        print("progress line that is not the result", flush=True)
+        print(json.dumps({"metric": "m", "value": float(t), "n_gpus": w,
+                          "argv": sys.argv[1:]}), flush=True)
+    dist.destroy_process_group()
+    sys.exit(int(os.environ.get("FAIL_RANK", "-1") == str(r)))
+""")
+
+
+def test_launch_ranks_relays_rank0_line(tmp_path):
+    import bench
+    script = tmp_path / "rank.py"
+    script.write_text(RANK_SCRIPT)
+    rc, line = bench.launch_ranks(["--steps", "2"], 2, script=str(script))
+    assert rc == 0
+    rec = json.loads(line)
+    assert rec["n_gpus"] == 2 and rec["value"] == 3.0 and rec["argv"] == ["--steps", "2"]
+
+
+def test_launch_ranks_reports_a_failed_rank(tmp_path):
+    import bench
+    script = tmp_path / "rank.py"
+    script.write_text(RANK_SCRIPT)
+    env = dict(os.environ, FAIL_RANK="1")
+    rc, line = bench.launch_ranks([], 2, script=str(script), env=env)
+    assert rc != 0
+
+
+def test_bench_gpus2_without_gpu_exits_nonzero():
+    """The real entry point takes the launcher branch (WORLD_SIZE unset) and propagates the ranks'
+    failure (no GPU here) as a non-zero exit without printing a result line."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["GSR_DIST_BACKEND"] = "gloo"
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps",
+                        "1", "--warmup", "0", "--no-cpu-baseline", "--no-extra-legs"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode != 0
+    assert '"metric"' not in p.stdout

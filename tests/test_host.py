@@ -86,3 +86,36 @@ def test_render_pkg_lazy_entries_behave_like_dict_items():
     import pytest
     with pytest.raises(KeyError):
         pkg2["nope"]
+
+
+def test_view_pipeline_reducer_with_deferral_needs_the_model():
+    """ADVICE r2: with deferred SH gradients the early all-reduce must leave the SH leaves out;
+    without the model they are unknown, so run() refuses (before any GPU work)."""
+    from gsr_amd.pipeline import ViewPipeline
+
+    class _Reducer:
+        def begin(self):
+            raise AssertionError("must not be reached")
+
+    vp = ViewPipeline(torch.device("cuda", 0), depth=1, defer_sh=True)
+    with pytest.raises(ValueError, match="model"):
+        vp.run([], lambda cam: cam, model=None, reducer=_Reducer())
+
+
+def test_C_shim_reads_the_deterministic_bit_from_the_binning_buffer():
+    """the `_C` shim's backward takes the forward's deterministic-backward bit from
+    the binning buffer's layout size, not from a bounded table of live forwards."""
+    from diff_gaussian_rasterization._C import _binning_is_deterministic
+    from gsr_amd import _lib
+    L = _lib.load()
+    import diff_gaussian_rasterization as dgr
+    for R in (1, 1000, 3_000_000):
+        det = torch.empty(int(L.gsr_binning_buffer_bytes_det(R)), dtype=torch.uint8)
+        std = torch.empty(int(L.gsr_binning_buffer_bytes(R)), dtype=torch.uint8)
+        if det.numel() == std.numel():  # rows layout by default: the current mode decides
+            assert _binning_is_deterministic(det, R) == dgr.deterministic()
+        else:
+            assert _binning_is_deterministic(det, R) and not _binning_is_deterministic(std, R)
+    with pytest.raises(RuntimeError):
+        _binning_is_deterministic(torch.empty(7, dtype=torch.uint8), 1000)
+    assert not _binning_is_deterministic(None, 0)

@@ -1,5 +1,5 @@
-"""The multi-GPU step's gradient plumbing on the HIP path, in one process (world size 1, gloo over
-the device tensors): gradient-as-bucket-view (the fused backward accumulates straight into the
+"""The multi-GPU step's gradient plumbing on the HIP path, in one process (world size 1, gloo
+and RCCL over the device tensors): gradient-as-bucket-view (the fused backward accumulates straight into the
 all-reduce buffer), the deferred SH flush written into the bucket in row slices, and the
 overlapped all-reduce of ViewPipeline.run(reducer=) give the gradients of the same step without a
 reducer (the collectives are issued at world size 1 too, so their stream ordering
@@ -54,18 +54,26 @@ def _step(model, cams, grads, views, reducer):
     return [p.grad.detach().clone() for p in model.parameters()]
 
 
-@pytest.fixture
-def gloo_world1(tmp_path):
+@pytest.fixture(params=["gloo", "nccl"])
+def world1(request, tmp_path):
+    """A world-size-1 process group.  gloo: every collective round-trips through host memory, so
+    a collective issued before its slice was flushed returns stale zeros.  nccl (= RCCL on ROCm):
+    the bench's multi-GPU backend -- its initialisation, its internal stream and the ordering of
+    each collective after the flush on the current stream run on the GPU."""
     init = "file://" + os.path.join(str(tmp_path), "pg")
-    dist.init_process_group("gloo", init_method=init, rank=0, world_size=1)
+    if request.param == "nccl":
+        dist.init_process_group("nccl", init_method=init, rank=0, world_size=1,
+                                device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group("gloo", init_method=init, rank=0, world_size=1)
     try:
-        yield
+        yield request.param
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("bucket_bytes", [64 << 20, 256 << 10])
-def test_bucket_view_grads_equal_plain_step(gloo_world1, bucket_bytes):
+def test_bucket_view_grads_equal_plain_step(world1, bucket_bytes):
     import diff_gaussian_rasterization as dgr
     from gsr_amd.parallel import GradAllReducer
     from gsr_amd.pipeline import ViewPipeline
@@ -93,5 +101,7 @@ def test_bucket_view_grads_equal_plain_step(gloo_world1, bucket_bytes):
             end = base + reducer.flat.numel() * 4
             assert all(base <= p.grad.data_ptr() < end for p in model.parameters())
         assert any(float(r.abs().max()) > 0 for r in ref)
+        if world1 == "nccl":
+            assert dist.get_backend() == "nccl"
     finally:
         dgr.grad_into_leaves(prev)
