@@ -735,6 +735,7 @@ static int backward_impl(
     rb.dL_dfeature = dL_dout_feature; rb.acc = g.acc; rb.include_feature = include_feature;
     rb.order = im.order; rb.sched = tile_schedule_mode();
     rb.einst = einst; rb.partial = rows ? b.partial : nullptr; rb.det = det ? 1 : 0;
+    rb.nrows = (uint32_t)R; rb.status = im.status;
     PROF_BEGIN(RENDER_BWD);
     GSR_CHECK(launch_render_backward(rb, stream));
     PROF_END(RENDER_BWD);

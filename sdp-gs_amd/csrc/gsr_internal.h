@@ -354,6 +354,10 @@ struct RenderBwdArgs {
   const uint32_t* einst;  // [R] emission index of tile-sorted instance q
   float* partial;         // [R][kAccFloats]
   int det;
+  // rows of partial (the binning capacity): emission indices are clamped to it, so the output of
+  // a sort that gave up cannot send a store out of bounds
+  uint32_t nrows;
+  const uint32_t* status;  // ImgState::status: a failed forward's backward blend writes nothing
 };
 hipError_t launch_render_backward(const RenderBwdArgs& a, hipStream_t s);
 // rows layout forward: point_list[q] = egid[einst[q]]

@@ -461,6 +461,9 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
   const size_t pix = (size_t)py * a.W + px;
   const size_t HW = (size_t)a.W * a.H;
 
+  // a failed forward (a sort gave up): its lists are not valid and the backward preprocess
+  // NaN-poisons every gradient; nothing is read from them here (grid-uniform)
+  if (ROWS && a.status && (*a.status & (kStatusDepthSort | kStatusTileSort))) return;
   const uint2 range = a.ranges[tile];
   const uint32_t tile_last = a.tile_last[tile];
   BLEND_STAT(8, 1);
@@ -711,14 +714,14 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
         if (DET) {  // every slot of the instance's row is stored (zeros too), then re-zeroed
           const uint32_t q = range.x + tile_last - 1 - done_cnt - jj;
           const float v = k < kAccDet ? s_acc[jj * kRow + k] : 0.0f;
-          a.partial[(size_t)a.einst[q] * kAccFloats + k] = v;
+          a.partial[(size_t)min(a.einst[q], a.nrows - 1u) * kAccFloats + k] = v;
           if (k < kAccDet)
 #pragma unroll
             for (int w = 0; w < 4; w++) s_acc[(w * kThreads + jj) * kRow + k] = 0.0f;
         } else if (ROWS) {  // every slot stored (16 lanes = one 64-B row), then re-zeroed
           const uint32_t q = range.x + tile_last - 1 - done_cnt - jj;
           const float v = s_acc[jj * kAccPad + k];
-          a.partial[(size_t)a.einst[q] * kAccFloats + k] = v;
+          a.partial[(size_t)min(a.einst[q], a.nrows - 1u) * kAccFloats + k] = v;
           s_acc[jj * kAccPad + k] = 0.0f;
         } else {
           const float v = s_acc[jj * kAccPad + k];
@@ -738,8 +741,8 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
   if (ROWS) {  // instances behind the tile's last contributor: zero rows
     const uint32_t n = range.y - range.x - min(tile_last, range.y - range.x);
     for (uint32_t idx = threadIdx.x; idx < n * kAccFloats; idx += kThreads)
-      a.partial[(size_t)a.einst[range.x + tile_last + idx / kAccFloats] * kAccFloats +
-                idx % kAccFloats] = 0.0f;
+      a.partial[(size_t)min(a.einst[range.x + tile_last + idx / kAccFloats], a.nrows - 1u) *
+                    kAccFloats + idx % kAccFloats] = 0.0f;
   }
 }
 

@@ -82,7 +82,8 @@ def _forced_failure(fn):
         _lib.check(L.gsr_test_force_sort_timeout(0))
 
 
-def test_backward_of_a_failed_forward_poisons_every_gradient():
+@pytest.mark.parametrize("det", [False, True])
+def test_backward_of_a_failed_forward_poisons_every_gradient(det):
     """a backward that runs although its forward failed (here: the failure was already
     reported by check_forwards, so the host-side check on entry passes) writes NaN to EVERY
     gradient it returns -- store mode through the reference's `_C` signature (all 8 outputs), and
@@ -92,6 +93,19 @@ def test_backward_of_a_failed_forward_poisons_every_gradient():
     import diff_gaussian_rasterization as dgr
     from diff_gaussian_rasterization import _C
     dgr.check_forwards(wait=True)
+    prev_det = dgr.deterministic()
+    dgr.deterministic(det)  # det: the per-instance-rows layout, whose indices the failed sort left
+    try:
+        _poison_case()
+    finally:
+        dgr.deterministic(prev_det)
+
+
+def _poison_case():
+    import numpy as np
+    from gsr_amd import _lib
+    import diff_gaussian_rasterization as dgr
+    from diff_gaussian_rasterization import _C
     kw = scene(P=60_000, W=320, H=240, seed=3, mode="sh", feature=None)
     d = lambda x: torch.tensor(np.asarray(x), device="cuda")  # noqa: E731
     E = torch.Tensor([]).cuda()
