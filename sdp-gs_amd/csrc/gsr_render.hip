@@ -81,7 +81,8 @@ __global__ __launch_bounds__(kSchedThreads) void tile_schedule_kernel(const uint
 #ifndef GSR_QUAD_WAVES
 #define GSR_QUAD_WAVES 1
 #endif
-// diagnostic builds (wrong gradients, timing only): 1 = no wave reduction of the pair terms
+// diagnostic builds (wrong gradients, timing only): 1 = no wave reduction of the pair terms,
+// 2 = the flush's global atomics as plain stores, 3 = no pair update / reduction at all
 #ifndef GSR_BWD_DIAG
 #define GSR_BWD_DIAG 0
 #endif
@@ -590,6 +591,11 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
       const bool contrib = cv[u];
       const uint64_t cmask = __ballot(contrib);
       if (cmask == 0ull) continue;  // wave-uniform skip
+#if GSR_BWD_DIAG == 3
+      // diagnostic build only (wrong gradients): no pair update / reduction -- what the batch
+      // loads, lists, alpha tests, barriers and flush cost by themselves
+      if (cmask != 0ull) continue;
+#endif
       BLEND_STAT(6, 1);
       BLEND_STAT(7, __popcll(cmask));
       // contributing-lane histogram of the backward's entries: <= 2, <= 4, <= 8, <= 16 lanes
