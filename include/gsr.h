@@ -188,8 +188,8 @@ int gsr_rasterize_gaussians_fused_backward(
 /* Deferred SH gradients for multi-view steps (gsr_amd/pipeline.py; no reference counterpart: the
  * reference steps after every view).  Same as gsr_rasterize_gaussians_fused_backward, but when
  * dL_dcolor_sh != NULL the SH gradients are NOT written (dL_dfeatures_dc / _rest may be NULL);
- * instead the clamp-masked colour gradient dL/dRGB of every Gaussian ([P,3], zeros when culled)
- * is stored there.  The SH gradient is basis(dir) x dL/dRGB (backward.cu:20-139), so
+ * instead the clamp-masked colour gradient dL/dRGB of every Gaussian (planar [3][P], zeros when
+ * culled) is stored there.  The SH gradient is basis(dir) x dL/dRGB (backward.cu:20-139), so
  * gsr_sh_grad_flush forms it for all deferred views of a step in one pass over the SH rows.
  * pre_jac (optional, needs dL_dcolor_sh): this view's colour Jacobian from gsr_sh_precolor; the
  * SH rows are then not read. */
@@ -235,11 +235,14 @@ int gsr_rasterize_gaussians_fused_precolor(
 /* dL/dfeatures_dc [P,1,3] and dL/dfeatures_rest [P,M-1,3] of nviews deferred views:
  * sum_v basis(normalize(means3D - campos[v])) x dL_dcolor_sh[v], coefficients above `degree`
  * zero; stored (accumulate = 0) or added (accumulate = 1).  campos / dL_dcolor_sh: HOST arrays
- * of nviews DEVICE pointers ([3] and [P,3]).  Views are summed in order in registers. */
+ * of nviews DEVICE pointers ([3] and planar dL/dRGB: channel c of Gaussian i at
+ * dL_dcolor_sh[v][c * rgb_plane_stride + i], rgb_plane_stride >= P, so a row slice [a, b) of a
+ * [3][P_total] plane is the pointer + a with the full stride).  Views are summed in order in
+ * registers. */
 int gsr_sh_grad_flush(int P, int M, int degree, const float* means3D, int nviews,
                       const float* const* campos, const float* const* dL_dcolor_sh,
-                      float* dL_dfeatures_dc, float* dL_dfeatures_rest, int accumulate,
-                      void* stream);
+                      int64_t rgb_plane_stride, float* dL_dfeatures_dc, float* dL_dfeatures_rest,
+                      int accumulate, void* stream);
 
 /* Replaces _C.mark_visible -> markVisible (rasterize_points.cu:198-217) -> checkFrustum
  * (rasterizer_impl.cu:54-66): present[i] = view-space z > 0.2 (bool as uint8). */

@@ -872,8 +872,8 @@ int gsr_sh_precolor(int P, int M, int degree, const float* means3D, const float*
 
 int gsr_sh_grad_flush(int P, int M, int degree, const float* means3D, int nviews,
                       const float* const* campos, const float* const* dL_dcolor_sh,
-                      float* dL_dfeatures_dc, float* dL_dfeatures_rest, int accumulate,
-                      void* stream_ptr) {
+                      int64_t rgb_plane_stride, float* dL_dfeatures_dc, float* dL_dfeatures_rest,
+                      int accumulate, void* stream_ptr) {
   g_err.clear();
   hipStream_t stream = (hipStream_t)stream_ptr;
   const int debug = 0;
@@ -883,11 +883,13 @@ int gsr_sh_grad_flush(int P, int M, int degree, const float* means3D, int nviews
     return fail(GSR_ERR_ARGUMENT, "invalid sh degree %d for M = %d", degree, M);
   if (!means3D || !campos || !dL_dcolor_sh || !dL_dfeatures_dc || (M > 1 && !dL_dfeatures_rest))
     return fail(GSR_ERR_ARGUMENT, "null pointer");
+  if (rgb_plane_stride < P) return fail(GSR_ERR_ARGUMENT, "rgb_plane_stride < P");
   for (int v0 = 0; v0 < nviews; v0 += kShFlushMaxViews) {
     ShFlushArgs a{};
     a.P = P; a.M = M; a.D = degree; a.means3D = means3D;
     a.nviews = nviews - v0 < kShFlushMaxViews ? nviews - v0 : kShFlushMaxViews;
     a.accumulate = (v0 > 0 || accumulate) ? 1 : 0;
+    a.rgb_stride = (size_t)rgb_plane_stride;
     for (int v = 0; v < a.nviews; v++) {
       if (!campos[v0 + v] || !dL_dcolor_sh[v0 + v]) return fail(GSR_ERR_ARGUMENT, "null view pointer");
       a.campos[v] = campos[v0 + v];

@@ -22,6 +22,11 @@ constexpr int kThreads = GSR_BWD_THREADS;  // Gaussians per workgroup (LDS stagi
 __device__ __forceinline__ void put3(float* p, size_t i, V3 v) {
   p[3 * i] = v.x; p[3 * i + 1] = v.y; p[3 * i + 2] = v.z;
 }
+// planar [3][P] store (the deferred dL/dRGB: every store instruction of a wave is one contiguous
+// 256-byte run, and so is every load of the step's SH flush)
+__device__ __forceinline__ void put3p(float* p, size_t P, size_t i, V3 v) {
+  p[i] = v.x; p[P + i] = v.y; p[2 * P + i] = v.z;
+}
 // store or accumulate (fused path with accumulate = 1 adds into existing .grad buffers)
 template <bool ACC>
 __device__ __forceinline__ void st(float* p, float v) {
@@ -100,7 +105,7 @@ __device__ __forceinline__ void poison_outputs(const BwdPreArgs& a, size_t i) {
   if (a.dL_dsh_language) st3<ACC>(a.dL_dsh_language, i, n3);
   if (a.dL_dlanguage_feature) st3<ACC>(a.dL_dlanguage_feature, i, n3);
   if (a.dRGB_out) {
-    put3(a.dRGB_out, i, n3);  // deferred: the step's SH flush spreads the NaN to the SH rows
+    put3p(a.dRGB_out, (size_t)a.P, i, n3);  // deferred: the step's flush spreads the NaN
   } else if (a.fused) {
     if (a.dL_dsh) st3<ACC>(a.dL_dsh, i, n3);  // features_dc [P,1,3]
     if (a.dL_dsh_rest)
@@ -256,7 +261,7 @@ __device__ __forceinline__ void gaussian_bwd(const BwdPreArgs& a, size_t i, floa
     dRGB.z *= (cl & 4) ? 0 : 1;
     const V3 dir_orig = mean - v3(a.campos[0], a.campos[1], a.campos[2]);
     if (a.dRGB_out && a.pre_jac) {  // deferred, Jacobian from the multi-view pre-pass
-      put3(a.dRGB_out, i, dRGB);
+      put3p(a.dRGB_out, (size_t)a.P, i, dRGB);
       const float* j = a.pre_jac + i;  // planar [9][P]
       const size_t P = (size_t)a.P;
       const V3 jx = v3(j[0], j[P], j[2 * P]), jy = v3(j[3 * P], j[4 * P], j[5 * P]),
@@ -264,7 +269,7 @@ __device__ __forceinline__ void gaussian_bwd(const BwdPreArgs& a, size_t i, floa
       const V3 dL_ddir = v3(dot3(jx, dRGB), dot3(jy, dRGB), dot3(jz, dRGB));
       dmean = dmean + dnormvdv(dir_orig, dL_ddir);
     } else if (a.dRGB_out) {  // deferred: dL/dsh = basis(dir) x dRGB is formed by the step's flush
-      put3(a.dRGB_out, i, dRGB);
+      put3p(a.dRGB_out, (size_t)a.P, i, dRGB);
       dmean = dmean + sh_backward<false>(sh0, sh1, a.D, dir_orig, dRGB);
     } else {
       dmean = dmean + sh_backward<true>(sh0, sh1, a.D, dir_orig, dRGB);
@@ -405,7 +410,7 @@ __global__ __launch_bounds__(kThreads) void preprocess_bwd_kernel(BwdPreArgs a) 
   } else {
     if (!ACC && t < n) zero_outputs(a, i);
     if (ACC && t < n) put3(a.dL_dmeans2D, i, v3(0, 0, 0));  // stored output: zeros when culled
-    if (defer && t < n) put3(a.dRGB_out, i, v3(0, 0, 0));
+    if (defer && t < n) put3p(a.dRGB_out, (size_t)a.P, i, v3(0, 0, 0));
     if (has_sh && !defer && t < n) {  // culled: zero rows (written in store mode, skipped or +0 in ACC)
       for (int k = 0; k < 3; k++) r0[k] = 0.0f;
       for (int k = 3; k < a.M * 3; k++) r1[k - 3] = 0.0f;
@@ -443,8 +448,8 @@ __global__ __launch_bounds__(kThreads) void sh_flush_kernel(ShFlushArgs a) {
       const float* cp = a.campos[v];
       float b[16];
       sh_basis(mean - v3(cp[0], cp[1], cp[2]), a.D, b);  // gsr_sh.h
-      const float* d = a.dRGB[v] + 3 * i;
-      const V3 dRGB = v3(d[0], d[1], d[2]);
+      const float* d = a.dRGB[v] + i;  // planar [3][rgb_stride]
+      const V3 dRGB = v3(d[0], d[a.rgb_stride], d[2 * a.rgb_stride]);
 #pragma unroll
       for (int k = 0; k < 16; k++) g[k] = v == 0 ? b[k] * dRGB : g[k] + b[k] * dRGB;
     }

@@ -267,7 +267,7 @@ struct BwdPreArgs {
   const float *sh_dc, *sh_rest, *opacities_raw;
   float* dL_dsh_rest;
   // deferred SH gradients (fused only): when non-null, the SH grads are not written; instead the
-  // clamp-masked colour gradient dL/dRGB [P,3] (zeros when culled) is stored here for
+  // clamp-masked colour gradient dL/dRGB, planar [3][P] (zeros when culled), is stored here for
   // launch_sh_grad_flush, which forms dL/dsh = basis(dir) x dL/dRGB for all views of a step
   float* dRGB_out;
   // with dRGB_out: the SH colour's direction Jacobian of this view from the pre-pass ([P,9]); the
@@ -288,7 +288,8 @@ struct ShFlushArgs {
   int P, M, D, nviews, accumulate;
   const float* means3D;
   const float* campos[kShFlushMaxViews];  // device [3] each
-  const float* dRGB[kShFlushMaxViews];    // device [P,3] each
+  const float* dRGB[kShFlushMaxViews];    // device planar [3][rgb_stride] each
+  size_t rgb_stride;
   float *dL_dsh_dc, *dL_dsh_rest;         // features_dc [P,1,3] / features_rest [P,M-1,3] grads
 };
 hipError_t launch_sh_grad_flush(const ShFlushArgs& a, hipStream_t s);

@@ -39,7 +39,9 @@ __device__ __forceinline__ void stage(const ShPlane& p, int base, int n, const u
                                       float* lds) {
   if (p.w == 0) return;
   const uint32_t w = (uint32_t)p.w;
-  const uint32_t magic = (uint32_t)((0x100000000ull + w - 1) / w);
+  // e / w by multiply-high (w = 1: the identity; its magic 2^32 does not fit 32 bits)
+  const uint32_t magic = w == 1 ? 0u : (uint32_t)((0x100000000ull + w - 1) / w);
+  auto row = [&](uint32_t e) { return w == 1 ? e : div_small(e, magic); };
   const size_t gofs = (size_t)base * w;
   const float* src = p.src + gofs;
   float* dst = p.dst + gofs;
@@ -49,7 +51,7 @@ __device__ __forceinline__ void stage(const ShPlane& p, int base, int n, const u
   const int nvec = vec_ok ? (total >> 2) : 0;
   // in ACC mode (or when loading) vectors covering only culled rows are skipped
   auto needed = [&](int q) {
-    return live[div_small(4u * q, magic)] || live[div_small(4u * q + 3u, magic)];
+    return live[row(4u * q)] || live[row(4u * q + 3u)];
   };
   for (int q0 = (int)threadIdx.x; q0 < nvec; q0 += kStageBatch * NT) {
     float4 v[kStageBatch], o[kStageBatch];
@@ -86,7 +88,7 @@ __device__ __forceinline__ void stage(const ShPlane& p, int base, int n, const u
   // scalar tail (everything when the global pointer is not 16-byte aligned)
   for (int e = 4 * nvec + (int)threadIdx.x; e < total; e += NT) {
     if (IN) l[e] = src[e];
-    else if (ACC) { if (live[div_small((uint32_t)e, magic)]) dst[e] += l[e]; }
+    else if (ACC) { if (live[row((uint32_t)e)]) dst[e] += l[e]; }
     else dst[e] = l[e];
   }
 }

@@ -398,7 +398,7 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
             d_means3D, d_dc, d_rest, d_op, d_sc, d_rot, d_lf = grads
             d_means2D = torch.empty((P, 3), **fopts)  # always stored by the kernel
             if defer is not None:
-                d_rgb = torch.empty((P, 3), **fopts)
+                d_rgb = torch.empty((3, P), **fopts)  # planar dL/dRGB (include/gsr.h)
                 defer.add(ctx.leaves, d_rgb, campos, m3, int(rs.sh_degree), M)
         else:
             d_means2D = torch.empty((P, 3), **fopts)
@@ -602,9 +602,10 @@ class ShGradDeferral:
         L = _lib.load()
         for a in range(0, P, step):  # row slices: the kernel is per Gaussian, pointers offset
             b = min(P, a + step)
-            rgbs = (_lib.ctypes.c_void_p * n)(*[v[0].data_ptr() + 12 * a for v in self.views])
+            # planar [3][P] dL/dRGB: rows [a, b) start at element a of each plane
+            rgbs = (_lib.ctypes.c_void_p * n)(*[v[0].data_ptr() + 4 * a for v in self.views])
             with _lib.on_device(self.device):
-                rc = L.gsr_sh_grad_flush(b - a, M, degree, _ptr(m3) + 12 * a, n, camp, rgbs,
+                rc = L.gsr_sh_grad_flush(b - a, M, degree, _ptr(m3) + 12 * a, n, camp, rgbs, P,
                                          _ptr(dc.grad) + 12 * a,
                                          (_ptr(rest.grad) + 4 * rest_w * a)
                                          if rest is not None else None,

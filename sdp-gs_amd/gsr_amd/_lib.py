@@ -167,7 +167,7 @@ def load():
                                       ctypes.POINTER(_p), ctypes.POINTER(_p), ctypes.POINTER(_p), _p]
         L.gsr_sh_grad_flush.restype = _i
         L.gsr_sh_grad_flush.argtypes = [_i, _i, _i, _p, _i, ctypes.POINTER(_p),
-                                        ctypes.POINTER(_p), _p, _p, _i, _p]
+                                        ctypes.POINTER(_p), ctypes.c_int64, _p, _p, _i, _p]
         # include/gsr_optim.h
         _pp = ctypes.POINTER(_p)
         L.gsr_adam_step.restype = _i
