@@ -436,10 +436,13 @@ constexpr int kAccDet = 13;
 template <bool EXTRA, bool FEAT, int GROUP, bool DET, bool ROWS>
 __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
   static_assert(!DET || ROWS, "the deterministic backward stores per-instance rows");
+  // the batch's records in LDS, regrouped so that the colour dot product's packed FMAs read
+  // register pairs straight from the loads: s_r0 = {x, y, conic.a, conic.b}, s_r1 = {conic.c,
+  // opacity}, s_c0 = {r, g, b, depth}, s_c1 = {f0, f1, f2, 1} (alpha channel)
   __shared__ float4 s_r0[kThreads];
-  __shared__ float4 s_r1[kThreads];
-  __shared__ float4 s_r2[kThreads];
-  __shared__ float s_f2[FEAT ? kThreads : 1];  // rec[3].x (feature 2) only
+  __shared__ float2 s_r1[kThreads];
+  __shared__ float4 s_c0[kThreads];
+  __shared__ float4 s_c1[FEAT ? kThreads : 1];
   __shared__ uint32_t s_gid[kThreads];
   // accumulator rows padded to an odd stride (17 floats): the per-splat moments pass (lane t ->
   // row t) and the zero-fill are bank-conflict-free; the butterfly's adds (16 lanes -> 16 slots of
@@ -452,6 +455,9 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
   const int lane = (int)(threadIdx.x & 63);
   const int wid = (int)(threadIdx.x >> 6);
   const SwapOrient swap_orient = probe_swaps(lane);
+  // the lanes that hold a reduced gradient value (one of the four per value, value < kAccDet)
+  const int red_slot = reduce16_slot(lane, swap_orient);
+  const bool red_lane = (lane & 3) == 0 && red_slot < kAccDet;
   const uint32_t ntiles = a.gx * a.gy;
   const uint32_t tile = sched_tile(blockIdx.x, ntiles, a.sched, a.order);
   const uint32_t tx = tile % a.gx, ty = tile / a.gx;
@@ -514,6 +520,10 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
   static_assert(kAccMx == 0 && kAccMy == 1 && kAccCa == 2 && kAccCb == 3 && kAccCc == 4 &&
                 kAccOp == 5 && kAccR == 6 && kAccG == 7 && kAccB == 8 && kAccDepth == 9 &&
                 kAccF0 == 10 && kAccF1 == 11 && kAccF2 == 12, "pair layout of the gradient row");
+  // the upstream gradients' loads are waited for here: left to their first use inside the pair
+  // loop, that wait (vmcnt is in-order) would also cover the previous batch's flush atomics
+  asm volatile("" ::"v"(dpA.x), "v"(dpA.y), "v"(dpB.x), "v"(dpB.y), "v"(dpC.x), "v"(dpC.y),
+               "v"(dpD.x), "v"(dpD.y));
   float acc_dot = 0.0f, last_cdot = 0.0f;
   float last_alpha = 0.0f;
   const float ddelx_dx = (float)(0.5 * a.W);
@@ -530,12 +540,12 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
       const uint32_t gid = min(a.point_list[range.x + rel], a.P - 1u);
       s_gid[threadIdx.x] = gid;
       const float4* rec = a.rec + 4 * (size_t)gid;
-      const float4 q0 = rec[0], q1 = rec[1], q3 = rec[3];
+      const float4 q0 = rec[0], q1 = rec[1], q2 = rec[2], q3 = rec[3];
       s_r0[threadIdx.x] = q0;
-      s_r1[threadIdx.x] = q1;
+      s_r1[threadIdx.x] = make_float2(q1.x, q1.y);
       s_mask[threadIdx.x] = (uint8_t)wave_mask(q0, q1, q3.z, tx, ty);
-      s_r2[threadIdx.x] = rec[2];
-      if (FEAT) s_f2[threadIdx.x] = q3.x;
+      s_c0[threadIdx.x] = make_float4(q1.w, q2.x, q2.y, q1.z);
+      if (FEAT) s_c1[threadIdx.x] = make_float4(q2.z, q2.w, q3.x, 1.0f);
     }
     __syncthreads();
     const uint32_t nlist = build_wave_list(s_mask, s_list[wid], cnt, wid, lane);
@@ -558,33 +568,70 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
       if (tile_last - 1 - done_cnt - jl >= wave_last) continue;  // wave-uniform
     }
     BLEND_STAT(5, 1);
-    float Gv[GROUP], av[GROUP];
+    // Every LDS read of the group's entries is issued here, before any arithmetic (one wait per
+    // group instead of one per entry and phase); the colours are consumed at once by the colour
+    // dot product, so the pair phase below reads no LDS and keeps only per-entry scalars.
+    float Gv[GROUP], av[GROUP], pw[GROUP], cdv[GROUP];
+    f2 dxyv[GROUP];
     bool cv[GROUP];
+    {
+      float4 r0v[GROUP], c0v[GROUP], c1v[GROUP];
+      float2 r1v[GROUP];
 #pragma unroll
-    for (int u = 0; u < GROUP; u++) {
-      const uint32_t j = (packed >> (8 * u)) & 0xffu;
-      const uint32_t rel = tile_last - 1 - done_cnt - j;
-      const float4 r0 = s_r0[j];
-      const float4 r1 = s_r1[j];
-      const float dx = r0.x - pfx, dy = r0.y - pfy;
-      const float power = -0.5f * (r0.z * dx * dx + r1.x * dy * dy) - r0.w * dx * dy;
-#if GSR_BWD_FAST_EXP
-      // The backward needs the forward's alpha >= 1/255 DECISION exactly, its G only to gradient
-      // precision: G by the hardware exp2 (v_exp_f32, ~1 ulp; 3 instructions instead of the 17 of
-      // splat_exp), and splat_exp -- the forward's and the oracle's sequence -- wherever op * G
-      // lies within 2e-6 (relative) of 1/255, so the decision is the forward's at every pixel.
-      {
-        float G = __builtin_amdgcn_exp2f(power * 1.44269504088896341f);
-        const float t = r1.y * G;
-        if (fabsf(t - (1.0f / 255.0f)) <= 2e-6f * (1.0f / 255.0f)) G = splat_exp(power);
-        Gv[u] = G;
+      for (int u = 0; u < GROUP; u++) {
+        const uint32_t j = (packed >> (8 * u)) & 0xffu;
+        r0v[u] = s_r0[j];
+        r1v[u] = s_r1[j];
+        c0v[u] = s_c0[j];
+        if (FEAT) c1v[u] = s_c1[j];
       }
+      float tdist = 1.0f;  // min over the group of |op * G - 1/255| (the exact-path test)
+#pragma unroll
+      for (int u = 0; u < GROUP; u++) {
+        const float4 r0 = r0v[u];
+        const float dx = r0.x - pfx, dy = r0.y - pfy;
+        dxyv[u] = mk2(dx, dy);
+        pw[u] = -0.5f * (r0.z * dx * dx + r1v[u].x * dy * dy) - r0.w * dx * dy;
+#if GSR_BWD_FAST_EXP
+        // The backward needs the forward's alpha >= 1/255 DECISION exactly, its G only to
+        // gradient precision: G by the hardware exp2 (v_exp_f32, ~1 ulp; 3 instructions instead
+        // of the 17 of splat_exp), and splat_exp -- the forward's and the oracle's sequence --
+        // wherever op * G lies within 2e-6 (relative) of 1/255, so the decision is the forward's
+        // at every pixel.  The exact path is one wave-uniform branch per group (rarely taken).
+        Gv[u] = __builtin_amdgcn_exp2f(pw[u] * 1.44269504088896341f);
+        {
+          const float d = fabsf(r1v[u].y * Gv[u] - (1.0f / 255.0f));
+          tdist = d < tdist ? d : tdist;
+        }
 #else
-      Gv[u] = splat_exp(power);
+        Gv[u] = splat_exp(pw[u]);
 #endif
-      av[u] = fminf(0.99f, r1.y * Gv[u]);
-      cv[u] = (k0 + u < nlist) && rel < last_contributor && !(power > 0.0f) &&
-              !(av[u] < 1.0f / 255.0f);
+        // cdot = sum_c col_c * dpix_c as packed FMAs over the colour pairs (gradient-only
+        // arithmetic: the forward-consistent quantities G, alpha, T are computed unfused)
+        const float4 c0 = c0v[u];
+        f2 c2 = mk2(c0.x, c0.y) * dpA;
+        c2 = fma2(mk2(c0.z, NC > 3 ? c0.w : 0.f), dpB, c2);
+        if (FEAT) c2 = fma2(mk2(c1v[u].x, c1v[u].y), dpC, c2);
+        if (NC > 3) c2 = fma2(mk2(FEAT ? c1v[u].z : 0.f, 1.0f), dpD, c2);
+        cdv[u] = c2.x + c2.y;
+      }
+#if GSR_BWD_FAST_EXP
+      if (__ballot(tdist <= 2e-6f * (1.0f / 255.0f))) {
+#pragma unroll
+        for (int u = 0; u < GROUP; u++) {
+          if (fabsf(r1v[u].y * Gv[u] - (1.0f / 255.0f)) <= 2e-6f * (1.0f / 255.0f))
+            Gv[u] = splat_exp(pw[u]);
+        }
+      }
+#endif
+#pragma unroll
+      for (int u = 0; u < GROUP; u++) {
+        const uint32_t j = (packed >> (8 * u)) & 0xffu;
+        const uint32_t rel = tile_last - 1 - done_cnt - j;
+        av[u] = fminf(0.99f, r1v[u].y * Gv[u]);
+        cv[u] = (k0 + u < nlist) && rel < last_contributor && !(pw[u] > 0.0f) &&
+                !(av[u] < 1.0f / 255.0f);
+      }
     }
 #pragma unroll
     for (int u = 0; u < GROUP; u++) {
@@ -613,10 +660,7 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
       // of the reference (backward.cu:486-555).
       const float G = contrib ? Gv[u] : 0.0f;
       const float alpha = contrib ? av[u] : 0.0f;
-      const float4 r0 = s_r0[j];
-      const float4 r1 = s_r1[j];
-      const float4 r2 = s_r2[j];
-      const f2 dxy = mk2(r0.x - pfx, r0.y - pfy);
+      const f2 dxy = dxyv[u];
 
 #if GSR_BWD_FAST_DIV
       {
@@ -633,14 +677,7 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
       T = T / (1.f - alpha);
 #endif
       const float dchannel_dcolor = alpha * T;
-      // cdot = sum_c col_c * dpix_c as packed FMAs over the record's natural pairs (gradient-only
-      // arithmetic: the forward-consistent quantities G, alpha, T above are computed unfused)
-      f2 c2 = mk2(r1.w, r2.x) * dpA;
-      if (NC > 3) c2 = fma2(mk2(r2.y, r1.z), dpB, c2);
-      else c2 = fma2(mk2(r2.y, 0.f), dpB, c2);
-      if (FEAT) c2 = fma2(mk2(r2.z, r2.w), dpC, c2);
-      if (NC > 3) c2 = fma2(mk2(FEAT ? s_f2[j] : 0.f, 1.0f), dpD, c2);
-      const float cdot = c2.x + c2.y;
+      const float cdot = cdv[u];
       const float acc_new = last_alpha * last_cdot + (1.f - last_alpha) * acc_dot;
       float dL_dalpha = cdot - acc_new;
       acc_dot = contrib ? acc_new : acc_dot;
@@ -662,7 +699,9 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
       g[4] = dchannel_dcolor * dpB;                  // kAccB, kAccDepth
       g[5] = FEAT ? dchannel_dcolor * dpC : mk2(0.f, 0.f);          // kAccF0, kAccF1
       g[6] = mk2(FEAT ? dchannel_dcolor * dpD.x : 0.f, 0.f);       // kAccF2, (13)
-      g[7] = mk2(0.f, 0.f);                                         // (14, 15)
+      // slots 14, 15 are never read (only k < kAccDet reaches the accumulator): the dead dxy
+      // pair rides along instead of two freshly zeroed registers for the butterfly's swaps
+      g[7] = dxy;                                                   // (14, 15), ignored
 #if GSR_BWD_DIAG == 1
       // diagnostic build only (wrong gradients): no wave reduction, one lane-local LDS add
       {
@@ -671,13 +710,9 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
       }
 #else
       const float sum = wave_reduce16_dpp(g, lane);
-      if ((lane & 3) == 0) {
-        const int k = reduce16_slot(lane, swap_orient);
-        if (DET) {
-          if (k < kAccDet) s_acc[(wid * kThreads + j) * kRow + k] = sum;
-        } else if (sum != 0.0f) {
-          atomicAdd(&s_acc[j * kAccPad + k], sum);
-        }
+      if (red_lane) {
+        if (DET) s_acc[(wid * kThreads + j) * kRow + red_slot] = sum;
+        else if (sum != 0.0f) atomicAdd(&s_acc[j * kAccPad + red_slot], sum);
       }
 #endif
     }
@@ -694,7 +729,7 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
     // moments -> the reference's dL/dmean2D (NDC-scaled) and dL/dconic, once per (splat, tile)
     if (threadIdx.x < cnt) {
       const float4 r0 = s_r0[threadIdx.x];
-      const float4 r1 = s_r1[threadIdx.x];
+      const float2 r1 = s_r1[threadIdx.x];
       float* row = s_acc + threadIdx.x * kRow;
       if (DET) {  // the four waves' rows, added in wave order, into wave 0's row
 #pragma unroll
