@@ -91,6 +91,23 @@ __global__ __launch_bounds__(kSchedThreads) void tile_schedule_kernel(const uint
 #ifndef GSR_BWD_FAST_EXP
 #define GSR_BWD_FAST_EXP 1
 #endif
+// backward group replay: 1 = every entry of a group is replayed straight-line (no wave-uniform
+// skip of entries without a contributing lane), 0 = such entries are skipped.  Round 3, after the
+// hoisted loads: 0.2115 -> 0.235 ms with 1 (profiles/r03_bwd_flush_noskip_ab.txt), not kept
+#ifndef GSR_BWD_NOSKIP
+#define GSR_BWD_NOSKIP 0
+#endif
+// backward batch order: 1 = the next batch is staged before this batch's flush (its loads not
+// queued behind the flush's atomics), 0 = after it.  Measured 0.2115 -> 0.2185 ms with 1 (the
+// workgroup then waits for the staged loads before it can flush), not kept
+#ifndef GSR_BWD_FLUSH_LATE
+#define GSR_BWD_FLUSH_LATE 0
+#endif
+// backward colour dot product: 1 = formed in the group's test phase for every entry (the colour
+// registers die early), 0 = where the compiler places it
+#ifndef GSR_BWD_CDOT_EARLY
+#define GSR_BWD_CDOT_EARLY 0
+#endif
 // backward transmittance recovery T / (1 - alpha): 0 = IEEE division, 1 = rcp + Newton step
 #ifndef GSR_BWD_FAST_DIV
 #define GSR_BWD_FAST_DIV 1
@@ -443,7 +460,9 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
   __shared__ float2 s_r1[kThreads];
   __shared__ float4 s_c0[kThreads];
   __shared__ float4 s_c1[FEAT ? kThreads : 1];
-  __shared__ uint32_t s_gid[kThreads];
+  // double-buffered under GSR_BWD_FLUSH_LATE: the flush of batch k reads its ids after batch k + 1
+  // has been staged
+  __shared__ uint32_t s_gid[GSR_BWD_FLUSH_LATE ? 2 : 1][kThreads];
   // accumulator rows padded to an odd stride (17 floats): the per-splat moments pass (lane t ->
   // row t) and the zero-fill are bank-conflict-free; the butterfly's adds (16 lanes -> 16 slots of
   // one row) and the flush (4 rows x 16 slots per wave) stay conflict-free as well
@@ -531,14 +550,13 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
 
   for (int k = (int)threadIdx.x; k < (DET ? 4 : 1) * kThreads * kRow; k += kThreads) s_acc[k] = 0.0f;
 
-  // rel = position inside the tile's list; every pixel only uses rel < its n_contrib <= tile_last
-  for (uint32_t done_cnt = 0; done_cnt < tile_last; done_cnt += kThreads) {
-    __syncthreads();
-    const uint32_t cnt = min((uint32_t)kThreads, tile_last - done_cnt);
-    if (threadIdx.x < cnt) {
-      const uint32_t rel = tile_last - 1 - done_cnt - threadIdx.x;
+  // stage the batch starting at list position dc (back to front) into LDS, ids into s_gid[buf]
+  auto stage_batch = [&](uint32_t dc, int buf) {
+    const uint32_t n = min((uint32_t)kThreads, tile_last - dc);
+    if (threadIdx.x < n) {
+      const uint32_t rel = tile_last - 1 - dc - threadIdx.x;
       const uint32_t gid = min(a.point_list[range.x + rel], a.P - 1u);
-      s_gid[threadIdx.x] = gid;
+      s_gid[buf][threadIdx.x] = gid;
       const float4* rec = a.rec + 4 * (size_t)gid;
       const float4 q0 = rec[0], q1 = rec[1], q2 = rec[2], q3 = rec[3];
       s_r0[threadIdx.x] = q0;
@@ -547,7 +565,19 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
       s_c0[threadIdx.x] = make_float4(q1.w, q2.x, q2.y, q1.z);
       if (FEAT) s_c1[threadIdx.x] = make_float4(q2.z, q2.w, q3.x, 1.0f);
     }
+  };
+#if GSR_BWD_FLUSH_LATE
+  if (tile_last > 0) stage_batch(0, 0);
+#endif
+  // rel = position inside the tile's list; every pixel only uses rel < its n_contrib <= tile_last
+  for (uint32_t done_cnt = 0; done_cnt < tile_last; done_cnt += kThreads) {
+    const int buf = GSR_BWD_FLUSH_LATE ? (int)((done_cnt / kThreads) & 1u) : 0;
     __syncthreads();
+    const uint32_t cnt = min((uint32_t)kThreads, tile_last - done_cnt);
+#if !GSR_BWD_FLUSH_LATE
+    stage_batch(done_cnt, buf);
+    __syncthreads();
+#endif
     const uint32_t nlist = build_wave_list(s_mask, s_list[wid], cnt, wid, lane);
     BLEND_STAT(4, nlist);
 #if GSR_BLEND_STATS
@@ -614,6 +644,11 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
         if (FEAT) c2 = fma2(mk2(c1v[u].x, c1v[u].y), dpC, c2);
         if (NC > 3) c2 = fma2(mk2(FEAT ? c1v[u].z : 0.f, 1.0f), dpD, c2);
         cdv[u] = c2.x + c2.y;
+#if GSR_BWD_CDOT_EARLY
+        // keep the dot product here (the compiler would sink it into the contributing branch and
+        // hold the colours live across the test phase)
+        asm volatile("" ::"v"(cdv[u]));
+#endif
       }
 #if GSR_BWD_FAST_EXP
       if (__ballot(tdist <= 2e-6f * (1.0f / 255.0f))) {
@@ -637,7 +672,9 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
     for (int u = 0; u < GROUP; u++) {
       const bool contrib = cv[u];
       const uint64_t cmask = __ballot(contrib);
-      if (cmask == 0ull) continue;  // wave-uniform skip
+      // wave-uniform skip (always in DET: its rows are stored, not added, so an entry past the
+      // list end must not write)
+      if ((DET || !GSR_BWD_NOSKIP) && cmask == 0ull) continue;
 #if GSR_BWD_DIAG == 3
       // diagnostic build only (wrong gradients): no pair update / reduction -- what the batch
       // loads, lists, alpha tests, barriers and flush cost by themselves
@@ -746,6 +783,11 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
       row[kAccCc] = (-0.5f * o) * row[kAccCc];
     }
     __syncthreads();
+#if GSR_BWD_FLUSH_LATE
+    // the next batch is staged BEFORE this batch's flush: its loads are not queued behind the
+    // flush's atomics (vmcnt is in-order), and those atomics retire during the next pair phase
+    if (done_cnt + kThreads < tile_last) stage_batch(done_cnt + kThreads, buf ^ 1);
+#endif
     // flush: lane l of wave-instruction `it` handles splat (it*16 + tid/16), slot tid%16
 #pragma unroll 4
     for (int it = 0; it < kThreads * kAccFloats / kThreads; it++) {
@@ -769,9 +811,9 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
           if (v != 0.0f) {
 #if GSR_BWD_DIAG == 2
             // diagnostic build only (wrong gradients): the flush's traffic as plain stores
-            a.acc[(size_t)s_gid[jj] * kAccFloats + k] = v;
+            a.acc[(size_t)s_gid[buf][jj] * kAccFloats + k] = v;
 #else
-            atomicAdd(&a.acc[(size_t)s_gid[jj] * kAccFloats + k], v);
+            atomicAdd(&a.acc[(size_t)s_gid[buf][jj] * kAccFloats + k], v);
 #endif
             s_acc[jj * kAccPad + k] = 0.0f;
           }
