@@ -160,6 +160,35 @@ __device__ __forceinline__ float splat_exp(float x) {
   const float res = __builtin_amdgcn_ldexpf(y, (int)k);
   return x < -104.0f ? 0.0f : res;
 }
+// splat_exp of N independent arguments, its steps interleaved across the N chains (the same
+// operations per element, so bit-identical to N splat_exp calls): one wave then has N independent
+// instructions in flight per step instead of one 15-deep dependent chain per argument
+template <int N>
+__device__ __forceinline__ void splat_exp_n(const float (&x)[N], float (&out)[N]) {
+  float k[N], r[N], p[N];
+#pragma unroll
+  for (int i = 0; i < N; i++) k[i] = __builtin_rintf(x[i] * 1.44269504088896341f);
+#pragma unroll
+  for (int i = 0; i < N; i++) r[i] = __builtin_fmaf(-k[i], 0.693359375f, x[i]);
+#pragma unroll
+  for (int i = 0; i < N; i++) r[i] = __builtin_fmaf(-k[i], -2.12194440e-4f, r[i]);
+#pragma unroll
+  for (int i = 0; i < N; i++) p[i] = __builtin_fmaf(1.9875691500e-4f, r[i], 1.3981999507e-3f);
+#pragma unroll
+  for (int i = 0; i < N; i++) p[i] = __builtin_fmaf(p[i], r[i], 8.3334519073e-3f);
+#pragma unroll
+  for (int i = 0; i < N; i++) p[i] = __builtin_fmaf(p[i], r[i], 4.1665795894e-2f);
+#pragma unroll
+  for (int i = 0; i < N; i++) p[i] = __builtin_fmaf(p[i], r[i], 1.6666665459e-1f);
+#pragma unroll
+  for (int i = 0; i < N; i++) p[i] = __builtin_fmaf(p[i], r[i], 5.0000001201e-1f);
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    const float y = __builtin_fmaf(p[i], r[i] * r[i], r[i]) + 1.0f;
+    const float res = __builtin_amdgcn_ldexpf(y, (int)k[i]);
+    out[i] = x[i] < -104.0f ? 0.0f : res;
+  }
+}
 __device__ __forceinline__ float sigmoid_f(float x) { return 1.0f / (1.0f + expf(-x)); }
 
 // Natural log for the culling threshold q_cut (positive normal x only): Cephes logf -- frexp to

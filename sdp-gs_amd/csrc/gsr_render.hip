@@ -126,6 +126,13 @@ __device__ unsigned long long g_blend_stats[16];
 #else
 #define BLEND_STAT(k, v) do { } while (0)
 #endif
+// block-list forward: 1 = the group's four alpha tests run ahead of the replay as four
+// interleaved exp chains (splat_exp_n), 0 = where the compiler puts them (inside the replay's
+// per-lane branches).  Round 3: render_fwd 0.1140 vs 0.1141 ms (3 alternating pairs at 1 stream,
+// profiles/r03_fwd_testfirst_ab.txt) -- the forward is not latency-bound on these chains; off
+#ifndef GSR_FWD_TEST_FIRST
+#define GSR_FWD_TEST_FIRST 0
+#endif
 // forward: 1 = blend weight alpha * T formed once per pair, 0 = col * alpha * T per channel
 #ifndef GSR_FWD_WEIGHT
 #define GSR_FWD_WEIGHT 1
@@ -1016,8 +1023,23 @@ __global__ __launch_bounds__(kThreads, GSR_FWD_BLK_WAVES) void render_fwd_blk_ke
         const float power = -0.5f * (r0.z * dx * dx + r1v[u].x * dy * dy) - r0.w * dx * dy;
         // entries past the group's list end get power = +1 and are skipped
         pw[u] = (k + u < nl) ? power : 1.0f;
+#if !GSR_FWD_TEST_FIRST
         al[u] = fminf(0.99f, r1v[u].y * splat_exp(pw[u]));
+#endif
       }
+#if GSR_FWD_TEST_FIRST
+      {
+        float G4[4];
+        splat_exp_n<4>(pw, G4);
+#pragma unroll
+        for (int u = 0; u < 4; u++) al[u] = fminf(0.99f, r1v[u].y * G4[u]);
+      }
+      // the four entries' power / exp / alpha are evaluated here, for every lane, as four
+      // independent chains: left alone, the compiler sinks each into the replay's per-lane
+      // `done` branches below and serialises the exps
+      asm volatile("" ::"v"(al[0]), "v"(al[1]), "v"(al[2]), "v"(al[3]), "v"(pw[0]), "v"(pw[1]),
+                   "v"(pw[2]), "v"(pw[3]));
+#endif
 #pragma unroll
       for (int u = 0; u < 4; u++) {
         if (done) continue;
