@@ -160,6 +160,10 @@ def main():
                     help="issue view i's backward after view i + lag's forward (0: each view's "
                          "forward and backward together; 1 measured 3.4%% faster at 3 streams, "
                          "scripts/step_times.py)")
+    ap.add_argument("--per-view", action="store_true",
+                    help="issue the step view by view (render() + autograd per view, lagged over "
+                         "the streams) instead of one multi-view call for all of the step's "
+                         "views (gaussian_renderer.render_views)")
     ap.add_argument("--no-precolor", action="store_true",
                     help="each view evaluates its SH colour itself instead of the step's pre-pass")
     ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_r03.json"))
@@ -181,7 +185,7 @@ def main():
     from gsr_amd.pipeline import ViewPipeline
     from gsr_amd.synthetic import make_cameras, make_gaussians, upstream_grads
     import diff_gaussian_rasterization as dgr
-    from gaussian_renderer import render
+    from gaussian_renderer import render, render_views
 
     dgr.grad_into_leaves(not args.autograd_grads)
     rank, world, local = init_from_env("nccl")
@@ -241,11 +245,30 @@ def main():
                 p.grad = None
         # with a reducer the all-reduce overlaps the step's tail (non-SH grads while the SH
         # gradients are flushed in row slices, each slice reduced as soon as it is written)
-        if args.lag > 0:
+        if not args.per_view and not args.autograd_grads:
+            views.run_views(my_cams, lambda cams, strs: all_views(cams, strs, record),
+                            model=model, reducer=reducer)
+        elif args.lag > 0:
             views.run(my_cams, view_forward, model=model, reducer=reducer,
                       bwd=lambda pkg: view_backward(pkg, record), lag=args.lag)
         else:
             views.run(my_cams, lambda cam: one_view(cam, record), model=model, reducer=reducer)
+
+    def all_views(cams, strs, record):
+        """Every view of the step in one multi-view call: forward of all views, then the
+        backward of the fixed upstream gradients seeded on the stacked [V,...] outputs."""
+        pkgs = render_views(cams, model, pipe, bg, opt, streams=strs)
+        st = pkgs[0]["views"]
+        V = len(pkgs)
+        torch.autograd.backward(
+            [st["render"], st["depth"], st["feature"]],
+            [dimg.expand(V, *dimg.shape), ddep.expand(V, *ddep.shape),
+             dfeat.expand(V, *dfeat.shape)])
+        if record:
+            for (nr, ni), pkg in zip(dgr.LAST_STATS["view_counts"], pkgs):
+                stats["R"].append(ni)
+                stats["R_ref"].append(nr)
+                stats["Pv"].append(int(pkg["visibility_filter"].sum()))
 
     def view_forward(cam):
         pkg = render(cam, model, pipe, bg, opt)
@@ -305,12 +328,14 @@ def main():
 
     elapsed = timed_region(lambda i: step())
     stages = dict(all_stages)
+    stage_steps = {n: 1 for n in stages}  # steps each stage's launches were collected over
     dom_elapsed = None
     if dom_stage is not None:
         timer.enable(True, stages=[dom_stage])
         dom_elapsed = timed_region(lambda i: step())
         timer.enable(False)
         stages[dom_stage] = timer.collect()[dom_stage]  # measured over the second timed region
+        stage_steps[dom_stage] = args.steps
 
     total_views = args.steps * n_views
     value = total_views / elapsed
@@ -326,14 +351,19 @@ def main():
         if calls == 0:
             continue
         avg_ms = ms / calls
-        b = algorithmic_bytes(name, P, Pv, R, T, HW, D=deg, acc=not args.autograd_grads,
-                              defer_sh=defer_sh, precolor=not args.no_precolor,
-                              views=len(my_cams))
+        # views one launch covers: 1, except the multi-view call's merged backward blend (all the
+        # step's views in one launch); the per-step stages' formulas already cover all views
+        vpl = 1
+        if name not in ("sh_precolor", "sh_flush"):
+            vpl = max(1, int(round(len(my_cams) * stage_steps.get(name, 1) / calls)))
+        b = vpl * algorithmic_bytes(name, P, Pv, R, T, HW, D=deg, acc=not args.autograd_grads,
+                                    defer_sh=defer_sh, precolor=not args.no_precolor,
+                                    views=len(my_cams))
         k = {"avg_ms": round(avg_ms, 4), "calls": int(calls), "bytes": int(b),
-             "gbs": round(b / (avg_ms * 1e-3) / 1e9, 1)}
+             "views_per_launch": vpl, "gbs": round(b / (avg_ms * 1e-3) / 1e9, 1)}
         if name in ("render_fwd", "render_bwd"):
             # (pixel, instance) candidate pairs per second: 256 pixels x R instances per view
-            k["pair_candidates_per_s_G"] = round(256.0 * R / (avg_ms * 1e-3) / 1e9, 1)
+            k["pair_candidates_per_s_G"] = round(vpl * 256.0 * R / (avg_ms * 1e-3) / 1e9, 1)
         kernels[name] = k
     roofline = None
     if kernels and dom_stage in kernels:
@@ -353,6 +383,7 @@ def main():
                     "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                     "algorithmic_bytes": kd["bytes"], "avg_ms": kd["avg_ms"],
+                    "views_per_launch": kd["views_per_launch"],
                     "timed_region_views_per_s": round(args.steps * n_views / dom_elapsed, 3)}
         try:
             with open(args.pmc_file) as fh:
@@ -378,7 +409,7 @@ def main():
             # instances behind a tile's last contributor and zero values are not flushed).  A
             # plain-store build of the same flush ran equally fast, so they are not
             # what bounds the kernel
-            ab = 13 * 4 * R
+            ab = 13 * 4 * R * kd["views_per_launch"]
             roofline["atomic_bytes_upper"] = int(ab)
             roofline["atomic_frac_upper"] = round(ab / (kd["avg_ms"] * 1e-3) / 1.3e12, 4)
 
@@ -415,6 +446,10 @@ def main():
                                        else "unfused"),
                        "grad_mode": "autograd" if args.autograd_grads else "into_leaves",
                        "view_streams": views.depth,
+                       "issue": ("per view (render() + autograd per view, lagged)"
+                                 if args.per_view or args.autograd_grads else
+                                 "multi-view call (gsr_rasterize_views_fused, one host call per "
+                                 "step for the forwards and one for the backwards)"),
                        "hw_queue_budget": (f"{views.depth} view streams + 1 RCCL stream <= "
                                            f"GPU_MAX_HW_QUEUES={hw_queues}") if world > 1 else
                                           f"{views.depth} view streams (no collectives)",

@@ -244,6 +244,67 @@ int gsr_sh_grad_flush(int P, int M, int degree, const float* means3D, int nviews
                       int64_t rgb_plane_stride, float* dL_dfeatures_dc, float* dL_dfeatures_rest,
                       int accumulate, void* stream);
 
+/* ---- multi-view calls (no reference counterpart: a step of several views in one host call) ----
+ * One camera of gsr_rasterize_views_fused / _backward.  The forward fills the scratch pointers
+ * and counts; the backward reads them back unchanged.  The per-view fields mean what the
+ * single-view entry points' arguments of the same names mean. */
+typedef struct gsr_view {
+  /* camera */
+  const float* viewmatrix; const float* projmatrix; const float* campos;
+  float tan_fovx, tan_fovy;
+  /* optional colour pre-pass of this view (gsr_sh_precolor): both or neither */
+  const float* pre_color; const uint8_t* pre_clamp;
+  /* forward outputs: [3,H,W], [1,H,W], [1,H,W], [3,H,W] (may be NULL as in the single-view
+   * call, except out_color), radii[P] (NULL -> internal) */
+  float* out_color; float* out_depth; float* out_alpha; float* out_feature; int* radii;
+  /* scratch of this view: requested by the forward through alloc(alloc_ctx, bytes, which) */
+  void* alloc_ctx;
+  void* geom_buffer; void* binning_buffer; void* image_buffer;   /* set by the forward */
+  int num_rendered;    /* set by the forward: the reference's count (as *num_rendered) */
+  int num_instances;   /* set by the forward: instances binned (gsr_last_forward_instances) */
+  /* HIP stream of this view's work (NULL = the call's stream) */
+  void* stream;
+  /* backward: upstream gradients (depth / alpha / feature may be NULL), the screen-space
+   * gradient dL_dmeans2D[P,3] (always stored), and -- deferred SH gradients -- the planar
+   * dL/dRGB [3][P] this view stores (NULL: the SH gradients are added directly) with the
+   * pre-pass Jacobian pre_jac (optional, needs dL_dcolor_sh) */
+  const float* dL_dout_color; const float* dL_dout_depth; const float* dL_dout_alpha;
+  const float* dL_dout_feature;
+  float* dL_dmeans2D; float* dL_dcolor_sh; const float* pre_jac;
+} gsr_view;
+
+/* Fused forward of V views of the same Gaussians (gsr_rasterize_gaussians_fused per view, same
+ * outputs bit for bit) issued from one host call: the first phase of up to `inflight` views
+ * (preprocess, depth sort, scan and the instance-count read-back) is queued ahead of the views'
+ * binning, so the host's wait for a view's read-back finds it done and every view stream stays
+ * fed.  View v's preprocess and binning run on views[v].stream (which first waits for `stream`,
+ * the call's stream); the blends of consecutive groups of views (up to 8 per group) run merged
+ * into one launch each on `stream`, which is ordered after every view's work on return. */
+int gsr_rasterize_views_fused(
+    int V, gsr_view* views, int image_height, int image_width,
+    int P, int M, const float* background, const float* means3D,
+    const float* features_dc, const float* features_rest, const float* opacity_raw,
+    const float* scaling_raw, const float* rotation_raw, float scale_modifier,
+    int degree, int prefiltered, const float* language_feature, const float* confidence,
+    int include_feature, gsr_alloc_fn alloc, int inflight, void* stream, int debug);
+
+/* Backward of gsr_rasterize_views_fused: the views' blend backwards merged into launches of up to
+ * 8 views on views[0].stream (after the call's `stream`, where the upstream gradients were
+ * produced), and the views' per-Gaussian backwards in view order on `stream`, adding into the
+ * raw leaves' gradients exactly as
+ * consecutive gsr_rasterize_gaussians_fused_backward[_deferred] calls with accumulate = 1 for
+ * every view after the first (the first uses `accumulate`).  With views[v].dL_dcolor_sh set the
+ * SH gradients are deferred (dL_dfeatures_dc / _rest may be NULL). */
+int gsr_rasterize_views_fused_backward(
+    int V, const gsr_view* views, int image_height, int image_width,
+    int P, int M, const float* background, const float* means3D,
+    const float* features_dc, const float* features_rest, const float* opacity_raw,
+    const float* scaling_raw, const float* rotation_raw, float scale_modifier,
+    int degree, const float* language_feature, const float* confidence, int include_feature,
+    float* dL_dmeans3D, float* dL_dfeatures_dc, float* dL_dfeatures_rest,
+    float* dL_dopacity_raw, float* dL_dscaling_raw, float* dL_drotation_raw,
+    float* dL_dlanguage_feature, int accumulate, void* stream, int debug);
+
 /* Replaces _C.mark_visible -> markVisible (rasterize_points.cu:198-217) -> checkFrustum
  * (rasterizer_impl.cu:54-66): present[i] = view-space z > 0.2 (bool as uint8). */
 int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,

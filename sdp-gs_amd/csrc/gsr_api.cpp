@@ -163,27 +163,6 @@ std::atomic<long long> g_wait_ns{0};
 // tile instances the last forward on this host thread actually binned (gsr_last_forward_instances)
 thread_local int g_last_instances = 0;
 
-// Pinned 16-byte landing zone for the one device->host read per forward.
-uint32_t* pinned_slot() {
-  thread_local uint32_t* p = nullptr;
-  if (!p) {
-    if (hipHostMalloc((void**)&p, 16, hipHostMallocDefault) != hipSuccess) p = nullptr;
-  }
-  return p;
-}
-
-// Event marking the arrival of the forward's readback in the pinned slot (per host thread; HIP
-// events are device-agnostic for synchronisation).
-hipEvent_t readback_event() {
-  constexpr int kMaxDev = 64;
-  thread_local hipEvent_t ev[kMaxDev] = {};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return nullptr;
-  if (!ev[dev] && hipEventCreateWithFlags(&ev[dev], hipEventDisableTiming) != hipSuccess)
-    ev[dev] = nullptr;
-  return ev[dev];
-}
-
 bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
 // ---- per-call forward status (the same-call backstop of the sorts' bounded look-back) -----------
@@ -392,98 +371,142 @@ size_t gsr_image_buffer_bytes(int H, int W) {
   return carve_img(nullptr, (size_t)(W > 0 ? W : 0), (size_t)(H > 0 ? H : 0)).bytes;
 }
 
-// Shared forward.  fused != 0: opacities / scales / rotations are GaussianModel's raw
-// _opacity / _scaling / _rotation and the SH come split as sh_dc + sh_rest (activations in-kernel).
-static int forward_impl(int P, int M, const float* background, const float* means3D,
-                        const float* colors_precomp, const float* opacities, const float* scales,
-                        const float* rotations, float scale_modifier, const float* cov3D_precomp,
-                        const float* viewmatrix, const float* projmatrix, float tan_fovx,
-                        float tan_fovy, int image_height, int image_width, const float* sh,
-                        int degree, const float* campos, int prefiltered, const float* sh_language,
-                        const float* language_feature_precomp, const float* confidence,
-                        int include_feature, float* out_color, float* out_depth, float* out_alpha,
-                        float* out_feature, int* radii, int* num_rendered, gsr_alloc_fn alloc,
-                        void* alloc_ctx, void* stream_ptr, int debug, int fused,
-                        const float* sh_dc, const float* sh_rest,
-                        const float* pre_color = nullptr, const uint8_t* pre_clamp = nullptr) {
-  g_err.clear();
-  const bool det = (debug & GSR_DEBUG_DETERMINISTIC) != 0;  // gsr.h: debug bit 1
-  const bool rows = det || bwd_rows_mode();  // per-instance gradient rows (binning layout)
-  debug &= 1;
-  if ((pre_color == nullptr) != (pre_clamp == nullptr) || (pre_color && !fused))
-    return fail(GSR_ERR_ARGUMENT, "pre_color / pre_clamp: both or neither, fused path only");
-  if (fused && P != 0) {  // P = 0: empty tensors have null data (rasterize_points.cu:81)
-    if (!sh_dc || (M > 1 && !sh_rest) || !scales || !rotations)
+// ---- forward, in two phases per view ----------------------------------------------------------
+// The model side of a forward (shared by every view of a multi-view call).  fused != 0:
+// opacities / scales / rotations are GaussianModel's raw _opacity / _scaling / _rotation and the
+// SH come split as sh_dc + sh_rest (activations in-kernel).
+struct FwdModel {
+  int P = 0, M = 0;
+  const float *background = nullptr, *means3D = nullptr, *colors_precomp = nullptr;
+  const float *opacities = nullptr, *scales = nullptr, *rotations = nullptr;
+  float scale_modifier = 1.0f;
+  const float *cov3D_precomp = nullptr, *sh = nullptr;
+  int degree = 0, prefiltered = 0;
+  const float *sh_language = nullptr, *lang_precomp = nullptr, *confidence = nullptr;
+  int include_feature = 0, fused = 0;
+  const float *sh_dc = nullptr, *sh_rest = nullptr;
+  int debug = 0;            // bit 0 only (synchronous checks)
+  bool det = false, rows = false;
+};
+// One camera of a forward, and the state its two phases hand over.
+struct FwdCam {
+  const float *view = nullptr, *proj = nullptr, *campos = nullptr;
+  float tanx = 0, tany = 0;
+  int W = 0, H = 0;
+  const float* pre_color = nullptr;
+  const uint8_t* pre_clamp = nullptr;
+  float *out_color = nullptr, *out_depth = nullptr, *out_alpha = nullptr, *out_feature = nullptr;
+  int* radii = nullptr;
+  gsr_alloc_fn alloc = nullptr;
+  void* alloc_ctx = nullptr;
+  hipStream_t stream = nullptr;
+  uint32_t* host = nullptr;    // pinned landing slot of the read-back
+  hipEvent_t ready = nullptr;  // recorded after the read-back's copy
+  // state of the first phase
+  char *gbase = nullptr, *ibase = nullptr, *bbase = nullptr;
+  GeomState g{};
+  ImgState im{};
+  int32_t* radii_ptr = nullptr;
+  uint32_t gx = 0, gy = 0;
+  bool done = false;  // P == 0: outputs written by the first phase
+  bool depth_in_b = false;  // which buffer pair holds the depth sort's result
+  // state of the binning half of the second phase (fwd_bin -> the blend)
+  RenderArgs ra{};
+  int mail_slot = -1;
+  // results
+  int num_rendered = 0, num_instances = 0;
+};
+
+// Argument checks of the model side (the reference's, rasterize_points.cu:57-59 and
+// rasterizer_impl.cu:229-232); `sh` is set to sh_dc on the fused path.
+static int fwd_check_model(FwdModel& m) {
+  if (m.fused && m.P != 0) {  // P = 0: empty tensors have null data (rasterize_points.cu:81)
+    if (!m.sh_dc || (m.M > 1 && !m.sh_rest) || !m.scales || !m.rotations)
       return fail(GSR_ERR_ARGUMENT, "fused path needs features_dc/_rest, _scaling, _rotation");
-    sh = sh_dc;  // "SH present" for the checks below; the kernels read sh_dc / sh_rest
+    m.sh = m.sh_dc;  // "SH present" for the checks below; the kernels read sh_dc / sh_rest
   }
-  hipStream_t stream = (hipStream_t)stream_ptr;
-  const int W = image_width, H = image_height;
-  if (P < 0) return fail(GSR_ERR_ARGUMENT, "means3D must have dimensions (num_points, 3)");
-  if (W <= 0 || H <= 0) return fail(GSR_ERR_ARGUMENT, "image size must be positive (got %dx%d)", W, H);
-  if (!num_rendered || !out_color) return fail(GSR_ERR_ARGUMENT, "out_color / num_rendered missing");
-  const size_t HW = (size_t)W * H;
-  if (P == 0) {
-    *num_rendered = 0;
-    g_last_instances = 0;
-    GSR_CHECK(hipMemsetAsync(out_color, 0, 3 * HW * sizeof(float), stream));
-    if (out_depth) GSR_CHECK(hipMemsetAsync(out_depth, 0, HW * sizeof(float), stream));
-    if (out_alpha) GSR_CHECK(hipMemsetAsync(out_alpha, 0, HW * sizeof(float), stream));
-    if (out_feature) GSR_CHECK(hipMemsetAsync(out_feature, 0, 3 * HW * sizeof(float), stream));
-    return GSR_OK;
-  }
-  if (!background || !means3D || !opacities || !viewmatrix || !projmatrix || !campos)
+  if (m.P < 0) return fail(GSR_ERR_ARGUMENT, "means3D must have dimensions (num_points, 3)");
+  if (m.P == 0) return GSR_OK;
+  if (!m.background || !m.means3D || !m.opacities)
     return fail(GSR_ERR_ARGUMENT, "background/means3D/opacities/viewmatrix/projmatrix/campos required");
-  if ((colors_precomp == nullptr) == (sh == nullptr))
+  if ((m.colors_precomp == nullptr) == (m.sh == nullptr))
     return fail(GSR_ERR_ARGUMENT, "Please provide excatly one of either SHs or precomputed colors!");
-  if ((cov3D_precomp == nullptr) == (scales == nullptr || rotations == nullptr))
+  if ((m.cov3D_precomp == nullptr) == (m.scales == nullptr || m.rotations == nullptr))
     return fail(GSR_ERR_ARGUMENT,
                 "Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!");
-  if (sh) {
-    if (degree < 0 || degree > 3) return fail(GSR_ERR_ARGUMENT, "sh_degree must be in [0, 3] (got %d)", degree);
-    if (M > 16)  // the kernels stage at most 16 coefficients per Gaussian in LDS
-      return fail(GSR_ERR_ARGUMENT, "sh has M = %d coefficients; at most 16 (degree 3) supported", M);
-    if ((degree + 1) * (degree + 1) > M)
-      return fail(GSR_ERR_ARGUMENT, "sh has %d coefficients but degree %d needs %d", M, degree,
-                  (degree + 1) * (degree + 1));
+  if (m.sh) {
+    if (m.degree < 0 || m.degree > 3)
+      return fail(GSR_ERR_ARGUMENT, "sh_degree must be in [0, 3] (got %d)", m.degree);
+    if (m.M > 16)  // the kernels stage at most 16 coefficients per Gaussian in LDS
+      return fail(GSR_ERR_ARGUMENT, "sh has M = %d coefficients; at most 16 (degree 3) supported", m.M);
+    if ((m.degree + 1) * (m.degree + 1) > m.M)
+      return fail(GSR_ERR_ARGUMENT, "sh has %d coefficients but degree %d needs %d", m.M, m.degree,
+                  (m.degree + 1) * (m.degree + 1));
   }
-  if (rotations && !aligned16(rotations)) return fail(GSR_ERR_ARGUMENT, "rotations must be 16-byte aligned");
-  if (!alloc) return fail(GSR_ERR_ARGUMENT, "allocator callback missing");
+  if (m.rotations && !aligned16(m.rotations))
+    return fail(GSR_ERR_ARGUMENT, "rotations must be 16-byte aligned");
+  if (scan_parts((size_t)m.P) > (size_t)kScanMaxParts)
+    return fail(GSR_ERR_TOO_LARGE, "P = %d exceeds the scan capacity", m.P);
+  return GSR_OK;
+}
 
-  const uint32_t gx = (uint32_t)((W + kTile - 1) / kTile), gy = (uint32_t)((H + kTile - 1) / kTile);
-  const uint32_t ntiles = gx * gy;
-  if (scan_parts((size_t)P) > (size_t)kScanMaxParts)
-    return fail(GSR_ERR_TOO_LARGE, "P = %d exceeds the scan capacity", P);
+// Phase 1: preprocess, the instance counts' read-back (queued, not waited for), depth sort and
+// scan.  Nothing here blocks the host.
+static int fwd_begin(const FwdModel& m, FwdCam& c) {
+  const int debug = m.debug;
+  hipStream_t stream = c.stream;
+  const int W = c.W, H = c.H, P = m.P;
+  if ((c.pre_color == nullptr) != (c.pre_clamp == nullptr) || (c.pre_color && !m.fused))
+    return fail(GSR_ERR_ARGUMENT, "pre_color / pre_clamp: both or neither, fused path only");
+  if (W <= 0 || H <= 0) return fail(GSR_ERR_ARGUMENT, "image size must be positive (got %dx%d)", W, H);
+  if (!c.out_color) return fail(GSR_ERR_ARGUMENT, "out_color / num_rendered missing");
+  const size_t HW = (size_t)W * H;
+  if (P == 0) {
+    c.done = true;
+    GSR_CHECK(hipMemsetAsync(c.out_color, 0, 3 * HW * sizeof(float), stream));
+    if (c.out_depth) GSR_CHECK(hipMemsetAsync(c.out_depth, 0, HW * sizeof(float), stream));
+    if (c.out_alpha) GSR_CHECK(hipMemsetAsync(c.out_alpha, 0, HW * sizeof(float), stream));
+    if (c.out_feature) GSR_CHECK(hipMemsetAsync(c.out_feature, 0, 3 * HW * sizeof(float), stream));
+    return GSR_OK;
+  }
+  if (!c.view || !c.proj || !c.campos)
+    return fail(GSR_ERR_ARGUMENT, "background/means3D/opacities/viewmatrix/projmatrix/campos required");
+  if (!c.alloc) return fail(GSR_ERR_ARGUMENT, "allocator callback missing");
+  if (!c.host || !c.ready) return fail(GSR_ERR_HIP, "pinned host slot / event creation failed");
+  c.gx = (uint32_t)((W + kTile - 1) / kTile);
+  c.gy = (uint32_t)((H + kTile - 1) / kTile);
 
   const size_t gbytes = carve_geom(nullptr, (size_t)P).bytes;
-  char* gbase = (char*)alloc(alloc_ctx, gbytes, GSR_BUF_GEOM);
-  if (!gbase) return fail(GSR_ERR_ALLOC, "geometry buffer allocation of %zu bytes failed", gbytes);
+  c.gbase = (char*)c.alloc(c.alloc_ctx, gbytes, GSR_BUF_GEOM);
+  if (!c.gbase) return fail(GSR_ERR_ALLOC, "geometry buffer allocation of %zu bytes failed", gbytes);
   const size_t ibytes = carve_img(nullptr, (size_t)W, (size_t)H).bytes;
-  char* ibase = (char*)alloc(alloc_ctx, ibytes, GSR_BUF_IMAGE);
-  if (!ibase) return fail(GSR_ERR_ALLOC, "image buffer allocation of %zu bytes failed", ibytes);
-  GeomState g = carve_geom(gbase, (size_t)P);
-  ImgState im = carve_img(ibase, (size_t)W, (size_t)H);
-  int32_t* radii_ptr = radii ? radii : g.radii;
+  c.ibase = (char*)c.alloc(c.alloc_ctx, ibytes, GSR_BUF_IMAGE);
+  if (!c.ibase) return fail(GSR_ERR_ALLOC, "image buffer allocation of %zu bytes failed", ibytes);
+  c.g = carve_geom(c.gbase, (size_t)P);
+  c.im = carve_img(c.ibase, (size_t)W, (size_t)H);
+  const GeomState& g = c.g;
+  c.radii_ptr = c.radii ? c.radii : g.radii;
 
   // flags[0] (prefiltered violation) is only written -- and only read back -- when prefiltered
-  if (prefiltered) GSR_CHECK(hipMemsetAsync(g.flags, 0, 4 * sizeof(uint32_t), stream));
+  if (m.prefiltered) GSR_CHECK(hipMemsetAsync(g.flags, 0, 4 * sizeof(uint32_t), stream));
   PreArgs pa{};
-  pa.P = P; pa.D = degree; pa.M = M; pa.W = W; pa.H = H; pa.gx = gx; pa.gy = gy;
-  pa.means3D = means3D; pa.scales = scales; pa.rotations = rotations; pa.opacities = opacities;
-  pa.shs = sh; pa.cov3D_precomp = cov3D_precomp; pa.colors_precomp = colors_precomp;
-  pa.sh_language = sh_language; pa.lang_precomp = language_feature_precomp;
-  pa.confidence = confidence;
-  pa.view = viewmatrix; pa.proj = projmatrix; pa.campos = campos;
-  pa.scale_modifier = scale_modifier; pa.tanx = tan_fovx; pa.tany = tan_fovy;
-  pa.fy = (float)H / (2.0f * tan_fovy);  // rasterizer_impl.cu:222-223
-  pa.fx = (float)W / (2.0f * tan_fovx);
-  pa.prefiltered = prefiltered; pa.include_feature = include_feature;
-  pa.radii = radii_ptr; pa.g = g;
-  pa.fused = fused; pa.sh_dc = sh_dc; pa.sh_rest = sh_rest;
-  pa.pre_color = pre_color; pa.pre_clamp = pre_clamp;
+  pa.P = P; pa.D = m.degree; pa.M = m.M; pa.W = W; pa.H = H; pa.gx = c.gx; pa.gy = c.gy;
+  pa.means3D = m.means3D; pa.scales = m.scales; pa.rotations = m.rotations;
+  pa.opacities = m.opacities;
+  pa.shs = m.sh; pa.cov3D_precomp = m.cov3D_precomp; pa.colors_precomp = m.colors_precomp;
+  pa.sh_language = m.sh_language; pa.lang_precomp = m.lang_precomp;
+  pa.confidence = m.confidence;
+  pa.view = c.view; pa.proj = c.proj; pa.campos = c.campos;
+  pa.scale_modifier = m.scale_modifier; pa.tanx = c.tanx; pa.tany = c.tany;
+  pa.fy = (float)H / (2.0f * c.tany);  // rasterizer_impl.cu:222-223
+  pa.fx = (float)W / (2.0f * c.tanx);
+  pa.prefiltered = m.prefiltered; pa.include_feature = m.include_feature;
+  pa.radii = c.radii_ptr; pa.g = g;
+  pa.fused = m.fused; pa.sh_dc = m.sh_dc; pa.sh_rest = m.sh_rest;
+  pa.pre_color = c.pre_color; pa.pre_clamp = c.pre_clamp;
   // the preprocess grid also zeroes the depth sort's scratch and the backward's accumulators
   pa.clear = SideClear{g.sort.aux, sort_clear_bytes(g.sort, (size_t)P, 32)};
-  pa.acc_zero = rows ? 0 : 1;  // the rows layout never reads the accumulator rows
+  pa.acc_zero = m.rows ? 0 : 1;  // the rows layout never reads the accumulator rows
   pa.parts = g.pre_parts;
   PROF_BEGIN(PREPROCESS);
   GSR_CHECK(launch_preprocess(pa, stream));
@@ -498,13 +521,10 @@ static int forward_impl(int P, int M, const float* background, const float* mean
   const size_t pre_blocks = ((size_t)P + 255) / 256;
   GSR_CHECK(sum_u32_parts(g.pre_parts, pre_blocks, g.flags + 1, stream, g.pre_parts + pre_blocks));
   PROF_END(PREPROCESS);
-  uint32_t* host = pinned_slot();
-  hipEvent_t ready = readback_event();
-  if (!host || !ready) return fail(GSR_ERR_HIP, "pinned host slot / event creation failed");
   // one read-back: flags[0] (prefiltered violation), R and the reference's count.  The sorts'
   // look-back timeouts are this call's status (mailbox below), not part of this wait.
-  GSR_CHECK(hipMemcpyAsync(host, g.flags, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
-  GSR_CHECK(hipEventRecord(ready, stream));
+  GSR_CHECK(hipMemcpyAsync(c.host, g.flags, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+  GSR_CHECK(hipEventRecord(c.ready, stream));
 
   bool in_b = false;
   PROF_BEGIN(DEPTH_SORT);
@@ -513,22 +533,40 @@ static int forward_impl(int P, int M, const float* background, const float* mean
                              g.sort, &in_b, stream, /*sentinel_anywhere=*/true,
                              /*precleared=*/true, /*key_payload=*/g.tiles_touched));
   PROF_END(DEPTH_SORT);
-  const uint32_t* order = in_b ? g.dval_b : g.dval_a;
+  c.depth_in_b = in_b;
   const uint32_t* counts_sorted = in_b ? g.dkey_b : g.dkey_a;
   PROF_BEGIN(SCAN);
   GSR_CHECK(scan_u32(counts_sorted, nullptr, g.offsets, (size_t)P, true, g.scan_parts, stream));
   PROF_END(SCAN);
+  return GSR_OK;
+}
 
+// Phase 2a: wait for the read-back (the one host synchronisation of a view, as
+// rasterizer_impl.cu:281), then duplicate, tile sort and ranges; the blend's arguments are left in
+// c.ra (launched by fwd_end, or with other views' by the multi-view call).
+static int fwd_bin(const FwdModel& m, FwdCam& c) {
+  if (c.done) {
+    c.num_rendered = c.num_instances = 0;
+    return GSR_OK;
+  }
+  int debug = m.debug;
+  hipStream_t stream = c.stream;
+  const int P = m.P;
+  const GeomState& g = c.g;
+  const ImgState& im = c.im;
+  const uint32_t ntiles = c.gx * c.gy;
+  const uint32_t* order = c.depth_in_b ? g.dval_b : g.dval_a;
   {
     const auto t0 = std::chrono::steady_clock::now();
-    GSR_CHECK(hipEventSynchronize(ready));
+    GSR_CHECK(hipEventSynchronize(c.ready));
     g_wait_ns.fetch_add((long long)std::chrono::duration_cast<std::chrono::nanoseconds>(
                             std::chrono::steady_clock::now() - t0).count(),
                         std::memory_order_relaxed);
   }
+  uint32_t* host = c.host;
   const uint32_t R = host[1];       // instances binned: tiles that pass the exact cull
   const uint32_t R_ref = host[2];   // the reference's num_rendered (full rectangles), R <= R_ref
-  if (prefiltered && host[0]) return fail(GSR_ERR_PREFILTERED,
+  if (m.prefiltered && host[0]) return fail(GSR_ERR_PREFILTERED,
                            "Point is filtered although prefiltered is set. This shouldn't happen!");
   if (R_ref > 0x7fffffffu || R > R_ref)
     return fail(GSR_ERR_TOO_LARGE, "num_rendered = %u exceeds the sort capacity", R_ref);
@@ -538,18 +576,18 @@ static int forward_impl(int P, int M, const float* background, const float* mean
     if (host[2]) return fail(GSR_ERR_HIP, "depth sort look-back timed out");
   }
 
-  const size_t bbytes = carve_bin(nullptr, R_ref, rows).bytes;
-  char* bbase = (char*)alloc(alloc_ctx, bbytes, GSR_BUF_BINNING);
-  if (!bbase) return fail(GSR_ERR_ALLOC, "binning buffer allocation of %zu bytes failed", bbytes);
-  BinState b = carve_bin(bbase, R_ref, rows);  // capacity R_ref, the first R entries used
+  const size_t bbytes = carve_bin(nullptr, R_ref, m.rows).bytes;
+  c.bbase = (char*)c.alloc(c.alloc_ctx, bbytes, GSR_BUF_BINNING);
+  if (!c.bbase) return fail(GSR_ERR_ALLOC, "binning buffer allocation of %zu bytes failed", bbytes);
+  BinState b = carve_bin(c.bbase, R_ref, m.rows);  // capacity R_ref, the first R entries used
 
   PROF_BEGIN(DUPLICATE);
   // the duplicate grid also zeroes the tile sort's scratch and the tile ranges
   const int tbits = tile_bits(ntiles);
-  GSR_CHECK(launch_duplicate(P, order, g.offsets, radii_ptr, g.rec, gx, gy, b.tkey_a, b.tval_a,
+  GSR_CHECK(launch_duplicate(P, order, g.offsets, c.radii_ptr, g.rec, c.gx, c.gy, b.tkey_a, b.tval_a,
                              (uint32_t)R, SideClear{b.sort.aux, sort_clear_bytes(b.sort, R, tbits)},
                              SideClear{im.ranges, sizeof(uint2) * ntiles}, stream,
-                             rows ? b.egid : nullptr, rows ? g.ebeg : nullptr));
+                             m.rows ? b.egid : nullptr, m.rows ? g.ebeg : nullptr));
   PROF_END(DUPLICATE);
   bool t_in_b = false;
   PROF_BEGIN(TILE_SORT);
@@ -563,38 +601,121 @@ static int forward_impl(int P, int M, const float* background, const float* mean
   }
   const uint32_t* tiles_sorted = t_in_b ? b.tkey_b : b.tkey_a;
   const uint32_t* point_list = t_in_b ? b.tval_b : b.tval_a;
-  if (rows) {  // the sorted values are emission indices: Gaussian ids into the other value array
+  if (m.rows) {  // the sorted values are emission indices: Gaussian ids into the other value array
     uint32_t* pl = t_in_b ? b.tval_a : b.tval_b;
     GSR_CHECK(launch_det_gather(R, point_list, b.egid, pl, stream));
     point_list = pl;
   }
   int mail_slot = -1;
-  uint32_t* host_status = mail_post(ibase, &mail_slot);
+  uint32_t* host_status = mail_post(c.ibase, &mail_slot);
   PROF_BEGIN(RANGES);
   GSR_CHECK(launch_tile_ranges(R, tiles_sorted, im.ranges, ntiles, g.sort.aux + kSortAuxErr,
                                b.sort.aux + kSortAuxErr, im.status, host_status,
                                forward_faults_word(), stream, /*ranges_cleared=*/true));
   PROF_END(RANGES);
 
-  RenderArgs ra{};
-  ra.W = W; ra.H = H; ra.gx = gx; ra.gy = gy;
-  ra.ranges = im.ranges; ra.point_list = point_list; ra.rec = g.rec; ra.P = (uint32_t)P; ra.bg = background;
+  RenderArgs& ra = c.ra;
+  ra.W = c.W; ra.H = c.H; ra.gx = c.gx; ra.gy = c.gy;
+  ra.ranges = im.ranges; ra.point_list = point_list; ra.rec = g.rec; ra.P = (uint32_t)P;
+  ra.bg = m.background;
   ra.final_T = im.final_T; ra.n_contrib = im.n_contrib; ra.tile_last = im.tile_last;
-  ra.out_color = out_color; ra.out_depth = out_depth; ra.out_alpha = out_alpha;
-  ra.out_feature = out_feature; ra.include_feature = include_feature;
+  ra.out_color = c.out_color; ra.out_depth = c.out_depth; ra.out_alpha = c.out_alpha;
+  ra.out_feature = c.out_feature; ra.include_feature = m.include_feature;
   ra.order = im.order; ra.sched = tile_schedule_mode();
   ra.status = im.status; ra.host_status = host_status; ra.fault = forward_faults_word();
-  PROF_BEGIN(RENDER_FWD);
-  GSR_CHECK(launch_render_forward(ra, stream));
-  PROF_END(RENDER_FWD);
-  GSR_CHECK(mail_arm(mail_slot, stream));
+  c.mail_slot = mail_slot;
+  c.num_rendered = (int)R_ref;
+  c.num_instances = (int)R;
+  return GSR_OK;
+}
+
+// After the view's blend has been issued on `stream`: its mailbox event, the debug check, and the
+// accumulator rows marked clean for the backward.
+static int fwd_blended(const FwdModel& m, FwdCam& c, hipStream_t stream) {
+  if (c.done) return GSR_OK;
+  const int debug = m.debug;
+  GSR_CHECK(mail_arm(c.mail_slot, stream));
   if (debug) {
-    const uint32_t v = mail_check(ibase, true);
+    const uint32_t v = mail_check(c.ibase, true);
     if (v) return fail(GSR_ERR_SORT, "%s", status_message(v).c_str());
   }
-  *num_rendered = (int)R_ref;
-  g_last_instances = (int)R;
-  if (!rows) acc_mark_clean(gbase);
+  if (!m.rows) acc_mark_clean(c.gbase);
+  return GSR_OK;
+}
+
+// Phase 2 of a single view: binning, then its blend on its own stream.
+static int fwd_end(const FwdModel& m, FwdCam& c) {
+  if (int rc = fwd_bin(m, c)) return rc;
+  if (c.done) return GSR_OK;
+  const int debug = m.debug;
+  hipStream_t stream = c.stream;
+  PROF_BEGIN(RENDER_FWD);
+  GSR_CHECK(launch_render_forward(c.ra, stream));
+  PROF_END(RENDER_FWD);
+  return fwd_blended(m, c, stream);
+}
+
+// Pinned read-back slots and their events for the views in flight of one host thread (a
+// multi-view call has up to kFwdSlots views between their two phases).
+constexpr int kFwdSlots = 64;
+static uint32_t* pinned_slot(int i) {
+  thread_local uint32_t* p = nullptr;
+  if (!p) {
+    if (hipHostMalloc((void**)&p, 16 * kFwdSlots, hipHostMallocDefault) != hipSuccess) p = nullptr;
+  }
+  return p ? p + 4 * i : nullptr;
+}
+static hipEvent_t readback_event(int i) {
+  constexpr int kMaxDev = 64;
+  thread_local hipEvent_t ev[kMaxDev][kFwdSlots] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return nullptr;
+  if (!ev[dev][i] && hipEventCreateWithFlags(&ev[dev][i], hipEventDisableTiming) != hipSuccess)
+    ev[dev][i] = nullptr;
+  return ev[dev][i];
+}
+
+static int forward_impl(int P, int M, const float* background, const float* means3D,
+                        const float* colors_precomp, const float* opacities, const float* scales,
+                        const float* rotations, float scale_modifier, const float* cov3D_precomp,
+                        const float* viewmatrix, const float* projmatrix, float tan_fovx,
+                        float tan_fovy, int image_height, int image_width, const float* sh,
+                        int degree, const float* campos, int prefiltered, const float* sh_language,
+                        const float* language_feature_precomp, const float* confidence,
+                        int include_feature, float* out_color, float* out_depth, float* out_alpha,
+                        float* out_feature, int* radii, int* num_rendered, gsr_alloc_fn alloc,
+                        void* alloc_ctx, void* stream_ptr, int debug, int fused,
+                        const float* sh_dc, const float* sh_rest,
+                        const float* pre_color = nullptr, const uint8_t* pre_clamp = nullptr) {
+  g_err.clear();
+  FwdModel m;
+  m.det = (debug & GSR_DEBUG_DETERMINISTIC) != 0;  // gsr.h: debug bit 1
+  m.rows = m.det || bwd_rows_mode();  // per-instance gradient rows (binning layout)
+  m.debug = debug & 1;
+  m.P = P; m.M = M; m.background = background; m.means3D = means3D;
+  m.colors_precomp = colors_precomp; m.opacities = opacities; m.scales = scales;
+  m.rotations = rotations; m.scale_modifier = scale_modifier; m.cov3D_precomp = cov3D_precomp;
+  m.sh = sh; m.degree = degree; m.prefiltered = prefiltered; m.sh_language = sh_language;
+  m.lang_precomp = language_feature_precomp; m.confidence = confidence;
+  m.include_feature = include_feature; m.fused = fused; m.sh_dc = sh_dc; m.sh_rest = sh_rest;
+  if (!num_rendered || !out_color) return fail(GSR_ERR_ARGUMENT, "out_color / num_rendered missing");
+  if (image_width <= 0 || image_height <= 0)
+    return fail(GSR_ERR_ARGUMENT, "image size must be positive (got %dx%d)", image_width, image_height);
+  if (int rc = fwd_check_model(m)) return rc;
+  FwdCam c;
+  c.view = viewmatrix; c.proj = projmatrix; c.campos = campos; c.tanx = tan_fovx; c.tany = tan_fovy;
+  c.W = image_width; c.H = image_height; c.pre_color = pre_color; c.pre_clamp = pre_clamp;
+  c.out_color = out_color; c.out_depth = out_depth; c.out_alpha = out_alpha;
+  c.out_feature = out_feature; c.radii = radii; c.alloc = alloc; c.alloc_ctx = alloc_ctx;
+  c.stream = (hipStream_t)stream_ptr;
+  if (P > 0) {
+    c.host = pinned_slot(0);
+    c.ready = readback_event(0);
+  }
+  if (int rc = fwd_begin(m, c)) return rc;
+  if (int rc = fwd_end(m, c)) return rc;
+  *num_rendered = c.num_rendered;
+  g_last_instances = c.num_instances;
   return GSR_OK;
 }
 
@@ -655,8 +776,22 @@ int gsr_rasterize_gaussians_fused_precolor(
                       debug, 1, features_dc, features_rest, pre_color, pre_clamp);
 }
 
-static int backward_impl(
-    int P, int M, int R, const float* background, const float* means3D, const int* radii,
+// ---- backward, in two parts per view ----------------------------------------------------------
+// The blend part (accumulator zeroing + backward blend) and the per-Gaussian part (backward
+// preprocess) of one view's backward, with their launch arguments.
+struct BwdCall {
+  bool done = false;       // P == 0: nothing to do
+  bool blend = false;      // R > 0
+  bool acc_zero = false;   // the accumulator rows were not zeroed by this buffer's forward
+  float* acc = nullptr;
+  size_t P = 0;
+  int debug = 0;
+  RenderBwdArgs rb{};
+  BwdPreArgs ba{};
+};
+
+static int bwd_setup(
+    BwdCall& call, int P, int M, int R, const float* background, const float* means3D, const int* radii,
     const float* colors_precomp, const float* scales, const float* rotations, float scale_modifier,
     const float* cov3D_precomp, const float* viewmatrix, const float* projmatrix, float tan_fovx,
     float tan_fovy, int image_height, int image_width, const float* dL_dout_color,
@@ -666,13 +801,13 @@ static int backward_impl(
     void* geom_buffer, void* binning_buffer, void* image_buffer, float* dL_dmeans2D,
     float* dL_dcolors, float* dL_dopacity, float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh,
     float* dL_dscales, float* dL_drotations, float* dL_dsh_language, float* dL_dlanguage_feature,
-    void* stream_ptr, int debug, int fused, const float* sh_dc, const float* sh_rest,
-    const float* opacity_raw, float* dL_dsh_rest, int accumulate, float* dRGB_sh = nullptr,
-    const float* pre_jac = nullptr) {
-  g_err.clear();
+    int debug, int fused, const float* sh_dc, const float* sh_rest,
+    const float* opacity_raw, float* dL_dsh_rest, int accumulate, float* dRGB_sh,
+    const float* pre_jac) {
   const bool det = (debug & GSR_DEBUG_DETERMINISTIC) != 0;  // must match the forward's flags
   const bool rows = det || bwd_rows_mode();
   debug &= 1;
+  call.debug = debug;
   if (fused && P != 0) {
     if (!sh_dc || (M > 1 && !sh_rest) || (M > 1 && !dL_dsh_rest && !dRGB_sh) || !scales ||
         !rotations || !opacity_raw)
@@ -683,10 +818,12 @@ static int backward_impl(
   }
   if (pre_jac && !dRGB_sh)
     return fail(GSR_ERR_ARGUMENT, "pre_jac needs the deferred SH gradients (dL_dcolor_sh)");
-  hipStream_t stream = (hipStream_t)stream_ptr;
   const int W = image_width, H = image_height;
   if (P < 0 || R < 0 || W <= 0 || H <= 0) return fail(GSR_ERR_ARGUMENT, "invalid sizes");
-  if (P == 0) return GSR_OK;
+  if (P == 0) {
+    call.done = true;
+    return GSR_OK;
+  }
   if (!geom_buffer || !image_buffer || (R > 0 && !binning_buffer))
     return fail(GSR_ERR_ARGUMENT, "forward scratch buffers missing");
   // the forward of these buffers failed and has already said so (no wait; the device side
@@ -721,26 +858,20 @@ static int backward_impl(
   }
   const int32_t* radii_ptr = radii ? radii : g.radii;
 
-  if (!rows && !acc_take_clean(geom_buffer)) {  // not freshly zeroed by this buffer's forward
-    PROF_BEGIN(ACC_ZERO);
-    GSR_CHECK(hipMemsetAsync(g.acc, 0, sizeof(float) * kAccFloats * (size_t)P, stream));
-    PROF_END(ACC_ZERO);
-  }
-  if (R > 0) {
-    RenderBwdArgs rb{};
-    rb.W = W; rb.H = H; rb.gx = gx; rb.gy = gy;
-    rb.ranges = im.ranges; rb.point_list = point_list; rb.rec = g.rec; rb.P = (uint32_t)P; rb.bg = background;
-    rb.final_T = im.final_T; rb.n_contrib = im.n_contrib; rb.tile_last = im.tile_last;
-    rb.dL_dcolor = dL_dout_color; rb.dL_ddepth = dL_dout_depth; rb.dL_dalpha = dL_dout_alpha;
-    rb.dL_dfeature = dL_dout_feature; rb.acc = g.acc; rb.include_feature = include_feature;
-    rb.order = im.order; rb.sched = tile_schedule_mode();
-    rb.einst = einst; rb.partial = rows ? b.partial : nullptr; rb.det = det ? 1 : 0;
-    rb.nrows = (uint32_t)R; rb.status = im.status;
-    PROF_BEGIN(RENDER_BWD);
-    GSR_CHECK(launch_render_backward(rb, stream));
-    PROF_END(RENDER_BWD);
-  }
-  BwdPreArgs ba{};
+  call.P = (size_t)P;
+  call.acc = g.acc;
+  call.acc_zero = !rows && !acc_take_clean(geom_buffer);  // not freshly zeroed by its forward
+  call.blend = R > 0;
+  RenderBwdArgs& rb = call.rb;
+  rb.W = W; rb.H = H; rb.gx = gx; rb.gy = gy;
+  rb.ranges = im.ranges; rb.point_list = point_list; rb.rec = g.rec; rb.P = (uint32_t)P; rb.bg = background;
+  rb.final_T = im.final_T; rb.n_contrib = im.n_contrib; rb.tile_last = im.tile_last;
+  rb.dL_dcolor = dL_dout_color; rb.dL_ddepth = dL_dout_depth; rb.dL_dalpha = dL_dout_alpha;
+  rb.dL_dfeature = dL_dout_feature; rb.acc = g.acc; rb.include_feature = include_feature;
+  rb.order = im.order; rb.sched = tile_schedule_mode();
+  rb.einst = einst; rb.partial = rows ? b.partial : nullptr; rb.det = det ? 1 : 0;
+  rb.nrows = (uint32_t)R; rb.status = im.status;
+  BwdPreArgs& ba = call.ba;
   ba.P = P; ba.D = degree; ba.M = M;
   ba.means3D = means3D; ba.scales = scales; ba.rotations = rotations; ba.shs = sh;
   ba.cov3D = cov3D_precomp; ba.colors_precomp = colors_precomp;
@@ -766,10 +897,65 @@ static int backward_impl(
   ba.rows = R > 0 && rows ? reinterpret_cast<const float4*>(b.partial) : nullptr;
   ba.ebeg = g.ebeg; ba.count = g.tiles_touched;
   if (dRGB_sh) ba.dL_dsh = ba.dL_dsh_rest = nullptr;
+  return GSR_OK;
+}
+
+// accumulator zeroing (when needed) + the backward blend
+static int bwd_blend(const BwdCall& call, hipStream_t stream) {
+  const int debug = call.debug;
+  if (call.done) return GSR_OK;
+  if (call.acc_zero) {
+    PROF_BEGIN(ACC_ZERO);
+    GSR_CHECK(hipMemsetAsync(call.acc, 0, sizeof(float) * kAccFloats * call.P, stream));
+    PROF_END(ACC_ZERO);
+  }
+  if (call.blend) {
+    PROF_BEGIN(RENDER_BWD);
+    GSR_CHECK(launch_render_backward(call.rb, stream));
+    PROF_END(RENDER_BWD);
+  }
+  return GSR_OK;
+}
+
+// the fused per-Gaussian backward (computeCov2DCUDA + preprocessCUDA backward + activations)
+static int bwd_pre(const BwdCall& call, hipStream_t stream) {
+  const int debug = call.debug;
+  if (call.done) return GSR_OK;
   PROF_BEGIN(PREPROCESS_BWD);
-  GSR_CHECK(launch_preprocess_backward(ba, stream));
+  GSR_CHECK(launch_preprocess_backward(call.ba, stream));
   PROF_END(PREPROCESS_BWD);
   return GSR_OK;
+}
+
+static int backward_impl(
+    int P, int M, int R, const float* background, const float* means3D, const int* radii,
+    const float* colors_precomp, const float* scales, const float* rotations, float scale_modifier,
+    const float* cov3D_precomp, const float* viewmatrix, const float* projmatrix, float tan_fovx,
+    float tan_fovy, int image_height, int image_width, const float* dL_dout_color,
+    const float* dL_dout_depth, const float* dL_dout_alpha, const float* dL_dout_feature,
+    const float* sh, int degree, const float* campos, const float* sh_language,
+    const float* language_feature_precomp, const float* confidence, int include_feature,
+    void* geom_buffer, void* binning_buffer, void* image_buffer, float* dL_dmeans2D,
+    float* dL_dcolors, float* dL_dopacity, float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh,
+    float* dL_dscales, float* dL_drotations, float* dL_dsh_language, float* dL_dlanguage_feature,
+    void* stream_ptr, int debug, int fused, const float* sh_dc, const float* sh_rest,
+    const float* opacity_raw, float* dL_dsh_rest, int accumulate, float* dRGB_sh = nullptr,
+    const float* pre_jac = nullptr) {
+  g_err.clear();
+  BwdCall call;
+  if (int rc = bwd_setup(call, P, M, R, background, means3D, radii, colors_precomp, scales,
+                         rotations, scale_modifier, cov3D_precomp, viewmatrix, projmatrix,
+                         tan_fovx, tan_fovy, image_height, image_width, dL_dout_color,
+                         dL_dout_depth, dL_dout_alpha, dL_dout_feature, sh, degree, campos,
+                         sh_language, language_feature_precomp, confidence, include_feature,
+                         geom_buffer, binning_buffer, image_buffer, dL_dmeans2D, dL_dcolors,
+                         dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations,
+                         dL_dsh_language, dL_dlanguage_feature, debug, fused, sh_dc, sh_rest,
+                         opacity_raw, dL_dsh_rest, accumulate, dRGB_sh, pre_jac))
+    return rc;
+  hipStream_t stream = (hipStream_t)stream_ptr;
+  if (int rc = bwd_blend(call, stream)) return rc;
+  return bwd_pre(call, stream);
 }
 
 int gsr_rasterize_gaussians_backward(
@@ -837,6 +1023,202 @@ int gsr_rasterize_gaussians_fused_backward_deferred(
                        dL_dfeatures_dc, dL_dscaling_raw, dL_drotation_raw, dL_dlanguage_feature,
                        nullptr, stream_ptr, debug, 1, features_dc, features_rest, opacity_raw,
                        dL_dfeatures_rest, accumulate, dL_dcolor_sh, pre_jac);
+}
+
+// ---- multi-view calls --------------------------------------------------------------------------
+namespace {
+// per host thread: events joining the views' streams with the call's stream
+hipEvent_t join_event(int i) {
+  constexpr int kMaxDev = 64;
+  thread_local hipEvent_t ev[kMaxDev][kFwdSlots + 1] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return nullptr;
+  if (!ev[dev][i] && hipEventCreateWithFlags(&ev[dev][i], hipEventDisableTiming) != hipSuccess)
+    ev[dev][i] = nullptr;
+  return ev[dev][i];
+}
+}  // namespace
+
+int gsr_rasterize_views_fused(int V, gsr_view* views, int image_height, int image_width, int P,
+                              int M, const float* background, const float* means3D,
+                              const float* features_dc, const float* features_rest,
+                              const float* opacity_raw, const float* scaling_raw,
+                              const float* rotation_raw, float scale_modifier, int degree,
+                              int prefiltered, const float* language_feature,
+                              const float* confidence, int include_feature, gsr_alloc_fn alloc,
+                              int inflight, void* stream_ptr, int debug) {
+  g_err.clear();
+  if (V < 0 || V > kFwdSlots) return fail(GSR_ERR_ARGUMENT, "V = %d views: 0 .. %d supported", V, kFwdSlots);
+  if (V > 0 && !views) return fail(GSR_ERR_ARGUMENT, "views missing");
+  if (image_width <= 0 || image_height <= 0)
+    return fail(GSR_ERR_ARGUMENT, "image size must be positive (got %dx%d)", image_width, image_height);
+  FwdModel m;
+  m.det = (debug & GSR_DEBUG_DETERMINISTIC) != 0;
+  m.rows = m.det || bwd_rows_mode();
+  m.debug = debug & 1;
+  m.P = P; m.M = M; m.background = background; m.means3D = means3D;
+  m.opacities = opacity_raw; m.scales = scaling_raw; m.rotations = rotation_raw;
+  m.scale_modifier = scale_modifier; m.degree = degree; m.prefiltered = prefiltered;
+  m.sh_language = language_feature; m.confidence = confidence;
+  m.include_feature = include_feature; m.fused = 1; m.sh_dc = features_dc; m.sh_rest = features_rest;
+  if (int rc = fwd_check_model(m)) return rc;
+  hipStream_t call_stream = (hipStream_t)stream_ptr;
+  std::vector<FwdCam> cams((size_t)V);
+  for (int v = 0; v < V; v++) {
+    const gsr_view& in = views[v];
+    FwdCam& c = cams[(size_t)v];
+    c.view = in.viewmatrix; c.proj = in.projmatrix; c.campos = in.campos;
+    c.tanx = in.tan_fovx; c.tany = in.tan_fovy; c.W = image_width; c.H = image_height;
+    c.pre_color = in.pre_color; c.pre_clamp = in.pre_clamp;
+    c.out_color = in.out_color; c.out_depth = in.out_depth; c.out_alpha = in.out_alpha;
+    c.out_feature = in.out_feature; c.radii = in.radii;
+    c.alloc = alloc; c.alloc_ctx = in.alloc_ctx;
+    c.stream = in.stream ? (hipStream_t)in.stream : call_stream;
+    c.host = pinned_slot(v);
+    c.ready = readback_event(v);
+  }
+  // the views' streams start after the call's stream (inputs prepared there)
+  hipEvent_t start = join_event(kFwdSlots);
+  if (!start || hipEventRecord(start, call_stream) != hipSuccess)
+    return fail(GSR_ERR_HIP, "event record on the call's stream failed");
+  for (int v = 0; v < V; v++)
+    if (cams[(size_t)v].stream != call_stream &&
+        hipStreamWaitEvent(cams[(size_t)v].stream, start, 0) != hipSuccess)
+      return fail(GSR_ERR_HIP, "stream wait failed");
+  // Software-pipelined issue: the first phase of view v + inflight goes out right after view v's
+  // binning, so per stream the order stays begin(v), bin(v), begin(v + inflight), ...  The blends
+  // of a group of views run merged into one launch on the call's stream once the group's binning
+  // is done (`groups` groups of consecutive views; GSR_VIEWS_FWD_GROUPS), while the views' streams
+  // go on with the next views' preprocess / sorts.
+  const int ahead = inflight < 1 ? 1 : inflight;
+  static const int groups_env = [] {
+    const char* e = getenv("GSR_VIEWS_FWD_GROUPS");
+    return e ? atoi(e) : 2;
+  }();
+  const int ng = groups_env < 1 ? 1 : groups_env;
+  int per = (V + ng - 1) / ng;
+  if (per < 1) per = 1;
+  if (per > kMaxFwdViews) per = kMaxFwdViews;
+  for (int v = 0; v < V && v < ahead; v++)
+    if (int rc = fwd_begin(m, cams[(size_t)v])) return rc;
+  for (int v0 = 0; v0 < V; v0 += per) {
+    const int n = V - v0 < per ? V - v0 : per;
+    RenderArgs ras[kMaxFwdViews];
+    int nb = 0;
+    for (int k = 0; k < n; k++) {
+      const int v = v0 + k;
+      FwdCam& c = cams[(size_t)v];
+      if (int rc = fwd_bin(m, c)) return rc;
+      if (!c.done) {
+        const int debug = m.debug;
+        hipStream_t stream = c.stream;
+        GSR_CHECK(launch_render_schedule(c.ra, stream));
+        ras[nb++] = c.ra;
+      }
+      if (v + ahead < V)
+        if (int rc = fwd_begin(m, cams[(size_t)(v + ahead)])) return rc;
+      gsr_view& out = views[v];
+      out.geom_buffer = c.gbase; out.binning_buffer = c.bbase; out.image_buffer = c.ibase;
+      out.num_rendered = c.num_rendered; out.num_instances = c.num_instances;
+      if (c.stream != call_stream) {
+        hipEvent_t e = join_event(v);
+        if (!e || hipEventRecord(e, c.stream) != hipSuccess ||
+            hipStreamWaitEvent(call_stream, e, 0) != hipSuccess)
+          return fail(GSR_ERR_HIP, "joining view %d's stream failed", v);
+      }
+    }
+    if (nb > 0) {
+      const int debug = m.debug;
+      hipStream_t stream = call_stream;
+      PROF_BEGIN(RENDER_FWD);
+      GSR_CHECK(launch_render_forward_views(ras, nb, call_stream));
+      PROF_END(RENDER_FWD);
+    }
+    for (int k = 0; k < n; k++)
+      if (int rc = fwd_blended(m, cams[(size_t)(v0 + k)], call_stream)) return rc;
+  }
+  if (V > 0) g_last_instances = cams[(size_t)V - 1].num_instances;
+  return GSR_OK;
+}
+
+int gsr_rasterize_views_fused_backward(
+    int V, const gsr_view* views, int image_height, int image_width, int P, int M,
+    const float* background, const float* means3D, const float* features_dc,
+    const float* features_rest, const float* opacity_raw, const float* scaling_raw,
+    const float* rotation_raw, float scale_modifier, int degree, const float* language_feature,
+    const float* confidence, int include_feature, float* dL_dmeans3D, float* dL_dfeatures_dc,
+    float* dL_dfeatures_rest, float* dL_dopacity_raw, float* dL_dscaling_raw,
+    float* dL_drotation_raw, float* dL_dlanguage_feature, int accumulate, void* stream_ptr,
+    int debug) {
+  g_err.clear();
+  if (V < 0 || V > kFwdSlots) return fail(GSR_ERR_ARGUMENT, "V = %d views: 0 .. %d supported", V, kFwdSlots);
+  if (V > 0 && !views) return fail(GSR_ERR_ARGUMENT, "views missing");
+  hipStream_t call_stream = (hipStream_t)stream_ptr;
+  std::vector<BwdCall> calls((size_t)V);
+  for (int v = 0; v < V; v++) {
+    const gsr_view& w = views[v];
+    if (int rc = bwd_setup(calls[(size_t)v], P, M, w.num_rendered, background, means3D, w.radii,
+                           nullptr, scaling_raw, rotation_raw, scale_modifier, nullptr,
+                           w.viewmatrix, w.projmatrix, w.tan_fovx, w.tan_fovy, image_height,
+                           image_width, w.dL_dout_color, w.dL_dout_depth, w.dL_dout_alpha,
+                           w.dL_dout_feature, nullptr, degree, w.campos, language_feature,
+                           nullptr, confidence, include_feature, w.geom_buffer,
+                           w.binning_buffer, w.image_buffer, w.dL_dmeans2D, nullptr,
+                           dL_dopacity_raw, dL_dmeans3D, nullptr, dL_dfeatures_dc,
+                           dL_dscaling_raw, dL_drotation_raw, dL_dlanguage_feature, nullptr,
+                           debug, 1, features_dc, features_rest, opacity_raw, dL_dfeatures_rest,
+                           (v > 0 || accumulate) ? 1 : 0, w.dL_dcolor_sh, w.pre_jac))
+      return rc;
+  }
+  if (V == 0) return GSR_OK;
+  // The backward blends of all views run on views[0].stream, merged into launches of up to
+  // kMaxBwdViews views (`chunks` launches; one launch's tiles are its views' tiles, so no per-view
+  // tail of idle CUs); the per-Gaussian parts read-modify-write the leaves' gradients and run in
+  // view order on the call's stream, each after the launch holding its view.
+  hipStream_t bs = views[0].stream ? (hipStream_t)views[0].stream : call_stream;
+  hipEvent_t start = join_event(kFwdSlots);  // the upstream gradients were produced on the call's stream
+  if (!start || hipEventRecord(start, call_stream) != hipSuccess)
+    return fail(GSR_ERR_HIP, "event record on the call's stream failed");
+  if (bs != call_stream && hipStreamWaitEvent(bs, start, 0) != hipSuccess)
+    return fail(GSR_ERR_HIP, "stream wait failed");
+  static const int chunks_env = [] {
+    const char* e = getenv("GSR_VIEWS_BWD_CHUNKS");
+    return e ? atoi(e) : 1;
+  }();
+  int per = (V + (chunks_env > 0 ? chunks_env : 1) - 1) / (chunks_env > 0 ? chunks_env : 1);
+  if (per > kMaxBwdViews) per = kMaxBwdViews;
+  const int debug_sync = debug & 1;
+  for (int v0 = 0; v0 < V; v0 += per) {
+    const int n = V - v0 < per ? V - v0 : per;
+    RenderBwdArgs rbs[kMaxBwdViews];
+    int nb = 0;
+    for (int k = 0; k < n; k++) {
+      BwdCall& c = calls[(size_t)(v0 + k)];
+      if (c.done) continue;
+      if (c.acc_zero) {
+        BwdCall z = c;
+        z.blend = false;  // the accumulator memset only
+        if (int rc = bwd_blend(z, bs)) return rc;
+      }
+      if (c.blend) rbs[nb++] = c.rb;
+    }
+    if (nb > 0) {
+      const int debug = debug_sync;
+      hipStream_t stream = bs;
+      PROF_BEGIN(RENDER_BWD);
+      GSR_CHECK(launch_render_backward_views(rbs, nb, bs));
+      PROF_END(RENDER_BWD);
+    }
+    hipEvent_t e = join_event(v0);
+    if (bs != call_stream) {
+      if (!e || hipEventRecord(e, bs) != hipSuccess ||
+          hipStreamWaitEvent(call_stream, e, 0) != hipSuccess)
+        return fail(GSR_ERR_HIP, "joining the blend stream failed");
+    }
+    for (int k = 0; k < n; k++)
+      if (int rc = bwd_pre(calls[(size_t)(v0 + k)], call_stream)) return rc;
+  }
+  return GSR_OK;
 }
 
 int gsr_sh_precolor(int P, int M, int degree, const float* means3D, const float* features_dc,
@@ -946,7 +1328,7 @@ static int test_radix_sort(uint32_t* keys, uint32_t* vals, size_t n, int bits, v
   sort_scratch_layout((char*)scratch, n, &kb, &vb, &sc);
   bool in_b = false;
   GSR_CHECK(radix_sort_pairs(keys, vals, kb, vb, n, bits, sc, &in_b, stream, sentinel_anywhere));
-  uint32_t* host = pinned_slot();
+  uint32_t* host = pinned_slot(0);
   if (!host) return fail(GSR_ERR_HIP, "pinned host allocation failed");
   GSR_CHECK(hipMemcpyAsync(host + 2, sc.aux + kSortAuxErr, 4, hipMemcpyDeviceToHost, stream));
   GSR_CHECK(hipStreamSynchronize(stream));

@@ -333,6 +333,16 @@ struct RenderArgs {
   uint32_t* fault;        // forward_faults_word() (may be null): kStatusClamp or-ed on a clamp
 };
 hipError_t launch_render_forward(const RenderArgs& a, hipStream_t s);
+// the two halves of launch_render_forward for multi-view calls: the heaviest-first tile schedule
+// of one view, and the blends of several views in one launch
+constexpr int kMaxFwdViews = 8;
+struct RenderFwdViews {
+  RenderArgs v[kMaxFwdViews];
+  uint32_t first[kMaxFwdViews + 1];  // first workgroup of view k; first[V] = total
+  int V;
+};
+hipError_t launch_render_schedule(const RenderArgs& a, hipStream_t s);
+hipError_t launch_render_forward_views(const RenderArgs* views, int V, hipStream_t s);
 
 struct RenderBwdArgs {
   int W, H;
@@ -361,6 +371,15 @@ struct RenderBwdArgs {
   const uint32_t* status;  // ImgState::status: a failed forward's backward blend writes nothing
 };
 hipError_t launch_render_backward(const RenderBwdArgs& a, hipStream_t s);
+// several views' backward blends in one launch (all views must share the template switches:
+// upstream depth/alpha present, feature, rows layout, deterministic)
+constexpr int kMaxBwdViews = 8;
+struct RenderBwdViews {
+  RenderBwdArgs v[kMaxBwdViews];
+  uint32_t first[kMaxBwdViews + 1];  // first workgroup of view k; first[V] = total
+  int V;
+};
+hipError_t launch_render_backward_views(const RenderBwdArgs* views, int V, hipStream_t s);
 // rows layout forward: point_list[q] = egid[einst[q]]
 hipError_t launch_det_gather(size_t R, const uint32_t* einst, const uint32_t* egid,
                              uint32_t* point_list, hipStream_t s);

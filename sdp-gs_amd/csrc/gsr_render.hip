@@ -457,8 +457,10 @@ constexpr int kAccDet = 13;
 // partial[emission index] -- one coalesced 64-B row per instance, no global float atomics (they
 // execute at the memory side at ~1.3 TB/s chip-wide, MI355X_MICROARCH.md "Global float atomics")
 // -- and the backward preprocess sums each Gaussian's rows.  DET implies ROWS.
+// One tile of the backward blend: workgroup `blk` of the view described by `a` (render_bwd_kernel:
+// one view per launch; render_bwd_views_kernel: the tiles of several views in one launch).
 template <bool EXTRA, bool FEAT, int GROUP, bool DET, bool ROWS>
-__global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
+__device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t blk) {
   static_assert(!DET || ROWS, "the deterministic backward stores per-instance rows");
   // the batch's records in LDS, regrouped so that the colour dot product's packed FMAs read
   // register pairs straight from the loads: s_r0 = {x, y, conic.a, conic.b}, s_r1 = {conic.c,
@@ -485,7 +487,7 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
   const int red_slot = reduce16_slot(lane, swap_orient);
   const bool red_lane = (lane & 3) == 0 && red_slot < kAccDet;
   const uint32_t ntiles = a.gx * a.gy;
-  const uint32_t tile = sched_tile(blockIdx.x, ntiles, a.sched, a.order);
+  const uint32_t tile = sched_tile(blk, ntiles, a.sched, a.order);
   const uint32_t tx = tile % a.gx, ty = tile / a.gx;
   uint32_t px, py;
   pixel_of(tx, ty, threadIdx.x, px, py);
@@ -836,6 +838,23 @@ __global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
   }
 }
 
+template <bool EXTRA, bool FEAT, int GROUP, bool DET, bool ROWS>
+__global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
+  render_bwd_tile<EXTRA, FEAT, GROUP, DET, ROWS>(a, blockIdx.x);
+}
+
+// The backward blends of several views of a step in ONE launch: workgroup b belongs to the view k
+// with first[k] <= b < first[k + 1] (view-major; inside a view the forward's heaviest-first tile
+// order), so the views' launches do not each end in a tail of idle CUs, and one launch's duration
+// is the time of all its views' blends.
+template <bool EXTRA, bool FEAT, int GROUP, bool DET, bool ROWS>
+__global__ __launch_bounds__(kThreads) void render_bwd_views_kernel(RenderBwdViews m) {
+  const uint32_t b = blockIdx.x;
+  int k = 0;
+  while (k + 1 < m.V && b >= m.first[k + 1]) k++;  // workgroup-uniform
+  render_bwd_tile<EXTRA, FEAT, GROUP, DET, ROWS>(m.v[k], b - m.first[k]);
+}
+
 // ================================================================================================
 // Forward with block lists: each wave's 64 lanes are four 16-lane groups, group g = lane bits
 // (1, 2) owning a 4x4 pixel block of the wave's 8x8 quadrant, and every group walks its OWN
@@ -929,7 +948,7 @@ __device__ __forceinline__ uint32_t build_group_lists(const uint16_t* s_mask, ui
 #define GSR_FWD_BLK_WAVES 1
 #endif
 template <bool FEAT>
-__global__ __launch_bounds__(kThreads, GSR_FWD_BLK_WAVES) void render_fwd_blk_kernel(RenderArgs a) {
+__device__ __forceinline__ void render_fwd_blk_tile(const RenderArgs& a, uint32_t blk) {
   __shared__ float4 s_r0[kThreads];
   __shared__ float4 s_r1[kThreads];
   __shared__ float4 s_r2[kThreads];
@@ -942,7 +961,7 @@ __global__ __launch_bounds__(kThreads, GSR_FWD_BLK_WAVES) void render_fwd_blk_ke
   const uint32_t grp = ((uint32_t)lane >> 1) & 3u;
 
   const uint32_t ntiles = a.gx * a.gy;
-  const uint32_t tile = sched_tile(blockIdx.x, ntiles, a.sched, a.order);
+  const uint32_t tile = sched_tile(blk, ntiles, a.sched, a.order);
   const uint32_t tx = tile % a.gx, ty = tile / a.gx;
   uint32_t px, py;
   pixel_of_blk(tx, ty, threadIdx.x, px, py);
@@ -1094,6 +1113,22 @@ __global__ __launch_bounds__(kThreads, GSR_FWD_BLK_WAVES) void render_fwd_blk_ke
   }
 }
 
+template <bool FEAT>
+__global__ __launch_bounds__(kThreads, GSR_FWD_BLK_WAVES) void render_fwd_blk_kernel(RenderArgs a) {
+  render_fwd_blk_tile<FEAT>(a, blockIdx.x);
+}
+
+// The forward blends of several views in ONE launch (view-major workgroups, as
+// render_bwd_views_kernel): no per-view tail of idle CUs.
+template <bool FEAT>
+__global__ __launch_bounds__(kThreads, GSR_FWD_BLK_WAVES) void render_fwd_blk_views_kernel(
+    RenderFwdViews m) {
+  const uint32_t b = blockIdx.x;
+  int k = 0;
+  while (k + 1 < m.V && b >= m.first[k + 1]) k++;  // workgroup-uniform
+  render_fwd_blk_tile<FEAT>(m.v[k], b - m.first[k]);
+}
+
 __global__ void expf_pair_kernel(const float* __restrict__ x, float* __restrict__ ref,
                                  float* __restrict__ fast, size_t n) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1156,6 +1191,45 @@ static bool block_lists() {
   return on;
 }
 
+hipError_t launch_render_schedule(const RenderArgs& a, hipStream_t s) {
+  const uint32_t ntiles = a.gx * a.gy;
+  if (ntiles == 0 || a.sched != 2) return hipSuccess;
+  hipLaunchKernelGGL(tile_schedule_kernel, dim3(1), dim3(kSchedThreads), 0, s, a.ranges,
+                     (const uint32_t*)nullptr, ntiles, a.order);
+  return hipGetLastError();
+}
+
+hipError_t launch_render_forward_views(const RenderArgs* views, int V, hipStream_t s) {
+  if (V <= 0) return hipSuccess;
+  if (V > kMaxFwdViews) return hipErrorInvalidValue;
+  if (!block_lists()) {  // the quadrant-list kernel: one launch per view
+    for (int k = 0; k < V; k++) {
+      const RenderArgs& a = views[k];
+      if (a.gx * a.gy == 0) continue;
+      if (a.include_feature)
+        hipLaunchKernelGGL(render_fwd_kernel<true>, dim3(a.gx * a.gy), dim3(kThreads), 0, s, a);
+      else
+        hipLaunchKernelGGL(render_fwd_kernel<false>, dim3(a.gx * a.gy), dim3(kThreads), 0, s, a);
+    }
+    return hipGetLastError();
+  }
+  RenderFwdViews m{};
+  m.V = V;
+  m.first[0] = 0;
+  const bool feat = views[0].include_feature != 0;
+  for (int k = 0; k < V; k++) {
+    if ((views[k].include_feature != 0) != feat) return hipErrorInvalidValue;
+    m.v[k] = views[k];
+    m.first[k + 1] = m.first[k] + views[k].gx * views[k].gy;
+  }
+  if (m.first[V] == 0) return hipSuccess;
+  if (feat)
+    hipLaunchKernelGGL(render_fwd_blk_views_kernel<true>, dim3(m.first[V]), dim3(kThreads), 0, s, m);
+  else
+    hipLaunchKernelGGL(render_fwd_blk_views_kernel<false>, dim3(m.first[V]), dim3(kThreads), 0, s, m);
+  return hipGetLastError();
+}
+
 hipError_t launch_render_forward(const RenderArgs& a, hipStream_t s) {
   const uint32_t ntiles = a.gx * a.gy;
   if (ntiles == 0) return hipSuccess;
@@ -1171,6 +1245,44 @@ hipError_t launch_render_forward(const RenderArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(render_fwd_kernel<true>, dim3(ntiles), dim3(kThreads), 0, s, a);
   else
     hipLaunchKernelGGL(render_fwd_kernel<false>, dim3(ntiles), dim3(kThreads), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_render_backward_views(const RenderBwdArgs* views, int V, hipStream_t s) {
+  if (V <= 0) return hipSuccess;
+  if (V > kMaxBwdViews) return hipErrorInvalidValue;
+  const RenderBwdArgs& a = views[0];
+  const bool extra = a.dL_ddepth != nullptr || a.dL_dalpha != nullptr;
+  const bool feat = a.include_feature && a.dL_dfeature != nullptr;
+  RenderBwdViews m{};
+  m.V = V;
+  m.first[0] = 0;
+  for (int k = 0; k < V; k++) {
+    const RenderBwdArgs& w = views[k];
+    // one kernel instance for all: the views must agree on the template switches
+    if ((w.dL_ddepth != nullptr || w.dL_dalpha != nullptr) != extra ||
+        (w.include_feature && w.dL_dfeature != nullptr) != feat ||
+        (w.partial != nullptr) != (a.partial != nullptr) || w.det != a.det ||
+        (a.sched == 2) != (w.sched == 2))
+      return hipErrorInvalidValue;
+    m.v[k] = w;
+    m.first[k + 1] = m.first[k] + w.gx * w.gy;
+  }
+  const uint32_t nblk = m.first[V];
+  if (nblk == 0) return hipSuccess;
+#define GSR_BWDV(E, F)                                                                            \
+  do {                                                                                           \
+    if (a.partial && a.det)                                                                      \
+      hipLaunchKernelGGL((render_bwd_views_kernel<E, F, 4, true, true>), dim3(nblk), dim3(kThreads), 0, s, m); \
+    else if (a.partial)                                                                          \
+      hipLaunchKernelGGL((render_bwd_views_kernel<E, F, 4, false, true>), dim3(nblk), dim3(kThreads), 0, s, m); \
+    else                                                                                         \
+      hipLaunchKernelGGL((render_bwd_views_kernel<E, F, 4, false, false>), dim3(nblk), dim3(kThreads), 0, s, m); \
+  } while (0)
+  if (feat) GSR_BWDV(true, true);
+  else if (extra) GSR_BWDV(true, false);
+  else GSR_BWDV(false, false);
+#undef GSR_BWDV
   return hipGetLastError();
 }
 

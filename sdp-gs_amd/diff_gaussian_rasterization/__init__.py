@@ -441,6 +441,242 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
         return d_means3D, d_means2D, d_dc, d_rest, d_op, d_sc, d_rot, d_lf, None
 
 
+def rasterize_views_fused(means3D, means2D, features_dc, features_rest, opacity_raw, scaling_raw,
+                          rotation_raw, language_feature, raster_settings_list, streams=None):
+    """Several views of the same Gaussians in one host call (include/gsr.h
+    gsr_rasterize_views_fused / _backward): per view exactly rasterize_gaussians_fused's outputs,
+    stacked along a leading view axis -- color [V,3,H,W], depth [V,1,H,W], alpha [V,1,H,W],
+    feature [V,3,H,W], radii [V,P] -- with means2D a [V,P,3] tensor whose gradient is every
+    view's screen-space gradient.  One forward and one backward call issue all views' kernels, so
+    per view the host costs a few launches instead of a Python render() + autograd node, and the
+    first phases of the next views (preprocess, depth sort, read-back) are queued before a view's
+    binning waits for its read-back.  streams: HIP streams the views are spread over (view v on
+    streams[v % len]); default the current stream.  Every view must share the image size and the
+    non-camera settings (background, scale modifier, SH degree, feature/confidence flags)."""
+    return _RasterizeViewsFused.apply(means3D, means2D, features_dc, features_rest, opacity_raw,
+                                      scaling_raw, rotation_raw, language_feature,
+                                      tuple(raster_settings_list), tuple(streams or ()))
+
+
+class _RasterizeViewsFused(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, means3D, means2D, features_dc, features_rest, opacity_raw, scaling_raw,
+                rotation_raw, language_feature, settings, streams):
+        V = len(settings)
+        if V == 0:
+            raise RuntimeError("rasterize_views_fused needs at least one view")
+        rs0 = settings[0]
+        if means3D.ndim != 2 or means3D.shape[1] != 3:
+            raise RuntimeError("means3D must have dimensions (num_points, 3)")
+        dev = means3D.device
+        P = int(means3D.shape[0])
+        H, W = int(rs0.image_height), int(rs0.image_width)
+        include_feature = bool(getattr(rs0, "include_feature", False))
+        for rs in settings[1:]:
+            if ((int(rs.image_height), int(rs.image_width)) != (H, W)
+                    or bool(getattr(rs, "include_feature", False)) != include_feature
+                    or rs.bg is not rs0.bg or float(rs.scale_modifier) != float(rs0.scale_modifier)
+                    or int(rs.sh_degree) != int(rs0.sh_degree)
+                    or bool(rs.prefiltered) != bool(rs0.prefiltered)
+                    or getattr(rs, "confidence", None) is not getattr(rs0, "confidence", None)
+                    or bool(rs.debug) != bool(rs0.debug)):
+                raise RuntimeError("rasterize_views_fused: views must share the image size and "
+                                   "the non-camera settings")
+        m3 = _dev_f32(means3D, "means3D", dev)
+        dc = _dev_f32(features_dc, "features_dc", dev)
+        rest = _dev_f32(_opt(features_rest), "features_rest", dev)
+        op = _dev_f32(opacity_raw, "opacity", dev)
+        sc = _dev_f32(scaling_raw, "scaling", dev)
+        rot = _dev_f32(rotation_raw, "rotation", dev)
+        lf = _dev_f32(_opt(language_feature), "language_feature", dev) if include_feature else None
+        conf = _dev_f32(_opt(getattr(rs0, "confidence", None)), "confidence", dev)
+        bg = _dev_f32(rs0.bg, "bg", dev)
+        if dc.numel() != 3 * P or (rest is not None and rest.numel() % (3 * max(P, 1))):
+            raise RuntimeError("features_dc must be [P,1,3] and features_rest [P,K,3]")
+        M = 1 + (rest.numel() // (3 * P) if rest is not None and P else 0)
+        degree = int(rs0.sh_degree)
+
+        fopts = dict(dtype=torch.float32, device=dev)
+        color = torch.empty((V, 3, H, W), **fopts)
+        depth = torch.empty((V, 1, H, W), **fopts)
+        alpha = torch.empty((V, 1, H, W), **fopts)
+        feature = torch.empty((V, 3, H, W), **fopts)
+        radii = torch.empty((V, P), dtype=torch.int32, device=dev)
+        views = (_lib.GsrView * V)()
+        holders = [_lib.BufferHolder(dev) for _ in range(V)]
+        # the views' preprocess / sorts / binning on the side streams (streams[1:]), their merged
+        # blends on the call's stream (include/gsr.h); with one stream everything runs there
+        vstreams = tuple(streams[1:]) if len(streams) > 1 else ()
+        cams, pres = [], []
+        n_img, n_rad = 4 * H * W, 4 * P
+        for v, rs in enumerate(settings):
+            view = _dev_f32(rs.viewmatrix, "viewmatrix", dev)
+            proj = _dev_f32(rs.projmatrix, "projmatrix", dev)
+            campos = _dev_f32(rs.campos, "campos", dev)
+            cams.append((view, proj, campos, float(rs.tanfovx), float(rs.tanfovy)))
+            pre = _precolor_lookup(dev, campos, m3, dc, rest, degree, M)
+            pres.append(pre)
+            w = views[v]
+            w.viewmatrix, w.projmatrix, w.campos = _ptr(view), _ptr(proj), _ptr(campos)
+            w.tan_fovx, w.tan_fovy = float(rs.tanfovx), float(rs.tanfovy)
+            if pre is not None:
+                w.pre_color, w.pre_clamp = _ptr(pre[0]), _ptr(pre[1])
+            w.out_color = color.data_ptr() + v * 3 * n_img
+            w.out_depth = depth.data_ptr() + v * n_img
+            w.out_alpha = alpha.data_ptr() + v * n_img
+            w.out_feature = feature.data_ptr() + v * 3 * n_img
+            w.radii = radii.data_ptr() + v * n_rad
+            w.alloc_ctx = holders[v].key
+            if vstreams:
+                w.stream = vstreams[v % len(vstreams)].cuda_stream
+        L = _lib.load()
+        cur = torch.cuda.current_stream(dev)
+        flags = _debug_flags(rs0.debug)
+        try:
+            with _lib.on_device(dev):
+                rc = L.gsr_rasterize_views_fused(
+                    V, views, H, W, P, M, _ptr(bg), _ptr(m3), _ptr(dc), _ptr(rest), _ptr(op),
+                    _ptr(sc), _ptr(rot), float(rs0.scale_modifier), degree,
+                    int(bool(rs0.prefiltered)), _ptr(lf), _ptr(conf), int(include_feature),
+                    _lib.alloc_callback(), max(1, len(vstreams)), cur.cuda_stream, flags)
+            _lib.check(rc)
+        finally:
+            for h in holders:
+                h.release()
+        LAST_STATS["num_rendered"] = int(views[V - 1].num_rendered)
+        LAST_STATS["num_instances"] = int(views[V - 1].num_instances)
+        LAST_STATS["P"] = P
+        ctx.view_counts = [(int(views[v].num_rendered), int(views[v].num_instances))
+                           for v in range(V)]
+        LAST_STATS["view_counts"] = list(ctx.view_counts)  # (num_rendered, num_instances) per view
+        ctx.views = views
+        ctx.streams = streams
+        ctx.gsr_flags = flags
+        ctx.cams = cams
+        ctx.pre_jacs = [None if p is None else p[2] for p in pres]
+        leaves = (means3D, features_dc, features_rest, opacity_raw, scaling_raw, rotation_raw,
+                  language_feature)
+        used = (m3, dc, rest, op, sc, rot, lf)
+        ctx.leaves = None
+        if grad_into_leaves() and all(
+                t is None or (t.is_leaf and t.requires_grad and u is not None
+                              and u.data_ptr() == t.data_ptr())
+                for t, u in zip(leaves, used)):
+            ctx.leaves = leaves
+        ctx.meta = dict(V=V, P=P, M=M, H=H, W=W, degree=degree, include_feature=include_feature,
+                        scale_modifier=float(rs0.scale_modifier),
+                        shapes=(tuple(features_dc.shape),
+                                None if rest is None else tuple(features_rest.shape),
+                                tuple(opacity_raw.shape), tuple(scaling_raw.shape),
+                                tuple(rotation_raw.shape)))
+        ctx.params = (m3, dc, rest, op, sc, rot, lf, conf, bg)
+        ctx.buffers = [h.bufs for h in holders]  # the views' scratch, alive until the backward
+        ctx.radii = radii
+        ctx.mark_non_differentiable(radii)
+        ctx.set_materialize_grads(False)
+        return color, depth, alpha, feature, radii
+
+    @staticmethod
+    def backward(ctx, grad_color, grad_depth, grad_alpha, grad_feature, _grad_radii):
+        mt = ctx.meta
+        V, P, M, H, W = mt["V"], mt["P"], mt["M"], mt["H"], mt["W"]
+        m3, dc, rest, op, sc, rot, lf, conf, bg = ctx.params
+        dev = m3.device
+        fopts = dict(dtype=torch.float32, device=dev)
+
+        def per_view(t, v, shape):
+            if t is None:
+                return None
+            x = t[v]
+            if x.dtype != torch.float32:
+                x = x.float()
+            return x if x.is_contiguous() else x.contiguous()
+
+        keep = []  # per-view upstream-gradient tensors that must outlive the call
+        zero_col = None
+        views = ctx.views
+        # the backward blends of all views run merged into one launch on views[0].stream
+        # (include/gsr.h), beside the per-Gaussian backwards on the call's stream: a side stream
+        views[0].stream = ctx.streams[1 % len(ctx.streams)].cuda_stream if ctx.streams else None
+        into_leaves = ctx.leaves is not None
+        defer = _SH_DEFER.get(dev.index) if into_leaves else None
+        d_means2D = torch.empty((V, P, 3), **fopts)
+        d_rgb = torch.empty((V, 3, P), **fopts) if defer is not None else None
+        for v in range(V):
+            w = views[v]
+            gc = per_view(grad_color, v, (3, H, W))
+            if gc is None:
+                if zero_col is None:
+                    zero_col = torch.zeros((3, H, W), **fopts)
+                gc = zero_col
+            gd = per_view(grad_depth, v, (1, H, W))
+            ga = per_view(grad_alpha, v, (1, H, W))
+            gf = per_view(grad_feature, v, (3, H, W)) if mt["include_feature"] else None
+            keep += [gc, gd, ga, gf]
+            w.dL_dout_color, w.dL_dout_depth = _ptr(gc), _ptr(gd)
+            w.dL_dout_alpha, w.dL_dout_feature = _ptr(ga), _ptr(gf)
+            w.dL_dmeans2D = d_means2D.data_ptr() + v * 12 * P
+            if d_rgb is not None:
+                w.dL_dcolor_sh = d_rgb.data_ptr() + v * 12 * P
+                w.pre_jac = _ptr(ctx.pre_jacs[v])
+            else:
+                w.dL_dcolor_sh = None
+                w.pre_jac = None
+        s_dc, s_rest, s_op, s_sc, s_rot = mt["shapes"]
+        accumulate = into_leaves
+        if into_leaves:
+            direct = ctx.leaves
+            if defer is not None:
+                direct = tuple(None if k in (1, 2) else t for k, t in enumerate(ctx.leaves))
+            if all(t is None or t.grad is None for t in direct):
+                accumulate = False  # first views after zero_grad(set_to_none=True): store mode
+                for t in direct:
+                    if t is not None:
+                        t.grad = torch.empty_like(t, memory_format=torch.contiguous_format)
+            grads = []
+            for t in direct:
+                if t is not None and t.grad is None:
+                    t.grad = torch.zeros_like(t, memory_format=torch.contiguous_format)
+                grads.append(None if t is None else t.grad)
+            if any(gr is not None and not gr.is_contiguous() for gr in grads):
+                raise RuntimeError("grad-into-leaves needs contiguous .grad tensors")
+            d_means3D, d_dc, d_rest, d_op, d_sc, d_rot, d_lf = grads
+            if defer is not None:
+                for v, (view, proj, campos, tx, ty) in enumerate(ctx.cams):
+                    defer.add(ctx.leaves, d_rgb[v], campos, m3, mt["degree"], M)
+        else:
+            d_means3D = torch.empty((P, 3), **fopts)
+            d_dc = torch.empty(s_dc, **fopts)
+            d_rest = torch.empty(s_rest, **fopts) if rest is not None else None
+            d_op = torch.empty(s_op, **fopts)
+            d_sc = torch.empty(s_sc, **fopts)
+            d_rot = torch.empty(s_rot, **fopts)
+            d_lf = torch.empty((P, 3), **fopts) if lf is not None else None
+        L = _lib.load()
+        cur = torch.cuda.current_stream(dev)
+        if into_leaves:
+            _order_leaf_grads(dev, cur)
+        with _lib.on_device(dev):
+            rc = L.gsr_rasterize_views_fused_backward(
+                V, views, H, W, P, M, _ptr(bg), _ptr(m3), _ptr(dc), _ptr(rest), _ptr(op),
+                _ptr(sc), _ptr(rot), mt["scale_modifier"], mt["degree"], _ptr(lf), _ptr(conf),
+                int(mt["include_feature"]), _ptr(d_means3D), _ptr(d_dc), _ptr(d_rest),
+                _ptr(d_op), _ptr(d_sc), _ptr(d_rot), _ptr(d_lf), int(accumulate),
+                cur.cuda_stream, ctx.gsr_flags)
+        _lib.check(rc)
+        if into_leaves:
+            prev = _LEAF_GRAD_EVENT.get(dev.index)
+            ev = prev[0] if prev is not None else torch.cuda.Event()
+            ev.record(cur)
+            _LEAF_GRAD_EVENT[dev.index] = (ev, cur.stream_id)
+        del keep  # read on the views' streams, which the call joined back into this stream
+        # inputs: means3D, means2D, features_dc, features_rest, opacity_raw, scaling_raw,
+        # rotation_raw, language_feature, settings, streams
+        if into_leaves:
+            return None, d_means2D, None, None, None, None, None, None, None, None
+        return d_means3D, d_means2D, d_dc, d_rest, d_op, d_sc, d_rot, d_lf, None, None
+
+
 _GRAD_INTO_LEAVES = None
 _DETERMINISTIC = None
 

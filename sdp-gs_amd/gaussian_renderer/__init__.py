@@ -17,7 +17,7 @@ if _PKG_ROOT not in sys.path:
     sys.path.insert(0, _PKG_ROOT)
 
 from diff_gaussian_rasterization import (GaussianRasterizationSettings, GaussianRasterizer,  # noqa: E402
-                                         rasterize_gaussians_fused)
+                                         rasterize_gaussians_fused, rasterize_views_fused)
 from gsr_amd.sh import eval_sh  # noqa: E402
 
 _RAW = ("_features_dc", "_features_rest", "_opacity", "_scaling", "_rotation")
@@ -94,17 +94,20 @@ class _RenderPkg(dict):
         return dict(dict.items(self._fill()))
 
 
-_ZEROS = {}  # device -> zero buffer of the last shape asked for (render()'s means2D leaves)
+_ZEROS = {}  # (device, views) -> zero buffer of the last shape asked for (means2D leaves)
 
 
-def _zero_leaf(xyz):
+def _zero_leaf(xyz, views=None):
     """A new leaf tensor (requires_grad, own .grad) whose values are zeros, like
-    torch.zeros_like(xyz, requires_grad=True), backed by a zero buffer shared by all views of the
-    same shape: the buffer is never written (the rasterizer only returns means2D's gradient)."""
-    z = _ZEROS.get(xyz.device)
-    if z is None or z.shape != xyz.shape or z.dtype != xyz.dtype:
-        z = torch.zeros_like(xyz, memory_format=torch.contiguous_format)
-        _ZEROS[xyz.device] = z
+    torch.zeros_like(xyz, requires_grad=True) -- shape [views, *xyz.shape] when views is given
+    (render_views) -- backed by a zero buffer shared by all calls of the same shape: the buffer is
+    never written (the rasterizer only returns means2D's gradient)."""
+    shape = tuple(xyz.shape) if views is None else (int(views),) + tuple(xyz.shape)
+    key = (xyz.device, views is not None)
+    z = _ZEROS.get(key)
+    if z is None or tuple(z.shape) != shape or z.dtype != xyz.dtype:
+        z = torch.zeros(shape, dtype=xyz.dtype, device=xyz.device)
+        _ZEROS[key] = z
     return z.detach().requires_grad_(True)
 
 
@@ -230,3 +233,67 @@ def render(viewpoint_camera, pc, pipe, bg_color: torch.Tensor, opt, scaling_modi
             "visibility_filter": radii > 0,
             "radii": radii,
             "color": colors_precomp}
+
+
+class ViewGrad:
+    """Per-view handle on the screen-space gradient of a multi-view call: `.grad` is view v's
+    [P,3] slice of the shared [V,P,3] leaf -- what the reference reads from
+    viewspace_point_tensor.grad (train.py:220, add_densification_stats)."""
+    __slots__ = ("leaf", "index")
+
+    def __init__(self, leaf, index):
+        self.leaf, self.index = leaf, index
+
+    @property
+    def grad(self):
+        g = self.leaf.grad
+        return None if g is None else g[self.index]
+
+
+def _settings(cam, pc, pipe, bg_color, scaling_modifier, confidence):
+    return GaussianRasterizationSettings(
+        image_height=int(cam.image_height), image_width=int(cam.image_width),
+        tanfovx=math.tan(cam.FoVx * 0.5), tanfovy=math.tan(cam.FoVy * 0.5), bg=bg_color,
+        scale_modifier=scaling_modifier, viewmatrix=cam.world_view_transform,
+        projmatrix=cam.full_proj_transform, sh_degree=pc.active_sh_degree,
+        campos=cam.camera_center, prefiltered=False, include_feature=True,
+        confidence=confidence, debug=pipe.debug)
+
+
+def render_views(viewpoint_cameras, pc, pipe, bg_color: torch.Tensor, opt, scaling_modifier=1.0,
+                 streams=None):
+    """render() for several cameras of one step: a list of render()'s dicts, one per camera,
+    with identical values.  Where render() would take the fused path and the cameras share an
+    image size, every view's forward is issued by ONE host call (and, through autograd, every
+    backward by one call): diff_gaussian_rasterization.rasterize_views_fused, views spread over
+    `streams`.  The dicts' images are views into [V,...] tensors; "viewspace_points" is a
+    ViewGrad whose .grad is that view's screen-space gradient.  Otherwise (unfused
+    configurations, mixed image sizes) this is render() per camera."""
+    cams = list(viewpoint_cameras)
+    if not cams:
+        return []
+    same = len({(int(c.image_height), int(c.image_width)) for c in cams}) == 1
+    if not (same and _fused_eligible(pc, pipe, opt, None, None)):
+        return [render(c, pc, pipe, bg_color, opt, scaling_modifier) for c in cams]
+    xyz = pc.get_xyz
+    V = len(cams)
+    means2D = _zero_leaf(xyz, V)
+    confidence = pc.confidence if pipe.use_confidence else None
+    settings = [_settings(c, pc, pipe, bg_color, scaling_modifier, confidence) for c in cams]
+    lang = pc._language_feature if opt.include_feature else None
+    color, depth, alpha, feature, radii = rasterize_views_fused(
+        xyz, means2D, pc._features_dc, pc._features_rest, pc._opacity, pc._scaling, pc._rotation,
+        lang, settings, streams)
+    # the stacked [V,...] outputs: a caller seeding the backward of every view at once uses
+    # these (autograd on the per-view slices would materialise a [V,...] zero gradient per view)
+    stacked = {"render": color, "depth": depth, "alpha": alpha, "feature": feature,
+               "viewspace_points": means2D, "radii": radii}
+    out = []
+    for v in range(V):
+        r = radii[v]
+        out.append(_RenderPkg({"render": color[v], "depth": depth[v], "alpha": alpha[v],
+                               "feature": feature[v], "viewspace_points": ViewGrad(means2D, v),
+                               "radii": r, "color": None, "views": stacked, "view_index": v},
+                              {"opacity": lambda: pc.get_opacity,
+                               "visibility_filter": (lambda r=r: r > 0)}))
+    return out

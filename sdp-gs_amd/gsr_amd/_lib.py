@@ -83,6 +83,22 @@ class on_stream:
         return False
 
 
+class GsrView(ctypes.Structure):
+    """include/gsr.h gsr_view: one camera of a multi-view call (field order and types as in C)."""
+    _fields_ = [("viewmatrix", _p), ("projmatrix", _p), ("campos", _p),
+                ("tan_fovx", _f), ("tan_fovy", _f),
+                ("pre_color", _p), ("pre_clamp", _p),
+                ("out_color", _p), ("out_depth", _p), ("out_alpha", _p), ("out_feature", _p),
+                ("radii", _p),
+                ("alloc_ctx", _p), ("geom_buffer", _p), ("binning_buffer", _p),
+                ("image_buffer", _p),
+                ("num_rendered", _i), ("num_instances", _i),
+                ("stream", _p),
+                ("dL_dout_color", _p), ("dL_dout_depth", _p), ("dL_dout_alpha", _p),
+                ("dL_dout_feature", _p),
+                ("dL_dmeans2D", _p), ("dL_dcolor_sh", _p), ("pre_jac", _p)]
+
+
 class GsrError(RuntimeError):
     pass
 
@@ -162,6 +178,24 @@ def load():
         L.gsr_rasterize_gaussians_fused_backward_deferred.restype = _i
         L.gsr_rasterize_gaussians_fused_backward_deferred.argtypes = (
             L.gsr_rasterize_gaussians_fused_backward.argtypes[:-3] + [_p, _p, _i, _p, _i])
+        _pv = ctypes.POINTER(GsrView)
+        L.gsr_rasterize_views_fused.restype = _i
+        L.gsr_rasterize_views_fused.argtypes = [
+            _i, _pv, _i, _i,             # V, views, H, W
+            _i, _i, _p, _p,              # P, M, bg, means3D
+            _p, _p, _p,                  # features_dc, features_rest, opacity_raw
+            _p, _p, _f,                  # scaling_raw, rotation_raw, scale_modifier
+            _i, _i, _p, _p, _i,          # degree, prefiltered, language_feature, confidence, incl
+            ALLOC_FN, _i, _p, _i]        # alloc, inflight, stream, debug
+        L.gsr_rasterize_views_fused_backward.restype = _i
+        L.gsr_rasterize_views_fused_backward.argtypes = [
+            _i, _pv, _i, _i,             # V, views, H, W
+            _i, _i, _p, _p,              # P, M, bg, means3D
+            _p, _p, _p,                  # features_dc, features_rest, opacity_raw
+            _p, _p, _f,                  # scaling_raw, rotation_raw, scale_modifier
+            _i, _p, _p, _i,              # degree, language_feature, confidence, include_feature
+            _p, _p, _p, _p, _p, _p, _p,  # grads: means3D, dc, rest, op, scale, rot, lang
+            _i, _p, _i]                  # accumulate, stream, debug
         L.gsr_sh_precolor.restype = _i
         L.gsr_sh_precolor.argtypes = [_i, _i, _i, _p, _p, _p, _i, ctypes.POINTER(_p),
                                       ctypes.POINTER(_p), ctypes.POINTER(_p), ctypes.POINTER(_p), _p]

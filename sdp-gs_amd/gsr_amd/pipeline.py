@@ -72,15 +72,59 @@ class ViewPipeline:
         its backward (same stream); view i's backward is issued after view i + lag's forward
         (software-pipelined issue: the next view's latency-bound binning is queued before this
         view's full-chip backward blend).  Returns bwd's results."""
-        import diff_gaussian_rasterization as dgr
+        self._check(reducer, model)
+        items = list(items)
+        main = torch.cuda.current_stream(self.device)
+        streams = [main] + self.side
+
+        def issue(out):
+            for i, it in enumerate(items):
+                s = streams[i % self.depth]
+                with _lib.on_stream(s):
+                    out.append(fn(it))
+                j = i - lag
+                if bwd is not None and j >= 0:
+                    with _lib.on_stream(streams[j % self.depth]):
+                        out[j] = bwd(out[j])
+            if bwd is not None:
+                for j in range(max(0, len(items) - lag), len(items)):
+                    with _lib.on_stream(streams[j % self.depth]):
+                        out[j] = bwd(out[j])
+            for s in self.side:
+                main.wait_stream(s)
+            return out
+
+        return self._step(items, issue, model, campos_of, reducer)
+
+    def run_views(self, items: Iterable[T], fn: Callable[[List[T], List[torch.cuda.Stream]], R],
+                  model=None, campos_of: Callable[[T], torch.Tensor] = lambda cam: cam.camera_center,
+                  reducer=None) -> R:
+        """The step's views in ONE multi-view call: fn(items, streams) renders all of them at once
+        (gaussian_renderer.render_views(items, ..., streams=streams): one host call issues every
+        view's forward, autograd one call for every backward) and runs their backward; the views
+        are spread over this pipeline's streams inside the library, which joins them back into the
+        current stream.  Pre-pass, deferred SH gradients and the overlapped all-reduce as run().
+        Returns fn's result."""
+        self._check(reducer, model)
+        items = list(items)
+        streams = [torch.cuda.current_stream(self.device)] + self.side
+
+        def issue(out):
+            out.append(fn(items, streams))
+            return out
+
+        return self._step(items, issue, model, campos_of, reducer)[0]
+
+    def _check(self, reducer, model):
         if reducer is not None and self.defer_sh and model is None:
             # the early all-reduce must leave out the SH leaves, whose deferred gradients are only
             # written by the flush at the end of the step; without the model they are unknown
             raise ValueError("ViewPipeline.run: a reducer with defer_sh needs model= (the SH "
                              "leaves are reduced after the deferred flush)")
-        items = list(items)
+
+    def _step(self, items, issue, model, campos_of, reducer):
+        import diff_gaussian_rasterization as dgr
         main = torch.cuda.current_stream(self.device)
-        streams = [main] + self.side
         pre = contextlib.nullcontext()
         if self.precolor and model is not None and items:
             pre = dgr.ShPrecolor(model._xyz, model._features_dc, model._features_rest,
@@ -107,20 +151,7 @@ class ViewPipeline:
         defer = (dgr.ShGradDeferral(self.device, on_rows=on_rows, chunk_rows=chunk)
                  if self.defer_sh else contextlib.nullcontext())
         with pre, defer:  # defer's exit: the SH gradients of all views, after the join
-            for i, it in enumerate(items):
-                s = streams[i % self.depth]
-                with _lib.on_stream(s):
-                    out.append(fn(it))
-                j = i - lag
-                if bwd is not None and j >= 0:
-                    with _lib.on_stream(streams[j % self.depth]):
-                        out[j] = bwd(out[j])
-            if bwd is not None:
-                for j in range(max(0, len(items) - lag), len(items)):
-                    with _lib.on_stream(streams[j % self.depth]):
-                        out[j] = bwd(out[j])
-            for s in self.side:
-                main.wait_stream(s)
+            issue(out)
             if reducer is not None:  # every view's backward is done: the non-SH grads are final
                 ids = {id(t) for t in sh_leaves}
                 reducer.reduce_async([p for p in reducer.current_params() if id(p) not in ids])

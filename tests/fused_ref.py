@@ -59,13 +59,15 @@ def kernel_activations(m):
     return op, sc, rot
 
 
-def run_bench_path(m, cams, grads, streams=3, defer_sh=True, precolor=True, lag=1):
-    """bench.py's step on `cams`: per view render() + backward of the fixed upstream grads
-    (image, depth, feature), grad-into-leaves, ViewPipeline over `streams` HIP streams, view i's
-    backward issued after view i + lag's forward (bench.py --lag, default 1; 0 = together).  Returns
-    (per-view numpy dicts of the images, radii and screen-space gradient, leaf grads float64)."""
+def run_bench_path(m, cams, grads, streams=3, defer_sh=True, precolor=True, lag=1, multi=False):
+    """bench.py's step on `cams`: render + backward of the fixed upstream grads (image, depth,
+    feature), grad-into-leaves, views over `streams` HIP streams.  multi: every view in one
+    multi-view call (gaussian_renderer.render_views, ViewPipeline.run_views -- bench.py's default
+    issue); else per view render() with view i's backward issued after view i + lag's forward
+    (bench.py --per-view --lag, default 1; 0 = together).  Returns (per-view numpy dicts of the
+    images, radii and screen-space gradient, leaf grads float64)."""
     import diff_gaussian_rasterization as dgr
-    from gaussian_renderer import render
+    from gaussian_renderer import render, render_views
     from gsr_amd.pipeline import ViewPipeline
     bg = torch.zeros(3, device=m._xyz.device)
     prev = dgr.grad_into_leaves()
@@ -84,7 +86,22 @@ def run_bench_path(m, cams, grads, streams=3, defer_sh=True, precolor=True, lag=
             out["means2D"] = pkg["viewspace_points"].grad.detach().clone()
             return out
 
-        if lag > 0:
+        def all_views(cs, strs):
+            pkgs = render_views(cs, m, Pipe(), bg, Opt(), streams=strs)
+            st = pkgs[0]["views"]
+            V = len(pkgs)
+            torch.autograd.backward([st["render"], st["depth"], st["feature"]],
+                                    [g.expand(V, *g.shape) for g in grads])
+            outs = []
+            for pkg in pkgs:
+                out = {k: pkg[k].detach().clone() for k in IMAGES + ("radii",)}
+                out["means2D"] = pkg["viewspace_points"].grad.detach().clone()
+                outs.append(out)
+            return outs
+
+        if multi:
+            outs = vp.run_views(cams, all_views, model=m)
+        elif lag > 0:
             outs = vp.run(cams, fwd, model=m, bwd=bwd, lag=lag)
         else:
             outs = vp.run(cams, lambda cam: bwd(fwd(cam)), model=m)

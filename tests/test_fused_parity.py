@@ -41,8 +41,16 @@ CASES = {
     "small_6views_3streams_lag0": dict(P=20_000, W=200, H=150, views=6, streams=3, seed=7,
                                        deg=3, lag=0),
     "cfg2_100k_800x800": dict(P=100_000, W=800, H=800, views=3, streams=3, seed=0, deg=3),
+    # bench.py's default issue: every view of the step in one multi-view call (render_views)
+    "small_6views_3streams_multi": dict(P=20_000, W=200, H=150, views=6, streams=3, seed=8,
+                                        deg=3, multi=True),
+    "small_deg1_1stream_multi": dict(P=20_000, W=200, H=150, views=3, streams=1, seed=9,
+                                     deg=1, multi=True),
+    "cfg3_1m_1008x756_multi": dict(P=1_000_000, W=1008, H=756, views=3, streams=3, seed=0,
+                                   deg=3, multi=True),
+    "cfg5_5m_1920x1080_multi": dict(P=5_000_000, W=1920, H=1080, views=2, streams=2, seed=0,
+                                    deg=3, multi=True),
     "cfg3_1m_1008x756": dict(P=1_000_000, W=1008, H=756, views=3, streams=3, seed=0, deg=3),
-    "cfg5_5m_1920x1080": dict(P=5_000_000, W=1920, H=1080, views=2, streams=2, seed=0, deg=3),
 }
 
 
@@ -79,7 +87,8 @@ def test_benchmarked_path_matches_oracle(case):
     cams = [x.to("cuda") for x in make_cameras(c["views"], c["W"], c["H"], seed=c["seed"])]
     grads = upstream_grads(c["H"], c["W"], seed=1, device="cuda")
     act = kernel_activations(m)
-    vg, gg = run_bench_path(m, cams, grads, streams=c["streams"], lag=c.get("lag", 1))
+    vg, gg = run_bench_path(m, cams, grads, streams=c["streams"], lag=c.get("lag", 1),
+                            multi=c.get("multi", False))
     _progress(f"[{case}] GPU path done")
     vo, go = run_oracle_path(m, cams, grads, act, progress=lambda s: _progress(f"[{case}] {s}"))
     st = compare(case, vg, vo, gg, go, STATS)
@@ -96,3 +105,26 @@ def test_benchmarked_path_matches_oracle(case):
         g = st["grads"][n]
         assert g["rel_max"] <= GRAD_REL, (case, n, g)
         assert g["rel_big_max"] <= ENTRY_REL, (case, n, g)
+
+
+@pytest.mark.parametrize("streams", [1, 3])
+def test_multi_view_call_equals_per_view_path(streams):
+    """The multi-view call (gsr_rasterize_views_fused / _backward) is the per-view path issued
+    differently: with the deterministic backward (no float atomics) every output and every
+    gradient is bitwise equal to the per-view render() pipeline's on the same views."""
+    import diff_gaussian_rasterization as dgr
+    m = SplatModel(make_gaussians(30_000, sh_degree=3, seed=11), device="cuda")
+    cams = [x.to("cuda") for x in make_cameras(5, 240, 180, seed=11)]
+    grads = upstream_grads(180, 240, seed=1, device="cuda")
+    prev = dgr.deterministic()
+    dgr.deterministic(True)
+    try:
+        va, ga = run_bench_path(m, cams, grads, streams=streams, multi=False)
+        vb, gb = run_bench_path(m, cams, grads, streams=streams, multi=True)
+    finally:
+        dgr.deterministic(prev)
+    for a, b in zip(va, vb):
+        for k in a:
+            assert (a[k] == b[k]).all(), k
+    for n in LEAVES:
+        assert (ga[n] == gb[n]).all(), n
