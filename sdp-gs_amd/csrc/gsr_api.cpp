@@ -1027,6 +1027,14 @@ int gsr_rasterize_gaussians_fused_backward_deferred(
 
 // ---- multi-view calls --------------------------------------------------------------------------
 namespace {
+// GSR_VIEWS_PRE_MERGED=0: one per-Gaussian backward launch per view in multi-view calls
+bool views_pre_merged() {
+  static const bool on = [] {
+    const char* e = getenv("GSR_VIEWS_PRE_MERGED");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
 // per host thread: events joining the views' streams with the call's stream
 hipEvent_t join_event(int i) {
   constexpr int kMaxDev = 64;
@@ -1215,8 +1223,30 @@ int gsr_rasterize_views_fused_backward(
           hipStreamWaitEvent(call_stream, e, 0) != hipSuccess)
         return fail(GSR_ERR_HIP, "joining the blend stream failed");
     }
+    // the chunk's per-Gaussian backwards: one launch for all of them where the configuration
+    // allows (launch_preprocess_backward_views), else one per view
+    BwdPreArgs bas[kMaxBwdViews];
+    int np = 0;
     for (int k = 0; k < n; k++)
-      if (int rc = bwd_pre(calls[(size_t)(v0 + k)], call_stream)) return rc;
+      if (!calls[(size_t)(v0 + k)].done) bas[np++] = calls[(size_t)(v0 + k)].ba;
+    hipError_t ve = hipErrorNotSupported;
+    if (np > 1 && views_pre_merged()) {
+      const int debug = debug_sync;
+      hipStream_t stream = call_stream;
+      PROF_BEGIN(PREPROCESS_BWD);
+      ve = launch_preprocess_backward_views(bas, np, call_stream);
+      if (ve != hipSuccess && ve != hipErrorNotSupported)
+        return fail(GSR_ERR_HIP, "launch_preprocess_backward_views: %s", hipGetErrorString(ve));
+      if (ve == hipSuccess) {
+        PROF_END(PREPROCESS_BWD);
+        if (debug) GSR_CHECK(hipStreamSynchronize(stream));
+      }
+    }
+    if (ve == hipErrorNotSupported) {
+      (void)hipGetLastError();
+      for (int k = 0; k < n; k++)
+        if (int rc = bwd_pre(calls[(size_t)(v0 + k)], call_stream)) return rc;
+    }
   }
   return GSR_OK;
 }

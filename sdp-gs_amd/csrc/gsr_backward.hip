@@ -140,11 +140,62 @@ __device__ __forceinline__ void grad_row(const BwdPreArgs& a, size_t i, float4& 
   }
 }
 
-// Backward of one visible Gaussian.  sh0 / sh1: its rows (coefficient 0 / coefficients 1..) of
-// the LDS staging planes: SH coefficients in, SH gradients out; unused without SH.
+// Where gaussian_bwd's per-Gaussian gradients go.  MemSink: stored (ACC = 0) or added (ACC = 1)
+// straight into the gradient buffers, one view per launch.  RegSink (preprocess_bwd_views_kernel):
+// summed over the views of a step in registers, in view order, and written once -- the same
+// operations in the same order as one launch per view (the first view stores unless ACC).
 template <bool ACC>
+struct MemSink {
+  const BwdPreArgs& a;
+  size_t i;
+  __device__ void colors(V3 v) { if (a.dL_dcolors) st3<ACC>(a.dL_dcolors, i, v); }
+  __device__ void opacity(float v) { st<ACC>(a.dL_dopacity + i, v); }
+  __device__ void cov3D(const float* d) {
+    if (a.dL_dcov3D)
+#pragma unroll
+      for (int k = 0; k < 6; k++) st<ACC>(a.dL_dcov3D + 6 * i + k, d[k]);
+  }
+  __device__ void scales(V3 v) { st3<ACC>(a.dL_dscales, i, v); }
+  __device__ void rotation(float4 dq) {
+    float4* dr = reinterpret_cast<float4*>(a.dL_drotations) + i;
+    if (ACC) {
+      const float4 o = *dr;
+      *dr = make_float4(o.x + dq.x, o.y + dq.y, o.z + dq.z, o.w + dq.w);
+    } else {
+      *dr = dq;
+    }
+  }
+  __device__ void means3D(V3 v) { st3<ACC>(a.dL_dmeans3D, i, v); }
+  __device__ void lang_feature(V3 v) { if (a.dL_dlanguage_feature) st3<ACC>(a.dL_dlanguage_feature, i, v); }
+  __device__ void sh_language(V3 v) { if (a.dL_dsh_language) st3<ACC>(a.dL_dsh_language, i, v); }
+};
+struct RegSink {
+  bool assign;  // the next contribution is the first one of store mode (assigned, not added)
+  float op;
+  V3 m3, sc, lf, shl;
+  float4 rot;
+  __device__ static V3 add3(bool as, V3 acc, V3 v) {
+    return as ? v : v3(acc.x + v.x, acc.y + v.y, acc.z + v.z);
+  }
+  __device__ void colors(V3) {}
+  __device__ void opacity(float v) { op = assign ? v : op + v; }
+  __device__ void cov3D(const float*) {}
+  __device__ void scales(V3 v) { sc = add3(assign, sc, v); }
+  __device__ void rotation(float4 dq) {
+    rot = assign ? dq : make_float4(rot.x + dq.x, rot.y + dq.y, rot.z + dq.z, rot.w + dq.w);
+  }
+  __device__ void means3D(V3 v) { m3 = add3(assign, m3, v); }
+  __device__ void lang_feature(V3 v) { lf = add3(assign, lf, v); }
+  __device__ void sh_language(V3 v) { shl = add3(assign, shl, v); }
+};
+
+// Backward of one visible Gaussian.  sh0 / sh1: its rows (coefficient 0 / coefficients 1..) of
+// the LDS staging planes: SH coefficients in, SH gradients out; unused without SH.  The
+// per-view outputs (screen-space gradient, deferred dL/dRGB, SH rows) are written here; the
+// per-Gaussian gradients go to `sk`.
+template <bool ACC, class Sink>
 __device__ __forceinline__ void gaussian_bwd(const BwdPreArgs& a, size_t i, float* sh0,
-                                             float* sh1) {
+                                             float* sh1, Sink& sk) {
   float4 q0, q1, q2, q3;
   grad_row(a, i, q0, q1, q2, q3);
   // slots: q0 = {mx, my, ca, cb}, q1 = {cc, op, r, g}, q2 = {b, depth, f0, f1}, q3 = {f2, used, -, -}
@@ -152,14 +203,14 @@ __device__ __forceinline__ void gaussian_bwd(const BwdPreArgs& a, size_t i, floa
   const float dcx = q0.z, dcy = q0.w, dcz = q1.x;
   put3(a.dL_dmeans2D, i, v3(gmx, gmy, 0.0f));  // per-call output, stored in both modes
   const V3 dL_dcolor = v3(q1.z, q1.w, q2.x);
-  if (a.dL_dcolors) st3<ACC>(a.dL_dcolors, i, dL_dcolor);
+  sk.colors(dL_dcolor);
   {
     float dop = a.confidence ? q1.y * a.confidence[i] : q1.y;
     if (a.fused) {  // through get_opacity = sigmoid(_opacity): go * (1 - y) * y
       const float y = sigmoid_f(a.opacities_raw[i]);
       dop = dop * (1.0f - y) * y;
     }
-    st<ACC>(a.dL_dopacity + i, dop);
+    sk.opacity(dop);
   }
 
   const V3 mean = v3(a.means3D[3 * i], a.means3D[3 * i + 1], a.means3D[3 * i + 2]);
@@ -208,10 +259,7 @@ __device__ __forceinline__ void gaussian_bwd(const BwdPreArgs& a, size_t i, floa
 #pragma unroll
     for (int k = 0; k < 6; k++) dcov[k] = 0.0f;
   }
-  if (a.dL_dcov3D) {
-#pragma unroll
-    for (int k = 0; k < 6; k++) st<ACC>(a.dL_dcov3D + 6 * i + k, dcov[k]);
-  }
+  sk.cov3D(dcov);
   const float dL_dT00 = 2 * (Tm(0, 0) * Vk(0, 0) + Tm(0, 1) * Vk(0, 1) + Tm(0, 2) * Vk(0, 2)) * dL_da +
                         (Tm(1, 0) * Vk(0, 0) + Tm(1, 1) * Vk(0, 1) + Tm(1, 2) * Vk(0, 2)) * dL_db;
   const float dL_dT01 = 2 * (Tm(0, 0) * Vk(1, 0) + Tm(0, 1) * Vk(1, 1) + Tm(0, 2) * Vk(1, 2)) * dL_da +
@@ -307,7 +355,7 @@ __device__ __forceinline__ void gaussian_bwd(const BwdPreArgs& a, size_t i, floa
     ds.y = dot3(v3(Rt.m[1][0], Rt.m[1][1], Rt.m[1][2]), v3(Dt.m[1][0], Dt.m[1][1], Dt.m[1][2]));
     ds.z = dot3(v3(Rt.m[2][0], Rt.m[2][1], Rt.m[2][2]), v3(Dt.m[2][0], Dt.m[2][1], Dt.m[2][2]));
     // fused: through exp (torch exp backward: grad * result)
-    st3<ACC>(a.dL_dscales, i, a.fused ? v3(ds.x * sc.x, ds.y * sc.y, ds.z * sc.z) : ds);
+    sk.scales(a.fused ? v3(ds.x * sc.x, ds.y * sc.y, ds.z * sc.z) : ds);
 #pragma unroll
     for (int w = 0; w < 3; w++) {
       Dt.m[0][w] *= s.x;
@@ -325,13 +373,7 @@ __device__ __forceinline__ void gaussian_bwd(const BwdPreArgs& a, size_t i, floa
            4 * z * (D(1, 1) + D(0, 0));
 #undef D
     if (a.fused) dq = normalize_quat_backward(qraw, dq);  // through F.normalize
-    float4* dr = reinterpret_cast<float4*>(a.dL_drotations) + i;
-    if (ACC) {
-      const float4 o = *dr;
-      *dr = make_float4(o.x + dq.x, o.y + dq.y, o.z + dq.z, o.w + dq.w);
-    } else {
-      *dr = dq;
-    }
+    sk.rotation(dq);
   }
 
   // ---- depth channel: z_view = view[2] x + view[6] y + view[10] z + view[14] ----
@@ -339,13 +381,10 @@ __device__ __forceinline__ void gaussian_bwd(const BwdPreArgs& a, size_t i, floa
   dmean.x += dz * a.view[2];
   dmean.y += dz * a.view[6];
   dmean.z += dz * a.view[10];
-  st3<ACC>(a.dL_dmeans3D, i, dmean);
+  sk.means3D(dmean);
 
   // ---- language feature channels ----
-  if (a.dL_dlanguage_feature) {
-    st3<ACC>(a.dL_dlanguage_feature, i,
-             (a.include_feature && a.lang_precomp) ? v3(q2.z, q2.w, q3.x) : v3(0, 0, 0));
-  }
+  sk.lang_feature((a.include_feature && a.lang_precomp) ? v3(q2.z, q2.w, q3.x) : v3(0, 0, 0));
   if (a.dL_dsh_language) {
     V3 out = v3(0, 0, 0);
     if (a.include_feature && a.lang_precomp == nullptr) {
@@ -358,7 +397,7 @@ __device__ __forceinline__ void gaussian_bwd(const BwdPreArgs& a, size_t i, floa
       const float k2 = n > 0.0f ? ug / (den * den * n) : 0.0f;
       out = v3(SH_C0 * (g0 / den - u0 * k2), SH_C0 * (g1 / den - u1 * k2), SH_C0 * (g2 / den - u2 * k2));
     }
-    st3<ACC>(a.dL_dsh_language, i, out);
+    sk.sh_language(out);
   }
 }
 
@@ -402,7 +441,8 @@ __global__ __launch_bounds__(kThreads) void preprocess_bwd_kernel(BwdPreArgs a) 
   float* r1 = a.fused ? s_sh + p1.lds + t * p1.w : r0 + 3;
   const bool defer = a.dRGB_out != nullptr;
   if (live) {
-    gaussian_bwd<ACC>(a, i, r0, r1);
+    MemSink<ACC> sk{a, i};
+    gaussian_bwd<ACC>(a, i, r0, r1, sk);
     if (has_sh && !defer) {  // coefficients above the active degree: zero gradient
       const int used = (a.D + 1) * (a.D + 1) * 3;
       for (int k = used; k < a.M * 3; k++) r1[k - 3] = 0.0f;
@@ -421,6 +461,67 @@ __global__ __launch_bounds__(kThreads) void preprocess_bwd_kernel(BwdPreArgs a) 
     stage<kThreads, false, ACC>(p0, base, n, s_live, s_sh);
     stage<kThreads, false, ACC>(p1, base, n, s_live, s_sh);
   }
+}
+
+// The per-Gaussian backwards of several views in ONE launch (multi-view calls, deferred SH
+// gradients with the pre-pass Jacobian): per Gaussian the views are processed in order with
+// gaussian_bwd, their gradients summed in registers (RegSink: the same additions, in the same
+// order, as one launch per view) and written once -- the parameters and the leaves' gradients
+// cross HBM once per step instead of once per view.  View 0's `accumulate` decides store / add.
+template <bool ACC>
+__global__ __launch_bounds__(kThreads) void preprocess_bwd_views_kernel(BwdPreViews m) {
+  const BwdPreArgs& a0 = m.v[0];
+  const size_t i = (size_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= (size_t)a0.P) return;
+  RegSink sk;
+  sk.assign = !ACC;
+  if (ACC) {
+    sk.op = a0.dL_dopacity[i];
+    sk.m3 = v3(a0.dL_dmeans3D[3 * i], a0.dL_dmeans3D[3 * i + 1], a0.dL_dmeans3D[3 * i + 2]);
+    sk.sc = a0.dL_dscales ? v3(a0.dL_dscales[3 * i], a0.dL_dscales[3 * i + 1], a0.dL_dscales[3 * i + 2])
+                          : v3(0, 0, 0);
+    sk.rot = a0.dL_drotations ? reinterpret_cast<const float4*>(a0.dL_drotations)[i]
+                              : make_float4(0, 0, 0, 0);
+    sk.shl = a0.dL_dsh_language ? v3(a0.dL_dsh_language[3 * i], a0.dL_dsh_language[3 * i + 1],
+                                     a0.dL_dsh_language[3 * i + 2]) : v3(0, 0, 0);
+    sk.lf = a0.dL_dlanguage_feature ? v3(a0.dL_dlanguage_feature[3 * i], a0.dL_dlanguage_feature[3 * i + 1],
+                                         a0.dL_dlanguage_feature[3 * i + 2]) : v3(0, 0, 0);
+  } else {  // a view-0-culled Gaussian is zero in store mode (zero_outputs)
+    sk.op = 0.0f;
+    sk.m3 = sk.sc = sk.shl = sk.lf = v3(0, 0, 0);
+    sk.rot = make_float4(0, 0, 0, 0);
+  }
+  bool touched = !ACC;
+  for (int v = 0; v < m.V; v++) {
+    const BwdPreArgs& a = m.v[v];
+    if (a.status && *a.status) {  // this view's forward failed (view-uniform): NaN gradients
+      const float nan = __builtin_nanf("");
+      const V3 n3 = v3(nan, nan, nan);
+      put3(a.dL_dmeans2D, i, n3);
+      put3p(a.dRGB_out, (size_t)a.P, i, n3);
+      sk.opacity(nan); sk.means3D(n3); sk.scales(n3); sk.rotation(make_float4(nan, nan, nan, nan));
+      sk.lang_feature(n3); sk.sh_language(n3);
+      sk.assign = false;
+      touched = true;
+      continue;
+    }
+    if (a.radii[i] > 0) {
+      gaussian_bwd<true>(a, i, nullptr, nullptr, sk);
+      sk.assign = false;
+      touched = true;
+    } else {
+      put3(a.dL_dmeans2D, i, v3(0, 0, 0));
+      put3p(a.dRGB_out, (size_t)a.P, i, v3(0, 0, 0));
+      if (v == 0) sk.assign = false;  // store mode: the zeros of the culled first view
+    }
+  }
+  if (!touched) return;  // accumulate mode, culled in every view: nothing to add
+  a0.dL_dopacity[i] = sk.op;
+  put3(a0.dL_dmeans3D, i, sk.m3);
+  if (a0.dL_dscales) put3(a0.dL_dscales, i, sk.sc);
+  if (a0.dL_drotations) reinterpret_cast<float4*>(a0.dL_drotations)[i] = sk.rot;
+  if (a0.dL_dsh_language) put3(a0.dL_dsh_language, i, sk.shl);
+  if (a0.dL_dlanguage_feature) put3(a0.dL_dlanguage_feature, i, sk.lf);
 }
 
 // Deferred SH gradients of a multi-view step: per Gaussian, for each view v in order,
@@ -478,6 +579,32 @@ hipError_t launch_sh_grad_flush(const ShFlushArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(sh_flush_kernel<true>, grid, dim3(kThreads), 0, s, a);
   else
     hipLaunchKernelGGL(sh_flush_kernel<false>, grid, dim3(kThreads), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_preprocess_backward_views(const BwdPreArgs* views, int V, hipStream_t s) {
+  if (V <= 0) return hipSuccess;
+  if (V > kMaxBwdViews) return hipErrorNotSupported;
+  BwdPreViews m{};
+  m.V = V;
+  for (int k = 0; k < V; k++) {
+    const BwdPreArgs& a = views[k];
+    // the multi-view kernel covers the fused, deferred-SH, pre-pass configuration of one model
+    if (!a.fused || !a.dRGB_out || !a.pre_jac || a.cov3D || a.colors_precomp || a.dL_dcolors ||
+        a.dL_dcov3D || a.use_rows || a.P != views[0].P || a.means3D != views[0].means3D ||
+        a.dL_dmeans3D != views[0].dL_dmeans3D || a.dL_dopacity != views[0].dL_dopacity ||
+        a.dL_dscales != views[0].dL_dscales || a.dL_drotations != views[0].dL_drotations ||
+        a.dL_dsh_language != views[0].dL_dsh_language ||
+        a.dL_dlanguage_feature != views[0].dL_dlanguage_feature || (k > 0 && !a.accumulate))
+      return hipErrorNotSupported;
+    m.v[k] = a;
+  }
+  if (views[0].P == 0) return hipSuccess;
+  const dim3 grid((views[0].P + kThreads - 1) / kThreads);
+  if (views[0].accumulate)
+    hipLaunchKernelGGL(preprocess_bwd_views_kernel<true>, grid, dim3(kThreads), 0, s, m);
+  else
+    hipLaunchKernelGGL(preprocess_bwd_views_kernel<false>, grid, dim3(kThreads), 0, s, m);
   return hipGetLastError();
 }
 

@@ -283,6 +283,14 @@ struct BwdPreArgs {
   const uint32_t* count;
 };
 hipError_t launch_preprocess_backward(const BwdPreArgs& a, hipStream_t s);
+// the per-Gaussian backwards of several views in one launch (fused, deferred SH with the pre-pass
+// Jacobian, shared gradient buffers, views after the first accumulating); hipErrorNotSupported
+// for any other configuration (the caller then launches per view)
+struct BwdPreViews {
+  BwdPreArgs v[8];
+  int V;
+};
+hipError_t launch_preprocess_backward_views(const BwdPreArgs* views, int V, hipStream_t s);
 constexpr int kShFlushMaxViews = 8;
 struct ShFlushArgs {
   int P, M, D, nviews, accumulate;
