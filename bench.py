@@ -164,6 +164,9 @@ def main():
                     help="issue the step view by view (render() + autograd per view, lagged over "
                          "the streams) instead of one multi-view call for all of the step's "
                          "views (gaussian_renderer.render_views)")
+    ap.add_argument("--view-chunks", type=int, default=1,
+                    help="multi-view calls per step (the step's views split into this many "
+                         "consecutive chunks, each forward + backward)")
     ap.add_argument("--no-precolor", action="store_true",
                     help="each view evaluates its SH colour itself instead of the step's pre-pass")
     ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_r03.json"))
@@ -195,7 +198,9 @@ def main():
     # hardware-queue budget: view streams + RCCL's stream within GPU_MAX_HW_QUEUES (default 4), so
     # a collective never shares a queue with a view's backward blend (it would serialise them)
     hw_queues = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
-    streams = args.streams or (3 if world == 1 else 2)
+    multi = not args.per_view and not args.autograd_grads
+    # multi-view calls: the call's stream (blends) + binning stream(s) + the backward-blend stream
+    streams = args.streams or ((4 if world == 1 else 3) if multi else (3 if world == 1 else 2))
     if world > 1:
         streams = max(1, min(streams, hw_queues - 1))
 
@@ -255,20 +260,25 @@ def main():
             views.run(my_cams, lambda cam: one_view(cam, record), model=model, reducer=reducer)
 
     def all_views(cams, strs, record):
-        """Every view of the step in one multi-view call: forward of all views, then the
-        backward of the fixed upstream gradients seeded on the stacked [V,...] outputs."""
-        pkgs = render_views(cams, model, pipe, bg, opt, streams=strs)
-        st = pkgs[0]["views"]
-        V = len(pkgs)
-        torch.autograd.backward(
-            [st["render"], st["depth"], st["feature"]],
-            [dimg.expand(V, *dimg.shape), ddep.expand(V, *ddep.shape),
-             dfeat.expand(V, *dfeat.shape)])
-        if record:
-            for (nr, ni), pkg in zip(dgr.LAST_STATS["view_counts"], pkgs):
-                stats["R"].append(ni)
-                stats["R_ref"].append(nr)
-                stats["Pv"].append(int(pkg["visibility_filter"].sum()))
+        """The step's views in `--view-chunks` multi-view calls: a chunk's forward of all its
+        views, then the backward of the fixed upstream gradients seeded on its stacked [V,...]
+        outputs, so the next chunk's binning (latency-bound, on the binning streams) runs beside
+        this chunk's backward blend (on the backward stream)."""
+        n = max(1, min(args.view_chunks, len(cams)))
+        bounds = [round(i * len(cams) / n) for i in range(n + 1)]
+        for a, b in zip(bounds[:-1], bounds[1:]):
+            pkgs = render_views(cams[a:b], model, pipe, bg, opt, streams=strs)
+            st = pkgs[0]["views"]
+            V = len(pkgs)
+            torch.autograd.backward(
+                [st["render"], st["depth"], st["feature"]],
+                [dimg.expand(V, *dimg.shape), ddep.expand(V, *ddep.shape),
+                 dfeat.expand(V, *dfeat.shape)])
+            if record:
+                for (nr, ni), pkg in zip(dgr.LAST_STATS["view_counts"], pkgs):
+                    stats["R"].append(ni)
+                    stats["R_ref"].append(nr)
+                    stats["Pv"].append(int(pkg["visibility_filter"].sum()))
 
     def view_forward(cam):
         pkg = render(cam, model, pipe, bg, opt)

@@ -16,6 +16,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/gsr.h"
@@ -1093,38 +1094,57 @@ int gsr_rasterize_views_fused(int V, gsr_view* views, int image_height, int imag
     if (cams[(size_t)v].stream != call_stream &&
         hipStreamWaitEvent(cams[(size_t)v].stream, start, 0) != hipSuccess)
       return fail(GSR_ERR_HIP, "stream wait failed");
-  // Software-pipelined issue: the first phase of view v + inflight goes out right after view v's
-  // binning, so per stream the order stays begin(v), bin(v), begin(v + inflight), ...  The blends
-  // of a group of views run merged into one launch on the call's stream once the group's binning
-  // is done (`groups` groups of consecutive views; GSR_VIEWS_FWD_GROUPS), while the views' streams
-  // go on with the next views' preprocess / sorts.
-  const int ahead = inflight < 1 ? 1 : inflight;
+  // Software-pipelined, readiness-driven issue.  Each view stream holds one view in flight: its
+  // first phase (preprocess .. scan, read-back) is queued, and when the host sees that view's
+  // read-back complete -- whichever stream's comes first -- it issues the view's binning and then
+  // the first phase of the next view assigned to that stream, so per stream the order stays
+  // begin(a), bin(a), begin(b), bin(b), ... and no stream idles behind the host waiting for
+  // another stream's view.  The blends of a group of consecutive views (`groups` groups;
+  // GSR_VIEWS_FWD_GROUPS) run merged into one launch on the call's stream once the group's
+  // binning has been issued, in group order.
   static const int groups_env = [] {
     const char* e = getenv("GSR_VIEWS_FWD_GROUPS");
     return e ? atoi(e) : 2;
   }();
+  (void)inflight;  // one view in flight per distinct view stream
   const int ng = groups_env < 1 ? 1 : groups_env;
   int per = (V + ng - 1) / ng;
   if (per < 1) per = 1;
   if (per > kMaxFwdViews) per = kMaxFwdViews;
-  for (int v = 0; v < V && v < ahead; v++)
-    if (int rc = fwd_begin(m, cams[(size_t)v])) return rc;
-  for (int v0 = 0; v0 < V; v0 += per) {
-    const int n = V - v0 < per ? V - v0 : per;
-    RenderArgs ras[kMaxFwdViews];
-    int nb = 0;
-    for (int k = 0; k < n; k++) {
-      const int v = v0 + k;
+  std::vector<int> state((size_t)V, 0);  // 0 = not begun, 1 = first phase queued, 2 = binned
+  auto begin_next_on = [&](hipStream_t st) -> int {
+    for (int u = 0; u < V; u++)
+      if (state[(size_t)u] == 0 && cams[(size_t)u].stream == st) {
+        for (int w = 0; w < u; w++)  // one view in flight per stream
+          if (state[(size_t)w] == 1 && cams[(size_t)w].stream == st) return GSR_OK;
+        if (int rc = fwd_begin(m, cams[(size_t)u])) return rc;
+        state[(size_t)u] = 1;
+        return GSR_OK;
+      }
+    return GSR_OK;
+  };
+  for (int v = 0; v < V; v++)
+    if (int rc = begin_next_on(cams[(size_t)v].stream)) return rc;
+  int binned = 0, next_group = 0;
+  while (binned < V || next_group * per < V) {
+    bool progressed = false;
+    for (int v = 0; v < V; v++) {
+      if (state[(size_t)v] != 1) continue;
       FwdCam& c = cams[(size_t)v];
+      if (!c.done) {
+        const hipError_t q = hipEventQuery(c.ready);
+        if (q == hipErrorNotReady) continue;
+        if (q != hipSuccess) return fail(GSR_ERR_HIP, "hipEventQuery: %s", hipGetErrorString(q));
+      }
       if (int rc = fwd_bin(m, c)) return rc;
       if (!c.done) {
         const int debug = m.debug;
         hipStream_t stream = c.stream;
         GSR_CHECK(launch_render_schedule(c.ra, stream));
-        ras[nb++] = c.ra;
       }
-      if (v + ahead < V)
-        if (int rc = fwd_begin(m, cams[(size_t)(v + ahead)])) return rc;
+      state[(size_t)v] = 2;
+      binned++;
+      progressed = true;
       gsr_view& out = views[v];
       out.geom_buffer = c.gbase; out.binning_buffer = c.bbase; out.image_buffer = c.ibase;
       out.num_rendered = c.num_rendered; out.num_instances = c.num_instances;
@@ -1134,16 +1154,32 @@ int gsr_rasterize_views_fused(int V, gsr_view* views, int image_height, int imag
             hipStreamWaitEvent(call_stream, e, 0) != hipSuccess)
           return fail(GSR_ERR_HIP, "joining view %d's stream failed", v);
       }
+      if (int rc = begin_next_on(c.stream)) return rc;
     }
-    if (nb > 0) {
-      const int debug = m.debug;
-      hipStream_t stream = call_stream;
-      PROF_BEGIN(RENDER_FWD);
-      GSR_CHECK(launch_render_forward_views(ras, nb, call_stream));
-      PROF_END(RENDER_FWD);
+    // merged blends of the groups whose views are all binned, in group order
+    while (next_group * per < V) {
+      const int v0 = next_group * per;
+      const int n = V - v0 < per ? V - v0 : per;
+      bool ready = true;
+      for (int k = 0; k < n; k++) ready = ready && state[(size_t)(v0 + k)] == 2;
+      if (!ready) break;
+      RenderArgs ras[kMaxFwdViews];
+      int nb = 0;
+      for (int k = 0; k < n; k++)
+        if (!cams[(size_t)(v0 + k)].done) ras[nb++] = cams[(size_t)(v0 + k)].ra;
+      if (nb > 0) {
+        const int debug = m.debug;
+        hipStream_t stream = call_stream;
+        PROF_BEGIN(RENDER_FWD);
+        GSR_CHECK(launch_render_forward_views(ras, nb, call_stream));
+        PROF_END(RENDER_FWD);
+      }
+      for (int k = 0; k < n; k++)
+        if (int rc = fwd_blended(m, cams[(size_t)(v0 + k)], call_stream)) return rc;
+      next_group++;
+      progressed = true;
     }
-    for (int k = 0; k < n; k++)
-      if (int rc = fwd_blended(m, cams[(size_t)(v0 + k)], call_stream)) return rc;
+    if (!progressed) std::this_thread::yield();  // every view in flight still computes
   }
   if (V > 0) g_last_instances = cams[(size_t)V - 1].num_instances;
   return GSR_OK;

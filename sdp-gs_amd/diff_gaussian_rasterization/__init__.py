@@ -10,6 +10,7 @@ The native side is libgsr.so (include/gsr.h), hand-written HIP for gfx950; there
 from __future__ import annotations
 
 import os
+import time
 import sys
 from typing import NamedTuple, Optional
 
@@ -458,6 +459,12 @@ def rasterize_views_fused(means3D, means2D, features_dc, features_rest, opacity_
                                       tuple(raster_settings_list), tuple(streams or ()))
 
 
+def _view_streams(streams):
+    """The streams a multi-view forward bins its views on: the side streams (streams[1:]).  The
+    backward's merged blend runs on the last of them, idle by then."""
+    return tuple(streams[1:])
+
+
 class _RasterizeViewsFused(torch.autograd.Function):
     @staticmethod
     def forward(ctx, means3D, means2D, features_dc, features_rest, opacity_raw, scaling_raw,
@@ -504,9 +511,9 @@ class _RasterizeViewsFused(torch.autograd.Function):
         radii = torch.empty((V, P), dtype=torch.int32, device=dev)
         views = (_lib.GsrView * V)()
         holders = [_lib.BufferHolder(dev) for _ in range(V)]
-        # the views' preprocess / sorts / binning on the side streams (streams[1:]), their merged
-        # blends on the call's stream (include/gsr.h); with one stream everything runs there
-        vstreams = tuple(streams[1:]) if len(streams) > 1 else ()
+        # the views' preprocess / sorts / binning on the side streams, their merged blends on the
+        # call's stream (include/gsr.h); with one stream everything runs there
+        vstreams = _view_streams(streams)
         cams, pres = [], []
         n_img, n_rad = 4 * H * W, 4 * P
         for v, rs in enumerate(settings):
@@ -532,6 +539,7 @@ class _RasterizeViewsFused(torch.autograd.Function):
         L = _lib.load()
         cur = torch.cuda.current_stream(dev)
         flags = _debug_flags(rs0.debug)
+        t_host = time.perf_counter()
         try:
             with _lib.on_device(dev):
                 rc = L.gsr_rasterize_views_fused(
@@ -543,6 +551,7 @@ class _RasterizeViewsFused(torch.autograd.Function):
         finally:
             for h in holders:
                 h.release()
+        LAST_STATS["views_fwd_host_s"] = time.perf_counter() - t_host  # host time of the call
         LAST_STATS["num_rendered"] = int(views[V - 1].num_rendered)
         LAST_STATS["num_instances"] = int(views[V - 1].num_instances)
         LAST_STATS["P"] = P
@@ -596,8 +605,9 @@ class _RasterizeViewsFused(torch.autograd.Function):
         zero_col = None
         views = ctx.views
         # the backward blends of all views run merged into one launch on views[0].stream
-        # (include/gsr.h), beside the per-Gaussian backwards on the call's stream: a side stream
-        views[0].stream = ctx.streams[1 % len(ctx.streams)].cuda_stream if ctx.streams else None
+        # (include/gsr.h), beside the per-Gaussian backwards on the call's stream: the last side
+        # stream
+        views[0].stream = ctx.streams[-1].cuda_stream if len(ctx.streams) > 1 else None
         into_leaves = ctx.leaves is not None
         defer = _SH_DEFER.get(dev.index) if into_leaves else None
         d_means2D = torch.empty((V, P, 3), **fopts)
@@ -656,6 +666,7 @@ class _RasterizeViewsFused(torch.autograd.Function):
         cur = torch.cuda.current_stream(dev)
         if into_leaves:
             _order_leaf_grads(dev, cur)
+        t_host = time.perf_counter()
         with _lib.on_device(dev):
             rc = L.gsr_rasterize_views_fused_backward(
                 V, views, H, W, P, M, _ptr(bg), _ptr(m3), _ptr(dc), _ptr(rest), _ptr(op),
@@ -664,6 +675,7 @@ class _RasterizeViewsFused(torch.autograd.Function):
                 _ptr(d_op), _ptr(d_sc), _ptr(d_rot), _ptr(d_lf), int(accumulate),
                 cur.cuda_stream, ctx.gsr_flags)
         _lib.check(rc)
+        LAST_STATS["views_bwd_host_s"] = time.perf_counter() - t_host
         if into_leaves:
             prev = _LEAF_GRAD_EVENT.get(dev.index)
             ev = prev[0] if prev is not None else torch.cuda.Event()
