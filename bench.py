@@ -169,7 +169,7 @@ def main():
                          "consecutive chunks, each forward + backward)")
     ap.add_argument("--no-precolor", action="store_true",
                     help="each view evaluates its SH colour itself instead of the step's pre-pass")
-    ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_r03.json"))
+    ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_r03b.json"))
     ap.add_argument("--no-extra-legs", action="store_true",
                     help="skip the train-step, reference-cadence and reference-API legs")
     ap.add_argument("--cpu-threads", type=int, default=0,
@@ -240,7 +240,8 @@ def main():
             stats["R_ref"].append(dgr.LAST_STATS["num_rendered"])
             stats["Pv"].append(int(pkg["visibility_filter"].sum()))
 
-    def step(record=False):
+    def step(record=False, vp=None):
+        views_ = vp or views
         my_cams = step_cams(step_no[0])
         step_no[0] += 1
         if reducer is not None:
@@ -251,13 +252,13 @@ def main():
         # with a reducer the all-reduce overlaps the step's tail (non-SH grads while the SH
         # gradients are flushed in row slices, each slice reduced as soon as it is written)
         if not args.per_view and not args.autograd_grads:
-            views.run_views(my_cams, lambda cams, strs: all_views(cams, strs, record),
-                            model=model, reducer=reducer)
+            views_.run_views(my_cams, lambda cams, strs: all_views(cams, strs, record),
+                             model=model, reducer=reducer)
         elif args.lag > 0:
-            views.run(my_cams, view_forward, model=model, reducer=reducer,
-                      bwd=lambda pkg: view_backward(pkg, record), lag=args.lag)
+            views_.run(my_cams, view_forward, model=model, reducer=reducer,
+                       bwd=lambda pkg: view_backward(pkg, record), lag=args.lag)
         else:
-            views.run(my_cams, lambda cam: one_view(cam, record), model=model, reducer=reducer)
+            views_.run(my_cams, lambda cam: one_view(cam, record), model=model, reducer=reducer)
 
     def all_views(cams, strs, record):
         """The step's views in `--view-chunks` multi-view calls: a chunk's forward of all its
@@ -308,9 +309,14 @@ def main():
     all_stages = {}
     dom_stage = None
     if not args.no_stage_timing:
+        # the per-stage table and the choice of the dominant kernel come from one instrumented step
+        # issued on ONE stream: with the views' work spread over several streams an event pair
+        # also spans the other streams' kernels, so a latency-bound stage that waits beside a
+        # full-chip launch would look dominant
+        serial = ViewPipeline(dev, depth=1, defer_sh=defer_sh, precolor=not args.no_precolor)
         timer.reset()
         timer.enable(True)
-        step()
+        step(vp=serial)
         timer.enable(False)
         all_stages = timer.collect()
         busy = {n: ms for n, (ms, c) in all_stages.items() if c}
@@ -498,10 +504,11 @@ def extra_legs(args, model, step_cams, pool, n_views, views, reducer, timed_regi
       after every view (gsr_amd.trainer.train_iteration), rank 0 at N = 1.
     These legs train the model (the headline is measured before them)."""
     import diff_gaussian_rasterization as dgr
-    from gaussian_renderer import render
+    from gaussian_renderer import render, render_views
     from gsr_amd import trainer
     from gsr_amd.synthetic import training_targets
     P, W, H, deg = wl
+    multi_issue = not args.per_view and not args.autograd_grads
     dimg, ddep, dfeat = grads
     out = {}
     k_step = [0]
@@ -528,7 +535,17 @@ def extra_legs(args, model, step_cams, pool, n_views, views, reducer, timed_regi
                 torch.autograd.backward([pkg["render"], pkg["depth"], pkg["feature"]],
                                         [dimg, ddep, dfeat])
             cams = next_cams()
-            if args.lag > 0:
+            if multi_issue:
+                def all_views(cs, strs):
+                    pkgs = render_views(cs, model, Pipe(), bg, Opt(), streams=strs)
+                    st = pkgs[0]["views"]
+                    V = len(pkgs)
+                    torch.autograd.backward(
+                        [st["render"], st["depth"], st["feature"]],
+                        [dimg.expand(V, *dimg.shape), ddep.expand(V, *ddep.shape),
+                         dfeat.expand(V, *dfeat.shape)])
+                views.run_views(cams, all_views, model=model, reducer=reducer)
+            elif args.lag > 0:
                 views.run(cams, fwd, model=model, reducer=reducer, bwd=bwd, lag=args.lag)
             else:
                 views.run(cams, lambda cam: bwd(fwd(cam)), model=model, reducer=reducer)
@@ -588,7 +605,7 @@ def extra_legs(args, model, step_cams, pool, n_views, views, reducer, timed_regi
         cams = next_cams()
         trainer.train_step_views(model, cams, [gts[c.uid] for c in cams],
                                  [monos[c.uid] for c in cams], bg, targs, it[0], extent, views,
-                                 reducer=reducer)
+                                 reducer=reducer, multi=multi_issue)
         it[0] += 1
     for _ in range(args.warmup):
         train_step()

@@ -18,6 +18,9 @@ STAGE = {"preprocess_kernel": "preprocess", "duplicate_kernel": "duplicate",
          "tile_ranges_kernel": "ranges", "render_fwd_kernel": "render_fwd",
          "render_fwd_blk_kernel": "render_fwd",
          "render_bwd_kernel": "render_bwd", "preprocess_bwd_kernel": "preprocess_bwd",
+         # multi-view calls: several views per launch
+         "render_bwd_views_kernel": "render_bwd", "render_fwd_blk_views_kernel": "render_fwd",
+         "preprocess_bwd_views_kernel": "preprocess_bwd",
          "radix_totals_kernel": "radix_totals", "radix_onesweep_kernel": "radix_onesweep",
          "scan_reduce_kernel": "scan_reduce", "scan_final_kernel": "scan_final",
          "scan_parts_kernel": "scan_parts", "sh_precolor_kernel": "sh_precolor",

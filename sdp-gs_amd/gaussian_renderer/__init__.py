@@ -288,11 +288,14 @@ def render_views(viewpoint_cameras, pc, pipe, bg_color: torch.Tensor, opt, scali
     # these (autograd on the per-view slices would materialise a [V,...] zero gradient per view)
     stacked = {"render": color, "depth": depth, "alpha": alpha, "feature": feature,
                "viewspace_points": means2D, "radii": radii}
+    # per-view images by unbind: a loss over some or all of them back-propagates through ONE
+    # stack of the per-view gradients (indexing would add a [V,...] zero tensor per view)
+    per = [t.unbind(0) for t in (color, depth, alpha, feature)]
     out = []
     for v in range(V):
         r = radii[v]
-        out.append(_RenderPkg({"render": color[v], "depth": depth[v], "alpha": alpha[v],
-                               "feature": feature[v], "viewspace_points": ViewGrad(means2D, v),
+        out.append(_RenderPkg({"render": per[0][v], "depth": per[1][v], "alpha": per[2][v],
+                               "feature": per[3][v], "viewspace_points": ViewGrad(means2D, v),
                                "radii": r, "color": None, "views": stacked, "view_index": v},
                               {"opacity": lambda: pc.get_opacity,
                                "visibility_filter": (lambda r=r: r > 0)}))

@@ -111,12 +111,15 @@ def train_iteration(model, cam, gt_image, depth_mono, bg, args: OptArgs, iterati
 def train_step_views(model, cams: Sequence, gt_images: Sequence[torch.Tensor],
                      depth_monos: Sequence[Optional[torch.Tensor]], bg, args: OptArgs,
                      iteration: int, extent: float, pipeline, reducer=None, pipe=None,
-                     generator=None) -> List[torch.Tensor]:
-    """The batched iteration: every camera's render + loss + backward + statistics on the
-    pipeline's streams (gradients summed over the views), the gradient all-reduce across ranks
-    (reducer, overlapped with the step's tail), densification when due (statistics summed / maxed
-    across ranks first, identical generator on every rank), one optimizer step."""
-    from gaussian_renderer import render
+                     generator=None, multi: bool = True) -> List[torch.Tensor]:
+    """The batched iteration: every camera's render + loss + backward + statistics (gradients
+    summed over the views), the gradient all-reduce across ranks (reducer, overlapped with the
+    step's tail), densification when due (statistics summed / maxed across ranks first,
+    identical generator on every rank), one optimizer step.  multi: all views in one multi-view
+    call (gaussian_renderer.render_views: one host call for the forwards, one for the backwards;
+    the per-view losses are back-propagated together); else view by view on the pipeline's
+    streams (render() per view, lagged)."""
+    from gaussian_renderer import render, render_views
     from .parallel import allreduce_densification_stats
     pipe = pipe or _Pipe()
     if reducer is not None:
@@ -124,6 +127,27 @@ def train_step_views(model, cams: Sequence, gt_images: Sequence[torch.Tensor],
     else:
         model.optimizer.zero_grad(set_to_none=True)
     gts = {id(c): (g, d) for c, g, d in zip(cams, gt_images, depth_monos)}
+
+    if multi:
+        def all_views(cs, strs):
+            pkgs = render_views(cs, model, pipe, bg, args, streams=strs)
+            losses = [_view_loss(pkg, *gts[id(c)], args) for c, pkg in zip(cs, pkgs)]
+            torch.autograd.backward(losses)
+            with torch.no_grad():
+                if iteration < args.densify_until_iter:
+                    for pkg in pkgs:
+                        model.update_densification_stats(pkg["viewspace_points"], pkg["radii"],
+                                                         pkg["visibility_filter"])
+            return [loss.detach() for loss in losses]
+        losses = pipeline.run_views(cams, all_views, model=model, reducer=reducer)
+        with torch.no_grad():
+            if _densify_due(iteration, args):
+                allreduce_densification_stats(model.xyz_gradient_accum, model.denom,
+                                               model.max_radii2D)
+                densify_step(model, args, iteration, extent, generator=generator)
+            _guard_step()
+            model.optimizer.step()
+        return losses
 
     def forward(cam):
         pkg = render(cam, model, pipe, bg, args)
