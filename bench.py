@@ -375,6 +375,10 @@ def main():
         b = vpl * algorithmic_bytes(name, P, Pv, R, T, HW, D=deg, acc=not args.autograd_grads,
                                     defer_sh=defer_sh, precolor=not args.no_precolor,
                                     views=len(my_cams))
+        if name == "preprocess" and vpl > 1:
+            # the multi-view preprocess reads each Gaussian's model rows (means, scale, rotation,
+            # opacity, language: 56 B) once for all the launch's views
+            b -= (vpl - 1) * (P * 12 + Pv * (12 + 16 + 4 + 12))
         k = {"avg_ms": round(avg_ms, 4), "calls": int(calls), "bytes": int(b),
              "views_per_launch": vpl, "gbs": round(b / (avg_ms * 1e-3) / 1e9, 1)}
         if name in ("render_fwd", "render_bwd"):

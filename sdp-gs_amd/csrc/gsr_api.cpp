@@ -16,6 +16,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <algorithm>
 #include <thread>
 #include <vector>
 
@@ -402,6 +403,7 @@ struct FwdCam {
   void* alloc_ctx = nullptr;
   hipStream_t stream = nullptr;
   uint32_t* host = nullptr;    // pinned landing slot of the read-back
+  uint32_t* host_dev = nullptr;  // its device pointer (batched binning: the sum kernel stores it)
   hipEvent_t ready = nullptr;  // recorded after the read-back's copy
   // state of the first phase
   char *gbase = nullptr, *ibase = nullptr, *bbase = nullptr;
@@ -411,7 +413,10 @@ struct FwdCam {
   uint32_t gx = 0, gy = 0;
   bool done = false;  // P == 0: outputs written by the first phase
   bool depth_in_b = false;  // which buffer pair holds the depth sort's result
+  bool defer_pre = false;  // fwd_prep leaves the preprocess arguments in pa (not launched)
+  PreArgs pa{};
   // state of the binning half of the second phase (fwd_bin -> the blend)
+  BinState b{};
   RenderArgs ra{};
   int mail_slot = -1;
   // results
@@ -451,9 +456,9 @@ static int fwd_check_model(FwdModel& m) {
   return GSR_OK;
 }
 
-// Phase 1: preprocess, the instance counts' read-back (queued, not waited for), depth sort and
-// scan.  Nothing here blocks the host.
-static int fwd_begin(const FwdModel& m, FwdCam& c) {
+// Phase 1a: the call's buffers and the preprocess launch (its per-workgroup instance counts in
+// g.pre_parts).
+static int fwd_prep(const FwdModel& m, FwdCam& c) {
   const int debug = m.debug;
   hipStream_t stream = c.stream;
   const int W = c.W, H = c.H, P = m.P;
@@ -509,8 +514,25 @@ static int fwd_begin(const FwdModel& m, FwdCam& c) {
   pa.clear = SideClear{g.sort.aux, sort_clear_bytes(g.sort, (size_t)P, 32)};
   pa.acc_zero = m.rows ? 0 : 1;  // the rows layout never reads the accumulator rows
   pa.parts = g.pre_parts;
+  if (c.defer_pre) {  // the multi-view call launches the views' preprocesses together
+    c.pa = pa;
+    return GSR_OK;
+  }
   PROF_BEGIN(PREPROCESS);
   GSR_CHECK(launch_preprocess(pa, stream));
+  PROF_END(PREPROCESS);
+  return GSR_OK;
+}
+
+// Phase 1: preprocess, the instance counts' read-back (queued, not waited for), depth sort and
+// scan.  Nothing here blocks the host.
+static int fwd_begin(const FwdModel& m, FwdCam& c) {
+  if (int rc = fwd_prep(m, c)) return rc;
+  if (c.done) return GSR_OK;
+  const int debug = m.debug;
+  hipStream_t stream = c.stream;
+  const int P = m.P;
+  const GeomState& g = c.g;
   // R = total tile count (order-independent): reduced right after the preprocess and read back
   // while the depth sort and the scan are already queued behind it, so the host's wait and the
   // binning-buffer allocation overlap GPU work instead of draining the stream
@@ -521,7 +543,6 @@ static int fwd_begin(const FwdModel& m, FwdCam& c) {
   // same offsets
   const size_t pre_blocks = ((size_t)P + 255) / 256;
   GSR_CHECK(sum_u32_parts(g.pre_parts, pre_blocks, g.flags + 1, stream, g.pre_parts + pre_blocks));
-  PROF_END(PREPROCESS);
   // one read-back: flags[0] (prefiltered violation), R and the reference's count.  The sorts'
   // look-back timeouts are this call's status (mailbox below), not part of this wait.
   GSR_CHECK(hipMemcpyAsync(c.host, g.flags, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
@@ -540,6 +561,48 @@ static int fwd_begin(const FwdModel& m, FwdCam& c) {
   GSR_CHECK(scan_u32(counts_sorted, nullptr, g.offsets, (size_t)P, true, g.scan_parts, stream));
   PROF_END(SCAN);
   return GSR_OK;
+}
+
+// The read-back's values (already landed in c.host) -> the argument checks of
+// rasterizer_impl.cu:281-283 and the binning buffer, carved for the reference's count.
+static int fwd_bin_alloc(const FwdModel& m, FwdCam& c) {
+  const int debug = m.debug;
+  hipStream_t stream = c.stream;
+  const GeomState& g = c.g;
+  uint32_t* host = c.host;
+  const uint32_t R = host[1];       // instances binned: tiles that pass the exact cull
+  const uint32_t R_ref = host[2];   // the reference's num_rendered (full rectangles), R <= R_ref
+  if (m.prefiltered && host[0]) return fail(GSR_ERR_PREFILTERED,
+                           "Point is filtered although prefiltered is set. This shouldn't happen!");
+  if (R_ref > 0x7fffffffu || R > R_ref)
+    return fail(GSR_ERR_TOO_LARGE, "num_rendered = %u exceeds the sort capacity", R_ref);
+  if (debug) {
+    GSR_CHECK(hipMemcpyAsync(host + 2, g.sort.aux + kSortAuxErr, 4, hipMemcpyDeviceToHost, stream));
+    GSR_CHECK(hipStreamSynchronize(stream));
+    if (host[2]) return fail(GSR_ERR_HIP, "depth sort look-back timed out");
+  }
+  const size_t bbytes = carve_bin(nullptr, R_ref, m.rows).bytes;
+  c.bbase = (char*)c.alloc(c.alloc_ctx, bbytes, GSR_BUF_BINNING);
+  if (!c.bbase) return fail(GSR_ERR_ALLOC, "binning buffer allocation of %zu bytes failed", bbytes);
+  c.b = carve_bin(c.bbase, R_ref, m.rows);  // capacity R_ref, the first R entries used
+  c.num_rendered = (int)R_ref;
+  c.num_instances = (int)R;
+  return GSR_OK;
+}
+
+// The blend's arguments of a binned view (left in c.ra).
+static void fwd_render_args(const FwdModel& m, FwdCam& c, const uint32_t* point_list,
+                            uint32_t* host_status) {
+  const ImgState& im = c.im;
+  RenderArgs& ra = c.ra;
+  ra.W = c.W; ra.H = c.H; ra.gx = c.gx; ra.gy = c.gy;
+  ra.ranges = im.ranges; ra.point_list = point_list; ra.rec = c.g.rec; ra.P = (uint32_t)m.P;
+  ra.bg = m.background;
+  ra.final_T = im.final_T; ra.n_contrib = im.n_contrib; ra.tile_last = im.tile_last;
+  ra.out_color = c.out_color; ra.out_depth = c.out_depth; ra.out_alpha = c.out_alpha;
+  ra.out_feature = c.out_feature; ra.include_feature = m.include_feature;
+  ra.order = im.order; ra.sched = tile_schedule_mode();
+  ra.status = im.status; ra.host_status = host_status; ra.fault = forward_faults_word();
 }
 
 // Phase 2a: wait for the read-back (the one host synchronisation of a view, as
@@ -564,23 +627,9 @@ static int fwd_bin(const FwdModel& m, FwdCam& c) {
                             std::chrono::steady_clock::now() - t0).count(),
                         std::memory_order_relaxed);
   }
-  uint32_t* host = c.host;
-  const uint32_t R = host[1];       // instances binned: tiles that pass the exact cull
-  const uint32_t R_ref = host[2];   // the reference's num_rendered (full rectangles), R <= R_ref
-  if (m.prefiltered && host[0]) return fail(GSR_ERR_PREFILTERED,
-                           "Point is filtered although prefiltered is set. This shouldn't happen!");
-  if (R_ref > 0x7fffffffu || R > R_ref)
-    return fail(GSR_ERR_TOO_LARGE, "num_rendered = %u exceeds the sort capacity", R_ref);
-  if (debug) {
-    GSR_CHECK(hipMemcpyAsync(host + 2, g.sort.aux + kSortAuxErr, 4, hipMemcpyDeviceToHost, stream));
-    GSR_CHECK(hipStreamSynchronize(stream));
-    if (host[2]) return fail(GSR_ERR_HIP, "depth sort look-back timed out");
-  }
-
-  const size_t bbytes = carve_bin(nullptr, R_ref, m.rows).bytes;
-  c.bbase = (char*)c.alloc(c.alloc_ctx, bbytes, GSR_BUF_BINNING);
-  if (!c.bbase) return fail(GSR_ERR_ALLOC, "binning buffer allocation of %zu bytes failed", bbytes);
-  BinState b = carve_bin(c.bbase, R_ref, m.rows);  // capacity R_ref, the first R entries used
+  if (int rc = fwd_bin_alloc(m, c)) return rc;
+  const uint32_t R = (uint32_t)c.num_instances;
+  const BinState& b = c.b;
 
   PROF_BEGIN(DUPLICATE);
   // the duplicate grid also zeroes the tile sort's scratch and the tile ranges
@@ -596,6 +645,7 @@ static int fwd_bin(const FwdModel& m, FwdCam& c) {
                              stream, false, /*precleared=*/true));
   PROF_END(TILE_SORT);
   if (debug) {
+    uint32_t* host = c.host;
     GSR_CHECK(hipMemcpyAsync(host + 2, b.sort.aux + kSortAuxErr, 4, hipMemcpyDeviceToHost, stream));
     GSR_CHECK(hipStreamSynchronize(stream));
     if (host[2]) return fail(GSR_ERR_HIP, "tile sort look-back timed out");
@@ -615,18 +665,8 @@ static int fwd_bin(const FwdModel& m, FwdCam& c) {
                                forward_faults_word(), stream, /*ranges_cleared=*/true));
   PROF_END(RANGES);
 
-  RenderArgs& ra = c.ra;
-  ra.W = c.W; ra.H = c.H; ra.gx = c.gx; ra.gy = c.gy;
-  ra.ranges = im.ranges; ra.point_list = point_list; ra.rec = g.rec; ra.P = (uint32_t)P;
-  ra.bg = m.background;
-  ra.final_T = im.final_T; ra.n_contrib = im.n_contrib; ra.tile_last = im.tile_last;
-  ra.out_color = c.out_color; ra.out_depth = c.out_depth; ra.out_alpha = c.out_alpha;
-  ra.out_feature = c.out_feature; ra.include_feature = m.include_feature;
-  ra.order = im.order; ra.sched = tile_schedule_mode();
-  ra.status = im.status; ra.host_status = host_status; ra.fault = forward_faults_word();
+  fwd_render_args(m, c, point_list, host_status);
   c.mail_slot = mail_slot;
-  c.num_rendered = (int)R_ref;
-  c.num_instances = (int)R;
   return GSR_OK;
 }
 
@@ -1046,6 +1086,247 @@ hipEvent_t join_event(int i) {
     ev[dev][i] = nullptr;
   return ev[dev][i];
 }
+
+// The batched path's preprocess: one multi-view launch (default) or one launch per view
+// (GSR_PRE_VIEWS=0).
+bool pre_views() {
+  static const bool on = [] {
+    const char* e = getenv("GSR_PRE_VIEWS");
+    return e ? atoi(e) != 0 : true;
+  }();
+  return on;
+}
+
+// Coherent, device-mapped pinned words (4 per view) that the batched sums store each view's
+// read-back into: no copy launch, one event per group.
+uint32_t* batch_slot(int i, uint32_t** dev_ptr) {
+  constexpr int kMaxDev = 64;
+  thread_local uint32_t* host[kMaxDev] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return nullptr;
+  if (!host[dev]) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, 16 * kFwdSlots, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess)
+      return nullptr;
+    host[dev] = (uint32_t*)p;
+  }
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, host[dev] + 4 * i, 0) != hipSuccess) return nullptr;
+  *dev_ptr = (uint32_t*)d;
+  return host[dev] + 4 * i;
+}
+
+// debug builds of the batched path: a sort's look-back error word, synchronously
+int check_sort_err(const uint32_t* err, hipStream_t stream, const char* what) {
+  const int debug = 1;
+  uint32_t v = 0;
+  GSR_CHECK(hipMemcpyAsync(&v, err, 4, hipMemcpyDeviceToHost, stream));
+  GSR_CHECK(hipStreamSynchronize(stream));
+  if (v) return fail(GSR_ERR_HIP, "%s look-back timed out", what);
+  return GSR_OK;
+}
+
+// Batched binning (GSR_VIEWS_BATCHED, default 1).  The views are split into `ng` groups, group g
+// on the g-th distinct view stream; inside a group every stage after the per-view preprocess is
+// ONE launch for all the group's views -- the instance-count sums (which also store the read-back
+// into pinned words), each depth-sort pass, the scan, the duplication, each tile-sort pass, the
+// ranges, the schedules and the blend.  A view's binning alone is a chain of ~14 small launches
+// whose latency, not HBM, sets its time (0.20 ms per view at 1 stream); batched, each launch is as
+// wide as the group.  Every kernel sees exactly its one-view arguments (own totals, tickets,
+// look-back words), so the results are bit-identical to the per-view path.  The host waits once
+// per group, for its read-back, while the group's depth sort and scan run; group g's blend then
+// overlaps group g + 1's binning on the other stream.
+int views_forward_batched(const FwdModel& m, std::vector<FwdCam>& cams, gsr_view* views,
+                          hipStream_t call_stream, int ng) {
+  const int V = (int)cams.size();
+  const int debug = m.debug;
+  if (V == 0) return GSR_OK;
+  std::vector<hipStream_t> distinct;
+  for (const FwdCam& c : cams)
+    if (std::find(distinct.begin(), distinct.end(), c.stream) == distinct.end())
+      distinct.push_back(c.stream);
+  if (ng < 1) ng = 1;
+  int per = (V + ng - 1) / ng;
+  if (per > kMaxBatchViews) per = kMaxBatchViews;
+  ng = (V + per - 1) / per;
+  struct Group {
+    int v0 = 0, n = 0;
+    hipStream_t st = nullptr;
+    hipEvent_t ready = nullptr;
+    std::vector<int> live;  // views with P > 0
+    bool depth_in_b = false;
+  };
+  std::vector<Group> grp((size_t)ng);
+  const int P = m.P;
+  const size_t pre_blocks = ((size_t)P + 255) / 256;
+  // phase 1 of a group: preprocess per view, then one launch per stage for the group
+  auto phase1 = [&](int gi) -> int {
+    Group& G = grp[(size_t)gi];
+    G.v0 = gi * per;
+    G.n = V - G.v0 < per ? V - G.v0 : per;
+    G.st = distinct[(size_t)gi % distinct.size()];
+    G.ready = readback_event(gi);
+    if (!G.ready) return fail(GSR_ERR_HIP, "event creation failed");
+    hipStream_t stream = G.st;
+    SumSpec sums[kMaxBatchViews];
+    SortSpec ds[kMaxBatchViews];
+    PreArgs pas[kMaxBatchViews];
+    for (int k = 0; k < G.n; k++) {
+      const int v = G.v0 + k;
+      FwdCam& c = cams[(size_t)v];
+      c.stream = G.st;
+      c.host = batch_slot(v, &c.host_dev);
+      if (!c.host) return fail(GSR_ERR_HIP, "pinned read-back slot unavailable");
+      c.ready = G.ready;
+      c.defer_pre = true;
+      if (int rc = fwd_prep(m, c)) return rc;
+      if (c.done) continue;
+      const GeomState& g = c.g;
+      const int l = (int)G.live.size();
+      pas[l] = c.pa;
+      sums[l] = SumSpec{g.pre_parts, g.pre_parts + pre_blocks, pre_blocks, g.flags + 1, c.host_dev,
+                        m.prefiltered ? g.flags : nullptr};
+      ds[l] = SortSpec{g.dkey_a, g.dval_a, g.dkey_b, g.dval_b, (size_t)P, g.sort, g.tiles_touched};
+      G.live.push_back(v);
+    }
+    const int nl = (int)G.live.size();
+    if (nl == 0) return GSR_OK;
+    PROF_BEGIN(PREPROCESS);
+    if (pre_views()) {
+      GSR_CHECK(launch_preprocess_views(pas, nl, stream));
+    } else {
+      for (int l = 0; l < nl; l++) GSR_CHECK(launch_preprocess(pas[l], stream));
+    }
+    PROF_END(PREPROCESS);
+    GSR_CHECK(sum_u32_parts_views(sums, nl, stream));
+    GSR_CHECK(hipEventRecord(G.ready, stream));
+    PROF_BEGIN(DEPTH_SORT);
+    GSR_CHECK(radix_sort_pairs_views(ds, nl, 32, &G.depth_in_b, stream, /*sentinel_anywhere=*/true,
+                                     /*precleared=*/true));
+    PROF_END(DEPTH_SORT);
+    ScanSpec sc[kMaxBatchViews];
+    for (int l = 0; l < nl; l++) {
+      FwdCam& c = cams[(size_t)G.live[(size_t)l]];
+      c.depth_in_b = G.depth_in_b;
+      sc[l] = ScanSpec{G.depth_in_b ? c.g.dkey_b : c.g.dkey_a, c.g.offsets, (size_t)P,
+                       c.g.scan_parts};
+    }
+    PROF_BEGIN(SCAN);
+    GSR_CHECK(scan_u32_views(sc, nl, true, stream));
+    PROF_END(SCAN);
+    return GSR_OK;
+  };
+  // phase 2 of a group: its read-back, then its binning and blend
+  auto phase2 = [&](int gi) -> int {
+    Group& G = grp[(size_t)gi];
+    hipStream_t stream = G.st;
+    const int nl = (int)G.live.size();
+    if (nl > 0) {
+      {
+        const auto t0 = std::chrono::steady_clock::now();
+        GSR_CHECK(hipEventSynchronize(G.ready));
+        g_wait_ns.fetch_add((long long)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                std::chrono::steady_clock::now() - t0).count(),
+                            std::memory_order_relaxed);
+      }
+      DupSpec dup[kMaxBatchViews];
+      SortSpec ts[kMaxBatchViews];
+      const uint32_t ntiles = cams[(size_t)G.live[0]].gx * cams[(size_t)G.live[0]].gy;
+      const int tbits = tile_bits(ntiles);
+      for (int l = 0; l < nl; l++) {
+        FwdCam& c = cams[(size_t)G.live[(size_t)l]];
+        if (int rc = fwd_bin_alloc(m, c)) return rc;  // (debug: checks the depth sort)
+        const GeomState& g = c.g;
+        const BinState& b = c.b;
+        const uint32_t R = (uint32_t)c.num_instances;
+        dup[l] = DupSpec{P, G.depth_in_b ? g.dval_b : g.dval_a, g.offsets, g.rec, c.gx, c.gy,
+                         b.tkey_a, b.tval_a, R,
+                         SideClear{b.sort.aux, sort_clear_bytes(b.sort, R, tbits)},
+                         SideClear{c.im.ranges, sizeof(uint2) * ntiles},
+                         m.rows ? b.egid : nullptr, m.rows ? g.ebeg : nullptr};
+        ts[l] = SortSpec{b.tkey_a, b.tval_a, b.tkey_b, b.tval_b, (size_t)R, b.sort, nullptr};
+      }
+      PROF_BEGIN(DUPLICATE);
+      GSR_CHECK(launch_duplicate_views(dup, nl, stream));
+      PROF_END(DUPLICATE);
+      bool t_in_b = false;
+      PROF_BEGIN(TILE_SORT);
+      GSR_CHECK(radix_sort_pairs_views(ts, nl, tbits, &t_in_b, stream, false, /*precleared=*/true));
+      PROF_END(TILE_SORT);
+      RangesSpec rs[kMaxBatchViews];
+      RenderArgs ras[kMaxBatchViews];
+      for (int l = 0; l < nl; l++) {
+        FwdCam& c = cams[(size_t)G.live[(size_t)l]];
+        const BinState& b = c.b;
+        const uint32_t R = (uint32_t)c.num_instances;
+        if (debug)
+          if (int rc = check_sort_err(b.sort.aux + kSortAuxErr, stream, "tile sort")) return rc;
+        const uint32_t* tiles_sorted = t_in_b ? b.tkey_b : b.tkey_a;
+        const uint32_t* point_list = t_in_b ? b.tval_b : b.tval_a;
+        if (m.rows) {
+          uint32_t* pl = t_in_b ? b.tval_a : b.tval_b;
+          GSR_CHECK(launch_det_gather(R, point_list, b.egid, pl, stream));
+          point_list = pl;
+        }
+        int mail_slot = -1;
+        uint32_t* host_status = mail_post(c.ibase, &mail_slot);
+        rs[l] = RangesSpec{R, tiles_sorted, c.im.ranges, ntiles, c.g.sort.aux + kSortAuxErr,
+                           b.sort.aux + kSortAuxErr, c.im.status, host_status,
+                           forward_faults_word()};
+        fwd_render_args(m, c, point_list, host_status);
+        c.mail_slot = mail_slot;
+        ras[l] = c.ra;
+      }
+      PROF_BEGIN(RANGES);
+      GSR_CHECK(launch_tile_ranges_views(rs, nl, stream));
+      GSR_CHECK(launch_render_schedule_views(ras, nl, stream));
+      PROF_END(RANGES);
+      PROF_BEGIN(RENDER_FWD);
+      GSR_CHECK(launch_render_forward_views(ras, nl, stream));
+      PROF_END(RENDER_FWD);
+    }
+    for (int k = 0; k < G.n; k++) {
+      const int v = G.v0 + k;
+      FwdCam& c = cams[(size_t)v];
+      if (c.done) c.num_rendered = c.num_instances = 0;
+      if (int rc = fwd_blended(m, c, stream)) return rc;
+      gsr_view& out = views[v];
+      out.geom_buffer = c.gbase; out.binning_buffer = c.bbase; out.image_buffer = c.ibase;
+      out.num_rendered = c.num_rendered; out.num_instances = c.num_instances;
+    }
+    if (G.st != call_stream) {
+      hipEvent_t e = join_event(gi);
+      if (!e || hipEventRecord(e, G.st) != hipSuccess ||
+          hipStreamWaitEvent(call_stream, e, 0) != hipSuccess)
+        return fail(GSR_ERR_HIP, "joining group %d's stream failed", gi);
+    }
+    return GSR_OK;
+  };
+  // `lead` groups' first phases are queued ahead of the first wait; each later group's right
+  // after the phase 2 of the group `lead` before it (GSR_VIEWS_LEAD, default all groups at once)
+  static const int lead_env = [] {
+    const char* e = getenv("GSR_VIEWS_LEAD");
+    return e ? atoi(e) : 0;
+  }();
+  const int lead = (lead_env < 1 || lead_env > ng) ? ng : lead_env;
+  for (int gi = 0; gi < lead; gi++)
+    if (int rc = phase1(gi)) return rc;
+  for (int gi = 0; gi < ng; gi++) {
+    if (int rc = phase2(gi)) return rc;
+    if (gi + lead < ng)
+      if (int rc = phase1(gi + lead)) return rc;
+  }
+  g_last_instances = cams[(size_t)V - 1].num_instances;
+  return GSR_OK;
+}
+
+bool views_batched() {
+  static const bool on = [] {
+    const char* e = getenv("GSR_VIEWS_BATCHED");
+    return e ? atoi(e) != 0 : true;
+  }();
+  return on;
+}
 }  // namespace
 
 int gsr_rasterize_views_fused(int V, gsr_view* views, int image_height, int image_width, int P,
@@ -1108,6 +1389,7 @@ int gsr_rasterize_views_fused(int V, gsr_view* views, int image_height, int imag
   }();
   (void)inflight;  // one view in flight per distinct view stream
   const int ng = groups_env < 1 ? 1 : groups_env;
+  if (views_batched()) return views_forward_batched(m, cams, views, call_stream, ng);
   int per = (V + ng - 1) / ng;
   if (per < 1) per = 1;
   if (per > kMaxFwdViews) per = kMaxFwdViews;

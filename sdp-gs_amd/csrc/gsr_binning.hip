@@ -21,20 +21,19 @@ constexpr int kThreads = 256;
 
 // One lane per depth-sorted Gaussian; the lane writes its tile ids row-major over its tile
 // rectangle (the reference's emission order inside one Gaussian, rasterizer_impl.cu:98-109).
-__global__ __launch_bounds__(kThreads) void duplicate_kernel(int P,
-                                                             const uint32_t* __restrict__ order,
-                                                             const uint32_t* __restrict__ offsets,
-                                                             const int32_t* __restrict__ radii,
-                                                             const float4* __restrict__ rec,
-                                                             uint32_t gx, uint32_t gy,
-                                                             uint32_t* __restrict__ tkey,
-                                                             uint32_t* __restrict__ tval,
-                                                             uint32_t R, SideClear clear0,
-                                                             SideClear clear1,
-                                                             uint32_t* __restrict__ egid,
-                                                             uint32_t* __restrict__ ebeg) {
-  const int s = (int)(blockIdx.x * kThreads + threadIdx.x);
-  const size_t nth = (size_t)gridDim.x * kThreads;
+// (body shared by the one-view kernel and the several-views kernel: blk / nblk = this
+// workgroup's index and the workgroup count of its view)
+__device__ __forceinline__ void duplicate_body(int P, const uint32_t* __restrict__ order,
+                                               const uint32_t* __restrict__ offsets,
+                                               const float4* __restrict__ rec, uint32_t gx,
+                                               uint32_t gy, uint32_t* __restrict__ tkey,
+                                               uint32_t* __restrict__ tval, uint32_t R,
+                                               SideClear clear0, SideClear clear1,
+                                               uint32_t* __restrict__ egid,
+                                               uint32_t* __restrict__ ebeg, uint32_t blk,
+                                               uint32_t nblk) {
+  const int s = (int)(blk * kThreads + threadIdx.x);
+  const size_t nth = (size_t)nblk * kThreads;
   side_clear(clear0.p, clear0.bytes, (size_t)s, nth);
   side_clear(clear1.p, clear1.bytes, (size_t)s, nth);
   if (s >= P) return;
@@ -70,16 +69,29 @@ __global__ __launch_bounds__(kThreads) void duplicate_kernel(int P,
   }
 }
 
-__global__ __launch_bounds__(kThreads) void tile_ranges_kernel(size_t R,
-                                                               const uint32_t* __restrict__ tiles,
-                                                               uint2* __restrict__ ranges,
-                                                               uint32_t ntiles,
-                                                               const uint32_t* __restrict__ derr,
-                                                               const uint32_t* __restrict__ terr,
-                                                               uint32_t* __restrict__ status,
-                                                               uint32_t* host_status,
-                                                               uint32_t* fault) {
-  const size_t idx = (size_t)blockIdx.x * kThreads + threadIdx.x;
+__global__ __launch_bounds__(kThreads) void duplicate_kernel(int P,
+                                                             const uint32_t* __restrict__ order,
+                                                             const uint32_t* __restrict__ offsets,
+                                                             const float4* __restrict__ rec,
+                                                             uint32_t gx, uint32_t gy,
+                                                             uint32_t* __restrict__ tkey,
+                                                             uint32_t* __restrict__ tval,
+                                                             uint32_t R, SideClear clear0,
+                                                             SideClear clear1,
+                                                             uint32_t* __restrict__ egid,
+                                                             uint32_t* __restrict__ ebeg) {
+  duplicate_body(P, order, offsets, rec, gx, gy, tkey, tval, R, clear0, clear1, egid, ebeg,
+                 blockIdx.x, gridDim.x);
+}
+
+__device__ __forceinline__ void tile_ranges_body(size_t R, const uint32_t* __restrict__ tiles,
+                                                 uint2* __restrict__ ranges, uint32_t ntiles,
+                                                 const uint32_t* __restrict__ derr,
+                                                 const uint32_t* __restrict__ terr,
+                                                 uint32_t* __restrict__ status,
+                                                 uint32_t* host_status, uint32_t* fault,
+                                                 uint32_t blk) {
+  const size_t idx = (size_t)blk * kThreads + threadIdx.x;
   if (idx >= (R ? R : 1)) return;
   // the call's status: both sorts have finished (stream order); a timed-out look-back of either
   // fails this call (render_fwd poisons the outputs, the backward the gradients)
@@ -107,6 +119,50 @@ __global__ __launch_bounds__(kThreads) void tile_ranges_kernel(size_t R,
   if (idx == R - 1 && cur_ok) ranges[cur].y = (uint32_t)R;
 }
 
+__global__ __launch_bounds__(kThreads) void tile_ranges_kernel(size_t R,
+                                                               const uint32_t* __restrict__ tiles,
+                                                               uint2* __restrict__ ranges,
+                                                               uint32_t ntiles,
+                                                               const uint32_t* __restrict__ derr,
+                                                               const uint32_t* __restrict__ terr,
+                                                               uint32_t* __restrict__ status,
+                                                               uint32_t* host_status,
+                                                               uint32_t* fault) {
+  tile_ranges_body(R, tiles, ranges, ntiles, derr, terr, status, host_status, fault, blockIdx.x);
+}
+
+// ---- several views per launch (the multi-view forward's batched binning, gsr_api.cpp) ----------
+struct DupViews {
+  DupSpec j[kMaxBatchViews];
+  uint32_t first[kMaxBatchViews + 1];
+  int V;
+};
+struct RangesViews {
+  RangesSpec j[kMaxBatchViews];
+  uint32_t first[kMaxBatchViews + 1];
+  int V;
+};
+
+__device__ __forceinline__ int batch_view(const uint32_t* first, int V, uint32_t b) {
+  int k = 0;
+  while (k + 1 < V && b >= first[k + 1]) k++;
+  return k;
+}
+
+__global__ __launch_bounds__(kThreads) void duplicate_views_kernel(DupViews m) {
+  const int k = batch_view(m.first, m.V, blockIdx.x);
+  const DupSpec& j = m.j[k];
+  duplicate_body(j.P, j.order, j.offsets, j.rec, j.gx, j.gy, j.tkey, j.tval, j.R, j.clear0,
+                 j.clear1, j.egid, j.ebeg, blockIdx.x - m.first[k], m.first[k + 1] - m.first[k]);
+}
+
+__global__ __launch_bounds__(kThreads) void tile_ranges_views_kernel(RangesViews m) {
+  const int k = batch_view(m.first, m.V, blockIdx.x);
+  const RangesSpec& j = m.j[k];
+  tile_ranges_body(j.R, j.tiles, j.ranges, j.ntiles, j.depth_err, j.tile_err, j.status,
+                   j.host_status, j.fault, blockIdx.x - m.first[k]);
+}
+
 __global__ __launch_bounds__(kThreads) void det_gather_kernel(size_t R,
                                                               const uint32_t* __restrict__ einst,
                                                               const uint32_t* __restrict__ egid,
@@ -131,8 +187,38 @@ hipError_t launch_duplicate(int P, const uint32_t* order, const uint32_t* offset
                             SideClear clear1, hipStream_t s, uint32_t* egid, uint32_t* ebeg) {
   if (P == 0) return hipSuccess;
   hipLaunchKernelGGL(duplicate_kernel, dim3((P + kThreads - 1) / kThreads), dim3(kThreads), 0, s,
-                     P, order, offsets, radii, rec, gx, gy, tkey, tval, R, clear0, clear1, egid,
-                     ebeg);
+                     P, order, offsets, rec, gx, gy, tkey, tval, R, clear0, clear1, egid, ebeg);
+  return hipGetLastError();
+}
+
+hipError_t launch_duplicate_views(const DupSpec* v, int V, hipStream_t s) {
+  if (V <= 0) return hipSuccess;
+  if (V > kMaxBatchViews) return hipErrorInvalidValue;
+  DupViews m{};
+  m.V = V;
+  m.first[0] = 0;
+  for (int k = 0; k < V; k++) {
+    m.j[k] = v[k];
+    m.first[k + 1] = m.first[k] + (uint32_t)((v[k].P + kThreads - 1) / kThreads);
+  }
+  if (m.first[V] == 0) return hipSuccess;
+  hipLaunchKernelGGL(duplicate_views_kernel, dim3(m.first[V]), dim3(kThreads), 0, s, m);
+  return hipGetLastError();
+}
+
+hipError_t launch_tile_ranges_views(const RangesSpec* v, int V, hipStream_t s) {
+  if (V <= 0) return hipSuccess;
+  if (V > kMaxBatchViews) return hipErrorInvalidValue;
+  RangesViews m{};
+  m.V = V;
+  m.first[0] = 0;
+  for (int k = 0; k < V; k++) {
+    m.j[k] = v[k];
+    if (!v[k].R) m.j[k].tile_err = nullptr;  // no instances: nothing tile-sorted
+    const size_t n = v[k].R ? v[k].R : 1;  // R == 0: one lane still publishes the status
+    m.first[k + 1] = m.first[k] + (uint32_t)((n + kThreads - 1) / kThreads);
+  }
+  hipLaunchKernelGGL(tile_ranges_views_kernel, dim3(m.first[V]), dim3(kThreads), 0, s, m);
   return hipGetLastError();
 }
 

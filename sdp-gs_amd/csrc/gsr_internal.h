@@ -129,6 +129,38 @@ hipError_t radix_sort_pairs(uint32_t* ka, uint32_t* va, uint32_t* kb, uint32_t* 
                             int bits, SortScratch scratch, bool* result_in_b, hipStream_t s,
                             bool sentinel_anywhere = false, bool precleared = false,
                             const uint32_t* key_payload = nullptr);
+// Several independent sorts / scans / sums, one launch per stage for all of them (the multi-view
+// forward's batched binning, gsr_api.cpp): a view's workgroups are a contiguous block range of
+// the launch, and inside it everything is the one-view kernel's (own totals, tickets, look-back
+// words), so each result is bit-identical to its own radix_sort_pairs / scan_u32 / sum_u32_parts.
+// The sorts ping-pong alike: *result_in_b holds for every view.
+constexpr int kMaxBatchViews = 8;
+struct SortSpec {
+  uint32_t *ka, *va, *kb, *vb;
+  size_t n;
+  SortScratch scratch;
+  const uint32_t* key_payload;
+};
+hipError_t radix_sort_pairs_views(const SortSpec* v, int V, int bits, bool* result_in_b,
+                                  hipStream_t s, bool sentinel_anywhere, bool precleared);
+struct ScanSpec {
+  const uint32_t* in;
+  uint32_t* out;
+  size_t n;
+  uint32_t* parts;
+};
+hipError_t scan_u32_views(const ScanSpec* v, int V, bool inclusive, hipStream_t s);
+// out[0..1] = sums of parts / parts2 (n partials each); host (device pointer of pinned words, or
+// null) receives {*flag0 (0 if null), out[0], out[1]}.
+struct SumSpec {
+  const uint32_t* parts;
+  const uint32_t* parts2;
+  size_t n;
+  uint32_t* out;
+  uint32_t* host;
+  const uint32_t* flag0;
+};
+hipError_t sum_u32_parts_views(const SumSpec* v, int V, hipStream_t s);
 // Device word counting look-back timeouts of any sort on the current device (sticky until the
 // host resets it); every forward reads it back with its instance count.
 uint32_t* sort_timeouts_word();
@@ -176,7 +208,7 @@ struct BinState {
   size_t bytes;
 };
 BinState carve_bin(char* base, size_t R, bool rows = false);
-// Backward gradient path (process-wide, env GSR_BWD_ROWS, default 1): true = the backward blend
+// Backward gradient path (process-wide, env GSR_BWD_ROWS, default 0): true = the backward blend
 // stores one 64-B gradient row per (splat, tile) instance (plain coalesced stores, no global float
 // atomics) and the backward preprocess sums each Gaussian's rows (contiguous in emission order);
 // false = float atomics into one accumulator row per Gaussian.  The deterministic backward always
@@ -229,6 +261,14 @@ struct PreArgs {
   const uint8_t* pre_clamp;
 };
 hipError_t launch_preprocess(const PreArgs& a, hipStream_t s);
+// Several views of one model in one launch (every view's PreArgs share the model fields): per
+// view the outputs of launch_preprocess, bit for bit.
+struct PreViews {
+  PreArgs v[kMaxBatchViews];
+  int V;
+};
+static_assert(sizeof(PreViews) <= 4096, "kernel argument size");
+hipError_t launch_preprocess_views(const PreArgs* views, int V, hipStream_t s);
 struct PrecolorArgs {
   int P, M, D, nviews;
   const float *means3D, *sh_dc, *sh_rest;
@@ -319,6 +359,34 @@ hipError_t launch_tile_ranges(size_t R, const uint32_t* sorted_tiles, uint2* ran
                               uint32_t ntiles, const uint32_t* depth_err, const uint32_t* tile_err,
                               uint32_t* status, uint32_t* host_status, uint32_t* fault,
                               hipStream_t s, bool ranges_cleared = false);
+// The same two stages for several views in one launch each (the batched binning; ranges must be
+// cleared already, by the duplicate's side clear).
+struct DupSpec {
+  int P;
+  const uint32_t* order;
+  const uint32_t* offsets;
+  const float4* rec;
+  uint32_t gx, gy;
+  uint32_t* tkey;
+  uint32_t* tval;
+  uint32_t R;
+  SideClear clear0, clear1;
+  uint32_t* egid;
+  uint32_t* ebeg;
+};
+hipError_t launch_duplicate_views(const DupSpec* v, int V, hipStream_t s);
+struct RangesSpec {
+  size_t R;
+  const uint32_t* tiles;
+  uint2* ranges;
+  uint32_t ntiles;
+  const uint32_t* depth_err;
+  const uint32_t* tile_err;
+  uint32_t* status;
+  uint32_t* host_status;
+  uint32_t* fault;
+};
+hipError_t launch_tile_ranges_views(const RangesSpec* v, int V, hipStream_t s);
 
 // ---- blend (gsr_render.hip) ----------------------------------------------------------------------
 struct RenderArgs {
@@ -350,6 +418,8 @@ struct RenderFwdViews {
   int V;
 };
 hipError_t launch_render_schedule(const RenderArgs& a, hipStream_t s);
+// the schedules of several views' tiles, one workgroup per view (views with sched != 2 skipped)
+hipError_t launch_render_schedule_views(const RenderArgs* views, int V, hipStream_t s);
 hipError_t launch_render_forward_views(const RenderArgs* views, int V, hipStream_t s);
 
 struct RenderBwdArgs {

@@ -21,35 +21,67 @@ namespace gsr {
 namespace {
 
 constexpr int kThreads = 256;
-#ifndef GSR_PRE_HOIST
-#define GSR_PRE_HOIST 0
-#endif
 
-// One Gaussian; returns its exact tile count (0 when culled), sets rect_tiles to the tile count of
-// its full 3-sigma rectangle (the reference's tiles_touched, forward.cu:255; 0 when culled) and
-// writes its splat record to rec[0..3] (the workgroup's LDS staging row; all zero when culled:
-// such a record is never read).
-// pm / ps / pl: this Gaussian's 3 floats of means3D / scales / sh_language (LDS-staged rows with
-// GSR_PRE_STAGE, else the global rows; ps / pl are only read when the arrays are in use)
+// The view-independent inputs of one Gaussian: its mean, 3D covariance (precomputed, or from
+// the activated scale / rotation), effective opacity and language feature.  The single-view kernel
+// evaluates them per view; the multi-view kernel once per Gaussian for all its views (the same
+// functions on the same inputs: bit-identical).
+struct PreModelIn {
+  V3 p_orig;
+  float c3[6];
+  float op, f0, f1, f2;
+};
+__device__ __forceinline__ void pre_model_in(const PreArgs& a, int idx, const float* pm,
+                                             const float* ps, const float* pl, PreModelIn& o) {
+  o.p_orig = v3(pm[0], pm[1], pm[2]);
+  if (a.cov3D_precomp) {
+#pragma unroll
+    for (int k = 0; k < 6; k++) o.c3[k] = a.cov3D_precomp[6 * (size_t)idx + k];
+  } else {
+    float4 q = reinterpret_cast<const float4*>(a.rotations)[idx];
+    float sx = ps[0], sy = ps[1], sz = ps[2];
+    if (a.fused) {  // GaussianModel activations: exp(_scaling), normalize(_rotation)
+      sx = expf(sx); sy = expf(sy); sz = expf(sz);
+      q = normalize_quat(q);
+    }
+    // not stored: the backward recomputes it bit-identically from the same inputs
+    cov3d_from_scale_rot(sx, sy, sz, a.scale_modifier, q.x, q.y, q.z, q.w, o.c3);
+  }
+  float op = a.opacities[idx];
+  if (a.fused) op = sigmoid_f(op);  // GaussianModel.get_opacity
+  if (a.confidence) op = op * a.confidence[idx];
+  o.op = op;
+  o.f0 = o.f1 = o.f2 = 0.f;
+  if (a.include_feature) {
+    if (a.lang_precomp) {
+      o.f0 = a.lang_precomp[3 * idx]; o.f1 = a.lang_precomp[3 * idx + 1];
+      o.f2 = a.lang_precomp[3 * idx + 2];
+    } else if (a.sh_language) {
+      const float u0 = SH_C0 * pl[0];
+      const float u1 = SH_C0 * pl[1];
+      const float u2 = SH_C0 * pl[2];
+      const float n = sqrtf(u0 * u0 + u1 * u1 + u2 * u2);
+      const float den = n + 1e-9f;
+      o.f0 = u0 / den; o.f1 = u1 / den; o.f2 = u2 / den;
+    }
+  }
+}
+
+// One Gaussian in the view of `a`; returns its exact tile count (0 when culled), sets rect_tiles
+// to the tile count of its full 3-sigma rectangle (the reference's tiles_touched, forward.cu:255;
+// 0 when culled) and writes its splat record to rec[0..3] (the workgroup's LDS staging row; all
+// zero when culled: such a record is never read).
+// pm / ps / pl: this Gaussian's 3 floats of means3D / scales / sh_language.  in: its
+// view-independent inputs if already evaluated (multi-view kernel), else null (evaluated here,
+// after the near-plane test).
 __device__ __forceinline__ uint32_t preprocess_gaussian(const PreArgs& a, int idx, float4* rec,
                                                         const float* pm, const float* ps,
-                                                        const float* pl, uint32_t& rect_tiles) {
+                                                        const float* pl, uint32_t& rect_tiles,
+                                                        const PreModelIn* in) {
 #pragma unroll
   for (int k = 0; k < 4; k++) rec[k] = make_float4(0.f, 0.f, 0.f, 0.f);
   rect_tiles = 0;
-#if GSR_PRE_HOIST
-  // the small per-Gaussian inputs are all put in flight before the first dependent computation
-  // (the compiler cannot hoist loads above the cull branches itself)
-  float4 q_in = make_float4(0.f, 0.f, 0.f, 0.f);
-  float s_in0 = 0.f, s_in1 = 0.f, s_in2 = 0.f;
-  if (!a.cov3D_precomp) {  // kernel-argument (uniform) test
-    q_in = reinterpret_cast<const float4*>(a.rotations)[idx];
-    s_in0 = ps[0]; s_in1 = ps[1]; s_in2 = ps[2];
-  }
-  const float op_in = a.opacities[idx];
-  const float conf_in = a.confidence ? a.confidence[idx] : 1.0f;
-#endif
-  const V3 p_orig = v3(pm[0], pm[1], pm[2]);
+  const V3 p_orig = in ? in->p_orig : v3(pm[0], pm[1], pm[2]);
   const V3 p_view = xform_point43(p_orig, a.view);
   // in_frustum: near-plane test only (auxiliary.h:154)
   const bool near_ok = !(p_view.z <= 0.2f);
@@ -66,27 +98,12 @@ __device__ __forceinline__ uint32_t preprocess_gaussian(const PreArgs& a, int id
   const float pw = 1.0f / (xform_w(p_orig, a.proj) + 0.0000001f);
   const float pproj_x = ph.x * pw, pproj_y = ph.y * pw;
 
-  float c3buf[6];  // always a register array (a pointer select would force it into scratch)
-  const float* c3 = c3buf;
-  if (a.cov3D_precomp) {
-#pragma unroll
-    for (int k = 0; k < 6; k++) c3buf[k] = a.cov3D_precomp[6 * (size_t)idx + k];
-  } else {
-#if GSR_PRE_HOIST
-    float4 q = q_in;
-    float sx = s_in0, sy = s_in1, sz = s_in2;
-#else
-    float4 q = reinterpret_cast<const float4*>(a.rotations)[idx];
-    float sx = ps[0], sy = ps[1], sz = ps[2];
-#endif
-    if (a.fused) {  // GaussianModel activations: exp(_scaling), normalize(_rotation)
-      sx = expf(sx); sy = expf(sy); sz = expf(sz);
-      q = normalize_quat(q);
-    }
-    // not stored: the backward recomputes it bit-identically from the same inputs
-    cov3d_from_scale_rot(sx, sy, sz, a.scale_modifier, q.x, q.y, q.z, q.w, c3buf);
+  PreModelIn own;
+  if (!in) {
+    pre_model_in(a, idx, pm, ps, pl, own);
+    in = &own;
   }
-  const Ewa e = ewa_project(p_orig, a.fx, a.fy, a.tanx, a.tany, c3, a.view);
+  const Ewa e = ewa_project(p_orig, a.fx, a.fy, a.tanx, a.tany, in->c3, a.view);
   const float det = (e.a * e.c - e.b * e.b);
   if (det == 0.0f) return 0;
   const float det_inv = 1.f / det;
@@ -121,28 +138,7 @@ __device__ __forceinline__ uint32_t preprocess_gaussian(const PreArgs& a, int id
     cg = a.colors_precomp[3 * idx + 1];
     cb = a.colors_precomp[3 * idx + 2];
   }
-#if GSR_PRE_HOIST
-  float op = op_in;
-  if (a.fused) op = sigmoid_f(op);  // GaussianModel.get_opacity
-  if (a.confidence) op = op * conf_in;
-#else
-  float op = a.opacities[idx];
-  if (a.fused) op = sigmoid_f(op);  // GaussianModel.get_opacity
-  if (a.confidence) op = op * a.confidence[idx];
-#endif
-  float f0 = 0.f, f1 = 0.f, f2 = 0.f;
-  if (a.include_feature) {
-    if (a.lang_precomp) {
-      f0 = a.lang_precomp[3 * idx]; f1 = a.lang_precomp[3 * idx + 1]; f2 = a.lang_precomp[3 * idx + 2];
-    } else if (a.sh_language) {
-      const float u0 = SH_C0 * pl[0];
-      const float u1 = SH_C0 * pl[1];
-      const float u2 = SH_C0 * pl[2];
-      const float n = sqrtf(u0 * u0 + u1 * u1 + u2 * u2);
-      const float den = n + 1e-9f;
-      f0 = u0 / den; f1 = u1 / den; f2 = u2 / den;
-    }
-  }
+  const float op = in->op;
   const float depth = p_view.z;
   a.radii[idx] = r;
   rect_tiles = (y1 - y0) * (x1 - x0);
@@ -165,8 +161,8 @@ __device__ __forceinline__ uint32_t preprocess_gaussian(const PreArgs& a, int id
   g.dkey_a[idx] = __float_as_uint(depth);
   rec[0] = make_float4(px, py, con_a, con_b);
   rec[1] = make_float4(con_c, op, depth, cr);
-  rec[2] = make_float4(cg, cb, f0, f1);
-  rec[3] = make_float4(f2, (float)r, qc, 0.f);
+  rec[2] = make_float4(cg, cb, in->f0, in->f1);
+  rec[3] = make_float4(in->f2, (float)r, qc, 0.f);
   return count;
 }
 
@@ -194,38 +190,16 @@ __device__ __forceinline__ void stage_rows3(const float* __restrict__ g, int n, 
 }
 constexpr int kRecStride = 5;  // float4s per LDS record row (4 + 1 pad)
 // (__launch_bounds__(256, 6), 80 VGPRs with a 12-byte spill, measured equal to the unbounded 82)
-__global__ __launch_bounds__(kThreads) void preprocess_kernel(PreArgs a) {
-  __shared__ float4 s_rec[kThreads * kRecStride];
-  const int base = (int)(blockIdx.x * kThreads);
-  const int idx = base + (int)threadIdx.x;
-  const int n = min(kThreads, a.P - base);
-  side_clear(a.clear.p, a.clear.bytes, (size_t)idx, (size_t)gridDim.x * kThreads);
-#if GSR_PRE_STAGE
-  // the [P,3] inputs (12-byte rows) enter as the workgroup's contiguous 3-KB segments in 16-byte
-  // loads instead of three 4-byte loads at a 12-byte lane stride; lane reads at a 3-dword LDS
-  // stride are bank-conflict free
-  __shared__ float s_m[3 * kThreads], s_s[3 * kThreads], s_l[3 * kThreads];
-  stage_rows3(a.means3D + 3 * (size_t)base, n, s_m);
-  const bool use_s = !a.cov3D_precomp, use_l = a.include_feature && !a.lang_precomp && a.sh_language;
-  if (use_s) stage_rows3(a.scales + 3 * (size_t)base, n, s_s);
-  if (use_l) stage_rows3(a.sh_language + 3 * (size_t)base, n, s_l);
-  __syncthreads();
-  const float* pm = s_m + 3 * threadIdx.x;
-  const float* ps = s_s + 3 * threadIdx.x;
-  const float* pl = s_l + 3 * threadIdx.x;
-#else
-  const float* pm = a.means3D + 3 * (size_t)idx;
-  const float* ps = a.scales + 3 * (size_t)idx;
-  const float* pl = a.sh_language + 3 * (size_t)idx;
-#endif
-  uint32_t rect = 0;
-  uint32_t count = idx < a.P ? preprocess_gaussian(a, idx, s_rec + threadIdx.x * kRecStride, pm, ps, pl, rect) : 0u;
+// The workgroup's outputs after its lanes' preprocess_gaussian: the records (from LDS), the
+// zeroed accumulator rows and the partial sums of the tile counts.
+__device__ __forceinline__ void pre_epilogue(const PreArgs& a, int base, int n, uint32_t count,
+                                             uint32_t rect, const float4* s_rec,
+                                             uint32_t* s_sum, uint32_t* s_rect) {
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) {
     count += (uint32_t)__shfl_xor((int)count, d, 64);
     rect += (uint32_t)__shfl_xor((int)rect, d, 64);
   }
-  __shared__ uint32_t s_sum[kThreads / 64], s_rect[kThreads / 64];
   if ((threadIdx.x & 63) == 0) {
     s_sum[threadIdx.x >> 6] = count;
     s_rect[threadIdx.x >> 6] = rect;
@@ -250,6 +224,69 @@ __global__ __launch_bounds__(kThreads) void preprocess_kernel(PreArgs a) {
     }
     a.parts[blockIdx.x] = t;
     a.parts[gridDim.x + blockIdx.x] = tr;
+  }
+}
+
+// (__launch_bounds__(256, 6), 80 VGPRs with a 12-byte spill, measured equal to the unbounded 82)
+__global__ __launch_bounds__(kThreads) void preprocess_kernel(PreArgs a) {
+  __shared__ float4 s_rec[kThreads * kRecStride];
+  __shared__ uint32_t s_sum[kThreads / 64], s_rect[kThreads / 64];
+  const int base = (int)(blockIdx.x * kThreads);
+  const int idx = base + (int)threadIdx.x;
+  const int n = min(kThreads, a.P - base);
+  side_clear(a.clear.p, a.clear.bytes, (size_t)idx, (size_t)gridDim.x * kThreads);
+#if GSR_PRE_STAGE
+  // the [P,3] inputs (12-byte rows) enter as the workgroup's contiguous 3-KB segments in 16-byte
+  // loads instead of three 4-byte loads at a 12-byte lane stride; lane reads at a 3-dword LDS
+  // stride are bank-conflict free
+  __shared__ float s_m[3 * kThreads], s_s[3 * kThreads], s_l[3 * kThreads];
+  stage_rows3(a.means3D + 3 * (size_t)base, n, s_m);
+  const bool use_s = !a.cov3D_precomp, use_l = a.include_feature && !a.lang_precomp && a.sh_language;
+  if (use_s) stage_rows3(a.scales + 3 * (size_t)base, n, s_s);
+  if (use_l) stage_rows3(a.sh_language + 3 * (size_t)base, n, s_l);
+  __syncthreads();
+  const float* pm = s_m + 3 * threadIdx.x;
+  const float* ps = s_s + 3 * threadIdx.x;
+  const float* pl = s_l + 3 * threadIdx.x;
+#else
+  const float* pm = a.means3D + 3 * (size_t)idx;
+  const float* ps = a.scales + 3 * (size_t)idx;
+  const float* pl = a.sh_language + 3 * (size_t)idx;
+#endif
+  uint32_t rect = 0;
+  const uint32_t count = idx < a.P ? preprocess_gaussian(a, idx, s_rec + threadIdx.x * kRecStride,
+                                                         pm, ps, pl, rect, nullptr) : 0u;
+  pre_epilogue(a, base, n, count, rect, s_rec, s_sum, s_rect);
+}
+
+// Several views of the same Gaussians in one launch (the multi-view call, gsr_api.cpp): a lane
+// reads its Gaussian's model inputs and evaluates the view-independent part (covariance,
+// opacity, feature) once, then runs every view's part with that view's arguments -- per view the
+// same outputs as preprocess_kernel, bit for bit, without re-reading 56 B of model rows and
+// re-evaluating exp / normalize / the covariance per view.  Views in m.v[0 .. V); the model
+// fields of m.v[0] are those of every view.
+__global__ __launch_bounds__(kThreads) void preprocess_views_kernel(PreViews m) {
+  __shared__ float4 s_rec[kThreads * kRecStride];
+  __shared__ uint32_t s_sum[kThreads / 64], s_rect[kThreads / 64];
+  const PreArgs& a0 = m.v[0];
+  const int base = (int)(blockIdx.x * kThreads);
+  const int idx = base + (int)threadIdx.x;
+  const int n = min(kThreads, a0.P - base);
+  for (int k = 0; k < m.V; k++)
+    side_clear(m.v[k].clear.p, m.v[k].clear.bytes, (size_t)idx, (size_t)gridDim.x * kThreads);
+  const bool live = idx < a0.P;
+  const float* pm = a0.means3D + 3 * (size_t)idx;
+  const float* ps = a0.scales + 3 * (size_t)idx;
+  const float* pl = a0.sh_language + 3 * (size_t)idx;
+  PreModelIn in;
+  if (live) pre_model_in(a0, idx, pm, ps, pl, in);
+  for (int k = 0; k < m.V; k++) {
+    const PreArgs& a = m.v[k];
+    uint32_t rect = 0;
+    const uint32_t count = live ? preprocess_gaussian(a, idx, s_rec + threadIdx.x * kRecStride, pm,
+                                                      ps, pl, rect, &in) : 0u;
+    pre_epilogue(a, base, n, count, rect, s_rec, s_sum, s_rect);
+    __syncthreads();  // s_rec / s_sum are the next view's
   }
 }
 
@@ -323,6 +360,30 @@ hipError_t launch_preprocess(const PreArgs& a, hipStream_t s) {
   if (a.P == 0) return hipSuccess;
   hipLaunchKernelGGL(preprocess_kernel, dim3((a.P + kThreads - 1) / kThreads), dim3(kThreads), 0,
                      s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_preprocess_views(const PreArgs* views, int V, hipStream_t s) {
+  if (V <= 0) return hipSuccess;
+  if (V > kMaxBatchViews) return hipErrorInvalidValue;
+  const PreArgs& a0 = views[0];
+  if (a0.P == 0) return hipSuccess;
+  PreViews m{};
+  m.V = V;
+  for (int k = 0; k < V; k++) {
+    const PreArgs& a = views[k];
+    // one model: the view-independent fields must agree
+    if (a.P != a0.P || a.means3D != a0.means3D || a.scales != a0.scales ||
+        a.rotations != a0.rotations || a.opacities != a0.opacities ||
+        a.cov3D_precomp != a0.cov3D_precomp || a.confidence != a0.confidence ||
+        a.sh_language != a0.sh_language || a.lang_precomp != a0.lang_precomp ||
+        a.fused != a0.fused || a.include_feature != a0.include_feature ||
+        a.scale_modifier != a0.scale_modifier)
+      return hipErrorInvalidValue;
+    m.v[k] = a;
+  }
+  hipLaunchKernelGGL(preprocess_views_kernel, dim3((a0.P + kThreads - 1) / kThreads),
+                     dim3(kThreads), 0, s, m);
   return hipGetLastError();
 }
 

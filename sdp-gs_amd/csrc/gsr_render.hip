@@ -49,10 +49,9 @@ __device__ __forceinline__ uint32_t sched_tile(uint32_t b, uint32_t ntiles, int 
 // One workgroup: bucket the tiles by log2 of their work (list length) and write them heaviest
 // bucket first.  Order inside a bucket is whatever the LDS atomics produce -- only a schedule.
 constexpr int kSchedThreads = 1024;
-__global__ __launch_bounds__(kSchedThreads) void tile_schedule_kernel(const uint2* __restrict__ ranges,
-                                                                      const uint32_t* __restrict__ work,
-                                                                      uint32_t ntiles,
-                                                                      uint32_t* __restrict__ order) {
+__device__ __forceinline__ void tile_schedule_body(const uint2* __restrict__ ranges,
+                                                   const uint32_t* __restrict__ work,
+                                                   uint32_t ntiles, uint32_t* __restrict__ order) {
   __shared__ uint32_t cnt[33];
   __shared__ uint32_t off[33];
   if (threadIdx.x < 33) cnt[threadIdx.x] = 0;
@@ -73,6 +72,23 @@ __global__ __launch_bounds__(kSchedThreads) void tile_schedule_kernel(const uint
     const uint32_t bkt = 32u - (uint32_t)__clz((int)w);
     order[atomicAdd(&off[32 - bkt], 1u)] = t;
   }
+}
+
+__global__ __launch_bounds__(kSchedThreads) void tile_schedule_kernel(const uint2* __restrict__ ranges,
+                                                                      const uint32_t* __restrict__ work,
+                                                                      uint32_t ntiles,
+                                                                      uint32_t* __restrict__ order) {
+  tile_schedule_body(ranges, work, ntiles, order);
+}
+
+struct SchedViews {
+  const uint2* ranges[kMaxBatchViews];
+  uint32_t* order[kMaxBatchViews];
+  uint32_t ntiles[kMaxBatchViews];
+};
+__global__ __launch_bounds__(kSchedThreads) void tile_schedule_views_kernel(SchedViews m) {
+  const int k = (int)blockIdx.x;  // one workgroup per view
+  tile_schedule_body(m.ranges[k], nullptr, m.ntiles[k], m.order[k]);
 }
 
 // Lane -> pixel map.  GSR_QUAD_WAVES: wave w owns the 8x8 quadrant (w & 1, w >> 1) of the tile
@@ -1196,6 +1212,23 @@ hipError_t launch_render_schedule(const RenderArgs& a, hipStream_t s) {
   if (ntiles == 0 || a.sched != 2) return hipSuccess;
   hipLaunchKernelGGL(tile_schedule_kernel, dim3(1), dim3(kSchedThreads), 0, s, a.ranges,
                      (const uint32_t*)nullptr, ntiles, a.order);
+  return hipGetLastError();
+}
+
+hipError_t launch_render_schedule_views(const RenderArgs* views, int V, hipStream_t s) {
+  if (V > kMaxBatchViews) return hipErrorInvalidValue;
+  SchedViews m{};
+  int n = 0;
+  for (int k = 0; k < V; k++) {
+    const RenderArgs& a = views[k];
+    if (a.gx * a.gy == 0 || a.sched != 2) continue;
+    m.ranges[n] = a.ranges;
+    m.order[n] = a.order;
+    m.ntiles[n] = a.gx * a.gy;
+    n++;
+  }
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(tile_schedule_views_kernel, dim3((unsigned)n), dim3(kSchedThreads), 0, s, m);
   return hipGetLastError();
 }
 

@@ -54,12 +54,11 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* lds, u
 }
 
 template <bool GATHER>
-__global__ __launch_bounds__(kThreads) void scan_reduce_kernel(const uint32_t* __restrict__ in,
-                                                               const uint32_t* __restrict__ gather,
-                                                               size_t n,
-                                                               uint32_t* __restrict__ parts) {
+__device__ __forceinline__ void scan_reduce_body(const uint32_t* __restrict__ in,
+                                                 const uint32_t* __restrict__ gather, size_t n,
+                                                 uint32_t* __restrict__ parts, uint32_t blk) {
   __shared__ uint32_t lds[kThreads / 64];
-  const size_t base = (size_t)blockIdx.x * kScanTile;
+  const size_t base = (size_t)blk * kScanTile;
   uint32_t s = 0;
 #pragma unroll
   for (int k = 0; k < kScanItems; k++) {
@@ -68,11 +67,19 @@ __global__ __launch_bounds__(kThreads) void scan_reduce_kernel(const uint32_t* _
   }
   uint32_t total;
   block_excl_scan<kThreads / 64>(s, lds, total);
-  if (threadIdx.x == 0) parts[blockIdx.x] = total;
+  if (threadIdx.x == 0) parts[blk] = total;
+}
+
+template <bool GATHER>
+__global__ __launch_bounds__(kThreads) void scan_reduce_kernel(const uint32_t* __restrict__ in,
+                                                               const uint32_t* __restrict__ gather,
+                                                               size_t n,
+                                                               uint32_t* __restrict__ parts) {
+  scan_reduce_body<GATHER>(in, gather, n, parts, blockIdx.x);
 }
 
 // One workgroup of 1024 threads: exclusive scan of the partials in place (<= kScanMaxParts).
-__global__ __launch_bounds__(1024) void scan_parts_kernel(uint32_t* __restrict__ parts, int n) {
+__device__ __forceinline__ void scan_parts_body(uint32_t* __restrict__ parts, int n) {
   __shared__ uint32_t lds[16];
   constexpr int kPer = kScanMaxParts / 1024;
   uint32_t v[kPer];
@@ -92,14 +99,17 @@ __global__ __launch_bounds__(1024) void scan_parts_kernel(uint32_t* __restrict__
   }
 }
 
+__global__ __launch_bounds__(1024) void scan_parts_kernel(uint32_t* __restrict__ parts, int n) {
+  scan_parts_body(parts, n);
+}
+
 template <bool GATHER, bool INCLUSIVE>
-__global__ __launch_bounds__(kThreads) void scan_final_kernel(const uint32_t* __restrict__ in,
-                                                              const uint32_t* __restrict__ gather,
-                                                              size_t n,
-                                                              const uint32_t* __restrict__ parts,
-                                                              uint32_t* __restrict__ out) {
+__device__ __forceinline__ void scan_final_body(const uint32_t* __restrict__ in,
+                                                const uint32_t* __restrict__ gather, size_t n,
+                                                const uint32_t* __restrict__ parts,
+                                                uint32_t* __restrict__ out, uint32_t blk) {
   __shared__ uint32_t lds[kThreads / 64];
-  const size_t base = (size_t)blockIdx.x * kScanTile + (size_t)threadIdx.x * kScanItems;
+  const size_t base = (size_t)blk * kScanTile + (size_t)threadIdx.x * kScanItems;
   uint32_t v[kScanItems];
   uint32_t s = 0;
 #pragma unroll
@@ -109,7 +119,7 @@ __global__ __launch_bounds__(kThreads) void scan_final_kernel(const uint32_t* __
     s += v[k];
   }
   uint32_t total;
-  uint32_t pre = block_excl_scan<kThreads / 64>(s, lds, total) + parts[blockIdx.x];
+  uint32_t pre = block_excl_scan<kThreads / 64>(s, lds, total) + parts[blk];
 #pragma unroll
   for (int k = 0; k < kScanItems; k++) {
     size_t i = base + k;
@@ -117,6 +127,15 @@ __global__ __launch_bounds__(kThreads) void scan_final_kernel(const uint32_t* __
     if (i < n) out[i] = INCLUSIVE ? incl : pre;
     pre = incl;
   }
+}
+
+template <bool GATHER, bool INCLUSIVE>
+__global__ __launch_bounds__(kThreads) void scan_final_kernel(const uint32_t* __restrict__ in,
+                                                              const uint32_t* __restrict__ gather,
+                                                              size_t n,
+                                                              const uint32_t* __restrict__ parts,
+                                                              uint32_t* __restrict__ out) {
+  scan_final_body<GATHER, INCLUSIVE>(in, gather, n, parts, out, blockIdx.x);
 }
 
 // Lanes of this wave whose digit equals mine (among lanes with valid == true).
@@ -191,11 +210,12 @@ constexpr uint32_t kResident1024 = 2 * 256;  // 1024-lane partitions resident at
 constexpr int kTotKPT = GSR_TOTALS_KPT;
 constexpr int kTotTile = kThreads * kTotKPT;
 
-__global__ __launch_bounds__(kThreads) void radix_totals_kernel(const uint32_t* __restrict__ keys,
-                                                                size_t n, int bits,
-                                                                uint32_t* __restrict__ totals,
-                                                                uint32_t* __restrict__ nsent_out,
-                                                                int skip_sentinel) {
+// (body shared by the one-sort kernel and the several-sorts kernel: blk / nblk = this
+// workgroup's index and the workgroup count of its sort)
+__device__ __forceinline__ void radix_totals_body(const uint32_t* __restrict__ keys, size_t n,
+                                                  int bits, uint32_t* __restrict__ totals,
+                                                  uint32_t* __restrict__ nsent_out,
+                                                  int skip_sentinel, uint32_t blk, uint32_t nblk) {
   __shared__ uint32_t cnt[kSortMaxPasses][256];
   __shared__ uint32_t nsent;  // sentinel keys of this workgroup (all digits 0xff)
 #pragma unroll
@@ -203,8 +223,7 @@ __global__ __launch_bounds__(kThreads) void radix_totals_kernel(const uint32_t* 
   if (threadIdx.x == 0) nsent = 0;
   __syncthreads();
   const int passes = (bits + 7) / 8;
-  for (size_t base = (size_t)blockIdx.x * kTotTile; base < n;
-       base += (size_t)gridDim.x * kTotTile) {
+  for (size_t base = (size_t)blk * kTotTile; base < n; base += (size_t)nblk * kTotTile) {
     // all loads of the tile in flight before any is consumed
     uint32_t key[kTotKPT];
 #pragma unroll
@@ -236,13 +255,21 @@ __global__ __launch_bounds__(kThreads) void radix_totals_kernel(const uint32_t* 
   }
   __syncthreads();
   // this workgroup's partial copy of the totals (see kSortTotShards)
-  const uint32_t shard = blockIdx.x % (uint32_t)kSortTotShards;
+  const uint32_t shard = blk % (uint32_t)kSortTotShards;
   uint32_t* tot = totals + (size_t)shard * kSortMaxPasses * 256;
   for (int p = 0; p < passes; p++) {
     const uint32_t c = cnt[p][threadIdx.x];
     if (c) atomicAdd(&tot[p * 256 + threadIdx.x], c);
   }
   if (threadIdx.x == 0 && nsent) atomicAdd(&nsent_out[shard], nsent);
+}
+
+__global__ __launch_bounds__(kThreads) void radix_totals_kernel(const uint32_t* __restrict__ keys,
+                                                                size_t n, int bits,
+                                                                uint32_t* __restrict__ totals,
+                                                                uint32_t* __restrict__ nsent_out,
+                                                                int skip_sentinel) {
+  radix_totals_body(keys, n, bits, totals, nsent_out, skip_sentinel, blockIdx.x, gridDim.x);
 }
 
 __device__ __forceinline__ uint64_t status_load(const uint64_t* p) {
@@ -253,11 +280,12 @@ __device__ __forceinline__ void status_store(uint64_t* p, uint64_t v) {
 }
 
 template <int NT>
-__global__ __launch_bounds__(NT, NT == 1024 ? 8 : (NT == 512 ? 6 : 1)) void radix_onesweep_kernel(
+__device__ __forceinline__ void onesweep_body(
     const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin, size_t n, int shift,
     int bits, const uint32_t* __restrict__ totals, const uint32_t* __restrict__ nsent_sh,
     uint32_t* __restrict__ ticket, uint64_t* __restrict__ status, uint32_t* __restrict__ err,
-    uint32_t* __restrict__ kout, uint32_t* __restrict__ vout, const uint32_t* __restrict__ kpay) {
+    uint32_t* __restrict__ kout, uint32_t* __restrict__ vout, const uint32_t* __restrict__ kpay,
+    uint32_t blk, uint32_t nblk) {
   constexpr int kSortWaves = NT / 64, kSortThreads = NT;
   constexpr int kKeysPerThread = kSortTile / NT, kKeysPerWave = kKeysPerThread * 64;
   static_assert(NT >= 256 && kSortTile % NT == 0, "one-sweep tile shape");
@@ -299,7 +327,7 @@ __global__ __launch_bounds__(NT, NT == 1024 ? 8 : (NT == 512 ? 6 : 1)) void radi
     __syncthreads();
     const uint32_t ndig = s_scan[0] + s_scan[1] + s_scan[2] + s_scan[3];
     if (ndig <= 1u) {
-      const size_t b0 = (size_t)blockIdx.x * kSortTile;
+      const size_t b0 = (size_t)blk * kSortTile;
       const size_t e0 = min(n, b0 + (size_t)kSortTile);
       for (size_t i = b0 + (size_t)t; i < e0; i += NT) {
         const uint32_t v = vin[i];
@@ -317,7 +345,7 @@ __global__ __launch_bounds__(NT, NT == 1024 ? 8 : (NT == 512 ? 6 : 1)) void radi
 #else
   // blockIdx order: every XCD dispatches its workgroups in index order, so the lowest unfinished
   // partition is always resident and the look-back always progresses (bounded spin as backstop)
-  if (t == 0) s_part = blockIdx.x;
+  if (t == 0) s_part = blk;
 #endif
   for (int e = t; e < kSortWaves * 256; e += kSortThreads) (&s_cnt[0][0])[e] = 0;
   __syncthreads();
@@ -353,7 +381,7 @@ __global__ __launch_bounds__(NT, NT == 1024 ? 8 : (NT == 512 ? 6 : 1)) void radi
     for (int w = 0; w < kSortWaves; w++) h += s_cnt[w][t];
   uint64_t* my = status + (size_t)part * 256 + dt;
   // super-partition words follow the partition words of this pass (sort_pass_words)
-  uint64_t* super = status + (size_t)gridDim.x * 256;
+  uint64_t* super = status + (size_t)nblk * 256;
   if (dig) {
     status_store(my, (part == 0 ? kStIncl : kStAgg) | (uint64_t)h);
     // one contributor and its count into the super-partition's word: self-describing (complete
@@ -491,6 +519,92 @@ __global__ __launch_bounds__(NT, NT == 1024 ? 8 : (NT == 512 ? 6 : 1)) void radi
 #undef SORT_TRACE
 }
 
+template <int NT>
+__global__ __launch_bounds__(NT, NT == 1024 ? 8 : (NT == 512 ? 6 : 1)) void radix_onesweep_kernel(
+    const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin, size_t n, int shift,
+    int bits, const uint32_t* __restrict__ totals, const uint32_t* __restrict__ nsent_sh,
+    uint32_t* __restrict__ ticket, uint64_t* __restrict__ status, uint32_t* __restrict__ err,
+    uint32_t* __restrict__ kout, uint32_t* __restrict__ vout, const uint32_t* __restrict__ kpay) {
+  onesweep_body<NT>(kin, vin, n, shift, bits, totals, nsent_sh, ticket, status, err, kout, vout,
+                    kpay, blockIdx.x, gridDim.x);
+}
+
+// ---- several independent sorts / scans / sums per launch (the multi-view forward's batched
+// binning).  Workgroup b belongs to view k with first[k] <= b < first[k + 1] (workgroup-uniform);
+// inside a view everything is exactly the one-view kernel: its own digit totals, tickets and
+// look-back words, so the views never wait on each other and each result is bit-identical to its
+// own one-view sort.
+struct SortPassJob {
+  const uint32_t* kin;
+  const uint32_t* vin;
+  uint32_t* kout;
+  uint32_t* vout;
+  const uint32_t* kpay;  // last pass: payload gathered in place of the key
+  uint32_t* aux;         // totals, sentinel counts, tickets, error word (kSortAux*)
+  uint64_t* status;      // this pass's look-back words
+  uint32_t n;
+};
+struct SortPassViews {
+  SortPassJob j[kMaxBatchViews];
+  uint32_t first[kMaxBatchViews + 1];
+  int V;
+};
+
+__device__ __forceinline__ int batch_view(const uint32_t* first, int V, uint32_t b) {
+  int k = 0;
+  while (k + 1 < V && b >= first[k + 1]) k++;
+  return k;
+}
+
+__global__ __launch_bounds__(kThreads) void radix_totals_views_kernel(SortPassViews m, int bits,
+                                                                      int skip_sentinel) {
+  const int k = batch_view(m.first, m.V, blockIdx.x);
+  const SortPassJob& j = m.j[k];
+  radix_totals_body(j.kin, j.n, bits, j.aux + kSortAuxTotals, j.aux + kSortAuxSent, skip_sentinel,
+                    blockIdx.x - m.first[k], m.first[k + 1] - m.first[k]);
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT, NT == 1024 ? 8 : (NT == 512 ? 6 : 1)) void radix_onesweep_views_kernel(
+    SortPassViews m, int pass, int bits, int sentinel) {
+  const int k = batch_view(m.first, m.V, blockIdx.x);
+  const SortPassJob& j = m.j[k];
+  onesweep_body<NT>(j.kin, j.vin, j.n, 8 * pass, bits, j.aux + kSortAuxTotals + 256 * pass,
+                    sentinel ? j.aux + kSortAuxSent : nullptr, j.aux + kSortAuxTickets + 8 * pass,
+                    j.status, j.aux + kSortAuxErr, j.kout, j.vout, j.kpay,
+                    blockIdx.x - m.first[k], m.first[k + 1] - m.first[k]);
+}
+
+struct ScanJob {
+  const uint32_t* in;
+  uint32_t* out;
+  uint32_t* parts;
+  uint32_t n;
+};
+struct ScanViews {
+  ScanJob j[kMaxBatchViews];
+  uint32_t first[kMaxBatchViews + 1];
+  int V;
+};
+
+__global__ __launch_bounds__(kThreads) void scan_reduce_views_kernel(ScanViews m) {
+  const int k = batch_view(m.first, m.V, blockIdx.x);
+  const ScanJob& j = m.j[k];
+  scan_reduce_body<false>(j.in, nullptr, j.n, j.parts, blockIdx.x - m.first[k]);
+}
+
+__global__ __launch_bounds__(1024) void scan_parts_views_kernel(ScanViews m) {
+  const ScanJob& j = m.j[blockIdx.x];  // one workgroup per view
+  scan_parts_body(j.parts, (int)(m.first[blockIdx.x + 1] - m.first[blockIdx.x]));
+}
+
+template <bool INCLUSIVE>
+__global__ __launch_bounds__(kThreads) void scan_final_views_kernel(ScanViews m) {
+  const int k = batch_view(m.first, m.V, blockIdx.x);
+  const ScanJob& j = m.j[k];
+  scan_final_body<false, INCLUSIVE>(j.in, nullptr, j.n, j.parts, j.out, blockIdx.x - m.first[k]);
+}
+
 // One workgroup: *out = sum of the n partials (n <= kScanMaxParts).
 // out[0] = sum of parts[0..n); with parts2: out[1] = sum of parts2[0..n) (the forward's exact
 // instance count and the reference's full-rectangle count, gsr_api.cpp, one read-back for both).
@@ -511,7 +625,77 @@ __global__ __launch_bounds__(1024) void sum_parts_kernel(const uint32_t* __restr
     if (parts2) out[1] = total2;
   }
 }
+
+// One workgroup per view: out = {sum parts, sum parts2}; host (device-mapped pinned words, may be
+// null) = {*flag0, the two sums}: the views' read-back is these stores plus one event, no copy.
+struct SumJob {
+  const uint32_t* parts;
+  const uint32_t* parts2;
+  uint32_t* out;
+  uint32_t* host;
+  const uint32_t* flag0;
+  int n;
+};
+struct SumViews {
+  SumJob j[kMaxBatchViews];
+  int V;
+};
+__global__ __launch_bounds__(1024) void sum_parts_views_kernel(SumViews m) {
+  __shared__ uint32_t lds[16], lds2[16];
+  const SumJob& j = m.j[blockIdx.x];
+  uint32_t s = 0, s2 = 0;
+  for (int i = (int)threadIdx.x; i < j.n; i += 1024) {
+    s += j.parts[i];
+    s2 += j.parts2[i];
+  }
+  uint32_t total, total2;
+  block_excl_scan<16>(s, lds, total);
+  block_excl_scan<16>(s2, lds2, total2);
+  if (threadIdx.x == 0) {
+    j.out[0] = total;
+    j.out[1] = total2;
+    if (j.host) {
+      j.host[0] = j.flag0 ? *j.flag0 : 0u;
+      j.host[1] = total;
+      j.host[2] = total2;
+    }
+  }
+}
 }  // namespace
+
+hipError_t sum_u32_parts_views(const SumSpec* v, int V, hipStream_t s) {
+  if (V <= 0) return hipSuccess;
+  if (V > kMaxBatchViews) return hipErrorInvalidValue;
+  SumViews m{};
+  m.V = V;
+  for (int k = 0; k < V; k++) {
+    if (v[k].n > 0x7fffffffull || !v[k].parts2) return hipErrorInvalidValue;
+    m.j[k] = SumJob{v[k].parts, v[k].parts2, v[k].out, v[k].host, v[k].flag0, (int)v[k].n};
+  }
+  hipLaunchKernelGGL(sum_parts_views_kernel, dim3((unsigned)V), dim3(1024), 0, s, m);
+  return hipGetLastError();
+}
+
+hipError_t scan_u32_views(const ScanSpec* v, int V, bool inclusive, hipStream_t s) {
+  if (V <= 0) return hipSuccess;
+  if (V > kMaxBatchViews) return hipErrorInvalidValue;
+  ScanViews m{};
+  m.V = V;
+  m.first[0] = 0;
+  for (int k = 0; k < V; k++) {
+    const size_t np = scan_parts(v[k].n);
+    if (np > (size_t)kScanMaxParts || v[k].n > 0xffffffffull) return hipErrorInvalidValue;
+    m.j[k] = ScanJob{v[k].in, v[k].out, v[k].parts, (uint32_t)v[k].n};
+    m.first[k + 1] = m.first[k] + (uint32_t)np;
+  }
+  if (m.first[V] == 0) return hipSuccess;
+  const dim3 grid(m.first[V]);
+  hipLaunchKernelGGL(scan_reduce_views_kernel, grid, dim3(kThreads), 0, s, m);
+  hipLaunchKernelGGL(scan_parts_views_kernel, dim3((unsigned)V), dim3(1024), 0, s, m);
+  if (inclusive) hipLaunchKernelGGL(scan_final_views_kernel<true>, grid, dim3(kThreads), 0, s, m);
+  else hipLaunchKernelGGL(scan_final_views_kernel<false>, grid, dim3(kThreads), 0, s, m);
+  return hipGetLastError();
+}
 
 hipError_t sum_u32_parts(const uint32_t* parts, size_t n, uint32_t* out, hipStream_t s,
                          const uint32_t* parts2) {
@@ -638,6 +822,70 @@ hipError_t radix_sort_pairs(uint32_t* ka, uint32_t* va, uint32_t* kb, uint32_t* 
     in_b = !in_b;
   }
   *result_in_b = in_b;
+  return hipGetLastError();
+}
+
+}  // namespace gsr
+
+namespace gsr {
+
+hipError_t radix_sort_pairs_views(const SortSpec* v, int V, int bits, bool* result_in_b,
+                                  hipStream_t s, bool sentinel_anywhere, bool precleared) {
+  *result_in_b = false;
+  if (V <= 0 || bits <= 0) return hipSuccess;
+  if (V > kMaxBatchViews || bits > 32) return hipErrorInvalidValue;
+  const int passes = sort_passes(bits);
+  SortPassViews m{};
+  m.V = V;
+  uint32_t tfirst[kMaxBatchViews + 1] = {0}, ofirst[kMaxBatchViews + 1] = {0};
+  for (int k = 0; k < V; k++) {
+    const size_t n = v[k].n;
+    if (n > 0xffffffffull) return hipErrorInvalidValue;
+    if (!precleared && n) {
+      hipError_t e = hipMemsetAsync(v[k].scratch.aux, 0, sort_clear_bytes(v[k].scratch, n, bits), s);
+      if (e != hipSuccess) return e;
+    }
+    const size_t tt = (n + kTotTile - 1) / kTotTile;
+    tfirst[k + 1] = tfirst[k] + (uint32_t)(tt < GSR_TOTALS_GROUPS ? tt : GSR_TOTALS_GROUPS);
+    ofirst[k + 1] = ofirst[k] + (uint32_t)sort_blocks(n);
+  }
+  if (ofirst[V] == 0) return hipSuccess;
+  auto fill = [&](int p, const uint32_t* first) {
+    for (int k = 0; k <= V; k++) m.first[k] = first[k];
+    const bool b_in = (p & 1) != 0;  // pass p reads the pair written by pass p - 1
+    for (int k = 0; k < V; k++) {
+      const SortSpec& w = v[k];
+      SortPassJob& j = m.j[k];
+      j.kin = b_in ? w.kb : w.ka;
+      j.vin = b_in ? w.vb : w.va;
+      j.kout = b_in ? w.ka : w.kb;
+      j.vout = b_in ? w.va : w.vb;
+      j.kpay = p == passes - 1 ? w.key_payload : nullptr;
+      j.aux = w.scratch.aux;
+      j.status = w.scratch.status + (size_t)p * sort_pass_words(w.n);
+      j.n = (uint32_t)w.n;
+    }
+  };
+  fill(0, tfirst);
+  hipLaunchKernelGGL(radix_totals_views_kernel, dim3(tfirst[V]), dim3(kThreads), 0, s, m, bits,
+                     sentinel_anywhere ? 1 : 0);
+  const uint32_t nb = ofirst[V];
+  const int nt = GSR_SORT_THREADS ? GSR_SORT_THREADS : (nb <= kResident1024 ? 1024 : 512);
+  for (int p = 0; p < passes; p++) {
+    fill(p, ofirst);
+    const int shift = 8 * p;
+    const int dbits = (bits - shift) < 8 ? (bits - shift) : 8;
+    if (nt == 1024)
+      hipLaunchKernelGGL(radix_onesweep_views_kernel<1024>, dim3(nb), dim3(1024), 0, s, m, p, dbits,
+                         sentinel_anywhere ? 1 : 0);
+    else if (nt == 512)
+      hipLaunchKernelGGL(radix_onesweep_views_kernel<512>, dim3(nb), dim3(512), 0, s, m, p, dbits,
+                         sentinel_anywhere ? 1 : 0);
+    else
+      hipLaunchKernelGGL(radix_onesweep_views_kernel<256>, dim3(nb), dim3(256), 0, s, m, p, dbits,
+                         sentinel_anywhere ? 1 : 0);
+  }
+  *result_in_b = (passes & 1) != 0;
   return hipGetLastError();
 }
 

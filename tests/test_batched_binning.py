@@ -1,0 +1,54 @@
+"""The multi-view call's batched forward (gsr_api.cpp views_forward_batched, the default
+GSR_VIEWS_BATCHED=1): the views' preprocesses in one multi-view launch, then one launch per
+binning stage for a group of views (instance-count sums with the pinned read-back, depth-sort
+passes, scan, duplication, tile-sort passes, ranges, schedules, blend).  The forward has no float
+atomics, so every view's images, radii and instance counts must be bitwise those of the
+single-view call (render() per camera, reference path rasterizer_impl.cu:200-340) -- including a
+view that sees no Gaussian (R = 0 inside a batch), a view count the groups do not divide evenly,
+and one view alone."""
+import numpy as np
+import pytest
+import torch
+
+from fused_ref import IMAGES, Opt, Pipe
+from gsr_amd.camera import look_at_R, make_camera
+from gsr_amd.model import SplatModel
+from gsr_amd.synthetic import make_cameras, make_gaussians
+
+pytestmark = pytest.mark.gpu
+
+
+def _away_camera(W, H, like):
+    """A camera at (0, 0, -4) looking away from the scene: every Gaussian behind its near plane."""
+    c = np.array([0.0, 0.0, -4.0])
+    R = look_at_R(c, target=np.array([0.0, 0.0, -8.0]))
+    return make_camera(R, -R.T @ c, like.FoVx, like.FoVy, W, H, uid=99, device="cuda")
+
+
+@pytest.mark.parametrize("nviews", [1, 7])
+def test_batched_forward_equals_single_view(nviews):
+    import diff_gaussian_rasterization as dgr
+    from gaussian_renderer import render, render_views
+    W, H = 240, 180
+    m = SplatModel(make_gaussians(30_000, sh_degree=3, seed=5), device="cuda")
+    cams = [c.to("cuda") for c in make_cameras(nviews, W, H, seed=5)]
+    if nviews > 3:
+        cams[3] = _away_camera(W, H, cams[0])
+    bg = torch.zeros(3, device="cuda")
+    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(2)]
+    pkgs = render_views(cams, m, Pipe(), bg, Opt(), streams=streams)
+    counts = list(dgr.LAST_STATS["view_counts"])
+    multi = [{k: p[k].detach().clone() for k in IMAGES + ("radii",)} for p in pkgs]
+    del pkgs
+    torch.cuda.synchronize()
+    assert len(counts) == nviews
+    for v, cam in enumerate(cams):
+        one = render(cam, m, Pipe(), bg, Opt())
+        torch.cuda.synchronize()
+        assert counts[v] == (dgr.LAST_STATS["num_rendered"], dgr.LAST_STATS["num_instances"]), v
+        for k in IMAGES + ("radii",):
+            assert torch.equal(multi[v][k], one[k].detach()), (v, k)
+    if nviews > 3:
+        assert counts[3] == (0, 0)
+        assert float(multi[3]["alpha"].abs().max()) == 0.0
+        assert counts[0][1] > 0
