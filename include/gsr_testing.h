@@ -82,4 +82,12 @@ const char* gsr_profile_stage_name(int stage);
 #ifdef __cplusplus
 }
 #endif
+/* Test-only bits of the multi-view backward's `debug` argument (gsr_rasterize_views_fused_backward):
+ * NO_BLEND skips the accumulator clear and the backward blend, so the per-Gaussian backward runs
+ * again on the gradient rows an earlier backward of the same forward left in the geometry
+ * buffers; PER_VIEW_PRE runs it as one launch per view instead of the merged multi-view launch.
+ * Together they compare the two per-Gaussian paths on identical inputs. */
+#define GSR_DEBUG_TEST_NO_BLEND 256
+#define GSR_DEBUG_TEST_PER_VIEW_PRE 512
+
 #endif /* GSR_TESTING_H */

@@ -1514,13 +1514,15 @@ int gsr_rasterize_views_fused_backward(
   int per = (V + (chunks_env > 0 ? chunks_env : 1) - 1) / (chunks_env > 0 ? chunks_env : 1);
   if (per > kMaxBwdViews) per = kMaxBwdViews;
   const int debug_sync = debug & 1;
+  const bool no_blend = (debug & GSR_DEBUG_TEST_NO_BLEND) != 0;
+  const bool per_view_pre = (debug & GSR_DEBUG_TEST_PER_VIEW_PRE) != 0;
   for (int v0 = 0; v0 < V; v0 += per) {
     const int n = V - v0 < per ? V - v0 : per;
     RenderBwdArgs rbs[kMaxBwdViews];
     int nb = 0;
     for (int k = 0; k < n; k++) {
       BwdCall& c = calls[(size_t)(v0 + k)];
-      if (c.done) continue;
+      if (c.done || no_blend) continue;
       if (c.acc_zero) {
         BwdCall z = c;
         z.blend = false;  // the accumulator memset only
@@ -1548,7 +1550,7 @@ int gsr_rasterize_views_fused_backward(
     for (int k = 0; k < n; k++)
       if (!calls[(size_t)(v0 + k)].done) bas[np++] = calls[(size_t)(v0 + k)].ba;
     hipError_t ve = hipErrorNotSupported;
-    if (np > 1 && views_pre_merged()) {
+    if (np > 1 && views_pre_merged() && !per_view_pre) {
       const int debug = debug_sync;
       hipStream_t stream = call_stream;
       PROF_BEGIN(PREPROCESS_BWD);

@@ -189,15 +189,52 @@ struct RegSink {
   __device__ void sh_language(V3 v) { shl = add3(assign, shl, v); }
 };
 
+// The view-independent inputs of one Gaussian's backward in the fused scale / rotation
+// configuration: its mean, raw and normalised rotation, activated scale, 3D covariance and
+// activated opacity.  The multi-view kernel evaluates them once for all views; gaussian_bwd
+// evaluates the same functions on the same inputs itself when handed none (bit-identical).
+struct BwdModel {
+  V3 mean;
+  float4 qraw, q;
+  V3 sc;
+  float c3[6];
+  float y;
+};
+// An opaque copy (no instruction emitted): what is derived from it inside the multi-view loop
+// cannot be hoisted out of the loop by the compiler, which otherwise keeps ~80 more registers
+// live across the views (207 vs 129 VGPRs measured)
+__device__ __forceinline__ BwdModel opaque(const BwdModel& m) {
+  BwdModel o = m;
+  float* f = reinterpret_cast<float*>(&o);
+#pragma unroll
+  for (int k = 0; k < (int)(sizeof(BwdModel) / sizeof(float)); k++) asm volatile("" : "+v"(f[k]));
+  return o;
+}
+__device__ __forceinline__ void bwd_model(const BwdPreArgs& a, size_t i, BwdModel& md) {
+  md.mean = v3(a.means3D[3 * i], a.means3D[3 * i + 1], a.means3D[3 * i + 2]);
+  md.qraw = reinterpret_cast<const float4*>(a.rotations)[i];
+  md.sc = v3(expf(a.scales[3 * i]), expf(a.scales[3 * i + 1]), expf(a.scales[3 * i + 2]));
+  md.q = normalize_quat(md.qraw);
+  cov3d_from_scale_rot(md.sc.x, md.sc.y, md.sc.z, a.scale_modifier, md.q.x, md.q.y, md.q.z,
+                       md.q.w, md.c3);
+  md.y = sigmoid_f(a.opacities_raw[i]);
+}
+
 // Backward of one visible Gaussian.  sh0 / sh1: its rows (coefficient 0 / coefficients 1..) of
 // the LDS staging planes: SH coefficients in, SH gradients out; unused without SH.  The
 // per-view outputs (screen-space gradient, deferred dL/dRGB, SH rows) are written here; the
-// per-Gaussian gradients go to `sk`.
+// per-Gaussian gradients go to `sk`.  md: the view-independent inputs if already evaluated
+// (fused scale / rotation only), row: the gradient row if already loaded.
 template <bool ACC, class Sink>
 __device__ __forceinline__ void gaussian_bwd(const BwdPreArgs& a, size_t i, float* sh0,
-                                             float* sh1, Sink& sk) {
+                                             float* sh1, Sink& sk, const BwdModel* md = nullptr,
+                                             const float4* row = nullptr) {
   float4 q0, q1, q2, q3;
-  grad_row(a, i, q0, q1, q2, q3);
+  if (row) {
+    q0 = row[0]; q1 = row[1]; q2 = row[2]; q3 = row[3];
+  } else {
+    grad_row(a, i, q0, q1, q2, q3);
+  }
   // slots: q0 = {mx, my, ca, cb}, q1 = {cc, op, r, g}, q2 = {b, depth, f0, f1}, q3 = {f2, used, -, -}
   const float gmx = q0.x, gmy = q0.y;
   const float dcx = q0.z, dcy = q0.w, dcz = q1.x;
@@ -207,18 +244,21 @@ __device__ __forceinline__ void gaussian_bwd(const BwdPreArgs& a, size_t i, floa
   {
     float dop = a.confidence ? q1.y * a.confidence[i] : q1.y;
     if (a.fused) {  // through get_opacity = sigmoid(_opacity): go * (1 - y) * y
-      const float y = sigmoid_f(a.opacities_raw[i]);
+      const float y = md ? md->y : sigmoid_f(a.opacities_raw[i]);
       dop = dop * (1.0f - y) * y;
     }
     sk.opacity(dop);
   }
 
-  const V3 mean = v3(a.means3D[3 * i], a.means3D[3 * i + 1], a.means3D[3 * i + 2]);
+  const V3 mean = md ? md->mean : v3(a.means3D[3 * i], a.means3D[3 * i + 1], a.means3D[3 * i + 2]);
   // 3D covariance: precomputed, or recomputed from scale / rotation with the forward's own
   // function and inputs (bit-identical to what the forward projected; not stored in between)
   float c3buf[6];  // always a register array (a pointer select would force it into scratch)
   const float* c3 = c3buf;
-  if (a.cov3D) {
+  if (md) {
+#pragma unroll
+    for (int k = 0; k < 6; k++) c3buf[k] = md->c3[k];
+  } else if (a.cov3D) {
 #pragma unroll
     for (int k = 0; k < 6; k++) c3buf[k] = a.cov3D[6 * i + k];
   } else {
@@ -326,16 +366,21 @@ __device__ __forceinline__ void gaussian_bwd(const BwdPreArgs& a, size_t i, floa
 
   // ---- cov3D -> scale / rotation (backward.cu:278-341, 393-395) ----
   if (a.scales) {
-    const float4 qraw = reinterpret_cast<const float4*>(a.rotations)[i];
+    const float4 qraw = md ? md->qraw : reinterpret_cast<const float4*>(a.rotations)[i];
     // fused: the kernel saw normalize(_rotation) and exp(_scaling) (gsr_preprocess.hip)
-    const float4 q = a.fused ? normalize_quat(qraw) : qraw;
+    const float4 q = md ? md->q : (a.fused ? normalize_quat(qraw) : qraw);
     const float r = q.x, x = q.y, y = q.z, z = q.w;
     M3 R = m3_cols(1.f - 2.f * (y * y + z * z), 2.f * (x * y - r * z), 2.f * (x * z + r * y),
                    2.f * (x * y + r * z), 1.f - 2.f * (x * x + z * z), 2.f * (y * z - r * x),
                    2.f * (x * z - r * y), 2.f * (y * z + r * x), 1.f - 2.f * (x * x + y * y));
     M3 S = m3_cols(1, 0, 0, 0, 1, 0, 0, 0, 1);
-    V3 sc = v3(a.scales[3 * i], a.scales[3 * i + 1], a.scales[3 * i + 2]);
-    if (a.fused) sc = v3(expf(sc.x), expf(sc.y), expf(sc.z));
+    V3 sc;
+    if (md) {
+      sc = md->sc;
+    } else {
+      sc = v3(a.scales[3 * i], a.scales[3 * i + 1], a.scales[3 * i + 2]);
+      if (a.fused) sc = v3(expf(sc.x), expf(sc.y), expf(sc.z));
+    }
     const V3 s = a.scale_modifier * sc;
     S.m[0][0] = s.x; S.m[1][1] = s.y; S.m[2][2] = s.z;
     const M3 Mm = m3_mul(S, R);
@@ -468,8 +513,15 @@ __global__ __launch_bounds__(kThreads) void preprocess_bwd_kernel(BwdPreArgs a) 
 // gaussian_bwd, their gradients summed in registers (RegSink: the same additions, in the same
 // order, as one launch per view) and written once -- the parameters and the leaves' gradients
 // cross HBM once per step instead of once per view.  View 0's `accumulate` decides store / add.
+#ifndef GSR_BWDV_MINBLK
+#define GSR_BWDV_MINBLK 1
+#endif
+// 1: each view's gradient row and radius are loaded one view ahead (registers)
+#ifndef GSR_BWDV_PREFETCH
+#define GSR_BWDV_PREFETCH 1
+#endif
 template <bool ACC>
-__global__ __launch_bounds__(kThreads) void preprocess_bwd_views_kernel(BwdPreViews m) {
+__global__ __launch_bounds__(kThreads, GSR_BWDV_MINBLK) void preprocess_bwd_views_kernel(BwdPreViews m) {
   const BwdPreArgs& a0 = m.v[0];
   const size_t i = (size_t)blockIdx.x * kThreads + threadIdx.x;
   if (i >= (size_t)a0.P) return;
@@ -492,8 +544,26 @@ __global__ __launch_bounds__(kThreads) void preprocess_bwd_views_kernel(BwdPreVi
     sk.rot = make_float4(0, 0, 0, 0);
   }
   bool touched = !ACC;
+  // the model side once; each view's gradient row and radius loaded one view ahead, so their
+  // latency hides behind the previous view's arithmetic
+  BwdModel md;
+  bwd_model(a0, i, md);
+  float4 cur[4], nxt[4];
+  int rcur = 0, rnxt = 0;
+  if (GSR_BWDV_PREFETCH) {
+    rcur = a0.radii[i];
+    grad_row(a0, i, cur[0], cur[1], cur[2], cur[3]);
+  }
+#pragma unroll 1
   for (int v = 0; v < m.V; v++) {
     const BwdPreArgs& a = m.v[v];
+    if (!GSR_BWDV_PREFETCH) {
+      rcur = a.radii[i];
+    } else if (v + 1 < m.V) {
+      const BwdPreArgs& an = m.v[v + 1];
+      rnxt = an.radii[i];
+      grad_row(an, i, nxt[0], nxt[1], nxt[2], nxt[3]);
+    }
     if (a.status && *a.status) {  // this view's forward failed (view-uniform): NaN gradients
       const float nan = __builtin_nanf("");
       const V3 n3 = v3(nan, nan, nan);
@@ -503,10 +573,9 @@ __global__ __launch_bounds__(kThreads) void preprocess_bwd_views_kernel(BwdPreVi
       sk.lang_feature(n3); sk.sh_language(n3);
       sk.assign = false;
       touched = true;
-      continue;
-    }
-    if (a.radii[i] > 0) {
-      gaussian_bwd<true>(a, i, nullptr, nullptr, sk);
+    } else if (rcur > 0) {
+      const BwdModel mv = opaque(md);
+      gaussian_bwd<true>(a, i, nullptr, nullptr, sk, &mv, GSR_BWDV_PREFETCH ? cur : nullptr);
       sk.assign = false;
       touched = true;
     } else {
@@ -514,6 +583,9 @@ __global__ __launch_bounds__(kThreads) void preprocess_bwd_views_kernel(BwdPreVi
       put3p(a.dRGB_out, (size_t)a.P, i, v3(0, 0, 0));
       if (v == 0) sk.assign = false;  // store mode: the zeros of the culled first view
     }
+#pragma unroll
+    for (int k = 0; k < 4; k++) cur[k] = nxt[k];
+    rcur = rnxt;
   }
   if (!touched) return;  // accumulate mode, culled in every view: nothing to add
   a0.dL_dopacity[i] = sk.op;

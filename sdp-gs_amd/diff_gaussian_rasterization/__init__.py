@@ -459,6 +459,10 @@ def rasterize_views_fused(means3D, means2D, features_dc, features_rest, opacity_
                                       tuple(raster_settings_list), tuple(streams or ()))
 
 
+# test hook: extra debug bits of the multi-view backward (include/gsr_testing.h GSR_DEBUG_TEST_*)
+_TEST_BWD_BITS = [0]
+
+
 def _view_streams(streams):
     """The streams a multi-view forward bins its views on: the side streams (streams[1:]).  The
     backward's merged blend runs on the last of them, idle by then."""
@@ -673,7 +677,7 @@ class _RasterizeViewsFused(torch.autograd.Function):
                 _ptr(sc), _ptr(rot), mt["scale_modifier"], mt["degree"], _ptr(lf), _ptr(conf),
                 int(mt["include_feature"]), _ptr(d_means3D), _ptr(d_dc), _ptr(d_rest),
                 _ptr(d_op), _ptr(d_sc), _ptr(d_rot), _ptr(d_lf), int(accumulate),
-                cur.cuda_stream, ctx.gsr_flags)
+                cur.cuda_stream, ctx.gsr_flags | _TEST_BWD_BITS[0])
         _lib.check(rc)
         LAST_STATS["views_bwd_host_s"] = time.perf_counter() - t_host
         if into_leaves:

@@ -52,3 +52,55 @@ def test_batched_forward_equals_single_view(nviews):
         assert counts[3] == (0, 0)
         assert float(multi[3]["alpha"].abs().max()) == 0.0
         assert counts[0][1] > 0
+
+
+def test_merged_preprocess_bwd_equals_per_view_launches():
+    """The multi-view backward's merged per-Gaussian launch (gsr_backward.hip
+    preprocess_bwd_views_kernel: model inputs evaluated once, rows loaded one view ahead,
+    per-view gradients summed in registers in view order) against one launch per view on the
+    SAME gradient rows (the blend skipped on the repeats, include/gsr_testing.h test bits):
+    every leaf gradient and every view's screen-space gradient bitwise equal."""
+    import diff_gaussian_rasterization as dgr
+    from fused_ref import LEAVES
+    from gaussian_renderer import render_views
+    from gsr_amd.pipeline import ViewPipeline
+    from gsr_amd.synthetic import upstream_grads
+    NO_BLEND, PER_VIEW = 256, 512
+    W, H = 240, 180
+    m = SplatModel(make_gaussians(30_000, sh_degree=3, seed=13), device="cuda")
+    cams = [c.to("cuda") for c in make_cameras(3, W, H, seed=13)]
+    grads = upstream_grads(H, W, seed=3, device="cuda")
+    bg = torch.zeros(3, device="cuda")
+    direct = [n for n in LEAVES if n not in ("_features_dc", "_features_rest")]  # SH: deferred
+    prev = dgr.grad_into_leaves()
+    dgr.grad_into_leaves(True)
+
+    def fn(cs, strs):
+        pkgs = render_views(cs, m, Pipe(), bg, Opt(), streams=strs)
+        st = pkgs[0]["views"]
+        V = len(pkgs)
+        seeds = [g.expand(V, *g.shape) for g in grads]
+        outs = []
+        for bits in (0, NO_BLEND, NO_BLEND | PER_VIEW):
+            for n in LEAVES:
+                getattr(m, n).grad = None
+            st["viewspace_points"].grad = None
+            dgr._TEST_BWD_BITS[0] = bits
+            torch.autograd.backward([st["render"], st["depth"], st["feature"]], seeds,
+                                    retain_graph=True)
+            o = {n: getattr(m, n).grad.detach().clone() for n in direct}
+            o["means2D"] = st["viewspace_points"].grad.detach().clone()
+            outs.append(o)
+        return outs
+
+    try:
+        vp = ViewPipeline(torch.device("cuda"), depth=3, defer_sh=True, precolor=True)
+        merged, merged_again, per_view = vp.run_views(cams, fn, model=m)
+        torch.cuda.synchronize()
+    finally:
+        dgr._TEST_BWD_BITS[0] = 0
+        dgr.grad_into_leaves(prev)
+    for k in merged:
+        assert torch.equal(merged[k], merged_again[k]), k  # the rows survive a backward
+        assert torch.equal(merged_again[k], per_view[k]), k
+    assert float(merged["_xyz"].abs().max()) > 0.0
