@@ -68,13 +68,42 @@ class Opt:
 
 
 def algorithmic_bytes(stage, P, Pv, R, T, HW, D=3, C=8, tile_passes=2, acc=True, defer_sh=False,
-                      precolor=False, views=6):
+                      precolor=False, views=6, launch_views=1):
     """Bytes each stage must move per launch.
     P Gaussians, Pv visible, R instances, T tiles, HW pixels, C blended channels (rgb, depth,
     alpha, feature x3), acc: the backward adds into existing gradients (read + write),
     defer_sh: the SH gradients are replaced by a stored 12-B dL/dRGB (flushed once per step),
     precolor: the SH rows are replaced by the pre-pass's colour + clamp (13 B, forward) and
-    colour Jacobian (36 B, backward)."""
+    colour Jacobian (36 B, backward).  launch_views: views one launch covers -- per-view stages
+    scale by it, except that the multi-view preprocess and per-Gaussian backward read the model
+    rows (and read-modify-write the leaf gradients) once per launch."""
+    if stage in ("preprocess", "preprocess_bwd") and launch_views > 1:
+        per, once = _model_split(stage, P, Pv, D, acc, defer_sh, precolor)
+        return launch_views * per + once
+    return launch_views * _stage_bytes(stage, P, Pv, R, T, HW, D, C, tile_passes, acc, defer_sh,
+                                       precolor, views)
+
+
+def _model_split(stage, P, Pv, D, acc, defer_sh, precolor):
+    """(per-view bytes, once-per-launch bytes) of the multi-view preprocess / backward launch."""
+    sh = 12 * (D + 1) ** 2
+    sh_fwd = 13 if precolor else sh
+    sh_bwd = 36 if (precolor and defer_sh) else sh
+    if stage == "preprocess":
+        # once: means, scale, rotation, opacity, language; per view: colour, radii/tiles/key/
+        # value, record + clamp, the zeroed accumulator row
+        return Pv * sh_fwd + P * 16 + Pv * (64 + 1) + P * 64, P * 12 + Pv * (12 + 16 + 4 + 12)
+    # once: means, scale, rotation, opacity, language in; the leaf gradients (means3D, opacity,
+    # scale, rotation, language; SH deferred or not) read-modify-written (acc) or stored once;
+    # per view: accumulator row, colour Jacobian + clamp, radii, screen-space gradient out,
+    # deferred dL/dRGB out
+    leaf = 12 + 4 + 12 + 16 + 12 + (0 if defer_sh else sh)
+    once = Pv * (12 + 12 + 16 + 4 + 12) + ((2 * Pv) if acc else P) * leaf
+    per = Pv * (64 + sh_bwd + 1) + P * 4 + P * 12 + (P * 12 if defer_sh else 0)
+    return per, once
+
+
+def _stage_bytes(stage, P, Pv, R, T, HW, D, C, tile_passes, acc, defer_sh, precolor, views):
     sh = 12 * (D + 1) ** 2
     sh_fwd = 13 if precolor else sh
     sh_bwd = 36 if (precolor and defer_sh) else sh
@@ -372,13 +401,9 @@ def main():
         vpl = 1
         if name not in ("sh_precolor", "sh_flush"):
             vpl = max(1, int(round(len(my_cams) * stage_steps.get(name, 1) / calls)))
-        b = vpl * algorithmic_bytes(name, P, Pv, R, T, HW, D=deg, acc=not args.autograd_grads,
-                                    defer_sh=defer_sh, precolor=not args.no_precolor,
-                                    views=len(my_cams))
-        if name == "preprocess" and vpl > 1:
-            # the multi-view preprocess reads each Gaussian's model rows (means, scale, rotation,
-            # opacity, language: 56 B) once for all the launch's views
-            b -= (vpl - 1) * (P * 12 + Pv * (12 + 16 + 4 + 12))
+        b = algorithmic_bytes(name, P, Pv, R, T, HW, D=deg, acc=not args.autograd_grads,
+                              defer_sh=defer_sh, precolor=not args.no_precolor,
+                              views=len(my_cams), launch_views=vpl)
         k = {"avg_ms": round(avg_ms, 4), "calls": int(calls), "bytes": int(b),
              "views_per_launch": vpl, "gbs": round(b / (avg_ms * 1e-3) / 1e9, 1)}
         if name in ("render_fwd", "render_bwd"):
