@@ -1,6 +1,7 @@
 """Host-side cost of the multi-view step (bench.py's headline workload): per step the wall time,
 the host time inside the forward / backward C calls, the host time waiting for read-backs, and the
-Python time around them.  usage: python scripts/host_views.py [steps] [streams]"""
+Python time around them.  usage: python scripts/host_views.py [steps] [streams] [P]
+(a small P, e.g. 1000, leaves only the host costs: the GPU work per step is then negligible)"""
 import os
 import sys
 import time
@@ -19,9 +20,10 @@ from tests.fused_ref import Opt, Pipe  # noqa: E402
 
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
 nstreams = int(sys.argv[2]) if len(sys.argv) > 2 else 4
+P = int(sys.argv[3]) if len(sys.argv) > 3 else 1_000_000
 dev = torch.device("cuda", 0)
 dgr.grad_into_leaves(True)
-m = SplatModel(make_gaussians(1_000_000, sh_degree=3, seed=0), device=dev)
+m = SplatModel(make_gaussians(P, sh_degree=3, seed=0), device=dev)
 cams = [c.to(dev) for c in make_cameras(12, 1008, 756, seed=0)]
 dimg, ddep, dfeat = upstream_grads(756, 1008, seed=1, device=dev)
 bg = torch.zeros(3, device=dev)

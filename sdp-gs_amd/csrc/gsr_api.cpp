@@ -414,6 +414,9 @@ struct FwdCam {
   bool done = false;  // P == 0: outputs written by the first phase
   bool depth_in_b = false;  // which buffer pair holds the depth sort's result
   bool defer_pre = false;  // fwd_prep leaves the preprocess arguments in pa (not launched)
+  // buffers already allocated by the caller (the multi-view call allocates a group's buffers in
+  // one callback and carves them), else allocated through `alloc`
+  char *given_g = nullptr, *given_i = nullptr, *given_b = nullptr;
   PreArgs pa{};
   // state of the binning half of the second phase (fwd_bin -> the blend)
   BinState b{};
@@ -483,10 +486,10 @@ static int fwd_prep(const FwdModel& m, FwdCam& c) {
   c.gy = (uint32_t)((H + kTile - 1) / kTile);
 
   const size_t gbytes = carve_geom(nullptr, (size_t)P).bytes;
-  c.gbase = (char*)c.alloc(c.alloc_ctx, gbytes, GSR_BUF_GEOM);
+  c.gbase = c.given_g ? c.given_g : (char*)c.alloc(c.alloc_ctx, gbytes, GSR_BUF_GEOM);
   if (!c.gbase) return fail(GSR_ERR_ALLOC, "geometry buffer allocation of %zu bytes failed", gbytes);
   const size_t ibytes = carve_img(nullptr, (size_t)W, (size_t)H).bytes;
-  c.ibase = (char*)c.alloc(c.alloc_ctx, ibytes, GSR_BUF_IMAGE);
+  c.ibase = c.given_i ? c.given_i : (char*)c.alloc(c.alloc_ctx, ibytes, GSR_BUF_IMAGE);
   if (!c.ibase) return fail(GSR_ERR_ALLOC, "image buffer allocation of %zu bytes failed", ibytes);
   c.g = carve_geom(c.gbase, (size_t)P);
   c.im = carve_img(c.ibase, (size_t)W, (size_t)H);
@@ -582,7 +585,7 @@ static int fwd_bin_alloc(const FwdModel& m, FwdCam& c) {
     if (host[2]) return fail(GSR_ERR_HIP, "depth sort look-back timed out");
   }
   const size_t bbytes = carve_bin(nullptr, R_ref, m.rows).bytes;
-  c.bbase = (char*)c.alloc(c.alloc_ctx, bbytes, GSR_BUF_BINNING);
+  c.bbase = c.given_b ? c.given_b : (char*)c.alloc(c.alloc_ctx, bbytes, GSR_BUF_BINNING);
   if (!c.bbase) return fail(GSR_ERR_ALLOC, "binning buffer allocation of %zu bytes failed", bbytes);
   c.b = carve_bin(c.bbase, R_ref, m.rows);  // capacity R_ref, the first R entries used
   c.num_rendered = (int)R_ref;
@@ -1097,6 +1100,23 @@ bool pre_views() {
   return on;
 }
 
+// GSR_HOST_TRACE=1: host timestamps of the batched forward's phases, printed per call (stderr)
+struct HostTrace {
+  bool on;
+  std::chrono::steady_clock::time_point t0;
+  char buf[512];
+  int n = 0;
+  HostTrace() : on(getenv("GSR_HOST_TRACE") != nullptr), t0(std::chrono::steady_clock::now()) {}
+  void mark(const char* what, int g) {
+    if (!on || n > 440) return;
+    const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    n += snprintf(buf + n, sizeof(buf) - (size_t)n, " %s%d=%.0f", what, g, us);
+  }
+  ~HostTrace() {
+    if (on) fprintf(stderr, "[gsr host]%s\n", buf);
+  }
+};
+
 // Coherent, device-mapped pinned words (4 per view) that the batched sums store each view's
 // read-back into: no copy launch, one event per group.
 uint32_t* batch_slot(int i, uint32_t** dev_ptr) {
@@ -1159,7 +1179,21 @@ int views_forward_batched(const FwdModel& m, std::vector<FwdCam>& cams, gsr_view
   std::vector<Group> grp((size_t)ng);
   const int P = m.P;
   const size_t pre_blocks = ((size_t)P + 255) / 256;
+  // every view's geometry and image buffer in ONE allocation callback (carved per view; the
+  // first view's allocation holds them all, so the caller keeps every view's scratch alive as
+  // before): a callback into the caller's allocator costs ~10-20 us of host time
+  if (P > 0 && cams[0].alloc) {
+    const size_t gb = carve_geom(nullptr, (size_t)P).bytes;
+    const size_t ib = carve_img(nullptr, (size_t)cams[0].W, (size_t)cams[0].H).bytes;
+    char* base = (char*)cams[0].alloc(cams[0].alloc_ctx, (size_t)V * (gb + ib), GSR_BUF_GEOM);
+    if (!base) return fail(GSR_ERR_ALLOC, "scratch allocation of %zu bytes failed", (size_t)V * (gb + ib));
+    for (int v = 0; v < V; v++) {
+      cams[(size_t)v].given_g = base + (size_t)v * (gb + ib);
+      cams[(size_t)v].given_i = cams[(size_t)v].given_g + gb;
+    }
+  }
   // phase 1 of a group: preprocess per view, then one launch per stage for the group
+  HostTrace ht;
   auto phase1 = [&](int gi) -> int {
     Group& G = grp[(size_t)gi];
     G.v0 = gi * per;
@@ -1224,7 +1258,9 @@ int views_forward_batched(const FwdModel& m, std::vector<FwdCam>& cams, gsr_view
     if (nl > 0) {
       {
         const auto t0 = std::chrono::steady_clock::now();
+        ht.mark("w", gi);
         GSR_CHECK(hipEventSynchronize(G.ready));
+        ht.mark("r", gi);
         g_wait_ns.fetch_add((long long)std::chrono::duration_cast<std::chrono::nanoseconds>(
                                 std::chrono::steady_clock::now() - t0).count(),
                             std::memory_order_relaxed);
@@ -1233,6 +1269,18 @@ int views_forward_batched(const FwdModel& m, std::vector<FwdCam>& cams, gsr_view
       SortSpec ts[kMaxBatchViews];
       const uint32_t ntiles = cams[(size_t)G.live[0]].gx * cams[(size_t)G.live[0]].gy;
       const int tbits = tile_bits(ntiles);
+      {  // the group's binning buffers in one allocation callback (sizes from the read-back)
+        size_t off[kMaxBatchViews + 1] = {0};
+        for (int l = 0; l < nl; l++) {
+          const uint32_t R_ref = cams[(size_t)G.live[(size_t)l]].host[2];
+          const size_t bb = R_ref <= 0x7fffffffu ? carve_bin(nullptr, R_ref, m.rows).bytes : 0;
+          off[l + 1] = off[l] + bb;  // (an invalid count is reported by fwd_bin_alloc)
+        }
+        FwdCam& c0 = cams[(size_t)G.live[0]];
+        char* base = (char*)c0.alloc(c0.alloc_ctx, off[nl] ? off[nl] : 256, GSR_BUF_BINNING);
+        if (!base) return fail(GSR_ERR_ALLOC, "binning buffer allocation of %zu bytes failed", off[nl]);
+        for (int l = 0; l < nl; l++) cams[(size_t)G.live[(size_t)l]].given_b = base + off[l];
+      }
       for (int l = 0; l < nl; l++) {
         FwdCam& c = cams[(size_t)G.live[(size_t)l]];
         if (int rc = fwd_bin_alloc(m, c)) return rc;  // (debug: checks the depth sort)
@@ -1247,6 +1295,7 @@ int views_forward_batched(const FwdModel& m, std::vector<FwdCam>& cams, gsr_view
         ts[l] = SortSpec{b.tkey_a, b.tval_a, b.tkey_b, b.tval_b, (size_t)R, b.sort, nullptr};
       }
       PROF_BEGIN(DUPLICATE);
+      ht.mark("a", gi);
       GSR_CHECK(launch_duplicate_views(dup, nl, stream));
       PROF_END(DUPLICATE);
       bool t_in_b = false;
@@ -1283,6 +1332,7 @@ int views_forward_batched(const FwdModel& m, std::vector<FwdCam>& cams, gsr_view
       PROF_END(RANGES);
       PROF_BEGIN(RENDER_FWD);
       GSR_CHECK(launch_render_forward_views(ras, nl, stream));
+      ht.mark("f", gi);
       PROF_END(RENDER_FWD);
     }
     for (int k = 0; k < G.n; k++) {
@@ -1309,13 +1359,16 @@ int views_forward_batched(const FwdModel& m, std::vector<FwdCam>& cams, gsr_view
     return e ? atoi(e) : 0;
   }();
   const int lead = (lead_env < 1 || lead_env > ng) ? ng : lead_env;
-  for (int gi = 0; gi < lead; gi++)
+  for (int gi = 0; gi < lead; gi++) {
     if (int rc = phase1(gi)) return rc;
+    ht.mark("p", gi);
+  }
   for (int gi = 0; gi < ng; gi++) {
     if (int rc = phase2(gi)) return rc;
     if (gi + lead < ng)
       if (int rc = phase1(gi + lead)) return rc;
   }
+  ht.mark("end", 0);
   g_last_instances = cams[(size_t)V - 1].num_instances;
   return GSR_OK;
 }
