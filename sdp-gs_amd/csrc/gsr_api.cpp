@@ -417,6 +417,7 @@ struct FwdCam {
   // buffers already allocated by the caller (the multi-view call allocates a group's buffers in
   // one callback and carves them), else allocated through `alloc`
   char *given_g = nullptr, *given_i = nullptr, *given_b = nullptr;
+  SideClear acc_clear{nullptr, 0};  // accumulator rows the forward blend zeroes (multi-view call)
   PreArgs pa{};
   // state of the binning half of the second phase (fwd_bin -> the blend)
   BinState b{};
@@ -1090,6 +1091,16 @@ hipEvent_t join_event(int i) {
   return ev[dev][i];
 }
 
+// The batched path zeroes the backward accumulator rows in the forward blend's grid (default)
+// instead of the preprocess's (GSR_BLEND_ZEROES_ACC=0)
+bool blend_zeroes_acc() {
+  static const bool on = [] {
+    const char* e = getenv("GSR_BLEND_ZEROES_ACC");
+    return e ? atoi(e) != 0 : true;
+  }();
+  return on;
+}
+
 // The batched path's preprocess: one multi-view launch (default) or one launch per view
 // (GSR_PRE_VIEWS=0).
 bool pre_views() {
@@ -1218,6 +1229,10 @@ int views_forward_batched(const FwdModel& m, std::vector<FwdCam>& cams, gsr_view
       const GeomState& g = c.g;
       const int l = (int)G.live.size();
       pas[l] = c.pa;
+      if (blend_zeroes_acc() && pas[l].acc_zero) {
+        pas[l].acc_zero = 0;  // the view's forward blend zeroes the accumulator rows instead
+        c.acc_clear = SideClear{g.acc, (size_t)P * kAccFloats * sizeof(float)};
+      }
       sums[l] = SumSpec{g.pre_parts, g.pre_parts + pre_blocks, pre_blocks, g.flags + 1, c.host_dev,
                         m.prefiltered ? g.flags : nullptr};
       ds[l] = SortSpec{g.dkey_a, g.dval_a, g.dkey_b, g.dval_b, (size_t)P, g.sort, g.tiles_touched};
@@ -1323,6 +1338,7 @@ int views_forward_batched(const FwdModel& m, std::vector<FwdCam>& cams, gsr_view
                            b.sort.aux + kSortAuxErr, c.im.status, host_status,
                            forward_faults_word()};
         fwd_render_args(m, c, point_list, host_status);
+        c.ra.clear = c.acc_clear;
         c.mail_slot = mail_slot;
         ras[l] = c.ra;
       }

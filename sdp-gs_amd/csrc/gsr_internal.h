@@ -407,6 +407,9 @@ struct RenderArgs {
   uint32_t* status;  // ImgState::status: non-zero -> NaN outputs; kStatusClamp or-ed on a clamp
   uint32_t* host_status;  // pinned, device-mapped mirror of the clamp bit (may be null)
   uint32_t* fault;        // forward_faults_word() (may be null): kStatusClamp or-ed on a clamp
+  // zero-fill done by the blend's grid (the multi-view call: the view's backward accumulator
+  // rows, moved off the memory-bound preprocess onto this VALU-bound kernel); p = null: none
+  SideClear clear;
 };
 hipError_t launch_render_forward(const RenderArgs& a, hipStream_t s);
 // the two halves of launch_render_forward for multi-view calls: the heaviest-first tile schedule

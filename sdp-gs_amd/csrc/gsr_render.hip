@@ -215,6 +215,8 @@ __global__ __launch_bounds__(kThreads) void render_fwd_kernel(RenderArgs a) {
   __shared__ uint8_t s_mask[kThreads];
   __shared__ uint8_t s_list[kThreads / 64][kThreads];
   __shared__ uint32_t s_max;
+  side_clear(a.clear.p, a.clear.bytes, (size_t)blockIdx.x * kThreads + threadIdx.x,
+             (size_t)gridDim.x * kThreads);
   const int lane = (int)(threadIdx.x & 63);
   const int wid = (int)(threadIdx.x >> 6);
 
@@ -977,6 +979,7 @@ __device__ __forceinline__ void render_fwd_blk_tile(const RenderArgs& a, uint32_
   const uint32_t grp = ((uint32_t)lane >> 1) & 3u;
 
   const uint32_t ntiles = a.gx * a.gy;
+  side_clear(a.clear.p, a.clear.bytes, (size_t)blk * kThreads + threadIdx.x, (size_t)ntiles * kThreads);
   const uint32_t tile = sched_tile(blk, ntiles, a.sched, a.order);
   const uint32_t tx = tile % a.gx, ty = tile / a.gx;
   uint32_t px, py;
