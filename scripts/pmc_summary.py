@@ -21,6 +21,12 @@ STAGE = {"preprocess_kernel": "preprocess", "duplicate_kernel": "duplicate",
          # multi-view calls: several views per launch
          "render_bwd_views_kernel": "render_bwd", "render_fwd_blk_views_kernel": "render_fwd",
          "preprocess_bwd_views_kernel": "preprocess_bwd",
+         # batched binning of the multi-view forward
+         "preprocess_views_kernel": "preprocess", "duplicate_views_kernel": "duplicate",
+         "tile_ranges_views_kernel": "ranges", "radix_totals_views_kernel": "radix_totals",
+         "radix_onesweep_views_kernel": "radix_onesweep", "scan_reduce_views_kernel": "scan_reduce",
+         "scan_final_views_kernel": "scan_final", "scan_parts_views_kernel": "scan_parts",
+         "sum_parts_views_kernel": "sum_parts", "tile_schedule_views_kernel": "schedule",
          "radix_totals_kernel": "radix_totals", "radix_onesweep_kernel": "radix_onesweep",
          "scan_reduce_kernel": "scan_reduce", "scan_final_kernel": "scan_final",
          "scan_parts_kernel": "scan_parts", "sh_precolor_kernel": "sh_precolor",

@@ -1180,6 +1180,23 @@ int views_forward_batched(const FwdModel& m, std::vector<FwdCam>& cams, gsr_view
   int per = (V + ng - 1) / ng;
   if (per > kMaxBatchViews) per = kMaxBatchViews;
   ng = (V + per - 1) / per;
+  // group boundaries: equal groups, or a first group of GSR_VIEWS_FWD_FIRST views and the rest
+  // split evenly (a smaller first group's blend starts earlier, beside the others' binning)
+  std::vector<int> gstart((size_t)ng + 1, 0);
+  {
+    static const int first_env = [] {
+      const char* e = getenv("GSR_VIEWS_FWD_FIRST");
+      return e ? atoi(e) : 0;
+    }();
+    if (first_env > 0 && first_env < V && ng > 1 && first_env <= kMaxBatchViews &&
+        (V - first_env + ng - 2) / (ng - 1) <= kMaxBatchViews) {
+      gstart[1] = first_env;
+      for (int gi = 2; gi <= ng; gi++)
+        gstart[(size_t)gi] = first_env + (int)((long long)(V - first_env) * (gi - 1) / (ng - 1));
+    } else {
+      for (int gi = 1; gi <= ng; gi++) gstart[(size_t)gi] = gi * per < V ? gi * per : V;
+    }
+  }
   struct Group {
     int v0 = 0, n = 0;
     hipStream_t st = nullptr;
@@ -1207,8 +1224,8 @@ int views_forward_batched(const FwdModel& m, std::vector<FwdCam>& cams, gsr_view
   HostTrace ht;
   auto phase1 = [&](int gi) -> int {
     Group& G = grp[(size_t)gi];
-    G.v0 = gi * per;
-    G.n = V - G.v0 < per ? V - G.v0 : per;
+    G.v0 = gstart[(size_t)gi];
+    G.n = gstart[(size_t)gi + 1] - G.v0;
     G.st = distinct[(size_t)gi % distinct.size()];
     G.ready = readback_event(gi);
     if (!G.ready) return fail(GSR_ERR_HIP, "event creation failed");
