@@ -68,7 +68,7 @@ class Opt:
 
 
 def algorithmic_bytes(stage, P, Pv, R, T, HW, D=3, C=8, tile_passes=2, acc=True, defer_sh=False,
-                      precolor=False, views=6, launch_views=1):
+                      precolor=False, views=6, launch_views=1, acc_in_blend=False):
     """Bytes each stage must move per launch.
     P Gaussians, Pv visible, R instances, T tiles, HW pixels, C blended channels (rgb, depth,
     alpha, feature x3), acc: the backward adds into existing gradients (read + write),
@@ -76,12 +76,18 @@ def algorithmic_bytes(stage, P, Pv, R, T, HW, D=3, C=8, tile_passes=2, acc=True,
     precolor: the SH rows are replaced by the pre-pass's colour + clamp (13 B, forward) and
     colour Jacobian (36 B, backward).  launch_views: views one launch covers -- per-view stages
     scale by it, except that the multi-view preprocess and per-Gaussian backward read the model
-    rows (and read-modify-write the leaf gradients) once per launch."""
+    rows (and read-modify-write the leaf gradients) once per launch.  acc_in_blend: the 64-B
+    backward accumulator rows are zeroed by the forward blend's grid (the batched multi-view
+    forward) instead of the preprocess's."""
     if stage in ("preprocess", "preprocess_bwd") and launch_views > 1:
         per, once = _model_split(stage, P, Pv, D, acc, defer_sh, precolor)
-        return launch_views * per + once
-    return launch_views * _stage_bytes(stage, P, Pv, R, T, HW, D, C, tile_passes, acc, defer_sh,
-                                       precolor, views)
+        b = launch_views * per + once
+    else:
+        b = launch_views * _stage_bytes(stage, P, Pv, R, T, HW, D, C, tile_passes, acc, defer_sh,
+                                        precolor, views)
+    if acc_in_blend and stage in ("preprocess", "render_fwd"):
+        b += launch_views * P * 64 * (1 if stage == "render_fwd" else -1)
+    return b
 
 
 def _model_split(stage, P, Pv, D, acc, defer_sh, precolor):
@@ -392,6 +398,11 @@ def main():
     T = ((W + 15) // 16) * ((H + 15) // 16)
     HW = W * H
     kernels = {}
+    # the batched multi-view forward zeroes the accumulator rows in its blend (gsr_api.cpp
+    # blend_zeroes_acc; GSR_VIEWS_BATCHED / GSR_BLEND_ZEROES_ACC = 0 turn it off)
+    acc_in_blend = (not args.per_view and os.environ.get("GSR_VIEWS_BATCHED", "1") != "0"
+                    and os.environ.get("GSR_BLEND_ZEROES_ACC", "1") != "0"
+                    and not args.autograd_grads)
     for name, (ms, calls) in stages.items():
         if calls == 0:
             continue
@@ -403,7 +414,7 @@ def main():
             vpl = max(1, int(round(len(my_cams) * stage_steps.get(name, 1) / calls)))
         b = algorithmic_bytes(name, P, Pv, R, T, HW, D=deg, acc=not args.autograd_grads,
                               defer_sh=defer_sh, precolor=not args.no_precolor,
-                              views=len(my_cams), launch_views=vpl)
+                              views=len(my_cams), launch_views=vpl, acc_in_blend=acc_in_blend)
         k = {"avg_ms": round(avg_ms, 4), "calls": int(calls), "bytes": int(b),
              "views_per_launch": vpl, "gbs": round(b / (avg_ms * 1e-3) / 1e9, 1)}
         if name in ("render_fwd", "render_bwd"):

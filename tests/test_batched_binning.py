@@ -25,7 +25,7 @@ def _away_camera(W, H, like):
     return make_camera(R, -R.T @ c, like.FoVx, like.FoVy, W, H, uid=99, device="cuda")
 
 
-@pytest.mark.parametrize("nviews", [1, 7])
+@pytest.mark.parametrize("nviews", [1, 7, 10])
 def test_batched_forward_equals_single_view(nviews):
     import diff_gaussian_rasterization as dgr
     from gaussian_renderer import render, render_views
