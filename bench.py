@@ -401,8 +401,7 @@ def main():
     # the batched multi-view forward zeroes the accumulator rows in its blend (gsr_api.cpp
     # blend_zeroes_acc; GSR_VIEWS_BATCHED / GSR_BLEND_ZEROES_ACC = 0 turn it off)
     acc_in_blend = (not args.per_view and os.environ.get("GSR_VIEWS_BATCHED", "1") != "0"
-                    and os.environ.get("GSR_BLEND_ZEROES_ACC", "1") != "0"
-                    and not args.autograd_grads)
+                    and os.environ.get("GSR_BLEND_ZEROES_ACC", "1") != "0")
     for name, (ms, calls) in stages.items():
         if calls == 0:
             continue
