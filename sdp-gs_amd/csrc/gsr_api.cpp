@@ -1101,6 +1101,14 @@ bool blend_zeroes_acc() {
   return on;
 }
 
+bool g0_on_call() {
+  static const bool on = [] {
+    const char* e = getenv("GSR_VIEWS_G0_CALL");
+    return e ? atoi(e) != 0 : true;
+  }();
+  return on;
+}
+
 // The batched path's preprocess: one multi-view launch (default) or one launch per view
 // (GSR_PRE_VIEWS=0).
 bool pre_views() {
@@ -1226,7 +1234,10 @@ int views_forward_batched(const FwdModel& m, std::vector<FwdCam>& cams, gsr_view
     Group& G = grp[(size_t)gi];
     G.v0 = gstart[(size_t)gi];
     G.n = gstart[(size_t)gi + 1] - G.v0;
-    G.st = distinct[(size_t)gi % distinct.size()];
+    // group 0 on the call's stream (GSR_VIEWS_G0_CALL, default 1): its preprocess follows the
+    // caller's last kernel (the colour pre-pass) on the same queue, without a cross-stream wait
+    G.st = (gi == 0 && g0_on_call()) ? call_stream
+                                      : distinct[(size_t)(gi - (g0_on_call() ? 1 : 0)) % distinct.size()];
     G.ready = readback_event(gi);
     if (!G.ready) return fail(GSR_ERR_HIP, "event creation failed");
     hipStream_t stream = G.st;
@@ -1587,18 +1598,27 @@ int gsr_rasterize_views_fused_backward(
   // kMaxBwdViews views (`chunks` launches; one launch's tiles are its views' tiles, so no per-view
   // tail of idle CUs); the per-Gaussian parts read-modify-write the leaves' gradients and run in
   // view order on the call's stream, each after the launch holding its view.
-  hipStream_t bs = views[0].stream ? (hipStream_t)views[0].stream : call_stream;
-  hipEvent_t start = join_event(kFwdSlots);  // the upstream gradients were produced on the call's stream
-  if (!start || hipEventRecord(start, call_stream) != hipSuccess)
-    return fail(GSR_ERR_HIP, "event record on the call's stream failed");
-  if (bs != call_stream && hipStreamWaitEvent(bs, start, 0) != hipSuccess)
-    return fail(GSR_ERR_HIP, "stream wait failed");
   static const int chunks_env = [] {
     const char* e = getenv("GSR_VIEWS_BWD_CHUNKS");
     return e ? atoi(e) : 1;
   }();
   int per = (V + (chunks_env > 0 ? chunks_env : 1) - 1) / (chunks_env > 0 ? chunks_env : 1);
   if (per > kMaxBwdViews) per = kMaxBwdViews;
+  // one chunk: the blend runs on the call's stream too (nothing to overlap it with, and no
+  // cross-stream hops before and after it); several: on views[0].stream, beside the previous
+  // chunk's per-Gaussian backward
+  static const bool side_env = [] {  // GSR_VIEWS_BWD_SIDE=1: the side stream even for one chunk
+    const char* e = getenv("GSR_VIEWS_BWD_SIDE");
+    return e && atoi(e) != 0;
+  }();
+  hipStream_t bs = (views[0].stream && (per < V || side_env)) ? (hipStream_t)views[0].stream
+                                                              : call_stream;
+  hipEvent_t start = join_event(kFwdSlots);  // the upstream gradients were produced on the call's stream
+  if (bs != call_stream) {
+    if (!start || hipEventRecord(start, call_stream) != hipSuccess)
+      return fail(GSR_ERR_HIP, "event record on the call's stream failed");
+    if (hipStreamWaitEvent(bs, start, 0) != hipSuccess) return fail(GSR_ERR_HIP, "stream wait failed");
+  }
   const int debug_sync = debug & 1;
   const bool no_blend = (debug & GSR_DEBUG_TEST_NO_BLEND) != 0;
   const bool per_view_pre = (debug & GSR_DEBUG_TEST_PER_VIEW_PRE) != 0;
