@@ -1101,12 +1101,12 @@ bool blend_zeroes_acc() {
   return on;
 }
 
-bool g0_on_call() {
-  static const bool on = [] {
+int g0_on_call() {
+  static const int mode = [] {
     const char* e = getenv("GSR_VIEWS_G0_CALL");
-    return e ? atoi(e) != 0 : true;
+    return e ? atoi(e) : 1;
   }();
-  return on;
+  return mode;
 }
 
 // The batched path's preprocess: one multi-view launch (default) or one launch per view
@@ -1236,8 +1236,13 @@ int views_forward_batched(const FwdModel& m, std::vector<FwdCam>& cams, gsr_view
     G.n = gstart[(size_t)gi + 1] - G.v0;
     // group 0 on the call's stream (GSR_VIEWS_G0_CALL, default 1): its preprocess follows the
     // caller's last kernel (the colour pre-pass) on the same queue, without a cross-stream wait
-    G.st = (gi == 0 && g0_on_call()) ? call_stream
-                                      : distinct[(size_t)(gi - (g0_on_call() ? 1 : 0)) % distinct.size()];
+    // (GSR_VIEWS_G0_CALL=2: the LAST group there instead -- the backward then follows it directly)
+    {
+      const int mode = g0_on_call();
+      const int cg = mode == 2 ? ng - 1 : (mode == 1 ? 0 : -1);  // the group on the call's stream
+      G.st = gi == cg ? call_stream
+                      : distinct[(size_t)(gi - (cg >= 0 && gi > cg ? 1 : 0)) % distinct.size()];
+    }
     G.ready = readback_event(gi);
     if (!G.ready) return fail(GSR_ERR_HIP, "event creation failed");
     hipStream_t stream = G.st;
