@@ -71,6 +71,11 @@ enum {
 // Host wall time (ms) the forward calls of this process spent waiting for their instance-count
 // read-back (hipEventSynchronize); reset != 0 zeroes the counter after reading it.
 double gsr_test_host_wait_ms(int reset);
+/* The batched forward's single-pass look-back scan (inclusive) of `views` arrays of n u32 each,
+ * back to back in `in` / `out`; scratch: views * gsr_test_scan_lookback_words(n) * 8 + 16 bytes. */
+size_t gsr_test_scan_lookback_words(size_t n);
+int gsr_test_scan_lookback(const uint32_t* in, uint32_t* out, size_t n, int views, void* scratch,
+                           void* stream);
 
 void gsr_profile_enable(int stage_mask);
 /* Waits for the recorded events, adds their durations into ms[GSR_NUM_STAGES] and

@@ -42,6 +42,7 @@ GeomState carve_geom(char* base, size_t P) {
   g.acc = c.take<float>((size_t)kAccFloats * P);
   g.ebeg = c.take<uint32_t>(P);
   g.sort = take_sort_scratch(c, P);
+  g.scan_status = c.take<uint64_t>(scan_lb_words(P));
   g.scan_parts = c.take<uint32_t>(scan_parts(P) + 1);
   g.pre_parts = c.take<uint32_t>(2 * ((P + 255) / 256) + 1);
   g.bytes = c.size();
@@ -514,8 +515,10 @@ static int fwd_prep(const FwdModel& m, FwdCam& c) {
   pa.radii = c.radii_ptr; pa.g = g;
   pa.fused = m.fused; pa.sh_dc = m.sh_dc; pa.sh_rest = m.sh_rest;
   pa.pre_color = c.pre_color; pa.pre_clamp = c.pre_clamp;
-  // the preprocess grid also zeroes the depth sort's scratch and the backward's accumulators
-  pa.clear = SideClear{g.sort.aux, sort_clear_bytes(g.sort, (size_t)P, 32)};
+  // the preprocess grid also zeroes the depth sort's scratch, the look-back scan's status words
+  // and (acc_zero) the backward's accumulators
+  pa.clear = SideClear{g.sort.aux, (size_t)((char*)(g.scan_status + scan_lb_words((size_t)P)) -
+                                            (char*)g.sort.aux)};
   pa.acc_zero = m.rows ? 0 : 1;  // the rows layout never reads the accumulator rows
   pa.parts = g.pre_parts;
   if (c.defer_pre) {  // the multi-view call launches the views' preprocesses together
@@ -1101,6 +1104,16 @@ bool blend_zeroes_acc() {
   return on;
 }
 
+// The batched forward's scan: reduce-then-scan, three launches (default), or one look-back launch
+// (GSR_SCAN_LB=1; measured 0.5-1.4 % slower per step, profiles/r03_scan_lookback_ab.txt)
+bool scan_lookback() {
+  static const bool on = [] {
+    const char* e = getenv("GSR_SCAN_LB");
+    return e ? atoi(e) != 0 : false;
+  }();
+  return on;
+}
+
 int g0_on_call() {
   static const int mode = [] {
     const char* e = getenv("GSR_VIEWS_G0_CALL");
@@ -1287,14 +1300,21 @@ int views_forward_batched(const FwdModel& m, std::vector<FwdCam>& cams, gsr_view
                                      /*precleared=*/true));
     PROF_END(DEPTH_SORT);
     ScanSpec sc[kMaxBatchViews];
+    ScanLbSpec sl[kMaxBatchViews];
     for (int l = 0; l < nl; l++) {
       FwdCam& c = cams[(size_t)G.live[(size_t)l]];
       c.depth_in_b = G.depth_in_b;
-      sc[l] = ScanSpec{G.depth_in_b ? c.g.dkey_b : c.g.dkey_a, c.g.offsets, (size_t)P,
-                       c.g.scan_parts};
+      const uint32_t* counts = G.depth_in_b ? c.g.dkey_b : c.g.dkey_a;
+      sc[l] = ScanSpec{counts, c.g.offsets, (size_t)P, c.g.scan_parts};
+      sl[l] = ScanLbSpec{counts, c.g.offsets, (size_t)P, c.g.scan_status,
+                         c.g.sort.aux + kSortAuxErr};
     }
     PROF_BEGIN(SCAN);
-    GSR_CHECK(scan_u32_views(sc, nl, true, stream));
+    if (scan_lookback()) {
+      GSR_CHECK(scan_u32_lookback_views(sl, nl, stream));
+    } else {
+      GSR_CHECK(scan_u32_views(sc, nl, true, stream));
+    }
     PROF_END(SCAN);
     return GSR_OK;
   };
@@ -1811,6 +1831,34 @@ int gsr_test_scan(const uint32_t* in, uint32_t* out, size_t n, int inclusive, vo
   if (n == 0) return GSR_OK;
   if (scan_parts(n) > (size_t)kScanMaxParts) return fail(GSR_ERR_TOO_LARGE, "n too large");
   GSR_CHECK(scan_u32(in, nullptr, out, n, inclusive != 0, (uint32_t*)scratch, stream));
+  return GSR_OK;
+}
+
+// look-back scan of `views` independent arrays in one launch (in/out: views x n u32, back to
+// back); scratch: views x gsr_test_scan_lookback_words(n) u64 words, zeroed here
+size_t gsr_test_scan_lookback_words(size_t n) { return scan_lb_words(n); }
+
+int gsr_test_scan_lookback(const uint32_t* in, uint32_t* out, size_t n, int views, void* scratch,
+                           void* stream_ptr) {
+  g_err.clear();
+  hipStream_t stream = (hipStream_t)stream_ptr;
+  const int debug = 0;
+  if (n == 0 || views <= 0) return GSR_OK;
+  if (views > kMaxBatchViews || n > 0xffffffffull) return fail(GSR_ERR_ARGUMENT, "bad sizes");
+  uint32_t* err = pinned_slot(0);
+  if (!err) return fail(GSR_ERR_HIP, "pinned host allocation failed");
+  uint64_t* st = (uint64_t*)scratch;
+  const size_t words = scan_lb_words(n);
+  // error word after the status words of every view
+  uint32_t* derr = (uint32_t*)(st + (size_t)views * words);
+  GSR_CHECK(hipMemsetAsync(scratch, 0, (size_t)views * words * 8 + 16, stream));
+  ScanLbSpec sp[kMaxBatchViews];
+  for (int k = 0; k < views; k++)
+    sp[k] = ScanLbSpec{in + (size_t)k * n, out + (size_t)k * n, n, st + (size_t)k * words, derr};
+  GSR_CHECK(scan_u32_lookback_views(sp, views, stream));
+  GSR_CHECK(hipMemcpyAsync(err, derr, 4, hipMemcpyDeviceToHost, stream));
+  GSR_CHECK(hipStreamSynchronize(stream));
+  if (*err) return fail(GSR_ERR_HIP, "scan look-back timed out");
   return GSR_OK;
 }
 

@@ -150,6 +150,18 @@ struct ScanSpec {
   uint32_t* parts;
 };
 hipError_t scan_u32_views(const ScanSpec* v, int V, bool inclusive, hipStream_t s);
+// Inclusive scans in ONE launch (decoupled look-back): status = scan_lb_words(n) zeroed u64 words
+// (a ticket counter, then one status word per kScanTile partition); err raised on a timed-out
+// look-back.
+inline size_t scan_lb_words(size_t n) { return scan_parts(n) + 1; }
+struct ScanLbSpec {
+  const uint32_t* in;
+  uint32_t* out;
+  size_t n;
+  uint64_t* status;
+  uint32_t* err;
+};
+hipError_t scan_u32_lookback_views(const ScanLbSpec* v, int V, hipStream_t s);
 // out[0..1] = sums of parts / parts2 (n partials each); host (device pointer of pinned words, or
 // null) receives {*flag0 (0 if null), out[0], out[1]}.
 struct SumSpec {
@@ -185,6 +197,9 @@ struct GeomState {
   uint32_t* flags;          // [4]  [0]: prefiltered violation
   SortScratch sort;         // depth-sort scratch
   uint32_t* scan_parts;
+  // [scan_lb_words(P)] look-back scan status (the batched forward's scan); follows the sort
+  // scratch so that the preprocess's side clear zeroes both (scan_clear_end)
+  uint64_t* scan_status;
   // [2 * ceil(P/256)] per preprocess workgroup: the sum of its exact tile counts, then (second
   // half) the sum of its full 3-sigma tile rectangles -- the reference's tiles_touched
   // (forward.cu:255), whose total is the num_rendered the boundary returns

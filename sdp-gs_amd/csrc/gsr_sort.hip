@@ -626,6 +626,96 @@ __global__ __launch_bounds__(1024) void sum_parts_kernel(const uint32_t* __restr
   }
 }
 
+// ---- single-pass inclusive scan with decoupled look-back, several views per launch -------------
+// One launch instead of scan_u32's three (reduce, one-workgroup partials scan, final): a
+// workgroup takes a ticket (its partition of kScanTile elements), scans it, publishes the
+// aggregate, and wave 0 walks back over the predecessors' status words 64 at a time until an
+// inclusive prefix (u64 words as the sort's: bits 32-33 flag, 0-31 count).  Bounded polling: a
+// timed-out look-back raises `err` (the depth sort's error word: the forward's status check
+// reports it) and the partition proceeds.  In the batched forward the one-workgroup middle pass
+// of scan_u32 waited ~80 us for a dispatch slot behind the other group's duplication.
+struct ScanLbJob {
+  const uint32_t* in;
+  uint32_t* out;
+  uint64_t* st;  // [0]: ticket counter; [1 + p]: partition p's status (zeroed before the launch)
+  uint32_t* err;
+  uint32_t n;
+};
+struct ScanLbViews {
+  ScanLbJob j[kMaxBatchViews];
+  uint32_t first[kMaxBatchViews + 1];
+  int V;
+};
+
+__global__ __launch_bounds__(kThreads) void scan_lookback_views_kernel(ScanLbViews m) {
+  __shared__ uint32_t lds[kThreads / 64];
+  __shared__ uint32_t s_part, s_prefix;
+  int k = 0;
+  while (k + 1 < m.V && blockIdx.x >= m.first[k + 1]) k++;  // workgroup-uniform
+  const ScanLbJob& job = m.j[k];
+  const int t = (int)threadIdx.x, lane = t & 63;
+  if (t == 0) s_part = atomicAdd(reinterpret_cast<uint32_t*>(job.st), 1u);
+  __syncthreads();
+  const uint32_t p = s_part;
+  const size_t base = (size_t)p * kScanTile + (size_t)t * kScanItems;
+  uint32_t v[kScanItems];
+  uint32_t sum = 0;
+#pragma unroll
+  for (int q = 0; q < kScanItems; q++) {
+    const size_t i = base + q;
+    v[q] = i < job.n ? job.in[i] : 0u;
+    sum += v[q];
+  }
+  uint32_t total;
+  const uint32_t excl = block_excl_scan<kThreads / 64>(sum, lds, total);
+  uint64_t* st = job.st + 1;
+  if (t == 0) status_store(st + p, (p == 0 ? kStIncl : kStAgg) | (uint64_t)total);
+  if (p > 0 && t < 64) {
+    uint32_t prefix = 0;
+    int64_t q = (int64_t)p - 1;
+    int spins = 0;
+    while (q >= 0) {
+      const int64_t src = q - lane;
+      const uint64_t w = src >= 0 ? status_load(st + src) : kStIncl;  // before partition 0: done
+      const uint64_t f = w & kStFlags;
+      const uint64_t incl = __ballot(f == kStIncl);
+      const uint64_t ready = __ballot(f != 0);
+      // lanes up to and including the first inclusive word (all of them if none is inclusive)
+      const int upto = incl ? __ffsll((long long)incl) - 1 : 63;
+      const uint64_t need = upto >= 63 ? ~0ull : ((2ull << upto) - 1ull);
+      if ((ready & need) == need) {
+        uint32_t x = (lane <= upto && src >= 0) ? (uint32_t)w : 0u;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) x += (uint32_t)__shfl_xor((int)x, d, 64);
+        prefix += x;
+        if (incl) break;
+        q -= 64;
+        continue;
+      }
+      if (++spins > kSpinLimit || g_force_lookback_timeout) {  // bounded: report and proceed
+        if (lane == 0) {
+          atomicOr(job.err, 1u);
+          atomicAdd(&g_lookback_timeouts, 1u);
+        }
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (lane == 0) {
+      status_store(st + p, kStIncl | (uint64_t)(prefix + total));
+      s_prefix = prefix;
+    }
+  }
+  __syncthreads();
+  uint32_t run = (p == 0 ? 0u : s_prefix) + excl;
+#pragma unroll
+  for (int q = 0; q < kScanItems; q++) {
+    const size_t i = base + q;
+    run += v[q];
+    if (i < job.n) job.out[i] = run;
+  }
+}
+
 // One workgroup per view: out = {sum parts, sum parts2}; host (device-mapped pinned words, may be
 // null) = {*flag0, the two sums}: the views' read-back is these stores plus one event, no copy.
 struct SumJob {
@@ -673,6 +763,22 @@ hipError_t sum_u32_parts_views(const SumSpec* v, int V, hipStream_t s) {
     m.j[k] = SumJob{v[k].parts, v[k].parts2, v[k].out, v[k].host, v[k].flag0, (int)v[k].n};
   }
   hipLaunchKernelGGL(sum_parts_views_kernel, dim3((unsigned)V), dim3(1024), 0, s, m);
+  return hipGetLastError();
+}
+
+hipError_t scan_u32_lookback_views(const ScanLbSpec* v, int V, hipStream_t s) {
+  if (V <= 0) return hipSuccess;
+  if (V > kMaxBatchViews) return hipErrorInvalidValue;
+  ScanLbViews m{};
+  m.V = V;
+  m.first[0] = 0;
+  for (int k = 0; k < V; k++) {
+    if (v[k].n > 0xffffffffull) return hipErrorInvalidValue;
+    m.j[k] = ScanLbJob{v[k].in, v[k].out, v[k].status, v[k].err, (uint32_t)v[k].n};
+    m.first[k + 1] = m.first[k] + (uint32_t)scan_parts(v[k].n);
+  }
+  if (m.first[V] == 0) return hipSuccess;
+  hipLaunchKernelGGL(scan_lookback_views_kernel, dim3(m.first[V]), dim3(kThreads), 0, s, m);
   return hipGetLastError();
 }
 

@@ -296,6 +296,10 @@ def load():
         L.gsr_profile_reset.argtypes = []
         L.gsr_profile_stage_name.restype = ctypes.c_char_p
         L.gsr_profile_stage_name.argtypes = [_i]
+        L.gsr_test_scan_lookback_words.restype = _sz
+        L.gsr_test_scan_lookback_words.argtypes = [_sz]
+        L.gsr_test_scan_lookback.restype = _i
+        L.gsr_test_scan_lookback.argtypes = [_p, _p, _sz, _i, _p, _p]
         L.gsr_test_host_wait_ms.restype = ctypes.c_double
         L.gsr_test_host_wait_ms.argtypes = [_i]
         _lib = L

@@ -309,6 +309,23 @@ def test_scan(n):
         np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), ref)
 
 
+@pytest.mark.parametrize("n,views", [(1, 1), (2049, 3), (1_000_000, 3), (5_000_001, 2)])
+def test_scan_lookback(n, views):
+    """The batched forward's single-pass look-back scan (gsr_sort.hip scan_lookback_views_kernel,
+    several views per launch, ticketed partitions) == numpy's inclusive cumsum of every view."""
+    from gsr_amd import _lib
+    L = _lib.load()
+    x = np.random.default_rng(n + views).integers(0, 50, size=views * n).astype(np.uint32)
+    xi = torch.tensor(x.view(np.int32), device="cuda")
+    out = torch.empty_like(xi)
+    words = int(L.gsr_test_scan_lookback_words(n))
+    scratch = torch.empty(views * words * 8 + 16, dtype=torch.uint8, device="cuda")
+    _lib.check(L.gsr_test_scan_lookback(xi.data_ptr(), out.data_ptr(), n, views,
+                                        scratch.data_ptr(), torch.cuda.current_stream().cuda_stream))
+    ref = np.cumsum(x.reshape(views, n), axis=1, dtype=np.uint64).astype(np.uint32)
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32).reshape(views, n), ref)
+
+
 def test_splat_exp_is_the_oracles_exp():
     """The blends' exp(power) (gsr_device.h splat_exp) is bit-identical to the oracle's
     (oracle/gsr_oracle.c splat_exp) -- so GPU and oracle take the same alpha >= 1/255 and
