@@ -1114,6 +1114,14 @@ bool scan_lookback() {
   return on;
 }
 
+bool render_on_call() {
+  static const bool on = [] {
+    const char* e = getenv("GSR_VIEWS_RENDER_CALL");
+    return e ? atoi(e) != 0 : false;
+  }();
+  return on;
+}
+
 int g0_on_call() {
   static const int mode = [] {
     const char* e = getenv("GSR_VIEWS_G0_CALL");
@@ -1321,6 +1329,7 @@ int views_forward_batched(const FwdModel& m, std::vector<FwdCam>& cams, gsr_view
   // phase 2 of a group: its read-back, then its binning and blend
   auto phase2 = [&](int gi) -> int {
     Group& G = grp[(size_t)gi];
+    RenderArgs ras[kMaxBatchViews];
     hipStream_t stream = G.st;
     const int nl = (int)G.live.size();
     if (nl > 0) {
@@ -1371,7 +1380,6 @@ int views_forward_batched(const FwdModel& m, std::vector<FwdCam>& cams, gsr_view
       GSR_CHECK(radix_sort_pairs_views(ts, nl, tbits, &t_in_b, stream, false, /*precleared=*/true));
       PROF_END(TILE_SORT);
       RangesSpec rs[kMaxBatchViews];
-      RenderArgs ras[kMaxBatchViews];
       for (int l = 0; l < nl; l++) {
         FwdCam& c = cams[(size_t)G.live[(size_t)l]];
         const BinState& b = c.b;
@@ -1399,6 +1407,24 @@ int views_forward_batched(const FwdModel& m, std::vector<FwdCam>& cams, gsr_view
       GSR_CHECK(launch_tile_ranges_views(rs, nl, stream));
       GSR_CHECK(launch_render_schedule_views(ras, nl, stream));
       PROF_END(RANGES);
+    }
+    // the group's stream joins the call's stream here; with GSR_VIEWS_RENDER_CALL the blend then
+    // runs on the call's stream (the blends in group order there, the backward right behind
+    // the last), else on the group's stream before the join
+    const bool on_call = render_on_call() && G.st != call_stream;
+    auto join = [&]() -> int {
+      if (G.st == call_stream) return GSR_OK;
+      hipEvent_t e = join_event(gi);
+      if (!e || hipEventRecord(e, G.st) != hipSuccess ||
+          hipStreamWaitEvent(call_stream, e, 0) != hipSuccess)
+        return fail(GSR_ERR_HIP, "joining group %d's stream failed", gi);
+      return GSR_OK;
+    };
+    if (on_call)
+      if (int rc = join()) return rc;
+    hipStream_t rstream = on_call ? call_stream : stream;
+    if (nl > 0) {
+      hipStream_t stream = rstream;
       PROF_BEGIN(RENDER_FWD);
       GSR_CHECK(launch_render_forward_views(ras, nl, stream));
       ht.mark("f", gi);
@@ -1408,17 +1434,13 @@ int views_forward_batched(const FwdModel& m, std::vector<FwdCam>& cams, gsr_view
       const int v = G.v0 + k;
       FwdCam& c = cams[(size_t)v];
       if (c.done) c.num_rendered = c.num_instances = 0;
-      if (int rc = fwd_blended(m, c, stream)) return rc;
+      if (int rc = fwd_blended(m, c, rstream)) return rc;
       gsr_view& out = views[v];
       out.geom_buffer = c.gbase; out.binning_buffer = c.bbase; out.image_buffer = c.ibase;
       out.num_rendered = c.num_rendered; out.num_instances = c.num_instances;
     }
-    if (G.st != call_stream) {
-      hipEvent_t e = join_event(gi);
-      if (!e || hipEventRecord(e, G.st) != hipSuccess ||
-          hipStreamWaitEvent(call_stream, e, 0) != hipSuccess)
-        return fail(GSR_ERR_HIP, "joining group %d's stream failed", gi);
-    }
+    if (!on_call)
+      if (int rc = join()) return rc;
     return GSR_OK;
   };
   // `lead` groups' first phases are queued ahead of the first wait; each later group's right
