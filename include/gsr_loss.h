@@ -72,6 +72,21 @@ int gsr_view_loss_backward(int C, int H, int W, const float* image, const float*
                            const float* depth_mono, float offset, float depth_weight,
                            const float* grad_total, float* grad_image, float* grad_depth,
                            void* scratch, void* stream);
+/* Up to 8 views of one training step in one launch per stage (the multi-view training step):
+ * images [V][C][H][W] and depths [V][N] back to back (the multi-view call's stacked outputs), one
+ * gt / depth_mono pointer per view, out [V][5], total [V], scratch V x
+ * gsr_view_loss_scratch_bytes(C, H, W); per view the outputs and gradients of gsr_view_loss /
+ * gsr_view_loss_backward, bit for bit (grad_total [V]: one scalar per view). */
+int gsr_view_loss_views(int V, int C, int H, int W, const float* images, const float* const* gts,
+                        float lambda_dssim, int64_t N, const float* depths,
+                        const float* const* depth_monos, float offset, float depth_weight,
+                        int need_grad, float* out, float* total, void* scratch, void* stream);
+int gsr_view_loss_views_backward(int V, int C, int H, int W, const float* images,
+                                 const float* const* gts, float lambda_dssim, int64_t N,
+                                 const float* depths, const float* const* depth_monos,
+                                 float offset, float depth_weight, const float* grad_total,
+                                 float* grad_images, float* grad_depths, void* scratch,
+                                 void* stream);
 
 #ifdef __cplusplus
 }

@@ -127,9 +127,10 @@ struct SsimArgs {
 
 // one 32x32 output tile (bx, by) of channel c; its partial sums go to parts[2 * b]
 __device__ __forceinline__ void ssim_fwd_tile(const SsimArgs& a, int bx, int by, int c, size_t b) {
-  // the blurs and the map may contract to FMA (the reference's conv2d fixes no evaluation order;
-  // parity is against float64, tests/test_losses.py)
-#pragma clang fp contract(fast)
+  // the blurs are explicit FMA chains and nothing else contracts: every kernel that inlines this
+  // tile (the photometric loss, the training views' loss) computes the same bits (the reference's
+  // conv2d fixes no evaluation order; parity is against float64, tests/test_losses.py)
+#pragma clang fp contract(off)
   __shared__ __attribute__((aligned(16))) float sxy[2][kIY][kSX];
   __shared__ float h[5][kIY][kTX];
   float (*sx)[kSX] = sxy[0];
@@ -152,11 +153,11 @@ __device__ __forceinline__ void ssim_fwd_tile(const SsimArgs& a, int bx, int by,
 #pragma unroll
       for (int k = 0; k < kW; k++) {
         const float uk = u[j + k], vk = v[j + k], w = a.win.w[k];
-        m1 += w * uk;
-        m2 += w * vk;
-        e11 += w * (uk * uk);
-        e22 += w * (vk * vk);
-        e12 += w * (uk * vk);
+        m1 = __builtin_fmaf(w, uk, m1);
+        m2 = __builtin_fmaf(w, vk, m2);
+        e11 = __builtin_fmaf(w, uk * uk, e11);
+        e22 = __builtin_fmaf(w, vk * vk, e22);
+        e12 = __builtin_fmaf(w, uk * vk, e12);
       }
       h[0][r][q0 + j] = m1;
       h[1][r][q0 + j] = m2;
@@ -182,11 +183,11 @@ __device__ __forceinline__ void ssim_fwd_tile(const SsimArgs& a, int bx, int by,
 #pragma unroll
     for (int k = 0; k < kW; k++) {
       const float w = a.win.w[k];
-      mu1 += w * col[0][i + k];
-      mu2 += w * col[1][i + k];
-      e11 += w * col[2][i + k];
-      e22 += w * col[3][i + k];
-      e12 += w * col[4][i + k];
+      mu1 = __builtin_fmaf(w, col[0][i + k], mu1);
+      mu2 = __builtin_fmaf(w, col[1][i + k], mu2);
+      e11 = __builtin_fmaf(w, col[2][i + k], e11);
+      e22 = __builtin_fmaf(w, col[3][i + k], e22);
+      e12 = __builtin_fmaf(w, col[4][i + k], e12);
     }
     // _ssim (loss_utils.py:143-162), same expression order
     const float mu1_sq = mu1 * mu1, mu2_sq = mu2 * mu2, mu1_mu2 = mu1 * mu2;
@@ -255,7 +256,7 @@ struct SsimBwdArgs {
 };
 
 __device__ __forceinline__ void ssim_bwd_tile(const SsimBwdArgs& a, int bx, int by, int c) {
-#pragma clang fp contract(fast)
+#pragma clang fp contract(off)  // explicit FMA blurs, as ssim_fwd_tile
   __shared__ __attribute__((aligned(16))) float s[3][kIY][kSX];
   __shared__ float h[3][kIY][kTX];
   const int x0 = bx * kTX, y0 = by * kTY;
@@ -279,7 +280,7 @@ __device__ __forceinline__ void ssim_bwd_tile(const SsimBwdArgs& a, int bx, int 
       for (int j = 0; j < kHS; j++) {
         float acc = 0.f;
 #pragma unroll
-        for (int k = 0; k < kW; k++) acc += a.win.w[k] * v[j + k];
+        for (int k = 0; k < kW; k++) acc = __builtin_fmaf(a.win.w[k], v[j + k], acc);
         h[m][r][q0 + j] = acc;
       }
     }
@@ -300,9 +301,9 @@ __device__ __forceinline__ void ssim_bwd_tile(const SsimBwdArgs& a, int bx, int 
 #pragma unroll
     for (int k = 0; k < kW; k++) {
       const float w = a.win.w[k];
-      u0 += w * col[0][i + k];
-      u1 += w * col[1][i + k];
-      u2 += w * col[2][i + k];
+      u0 = __builtin_fmaf(w, col[0][i + k], u0);
+      u1 = __builtin_fmaf(w, col[1][i + k], u1);
+      u2 = __builtin_fmaf(w, col[2][i + k], u2);
     }
     const size_t o = plane + (size_t)gy * a.W + gx;
     const float xv = a.x[o], yv = a.y[o];
@@ -523,19 +524,22 @@ __device__ void view_pearson_partial(const ViewLossArgs& a, int b) {
   }
 }
 
-__global__ __launch_bounds__(kThreads) void view_loss_fwd_kernel(ViewLossArgs a) {
+// (bodies shared by the one-view kernels and the several-views kernels: blk = the workgroup's
+// index inside its view's grid)
+__device__ __forceinline__ void view_loss_fwd_body(const ViewLossArgs& a, int blk) {
   // the Pearson blocks come first in the grid, so they run beside the SSIM tiles, not after them
-  const int b = (int)blockIdx.x - a.npb;
+  const int b = blk - a.npb;
   if (b >= 0) {
     const int per = a.gx * a.gy;
     const int c = b / per, r = b - c * per;
     ssim_fwd_tile(a.ss, r % a.gx, r / a.gx, c, (size_t)b);
   } else {
-    view_pearson_partial(a, (int)blockIdx.x);
+    view_pearson_partial(a, blk);
   }
 }
 
-__global__ __launch_bounds__(kThreads) void view_loss_finish_kernel(ViewLossArgs a) {
+
+__device__ __forceinline__ void view_loss_finish_body(const ViewLossArgs& a) {
   __shared__ double s[2][kThreads];
   __shared__ double q[kViewPearsonSums][kThreads / 64];
   // SSIM / L1 means exactly as ssim_reduce_kernel
@@ -605,6 +609,7 @@ __global__ __launch_bounds__(kThreads) void view_loss_finish_kernel(ViewLossArgs
   *a.total = total;
 }
 
+
 struct ViewLossBwdArgs {
   SsimBwdArgs ss;
   int nssim, gx, gy;
@@ -616,8 +621,8 @@ struct ViewLossBwdArgs {
   float* dd;
 };
 
-__global__ __launch_bounds__(kThreads) void view_loss_bwd_kernel(ViewLossBwdArgs a) {
-  const int b = (int)blockIdx.x - a.npe;
+__device__ __forceinline__ void view_loss_bwd_body(const ViewLossBwdArgs& a, int blk) {
+  const int b = blk - a.npe;
   if (b >= 0) {
     const int per = a.gx * a.gy;
     const int c = b / per, r = b - c * per;
@@ -625,7 +630,7 @@ __global__ __launch_bounds__(kThreads) void view_loss_bwd_kernel(ViewLossBwdArgs
     return;
   }
   // pearson_bwd_kernel's element work with grad_loss = g_total * depth_weight (as torch's g * w)
-  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  const int64_t i = (int64_t)blk * kThreads + threadIdx.x;
   if (i >= a.pa.N) return;
   const int v = *a.sel;
   const double* acc = a.pa.acc + (size_t)v * 8;
@@ -639,6 +644,40 @@ __global__ __launch_bounds__(kThreads) void view_loss_bwd_kernel(ViewLossBwdArgs
   const double yv = (double)a.pa.y[i];
   const double inv = 1.0 / sqrt(sxx * syy);
   a.dd[i] = (float)(gk * ((xv - mx) * inv - rr * (yv - my) / syy));
+}
+
+
+// Several training views' losses per launch (the multi-view training step, losses.train_views_loss):
+// workgroup b belongs to view k with first[k] <= b < first[k + 1]; per view exactly the one-view
+// kernels' arithmetic, so every view's outputs and gradients are bitwise those of gsr_view_loss.
+constexpr int kMaxLossViews = 8;
+struct ViewLossViews {
+  ViewLossArgs v[kMaxLossViews];
+  uint32_t first[kMaxLossViews + 1];
+  int V;
+};
+struct ViewLossBwdViews {
+  ViewLossBwdArgs v[kMaxLossViews];
+  uint32_t first[kMaxLossViews + 1];
+  int V;
+};
+static_assert(sizeof(ViewLossViews) <= 4096 && sizeof(ViewLossBwdViews) <= 4096,
+              "kernel argument size");
+__device__ __forceinline__ int loss_view(const uint32_t* first, int V, uint32_t b) {
+  int k = 0;
+  while (k + 1 < V && b >= first[k + 1]) k++;
+  return k;
+}
+__global__ __launch_bounds__(kThreads) void view_loss_fwd_views_kernel(ViewLossViews m) {
+  const int k = loss_view(m.first, m.V, blockIdx.x);
+  view_loss_fwd_body(m.v[k], (int)(blockIdx.x - m.first[k]));
+}
+__global__ __launch_bounds__(kThreads) void view_loss_finish_views_kernel(ViewLossViews m) {
+  view_loss_finish_body(m.v[blockIdx.x]);  // one workgroup per view
+}
+__global__ __launch_bounds__(kThreads) void view_loss_bwd_views_kernel(ViewLossBwdViews m) {
+  const int k = loss_view(m.first, m.V, blockIdx.x);
+  view_loss_bwd_body(m.v[k], (int)(blockIdx.x - m.first[k]));
 }
 
 }  // namespace
@@ -827,14 +866,10 @@ static void carve_view(void* scratch, int C, int H, int W, float** A, float** B,
   *pparts = c.take<double>((size_t)kViewPearsonMaxBlocks * kViewPearsonSums);
 }
 
-extern "C" int gsr_view_loss(int C, int H, int W, const float* image, const float* gt,
-                             float lambda_dssim, int64_t N, const float* depth,
-                             const float* depth_mono, float offset, float depth_weight,
-                             int need_grad, float* out, float* total, void* scratch,
-                             void* stream) {
-  if (C <= 0 || H <= 0 || W <= 0 || N < 2 || !image || !gt || !depth || !depth_mono || !out ||
-      !total || !scratch)
-    return 1;
+static ViewLossArgs view_loss_args(int C, int H, int W, const float* image, const float* gt,
+                                   float lambda_dssim, int64_t N, const float* depth,
+                                   const float* depth_mono, float offset, float depth_weight,
+                                   int need_grad, float* out, float* total, void* scratch) {
   ViewLossArgs a{};
   a.ss.C = C; a.ss.H = H; a.ss.W = W;
   a.ss.x = image; a.ss.y = gt;
@@ -855,21 +890,38 @@ extern "C" int gsr_view_loss(int C, int H, int W, const float* image, const floa
   a.out = out; a.total = total;
   a.inv_count = 1.0 / ((double)C * H * W);
   a.lambda = lambda_dssim;
+  return a;
+}
+
+extern "C" int gsr_view_loss(int C, int H, int W, const float* image, const float* gt,
+                             float lambda_dssim, int64_t N, const float* depth,
+                             const float* depth_mono, float offset, float depth_weight,
+                             int need_grad, float* out, float* total, void* scratch,
+                             void* stream) {
+  if (C <= 0 || H <= 0 || W <= 0 || N < 2 || !image || !gt || !depth || !depth_mono || !out ||
+      !total || !scratch)
+    return 1;
+  // the several-views kernels with one view: the single-view and the multi-view training steps
+  // run the same compiled code (the SSIM tiles contract to FMA per instance), so their losses and
+  // gradients agree bit for bit
+  ViewLossViews m{};
+  m.V = 1;
+  m.v[0] = view_loss_args(C, H, W, image, gt, lambda_dssim, N, depth, depth_mono, offset,
+                          depth_weight, need_grad, out, total, scratch);
+  m.first[0] = 0;
+  m.first[1] = (uint32_t)(m.v[0].nssim + m.v[0].npb);
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(view_loss_fwd_kernel, dim3((unsigned)(a.nssim + a.npb)), dim3(kThreads), 0, s,
-                     a);
-  hipLaunchKernelGGL(view_loss_finish_kernel, dim3(1), dim3(kThreads), 0, s, a);
+  hipLaunchKernelGGL(view_loss_fwd_views_kernel, dim3(m.first[1]), dim3(kThreads), 0, s, m);
+  hipLaunchKernelGGL(view_loss_finish_views_kernel, dim3(1), dim3(kThreads), 0, s, m);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
-extern "C" int gsr_view_loss_backward(int C, int H, int W, const float* image, const float* gt,
-                                      float lambda_dssim, int64_t N, const float* depth,
-                                      const float* depth_mono, float offset, float depth_weight,
-                                      const float* grad_total, float* grad_image,
-                                      float* grad_depth, void* scratch, void* stream) {
-  if (C <= 0 || H <= 0 || W <= 0 || N < 2 || !image || !gt || !depth || !depth_mono ||
-      !grad_total || !grad_image || !grad_depth || !scratch)
-    return 1;
+static ViewLossBwdArgs view_loss_bwd_args(int C, int H, int W, const float* image,
+                                          const float* gt, float lambda_dssim, int64_t N,
+                                          const float* depth, const float* depth_mono,
+                                          float offset, float depth_weight,
+                                          const float* grad_total, float* grad_image,
+                                          float* grad_depth, void* scratch) {
   ViewLossBwdArgs a{};
   a.ss.C = C; a.ss.H = H; a.ss.W = W;
   a.ss.x = image; a.ss.y = gt;
@@ -893,7 +945,80 @@ extern "C" int gsr_view_loss_backward(int C, int H, int W, const float* image, c
   a.depth_weight = depth_weight;
   a.dd = grad_depth;
   a.npe = (int)((N + kThreads - 1) / kThreads);
-  const unsigned nb = (unsigned)(a.nssim + a.npe);
-  hipLaunchKernelGGL(view_loss_bwd_kernel, dim3(nb), dim3(kThreads), 0, (hipStream_t)stream, a);
+  return a;
+}
+
+extern "C" int gsr_view_loss_backward(int C, int H, int W, const float* image, const float* gt,
+                                      float lambda_dssim, int64_t N, const float* depth,
+                                      const float* depth_mono, float offset, float depth_weight,
+                                      const float* grad_total, float* grad_image,
+                                      float* grad_depth, void* scratch, void* stream) {
+  if (C <= 0 || H <= 0 || W <= 0 || N < 2 || !image || !gt || !depth || !depth_mono ||
+      !grad_total || !grad_image || !grad_depth || !scratch)
+    return 1;
+  ViewLossBwdViews m{};  // (one view: see gsr_view_loss)
+  m.V = 1;
+  m.v[0] = view_loss_bwd_args(C, H, W, image, gt, lambda_dssim, N, depth, depth_mono, offset,
+                              depth_weight, grad_total, grad_image, grad_depth, scratch);
+  m.first[0] = 0;
+  m.first[1] = (uint32_t)(m.v[0].nssim + m.v[0].npe);
+  hipLaunchKernelGGL(view_loss_bwd_views_kernel, dim3(m.first[1]), dim3(kThreads), 0,
+                     (hipStream_t)stream, m);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+// V views back to back: images [V][C][H][W], depths [V][N], grads alike; gts / depth_monos one
+// pointer per view; out [V][5], total [V]; scratch V x gsr_view_loss_scratch_bytes(C, H, W).
+extern "C" int gsr_view_loss_views(int V, int C, int H, int W, const float* images,
+                                   const float* const* gts, float lambda_dssim, int64_t N,
+                                   const float* depths, const float* const* depth_monos,
+                                   float offset, float depth_weight, int need_grad, float* out,
+                                   float* total, void* scratch, void* stream) {
+  if (V <= 0 || V > kMaxLossViews || C <= 0 || H <= 0 || W <= 0 || N < 2 || !images || !gts ||
+      !depths || !depth_monos || !out || !total || !scratch)
+    return 1;
+  const size_t sb = gsr_view_loss_scratch_bytes(C, H, W);
+  const size_t img = (size_t)C * H * W;
+  ViewLossViews m{};
+  m.V = V;
+  m.first[0] = 0;
+  for (int k = 0; k < V; k++) {
+    if (!gts[k] || !depth_monos[k]) return 1;
+    m.v[k] = view_loss_args(C, H, W, images + (size_t)k * img, gts[k], lambda_dssim, N,
+                            depths + (size_t)k * N, depth_monos[k], offset, depth_weight,
+                            need_grad, out + 5 * k, total + k, (char*)scratch + (size_t)k * sb);
+    m.first[k + 1] = m.first[k] + (uint32_t)(m.v[k].nssim + m.v[k].npb);
+  }
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(view_loss_fwd_views_kernel, dim3(m.first[V]), dim3(kThreads), 0, s, m);
+  hipLaunchKernelGGL(view_loss_finish_views_kernel, dim3((unsigned)V), dim3(kThreads), 0, s, m);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+extern "C" int gsr_view_loss_views_backward(int V, int C, int H, int W, const float* images,
+                                            const float* const* gts, float lambda_dssim,
+                                            int64_t N, const float* depths,
+                                            const float* const* depth_monos, float offset,
+                                            float depth_weight, const float* grad_total,
+                                            float* grad_images, float* grad_depths,
+                                            void* scratch, void* stream) {
+  if (V <= 0 || V > kMaxLossViews || C <= 0 || H <= 0 || W <= 0 || N < 2 || !images || !gts ||
+      !depths || !depth_monos || !grad_total || !grad_images || !grad_depths || !scratch)
+    return 1;
+  const size_t sb = gsr_view_loss_scratch_bytes(C, H, W);
+  const size_t img = (size_t)C * H * W;
+  ViewLossBwdViews m{};
+  m.V = V;
+  m.first[0] = 0;
+  for (int k = 0; k < V; k++) {
+    if (!gts[k] || !depth_monos[k]) return 1;
+    m.v[k] = view_loss_bwd_args(C, H, W, images + (size_t)k * img, gts[k], lambda_dssim, N,
+                                depths + (size_t)k * N, depth_monos[k], offset, depth_weight,
+                                grad_total + k, grad_images + (size_t)k * img,
+                                grad_depths + (size_t)k * N, (char*)scratch + (size_t)k * sb);
+    m.first[k + 1] = m.first[k] + (uint32_t)(m.v[k].nssim + m.v[k].npe);
+  }
+  hipLaunchKernelGGL(view_loss_bwd_views_kernel, dim3(m.first[V]), dim3(kThreads), 0,
+                     (hipStream_t)stream, m);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }

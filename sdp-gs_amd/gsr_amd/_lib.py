@@ -248,6 +248,12 @@ def load():
         L.gsr_view_loss_backward.restype = _i
         L.gsr_view_loss_backward.argtypes = [_i, _i, _i, _p, _p, _f, _i64, _p, _p, _f, _f, _p, _p,
                                              _p, _p, _p]
+        L.gsr_view_loss_views.restype = _i
+        L.gsr_view_loss_views.argtypes = [_i, _i, _i, _i, _p, _p, _f, _i64, _p, _p, _f, _f, _i,
+                                          _p, _p, _p, _p]
+        L.gsr_view_loss_views_backward.restype = _i
+        L.gsr_view_loss_views_backward.argtypes = [_i, _i, _i, _i, _p, _p, _f, _i64, _p, _p, _f,
+                                                   _f, _p, _p, _p, _p, _p]
         # include/gsr_knn.h
         L.gsr_knn_scratch_bytes.restype = _sz
         L.gsr_knn_scratch_bytes.argtypes = [_i64]

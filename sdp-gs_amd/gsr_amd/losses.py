@@ -17,6 +17,8 @@ pearson_corrcoef, `depth` of depth_pearson_loss).  No CPU path.
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
 
 from . import _lib
@@ -245,6 +247,94 @@ class _TrainViewLoss(torch.autograd.Function):
         return (dx if ctx.needs_input_grad[0] else None,
                 dd.view(ctx.dshape) if ctx.needs_input_grad[1] else None,
                 None, None, None, None, None)
+
+
+class _TrainViewsLoss(torch.autograd.Function):
+    """train_view_loss for the V views of a multi-view step as ONE autograd node over
+    gsr_view_loss_views: images [V,C,H,W] and depths [V,...] are the multi-view call's stacked
+    outputs, so the gradient reaches them as [V,...] tensors directly (no per-view slices to
+    stack); per view the values are gsr_view_loss's, bit for bit."""
+
+    @staticmethod
+    def forward(ctx, images, depths, gts, monos, lambda_dssim, depth_weight, offset):
+        _cuda(images, depths, *gts, *monos)
+        V = int(images.shape[0])
+        if images.dim() != 4 or len(gts) != V or len(monos) != V or depths.shape[0] != V:
+            raise ValueError("train_views_loss expects images [V,C,H,W], depths [V,...] and V "
+                             "ground truths / monocular depths")
+        x = images.detach().contiguous().float()
+        d = depths.detach().reshape(V, -1).contiguous().float()
+        C, H, W = (int(n) for n in x.shape[1:])
+        N = int(d.shape[1])
+        ys = [g.detach().contiguous().float() for g in gts]
+        ms = [m.detach().reshape(-1).contiguous().float() for m in monos]
+        for y, m in zip(ys, ms):
+            if tuple(y.shape) != (C, H, W) or m.numel() != N:
+                raise ValueError("every gt must be [C,H,W] and every depth_mono N pixels")
+        L = _lib.load()
+        dev = x.device
+        s = _stream(x)
+        kv = ("views", V, C, H, W, dev.index, s)
+        sv = _take(kv, V * int(L.gsr_view_loss_scratch_bytes(C, H, W)), dev)
+        out = torch.empty((V, 5), dtype=torch.float32, device=dev)
+        total = torch.empty(V, dtype=torch.float32, device=dev)
+        need = int(images.requires_grad or depths.requires_grad)
+        gp = (ctypes.c_void_p * V)(*[y.data_ptr() for y in ys])
+        mp = (ctypes.c_void_p * V)(*[m.data_ptr() for m in ms])
+        with _lib.on_device(dev):
+            _check(L.gsr_view_loss_views(V, C, H, W, x.data_ptr(), gp, float(lambda_dssim), N,
+                                         d.data_ptr(), mp, float(offset), float(depth_weight),
+                                         need, out.data_ptr(), total.data_ptr(), sv.data_ptr(), s),
+                   "gsr_view_loss_views")
+        if need:
+            ctx.save_for_backward(x, d, *ys, *ms)
+            ctx.V = V
+            ctx.bufs = (kv, sv)
+            ctx.args = (float(lambda_dssim), float(depth_weight), float(offset))
+            ctx.dshape = depths.shape
+        else:
+            _give(kv, sv)
+        ctx.mark_non_differentiable(out)
+        ctx.set_materialize_grads(False)
+        return total, out
+
+    @staticmethod
+    def backward(ctx, g_total, g_out):
+        saved = ctx.saved_tensors
+        V = ctx.V
+        x, d, ys, ms = saved[0], saved[1], saved[2:2 + V], saved[2 + V:]
+        kv, sv = ctx.bufs
+        lam, w, offset = ctx.args
+        C, H, W = (int(n) for n in x.shape[1:])
+        if g_total is None:
+            _give(kv, sv)
+            return None, None, None, None, None, None, None
+        L = _lib.load()
+        g = g_total.reshape(V).contiguous().float()
+        dx = torch.empty_like(x)
+        dd = torch.empty_like(d)
+        gp = (ctypes.c_void_p * V)(*[y.data_ptr() for y in ys])
+        mp = (ctypes.c_void_p * V)(*[m.data_ptr() for m in ms])
+        with _lib.on_device(x.device):
+            _check(L.gsr_view_loss_views_backward(V, C, H, W, x.data_ptr(), gp, lam,
+                                                  int(d.shape[1]), d.data_ptr(), mp, offset, w,
+                                                  g.data_ptr(), dx.data_ptr(), dd.data_ptr(),
+                                                  sv.data_ptr(), _stream(x)),
+                   "gsr_view_loss_views_backward")
+        _give(kv, sv)
+        return (dx if ctx.needs_input_grad[0] else None,
+                dd.view(ctx.dshape) if ctx.needs_input_grad[1] else None,
+                None, None, None, None, None)
+
+
+def train_views_loss(images, depths, gt_images, depth_monos, lambda_dssim=0.2, depth_weight=0.05,
+                     offset=200.0):
+    """train_view_loss of V views at once (at most 8): images [V,C,H,W], depths [V,...] (e.g.
+    gaussian_renderer.render_views' stacked outputs), sequences of V ground truths and monocular
+    depths.  Returns (the V totals [V], the outputs [V,5]: photometric, L1, SSIM, depth term,
+    total); every view's values equal train_view_loss's."""
+    return _TrainViewsLoss.apply(images, depths, tuple(gt_images), tuple(depth_monos),
+                                 lambda_dssim, depth_weight, offset)
 
 
 def train_view_loss(image, depth, gt_image, depth_mono, lambda_dssim=0.2, depth_weight=0.05,

@@ -130,9 +130,20 @@ def train_step_views(model, cams: Sequence, gt_images: Sequence[torch.Tensor],
 
     if multi:
         def all_views(cs, strs):
+            from .losses import train_views_loss
             pkgs = render_views(cs, model, pipe, bg, args, streams=strs)
-            losses = [_view_loss(pkg, *gts[id(c)], args) for c, pkg in zip(cs, pkgs)]
-            torch.autograd.backward(losses)
+            st = pkgs[0].get("views") if pkgs else None
+            monos_ = [gts[id(c)][1] for c in cs]
+            if st is not None and len(cs) <= 8 and all(m is not None for m in monos_):
+                # every view's loss in one node over the stacked outputs (one launch per stage)
+                totals, _ = train_views_loss(st["render"], st["depth"],
+                                             [gts[id(c)][0] for c in cs], monos_,
+                                             args.lambda_dssim, args.depth_weight)
+                totals.backward(torch.ones_like(totals))
+                losses = list(totals.detach().unbind(0))
+            else:
+                losses = [_view_loss(pkg, *gts[id(c)], args) for c, pkg in zip(cs, pkgs)]
+                torch.autograd.backward(losses)
             with torch.no_grad():
                 if iteration < args.densify_until_iter:
                     for pkg in pkgs:

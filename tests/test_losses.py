@@ -138,3 +138,36 @@ def test_train_view_loss_equals_the_two_terms(flip):
         torch.testing.assert_close(a_img.grad, b_img.grad, atol=0, rtol=0)
         torch.testing.assert_close(a_dep.grad, b_dep.grad,
                                    atol=1e-6 * float(b_dep.grad.abs().max()), rtol=0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("V", [1, 3, 6])
+def test_train_views_loss_equals_per_view(V):
+    """The multi-view step's loss node (losses.train_views_loss: every view's SSIM / L1 / Pearson in
+    one launch per stage over the stacked [V,...] outputs) equals train_view_loss view by view,
+    bitwise: totals, outputs and both gradients (each view's own upstream scalar)."""
+    g = torch.Generator(device="cuda").manual_seed(5)
+    H, W = 61, 97
+    imgs, gts, monos, deps = [], [], [], []
+    for v in range(V):
+        img, gt = _images(3, H, W, seed=40 + v)
+        mono = torch.rand((1, H, W), generator=g, device="cuda") * 50 + 1
+        base = (1 / (-mono + 200)) if v % 2 else mono
+        deps.append(base * 3 + 0.05 * base.std() * torch.randn(mono.shape, generator=g, device="cuda"))
+        imgs.append(img)
+        gts.append(gt)
+        monos.append(mono)
+    scale = torch.arange(1, V + 1, dtype=torch.float32, device="cuda")
+    a_img = torch.stack(imgs).requires_grad_(True)
+    a_dep = torch.stack(deps).requires_grad_(True)
+    tot, out = losses.train_views_loss(a_img, a_dep, gts, monos, 0.2, 0.05)
+    (tot * scale).sum().backward()
+    for v in range(V):
+        b_img = imgs[v].clone().requires_grad_(True)
+        b_dep = deps[v].clone().requires_grad_(True)
+        t1, l1 = losses.train_view_loss(b_img, b_dep, gts[v], monos[v], 0.2, 0.05)
+        (t1 * scale[v]).backward()
+        assert torch.equal(tot[v], t1), v
+        assert torch.equal(out[v, 1], l1), v
+        assert torch.equal(a_img.grad[v], b_img.grad), v
+        assert torch.equal(a_dep.grad[v], b_dep.grad), v
