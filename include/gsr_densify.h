@@ -33,6 +33,12 @@ extern "C" {
 int gsr_densify_stats(int64_t P, const float* viewspace_grad, int64_t grad_stride,
                       const int32_t* radii, const uint8_t* update_filter, float* max_radii2D,
                       float* grad_accum, float* denom, void* stream);
+/* The same for the V views of a multi-view step in one launch (filter radii > 0): view v's
+ * gradient rows start at viewspace_grad + v * grad_view_stride, its radii at radii + v * P; per
+ * Gaussian the views are applied in order, so the result equals V calls of gsr_densify_stats. */
+int gsr_densify_stats_views(int V, int64_t P, const float* viewspace_grad, int64_t grad_stride,
+                            int64_t grad_view_stride, const int32_t* radii, float* max_radii2D,
+                            float* grad_accum, float* denom, void* stream);
 
 /* flag bits written by gsr_densify_classify */
 #define GSR_DENSIFY_CLONE 1u       /* |accum/denom| >= grad_threshold && max scale <= scale_limit */

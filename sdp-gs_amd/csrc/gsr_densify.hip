@@ -51,6 +51,40 @@ __global__ __launch_bounds__(kThreads) void stats_kernel(int64_t P, const float*
   }
 }
 
+// The same update for the V views of a multi-view step in one launch: per Gaussian the views in
+// order (the per-view launches' additions and maxima, in the same order), filter radii > 0.
+__global__ __launch_bounds__(kThreads) void stats_views_kernel(int V, int64_t P,
+                                                               const float* __restrict__ g,
+                                                               int64_t ld, int64_t gview,
+                                                               const int32_t* __restrict__ radii,
+                                                               float* __restrict__ maxr,
+                                                               float* __restrict__ accum,
+                                                               float* __restrict__ denom) {
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= P) return;
+  float m = maxr ? maxr[i] : 0.f, acc = accum ? accum[i] : 0.f, den = accum ? denom[i] : 0.f;
+  bool any = false;
+  for (int v = 0; v < V; v++) {
+    const int32_t rv = radii[(size_t)v * P + i];
+    if (!(rv > 0)) continue;
+    any = true;
+    const float r = (float)rv;
+    m = (m > r || m != m) ? m : r;  // torch.maximum: NaN propagates
+    const float* gv = g + (size_t)v * gview + i * ld;
+    if (accum) {
+      const float gx = gv[0], gy = gv[1];
+      acc = acc + sqrtf(gx * gx + gy * gy);
+      den = den + 1.0f;
+    }
+  }
+  if (!any) return;
+  if (maxr) maxr[i] = m;
+  if (accum) {
+    accum[i] = acc;
+    denom[i] = den;
+  }
+}
+
 // ---- densify_and_prune decisions -------------------------------------------------------------------
 struct ClassifyArgs {
   int64_t P;
@@ -258,6 +292,20 @@ extern "C" int gsr_densify_stats(int64_t P, const float* viewspace_grad, int64_t
   hipLaunchKernelGGL(stats_kernel, dim3((unsigned)((P + kThreads - 1) / kThreads)), dim3(kThreads),
                      0, (hipStream_t)stream, P, viewspace_grad, grad_stride, radii, update_filter,
                      max_radii2D, grad_accum, denom);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+extern "C" int gsr_densify_stats_views(int V, int64_t P, const float* viewspace_grad,
+                                       int64_t grad_stride, int64_t grad_view_stride,
+                                       const int32_t* radii, float* max_radii2D,
+                                       float* grad_accum, float* denom, void* stream) {
+  if (V < 0 || P < 0 || !radii || ((grad_accum != nullptr) != (denom != nullptr)) ||
+      (grad_accum && (!viewspace_grad || grad_stride < 2)))
+    return 1;
+  if (P == 0 || V == 0) return 0;
+  hipLaunchKernelGGL(stats_views_kernel, dim3((unsigned)((P + kThreads - 1) / kThreads)),
+                     dim3(kThreads), 0, (hipStream_t)stream, V, P, viewspace_grad, grad_stride,
+                     grad_view_stride, radii, max_radii2D, grad_accum, denom);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 

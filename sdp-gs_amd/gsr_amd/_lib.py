@@ -217,6 +217,8 @@ def load():
         _u32 = ctypes.c_uint32
         L.gsr_densify_stats.restype = _i
         L.gsr_densify_stats.argtypes = [_i64, _p, _i64, _p, _p, _p, _p, _p, _p]
+        L.gsr_densify_stats_views.restype = _i
+        L.gsr_densify_stats_views.argtypes = [_i, _i64, _p, _i64, _i64, _p, _p, _p, _p, _p]
         L.gsr_densify_classify.restype = _i
         L.gsr_densify_classify.argtypes = [_i64, _p, _p, _p, _p, _f, _f, _f, _i, _f, _p, _p, _p]
         L.gsr_select_scratch_bytes.restype = _sz

@@ -164,6 +164,33 @@ def _stats(self, grad, radii, filt, with_radii, with_grad):
     _STATS_EVENT[dev.index] = (ev, stream.stream_id)
 
 
+def update_densification_stats_views(self, viewspace_grads, radii):
+    """update_densification_stats of the V views of a multi-view step (render_views' stacked
+    outputs: viewspace_grads [V,P,>=2] = the stacked means2D's .grad, radii [V,P]) in one launch,
+    visibility radii > 0; equals V calls in view order."""
+    P = _rows(self.xyz_gradient_accum)
+    _cuda(viewspace_grads, radii)
+    V = int(radii.shape[0])
+    assert radii.dtype == torch.int32 and radii.is_contiguous() and radii.numel() == V * P
+    g = viewspace_grads
+    assert g.dim() == 3 and g.shape[0] == V and g.shape[1] == P and g.stride(2) == 1
+    for t in (self.xyz_gradient_accum, self.denom, self.max_radii2D):
+        assert t.is_contiguous() and t.numel() == P
+    dev = self.xyz_gradient_accum.device
+    stream = torch.cuda.current_stream(dev)
+    prev = _STATS_EVENT.get(dev.index)
+    if prev is not None and prev[1] != stream.stream_id:
+        stream.wait_event(prev[0])
+    with _lib.on_device(dev):
+        _check(_lib.load().gsr_densify_stats_views(
+            V, P, _ptr(g), g.stride(1), g.stride(0), _ptr(radii), _ptr(self.max_radii2D),
+            _ptr(self.xyz_gradient_accum), _ptr(self.denom), _stream(dev)),
+            "gsr_densify_stats_views")
+    ev = torch.cuda.Event()
+    ev.record(stream)
+    _STATS_EVENT[dev.index] = (ev, stream.stream_id)
+
+
 def add_densification_stats(self, viewspace_point_tensor, update_filter):
     """scene/gaussian_model.py:606-609 (xyz_gradient_accum[f] += |grad[f,:2]|; denom[f] += 1)."""
     _stats(self, viewspace_point_tensor.grad, None, update_filter, False, True)
@@ -415,7 +442,8 @@ def proximity(self, scene_extent, include_feature, N=3):
         _rebuild(self, None, _rows(self._xyz) + new_xyz.shape[0], ext, fresh_stats=True)
 
 
-METHODS = ("add_densification_stats", "update_densification_stats", "prune_points",
+METHODS = ("add_densification_stats", "update_densification_stats",
+           "update_densification_stats_views", "prune_points",
            "densification_postfix", "densify_and_clone", "densify_and_split", "densify_and_prune",
            "proximity")
 

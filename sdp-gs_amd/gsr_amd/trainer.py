@@ -146,9 +146,15 @@ def train_step_views(model, cams: Sequence, gt_images: Sequence[torch.Tensor],
                 torch.autograd.backward(losses)
             with torch.no_grad():
                 if iteration < args.densify_until_iter:
-                    for pkg in pkgs:
-                        model.update_densification_stats(pkg["viewspace_points"], pkg["radii"],
-                                                         pkg["visibility_filter"])
+                    if st is not None and hasattr(model, "update_densification_stats_views"):
+                        # every view's statistics in one launch (visibility = radii > 0)
+                        model.update_densification_stats_views(st["viewspace_points"].grad,
+                                                               st["radii"])
+                    else:
+                        for pkg in pkgs:
+                            model.update_densification_stats(pkg["viewspace_points"],
+                                                             pkg["radii"],
+                                                             pkg["visibility_filter"])
             return [loss.detach() for loss in losses]
         losses = pipeline.run_views(cams, all_views, model=model, reducer=reducer)
         with torch.no_grad():
