@@ -25,13 +25,15 @@ def _away_camera(W, H, like):
     return make_camera(R, -R.T @ c, like.FoVx, like.FoVy, W, H, uid=99, device="cuda")
 
 
-@pytest.mark.parametrize("nviews", [1, 7, 10])
-def test_batched_forward_equals_single_view(nviews):
+@pytest.mark.parametrize("nviews,distance", [(1, 4.0), (7, 4.0), (10, 4.0), (5, 1.6)])
+def test_batched_forward_equals_single_view(nviews, distance):
+    """(distance 4: every binned depth in [2, 8), one top byte -- the batched depth sort leaves its
+    last pass out; distance 1.6: depths on both sides of 2 -- all four passes.)"""
     import diff_gaussian_rasterization as dgr
     from gaussian_renderer import render, render_views
     W, H = 240, 180
     m = SplatModel(make_gaussians(30_000, sh_degree=3, seed=5), device="cuda")
-    cams = [c.to("cuda") for c in make_cameras(nviews, W, H, seed=5)]
+    cams = [c.to("cuda") for c in make_cameras(nviews, W, H, seed=5, distance=distance)]
     if nviews > 3:
         cams[3] = _away_camera(W, H, cams[0])
     bg = torch.zeros(3, device="cuda")
