@@ -19,6 +19,94 @@ namespace {
 
 constexpr int kThreads = 256;
 
+// 1 (default): the LDS-staged duplication below; 0: each lane stores at its own offsets
+#ifndef GSR_DUP_LDS
+#define GSR_DUP_LDS 1
+#endif
+#ifndef GSR_DUP_WIN
+#define GSR_DUP_WIN 256
+#endif
+// wave-scope ordering of LDS stores before other lanes' loads of the same wave
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Staged variant: a wave's 64 depth-consecutive Gaussians own one contiguous range of instances;
+// every lane enumerates its tiles (same order) into a per-wave LDS window, then the wave copies
+// the window out with coalesced stores (the direct variant stores each lane's ids at its own
+// offsets: 64 scattered lines per store instruction).
+__device__ __forceinline__ void duplicate_body_lds(int P, const uint32_t* __restrict__ order,
+                                                   const uint32_t* __restrict__ offsets,
+                                                   const float4* __restrict__ rec, uint32_t gx,
+                                                   uint32_t gy, uint32_t* __restrict__ tkey,
+                                                   uint32_t* __restrict__ tval, uint32_t R,
+                                                   SideClear clear0, SideClear clear1,
+                                                   uint32_t* __restrict__ egid,
+                                                   uint32_t* __restrict__ ebeg, uint32_t blk,
+                                                   uint32_t nblk) {
+  constexpr int kWin = GSR_DUP_WIN;  // instances per wave window
+  __shared__ uint32_t s_key[kThreads / 64][kWin];
+  __shared__ uint32_t s_val[kThreads / 64][kWin];
+  __shared__ uint32_t s_eg[kThreads / 64][kWin];
+  const int s = (int)(blk * kThreads + threadIdx.x);
+  const size_t nth = (size_t)nblk * kThreads;
+  side_clear(clear0.p, clear0.bytes, (size_t)s, nth);
+  side_clear(clear1.p, clear1.bytes, (size_t)s, nth);
+  const int lane = (int)(threadIdx.x & 63), wid = (int)(threadIdx.x >> 6);
+  const int sw0 = s - lane;
+  if (sw0 >= P) return;  // wave-uniform
+  const bool valid = s < P;
+  uint32_t off = valid ? ((s == 0) ? 0u : offsets[s - 1]) : 0u;
+  const uint32_t end = valid ? min(offsets[s], R) : 0u;
+  // the wave's instance range: offsets are a prefix sum, so it runs from lane 0's first to the
+  // last valid lane's end
+  const uint32_t obase = (uint32_t)__shfl((int)off, 0, 64);
+  const uint32_t oend = (uint32_t)__shfl((int)end, min(P - 1 - sw0, 63), 64);
+  uint32_t gid = 0, y = 0, y1 = 0, x0 = 0, x1 = 0, x = 0, xe = 0;
+  SplatCut cut{};
+  if (off < end) {
+    gid = min(order[s], (uint32_t)P - 1u);
+    const float4 r0 = rec[4 * (size_t)gid];
+    const float4 r1 = rec[4 * (size_t)gid + 1];
+    const float4 r3 = rec[4 * (size_t)gid + 3];
+    if (egid) ebeg[gid] = off;
+    uint32_t y0;
+    tile_rect(r0.x, r0.y, (int)r3.y, gx, gy, x0, y0, x1, y1);
+    cut = make_cut(r0.x, r0.y, r0.z, r0.w, r1.x, r3.z);
+    y = y0;
+    if (y < y1) cut_row_range(cut, y, x0, x1, x, xe);
+    else off = end;
+  }
+  for (uint32_t wbeg = obase; wbeg < oend; wbeg += kWin) {
+    const uint32_t wend = min(wbeg + (uint32_t)kWin, oend);
+    const uint32_t lim = min(end, wend);
+    while (off < lim) {
+      if (x >= xe) {  // next row of the rectangle (rows may be empty after the cut)
+        if (++y >= y1) {
+          off = end;
+          break;
+        }
+        cut_row_range(cut, y, x0, x1, x, xe);
+        continue;
+      }
+      s_key[wid][off - wbeg] = y * gx + x;
+      s_val[wid][off - wbeg] = egid ? off : gid;
+      if (egid) s_eg[wid][off - wbeg] = gid;
+      x++;
+      off++;
+    }
+    wave_sync();
+    for (uint32_t i = (uint32_t)lane; i < wend - wbeg; i += 64) {
+      tkey[wbeg + i] = s_key[wid][i];
+      tval[wbeg + i] = s_val[wid][i];
+      if (egid) egid[wbeg + i] = s_eg[wid][i];
+    }
+    wave_sync();
+  }
+}
+
 // One lane per depth-sorted Gaussian; the lane writes its tile ids row-major over its tile
 // rectangle (the reference's emission order inside one Gaussian, rasterizer_impl.cu:98-109).
 // (body shared by the one-view kernel and the several-views kernel: blk / nblk = this
@@ -32,6 +120,11 @@ __device__ __forceinline__ void duplicate_body(int P, const uint32_t* __restrict
                                                uint32_t* __restrict__ egid,
                                                uint32_t* __restrict__ ebeg, uint32_t blk,
                                                uint32_t nblk) {
+  if (GSR_DUP_LDS) {
+    duplicate_body_lds(P, order, offsets, rec, gx, gy, tkey, tval, R, clear0, clear1, egid, ebeg,
+                       blk, nblk);
+    return;
+  }
   const int s = (int)(blk * kThreads + threadIdx.x);
   const size_t nth = (size_t)nblk * kThreads;
   side_clear(clear0.p, clear0.bytes, (size_t)s, nth);
