@@ -171,8 +171,8 @@ def launch_ranks(argv, nproc, script=None, env=None):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="llff_1m_1008x756", choices=sorted(WORKLOADS))
     ap.add_argument("--views-per-gpu", type=int, default=6)
     ap.add_argument("--cpu-baseline-views", type=int, default=2)
@@ -204,7 +204,7 @@ def main():
                          "consecutive chunks, each forward + backward)")
     ap.add_argument("--no-precolor", action="store_true",
                     help="each view evaluates its SH colour itself instead of the step's pre-pass")
-    ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_r03d.json"))
+    ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_r03e.json"))
     ap.add_argument("--no-extra-legs", action="store_true",
                     help="skip the train-step, reference-cadence and reference-API legs")
     ap.add_argument("--cpu-threads", type=int, default=0,
