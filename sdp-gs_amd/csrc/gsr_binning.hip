@@ -177,6 +177,14 @@ __global__ __launch_bounds__(kThreads) void duplicate_kernel(int P,
                  blockIdx.x, gridDim.x);
 }
 
+// Instances per lane of the ranges kernel: consecutive keys, one 16-B load when aligned (one
+// key per lane made the launch ~4x more workgroups than its 4-byte loads can keep busy).
+#ifndef GSR_RANGES_KPT
+#define GSR_RANGES_KPT 4
+#endif
+constexpr int kRangesKPT = GSR_RANGES_KPT;
+static_assert(kRangesKPT == 1 || kRangesKPT == 4, "ranges keys per lane");
+
 __device__ __forceinline__ void tile_ranges_body(size_t R, const uint32_t* __restrict__ tiles,
                                                  uint2* __restrict__ ranges, uint32_t ntiles,
                                                  const uint32_t* __restrict__ derr,
@@ -184,11 +192,11 @@ __device__ __forceinline__ void tile_ranges_body(size_t R, const uint32_t* __res
                                                  uint32_t* __restrict__ status,
                                                  uint32_t* host_status, uint32_t* fault,
                                                  uint32_t blk) {
-  const size_t idx = (size_t)blk * kThreads + threadIdx.x;
-  if (idx >= (R ? R : 1)) return;
+  const size_t base = ((size_t)blk * kThreads + threadIdx.x) * kRangesKPT;
+  if (base >= (R ? R : 1)) return;
   // the call's status: both sorts have finished (stream order); a timed-out look-back of either
   // fails this call (render_fwd poisons the outputs, the backward the gradients)
-  if (idx == 0) {
+  if (base == 0) {
     const uint32_t st =
         ((derr && *derr) ? kStatusDepthSort : 0u) | ((terr && *terr) ? kStatusTileSort : 0u);
     *status = st;
@@ -198,18 +206,33 @@ __device__ __forceinline__ void tile_ranges_body(size_t R, const uint32_t* __res
   if (R == 0) return;
   // tile ids are < ntiles by construction; the bounds tests only keep the output of a sort whose
   // look-back gave up (reported by the next read-back) from writing outside the table
-  const uint32_t cur = tiles[idx];
-  const bool cur_ok = cur < ntiles;
-  if (idx == 0) {
-    if (cur_ok) ranges[cur].x = 0;
+  uint32_t t[kRangesKPT];
+  if (kRangesKPT == 4 && base + 4 <= R && ((uintptr_t)(tiles + base) & 15u) == 0) {
+    const uint4 q = *reinterpret_cast<const uint4*>(tiles + base);
+    t[0] = q.x;
+    t[kRangesKPT > 1 ? 1 : 0] = q.y;
+    t[kRangesKPT > 2 ? 2 : 0] = q.z;
+    t[kRangesKPT > 3 ? 3 : 0] = q.w;
   } else {
-    const uint32_t prev = tiles[idx - 1];
-    if (cur != prev) {
+#pragma unroll
+    for (int k = 0; k < kRangesKPT; k++) t[k] = base + k < R ? tiles[base + k] : 0u;
+  }
+  uint32_t prev = base ? tiles[base - 1] : 0u;
+#pragma unroll
+  for (int k = 0; k < kRangesKPT; k++) {
+    const size_t idx = base + k;
+    if (idx >= R) break;
+    const uint32_t cur = t[k];
+    const bool cur_ok = cur < ntiles;
+    if (idx == 0) {
+      if (cur_ok) ranges[cur].x = 0;
+    } else if (cur != prev) {
       if (prev < ntiles) ranges[prev].y = (uint32_t)idx;
       if (cur_ok) ranges[cur].x = (uint32_t)idx;
     }
+    if (idx == R - 1 && cur_ok) ranges[cur].y = (uint32_t)R;
+    prev = cur;
   }
-  if (idx == R - 1 && cur_ok) ranges[cur].y = (uint32_t)R;
 }
 
 __global__ __launch_bounds__(kThreads) void tile_ranges_kernel(size_t R,
@@ -309,7 +332,8 @@ hipError_t launch_tile_ranges_views(const RangesSpec* v, int V, hipStream_t s) {
     m.j[k] = v[k];
     if (!v[k].R) m.j[k].tile_err = nullptr;  // no instances: nothing tile-sorted
     const size_t n = v[k].R ? v[k].R : 1;  // R == 0: one lane still publishes the status
-    m.first[k + 1] = m.first[k] + (uint32_t)((n + kThreads - 1) / kThreads);
+    const size_t per = (size_t)kThreads * kRangesKPT;
+    m.first[k + 1] = m.first[k] + (uint32_t)((n + per - 1) / per);
   }
   hipLaunchKernelGGL(tile_ranges_views_kernel, dim3(m.first[V]), dim3(kThreads), 0, s, m);
   return hipGetLastError();
@@ -325,7 +349,8 @@ hipError_t launch_tile_ranges(size_t R, const uint32_t* sorted_tiles, uint2* ran
   }
   // R == 0: no instances, nothing tile-sorted; one lane still publishes the depth sort's word
   const size_t n = R ? R : 1;
-  hipLaunchKernelGGL(tile_ranges_kernel, dim3((unsigned)((n + kThreads - 1) / kThreads)),
+  const size_t per = (size_t)kThreads * kRangesKPT;
+  hipLaunchKernelGGL(tile_ranges_kernel, dim3((unsigned)((n + per - 1) / per)),
                      dim3(kThreads), 0, s, R, sorted_tiles, ranges, ntiles, depth_err,
                      R ? tile_err : nullptr, status, host_status, fault);
   return hipGetLastError();
