@@ -103,29 +103,58 @@ __global__ __launch_bounds__(1024) void scan_parts_kernel(uint32_t* __restrict__
   scan_parts_body(parts, n);
 }
 
+// GSR_SCAN_VEC: a lane's kScanItems consecutive counts as 16-byte loads and stores when the
+// arrays are aligned (workgroup-uniform test); else one 4-byte access per item
+#ifndef GSR_SCAN_VEC
+#define GSR_SCAN_VEC 1
+#endif
 template <bool GATHER, bool INCLUSIVE>
 __device__ __forceinline__ void scan_final_body(const uint32_t* __restrict__ in,
                                                 const uint32_t* __restrict__ gather, size_t n,
                                                 const uint32_t* __restrict__ parts,
                                                 uint32_t* __restrict__ out, uint32_t blk) {
+  static_assert(kScanItems % 4 == 0, "vector scan items");
   __shared__ uint32_t lds[kThreads / 64];
   const size_t base = (size_t)blk * kScanTile + (size_t)threadIdx.x * kScanItems;
+  const bool vec = GSR_SCAN_VEC && !GATHER && base + kScanItems <= n &&
+                   (((uintptr_t)in | (uintptr_t)out) & 15u) == 0;
   uint32_t v[kScanItems];
   uint32_t s = 0;
+  if (vec) {
 #pragma unroll
-  for (int k = 0; k < kScanItems; k++) {
-    size_t i = base + k;
-    v[k] = (i < n) ? (GATHER ? in[min(gather[i], (uint32_t)n - 1u)] : in[i]) : 0u;
-    s += v[k];
+    for (int k = 0; k < kScanItems; k += 4) {
+      const uint4 q = *reinterpret_cast<const uint4*>(in + base + k);
+      v[k] = q.x;
+      v[k + 1] = q.y;
+      v[k + 2] = q.z;
+      v[k + 3] = q.w;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < kScanItems; k++) {
+      size_t i = base + k;
+      v[k] = (i < n) ? (GATHER ? in[min(gather[i], (uint32_t)n - 1u)] : in[i]) : 0u;
+    }
   }
+#pragma unroll
+  for (int k = 0; k < kScanItems; k++) s += v[k];
   uint32_t total;
   uint32_t pre = block_excl_scan<kThreads / 64>(s, lds, total) + parts[blk];
+  uint32_t o[kScanItems];
 #pragma unroll
   for (int k = 0; k < kScanItems; k++) {
-    size_t i = base + k;
     uint32_t incl = pre + v[k];
-    if (i < n) out[i] = INCLUSIVE ? incl : pre;
+    o[k] = INCLUSIVE ? incl : pre;
     pre = incl;
+  }
+  if (vec) {
+#pragma unroll
+    for (int k = 0; k < kScanItems; k += 4)
+      *reinterpret_cast<uint4*>(out + base + k) = make_uint4(o[k], o[k + 1], o[k + 2], o[k + 3]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < kScanItems; k++)
+      if (base + k < n) out[base + k] = o[k];
   }
 }
 
