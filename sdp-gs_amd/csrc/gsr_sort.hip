@@ -334,8 +334,13 @@ __device__ __forceinline__ void onesweep_body(
 #define SORT_TRACE(k)
 #endif
   SORT_TRACE(0)
-  // thread t < 256 <-> digit t: this pass's digit total, summed over the partial copies
-  const bool dig = t < 256;
+  // thread t < 2^bits <-> digit t: this pass's digit total, summed over the partial copies (a
+  // narrower last digit -- 4 bits for 3024 tiles -- publishes and looks back 16 words per
+  // partition instead of 256)
+#ifndef GSR_SORT_NARROW
+#define GSR_SORT_NARROW 1
+#endif
+  const bool dig = t < (GSR_SORT_NARROW ? (1 << bits) : 256);
   const int dt = dig ? t : 0;
   uint32_t dtotal = 0;
   if (dig) {
