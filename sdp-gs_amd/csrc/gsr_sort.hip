@@ -239,6 +239,17 @@ constexpr uint32_t kResident1024 = 2 * 256;  // 1024-lane partitions resident at
 constexpr int kTotKPT = GSR_TOTALS_KPT;
 constexpr int kTotTile = kThreads * kTotKPT;
 
+// Digit width of a sort over `bits` key bits: the passes (ceil(bits / 8)) split the bits evenly
+// (12-bit tile ids: 6 + 6 instead of 8 + 4) -- fewer, longer runs per bucket in the scatter of the
+// first pass.  Any split gives the same stable order.
+#ifndef GSR_SORT_EVEN
+#define GSR_SORT_EVEN 1
+#endif
+__host__ __device__ __forceinline__ int sort_digit_width(int bits) {
+  const int passes = (bits + 7) / 8;
+  return GSR_SORT_EVEN ? (bits + passes - 1) / passes : 8;
+}
+
 // (body shared by the one-sort kernel and the several-sorts kernel: blk / nblk = this
 // workgroup's index and the workgroup count of its sort)
 __device__ __forceinline__ void radix_totals_body(const uint32_t* __restrict__ keys, size_t n,
@@ -252,6 +263,8 @@ __device__ __forceinline__ void radix_totals_body(const uint32_t* __restrict__ k
   if (threadIdx.x == 0) nsent = 0;
   __syncthreads();
   const int passes = (bits + 7) / 8;
+  const int dw = sort_digit_width(bits);
+  const uint32_t dmask = (1u << dw) - 1u;
   for (size_t base = (size_t)blk * kTotTile; base < n; base += (size_t)nblk * kTotTile) {
     // all loads of the tile in flight before any is consumed
     uint32_t key[kTotKPT];
@@ -270,7 +283,7 @@ __device__ __forceinline__ void radix_totals_body(const uint32_t* __restrict__ k
         if (sm && (threadIdx.x & 63) == 0) atomicAdd(&nsent, (uint32_t)__popcll(sm));
       }
       for (int p = 0; p < passes; p++) {
-        const uint32_t d = (key[r] >> (8 * p)) & 0xffu;
+        const uint32_t d = (key[r] >> (dw * p)) & dmask;
         // typical depth keys share their top byte across a wave: one LDS add instead of 64
         // serialised same-address atomics
         const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
@@ -600,10 +613,10 @@ __global__ __launch_bounds__(kThreads) void radix_totals_views_kernel(SortPassVi
 
 template <int NT>
 __global__ __launch_bounds__(NT, NT == 1024 ? 8 : (NT == 512 ? 6 : 1)) void radix_onesweep_views_kernel(
-    SortPassViews m, int pass, int bits, int sentinel) {
+    SortPassViews m, int pass, int shift, int bits, int sentinel) {
   const int k = batch_view(m.first, m.V, blockIdx.x);
   const SortPassJob& j = m.j[k];
-  onesweep_body<NT>(j.kin, j.vin, j.n, 8 * pass, bits, j.aux + kSortAuxTotals + 256 * pass,
+  onesweep_body<NT>(j.kin, j.vin, j.n, shift, bits, j.aux + kSortAuxTotals + 256 * pass,
                     sentinel ? j.aux + kSortAuxSent : nullptr, j.aux + kSortAuxTickets + 8 * pass,
                     j.status, j.aux + kSortAuxErr, j.kout, j.vout, j.kpay,
                     blockIdx.x - m.first[k], m.first[k + 1] - m.first[k]);
@@ -941,8 +954,9 @@ hipError_t radix_sort_pairs(uint32_t* ka, uint32_t* va, uint32_t* kb, uint32_t* 
   uint32_t *kin = ka, *vin = va, *kout = kb, *vout = vb;
   bool in_b = false;
   for (int p = 0; p < passes; p++) {
-    const int shift = 8 * p;
-    const int dbits = (bits - shift) < 8 ? (bits - shift) : 8;
+    const int dw = sort_digit_width(bits);
+    const int shift = dw * p;
+    const int dbits = (bits - shift) < dw ? (bits - shift) : dw;
     const int nt = GSR_SORT_THREADS ? GSR_SORT_THREADS : (nb <= kResident1024 ? 1024 : 512);
 #define GSR_ONESWEEP(NT)                                                                          \
   hipLaunchKernelGGL(radix_onesweep_kernel<NT>, dim3(nb), dim3(NT), 0, s, kin, vin, n, shift,    \
@@ -1013,16 +1027,17 @@ hipError_t radix_sort_pairs_views(const SortSpec* v, int V, int bits, bool* resu
   const int nt = GSR_SORT_THREADS ? GSR_SORT_THREADS : (nb <= kResident1024 ? 1024 : 512);
   for (int p = 0; p < passes; p++) {
     fill(p, ofirst);
-    const int shift = 8 * p;
-    const int dbits = (bits - shift) < 8 ? (bits - shift) : 8;
+    const int dw = sort_digit_width(bits);
+    const int shift = dw * p;
+    const int dbits = (bits - shift) < dw ? (bits - shift) : dw;
     if (nt == 1024)
-      hipLaunchKernelGGL(radix_onesweep_views_kernel<1024>, dim3(nb), dim3(1024), 0, s, m, p, dbits,
+      hipLaunchKernelGGL(radix_onesweep_views_kernel<1024>, dim3(nb), dim3(1024), 0, s, m, p, shift, dbits,
                          sentinel_anywhere ? 1 : 0);
     else if (nt == 512)
-      hipLaunchKernelGGL(radix_onesweep_views_kernel<512>, dim3(nb), dim3(512), 0, s, m, p, dbits,
+      hipLaunchKernelGGL(radix_onesweep_views_kernel<512>, dim3(nb), dim3(512), 0, s, m, p, shift, dbits,
                          sentinel_anywhere ? 1 : 0);
     else
-      hipLaunchKernelGGL(radix_onesweep_views_kernel<256>, dim3(nb), dim3(256), 0, s, m, p, dbits,
+      hipLaunchKernelGGL(radix_onesweep_views_kernel<256>, dim3(nb), dim3(256), 0, s, m, p, shift, dbits,
                          sentinel_anywhere ? 1 : 0);
   }
   *result_in_b = (passes & 1) != 0;

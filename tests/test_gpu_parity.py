@@ -185,7 +185,9 @@ def test_forward_is_deterministic():
                                          (1_000_003, 32, "int"), (3_000_000, 13, "int"),
                                          (8191, 4, "int"), (1_000_000, 32, "depth"),
                                          (1_000_000, 32, "depth_narrow"),
-                                         (2_500_000, 12, "tiles")])
+                                         (2_500_000, 12, "tiles"),
+                                         # even digit splits: 17 bits = 6 + 6 + 5, 20 = 7 + 7 + 6
+                                         (300_001, 17, "int"), (65_537, 20, "int")])
 def test_radix_sort_sorted_and_stable(n, bits, kind):
     """One-sweep radix sort (gsr_sort.hip) == numpy's stable argsort, bit for bit: full 32-bit
     keys, float-bit depth keys (shared top bytes), skewed tile ids, partial last partitions."""
