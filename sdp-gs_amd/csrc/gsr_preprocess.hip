@@ -351,15 +351,15 @@ __global__ __launch_bounds__(kThreads) void sh_precolor_kernel(PrecolorArgs a) {
     // one contiguous 256-byte run, and so is every load of the consuming preprocesses
     const size_t P = (size_t)a.P;
     float* co = a.color[v] + i;
-    co[0] = col.x; co[P] = col.y; co[2 * P] = col.z;
-    a.clamp[v][i] = cl;
+    stream_st(co, col.x); stream_st(co + P, col.y); stream_st(co + 2 * P, col.z);
+    stream_st(a.clamp[v] + i, cl);
     // backward: sh_backward's Jacobian at the same normalised direction
     V3 jx, jy, jz;
     sh_dir_jacobian(c, a.D, dir, jx, jy, jz);
     float* jo = a.jac[v] + i;
-    jo[0] = jx.x; jo[P] = jx.y; jo[2 * P] = jx.z;
-    jo[3 * P] = jy.x; jo[4 * P] = jy.y; jo[5 * P] = jy.z;
-    jo[6 * P] = jz.x; jo[7 * P] = jz.y; jo[8 * P] = jz.z;
+    stream_st(jo, jx.x); stream_st(jo + P, jx.y); stream_st(jo + 2 * P, jx.z);
+    stream_st(jo + 3 * P, jy.x); stream_st(jo + 4 * P, jy.y); stream_st(jo + 5 * P, jy.z);
+    stream_st(jo + 6 * P, jz.x); stream_st(jo + 7 * P, jz.y); stream_st(jo + 8 * P, jz.z);
   }
 }
 

@@ -22,6 +22,36 @@ constexpr int kShMaxFloats = 48;  // 16 coefficients x 3 per Gaussian (M <= 16, 
 #endif
 constexpr int kStageBatch = GSR_STAGE_BATCH;
 
+// 1: the staged global rows are loaded and stored nontemporally (read / written once per step,
+// larger than the caches) -- and so are sh_precolor's per-view outputs
+#ifndef GSR_STAGE_NT
+#define GSR_STAGE_NT 1
+#endif
+__device__ __forceinline__ float4 stream_ld4(const float4* p) {
+  if (GSR_STAGE_NT) {
+    const float* f = reinterpret_cast<const float*>(p);
+    return make_float4(__builtin_nontemporal_load(f), __builtin_nontemporal_load(f + 1),
+                       __builtin_nontemporal_load(f + 2), __builtin_nontemporal_load(f + 3));
+  }
+  return *p;
+}
+__device__ __forceinline__ void stream_st4(float4* p, float4 v) {
+  if (GSR_STAGE_NT) {
+    float* f = reinterpret_cast<float*>(p);
+    __builtin_nontemporal_store(v.x, f);
+    __builtin_nontemporal_store(v.y, f + 1);
+    __builtin_nontemporal_store(v.z, f + 2);
+    __builtin_nontemporal_store(v.w, f + 3);
+    return;
+  }
+  *p = v;
+}
+template <typename T>
+__device__ __forceinline__ void stream_st(T* p, T v) {
+  if (GSR_STAGE_NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
 struct ShPlane {
   const float* src;  // global input plane (row-major [P, w])
   float* dst;        // global gradient plane
@@ -64,10 +94,10 @@ __device__ __forceinline__ void stage(const ShPlane& p, int base, int n, const u
       o[j] = v[j];
       if (on[j]) {
         if (IN) {
-          v[j] = reinterpret_cast<const float4*>(src)[q];
+          v[j] = stream_ld4(reinterpret_cast<const float4*>(src) + q);
         } else {
           v[j] = reinterpret_cast<const float4*>(l)[q];
-          if (ACC) o[j] = reinterpret_cast<const float4*>(dst)[q];
+          if (ACC) o[j] = stream_ld4(reinterpret_cast<const float4*>(dst) + q);
         }
       }
     }
@@ -80,7 +110,7 @@ __device__ __forceinline__ void stage(const ShPlane& p, int base, int n, const u
         } else {
           float4 r = v[j];
           if (ACC) r = make_float4(o[j].x + r.x, o[j].y + r.y, o[j].z + r.z, o[j].w + r.w);
-          reinterpret_cast<float4*>(dst)[q] = r;
+          stream_st4(reinterpret_cast<float4*>(dst) + q, r);
         }
       }
     }
