@@ -118,13 +118,22 @@ __device__ __forceinline__ void poison_outputs(const BwdPreArgs& a, size_t i) {
 __device__ __forceinline__ void add4(float4& t, float4 x) {
   t.x += x.x; t.y += x.y; t.z += x.z; t.w += x.w;
 }
+// 1: the once-read per-view streams of the backward preprocess (accumulator rows, the pre-pass
+// Jacobian planes) are loaded nontemporally
+#ifndef GSR_BWD_NT
+#define GSR_BWD_NT 0
+#endif
 // The Gaussian's 16-float gradient row (gsr_internal.h AccSlot): its accumulator row (atomic
 // mode), or the sum of its instances' rows in emission order (rows layout; zero without any).
 __device__ __forceinline__ void grad_row(const BwdPreArgs& a, size_t i, float4& q0, float4& q1,
                                          float4& q2, float4& q3) {
   if (!a.use_rows) {
     const float4* accp = reinterpret_cast<const float4*>(a.acc + i * kAccFloats);
-    q0 = accp[0]; q1 = accp[1]; q2 = accp[2]; q3 = accp[3];
+    if (GSR_BWD_NT) {  // read once per step (the next forward re-zeroes the rows)
+      q0 = stream_ld4(accp); q1 = stream_ld4(accp + 1); q2 = stream_ld4(accp + 2); q3 = stream_ld4(accp + 3);
+    } else {
+      q0 = accp[0]; q1 = accp[1]; q2 = accp[2]; q3 = accp[3];
+    }
     return;
   }
   const uint32_t n = a.count[i];
@@ -352,8 +361,9 @@ __device__ __forceinline__ void gaussian_bwd(const BwdPreArgs& a, size_t i, floa
       put3p(a.dRGB_out, (size_t)a.P, i, dRGB);
       const float* j = a.pre_jac + i;  // planar [9][P]
       const size_t P = (size_t)a.P;
-      const V3 jx = v3(j[0], j[P], j[2 * P]), jy = v3(j[3 * P], j[4 * P], j[5 * P]),
-               jz = v3(j[6 * P], j[7 * P], j[8 * P]);
+      auto jl = [&](size_t o) { return GSR_BWD_NT ? __builtin_nontemporal_load(j + o) : j[o]; };
+      const V3 jx = v3(jl(0), jl(P), jl(2 * P)), jy = v3(jl(3 * P), jl(4 * P), jl(5 * P)),
+               jz = v3(jl(6 * P), jl(7 * P), jl(8 * P));
       const V3 dL_ddir = v3(dot3(jx, dRGB), dot3(jy, dRGB), dot3(jz, dRGB));
       dmean = dmean + dnormvdv(dir_orig, dL_ddir);
     } else if (a.dRGB_out) {  // deferred: dL/dsh = basis(dir) x dRGB is formed by the step's flush
