@@ -32,11 +32,26 @@ __device__ constexpr float SH_C3_5 = 1.445305721320277f;
 __device__ constexpr float SH_C3_6 = -0.5900435899266435f;
 
 // Grid-stride share of a SideClear (gsr_internal.h) for thread `tid` of `nthreads`.
+// GSR_CLEAR_NT: the zeroes are stored nontemporally (the accumulator rows are next touched by the
+// backward blend's atomics, long after)
+#ifndef GSR_CLEAR_NT
+#define GSR_CLEAR_NT 0
+#endif
 __device__ __forceinline__ void side_clear(void* p, size_t bytes, size_t tid, size_t nthreads) {
   if (!p) return;
   uint4* q = reinterpret_cast<uint4*>(p);
   const size_t n16 = bytes >> 4;
-  for (size_t i = tid; i < n16; i += nthreads) q[i] = make_uint4(0u, 0u, 0u, 0u);
+  for (size_t i = tid; i < n16; i += nthreads) {
+#if GSR_CLEAR_NT
+    uint32_t* f = reinterpret_cast<uint32_t*>(q + i);
+    __builtin_nontemporal_store(0u, f);
+    __builtin_nontemporal_store(0u, f + 1);
+    __builtin_nontemporal_store(0u, f + 2);
+    __builtin_nontemporal_store(0u, f + 3);
+#else
+    q[i] = make_uint4(0u, 0u, 0u, 0u);
+#endif
+  }
   uint32_t* w = reinterpret_cast<uint32_t*>(p);
   const size_t tail = (bytes & 15u) >> 2;
   if (tid < tail) w[4 * n16 + tid] = 0u;
