@@ -611,18 +611,22 @@ __global__ __launch_bounds__(kThreads, GSR_BWDV_MINBLK) void preprocess_bwd_view
 // with the same basis arithmetic as sh_backward, summed in registers, written once (store) or
 // added once (ACC) through the LDS staging planes -- instead of one 192-byte read-modify-write of
 // the SH gradient rows per view.
+#ifndef GSR_SH_THREADS
+#define GSR_SH_THREADS 256
+#endif
+constexpr int kShThreads = GSR_SH_THREADS;  // see gsr_preprocess.hip kPcThreads
 template <bool ACC>
-__global__ __launch_bounds__(kThreads) void sh_flush_kernel(ShFlushArgs a) {
-  __shared__ float4 s_sh4[kThreads * kShMaxFloats / 4];
-  __shared__ uint8_t s_live[kThreads];
+__global__ __launch_bounds__(kShThreads) void sh_flush_kernel(ShFlushArgs a) {
+  __shared__ float4 s_sh4[kShThreads * kShMaxFloats / 4];
+  __shared__ uint8_t s_live[kShThreads];
   float* s_sh = reinterpret_cast<float*>(s_sh4);
-  const int base = (int)(blockIdx.x * kThreads);
-  const int n = min(kThreads, a.P - base);
+  const int base = (int)(blockIdx.x * kShThreads);
+  const int n = min(kShThreads, a.P - base);
   const int t = (int)threadIdx.x;
   const size_t i = (size_t)base + t;
   s_live[t] = t < n;
   const ShPlane p0{nullptr, a.dL_dsh_dc, 3, 0};
-  const ShPlane p1{nullptr, a.dL_dsh_rest, (a.M - 1) * 3, kThreads * 3};
+  const ShPlane p1{nullptr, a.dL_dsh_rest, (a.M - 1) * 3, kShThreads * 3};
   if (t < n) {
     const V3 mean = v3(a.means3D[3 * i], a.means3D[3 * i + 1], a.means3D[3 * i + 2]);
     V3 g[16];
@@ -648,19 +652,19 @@ __global__ __launch_bounds__(kThreads) void sh_flush_kernel(ShFlushArgs a) {
     }
   }
   __syncthreads();
-  stage<kThreads, false, ACC>(p0, base, n, s_live, s_sh);
-  stage<kThreads, false, ACC>(p1, base, n, s_live, s_sh);
+  stage<kShThreads, false, ACC>(p0, base, n, s_live, s_sh);
+  stage<kShThreads, false, ACC>(p1, base, n, s_live, s_sh);
 }
 
 }  // namespace
 
 hipError_t launch_sh_grad_flush(const ShFlushArgs& a, hipStream_t s) {
   if (a.P == 0 || a.nviews <= 0) return hipSuccess;
-  const dim3 grid((a.P + kThreads - 1) / kThreads);
+  const dim3 grid((a.P + kShThreads - 1) / kShThreads);
   if (a.accumulate)
-    hipLaunchKernelGGL(sh_flush_kernel<true>, grid, dim3(kThreads), 0, s, a);
+    hipLaunchKernelGGL(sh_flush_kernel<true>, grid, dim3(kShThreads), 0, s, a);
   else
-    hipLaunchKernelGGL(sh_flush_kernel<false>, grid, dim3(kThreads), 0, s, a);
+    hipLaunchKernelGGL(sh_flush_kernel<false>, grid, dim3(kShThreads), 0, s, a);
   return hipGetLastError();
 }
 

@@ -308,26 +308,34 @@ __global__ __launch_bounds__(kThreads, GSR_PRE_VIEWS_MINBLK) void preprocess_vie
   }
 }
 
+// Workgroup size of the SH-row kernels (colour pre-pass here, SH flush in gsr_backward.hip):
+// their LDS staging takes 192 B per lane, so the CU holds the same number of lanes at any size;
+// smaller workgroups only desynchronise the load / compute / store phases of its residents.
+#ifndef GSR_SH_THREADS
+#define GSR_SH_THREADS 256
+#endif
+constexpr int kPcThreads = GSR_SH_THREADS;
+
 // Multi-view colour pre-pass (gsr_amd/pipeline.py): one pass over the SH rows serves the
 // forward colour and the backward's colour Jacobian of every view of a step, instead of every
 // view's preprocess and backward preprocess reading the 192-byte rows again.  Per Gaussian and
 // view: sh_to_rgb (forward.cu:20-71, the forward's own function) -> colour [3][P] + clamp bits,
 // and sh_dir_jacobian (backward.cu:56-131) -> dRGB/ddir [9][P].  The rows go through LDS
 // (gsr_stage.h) so the global reads are coalesced 16-byte vectors.
-__global__ __launch_bounds__(kThreads) void sh_precolor_kernel(PrecolorArgs a) {
-  __shared__ float4 s_sh4[kThreads * kShMaxFloats / 4];
-  __shared__ uint8_t s_live[kThreads];
+__global__ __launch_bounds__(kPcThreads) void sh_precolor_kernel(PrecolorArgs a) {
+  __shared__ float4 s_sh4[kPcThreads * kShMaxFloats / 4];
+  __shared__ uint8_t s_live[kPcThreads];
   float* s_sh = reinterpret_cast<float*>(s_sh4);
-  const int base = (int)(blockIdx.x * kThreads);
-  const int n = min(kThreads, a.P - base);
+  const int base = (int)(blockIdx.x * kPcThreads);
+  const int n = min(kPcThreads, a.P - base);
   const int t = (int)threadIdx.x;
   const size_t i = (size_t)base + t;
   s_live[t] = t < n;
   const ShPlane p0{a.sh_dc, nullptr, 3, 0};
-  const ShPlane p1{a.sh_rest, nullptr, (a.M - 1) * 3, kThreads * 3};
+  const ShPlane p1{a.sh_rest, nullptr, (a.M - 1) * 3, kPcThreads * 3};
   __syncthreads();
-  stage<kThreads, true, false>(p0, base, n, s_live, s_sh);
-  stage<kThreads, true, false>(p1, base, n, s_live, s_sh);
+  stage<kPcThreads, true, false>(p0, base, n, s_live, s_sh);
+  stage<kPcThreads, true, false>(p1, base, n, s_live, s_sh);
   __syncthreads();
   if (t >= n) return;
   const float* r0 = s_sh + p0.lds + t * p0.w;
@@ -407,7 +415,7 @@ hipError_t launch_preprocess_views(const PreArgs* views, int V, hipStream_t s) {
 
 hipError_t launch_sh_precolor(const PrecolorArgs& a, hipStream_t s) {
   if (a.P == 0 || a.nviews <= 0) return hipSuccess;
-  hipLaunchKernelGGL(sh_precolor_kernel, dim3((a.P + kThreads - 1) / kThreads), dim3(kThreads), 0,
+  hipLaunchKernelGGL(sh_precolor_kernel, dim3((a.P + kPcThreads - 1) / kPcThreads), dim3(kPcThreads), 0,
                      s, a);
   return hipGetLastError();
 }
