@@ -231,7 +231,7 @@ constexpr uint32_t kResident1024 = 2 * 256;  // 1024-lane partitions resident at
 // thread) and a bounded grid striding over tiles: short per-workgroup chains for latency, and at
 // most GSR_TOTALS_GROUPS global atomics per counter at the end.
 #ifndef GSR_TOTALS_KPT
-#define GSR_TOTALS_KPT 16
+#define GSR_TOTALS_KPT 8
 #endif
 #ifndef GSR_TOTALS_GROUPS
 #define GSR_TOTALS_GROUPS 1024
