@@ -54,6 +54,11 @@ enum { GSR_BUF_GEOM = 0, GSR_BUF_BINNING = 1, GSR_BUF_IMAGE = 2 };
  * gradients are bitwise reproducible; slower, and its binning buffer holds two more arrays.  A
  * backward must get the same bit 1 as its forward. */
 #define GSR_DEBUG_DETERMINISTIC 2
+/* Backward only, bit 2: take the layout (deterministic or not, per-instance rows or atomics) from
+ * the tag word the forward wrote into its binning buffer instead of from bit 1 -- for callers
+ * that keep only the buffers (the reference's `_C.rasterize_gaussians_backward` signature carries
+ * just `debug`).  Costs one synchronous 4-byte read. */
+#define GSR_DEBUG_LAYOUT_FROM_BUFFER 4
 
 /* Returns a device pointer to at least `bytes` bytes (16-byte aligned) or NULL. */
 typedef void* (*gsr_alloc_fn)(void* ctx, size_t bytes, int which);

@@ -18,6 +18,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+#include <mutex>
+
 #include "../../include/gsr_optim.h"
 
 namespace gsr {
@@ -43,9 +46,12 @@ struct AdamArgs {
   float wd[GSR_ADAM_MAX_TENSORS];
   uint32_t vec_ok;                           // bit t: all four arrays of tensor t 16-B aligned
   float w1, beta2, one_m_beta2, eps;
-  // the device's forward fault word: non-zero = a rasterizer forward failed (its gradients are
-  // NaN), so the step leaves parameters and moments untouched (include/gsr_optim.h)
-  const uint32_t* fault;
+  // the step's skip decision, read once per workgroup from one float written before this
+  // launch (step_guard_kernel's snapshot of the device's forward fault word, or that snapshot
+  // SUM-all-reduced over the ranks): != 0 = some forward of the step failed (its gradients are
+  // NaN), so every parameter and moment stays untouched (include/gsr_optim.h)
+  const float* skip;
+  uint32_t* host_skipped;  // pinned host word: 1 = this step was skipped, 0 = applied (or NULL)
 };
 
 __device__ __forceinline__ float lerp_torch(float a, float b, float w) {
@@ -92,8 +98,20 @@ __device__ __forceinline__ void st4(float4* p, float4 v) {
   *p = v;
 }
 
+// One lane: slot[0] = (the device's sticky forward fault word != 0) ? 1 : 0.  Every workgroup of
+// the Adam launch behind it reads this one snapshot, so a forward failing on another stream while
+// Adam runs cannot leave some tensors updated and others not.
+__global__ void step_guard_kernel(const uint32_t* __restrict__ fault, float* __restrict__ slot) {
+  if (threadIdx.x == 0)
+    slot[0] = (fault && __hip_atomic_load(fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) ? 1.0f
+                                                                                                : 0.0f;
+}
+
 __global__ __launch_bounds__(kThreads) void adam_kernel(AdamArgs a) {
-  if (a.fault && __hip_atomic_load(a.fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+  const bool skipped = !(*a.skip == 0.0f);  // workgroup-uniform; NaN counts as a failure
+  if (a.host_skipped && blockIdx.x == 0 && threadIdx.x == 0)
+    __hip_atomic_store(a.host_skipped, skipped ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (skipped) return;
   const uint32_t b = blockIdx.x;
   int t = 0;
   while (t + 1 < a.n && b >= a.block0[t + 1]) t++;  // workgroup-uniform, <= 16 tensors
@@ -141,13 +159,50 @@ __global__ __launch_bounds__(kThreads) void adam_kernel(AdamArgs a) {
 
 bool aligned(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
+// One float per device for the guard snapshot of a step without a caller-provided skip slot.
+float* device_guard_slot() {
+  constexpr int kMaxDev = 64;
+  static std::atomic<float*> cache[kMaxDev];
+  static std::mutex mu;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return nullptr;
+  float* s = cache[dev].load(std::memory_order_acquire);
+  if (s) return s;
+  std::lock_guard<std::mutex> lock(mu);
+  s = cache[dev].load(std::memory_order_relaxed);
+  if (!s) {
+    void* p = nullptr;
+    if (hipMalloc(&p, 256) != hipSuccess) return nullptr;
+    s = (float*)p;
+    cache[dev].store(s, std::memory_order_release);
+  }
+  return s;
+}
+
 }  // namespace
+
+extern "C" int gsr_step_guard(float* slot, void* stream) {
+  if (!slot) return 1;
+  hipLaunchKernelGGL(step_guard_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream,
+                     gsr::forward_faults_word(), slot);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
 
 extern "C" int gsr_adam_step(int n_tensors, float* const* params, const float* const* grads,
                              float* const* exp_avg, float* const* exp_avg_sq,
                              const int64_t* numel, const double* lr, const double* weight_decay,
                              const double* step, double beta1, double beta2, double eps,
                              void* stream) {
+  return gsr_adam_step_guarded(n_tensors, params, grads, exp_avg, exp_avg_sq, numel, lr,
+                               weight_decay, step, beta1, beta2, eps, nullptr, nullptr, stream);
+}
+
+extern "C" int gsr_adam_step_guarded(int n_tensors, float* const* params, const float* const* grads,
+                                     float* const* exp_avg, float* const* exp_avg_sq,
+                                     const int64_t* numel, const double* lr,
+                                     const double* weight_decay, const double* step, double beta1,
+                                     double beta2, double eps, const float* skip,
+                                     uint32_t* host_skipped, void* stream) {
   if (n_tensors < 0 || n_tensors > GSR_ADAM_MAX_TENSORS) return 1;
   if (n_tensors == 0) return 0;
   AdamArgs a{};
@@ -177,8 +232,15 @@ extern "C" int gsr_adam_step(int n_tensors, float* const* params, const float* c
   a.beta2 = (float)beta2;
   a.one_m_beta2 = (float)(1.0 - beta2);
   a.eps = (float)eps;
-  a.fault = gsr::forward_faults_word();
   if (blocks == 0) return 0;
+  if (!skip) {  // snapshot the device's fault word into this device's guard slot first
+    float* slot = device_guard_slot();
+    if (!slot) return 2;
+    if (gsr_step_guard(slot, stream) != 0) return 2;
+    skip = slot;
+  }
+  a.skip = skip;
+  a.host_skipped = host_skipped;
   hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(kThreads), 0, (hipStream_t)stream, a);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }

@@ -60,6 +60,7 @@ bool bwd_rows_mode() {
 BinState carve_bin(char* base, size_t R, bool rows) {
   Carver c(base);
   BinState b{};
+  b.tag = c.take<uint32_t>(4);
   b.tkey_a = c.take<uint32_t>(R);
   b.tval_a = c.take<uint32_t>(R);
   b.tkey_b = c.take<uint32_t>(R);
@@ -592,6 +593,9 @@ static int fwd_bin_alloc(const FwdModel& m, FwdCam& c) {
   c.bbase = c.given_b ? c.given_b : (char*)c.alloc(c.alloc_ctx, bbytes, GSR_BUF_BINNING);
   if (!c.bbase) return fail(GSR_ERR_ALLOC, "binning buffer allocation of %zu bytes failed", bbytes);
   c.b = carve_bin(c.bbase, R_ref, m.rows);  // capacity R_ref, the first R entries used
+  // the layout this forward binned with, for a backward that only holds the buffer (the `_C`
+  // signature: GSR_DEBUG_LAYOUT_FROM_BUFFER)
+  GSR_CHECK(hipMemsetD32Async((hipDeviceptr_t)c.b.tag, (int)bin_layout_tag(m.det, m.rows), 1, stream));
   c.num_rendered = (int)R_ref;
   c.num_instances = (int)R;
   return GSR_OK;
@@ -990,6 +994,23 @@ static int backward_impl(
     const float* opacity_raw, float* dL_dsh_rest, int accumulate, float* dRGB_sh = nullptr,
     const float* pre_jac = nullptr) {
   g_err.clear();
+  if (debug & GSR_DEBUG_LAYOUT_FROM_BUFFER) {
+    debug &= ~GSR_DEBUG_LAYOUT_FROM_BUFFER;
+    if (R > 0 && binning_buffer) {
+      // the caller holds only the buffers (the reference's `_C` signature): the forward wrote its
+      // layout into the binning buffer's tag word -- one synchronous 4-byte read
+      uint32_t tag = 0;
+      const BinState hb = carve_bin((char*)binning_buffer, 0, false);
+      hipStream_t stream = (hipStream_t)stream_ptr;
+      GSR_CHECK(hipMemcpyAsync(&tag, hb.tag, sizeof(tag), hipMemcpyDeviceToHost, stream));
+      GSR_CHECK(hipStreamSynchronize(stream));
+      const bool det = (tag & 2u) != 0;
+      if ((tag & ~3u) != kBinLayoutMagic || ((tag & 1u) != 0) != (det || bwd_rows_mode()))
+        return fail(GSR_ERR_ARGUMENT, "binningBuffer does not come from a libgsr forward of this "
+                                      "process (layout tag 0x%08x)", tag);
+      debug = (debug & ~GSR_DEBUG_DETERMINISTIC) | (det ? GSR_DEBUG_DETERMINISTIC : 0);
+    }
+  }
   BwdCall call;
   if (int rc = bwd_setup(call, P, M, R, background, means3D, radii, colors_precomp, scales,
                          rotations, scale_modifier, cov3D_precomp, viewmatrix, projmatrix,

@@ -209,6 +209,7 @@ struct GeomState {
 GeomState carve_geom(char* base, size_t P);
 
 struct BinState {
+  uint32_t* tag;     // [4] the forward's layout: bin_layout_tag(det, rows) (first 256-B granule)
   uint32_t* tkey_a;  // [R] tile ids of the duplicated instances
   uint32_t* tval_a;  // [R] Gaussian ids
   uint32_t* tkey_b;
@@ -229,6 +230,10 @@ BinState carve_bin(char* base, size_t R, bool rows = false);
 // false = float atomics into one accumulator row per Gaussian.  The deterministic backward always
 // uses rows.  Fixed for the process, so a forward's layout is the one its backward expects.
 bool bwd_rows_mode();
+constexpr uint32_t kBinLayoutMagic = 0x47535200u;  // "GSR\0"
+inline uint32_t bin_layout_tag(bool det, bool rows) {
+  return kBinLayoutMagic | (det ? 2u : 0u) | (rows ? 1u : 0u);
+}
 
 struct ImgState {
   float* final_T;       // [H*W]

@@ -71,26 +71,6 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
     return int(nr.value), out_color, radii, geom, binning, img
 
 
-def _binning_is_deterministic(binning, R) -> bool:
-    """The forward's binning layout travels with its binning buffer, by size (include/gsr.h
-    gsr_binning_buffer_bytes / _det): no table of live forwards to keep or evict.  When the
-    default layout is the per-instance-rows one (GSR_BWD_ROWS=1) both sizes are equal and the
-    bit only selects the deterministic summation order, so the current mode is used; otherwise
-    the deterministic layout is recognised by its larger size (for every R > 0)."""
-    if binning is None or int(R) <= 0:
-        return False
-    L = _lib.load()
-    n = int(binning.numel())
-    det_n = int(L.gsr_binning_buffer_bytes_det(int(R)))
-    std_n = int(L.gsr_binning_buffer_bytes(int(R)))
-    if n not in (det_n, std_n):
-        raise RuntimeError("binningBuffer does not belong to a forward with this num_rendered")
-    if det_n == std_n:
-        from . import deterministic
-        return deterministic()
-    return n == det_n
-
-
 def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rotations,
                                  scale_modifier, cov3D_precomp, viewmatrix, projmatrix, tan_fovx,
                                  tan_fovy, dL_dout_color, sh, degree, campos, geomBuffer, R,
@@ -118,7 +98,9 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     g = geomBuffer if geomBuffer.numel() else None
     b = binningBuffer if binningBuffer.numel() else None
     i = imageBuffer if imageBuffer.numel() else None
-    flags = int(bool(debug)) | (2 if _binning_is_deterministic(b, R) else 0)
+    # the forward's layout travels in its binning buffer (a tag word the forward writes; include/
+    # gsr.h GSR_DEBUG_LAYOUT_FROM_BUFFER): no table of live forwards, no global mode
+    flags = int(bool(debug)) | 4
     with torch.cuda.device(dev):
         rc = _lib.load().gsr_rasterize_gaussians_backward(
             P, M, int(R), _p(bg), _p(m3), _p(rad), _p(col), _p(sc), _p(rot), float(scale_modifier),

@@ -37,6 +37,14 @@ def _fused_eligible(pc, pipe, opt, override_color, override_language) -> bool:
         return False
     if pipe.compute_cov3D_python or override_color is not None:
         return False
+    # opt.include_feature = False with the Python colour path: the reference renders the colours
+    # again as the feature channels (language_feature_precomp = colors_precomp, :296-298), so
+    # "feature" is the bg-0 colour blend and its gradient reaches the SH leaves through the
+    # colours -- the unfused branch below does exactly that.  With the
+    # in-kernel SH path (convert_SHs_python = False) colors_precomp is None and both branches
+    # render zero feature channels.
+    if not opt.include_feature and pipe.convert_SHs_python:
+        return False
     if opt.include_feature and (override_language is not None
                                 or getattr(pc, "_language_feature", None) is None):
         return False

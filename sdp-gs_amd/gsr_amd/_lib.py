@@ -212,6 +212,10 @@ def load():
             ctypes.POINTER(ctypes.c_double),             # step
             ctypes.c_double, ctypes.c_double, ctypes.c_double,  # beta1, beta2, eps
             _p]                                          # stream
+        L.gsr_adam_step_guarded.restype = _i
+        L.gsr_adam_step_guarded.argtypes = list(L.gsr_adam_step.argtypes[:-1]) + [_p, _p, _p]
+        L.gsr_step_guard.restype = _i
+        L.gsr_step_guard.argtypes = [_p, _p]
         # include/gsr_densify.h
         _i64 = ctypes.c_int64
         _u32 = ctypes.c_uint32
@@ -325,10 +329,28 @@ def forward_faults() -> int:
     return int(load().gsr_forward_faults())
 
 
+_FAULT_RESETS = [0]  # how many times reset_forward_faults() ran (gsr_amd.optim reads it)
+
+
 def reset_forward_faults():
     """Clear the fault word (after a failure has been handled); FusedAdam steps again."""
     if load().gsr_reset_forward_faults() != 0:
         raise GsrError("gsr_reset_forward_faults failed")
+    _FAULT_RESETS[0] += 1
+
+
+def fault_resets() -> int:
+    return _FAULT_RESETS[0]
+
+
+def step_guard(slot: "torch.Tensor"):
+    """Write the device's forward-fault snapshot (1.0 failed / 0.0 ok) into the one-float device
+    tensor `slot` on the current stream (include/gsr_optim.h gsr_step_guard)."""
+    import torch
+    if slot.dtype != torch.float32 or slot.numel() < 1 or not slot.is_cuda:
+        raise ValueError("step_guard: slot must be a float32 device tensor")
+    with on_device(slot.device):
+        check(load().gsr_step_guard(slot.data_ptr(), raw_stream(slot.device)))
 
 
 def check_forwards(wait: bool = True):

@@ -7,6 +7,15 @@ the reference's learning-rate schedule (`update_learning_rate`, :277) and its de
 which edits `optimizer.state` and `group["params"]` directly (:400-470), work unchanged.  Only
 `step()` differs: every tensor of every group is updated by ONE HIP launch (one streaming pass,
 28 B per element) instead of PyTorch's per-group foreach passes.  There is no CPU path.
+
+Failed forwards (include/gsr_optim.h): the step is skipped ON THE DEVICE when the step's guard
+slot is set -- the device's forward fault word snapshot, or, with a multi-GPU reducer, that
+snapshot summed over the ranks (``step(skip=reducer.skip_flag())``), so every rank skips together
+when any rank's forward failed.  The launch also reports the decision into a pinned host word; the
+next step() reads it (no synchronisation in the normal case) and, for a skipped step, takes back
+the step counts it had advanced (state["step"]: a skipped step leaves parameters, moments AND
+counts as they were) and raises, unless reset_forward_faults() ran since the skipped step -- a
+caller that swallows one error does not silently stall.
 """
 from __future__ import annotations
 
@@ -26,9 +35,37 @@ class FusedAdam(torch.optim.Adam):
             raise ValueError("FusedAdam implements Adam without amsgrad / maximize")
         super().__init__(params, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay,
                          amsgrad=False, foreach=False)
+        self._mailbox = {}     # device -> pinned int32 [1]: 1 = the last launch skipped the step
+        self._pending = None   # (events, mailboxes, stepped states, fault-reset count)
+        self.skipped_steps = 0
+
+    def _resolve_pending(self):
+        """The previous step's device decision: undo its step counts if it was skipped."""
+        pend, self._pending = self._pending, None
+        if pend is None:
+            return
+        events, boxes, states, resets = pend
+        for ev in events:
+            if not ev.query():
+                ev.synchronize()  # rare: the previous step's launch has not finished yet
+        if not any(int(b[0]) for b in boxes):
+            return
+        for st in states:
+            st["step"] -= 1
+        self.skipped_steps += 1
+        if _lib.fault_resets() == resets:
+            raise RuntimeError(
+                "FusedAdam: the previous step was skipped on the device because a rasterizer "
+                "forward of that step failed (on this or another rank); parameters, moments and "
+                "step counts are unchanged.  Handle the failure and call "
+                "gsr_amd._lib.reset_forward_faults() before stepping again.")
 
     @torch.no_grad()
-    def step(self, closure=None):
+    def step(self, closure=None, *, skip=None):
+        """One Adam step of every parameter with a gradient.  skip: a one-float device tensor
+        whose non-zero value skips the step (GradAllReducer.skip_flag(): the ranks' summed fault
+        snapshots); None = this device's own fault word."""
+        self._resolve_pending()
         loss = None
         if closure is not None:
             with torch.enable_grad():
@@ -62,8 +99,17 @@ class FusedAdam(torch.optim.Adam):
                     (p, g, m, v, float(group["lr"]), float(group["weight_decay"]),
                      float(state["step"])))
         L = _lib.load()
+        events, boxes, states = [], [], [self.state[it[0]] for its in batches.values() for it in its]
         for (dev, beta1, beta2, eps), items in batches.items():
             stream = _lib.raw_stream(dev)
+            box = self._mailbox.get(dev)
+            if box is None:
+                box = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+                self._mailbox[dev] = box
+            box[0] = 0
+            if skip is not None and (skip.device != dev or skip.dtype != torch.float32):
+                raise ValueError("FusedAdam.step: skip must be a float32 tensor on the parameters' device")
+            skip_ptr = None if skip is None else skip.data_ptr()
             for c in range(0, len(items), MAX_TENSORS):
                 chunk = items[c:c + MAX_TENSORS]
                 n = len(chunk)
@@ -73,8 +119,16 @@ class FusedAdam(torch.optim.Adam):
                 wd = (ctypes.c_double * n)(*[it[5] for it in chunk])
                 steps = (ctypes.c_double * n)(*[it[6] for it in chunk])
                 with _lib.on_device(dev):
-                    rc = L.gsr_adam_step(n, ptrs[0], ptrs[1], ptrs[2], ptrs[3], numel, lr, wd,
-                                         steps, beta1, beta2, eps, stream)
+                    rc = L.gsr_adam_step_guarded(n, ptrs[0], ptrs[1], ptrs[2], ptrs[3], numel, lr,
+                                                 wd, steps, beta1, beta2, eps, skip_ptr,
+                                                 box.data_ptr(), stream)
                 if rc != 0:
                     raise RuntimeError(f"gsr_adam_step failed with status {rc}")
+            with _lib.on_device(dev):
+                ev = torch.cuda.Event()
+                ev.record(torch.cuda.current_stream(dev))
+            events.append(ev)
+            boxes.append(box)
+        if events:
+            self._pending = (events, boxes, states, _lib.fault_resets())
         return loss

@@ -42,6 +42,13 @@ class GradAllReducer:
         gradients, flushed in bucket-sized row ranges), then ``wait()``.  RCCL runs the
         collectives on its own stream, ordered after the work already issued on the current
         stream, so they overlap the flush of the next slice.
+
+    Failed forwards: one extra float after the gradients, ``guard``, carries the
+    device's forward-fault snapshot (include/gsr_optim.h gsr_step_guard, written on the current
+    stream once every forward of the step is done) through the same SUM all-reduce, merged into
+    the collective of the last parameter.  After ``wait()``, ``skip_flag()`` is that slot: non-zero
+    on EVERY rank when any rank's forward failed, and ``FusedAdam.step(skip=...)`` then skips the
+    step everywhere -- a failed rank's NaN gradients are in every rank's summed gradients.
     """
 
     def __init__(self, params, bucket_bytes: int = 64 << 20, group=None, average: bool = False):
@@ -75,7 +82,8 @@ class GradAllReducer:
         self.params = params
         dev = params[0].device
         self.numel = sum(p.numel() for p in params)
-        self.flat = torch.zeros(self.numel, dtype=torch.float32, device=dev)
+        self.flat = torch.zeros(self.numel + 1, dtype=torch.float32, device=dev)
+        self.guard = self.flat[self.numel:]  # the step's fault snapshot (see the class docstring)
         per = max(1, self.bucket_bytes // 4)
         self.buckets = [(s, min(s + per, self.numel)) for s in range(0, self.numel, per)]
         self.offsets = []
@@ -138,12 +146,29 @@ class GradAllReducer:
         self._sync_layout()
         self._works = []
         self._done = set()
+        self._guarded = False
 
-    def reduce_async(self, params: Iterable[torch.Tensor]):
-        """Start the all-reduce of these parameters' whole gradients (no-op at world size 1)."""
+    def _write_guard(self):
+        """The device's fault snapshot into the guard slot, on the current stream."""
+        if self.flat.is_cuda:
+            from . import _lib
+            _lib.step_guard(self.guard)
+
+    def skip_flag(self):
+        """The all-reduced fault slot of this step (a one-float device tensor for
+        FusedAdam.step(skip=...)), or None when no guard went through a collective."""
+        return self.guard if getattr(self, "_guarded", False) else None
+
+    def reduce_async(self, params: Iterable[torch.Tensor], guard: bool = False):
+        """Start the all-reduce of these parameters' whole gradients (no-op at world size 1).
+        guard: also reduce the step's fault snapshot (call once the step's forwards are done)."""
         if not self._active():
             return
         spans = []
+        if guard:
+            self._write_guard()
+            spans.append((self.numel, self.numel + 1))
+            self._guarded = True
         for p in params:
             i, lo, hi = self._range(p)
             self._pack(i, lo, hi)
@@ -192,7 +217,7 @@ class GradAllReducer:
         if not self._active():
             return
         self.begin()
-        self.reduce_async(self.params)
+        self.reduce_async(self.params, guard=True)
         self.wait()
 
 

@@ -154,7 +154,9 @@ class ViewPipeline:
             issue(out)
             if reducer is not None:  # every view's backward is done: the non-SH grads are final
                 ids = {id(t) for t in sh_leaves}
-                reducer.reduce_async([p for p in reducer.current_params() if id(p) not in ids])
+                # (with the step's fault snapshot: every forward of the step is done)
+                reducer.reduce_async([p for p in reducer.current_params() if id(p) not in ids],
+                                     guard=True)
         if reducer is not None:
             if sh_leaves and not defer.views_flushed:
                 reducer.reduce_async(sh_leaves)  # no view produced deferred SH gradients

@@ -83,9 +83,21 @@ def _guard_step():
     """Before the optimizer step: raise if a forward of this step already reported a failure
     (non-blocking, include/gsr.h gsr_check_forwards).  A failure not yet published by then is
     caught on the device: FusedAdam leaves the parameters and moments untouched while the
-    device's forward fault word is set (include/gsr_optim.h), and the next check raises."""
+    step's fault snapshot is set (include/gsr_optim.h), and its next step() raises."""
     import diff_gaussian_rasterization as dgr
     dgr.check_forwards(wait=False)
+
+
+def _optimizer_step(model, reducer=None):
+    """optimizer.step(); with a multi-GPU reducer FusedAdam takes the ranks' summed fault
+    snapshot as its skip decision (any rank failed -> every rank skips)."""
+    from .optim import FusedAdam
+    opt = model.optimizer
+    skip = reducer.skip_flag() if reducer is not None else None
+    if isinstance(opt, FusedAdam):
+        opt.step(skip=skip)
+    else:
+        opt.step()
 
 
 def train_iteration(model, cam, gt_image, depth_mono, bg, args: OptArgs, iteration: int,
@@ -103,7 +115,7 @@ def train_iteration(model, cam, gt_image, depth_mono, bg, args: OptArgs, iterati
             if _densify_due(iteration, args):
                 densify_step(model, args, iteration, extent)
         _guard_step()
-        model.optimizer.step()
+        _optimizer_step(model)
         model.optimizer.zero_grad(set_to_none=True)
     return loss.detach()
 
@@ -163,7 +175,7 @@ def train_step_views(model, cams: Sequence, gt_images: Sequence[torch.Tensor],
                                                model.max_radii2D)
                 densify_step(model, args, iteration, extent, generator=generator)
             _guard_step()
-            model.optimizer.step()
+            _optimizer_step(model, reducer)
         return losses
 
     def forward(cam):
@@ -190,5 +202,5 @@ def train_step_views(model, cams: Sequence, gt_images: Sequence[torch.Tensor],
         # after a densification the new parameters have no .grad: Adam skips them, as in the
         # reference (train.py:223-231)
         _guard_step()
-        model.optimizer.step()
+        _optimizer_step(model, reducer)
     return losses

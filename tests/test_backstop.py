@@ -185,19 +185,127 @@ def test_train_step_with_a_failed_forward_leaves_parameters_unchanged():
     assert _lib.forward_faults() != 0
     for p, b in zip(m.parameters(), before):
         assert torch.equal(p.detach(), b)
-    # FusedAdam skips on the device as long as the fault word is set, even with a step issued
-    for p in m.parameters():
-        p.grad = torch.full_like(p, float("nan"))
-    m.optimizer.step()
-    torch.cuda.synchronize()
-    for p, b in zip(m.parameters(), before):
-        assert torch.equal(p.detach(), b)
+    # the failure is handled: reset the fault word; the next iteration steps normally (a step
+    # FusedAdam skipped on the device above, if any, had its step counts taken back)
     _lib.reset_forward_faults()
     m.optimizer.zero_grad(set_to_none=True)
     trainer.train_iteration(m, cam, gts[0], monos[0], bg, args, 2, 2.78)
     torch.cuda.synchronize()
     assert any(not torch.equal(p.detach(), b) for p, b in zip(m.parameters(), before))
     assert all(torch.isfinite(p).all() for p in m.parameters())
+    assert all(float(st["step"]) == 1.0 for st in m.optimizer.state.values())
+
+
+def test_fused_adam_skip_is_one_decision_and_reported():
+    """the skip is decided once per step (a guard snapshot every tensor's workgroups
+    read), reported to the host through a pinned word, and the next step() takes back the step
+    counts of the skipped step and raises -- unless reset_forward_faults() ran since."""
+    from gsr_amd import _lib
+    from gsr_amd.optim import FusedAdam
+    import diff_gaussian_rasterization as dgr
+    dgr.check_forwards(wait=True)
+    _lib.reset_forward_faults()
+    ps = [torch.randn(n, device="cuda").requires_grad_(True) for n in (5000, 333, 70000)]
+    opt = FusedAdam([{"params": [p], "lr": 1e-2} for p in ps], eps=1e-15)
+    for p in ps:
+        p.grad = torch.randn_like(p)
+    opt.step()  # a normal step
+    torch.cuda.synchronize()
+    before = [p.detach().clone() for p in ps]
+    moments = [opt.state[p]["exp_avg"].clone() for p in ps]
+    # a failed forward: the fault word is set
+    with torch.no_grad():
+        _forced_failure(_call)
+    torch.cuda.synchronize()
+    with pytest.raises(_lib.GsrError):
+        dgr.check_forwards(wait=True)
+    for p in ps:
+        p.grad = torch.full_like(p, float("nan"))
+    opt.step()  # skipped on the device (no host synchronisation, no error yet)
+    torch.cuda.synchronize()
+    for p, b, m0 in zip(ps, before, moments):
+        assert torch.equal(p.detach(), b) and torch.equal(opt.state[p]["exp_avg"], m0)
+    with pytest.raises(RuntimeError, match="skipped"):
+        opt.step()  # reports the skipped step; nothing launched
+    assert all(float(opt.state[p]["step"]) == 1.0 for p in ps) and opt.skipped_steps == 1
+    for p, b in zip(ps, before):
+        assert torch.equal(p.detach(), b)
+    # handled: reset, finite gradients, the step applies with the right bias correction (step 2)
+    _lib.reset_forward_faults()
+    for p in ps:
+        p.grad = torch.randn_like(p)
+    opt.step()
+    opt.step()  # resolves the previous (applied) step: no error
+    torch.cuda.synchronize()
+    assert all(float(opt.state[p]["step"]) == 3.0 for p in ps)
+    assert all(not torch.equal(p.detach(), b) for p, b in zip(ps, before))
+    # a caller-provided skip slot (the reducer's all-reduced guard) decides alone
+    slot = torch.ones(1, device="cuda")
+    now = [p.detach().clone() for p in ps]
+    opt.step(skip=slot)
+    torch.cuda.synchronize()
+    assert all(torch.equal(p.detach(), b) for p, b in zip(ps, now))
+    with pytest.raises(RuntimeError, match="skipped"):
+        opt.step()
+    assert all(float(opt.state[p]["step"]) == 3.0 for p in ps)
+
+
+def test_reducer_guard_skips_the_step_on_the_device():
+    """The multi-GPU form at world size 1 (collectives forced on, gloo over the device tensors):
+    the step's forward-fault snapshot goes through the gradient all-reduce and FusedAdam skips on
+    the reduced slot (tests/test_parallel.py checks the cross-rank sum on CPU)."""
+    import os
+    import tempfile
+    import torch.distributed as dist
+    from gsr_amd import _lib, trainer
+    from gsr_amd.model import SplatModel
+    from gsr_amd.parallel import GradAllReducer
+    from gsr_amd.pipeline import ViewPipeline
+    from gsr_amd.synthetic import make_cameras, make_gaussians, training_targets
+    import diff_gaussian_rasterization as dgr
+    dgr.check_forwards(wait=True)
+    _lib.reset_forward_faults()
+    fd, path = tempfile.mkstemp(prefix="gsr_pg_")
+    os.close(fd)
+    os.unlink(path)
+    dist.init_process_group("gloo", init_method="file://" + path, rank=0, world_size=1)
+    try:
+        m = SplatModel(make_gaussians(40_000, sh_degree=3, seed=6), device="cuda")
+        args = trainer.OptArgs()
+        trainer.make_trainable(m, args)
+        cams = [c.to("cuda") for c in make_cameras(2, 320, 240, seed=6)]
+        gts, monos = training_targets(2, 240, 320, seed=2, device="cuda")
+        bg = torch.zeros(3, device="cuda")
+        reducer = GradAllReducer(m)
+        reducer._active = lambda: True
+        pipe = ViewPipeline(torch.device("cuda"), depth=2)
+        step = lambda it: trainer.train_step_views(m, cams, gts, monos, bg, args, it, 2.78,  # noqa: E731
+                                                   pipe, reducer=reducer)
+        step(1)
+        torch.cuda.synchronize()
+        assert float(reducer.skip_flag()) == 0.0
+        before = [p.detach().clone() for p in m.parameters()]
+        raised = False
+        try:
+            _forced_failure(lambda: step(2))
+            torch.cuda.synchronize()
+        except Exception:
+            raised = True
+        try:
+            dgr.check_forwards(wait=True)
+        except _lib.GsrError:
+            raised = True
+        assert raised
+        for p, b in zip(m.parameters(), before):
+            assert torch.equal(p.detach(), b)
+        _lib.reset_forward_faults()
+        step(3)
+        torch.cuda.synchronize()
+        assert float(reducer.skip_flag()) == 0.0
+        assert any(not torch.equal(p.detach(), b) for p, b in zip(m.parameters(), before))
+    finally:
+        dist.destroy_process_group()
+        _lib.reset_forward_faults()
 
 
 def test_sh_deferral_flush_with_one_plane_grad_present():

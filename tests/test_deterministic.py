@@ -107,3 +107,57 @@ def test_deterministic_backward_full_size_rows():
     for a, b, d in zip(g_a, g_b, g_d):
         assert torch.equal(a, b)
         assert float((a - d).abs().max()) <= 1e-5 * float(d.abs().max()) + 1e-30
+
+
+def test_C_backward_takes_the_layout_from_the_binning_buffer():
+    """the reference-signature `_C` backward (only `debug` travels with the buffers)
+    uses the layout its forward wrote into the binning buffer's tag word, whatever the global
+    deterministic() mode is at backward time: a deterministic forward's backward stays bitwise
+    reproducible after the mode was switched off, a default forward's backward runs its atomic
+    layout after the mode was switched on, and a buffer without the tag is refused."""
+    import numpy as np
+    import diff_gaussian_rasterization as dgr
+    from diff_gaussian_rasterization import _C
+    from gsr_amd import _lib
+    from scenes import scene
+    kw = scene(P=40_000, W=320, H=240, seed=3, mode="sh", feature=None)
+    d = lambda x: torch.tensor(np.asarray(x), device="cuda")  # noqa: E731
+    E = torch.Tensor([]).cuda()
+    P = kw["means3D"].shape[0]
+
+    def fwd():
+        return _C.rasterize_gaussians(
+            d(kw["bg"]), d(kw["means3D"]), E, d(kw["opacities"]).view(P, 1), d(kw["scales"]),
+            d(kw["rotations"]), 1.0, E, d(kw["viewmatrix"]), d(kw["projmatrix"]), kw["tanfovx"],
+            kw["tanfovy"], kw["image_height"], kw["image_width"], d(kw["shs"]), kw["sh_degree"],
+            d(kw["campos"]), False, False)
+
+    def bwd(f, dpix, binning=None):
+        nr, color, radii, geom, b, img = f
+        g = _C.rasterize_gaussians_backward(
+            d(kw["bg"]), d(kw["means3D"]), radii, E, d(kw["scales"]), d(kw["rotations"]), 1.0, E,
+            d(kw["viewmatrix"]), d(kw["projmatrix"]), kw["tanfovx"], kw["tanfovy"], dpix,
+            d(kw["shs"]), kw["sh_degree"], d(kw["campos"]), geom, nr, b if binning is None else binning,
+            img, False)
+        torch.cuda.synchronize()
+        return g
+
+    prev = dgr.deterministic()
+    try:
+        dgr.deterministic(True)
+        f_det = fwd()
+        dgr.deterministic(False)
+        f_std = fwd()
+        dpix = torch.randn_like(f_det[1])
+        a, b = bwd(f_det, dpix), bwd(f_det, dpix)  # mode off now: the buffer says deterministic
+        for x, y in zip(a, b):
+            assert torch.equal(x, y)
+        dgr.deterministic(True)
+        c = bwd(f_std, dpix)  # mode on now: the buffer says atomics
+        for x, y in zip(a, c):
+            assert float((x - y).abs().max()) <= 1e-5 * float(y.abs().max()) + 1e-30
+        junk = torch.zeros_like(f_std[4])
+        with pytest.raises(_lib.GsrError, match="binningBuffer"):
+            bwd(f_std, dpix, binning=junk)
+    finally:
+        dgr.deterministic(prev)

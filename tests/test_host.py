@@ -102,20 +102,11 @@ def test_view_pipeline_reducer_with_deferral_needs_the_model():
         vp.run([], lambda cam: cam, model=None, reducer=_Reducer())
 
 
-def test_C_shim_reads_the_deterministic_bit_from_the_binning_buffer():
-    """the `_C` shim's backward takes the forward's deterministic-backward bit from
-    the binning buffer's layout size, not from a bounded table of live forwards."""
-    from diff_gaussian_rasterization._C import _binning_is_deterministic
-    from gsr_amd import _lib
-    L = _lib.load()
-    import diff_gaussian_rasterization as dgr
-    for R in (1, 1000, 3_000_000):
-        det = torch.empty(int(L.gsr_binning_buffer_bytes_det(R)), dtype=torch.uint8)
-        std = torch.empty(int(L.gsr_binning_buffer_bytes(R)), dtype=torch.uint8)
-        if det.numel() == std.numel():  # rows layout by default: the current mode decides
-            assert _binning_is_deterministic(det, R) == dgr.deterministic()
-        else:
-            assert _binning_is_deterministic(det, R) and not _binning_is_deterministic(std, R)
-    with pytest.raises(RuntimeError):
-        _binning_is_deterministic(torch.empty(7, dtype=torch.uint8), 1000)
-    assert not _binning_is_deterministic(None, 0)
+def test_C_shim_asks_for_the_layout_from_the_buffer():
+    """the `_C` shim's backward passes GSR_DEBUG_LAYOUT_FROM_BUFFER, so the library
+    reads the forward's layout from the tag word in its binning buffer -- no size inference, no
+    global mode (the GPU side: tests/test_deterministic.py)."""
+    import inspect
+    from diff_gaussian_rasterization import _C
+    src = inspect.getsource(_C.rasterize_gaussians_backward)
+    assert "| 4" in src and "deterministic" not in src.split("flags =")[1].split("\n")[0]

@@ -166,3 +166,56 @@ def test_shard_views_partition():
             assert flat == list(range(n))
             sizes = [len(s) for s in shards]
             assert max(sizes) - min(sizes) <= 1
+
+
+def _guard_worker(rank, world, init, fail_rank, q):
+    """the step's fault snapshot rides the gradient all-reduce (one float after the
+    gradients, summed), so every rank learns that some rank's forward failed.  On CPU the device
+    guard kernel does not run; the failing rank writes its slot the way gsr_step_guard would."""
+    dist.init_process_group("gloo", init_method=init, rank=rank, world_size=world)
+    params = _params()
+    reducer = GradAllReducer(params, bucket_bytes=4096)
+    if rank == fail_rank:
+        reducer._write_guard = lambda: reducer.guard.fill_(1.0)
+    out = []
+    for step in range(2):
+        reducer.attach_grads()
+        assert float(reducer.guard) == 0.0  # zeroed with the gradients every step
+        for v in shard_views(4, rank, world):
+            _view_loss(params, v).backward()
+        if step == 1:
+            reducer._write_guard = lambda: None  # the failure was handled: a clean step
+        reducer.begin()
+        reducer.reduce_async([params[0], params[2]], guard=True)  # ViewPipeline's early batch
+        rows = params[1].shape[0]
+        for a in range(0, rows, 256):
+            reducer.reduce_rows_async(params[1], a, min(rows, a + 256))
+        reducer.wait()
+        flag = reducer.skip_flag()
+        out.append((None if flag is None else float(flag), [p.grad.numpy().copy() for p in params]))
+    q.put((rank, out))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_fault_guard_rides_the_allreduce():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    init = _init_method()
+    procs = [ctx.Process(target=_guard_worker, args=(r, 2, init, 1, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref = _params()
+    for v in range(4):
+        _view_loss(ref, v).backward()
+    for rank in (0, 1):
+        (flag0, g0), (flag1, g1) = res[rank]
+        assert flag0 == 1.0, (rank, flag0)  # rank 1 failed: every rank skips step 0
+        assert flag1 == 0.0, (rank, flag1)
+        for gs in (g0, g1):  # the gradient sums are unaffected by the extra slot
+            for g, r in zip(gs, ref):
+                torch.testing.assert_close(torch.from_numpy(g), r.grad, rtol=1e-5, atol=1e-6)
