@@ -14,8 +14,8 @@
  */
 #include "gsr_oracle.h"
 
-#include <math.h>
 #include <pthread.h>
+#include <tgmath.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -23,6 +23,14 @@
 #define BLOCK_X 16 /* config.h:16 */
 #define BLOCK_Y 16 /* config.h:17 */
 #define NCH 8      /* blend channels: r g b | depth | alpha | f0 f1 f2 */
+
+/* Arithmetic type of the restatement (gsr_oracle.h ORACLE_REAL): float, the reference's own
+ * type, for the checker the GPU path is compared with; double for the float64 build
+ * (oracle/Makefile: _build/libgsr_oracle_f64.so), which evaluates the same expressions, in the
+ * same order, on the same float32 inputs with the same float constants, so that per-entry
+ * differences of float32 results against it measure float32 rounding (tests/test_f64_parity.py).
+ * The float-defined helpers (splat_exp / splat_log and the exact tile cull) stay float. */
+typedef ORACLE_REAL real;
 
 /* SH constants, auxiliary.h:22-39 */
 static const float SH_C0 = 0.28209479177387814f;
@@ -37,11 +45,11 @@ static const float SH_C3[7] = {-0.5900435899266435f, 2.890611442640554f, -0.4570
 /* glm-like column-major 3x3 maths with glm's evaluation order (the reference uses glm, which  */
 /* is un-vendored; column-major constructor semantics matter).                   */
 /* ------------------------------------------------------------------------------------------ */
-typedef struct { float x, y, z; } v3;
-typedef struct { float m[3][3]; } m3; /* m[col][row] like glm::mat3 */
+typedef struct { real x, y, z; } v3;
+typedef struct { real m[3][3]; } m3; /* m[col][row] like glm::mat3 */
 
-static m3 m3_cols(float a0, float a1, float a2, float b0, float b1, float b2, float c0, float c1,
-                  float c2) {
+static m3 m3_cols(real a0, real a1, real a2, real b0, real b1, real b2, real c0, real c1,
+                  real c2) {
     m3 r;
     r.m[0][0] = a0; r.m[0][1] = a1; r.m[0][2] = a2;
     r.m[1][0] = b0; r.m[1][1] = b1; r.m[1][2] = b2;
@@ -53,9 +61,9 @@ static m3 m3_mul(m3 a, m3 b) {
     m3 r;
     for (int c = 0; c < 3; c++)
         for (int w = 0; w < 3; w++) {
-            float t0 = a.m[0][w] * b.m[c][0];
-            float t1 = a.m[1][w] * b.m[c][1];
-            float t2 = a.m[2][w] * b.m[c][2];
+            real t0 = a.m[0][w] * b.m[c][0];
+            real t1 = a.m[1][w] * b.m[c][1];
+            real t2 = a.m[2][w] * b.m[c][2];
             r.m[c][w] = t0 + t1 + t2;
         }
     return r;
@@ -66,31 +74,31 @@ static m3 m3_T(m3 a) {
         for (int w = 0; w < 3; w++) r.m[c][w] = a.m[w][c];
     return r;
 }
-static m3 m3_scale(float s, m3 a) {
+static m3 m3_scale(real s, m3 a) {
     m3 r;
     for (int c = 0; c < 3; c++)
         for (int w = 0; w < 3; w++) r.m[c][w] = s * a.m[c][w];
     return r;
 }
-static float v3_dot(v3 a, v3 b) {
-    float tx = a.x * b.x, ty = a.y * b.y, tz = a.z * b.z;
+static real v3_dot(v3 a, v3 b) {
+    real tx = a.x * b.x, ty = a.y * b.y, tz = a.z * b.z;
     return tx + ty + tz;
 }
-static v3 v3_mk(float x, float y, float z) { v3 r = {x, y, z}; return r; }
+static v3 v3_mk(real x, real y, real z) { v3 r = {x, y, z}; return r; }
 static v3 v3_add(v3 a, v3 b) { return v3_mk(a.x + b.x, a.y + b.y, a.z + b.z); }
 static v3 v3_sub(v3 a, v3 b) { return v3_mk(a.x - b.x, a.y - b.y, a.z - b.z); }
-static v3 v3_muls(float s, v3 a) { return v3_mk(s * a.x, s * a.y, s * a.z); }
-static v3 v3_mul_s(v3 a, float s) { return v3_mk(a.x * s, a.y * s, a.z * s); }
+static v3 v3_muls(real s, v3 a) { return v3_mk(s * a.x, s * a.y, s * a.z); }
+static v3 v3_mul_s(v3 a, real s) { return v3_mk(a.x * s, a.y * s, a.z * s); }
 
 /* CUDA/HIP float->int conversion semantics: round toward zero, saturate, NaN -> 0. */
-static int f2i_sat(float f) {
+static int f2i_sat(real f) {
     if (f != f) return 0;
     if (f >= 2147483648.0f) return 2147483647;
     if (f <= -2147483648.0f) return (-2147483647 - 1);
     return (int)f;
 }
-static float fminf_cuda(float a, float b) { return fminf(a, b); }
-static float fmaxf_cuda(float a, float b) { return fmaxf(a, b); }
+static real fminf_cuda(real a, real b) { return fmin(a, b); }
+static real fmaxf_cuda(real a, real b) { return fmax(a, b); }
 
 /* The blend's Gaussian weight exp(power) (forward.cu:343, backward.cu:498 call expf): the same
  * deterministic single-precision exp the HIP kernels evaluate (sdp-gs_amd/csrc/gsr_device.h
@@ -111,6 +119,17 @@ static float splat_exp(float x) {
     const float y = fmaf(p, r2, r) + 1.0f;
     const float res = ldexpf(y, (int)k);
     return x < -104.0f ? 0.0f : res;
+}
+/* The blend's G = exp(power) in the arithmetic type: splat_exp for the float checker (or libm's
+ * expf under -DORACLE_LIBM_EXP, the build the threshold census compares with), exp() in the
+ * float64 build. */
+static real blend_exp(real x) {
+#if defined(ORACLE_LIBM_EXP)
+    return expf(x);
+#else
+    if (sizeof(real) == sizeof(float)) return splat_exp((float)x);
+    return exp(x);
+#endif
 }
 void oracle_splat_exp(long n, const float* x, float* out) {
     for (long i = 0; i < n; i++) out[i] = splat_exp(x[i]);
@@ -208,16 +227,16 @@ static void cut_row_range(const splat_cut* s, unsigned ty, unsigned x0, unsigned
 }
 
 /* auxiliary.h:41-44: promoted to double */
-static float ndc2Pix(float v, int S) { return (float)((((double)v + 1.0) * S - 1.0) * 0.5); }
+static real ndc2Pix(real v, int S) { return (real)((((double)v + 1.0) * S - 1.0) * 0.5); }
 
 typedef struct { unsigned x, y; } u2;
 /* auxiliary.h:46-56 */
-static void getRect(float px, float py, int max_radius, u2* rmin, u2* rmax, unsigned gx,
+static void getRect(real px, real py, int max_radius, u2* rmin, u2* rmax, unsigned gx,
                     unsigned gy) {
-    int a = f2i_sat((px - (float)max_radius) / (float)BLOCK_X);
-    int b = f2i_sat((py - (float)max_radius) / (float)BLOCK_Y);
-    int c = f2i_sat((((px + (float)max_radius) + (float)BLOCK_X) - 1.0f) / (float)BLOCK_X);
-    int d = f2i_sat((((py + (float)max_radius) + (float)BLOCK_Y) - 1.0f) / (float)BLOCK_Y);
+    int a = f2i_sat((px - (real)max_radius) / (real)BLOCK_X);
+    int b = f2i_sat((py - (real)max_radius) / (real)BLOCK_Y);
+    int c = f2i_sat((((px + (real)max_radius) + (real)BLOCK_X) - 1.0f) / (real)BLOCK_X);
+    int d = f2i_sat((((py + (real)max_radius) + (real)BLOCK_Y) - 1.0f) / (real)BLOCK_Y);
     a = a > 0 ? a : 0; b = b > 0 ? b : 0; c = c > 0 ? c : 0; d = d > 0 ? d : 0;
     rmin->x = (unsigned)a < gx ? (unsigned)a : gx;
     rmin->y = (unsigned)b < gy ? (unsigned)b : gy;
@@ -226,26 +245,26 @@ static void getRect(float px, float py, int max_radius, u2* rmin, u2* rmax, unsi
 }
 
 /* auxiliary.h:58-87 */
-static v3 transformPoint4x3(v3 p, const float* m) {
+static v3 transformPoint4x3(v3 p, const real* m) {
     return v3_mk(m[0] * p.x + m[4] * p.y + m[8] * p.z + m[12],
                  m[1] * p.x + m[5] * p.y + m[9] * p.z + m[13],
                  m[2] * p.x + m[6] * p.y + m[10] * p.z + m[14]);
 }
-static void transformPoint4x4(v3 p, const float* m, float out[4]) {
+static void transformPoint4x4(v3 p, const real* m, real out[4]) {
     out[0] = m[0] * p.x + m[4] * p.y + m[8] * p.z + m[12];
     out[1] = m[1] * p.x + m[5] * p.y + m[9] * p.z + m[13];
     out[2] = m[2] * p.x + m[6] * p.y + m[10] * p.z + m[14];
     out[3] = m[3] * p.x + m[7] * p.y + m[11] * p.z + m[15];
 }
 /* auxiliary.h:89-97 */
-static v3 transformVec4x3Transpose(v3 p, const float* m) {
+static v3 transformVec4x3Transpose(v3 p, const real* m) {
     return v3_mk(m[0] * p.x + m[1] * p.y + m[2] * p.z, m[4] * p.x + m[5] * p.y + m[6] * p.z,
                  m[8] * p.x + m[9] * p.y + m[10] * p.z);
 }
 /* auxiliary.h:107-117 */
 static v3 dnormvdv(v3 v, v3 dv) {
-    float sum2 = v.x * v.x + v.y * v.y + v.z * v.z;
-    float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
+    real sum2 = v.x * v.x + v.y * v.y + v.z * v.z;
+    real invsum32 = 1.0f / sqrt(sum2 * sum2 * sum2);
     v3 r;
     r.x = ((+sum2 - v.x * v.x) * dv.x - v.y * v.x * dv.y - v.z * v.x * dv.z) * invsum32;
     r.y = (-v.x * v.y * dv.x + (sum2 - v.y * v.y) * dv.y - v.z * v.y * dv.z) * invsum32;
@@ -259,48 +278,48 @@ static v3 dnormvdv(v3 v, v3 dv) {
 struct oracle_state {
     int P, M, D, W, H, prefiltered, include_feature;
     unsigned gx, gy;
-    float scale_modifier, tan_fovx, tan_fovy, focal_x, focal_y;
-    float bg[3], view[16], proj[16], campos[3];
+    real scale_modifier, tan_fovx, tan_fovy, focal_x, focal_y;
+    real bg[3], view[16], proj[16], campos[3];
     /* inputs (borrowed: the caller keeps them alive between forward and backward) */
     const float *means3D, *colors_precomp, *opacities, *scales, *rotations, *cov3D_precomp, *sh,
         *sh_language, *lang_precomp, *confidence;
     /* geometry (GeometryState, rasterizer_impl.h:21-37) */
-    float* depths;
+    real* depths;
     unsigned char* clamped; /* [P*3] */
     int* radii;
-    float* means2D;       /* [P*2] */
-    float* cov3D;         /* [P*6] */
-    float* conic_opacity; /* [P*4] (opacity already multiplied by confidence) */
-    float* rgb;           /* [P*3] */
-    float* feat;          /* [P*3] */
+    real* means2D;       /* [P*2] */
+    real* cov3D;         /* [P*6] */
+    real* conic_opacity; /* [P*4] (opacity already multiplied by confidence) */
+    real* rgb;           /* [P*3] */
+    real* feat;          /* [P*3] */
     unsigned* tiles_touched;
     /* binning */
     int R;
     unsigned* point_list;
     unsigned* ranges; /* [tiles*2] */
     /* image */
-    float* final_T;
+    real* final_T;
     unsigned* n_contrib;
-    float* margin; /* [H*W] test-side diagnostic, see oracle_get_margin */
+    real* margin; /* [H*W] test-side diagnostic, see oracle_get_margin */
 };
 
 /* forward.cu:20-71 computeColorFromSH */
-static v3 color_from_sh(int idx, int deg, int max_coeffs, const float* means, const float* campos,
+static v3 color_from_sh(int idx, int deg, int max_coeffs, const float* means, const real* campos,
                         const float* shs, unsigned char* clamped) {
     v3 pos = v3_mk(means[3 * idx], means[3 * idx + 1], means[3 * idx + 2]);
     v3 dir = v3_sub(pos, v3_mk(campos[0], campos[1], campos[2]));
-    float len = sqrtf(v3_dot(dir, dir));
+    real len = sqrt(v3_dot(dir, dir));
     dir = v3_mk(dir.x / len, dir.y / len, dir.z / len);
     const float* s = shs + (size_t)idx * max_coeffs * 3;
 #define SH(k) v3_mk(s[3 * (k)], s[3 * (k) + 1], s[3 * (k) + 2])
     v3 result = v3_muls(SH_C0, SH(0));
     if (deg > 0) {
-        float x = dir.x, y = dir.y, z = dir.z;
+        real x = dir.x, y = dir.y, z = dir.z;
         result = v3_sub(v3_add(v3_sub(result, v3_muls(SH_C1 * y, SH(1))), v3_muls(SH_C1 * z, SH(2))),
                         v3_muls(SH_C1 * x, SH(3)));
         if (deg > 1) {
-            float xx = x * x, yy = y * y, zz = z * z;
-            float xy = x * y, yz = y * z, xz = x * z;
+            real xx = x * x, yy = y * y, zz = z * z;
+            real xy = x * y, yz = y * z, xz = x * z;
             result = v3_add(result, v3_muls(SH_C2[0] * xy, SH(4)));
             result = v3_add(result, v3_muls(SH_C2[1] * yz, SH(5)));
             result = v3_add(result, v3_muls(SH_C2[2] * (2.0f * zz - xx - yy), SH(6)));
@@ -327,13 +346,13 @@ static v3 color_from_sh(int idx, int deg, int max_coeffs, const float* means, co
 }
 
 /* forward.cu:74-113 computeCov2D */
-static void cov2d(v3 mean, float fx, float fy, float tanx, float tany, const float* c3,
-                  const float* view, float out[3]) {
+static void cov2d(v3 mean, real fx, real fy, real tanx, real tany, const real* c3,
+                  const real* view, real out[3]) {
     v3 t = transformPoint4x3(mean, view);
-    const float limx = 1.3f * tanx;
-    const float limy = 1.3f * tany;
-    const float txtz = t.x / t.z;
-    const float tytz = t.y / t.z;
+    const real limx = 1.3f * tanx;
+    const real limy = 1.3f * tany;
+    const real txtz = t.x / t.z;
+    const real tytz = t.y / t.z;
     t.x = fminf_cuda(limx, fmaxf_cuda(-limx, txtz)) * t.z;
     t.y = fminf_cuda(limy, fmaxf_cuda(-limy, tytz)) * t.z;
     m3 J = m3_cols(fx / t.z, 0.0f, -(fx * t.x) / (t.z * t.z), 0.0f, fy / t.z,
@@ -351,12 +370,12 @@ static void cov2d(v3 mean, float fx, float fy, float tanx, float tany, const flo
 }
 
 /* forward.cu:118-152 computeCov3D (no quaternion normalisation, :127) */
-static void cov3d(const float* scale, float mod, const float* rot, float* out) {
+static void cov3d(const float* scale, real mod, const float* rot, real* out) {
     m3 S = m3_cols(1, 0, 0, 0, 1, 0, 0, 0, 1);
     S.m[0][0] = mod * scale[0];
     S.m[1][1] = mod * scale[1];
     S.m[2][2] = mod * scale[2];
-    float r = rot[0], x = rot[1], y = rot[2], z = rot[3];
+    real r = rot[0], x = rot[1], y = rot[2], z = rot[3];
     m3 R = m3_cols(1.f - 2.f * (y * y + z * z), 2.f * (x * y - r * z), 2.f * (x * z + r * y),
                    2.f * (x * y + r * z), 1.f - 2.f * (x * x + z * z), 2.f * (y * z - r * x),
                    2.f * (x * z - r * y), 2.f * (y * z + r * x), 1.f - 2.f * (x * x + y * y));
@@ -371,7 +390,7 @@ static void cov3d(const float* scale, float mod, const float* rot, float* out) {
 }
 
 /* auxiliary.h:139-164 in_frustum (near-plane test only) */
-static int in_frustum(int idx, const float* pts, const float* view, v3* p_view) {
+static int in_frustum(int idx, const float* pts, const real* view, v3* p_view) {
     v3 p = v3_mk(pts[3 * idx], pts[3 * idx + 1], pts[3 * idx + 2]);
     *p_view = transformPoint4x3(p, view);
     return !(p_view->z <= 0.2f);
@@ -380,9 +399,11 @@ static int in_frustum(int idx, const float* pts, const float* view, v3* p_view) 
 int oracle_mark_visible(int P, const float* means3D, const float* viewmatrix,
                         const float* projmatrix, unsigned char* present) {
     (void)projmatrix; /* in_frustum computes p_proj but only uses p_view (auxiliary.h:149-154) */
+    real view[16];
+    for (int k = 0; k < 16; k++) view[k] = viewmatrix[k];
     for (int i = 0; i < P; i++) {
         v3 pv;
-        present[i] = (unsigned char)in_frustum(i, means3D, viewmatrix, &pv);
+        present[i] = (unsigned char)in_frustum(i, means3D, view, &pv);
     }
     return 0;
 }
@@ -457,29 +478,26 @@ static void preprocess_one(oracle_state* st, int idx) {
     v3 p_view;
     if (!in_frustum(idx, means3D, st->view, &p_view)) return;
     v3 p_orig = v3_mk(means3D[3 * idx], means3D[3 * idx + 1], means3D[3 * idx + 2]);
-    float p_hom[4];
+    real p_hom[4];
     transformPoint4x4(p_orig, st->proj, p_hom);
-    float p_w = 1.0f / (p_hom[3] + 0.0000001f);
-    float p_proj_x = p_hom[0] * p_w, p_proj_y = p_hom[1] * p_w;
-    const float* c3;
-    if (st->cov3D_precomp) {
-        c3 = st->cov3D_precomp + (size_t)idx * 6;
-    } else {
+    real p_w = 1.0f / (p_hom[3] + 0.0000001f);
+    real p_proj_x = p_hom[0] * p_w, p_proj_y = p_hom[1] * p_w;
+    /* cov3D_precomp was converted into st->cov3D by oracle_forward */
+    if (!st->cov3D_precomp)
         cov3d(st->scales + 3 * (size_t)idx, st->scale_modifier, st->rotations + 4 * (size_t)idx,
               st->cov3D + (size_t)idx * 6);
-        c3 = st->cov3D + (size_t)idx * 6;
-    }
-    float cov[3];
+    const real* c3 = st->cov3D + (size_t)idx * 6;
+    real cov[3];
     cov2d(p_orig, st->focal_x, st->focal_y, st->tan_fovx, st->tan_fovy, c3, st->view, cov);
-    float det = (cov[0] * cov[2] - cov[1] * cov[1]);
+    real det = (cov[0] * cov[2] - cov[1] * cov[1]);
     if (det == 0.0f) return;
-    float det_inv = 1.f / det;
-    float conic[3] = {cov[2] * det_inv, -cov[1] * det_inv, cov[0] * det_inv};
-    float mid = 0.5f * (cov[0] + cov[2]);
-    float lambda1 = mid + sqrtf(fmaxf_cuda(0.1f, mid * mid - det));
-    float lambda2 = mid - sqrtf(fmaxf_cuda(0.1f, mid * mid - det));
-    float my_radius = ceilf(3.f * sqrtf(fmaxf_cuda(lambda1, lambda2)));
-    float pix_x = ndc2Pix(p_proj_x, W), pix_y = ndc2Pix(p_proj_y, H);
+    real det_inv = 1.f / det;
+    real conic[3] = {cov[2] * det_inv, -cov[1] * det_inv, cov[0] * det_inv};
+    real mid = 0.5f * (cov[0] + cov[2]);
+    real lambda1 = mid + sqrt(fmaxf_cuda(0.1f, mid * mid - det));
+    real lambda2 = mid - sqrt(fmaxf_cuda(0.1f, mid * mid - det));
+    real my_radius = ceil(3.f * sqrt(fmaxf_cuda(lambda1, lambda2)));
+    real pix_x = ndc2Pix(p_proj_x, W), pix_y = ndc2Pix(p_proj_y, H);
     u2 rmin, rmax;
     getRect(pix_x, pix_y, f2i_sat(my_radius), &rmin, &rmax, st->gx, st->gy);
     if ((rmax.x - rmin.x) * (rmax.y - rmin.y) == 0) return;
@@ -493,7 +511,7 @@ static void preprocess_one(oracle_state* st, int idx) {
     st->radii[idx] = f2i_sat(my_radius);
     st->means2D[2 * idx] = pix_x;
     st->means2D[2 * idx + 1] = pix_y;
-    float op = st->opacities[idx];
+    real op = st->opacities[idx];
     if (st->confidence) op = op * st->confidence[idx]; /* confidence = opacity multiplier */
     st->conic_opacity[4 * idx + 0] = conic[0];
     st->conic_opacity[4 * idx + 1] = conic[1];
@@ -505,9 +523,9 @@ static void preprocess_one(oracle_state* st, int idx) {
             for (int k = 0; k < 3; k++) st->feat[3 * idx + k] = st->lang_precomp[3 * idx + k];
         } else if (st->sh_language) {
             const float* l = st->sh_language;
-            float u0 = SH_C0 * l[3 * idx], u1 = SH_C0 * l[3 * idx + 1], u2v = SH_C0 * l[3 * idx + 2];
-            float n = sqrtf(u0 * u0 + u1 * u1 + u2v * u2v);
-            float den = n + 1e-9f;
+            real u0 = SH_C0 * l[3 * idx], u1 = SH_C0 * l[3 * idx + 1], u2v = SH_C0 * l[3 * idx + 2];
+            real n = sqrt(u0 * u0 + u1 * u1 + u2v * u2v);
+            real den = n + 1e-9f;
             st->feat[3 * idx + 0] = u0 / den;
             st->feat[3 * idx + 1] = u1 / den;
             st->feat[3 * idx + 2] = u2v / den;
@@ -571,7 +589,7 @@ static void sort_instances(inst_t* a, long n) {
 typedef struct {
     oracle_state* st;
     const float* background;
-    float *out_color, *out_depth, *out_alpha, *out_feature;
+    real *out_color, *out_depth, *out_alpha, *out_feature;
 } blend_fwd_ctx;
 static void blend_fwd_rows(void* ctx, long lo, long hi, int chunk) {
     (void)chunk;
@@ -579,32 +597,32 @@ static void blend_fwd_rows(void* ctx, long lo, long hi, int chunk) {
     oracle_state* st = c->st;
     const int W = st->W, H = st->H;
     const unsigned gx = st->gx;
-    const float* feat_ptr = st->colors_precomp ? st->colors_precomp : st->rgb;
+    const real* feat_ptr = st->rgb; /* colors_precomp converted into rgb by oracle_forward */
     const int nch = st->include_feature ? NCH : 5;
     for (long py = lo; py < hi; py++)
         for (int px = 0; px < W; px++) {
             const unsigned tile = (unsigned)(py / BLOCK_Y) * gx + (unsigned)(px / BLOCK_X);
             const unsigned rs = st->ranges[2 * tile], re = st->ranges[2 * tile + 1];
-            const float pfx = (float)px, pfy = (float)py;
-            float T = 1.0f;
+            const real pfx = (real)px, pfy = (real)py;
+            real T = 1.0f;
             unsigned contributor = 0, last_contributor = 0;
-            float C[NCH] = {0};
-            float margin = 1.0f;
+            real C[NCH] = {0};
+            real margin = 1.0f;
             for (unsigned k = rs; k < re; k++) {
                 contributor++;
                 const unsigned g = st->point_list[k];
-                const float dx = st->means2D[2 * g] - pfx, dy = st->means2D[2 * g + 1] - pfy;
-                const float* co = st->conic_opacity + 4 * (size_t)g;
-                float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
-                if (fabsf(power) < 1e-6f) margin = 0.0f;
+                const real dx = st->means2D[2 * g] - pfx, dy = st->means2D[2 * g + 1] - pfy;
+                const real* co = st->conic_opacity + 4 * (size_t)g;
+                real power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
+                if (fabs(power) < 1e-6f) margin = 0.0f;
                 if (power > 0.0f) continue;
-                float alpha = fminf_cuda(0.99f, co[3] * splat_exp(power));
-                margin = fminf(margin, fabsf(alpha * 255.0f - 1.0f));
+                real alpha = fminf_cuda(0.99f, co[3] * blend_exp(power));
+                margin = fmin(margin, fabs(alpha * 255.0f - 1.0f));
                 if (alpha < 1.0f / 255.0f) continue;
-                float test_T = T * (1 - alpha);
-                margin = fminf(margin, fabsf(test_T * 1e4f - 1.0f));
+                real test_T = T * (1 - alpha);
+                margin = fmin(margin, fabs(test_T * 1e4f - 1.0f));
                 if (test_T < 0.0001f) break; /* done: nothing later changes this pixel */
-                float v[NCH];
+                real v[NCH];
                 v[0] = feat_ptr[3 * g]; v[1] = feat_ptr[3 * g + 1]; v[2] = feat_ptr[3 * g + 2];
                 v[3] = st->depths[g]; v[4] = 1.0f;
                 v[5] = st->feat[3 * g]; v[6] = st->feat[3 * g + 1]; v[7] = st->feat[3 * g + 2];
@@ -633,8 +651,8 @@ oracle_state* oracle_forward(int P, int M, const float* background, const float*
                              int image_height, int image_width, const float* sh, int degree,
                              const float* campos, int prefiltered, const float* sh_language,
                              const float* language_feature_precomp, const float* confidence,
-                             int include_feature, float* out_color, float* out_depth,
-                             float* out_alpha, float* out_feature, int* radii_out,
+                             int include_feature, real* out_color, real* out_depth,
+                             real* out_alpha, real* out_feature, int* radii_out,
                              int* num_rendered) {
     if (P < 0 || image_height <= 0 || image_width <= 0) return NULL;
     if (!colors_precomp && !sh) return NULL;
@@ -645,12 +663,12 @@ oracle_state* oracle_forward(int P, int M, const float* background, const float*
     st->prefiltered = prefiltered; st->include_feature = include_feature;
     st->scale_modifier = scale_modifier; st->tan_fovx = tan_fovx; st->tan_fovy = tan_fovy;
     /* rasterizer_impl.cu:222-223 */
-    st->focal_y = (float)H / (2.0f * tan_fovy);
-    st->focal_x = (float)W / (2.0f * tan_fovx);
-    memcpy(st->bg, background, sizeof(st->bg));
-    memcpy(st->view, viewmatrix, sizeof(st->view));
-    memcpy(st->proj, projmatrix, sizeof(st->proj));
-    memcpy(st->campos, campos, sizeof(st->campos));
+    st->focal_y = (real)H / (2.0f * tan_fovy);
+    st->focal_x = (real)W / (2.0f * tan_fovx);
+    for (int k = 0; k < 3; k++) st->bg[k] = background[k];
+    for (int k = 0; k < 16; k++) st->view[k] = viewmatrix[k];
+    for (int k = 0; k < 16; k++) st->proj[k] = projmatrix[k];
+    for (int k = 0; k < 3; k++) st->campos[k] = campos[k];
     st->means3D = means3D; st->colors_precomp = colors_precomp; st->opacities = opacities;
     st->scales = scales; st->rotations = rotations; st->cov3D_precomp = cov3D_precomp;
     st->sh = sh; st->sh_language = sh_language; st->lang_precomp = language_feature_precomp;
@@ -660,17 +678,22 @@ oracle_state* oracle_forward(int P, int M, const float* background, const float*
     st->gy = (unsigned)((H + BLOCK_Y - 1) / BLOCK_Y);
     const unsigned gx = st->gx, gy = st->gy;
 
-    st->depths = (float*)xcalloc(P, sizeof(float));
+    st->depths = (real*)xcalloc(P, sizeof(real));
     st->clamped = (unsigned char*)xcalloc((size_t)P * 3, 1);
     st->radii = (int*)xcalloc(P, sizeof(int));
-    st->means2D = (float*)xcalloc((size_t)P * 2, sizeof(float));
-    st->cov3D = (float*)xcalloc((size_t)P * 6, sizeof(float));
-    st->conic_opacity = (float*)xcalloc((size_t)P * 4, sizeof(float));
-    st->rgb = (float*)xcalloc((size_t)P * 3, sizeof(float));
-    st->feat = (float*)xcalloc((size_t)P * 3, sizeof(float));
+    st->means2D = (real*)xcalloc((size_t)P * 2, sizeof(real));
+    st->cov3D = (real*)xcalloc((size_t)P * 6, sizeof(real));
+    st->conic_opacity = (real*)xcalloc((size_t)P * 4, sizeof(real));
+    st->rgb = (real*)xcalloc((size_t)P * 3, sizeof(real));
+    st->feat = (real*)xcalloc((size_t)P * 3, sizeof(real));
     st->tiles_touched = (unsigned*)xcalloc(P, sizeof(unsigned));
 
     /* ---- preprocessCUDA, forward.cu:155-256 ---- */
+    /* precomputed colours / covariances in the arithmetic type (exact for float) */
+    if (colors_precomp)
+        for (size_t i = 0; i < (size_t)P * 3; i++) st->rgb[i] = colors_precomp[i];
+    if (cov3D_precomp)
+        for (size_t i = 0; i < (size_t)P * 6; i++) st->cov3D[i] = cov3D_precomp[i];
     par_for(P, preprocess_range, st);
     if (radii_out) memcpy(radii_out, st->radii, sizeof(int) * (size_t)P);
 
@@ -687,7 +710,8 @@ oracle_state* oracle_forward(int P, int M, const float* background, const float*
             getRect(st->means2D[2 * idx], st->means2D[2 * idx + 1], st->radii[idx], &rmin, &rmax,
                     gx, gy);
             uint32_t dbits;
-            memcpy(&dbits, &st->depths[idx], 4);
+            const float dkey = (float)st->depths[idx]; /* the float32 depth bits of the key */
+            memcpy(&dbits, &dkey, 4);
             for (unsigned y = rmin.y; y < rmax.y; y++)
                 for (unsigned x = rmin.x; x < rmax.x; x++) {
                     uint64_t key = (uint64_t)(y * gx + x);
@@ -722,21 +746,21 @@ oracle_state* oracle_forward(int P, int M, const float* background, const float*
     if (num_rendered) *num_rendered = R;
 
     /* ---- renderCUDA (fwd), forward.cu:261-374, extended to NCH channels ---- */
-    st->final_T = (float*)xcalloc((size_t)W * H, sizeof(float));
+    st->final_T = (real*)xcalloc((size_t)W * H, sizeof(real));
     st->n_contrib = (unsigned*)xcalloc((size_t)W * H, sizeof(unsigned));
-    st->margin = (float*)xcalloc((size_t)W * H, sizeof(float));
+    st->margin = (real*)xcalloc((size_t)W * H, sizeof(real));
     blend_fwd_ctx bc = {st, background, out_color, out_depth, out_alpha, out_feature};
     par_for(H, blend_fwd_rows, &bc);
     return st;
 }
 
 /* backward.cu:20-139 computeColorFromSH (bwd) */
-static void sh_backward(int idx, int deg, int max_coeffs, const float* means, const float* campos,
-                        const float* shs, const unsigned char* clamped, const float* dL_dcolor,
-                        float* dL_dmeans, float* dL_dshs) {
+static void sh_backward(int idx, int deg, int max_coeffs, const float* means, const real* campos,
+                        const float* shs, const unsigned char* clamped, const real* dL_dcolor,
+                        real* dL_dmeans, real* dL_dshs) {
     v3 pos = v3_mk(means[3 * idx], means[3 * idx + 1], means[3 * idx + 2]);
     v3 dir_orig = v3_sub(pos, v3_mk(campos[0], campos[1], campos[2]));
-    float len = sqrtf(v3_dot(dir_orig, dir_orig));
+    real len = sqrt(v3_dot(dir_orig, dir_orig));
     v3 dir = v3_mk(dir_orig.x / len, dir_orig.y / len, dir_orig.z / len);
     const float* s = shs + (size_t)idx * max_coeffs * 3;
 #define SH(k) v3_mk(s[3 * (k)], s[3 * (k) + 1], s[3 * (k) + 2])
@@ -745,15 +769,15 @@ static void sh_backward(int idx, int deg, int max_coeffs, const float* means, co
     dL_dRGB.y *= clamped[3 * idx + 1] ? 0 : 1;
     dL_dRGB.z *= clamped[3 * idx + 2] ? 0 : 1;
     v3 dRGBdx = v3_mk(0, 0, 0), dRGBdy = v3_mk(0, 0, 0), dRGBdz = v3_mk(0, 0, 0);
-    float x = dir.x, y = dir.y, z = dir.z;
-    float* d = dL_dshs + (size_t)idx * max_coeffs * 3;
+    real x = dir.x, y = dir.y, z = dir.z;
+    real* d = dL_dshs + (size_t)idx * max_coeffs * 3;
 #define PUT(k, v) do { v3 _t = (v); d[3 * (k)] = _t.x; d[3 * (k) + 1] = _t.y; d[3 * (k) + 2] = _t.z; } while (0)
-    float dRGBdsh0 = SH_C0;
+    real dRGBdsh0 = SH_C0;
     PUT(0, v3_muls(dRGBdsh0, dL_dRGB));
     if (deg > 0) {
-        float dRGBdsh1 = -SH_C1 * y;
-        float dRGBdsh2 = SH_C1 * z;
-        float dRGBdsh3 = -SH_C1 * x;
+        real dRGBdsh1 = -SH_C1 * y;
+        real dRGBdsh2 = SH_C1 * z;
+        real dRGBdsh3 = -SH_C1 * x;
         PUT(1, v3_muls(dRGBdsh1, dL_dRGB));
         PUT(2, v3_muls(dRGBdsh2, dL_dRGB));
         PUT(3, v3_muls(dRGBdsh3, dL_dRGB));
@@ -761,13 +785,13 @@ static void sh_backward(int idx, int deg, int max_coeffs, const float* means, co
         dRGBdy = v3_muls(-SH_C1, SH(1));
         dRGBdz = v3_muls(SH_C1, SH(2));
         if (deg > 1) {
-            float xx = x * x, yy = y * y, zz = z * z;
-            float xy = x * y, yz = y * z, xz = x * z;
-            float dRGBdsh4 = SH_C2[0] * xy;
-            float dRGBdsh5 = SH_C2[1] * yz;
-            float dRGBdsh6 = SH_C2[2] * (2.f * zz - xx - yy);
-            float dRGBdsh7 = SH_C2[3] * xz;
-            float dRGBdsh8 = SH_C2[4] * (xx - yy);
+            real xx = x * x, yy = y * y, zz = z * z;
+            real xy = x * y, yz = y * z, xz = x * z;
+            real dRGBdsh4 = SH_C2[0] * xy;
+            real dRGBdsh5 = SH_C2[1] * yz;
+            real dRGBdsh6 = SH_C2[2] * (2.f * zz - xx - yy);
+            real dRGBdsh7 = SH_C2[3] * xz;
+            real dRGBdsh8 = SH_C2[4] * (xx - yy);
             PUT(4, v3_muls(dRGBdsh4, dL_dRGB));
             PUT(5, v3_muls(dRGBdsh5, dL_dRGB));
             PUT(6, v3_muls(dRGBdsh6, dL_dRGB));
@@ -785,13 +809,13 @@ static void sh_backward(int idx, int deg, int max_coeffs, const float* means, co
             dRGBdy = v3_add(dRGBdy, ty);
             dRGBdz = v3_add(dRGBdz, tz);
             if (deg > 2) {
-                float dRGBdsh9 = SH_C3[0] * y * (3.f * xx - yy);
-                float dRGBdsh10 = SH_C3[1] * xy * z;
-                float dRGBdsh11 = SH_C3[2] * y * (4.f * zz - xx - yy);
-                float dRGBdsh12 = SH_C3[3] * z * (2.f * zz - 3.f * xx - 3.f * yy);
-                float dRGBdsh13 = SH_C3[4] * x * (4.f * zz - xx - yy);
-                float dRGBdsh14 = SH_C3[5] * z * (xx - yy);
-                float dRGBdsh15 = SH_C3[6] * x * (xx - 3.f * yy);
+                real dRGBdsh9 = SH_C3[0] * y * (3.f * xx - yy);
+                real dRGBdsh10 = SH_C3[1] * xy * z;
+                real dRGBdsh11 = SH_C3[2] * y * (4.f * zz - xx - yy);
+                real dRGBdsh12 = SH_C3[3] * z * (2.f * zz - 3.f * xx - 3.f * yy);
+                real dRGBdsh13 = SH_C3[4] * x * (4.f * zz - xx - yy);
+                real dRGBdsh14 = SH_C3[5] * z * (xx - yy);
+                real dRGBdsh15 = SH_C3[6] * x * (xx - 3.f * yy);
                 PUT(9, v3_muls(dRGBdsh9, dL_dRGB));
                 PUT(10, v3_muls(dRGBdsh10, dL_dRGB));
                 PUT(11, v3_muls(dRGBdsh11, dL_dRGB));
@@ -835,21 +859,21 @@ static void sh_backward(int idx, int deg, int max_coeffs, const float* means, co
 }
 
 /* backward.cu:144-274 computeCov2DCUDA (per Gaussian) */
-static void cov2d_backward(int idx, const float* means, const float* cov3D, float h_x, float h_y,
-                           float tan_fovx, float tan_fovy, const float* view,
-                           const float* dL_dconics, float* dL_dmeans, float* dL_dcov) {
-    const float* c3 = cov3D + 6 * (size_t)idx;
+static void cov2d_backward(int idx, const float* means, const real* cov3D, real h_x, real h_y,
+                           real tan_fovx, real tan_fovy, const real* view,
+                           const real* dL_dconics, real* dL_dmeans, real* dL_dcov) {
+    const real* c3 = cov3D + 6 * (size_t)idx;
     v3 mean = v3_mk(means[3 * idx], means[3 * idx + 1], means[3 * idx + 2]);
-    float dcx = dL_dconics[4 * idx], dcy = dL_dconics[4 * idx + 1], dcz = dL_dconics[4 * idx + 3];
+    real dcx = dL_dconics[4 * idx], dcy = dL_dconics[4 * idx + 1], dcz = dL_dconics[4 * idx + 3];
     v3 t = transformPoint4x3(mean, view);
-    const float limx = 1.3f * tan_fovx;
-    const float limy = 1.3f * tan_fovy;
-    const float txtz = t.x / t.z;
-    const float tytz = t.y / t.z;
+    const real limx = 1.3f * tan_fovx;
+    const real limy = 1.3f * tan_fovy;
+    const real txtz = t.x / t.z;
+    const real tytz = t.y / t.z;
     t.x = fminf_cuda(limx, fmaxf_cuda(-limx, txtz)) * t.z;
     t.y = fminf_cuda(limy, fmaxf_cuda(-limy, tytz)) * t.z;
-    const float x_grad_mul = txtz < -limx || txtz > limx ? 0 : 1;
-    const float y_grad_mul = tytz < -limy || tytz > limy ? 0 : 1;
+    const real x_grad_mul = txtz < -limx || txtz > limx ? 0 : 1;
+    const real y_grad_mul = tytz < -limy || tytz > limy ? 0 : 1;
     m3 J = m3_cols(h_x / t.z, 0.0f, -(h_x * t.x) / (t.z * t.z), 0.0f, h_y / t.z,
                    -(h_y * t.y) / (t.z * t.z), 0, 0, 0);
     m3 Wm = m3_cols(view[0], view[4], view[8], view[1], view[5], view[9], view[2], view[6],
@@ -857,13 +881,13 @@ static void cov2d_backward(int idx, const float* means, const float* cov3D, floa
     m3 Vrk = m3_cols(c3[0], c3[1], c3[2], c3[1], c3[3], c3[4], c3[2], c3[4], c3[5]);
     m3 T = m3_mul(Wm, J);
     m3 cov2D = m3_mul(m3_mul(m3_T(T), m3_T(Vrk)), T);
-    float a = cov2D.m[0][0] += 0.3f;
-    float b = cov2D.m[0][1];
-    float c = cov2D.m[1][1] += 0.3f;
-    float denom = a * c - b * b;
-    float dL_da = 0, dL_db = 0, dL_dc = 0;
-    float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
-    float* dc = dL_dcov + 6 * (size_t)idx;
+    real a = cov2D.m[0][0] += 0.3f;
+    real b = cov2D.m[0][1];
+    real c = cov2D.m[1][1] += 0.3f;
+    real denom = a * c - b * b;
+    real dL_da = 0, dL_db = 0, dL_dc = 0;
+    real denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
+    real* dc = dL_dcov + 6 * (size_t)idx;
 #define Tm(cc, rr) T.m[cc][rr]
 #define V(cc, rr) Vrk.m[cc][rr]
     if (denom2inv != 0) {
@@ -882,30 +906,30 @@ static void cov2d_backward(int idx, const float* means, const float* cov3D, floa
     } else {
         for (int i = 0; i < 6; i++) dc[i] = 0;
     }
-    float dL_dT00 = 2 * (Tm(0, 0) * V(0, 0) + Tm(0, 1) * V(0, 1) + Tm(0, 2) * V(0, 2)) * dL_da +
+    real dL_dT00 = 2 * (Tm(0, 0) * V(0, 0) + Tm(0, 1) * V(0, 1) + Tm(0, 2) * V(0, 2)) * dL_da +
                     (Tm(1, 0) * V(0, 0) + Tm(1, 1) * V(0, 1) + Tm(1, 2) * V(0, 2)) * dL_db;
-    float dL_dT01 = 2 * (Tm(0, 0) * V(1, 0) + Tm(0, 1) * V(1, 1) + Tm(0, 2) * V(1, 2)) * dL_da +
+    real dL_dT01 = 2 * (Tm(0, 0) * V(1, 0) + Tm(0, 1) * V(1, 1) + Tm(0, 2) * V(1, 2)) * dL_da +
                     (Tm(1, 0) * V(1, 0) + Tm(1, 1) * V(1, 1) + Tm(1, 2) * V(1, 2)) * dL_db;
-    float dL_dT02 = 2 * (Tm(0, 0) * V(2, 0) + Tm(0, 1) * V(2, 1) + Tm(0, 2) * V(2, 2)) * dL_da +
+    real dL_dT02 = 2 * (Tm(0, 0) * V(2, 0) + Tm(0, 1) * V(2, 1) + Tm(0, 2) * V(2, 2)) * dL_da +
                     (Tm(1, 0) * V(2, 0) + Tm(1, 1) * V(2, 1) + Tm(1, 2) * V(2, 2)) * dL_db;
-    float dL_dT10 = 2 * (Tm(1, 0) * V(0, 0) + Tm(1, 1) * V(0, 1) + Tm(1, 2) * V(0, 2)) * dL_dc +
+    real dL_dT10 = 2 * (Tm(1, 0) * V(0, 0) + Tm(1, 1) * V(0, 1) + Tm(1, 2) * V(0, 2)) * dL_dc +
                     (Tm(0, 0) * V(0, 0) + Tm(0, 1) * V(0, 1) + Tm(0, 2) * V(0, 2)) * dL_db;
-    float dL_dT11 = 2 * (Tm(1, 0) * V(1, 0) + Tm(1, 1) * V(1, 1) + Tm(1, 2) * V(1, 2)) * dL_dc +
+    real dL_dT11 = 2 * (Tm(1, 0) * V(1, 0) + Tm(1, 1) * V(1, 1) + Tm(1, 2) * V(1, 2)) * dL_dc +
                     (Tm(0, 0) * V(1, 0) + Tm(0, 1) * V(1, 1) + Tm(0, 2) * V(1, 2)) * dL_db;
-    float dL_dT12 = 2 * (Tm(1, 0) * V(2, 0) + Tm(1, 1) * V(2, 1) + Tm(1, 2) * V(2, 2)) * dL_dc +
+    real dL_dT12 = 2 * (Tm(1, 0) * V(2, 0) + Tm(1, 1) * V(2, 1) + Tm(1, 2) * V(2, 2)) * dL_dc +
                     (Tm(0, 0) * V(2, 0) + Tm(0, 1) * V(2, 1) + Tm(0, 2) * V(2, 2)) * dL_db;
 #undef Tm
 #undef V
-    float dL_dJ00 = Wm.m[0][0] * dL_dT00 + Wm.m[0][1] * dL_dT01 + Wm.m[0][2] * dL_dT02;
-    float dL_dJ02 = Wm.m[2][0] * dL_dT00 + Wm.m[2][1] * dL_dT01 + Wm.m[2][2] * dL_dT02;
-    float dL_dJ11 = Wm.m[1][0] * dL_dT10 + Wm.m[1][1] * dL_dT11 + Wm.m[1][2] * dL_dT12;
-    float dL_dJ12 = Wm.m[2][0] * dL_dT10 + Wm.m[2][1] * dL_dT11 + Wm.m[2][2] * dL_dT12;
-    float tz = 1.f / t.z;
-    float tz2 = tz * tz;
-    float tz3 = tz2 * tz;
-    float dL_dtx = x_grad_mul * -h_x * tz2 * dL_dJ02;
-    float dL_dty = y_grad_mul * -h_y * tz2 * dL_dJ12;
-    float dL_dtz = -h_x * tz2 * dL_dJ00 - h_y * tz2 * dL_dJ11 + (2 * h_x * t.x) * tz3 * dL_dJ02 +
+    real dL_dJ00 = Wm.m[0][0] * dL_dT00 + Wm.m[0][1] * dL_dT01 + Wm.m[0][2] * dL_dT02;
+    real dL_dJ02 = Wm.m[2][0] * dL_dT00 + Wm.m[2][1] * dL_dT01 + Wm.m[2][2] * dL_dT02;
+    real dL_dJ11 = Wm.m[1][0] * dL_dT10 + Wm.m[1][1] * dL_dT11 + Wm.m[1][2] * dL_dT12;
+    real dL_dJ12 = Wm.m[2][0] * dL_dT10 + Wm.m[2][1] * dL_dT11 + Wm.m[2][2] * dL_dT12;
+    real tz = 1.f / t.z;
+    real tz2 = tz * tz;
+    real tz3 = tz2 * tz;
+    real dL_dtx = x_grad_mul * -h_x * tz2 * dL_dJ02;
+    real dL_dty = y_grad_mul * -h_y * tz2 * dL_dJ12;
+    real dL_dtz = -h_x * tz2 * dL_dJ00 - h_y * tz2 * dL_dJ11 + (2 * h_x * t.x) * tz3 * dL_dJ02 +
                    (2 * h_y * t.y) * tz3 * dL_dJ12;
     v3 dm = transformVec4x3Transpose(v3_mk(dL_dtx, dL_dty, dL_dtz), view);
     dL_dmeans[3 * idx + 0] = dm.x; /* assigned, backward.cu:273 */
@@ -914,9 +938,9 @@ static void cov2d_backward(int idx, const float* means, const float* cov3D, floa
 }
 
 /* backward.cu:278-341 computeCov3D (bwd) */
-static void cov3d_backward(int idx, const float* scale, float mod, const float* rot,
-                           const float* dL_dcov3Ds, float* dL_dscales, float* dL_drots) {
-    float r = rot[0], x = rot[1], y = rot[2], z = rot[3];
+static void cov3d_backward(int idx, const float* scale, real mod, const float* rot,
+                           const real* dL_dcov3Ds, real* dL_dscales, real* dL_drots) {
+    real r = rot[0], x = rot[1], y = rot[2], z = rot[3];
     m3 R = m3_cols(1.f - 2.f * (y * y + z * z), 2.f * (x * y - r * z), 2.f * (x * z + r * y),
                    2.f * (x * y + r * z), 1.f - 2.f * (x * x + z * z), 2.f * (y * z - r * x),
                    2.f * (x * z - r * y), 2.f * (y * z + r * x), 1.f - 2.f * (x * x + y * y));
@@ -924,13 +948,13 @@ static void cov3d_backward(int idx, const float* scale, float mod, const float* 
     v3 s = v3_muls(mod, v3_mk(scale[0], scale[1], scale[2]));
     S.m[0][0] = s.x; S.m[1][1] = s.y; S.m[2][2] = s.z;
     m3 M = m3_mul(S, R);
-    const float* g = dL_dcov3Ds + 6 * (size_t)idx;
+    const real* g = dL_dcov3Ds + 6 * (size_t)idx;
     m3 dL_dSigma = m3_cols(g[0], 0.5f * g[1], 0.5f * g[2], 0.5f * g[1], g[3], 0.5f * g[4],
                            0.5f * g[2], 0.5f * g[4], g[5]);
     m3 dL_dM = m3_mul(m3_scale(2.0f, M), dL_dSigma);
     m3 Rt = m3_T(R);
     m3 dL_dMt = m3_T(dL_dM);
-    float* ds = dL_dscales + 3 * (size_t)idx;
+    real* ds = dL_dscales + 3 * (size_t)idx;
     for (int k = 0; k < 3; k++) {
         v3 a = v3_mk(Rt.m[k][0], Rt.m[k][1], Rt.m[k][2]);
         v3 b = v3_mk(dL_dMt.m[k][0], dL_dMt.m[k][1], dL_dMt.m[k][2]);
@@ -942,7 +966,7 @@ static void cov3d_backward(int idx, const float* scale, float mod, const float* 
         dL_dMt.m[2][w] *= s.z;
     }
 #define D(cc, rr) dL_dMt.m[cc][rr]
-    float* dq = dL_drots + 4 * (size_t)idx;
+    real* dq = dL_drots + 4 * (size_t)idx;
     dq[0] = 2 * z * (D(0, 1) - D(1, 0)) + 2 * y * (D(2, 0) - D(0, 2)) + 2 * x * (D(1, 2) - D(2, 1));
     dq[1] = 2 * y * (D(1, 0) + D(0, 1)) + 2 * z * (D(2, 0) + D(0, 2)) + 2 * r * (D(1, 2) - D(2, 1)) -
             4 * x * (D(2, 2) + D(1, 1));
@@ -960,16 +984,17 @@ enum { ACC_COL = 0, ACC_DEP = 3, ACC_FEAT = 4, ACC_M2D = 7, ACC_CON = 10, ACC_OP
 typedef struct {
     oracle_state* st;
     const float *dc, *dd, *da, *df;
-    float* priv;                                        /* private blocks, or NULL */
-    float *dcolors, *ddepth, *dfeat, *dmeans2D, *dconic, *dopacity; /* shared targets */
+    real* priv;                                        /* private blocks, or NULL */
+    real *dcolors, *ddepth, *dfeat, *dmeans2D, *dconic, *dopacity; /* shared targets */
+    int mass; /* oracle_blend_rows(mass = 1): sums of the terms' absolute values instead */
 } blend_bwd_ctx;
 static void blend_bwd_rows(void* ctx, long lo, long hi, int chunk) {
     const blend_bwd_ctx* c = (const blend_bwd_ctx*)ctx;
     oracle_state* st = c->st;
     const size_t P = (size_t)st->P;
-    float *dL_dcolors, *ddepth, *dfeat, *dL_dmeans2D, *dconic, *dL_dopacity;
+    real *dL_dcolors, *ddepth, *dfeat, *dL_dmeans2D, *dconic, *dL_dopacity;
     if (c->priv) {
-        float* b = c->priv + (size_t)chunk * ACC_ROW * P;
+        real* b = c->priv + (size_t)chunk * ACC_ROW * P;
         dL_dcolors = b + ACC_COL * P; ddepth = b + ACC_DEP * P; dfeat = b + ACC_FEAT * P;
         dL_dmeans2D = b + ACC_M2D * P; dconic = b + ACC_CON * P; dL_dopacity = b + ACC_OP * P;
     } else {
@@ -979,65 +1004,99 @@ static void blend_bwd_rows(void* ctx, long lo, long hi, int chunk) {
     const int W = st->W, H = st->H;
     const size_t HW = (size_t)W * H;
     const unsigned gx = st->gx;
-    const float* color_ptr = st->colors_precomp ? st->colors_precomp : st->rgb;
+    const real* color_ptr = st->rgb; /* colors_precomp converted into rgb by oracle_forward */
     const int nch = st->include_feature ? NCH : 5;
-    const float ddelx_dx = (float)(0.5 * W);
-    const float ddely_dy = (float)(0.5 * H);
+    const real ddelx_dx = (real)(0.5 * W);
+    const real ddely_dy = (real)(0.5 * H);
     for (long py = lo; py < hi; py++)
         for (int px = 0; px < W; px++) {
             const unsigned tile = (unsigned)(py / BLOCK_Y) * gx + (unsigned)(px / BLOCK_X);
             const unsigned rs = st->ranges[2 * tile], re = st->ranges[2 * tile + 1];
             const size_t pix = (size_t)py * W + px;
-            const float pfx = (float)px, pfy = (float)py;
-            const float T_final = st->final_T[pix];
-            float T = T_final;
+            const real pfx = (real)px, pfy = (real)py;
+            const real T_final = st->final_T[pix];
+            real T = T_final;
             unsigned contributor = re - rs;
             const unsigned last_contributor = st->n_contrib[pix];
-            float accum_rec[NCH] = {0}, last_color[NCH] = {0}, dL_dpixel[NCH] = {0};
+            real accum_rec[NCH] = {0}, last_color[NCH] = {0}, dL_dpixel[NCH] = {0};
             for (int i = 0; i < 3; i++) dL_dpixel[i] = c->dc[i * HW + pix];
             dL_dpixel[3] = c->dd ? c->dd[pix] : 0.0f;
             dL_dpixel[4] = c->da ? c->da[pix] : 0.0f;
             for (int i = 0; i < 3; i++) dL_dpixel[5 + i] = c->df ? c->df[i * HW + pix] : 0.0f;
-            float last_alpha = 0;
+            real last_alpha = 0;
+            /* mass mode: the float32 chain length of T at each splat -- the forward's product over
+             * the pixel's contributors, then one division per splat replayed -- weights the terms
+             * (T, and with it every term, carries ~ one rounding per link of that chain) */
+            real chain = 0;
+            if (c->mass) {
+                unsigned pos = 0;
+                for (unsigned k = rs; k < re && pos < last_contributor; k++, pos++) {
+                    const unsigned g = st->point_list[k];
+                    const real dx = st->means2D[2 * g] - pfx, dy = st->means2D[2 * g + 1] - pfy;
+                    const real* co = st->conic_opacity + 4 * (size_t)g;
+                    const real power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
+                    if (power > 0.0f) continue;
+                    if (fminf_cuda(0.99f, co[3] * blend_exp(power)) < 1.0f / 255.0f) continue;
+                    chain += 1;
+                }
+            }
             for (unsigned k = re; k-- > rs;) {
                 contributor--;
                 if (contributor >= last_contributor) continue;
                 const unsigned g = st->point_list[k];
-                const float dx = st->means2D[2 * g] - pfx, dy = st->means2D[2 * g + 1] - pfy;
-                const float* co = st->conic_opacity + 4 * (size_t)g;
-                const float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
+                const real dx = st->means2D[2 * g] - pfx, dy = st->means2D[2 * g + 1] - pfy;
+                const real* co = st->conic_opacity + 4 * (size_t)g;
+                const real power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
                 if (power > 0.0f) continue;
-                const float G = splat_exp(power);
-                const float alpha = fminf_cuda(0.99f, co[3] * G);
+                const real G = blend_exp(power);
+                const real alpha = fminf_cuda(0.99f, co[3] * G);
                 if (alpha < 1.0f / 255.0f) continue;
                 T = T / (1.f - alpha);
-                const float dchannel_dcolor = alpha * T;
-                float dL_dalpha = 0.0f;
-                float v[NCH];
+                const real dchannel_dcolor = alpha * T;
+                real dL_dalpha = 0.0f;
+                real amass = 0.0f; /* mass mode: the absolute values of dL_dalpha's terms */
+                real v[NCH];
                 v[0] = color_ptr[3 * g]; v[1] = color_ptr[3 * g + 1]; v[2] = color_ptr[3 * g + 2];
                 v[3] = st->depths[g]; v[4] = 1.0f;
                 v[5] = st->feat[3 * g]; v[6] = st->feat[3 * g + 1]; v[7] = st->feat[3 * g + 2];
                 for (int ch = 0; ch < nch; ch++) {
-                    const float cv = v[ch];
+                    const real cv = v[ch];
                     accum_rec[ch] = last_alpha * last_color[ch] + (1.f - last_alpha) * accum_rec[ch];
                     last_color[ch] = cv;
-                    const float dL_dchannel = dL_dpixel[ch];
+                    const real dL_dchannel = dL_dpixel[ch];
                     dL_dalpha += (cv - accum_rec[ch]) * dL_dchannel;
-                    const float gv = dchannel_dcolor * dL_dchannel;
+                    if (c->mass) amass += (fabs(cv) + fabs(accum_rec[ch])) * fabs(dL_dchannel);
+                    const real gv = c->mass ? fabs(dchannel_dcolor * dL_dchannel) * (2 + chain)
+                                            : dchannel_dcolor * dL_dchannel;
                     if (ch < 3) dL_dcolors[3 * (size_t)g + ch] += gv;
                     else if (ch == 3) ddepth[g] += gv;
                     else if (ch >= 5) dfeat[3 * (size_t)g + ch - 5] += gv;
                 }
                 dL_dalpha *= T;
                 last_alpha = alpha;
-                float bg_dot_dpixel = 0;
+                real bg_dot_dpixel = 0;
                 for (int i = 0; i < 3; i++) bg_dot_dpixel += st->bg[i] * dL_dpixel[i];
                 dL_dalpha += (-T_final / (1.f - alpha)) * bg_dot_dpixel;
-                const float dL_dG = co[3] * dL_dalpha;
-                const float gdx = G * dx;
-                const float gdy = G * dy;
-                const float dG_ddelx = -gdx * co[0] - gdy * co[1];
-                const float dG_ddely = -gdy * co[2] - gdx * co[1];
+                if (c->mass) {
+                    chain += 1;
+                    real bgm = 0;
+                    for (int i = 0; i < 3; i++) bgm += fabs(st->bg[i] * dL_dpixel[i]);
+                    const real am = (amass * T + T_final / (1.f - alpha) * bgm) * (1 + chain);
+                    const real gm = co[3] * am;
+                    const real ax = fabs(G * dx), ay = fabs(G * dy);
+                    dL_dmeans2D[3 * (size_t)g + 0] += gm * (ax * fabs(co[0]) + ay * fabs(co[1])) * ddelx_dx;
+                    dL_dmeans2D[3 * (size_t)g + 1] += gm * (ay * fabs(co[2]) + ax * fabs(co[1])) * ddely_dy;
+                    dconic[4 * (size_t)g + 0] += 0.5f * ax * fabs(dx) * gm;
+                    dconic[4 * (size_t)g + 1] += 0.5f * ax * fabs(dy) * gm;
+                    dconic[4 * (size_t)g + 3] += 0.5f * ay * fabs(dy) * gm;
+                    dL_dopacity[g] += G * am;
+                    continue;
+                }
+                const real dL_dG = co[3] * dL_dalpha;
+                const real gdx = G * dx;
+                const real gdy = G * dy;
+                const real dG_ddelx = -gdx * co[0] - gdy * co[1];
+                const real dG_ddely = -gdy * co[2] - gdx * co[1];
                 dL_dmeans2D[3 * (size_t)g + 0] += dL_dG * dG_ddelx * ddelx_dx;
                 dL_dmeans2D[3 * (size_t)g + 1] += dL_dG * dG_ddely * ddely_dy;
                 dconic[4 * (size_t)g + 0] += -0.5f * gdx * dx * dL_dG;
@@ -1048,12 +1107,12 @@ static void blend_bwd_rows(void* ctx, long lo, long hi, int chunk) {
         }
 }
 /* target[i] = sum over chunks (in chunk order) of private slot `slot0`+.. element i */
-typedef struct { const float* priv; int nchunks; size_t P; size_t slot; float* dst; } reduce_ctx;
+typedef struct { const real* priv; int nchunks; size_t P; size_t slot; real* dst; } reduce_ctx;
 static void reduce_range(void* ctx, long lo, long hi, int chunk) {
     (void)chunk;
     const reduce_ctx* r = (const reduce_ctx*)ctx;
     for (long i = lo; i < hi; i++) {
-        float s = 0.0f;
+        real s = 0.0f;
         for (int c = 0; c < r->nchunks; c++) s += r->priv[(size_t)c * ACC_ROW * r->P + r->slot * r->P + i];
         r->dst[i] = s;
     }
@@ -1062,8 +1121,8 @@ static void reduce_range(void* ctx, long lo, long hi, int chunk) {
 /* ---- BACKWARD::preprocess, backward.cu:559-622, per Gaussian ---- */
 typedef struct {
     oracle_state* st;
-    const float* cov3D_ptr;
-    float *dL_dmeans2D, *dL_dcolors, *dL_dopacity, *dL_dmeans3D, *dL_dcov3D, *dL_dsh, *dL_dscales,
+    const real* cov3D_ptr;
+    real *dL_dmeans2D, *dL_dcolors, *dL_dopacity, *dL_dmeans3D, *dL_dcov3D, *dL_dsh, *dL_dscales,
         *dL_drotations, *dL_dsh_language, *dL_dlanguage_feature, *dconic, *ddepth, *dfeat;
 } pre_bwd_ctx;
 static void cov2d_bwd_range(void* ctx, long lo, long hi, int chunk) {
@@ -1081,18 +1140,18 @@ static void pre_bwd_range(void* ctx, long lo, long hi, int chunk) {
     (void)chunk;
     const pre_bwd_ctx* c = (const pre_bwd_ctx*)ctx;
     oracle_state* st = c->st;
-    const float* proj = st->proj;
+    const real* proj = st->proj;
     for (long i = lo; i < hi; i++) {
         const int idx = (int)i;
         if (!(st->radii[idx] > 0)) continue;
         /* backward.cu:370-387 */
         v3 m = v3_mk(st->means3D[3 * idx], st->means3D[3 * idx + 1], st->means3D[3 * idx + 2]);
-        float m_hom[4];
+        real m_hom[4];
         transformPoint4x4(m, proj, m_hom);
-        float m_w = 1.0f / (m_hom[3] + 0.0000001f);
-        float mul1 = (proj[0] * m.x + proj[4] * m.y + proj[8] * m.z + proj[12]) * m_w * m_w;
-        float mul2 = (proj[1] * m.x + proj[5] * m.y + proj[9] * m.z + proj[13]) * m_w * m_w;
-        const float gx2 = c->dL_dmeans2D[3 * idx], gy2 = c->dL_dmeans2D[3 * idx + 1];
+        real m_w = 1.0f / (m_hom[3] + 0.0000001f);
+        real mul1 = (proj[0] * m.x + proj[4] * m.y + proj[8] * m.z + proj[12]) * m_w * m_w;
+        real mul2 = (proj[1] * m.x + proj[5] * m.y + proj[9] * m.z + proj[13]) * m_w * m_w;
+        const real gx2 = c->dL_dmeans2D[3 * idx], gy2 = c->dL_dmeans2D[3 * idx + 1];
         v3 dm;
         dm.x = (proj[0] * m_w - proj[3] * mul1) * gx2 + (proj[1] * m_w - proj[3] * mul2) * gy2;
         dm.y = (proj[4] * m_w - proj[7] * mul1) * gx2 + (proj[5] * m_w - proj[7] * mul2) * gy2;
@@ -1108,25 +1167,25 @@ static void pre_bwd_range(void* ctx, long lo, long hi, int chunk) {
                            st->rotations + 4 * (size_t)idx, c->dL_dcov3D, c->dL_dscales,
                            c->dL_drotations);
         /* depth channel -> view-space z = view[2]x + view[6]y + view[10]z + view[14] */
-        const float dz = c->ddepth[idx];
+        const real dz = c->ddepth[idx];
         c->dL_dmeans3D[3 * idx + 0] += dz * st->view[2];
         c->dL_dmeans3D[3 * idx + 1] += dz * st->view[6];
         c->dL_dmeans3D[3 * idx + 2] += dz * st->view[10];
         /* confidence is an opacity multiplier */
         if (st->confidence) c->dL_dopacity[idx] = c->dL_dopacity[idx] * st->confidence[idx];
         if (st->include_feature) {
-            const float* gf = c->dfeat + 3 * (size_t)idx;
+            const real* gf = c->dfeat + 3 * (size_t)idx;
             if (st->lang_precomp) {
                 if (c->dL_dlanguage_feature)
                     for (int k = 0; k < 3; k++) c->dL_dlanguage_feature[3 * idx + k] = gf[k];
             } else if (st->sh_language && c->dL_dsh_language) {
                 /* f = u / (|u| + 1e-9), u = SH_C0 * l */
                 const float* l = st->sh_language + 3 * (size_t)idx;
-                float u0 = SH_C0 * l[0], u1 = SH_C0 * l[1], u2v = SH_C0 * l[2];
-                float n = sqrtf(u0 * u0 + u1 * u1 + u2v * u2v);
-                float den = n + 1e-9f;
-                float ug = u0 * gf[0] + u1 * gf[1] + u2v * gf[2];
-                float k2 = n > 0.0f ? ug / (den * den * n) : 0.0f;
+                real u0 = SH_C0 * l[0], u1 = SH_C0 * l[1], u2v = SH_C0 * l[2];
+                real n = sqrt(u0 * u0 + u1 * u1 + u2v * u2v);
+                real den = n + 1e-9f;
+                real ug = u0 * gf[0] + u1 * gf[1] + u2v * gf[2];
+                real k2 = n > 0.0f ? ug / (den * den * n) : 0.0f;
                 c->dL_dsh_language[3 * idx + 0] = SH_C0 * (gf[0] / den - u0 * k2);
                 c->dL_dsh_language[3 * idx + 1] = SH_C0 * (gf[1] / den - u1 * k2);
                 c->dL_dsh_language[3 * idx + 2] = SH_C0 * (gf[2] / den - u2v * k2);
@@ -1135,57 +1194,94 @@ static void pre_bwd_range(void* ctx, long lo, long hi, int chunk) {
     }
 }
 
-int oracle_backward(oracle_state* st, const float* dL_dout_color, const float* dL_dout_depth,
-                    const float* dL_dout_alpha, const float* dL_dout_feature, float* dL_dmeans2D,
-                    float* dL_dcolors, float* dL_dopacity, float* dL_dmeans3D, float* dL_dcov3D,
-                    float* dL_dsh, float* dL_dscales, float* dL_drotations,
-                    float* dL_dsh_language, float* dL_dlanguage_feature) {
-    if (!st) return 1;
-    const int P = st->P, M = st->M, H = st->H;
-    /* rasterize_points.cu:151-159 zero-initialised grads */
-    memset(dL_dmeans2D, 0, sizeof(float) * 3 * (size_t)P);
-    memset(dL_dcolors, 0, sizeof(float) * 3 * (size_t)P);
-    memset(dL_dopacity, 0, sizeof(float) * (size_t)P);
-    memset(dL_dmeans3D, 0, sizeof(float) * 3 * (size_t)P);
-    memset(dL_dcov3D, 0, sizeof(float) * 6 * (size_t)P);
-    if (dL_dsh) memset(dL_dsh, 0, sizeof(float) * 3 * (size_t)P * M);
-    if (dL_dscales) memset(dL_dscales, 0, sizeof(float) * 3 * (size_t)P);
-    if (dL_drotations) memset(dL_drotations, 0, sizeof(float) * 4 * (size_t)P);
-    if (dL_dsh_language) memset(dL_dsh_language, 0, sizeof(float) * 3 * (size_t)P);
-    if (dL_dlanguage_feature) memset(dL_dlanguage_feature, 0, sizeof(float) * 3 * (size_t)P);
-    float* dconic = (float*)xcalloc((size_t)P * 4, sizeof(float));
-    float* ddepth = (float*)xcalloc((size_t)P, sizeof(float));
-    float* dfeat = (float*)xcalloc((size_t)P * 3, sizeof(float));
-
-    /* ---- renderCUDA (bwd), backward.cu:399-557 ---- */
+/* The blend backward's per-Gaussian sums (renderCUDA bwd) into `rows`, the ACC block
+ * [colors 3P | depth P | feat 3P | means2D 3P | conic 4P | opacity P] (zeroed here); mass: the sums
+ * of the terms' absolute values (oracle_blend_rows). */
+static void blend_backward(oracle_state* st, const float* dL_dout_color, const float* dL_dout_depth,
+                           const float* dL_dout_alpha, const float* dL_dout_feature, int mass,
+                           real* rows) {
+    const size_t P = (size_t)st->P;
+    const int H = st->H;
+    memset(rows, 0, sizeof(real) * ACC_ROW * P);
     blend_bwd_ctx bc = {st, dL_dout_color, dL_dout_depth, dL_dout_alpha, dL_dout_feature, NULL,
-                        dL_dcolors, ddepth, dfeat, dL_dmeans2D, dconic, dL_dopacity};
+                        rows + ACC_COL * P, rows + ACC_DEP * P, rows + ACC_FEAT * P,
+                        rows + ACC_M2D * P, rows + ACC_CON * P, rows + ACC_OP * P, mass};
     const int nchunks = par_chunks(H);
-    if (nchunks > 1) bc.priv = (float*)calloc((size_t)nchunks * ACC_ROW * (size_t)P, sizeof(float));
+    if (nchunks > 1) bc.priv = (real*)calloc((size_t)nchunks * ACC_ROW * P, sizeof(real));
     if (bc.priv) par_for(H, blend_bwd_rows, &bc);
-    else blend_bwd_rows(&bc, 0, H, 0); /* one chunk straight into the outputs */
+    else blend_bwd_rows(&bc, 0, H, 0); /* one chunk straight into the rows */
     if (bc.priv) {
-        float* dst[6] = {dL_dcolors, ddepth, dfeat, dL_dmeans2D, dconic, dL_dopacity};
-        const size_t slot[6] = {ACC_COL, ACC_DEP, ACC_FEAT, ACC_M2D, ACC_CON, ACC_OP};
-        const size_t len[6] = {3, 1, 3, 3, 4, 1};
-        for (int a = 0; a < 6; a++)
-            for (size_t s = 0; s < len[a]; s++) {
-                reduce_ctx rc = {bc.priv, nchunks, (size_t)P, slot[a] + s, dst[a] + s * (size_t)P};
-                par_for(P, reduce_range, &rc);
-            }
+        for (size_t s = 0; s < ACC_ROW; s++) {
+            reduce_ctx rc = {bc.priv, nchunks, P, s, rows + s * P};
+            par_for((long)P, reduce_range, &rc);
+        }
         free(bc.priv);
     }
+}
 
-    /* ---- BACKWARD::preprocess, backward.cu:559-622 ---- */
-    pre_bwd_ctx pc = {st, st->cov3D_precomp ? st->cov3D_precomp : st->cov3D, dL_dmeans2D,
+/* BACKWARD::preprocess (backward.cu:559-622) from the blend's rows (ACC block, read-only). */
+static void backward_from_rows(oracle_state* st, const real* rows, real* dL_dmeans2D,
+                               real* dL_dcolors, real* dL_dopacity, real* dL_dmeans3D,
+                               real* dL_dcov3D, real* dL_dsh, real* dL_dscales,
+                               real* dL_drotations, real* dL_dsh_language,
+                               real* dL_dlanguage_feature) {
+    const size_t P = (size_t)st->P, M = (size_t)st->M;
+    /* rasterize_points.cu:151-159 zero-initialised grads */
+    memset(dL_dmeans3D, 0, sizeof(real) * 3 * P);
+    memset(dL_dcov3D, 0, sizeof(real) * 6 * P);
+    if (dL_dsh) memset(dL_dsh, 0, sizeof(real) * 3 * P * M);
+    if (dL_dscales) memset(dL_dscales, 0, sizeof(real) * 3 * P);
+    if (dL_drotations) memset(dL_drotations, 0, sizeof(real) * 4 * P);
+    if (dL_dsh_language) memset(dL_dsh_language, 0, sizeof(real) * 3 * P);
+    if (dL_dlanguage_feature) memset(dL_dlanguage_feature, 0, sizeof(real) * 3 * P);
+    memcpy(dL_dmeans2D, rows + ACC_M2D * P, sizeof(real) * 3 * P);
+    memcpy(dL_dcolors, rows + ACC_COL * P, sizeof(real) * 3 * P);
+    memcpy(dL_dopacity, rows + ACC_OP * P, sizeof(real) * P);
+    real* priv = (real*)xcalloc(8 * P, sizeof(real)); /* conic 4P | depth P | feat 3P */
+    memcpy(priv, rows + ACC_CON * P, sizeof(real) * 4 * P);
+    memcpy(priv + 4 * P, rows + ACC_DEP * P, sizeof(real) * P);
+    memcpy(priv + 5 * P, rows + ACC_FEAT * P, sizeof(real) * 3 * P);
+    pre_bwd_ctx pc = {st, st->cov3D, dL_dmeans2D,
                       dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales,
-                      dL_drotations, dL_dsh_language, dL_dlanguage_feature, dconic, ddepth, dfeat};
-    par_for(P, cov2d_bwd_range, &pc);
-    par_for(P, pre_bwd_range, &pc);
+                      dL_drotations, dL_dsh_language, dL_dlanguage_feature, priv, priv + 4 * P,
+                      priv + 5 * P};
+    par_for((long)P, cov2d_bwd_range, &pc);
+    par_for((long)P, pre_bwd_range, &pc);
     /* invisible Gaussians: the grads of the colour channels etc. are already zero. */
-    free(dconic);
-    free(ddepth);
-    free(dfeat);
+    free(priv);
+}
+
+int oracle_backward(oracle_state* st, const float* dL_dout_color, const float* dL_dout_depth,
+                    const float* dL_dout_alpha, const float* dL_dout_feature, real* dL_dmeans2D,
+                    real* dL_dcolors, real* dL_dopacity, real* dL_dmeans3D, real* dL_dcov3D,
+                    real* dL_dsh, real* dL_dscales, real* dL_drotations,
+                    real* dL_dsh_language, real* dL_dlanguage_feature) {
+    if (!st) return 1;
+    real* rows = (real*)xcalloc((size_t)ACC_ROW * st->P, sizeof(real));
+    /* ---- renderCUDA (bwd), backward.cu:399-557 ---- */
+    blend_backward(st, dL_dout_color, dL_dout_depth, dL_dout_alpha, dL_dout_feature, 0, rows);
+    /* ---- BACKWARD::preprocess, backward.cu:559-622 ---- */
+    backward_from_rows(st, rows, dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D,
+                       dL_dsh, dL_dscales, dL_drotations, dL_dsh_language, dL_dlanguage_feature);
+    free(rows);
+    return 0;
+}
+
+int oracle_blend_rows(oracle_state* st, const float* dL_dout_color, const float* dL_dout_depth,
+                      const float* dL_dout_alpha, const float* dL_dout_feature, int mass,
+                      real* rows) {
+    if (!st || !rows) return 1;
+    blend_backward(st, dL_dout_color, dL_dout_depth, dL_dout_alpha, dL_dout_feature, mass, rows);
+    return 0;
+}
+
+int oracle_backward_rows(oracle_state* st, const real* rows, real* dL_dmeans2D, real* dL_dcolors,
+                         real* dL_dopacity, real* dL_dmeans3D, real* dL_dcov3D, real* dL_dsh,
+                         real* dL_dscales, real* dL_drotations, real* dL_dsh_language,
+                         real* dL_dlanguage_feature) {
+    if (!st || !rows) return 1;
+    backward_from_rows(st, rows, dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D,
+                       dL_dsh, dL_dscales, dL_drotations, dL_dsh_language, dL_dlanguage_feature);
     return 0;
 }
 
@@ -1208,8 +1304,10 @@ int oracle_cut_lists(const oracle_state* st, unsigned* point_list_out, unsigned*
         const unsigned start = n;
         for (unsigned k = rs; k < re; k++) {
             const unsigned g = st->point_list[k];
-            const float* co = st->conic_opacity + 4 * (size_t)g;
-            const float mx = st->means2D[2 * (size_t)g], my = st->means2D[2 * (size_t)g + 1];
+            /* the cut is float-defined (gsr_device.h): float values of the record */
+            const real* cr = st->conic_opacity + 4 * (size_t)g;
+            const float co[4] = {(float)cr[0], (float)cr[1], (float)cr[2], (float)cr[3]};
+            const float mx = (float)st->means2D[2 * (size_t)g], my = (float)st->means2D[2 * (size_t)g + 1];
             u2 rmin, rmax;
             getRect(mx, my, st->radii[g], &rmin, &rmax, st->gx, st->gy);
             const splat_cut c = make_cut(mx, my, co[0], co[1], co[2], cut_q(co[0], co[1], co[2], co[3]));
@@ -1225,12 +1323,15 @@ int oracle_cut_lists(const oracle_state* st, unsigned* point_list_out, unsigned*
 
 int oracle_get_point_list(const oracle_state* st, unsigned* out) { memcpy(out, st->point_list, sizeof(unsigned) * (size_t)st->R); return st->R; }
 int oracle_get_ranges(const oracle_state* st, unsigned* out) { memcpy(out, st->ranges, sizeof(unsigned) * 2 * (size_t)st->gx * st->gy); return 0; }
-int oracle_get_final_T(const oracle_state* st, float* out) { memcpy(out, st->final_T, sizeof(float) * (size_t)st->W * st->H); return 0; }
+static void to_float(float* out, const real* in, size_t n) {
+    for (size_t i = 0; i < n; i++) out[i] = (float)in[i];
+}
+int oracle_get_final_T(const oracle_state* st, float* out) { to_float(out, st->final_T, (size_t)st->W * st->H); return 0; }
 int oracle_get_n_contrib(const oracle_state* st, unsigned* out) { memcpy(out, st->n_contrib, sizeof(unsigned) * (size_t)st->W * st->H); return 0; }
-int oracle_get_margin(const oracle_state* st, float* out) { memcpy(out, st->margin, sizeof(float) * (size_t)st->W * st->H); return 0; }
-int oracle_get_means2D(const oracle_state* st, float* out) { memcpy(out, st->means2D, sizeof(float) * 2 * (size_t)st->P); return 0; }
-int oracle_get_conic_opacity(const oracle_state* st, float* out) { memcpy(out, st->conic_opacity, sizeof(float) * 4 * (size_t)st->P); return 0; }
-int oracle_get_depths(const oracle_state* st, float* out) { memcpy(out, st->depths, sizeof(float) * (size_t)st->P); return 0; }
-int oracle_get_rgb(const oracle_state* st, float* out) { memcpy(out, st->rgb, sizeof(float) * 3 * (size_t)st->P); return 0; }
+int oracle_get_margin(const oracle_state* st, float* out) { to_float(out, st->margin, (size_t)st->W * st->H); return 0; }
+int oracle_get_means2D(const oracle_state* st, float* out) { to_float(out, st->means2D, 2 * (size_t)st->P); return 0; }
+int oracle_get_conic_opacity(const oracle_state* st, float* out) { to_float(out, st->conic_opacity, 4 * (size_t)st->P); return 0; }
+int oracle_get_depths(const oracle_state* st, float* out) { to_float(out, st->depths, (size_t)st->P); return 0; }
+int oracle_get_rgb(const oracle_state* st, float* out) { to_float(out, st->rgb, 3 * (size_t)st->P); return 0; }
 int oracle_get_tiles_touched(const oracle_state* st, unsigned* out) { memcpy(out, st->tiles_touched, sizeof(unsigned) * (size_t)st->P); return 0; }
-int oracle_get_cov3D(const oracle_state* st, float* out) { memcpy(out, st->cov3D, sizeof(float) * 6 * (size_t)st->P); return 0; }
+int oracle_get_cov3D(const oracle_state* st, float* out) { to_float(out, st->cov3D, 6 * (size_t)st->P); return 0; }

@@ -32,6 +32,14 @@
 
 #include <stdint.h>
 
+/* The restatement's arithmetic type: float (the checker) or double (-DORACLE_REAL=double, the
+ * float64 build used to show that the float32 results differ only by rounding).  Output images
+ * and gradients are written in this type; inputs are the reference's float32 tensors. */
+#ifndef ORACLE_REAL
+#define ORACLE_REAL float
+#endif
+typedef ORACLE_REAL oreal;
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -68,10 +76,10 @@ oracle_state* oracle_forward(
     const float* language_feature_precomp,   /* [P,3] or NULL */
     const float* confidence,                 /* [P] or NULL (== all ones) */
     int include_feature,
-    float* out_color,                        /* [3,H,W] */
-    float* out_depth,                        /* [1,H,W] */
-    float* out_alpha,                        /* [1,H,W] */
-    float* out_feature,                      /* [3,H,W] */
+    oreal* out_color,                        /* [3,H,W] */
+    oreal* out_depth,                        /* [1,H,W] */
+    oreal* out_alpha,                        /* [1,H,W] */
+    oreal* out_feature,                      /* [3,H,W] */
     int* radii,                              /* [P] */
     int* num_rendered);
 
@@ -83,16 +91,34 @@ int oracle_backward(
     const float* dL_dout_depth,              /* [1,H,W] or NULL */
     const float* dL_dout_alpha,              /* [1,H,W] or NULL */
     const float* dL_dout_feature,            /* [3,H,W] or NULL */
-    float* dL_dmeans2D,                      /* [P,3] */
-    float* dL_dcolors,                       /* [P,3] */
-    float* dL_dopacity,                      /* [P] */
-    float* dL_dmeans3D,                      /* [P,3] */
-    float* dL_dcov3D,                        /* [P,6] */
-    float* dL_dsh,                           /* [P,M,3] or NULL */
-    float* dL_dscales,                       /* [P,3] or NULL */
-    float* dL_drotations,                    /* [P,4] or NULL */
-    float* dL_dsh_language,                  /* [P,3] or NULL */
-    float* dL_dlanguage_feature);            /* [P,3] or NULL */
+    oreal* dL_dmeans2D,                      /* [P,3] */
+    oreal* dL_dcolors,                       /* [P,3] */
+    oreal* dL_dopacity,                      /* [P] */
+    oreal* dL_dmeans3D,                      /* [P,3] */
+    oreal* dL_dcov3D,                        /* [P,6] */
+    oreal* dL_dsh,                           /* [P,M,3] or NULL */
+    oreal* dL_dscales,                       /* [P,3] or NULL */
+    oreal* dL_drotations,                    /* [P,4] or NULL */
+    oreal* dL_dsh_language,                  /* [P,3] or NULL */
+    oreal* dL_dlanguage_feature);            /* [P,3] or NULL */
+
+/* The backward in two parts, for the float64 rounding analysis (tests/test_f64_parity.py).
+ * rows: [15*P] in the oracle's accumulator layout -- colours [P,3] | depth [P] | feature [P,3] |
+ * means2D [P,3] | conic [P,4] (a, b, -, c) | opacity [P].
+ * oracle_blend_rows: the blend backward's per-Gaussian sums (renderCUDA bwd); with mass != 0 each
+ * entry is instead the sum of the ABSOLUTE values of its per-pixel terms (dL/dalpha replaced by
+ * the sum of its channel terms' absolute values): the scale of the rounding error any float32
+ * evaluation of the sum can make.
+ * oracle_backward_rows: the per-Gaussian backward (preprocess bwd) from given rows; linear in the
+ * rows, so unit rows give its Jacobian.  Outputs as oracle_backward. */
+int oracle_blend_rows(oracle_state* st, const float* dL_dout_color, const float* dL_dout_depth,
+                      const float* dL_dout_alpha, const float* dL_dout_feature, int mass,
+                      oreal* rows);
+int oracle_backward_rows(oracle_state* st, const oreal* rows, oreal* dL_dmeans2D,
+                         oreal* dL_dcolors, oreal* dL_dopacity, oreal* dL_dmeans3D,
+                         oreal* dL_dcov3D, oreal* dL_dsh, oreal* dL_dscales,
+                         oreal* dL_drotations, oreal* dL_dsh_language,
+                         oreal* dL_dlanguage_feature);
 
 void oracle_free(oracle_state* st);
 

@@ -16,8 +16,12 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "_build", "libgsr_oracle.so")
-_lib = None
+# variants of the same source (oracle/Makefile): "f32" the checker, "f64" the float64 build,
+# "expf" float32 with libm's expf as the blend exp (threshold census)
+_LIB_FILES = {"f32": "libgsr_oracle.so", "f64": "libgsr_oracle_f64.so",
+              "expf": "libgsr_oracle_expf.so"}
+_LIB_PATH = os.path.join(_HERE, "_build", _LIB_FILES["f32"])
+_libs = {}
 
 _f = ctypes.c_float
 _i = ctypes.c_int
@@ -30,18 +34,23 @@ def build() -> str:
     return _LIB_PATH
 
 
-def lib():
-    global _lib
-    if _lib is None:
-        if not os.path.exists(_LIB_PATH):
+def lib(variant: str = "f32"):
+    L = _libs.get(variant)
+    if L is None:
+        path = os.path.join(_HERE, "_build", _LIB_FILES[variant])
+        if not os.path.exists(path):
             build()
-        L = ctypes.CDLL(_LIB_PATH)
+        L = ctypes.CDLL(path)
         L.oracle_forward.restype = _p
         L.oracle_forward.argtypes = [
             _i, _i, _p, _p, _p, _p, _p, _p, _f, _p, _p, _p, _f, _f, _i, _i, _p, _i, _p, _i,
             _p, _p, _p, _i, _p, _p, _p, _p, _p, ctypes.POINTER(_i)]
         L.oracle_backward.restype = _i
         L.oracle_backward.argtypes = [_p] + [_p] * 14
+        L.oracle_blend_rows.restype = _i
+        L.oracle_blend_rows.argtypes = [_p, _p, _p, _p, _p, _i, _p]
+        L.oracle_backward_rows.restype = _i
+        L.oracle_backward_rows.argtypes = [_p] * 12
         L.oracle_free.restype = None
         L.oracle_free.argtypes = [_p]
         L.oracle_mark_visible.restype = _i
@@ -63,13 +72,15 @@ def lib():
             fn = getattr(L, "oracle_get_" + name)
             fn.restype = _i
             fn.argtypes = [_p, _p]
-        _lib = L
-    return _lib
+        _libs[variant] = L
+    return L
 
 
 def set_threads(n: int) -> int:
-    """Host threads of the oracle's loops (1 = the sequential restatement); returns the value set."""
-    lib().oracle_set_threads(int(n))
+    """Host threads of the oracle's loops (1 = the sequential restatement); returns the value set
+    (every variant)."""
+    for v in _LIB_FILES:
+        lib(v).oracle_set_threads(int(n))
     return int(lib().oracle_get_threads())
 
 
@@ -85,14 +96,20 @@ def _ptr(a):
 
 
 class OracleRaster:
-    """One forward (+ optional backward) of the restated rasterizer on host arrays."""
+    """One forward (+ optional backward) of the restated rasterizer on host arrays.  variant:
+    "f32" (the checker), "f64" (the same restatement in float64: images and gradients come back
+    as float64) or "expf" (float32 with libm's expf as the blend exp)."""
 
-    def __init__(self, *, means3D, opacities, viewmatrix, projmatrix, campos, tanfovx, tanfovy,
+    def __init__(self, *, variant="f32", means3D, opacities, viewmatrix, projmatrix, campos, tanfovx, tanfovy,
                  image_height, image_width, bg, scale_modifier=1.0, sh_degree=0, shs=None,
                  colors_precomp=None, scales=None, rotations=None, cov3D_precomp=None,
                  shs_language=None, language_feature_precomp=None, confidence=None,
                  include_feature=True, prefiltered=False):
-        L = lib()
+        L = lib(variant)
+        self.variant = variant
+        self._L = L
+        od = np.float64 if variant == "f64" else np.float32
+        self._od = od
         self._keep = {}
         k = self._keep
         k["means3D"] = _arr(means3D).reshape(-1, 3)
@@ -113,10 +130,10 @@ class OracleRaster:
         k["conf"] = None if confidence is None else _arr(confidence).reshape(P)
         H, W = int(image_height), int(image_width)
         self.P, self.M, self.H, self.W = P, M, H, W
-        self.color = np.zeros((3, H, W), np.float32)
-        self.depth = np.zeros((1, H, W), np.float32)
-        self.alpha = np.zeros((1, H, W), np.float32)
-        self.feature = np.zeros((3, H, W), np.float32)
+        self.color = np.zeros((3, H, W), od)
+        self.depth = np.zeros((1, H, W), od)
+        self.alpha = np.zeros((1, H, W), od)
+        self.feature = np.zeros((3, H, W), od)
         self.radii = np.zeros((P,), np.int32)
         nr = _i(0)
         self._st = L.oracle_forward(
@@ -136,13 +153,13 @@ class OracleRaster:
     def __del__(self):
         st = getattr(self, "_st", None)
         if st:
-            lib().oracle_free(st)
+            self._L.oracle_free(st)
             self._st = None
 
     # ---- state introspection -------------------------------------------------------------
     def _get(self, name, shape, dtype):
         out = np.zeros(shape, dtype)
-        getattr(lib(), "oracle_get_" + name)(self._st, _ptr(out))
+        getattr(self._L, "oracle_get_" + name)(self._st, _ptr(out))
         return out
 
     def point_list(self):
@@ -157,7 +174,7 @@ class OracleRaster:
         the reference's order."""
         pl = np.zeros((max(self.num_rendered, 1),), np.uint32)
         rg = np.zeros((self.gx * self.gy, 2), np.uint32)
-        n = lib().oracle_cut_lists(self._st, _ptr(pl), _ptr(rg))
+        n = self._L.oracle_cut_lists(self._st, _ptr(pl), _ptr(rg))
         return pl[:n].copy(), rg
 
     def final_T(self):
@@ -195,30 +212,72 @@ class OracleRaster:
     def backward(self, dL_dcolor, dL_ddepth=None, dL_dalpha=None, dL_dfeature=None):
         k = self._keep
         P, M = self.P, self.M
+        od = self._od
         dc = _arr(dL_dcolor).reshape(3, self.H, self.W)
         dd = None if dL_ddepth is None else _arr(dL_ddepth).reshape(1, self.H, self.W)
         da = None if dL_dalpha is None else _arr(dL_dalpha).reshape(1, self.H, self.W)
         df = None if dL_dfeature is None else _arr(dL_dfeature).reshape(3, self.H, self.W)
         g = {
-            "means2D": np.zeros((P, 3), np.float32),
-            "colors": np.zeros((P, 3), np.float32),
-            "opacity": np.zeros((P, 1), np.float32),
-            "means3D": np.zeros((P, 3), np.float32),
-            "cov3D": np.zeros((P, 6), np.float32),
-            "sh": np.zeros((P, M, 3), np.float32) if k["shs"] is not None else None,
-            "scales": np.zeros((P, 3), np.float32) if k["scales"] is not None else None,
-            "rotations": np.zeros((P, 4), np.float32) if k["rot"] is not None else None,
-            "sh_language": np.zeros((P, 3), np.float32) if k["shl"] is not None else None,
-            "language_feature": np.zeros((P, 3), np.float32) if k["lfp"] is not None else None,
+            "means2D": np.zeros((P, 3), od),
+            "colors": np.zeros((P, 3), od),
+            "opacity": np.zeros((P, 1), od),
+            "means3D": np.zeros((P, 3), od),
+            "cov3D": np.zeros((P, 6), od),
+            "sh": np.zeros((P, M, 3), od) if k["shs"] is not None else None,
+            "scales": np.zeros((P, 3), od) if k["scales"] is not None else None,
+            "rotations": np.zeros((P, 4), od) if k["rot"] is not None else None,
+            "sh_language": np.zeros((P, 3), od) if k["shl"] is not None else None,
+            "language_feature": np.zeros((P, 3), od) if k["lfp"] is not None else None,
         }
         self._keep_bwd = (dc, dd, da, df)
-        rc = lib().oracle_backward(
+        rc = self._L.oracle_backward(
             self._st, _ptr(dc), _ptr(dd), _ptr(da), _ptr(df), _ptr(g["means2D"]), _ptr(g["colors"]),
             _ptr(g["opacity"]), _ptr(g["means3D"]), _ptr(g["cov3D"]), _ptr(g["sh"]),
             _ptr(g["scales"]), _ptr(g["rotations"]), _ptr(g["sh_language"]),
             _ptr(g["language_feature"]))
         if rc != 0:
             raise RuntimeError("oracle_backward failed")
+        return g
+
+
+    # ---- the backward in two parts (float64 rounding analysis, tests/f64_ref.py) ---------------
+    ROW_SLOTS = 15  # colours 3 | depth 1 | feature 3 | means2D 3 | conic 4 | opacity 1 (per P)
+
+    def blend_rows(self, dL_dcolor, dL_ddepth=None, dL_dalpha=None, dL_dfeature=None, mass=False):
+        """The blend backward's per-Gaussian sums as the oracle's [15 * P] accumulator block
+        (gsr_oracle.h oracle_blend_rows); mass: sums of the terms' absolute values."""
+        dc = _arr(dL_dcolor).reshape(3, self.H, self.W)
+        dd = None if dL_ddepth is None else _arr(dL_ddepth).reshape(1, self.H, self.W)
+        da = None if dL_dalpha is None else _arr(dL_dalpha).reshape(1, self.H, self.W)
+        df = None if dL_dfeature is None else _arr(dL_dfeature).reshape(3, self.H, self.W)
+        rows = np.zeros(self.ROW_SLOTS * self.P, self._od)
+        if self._L.oracle_blend_rows(self._st, _ptr(dc), _ptr(dd), _ptr(da), _ptr(df),
+                                     int(bool(mass)), _ptr(rows)) != 0:
+            raise RuntimeError("oracle_blend_rows failed")
+        return rows
+
+    def backward_rows(self, rows):
+        """The per-Gaussian backward from an accumulator block (linear in it); the gradient dict
+        of backward()."""
+        k = self._keep
+        P, M, od = self.P, self.M, self._od
+        rows = np.ascontiguousarray(rows, od).reshape(-1)
+        assert rows.size == self.ROW_SLOTS * P
+        g = {
+            "means2D": np.zeros((P, 3), od), "colors": np.zeros((P, 3), od),
+            "opacity": np.zeros((P, 1), od), "means3D": np.zeros((P, 3), od),
+            "cov3D": np.zeros((P, 6), od),
+            "sh": np.zeros((P, M, 3), od) if k["shs"] is not None else None,
+            "scales": np.zeros((P, 3), od) if k["scales"] is not None else None,
+            "rotations": np.zeros((P, 4), od) if k["rot"] is not None else None,
+            "sh_language": np.zeros((P, 3), od) if k["shl"] is not None else None,
+            "language_feature": np.zeros((P, 3), od) if k["lfp"] is not None else None,
+        }
+        if self._L.oracle_backward_rows(
+                self._st, _ptr(rows), _ptr(g["means2D"]), _ptr(g["colors"]), _ptr(g["opacity"]),
+                _ptr(g["means3D"]), _ptr(g["cov3D"]), _ptr(g["sh"]), _ptr(g["scales"]),
+                _ptr(g["rotations"]), _ptr(g["sh_language"]), _ptr(g["language_feature"])) != 0:
+            raise RuntimeError("oracle_backward_rows failed")
         return g
 
 

@@ -137,7 +137,8 @@ def run_oracle_path(m, cams, grads, act, progress=None):
         og = orc.backward(dimg, ddep, None, dfeat)
         views.append(dict(render=orc.color, depth=orc.depth, alpha=orc.alpha,
                           feature=orc.feature, radii=orc.radii, means2D=og["means2D"],
-                          margin=orc.margin(), ranges=orc.ranges(), point_list=orc.point_list()))
+                          margin=orc.margin(), ranges=orc.ranges(), point_list=orc.point_list(),
+                          n_contrib=orc.n_contrib(), final_T=orc.final_T()))
         g = {k: og[k].astype(np.float64)
              for k in ("means3D", "sh", "opacity", "scales", "rotations", "sh_language")}
         gq = g["rotations"]
@@ -172,6 +173,14 @@ def flipped_pixels(a, b, tol=FLIP_TOL):
         d = np.abs(a[k] - b[k])
         off |= (d.reshape(-1, *b["margin"].shape).max(0) > tol)
     return off, off & (b["margin"] < FLIP_MARGIN)
+
+
+def decision_flips(a, b):
+    """Pixels whose blend decisions differ between two oracle evaluations (float32 vs float64):
+    their n_contrib differs, or their final T by more than rounding (a flipped 1/255 splat moves
+    T by ~0.4 %, a flipped T < 1e-4 stop changes n_contrib)."""
+    Ta, Tb = a["final_T"].astype(np.float64), b["final_T"].astype(np.float64)
+    return (a["n_contrib"] != b["n_contrib"]) | (np.abs(Ta - Tb) > 1e-4 * np.maximum(Tb, 1e-4))
 
 
 def flip_gaussians(b, flips, P):

@@ -1,0 +1,110 @@
+"""Per-entry gradient parity against a float64 evaluation.
+
+The benchmarked path (tests/fused_ref.py run_bench_path: render() with the reference's default
+flags through the fused multi-view call) is compared entry by entry with the float64 build of the
+oracle (tests/f64_ref.py): every raw-leaf gradient entry at >= 1 % of its tensor's maximum must
+satisfy
+
+    |gpu - f64| <= max(1e-5 |f64|, C u B)        u = 2^-24, C = 8
+
+where B is the entry's float32 rounding scale: the sum over its per-pixel terms of |term| times
+the length of the float32 chain that term went through (T's recovery over the pixel's list),
+propagated through the per-Gaussian backward with |J| (f64_ref.py explains it).  The float32
+oracle -- the reference's own arithmetic, restated -- is held to the same bound (it is the
+calibration: its worst ratio |f32 - f64| / (u B) is ~1.6 at these sizes), so passing says the
+GPU is as accurate as the reference's float32 arithmetic, entry by entry.  A negative control
+shows the bound catches a 1e-4 systematic error in the colour terms.  The scale-relative 1e-5 check
+stays in tests/test_fused_parity.py.  Statistics: gpurun_out/f64_stats.jsonl.
+
+VERDICT r3 also proposed |gpu - f64| <= max(2 |f32 - f64|, 1e-5 |f64|); it is reported
+(`gpu_within_2x_f32`) but not asserted: two float32 evaluations with different (equally valid)
+arithmetic have independent rounding, and the 2x test fails a sizeable fraction of entries for
+independent errors of equal size.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from f64_ref import oracle_inputs, rounding_stats, run_f64_path
+from fused_ref import LEAVES, decision_flips, flip_gaussians, flipped_pixels, kernel_activations, \
+    run_bench_path, run_oracle_path
+from gsr_amd.model import SplatModel
+from gsr_amd.synthetic import make_cameras, make_gaussians, upstream_grads
+from oracle.oracle import set_threads
+
+pytestmark = pytest.mark.gpu
+
+C_BOUND = 8.0
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+STATS = os.path.join(ROOT, "gpurun_out", "f64_stats.jsonl")
+
+CASES = {
+    "small_6views_multi": dict(P=20_000, W=200, H=150, views=6, streams=3, seed=8, deg=3),
+    "cfg2_100k_800x800_multi": dict(P=100_000, W=800, H=800, views=3, streams=3, seed=0, deg=3),
+    "cfg3_1m_1008x756_multi": dict(P=1_000_000, W=1008, H=756, views=3, streams=3, seed=0, deg=3),
+    "cfg5_5m_1920x1080_multi": dict(P=5_000_000, W=1920, H=1080, views=2, streams=2, seed=0,
+                                    deg=3),
+}
+
+
+def _threads():
+    n = int(os.environ.get("OMP_NUM_THREADS") or 0) or (os.cpu_count() or 1)
+    return set_threads(min(n, 32))
+
+
+@pytest.mark.timeout(1500)
+@pytest.mark.parametrize("case", list(CASES))
+def test_gradients_within_float32_rounding_of_f64(case):
+    c = CASES[case]
+    _threads()
+    m = SplatModel(make_gaussians(c["P"], sh_degree=3, seed=c["seed"]), device="cuda",
+                   active_sh_degree=c["deg"])
+    cams = [x.to("cuda") for x in make_cameras(c["views"], c["W"], c["H"], seed=c["seed"])]
+    grads = upstream_grads(c["H"], c["W"], seed=1, device="cuda")
+    act = kernel_activations(m)
+    vg, gg = run_bench_path(m, cams, grads, streams=c["streams"], multi=True)
+    print(f"[{case}] GPU path done", flush=True)
+    vo, go = run_oracle_path(m, cams, grads, act)
+    print(f"[{case}] f32 oracle done", flush=True)
+    inp = oracle_inputs(m, act)
+    del m
+    v64, g64, B = run_f64_path(inp, cams, grads,
+                               progress=lambda s: print(f"[{case}] {s}", flush=True))
+    # Gaussians behind a pixel whose blend decisions differ (GPU vs f32, f32 vs f64) see a
+    # different set of terms: left out of the entry-wise statistics (counted)
+    P = vo[0]["radii"].shape[0]
+    hit = np.zeros(P, bool)
+    nflip64 = 0
+    for a, b, d in zip(vg, vo, v64):
+        off, _ = flipped_pixels(a, b)  # GPU vs f32: images off by > 1e-5 (test_fused_parity)
+        f64flip = decision_flips(d, b)  # f32 vs f64: decisions (images differ by rounding ~1e-5)
+        nflip64 += int(f64flip.sum())
+        hit |= flip_gaussians(b, off | f64flip, P)
+        assert np.array_equal(a["radii"], b["radii"]), case
+    rec = {"case": case, "gaussians_excluded": int(hit.sum()), "f64_decision_flips": nflip64,
+           "C": C_BOUND, "grads": {}}
+    for n in LEAVES:
+        st = rounding_stats(gg[n], go[n], g64[n], B[n], exclude=hit, C=C_BOUND)
+        rec["grads"][n] = st
+    os.makedirs(os.path.dirname(STATS), exist_ok=True)
+    with open(STATS, "a") as fh:
+        fh.write(json.dumps(rec) + "\n")
+    assert rec["gaussians_excluded"] <= max(50, 1e-4 * P), rec["gaussians_excluded"]
+    for n in LEAVES:
+        st = rec["grads"][n]
+        # calibration: the reference's float32 arithmetic meets the bound ...
+        assert st["f32_fail"] == 0, (case, n, st)
+        # ... and so does every GPU entry
+        assert st["gpu_fail"] == 0, (case, n, st)
+
+    if case == "small_6views_multi":
+        # negative control: a 1e-4 systematic error in the colour terms (the image's upstream
+        # gradient scaled) is caught by the same bound
+        gd = (grads[0] * (1.0 + 1e-4), grads[1], grads[2])
+        _, g64d, _ = run_f64_path(inp, cams, gd, bound=False)
+        st = rounding_stats(gg["_features_dc"], go["_features_dc"], g64d["_features_dc"],
+                            B["_features_dc"], exclude=hit, C=C_BOUND)
+        assert st["gpu_fail"] > 0.05 * st["n_big"], st

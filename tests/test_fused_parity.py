@@ -8,10 +8,10 @@ compared with the CPU oracle (tests/fused_ref.py explains both sides):
 * per view: radii exact; image, depth, alpha and feature within atol 1e-5; the screen-space
   gradient (viewspace_points.grad) within 1e-5 of its maximum;
 * summed over the views, every raw-leaf gradient (_xyz, _features_dc, _features_rest, _opacity,
-  _scaling, _rotation, _language_feature): max|gpu - oracle| / max|oracle| <= 1e-5, and entries
-  at >= 1 % of the maximum within 1e-4 of their own value (ENTRY_REL) -- the float atomics sum
-  the per-pixel terms in another order than the oracle's loop, so entry-wise agreement is only
-  meaningful where the entry is not a cancellation of much larger terms.
+  _scaling, _rotation, _language_feature): max|gpu - oracle| / max|oracle| <= 1e-5.  Entry by
+  entry the gradients are checked against a float64 evaluation of the same restatement, within
+  the entry's own float32 rounding scale (tests/test_f64_parity.py); the
+  entry-wise statistics against the float32 oracle are still recorded here.
 Sizes: a small scene, BASELINE config 2 (100k, 800x800), config 3 (1M, 1008x756) and config 5
 (5M, 1920x1080), all with SH degree 3 and the extended outputs.  Statistics are appended to
 gpurun_out/parity_stats.jsonl.
@@ -30,7 +30,6 @@ pytestmark = pytest.mark.gpu
 
 IMG_ATOL = 1e-5
 GRAD_REL = 1e-5
-ENTRY_REL = 1e-4
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 STATS = os.path.join(ROOT, "gpurun_out", "parity_stats.jsonl")
 
@@ -104,7 +103,6 @@ def test_benchmarked_path_matches_oracle(case):
     for n in LEAVES:
         g = st["grads"][n]
         assert g["rel_max"] <= GRAD_REL, (case, n, g)
-        assert g["rel_big_max"] <= ENTRY_REL, (case, n, g)
 
 
 @pytest.mark.parametrize("streams", [1, 3])
