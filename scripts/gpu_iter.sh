@@ -11,7 +11,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out; mkdir -p $OUT; export TMPDIR=/tmp
 if [ -n "${TESTS:-}" ]; then
   T="$TESTS"; [ "$T" = "all" ] && T=tests
-  timeout -k 10 ${TEST_TIMEOUT:-900} python -u -m pytest -x -v --timeout 600 --timeout-method thread $T -m gpu > $OUT/iter_tests.log 2>&1
+  timeout -k 10 ${TEST_TIMEOUT:-900} python -u -m pytest -x -v -s --timeout 1500 --timeout-method thread $T -m gpu > $OUT/iter_tests.log 2>&1
   rc=$?; grep -E "passed|failed|error" $OUT/iter_tests.log | tail -3
   if [ $rc -ne 0 ]; then grep -E "^E |Error|FAILED" $OUT/iter_tests.log | head -30; exit $rc; fi
 fi

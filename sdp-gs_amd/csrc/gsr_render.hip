@@ -477,9 +477,19 @@ constexpr int kAccDet = 13;
 // -- and the backward preprocess sums each Gaussian's rows.  DET implies ROWS.
 // One tile of the backward blend: workgroup `blk` of the view described by `a` (render_bwd_kernel:
 // one view per launch; render_bwd_views_kernel: the tiles of several views in one launch).
-template <bool EXTRA, bool FEAT, int GROUP, bool DET, bool ROWS>
+// 4 waves per SIMD (128 VGPRs): the pipelined variant holds one pending entry more
+#define GSR_BWD_WAVES(PIPE) __attribute__((amdgpu_waves_per_eu((PIPE) ? 4 : 1)))
+// PIPE (GSR_BWD_PIPE, round 4): the wave reduction of a contributing entry is issued together
+// with the next contributing entry's recurrence, in one basic block -- the two are independent
+// (the reduction needs only the entry's u = G dL/dalpha, w = alpha T and (dx, dy)), so the
+// butterfly's six dependent permlane / DPP stages overlap the recurrence's T-recovery chain
+// instead of serialising behind it.  The last entry of a batch is reduced before the batch's
+// barrier.  Same values, same LDS adds: results equal to the unpipelined kernel up to the order
+// of the LDS float adds (as between waves already).
+template <bool EXTRA, bool FEAT, int GROUP, bool DET, bool ROWS, bool PIPE>
 __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t blk) {
   static_assert(!DET || ROWS, "the deterministic backward stores per-instance rows");
+  static_assert(!(PIPE && DET), "the pipelined reduction is a default-mode kernel");
   // the batch's records in LDS, regrouped so that the colour dot product's packed FMAs read
   // register pairs straight from the loads: s_r0 = {x, y, conic.a, conic.b}, s_r1 = {conic.c,
   // opacity}, s_c0 = {r, g, b, depth}, s_c1 = {f0, f1, f2, 1} (alpha channel)
@@ -572,6 +582,31 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
                "v"(dpD.x), "v"(dpD.y));
   float acc_dot = 0.0f, last_cdot = 0.0f;
   float last_alpha = 0.0f;
+  // PIPE: the contributing entry whose wave reduction is still to be issued (u, w, (dx, dy), its
+  // batch slot); zeros reduce to zeros, so an empty pending entry needs no branch
+  float p_uu = 0.0f, p_w = 0.0f;
+  uint32_t p_j = 0;
+  // (dx, dy) of a batch slot, re-read from LDS (one broadcast read instead of two live registers)
+  auto slot_dxy = [&](uint32_t j) {
+    const float4 r0 = s_r0[j];
+    return mk2(r0.x - pfx, r0.y - pfy);
+  };
+  // the moments and colour terms of one (u, w, d) as the butterfly's 8 pairs (slot order of the
+  // accumulator row: kAccMx.. kAccF2; slots 14, 15 never reach the accumulator)
+  auto pair_terms = [&](float uu, float w, f2 dxy, f2 (&g)[8]) {
+    g[0] = uu * dxy;                               // kAccMx, kAccMy   <- sum u dx, sum u dy
+    g[1] = (uu * dxy.x) * dxy;                     // kAccCa, kAccCb   <- sum u dx dx, sum u dx dy
+    g[2] = mk2((uu * dxy.y) * dxy.y, uu);          // kAccCc, kAccOp   <- sum u dy dy, sum u
+    g[3] = w * dpA;                                // kAccR, kAccG
+    g[4] = w * dpB;                                // kAccB, kAccDepth
+    g[5] = FEAT ? w * dpC : mk2(0.f, 0.f);         // kAccF0, kAccF1
+    g[6] = mk2(FEAT ? w * dpD.x : 0.f, 0.f);       // kAccF2, (13)
+    g[7] = dxy;                                    // (14, 15), ignored
+  };
+  auto reduce_add = [&](f2 (&g)[8], uint32_t j) {
+    const float sum = wave_reduce16_dpp(g, lane);
+    if (red_lane && sum != 0.0f) atomicAdd(&s_acc[j * kAccPad + red_slot], sum);
+  };
   const float ddelx_dx = (float)(0.5 * a.W);
   const float ddely_dy = (float)(0.5 * a.H);
 
@@ -755,17 +790,20 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
       //   dL/dconic.{x,y,w} = -1/2 o sum u {dx dx, dx dy, dy dy},   dL/dopacity = sum u
       // The per-splat constants (a, b, c, o) are applied once per (splat, tile) at the flush.
       const float uu = G * dL_dalpha;
+      if (PIPE) {
+        // the previous contributing entry's reduction, beside this entry's recurrence
+        f2 g[8];
+        pair_terms(p_uu, p_w, slot_dxy(p_j), g);
+        reduce_add(g, p_j);
+        p_uu = uu;
+        p_w = dchannel_dcolor;
+        p_j = j;
+        continue;
+      }
       f2 g[8];
-      g[0] = uu * dxy;                               // kAccMx, kAccMy   <- sum u dx, sum u dy
-      g[1] = (uu * dxy.x) * dxy;                     // kAccCa, kAccCb   <- sum u dx dx, sum u dx dy
-      g[2] = mk2((uu * dxy.y) * dxy.y, uu);          // kAccCc, kAccOp   <- sum u dy dy, sum u
-      g[3] = dchannel_dcolor * dpA;                  // kAccR, kAccG
-      g[4] = dchannel_dcolor * dpB;                  // kAccB, kAccDepth
-      g[5] = FEAT ? dchannel_dcolor * dpC : mk2(0.f, 0.f);          // kAccF0, kAccF1
-      g[6] = mk2(FEAT ? dchannel_dcolor * dpD.x : 0.f, 0.f);       // kAccF2, (13)
       // slots 14, 15 are never read (only k < kAccDet reaches the accumulator): the dead dxy
       // pair rides along instead of two freshly zeroed registers for the butterfly's swaps
-      g[7] = dxy;                                                   // (14, 15), ignored
+      pair_terms(uu, dchannel_dcolor, dxy, g);
 #if GSR_BWD_DIAG == 1
       // diagnostic build only (wrong gradients): no wave reduction, one lane-local LDS add
       {
@@ -780,6 +818,13 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
       }
 #endif
     }
+    }
+    if (PIPE) {  // the batch's last contributing entry
+      f2 g[8];
+      pair_terms(p_uu, p_w, slot_dxy(p_j), g);
+      reduce_add(g, p_j);
+      p_uu = 0.0f;
+      p_w = 0.0f;
     }
 #if GSR_BLEND_STATS
     if ((threadIdx.x & 63) == 0) atomicMax(&s_maxc, ncw);
@@ -856,21 +901,30 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
   }
 }
 
-template <bool EXTRA, bool FEAT, int GROUP, bool DET, bool ROWS>
-__global__ __launch_bounds__(kThreads) void render_bwd_kernel(RenderBwdArgs a) {
-  render_bwd_tile<EXTRA, FEAT, GROUP, DET, ROWS>(a, blockIdx.x);
+template <bool EXTRA, bool FEAT, int GROUP, bool DET, bool ROWS, bool PIPE>
+__global__ __launch_bounds__(kThreads) GSR_BWD_WAVES(PIPE) void render_bwd_kernel(RenderBwdArgs a) {
+  render_bwd_tile<EXTRA, FEAT, GROUP, DET, ROWS, PIPE>(a, blockIdx.x);
 }
 
 // The backward blends of several views of a step in ONE launch: workgroup b belongs to the view k
 // with first[k] <= b < first[k + 1] (view-major; inside a view the forward's heaviest-first tile
 // order), so the views' launches do not each end in a tail of idle CUs, and one launch's duration
 // is the time of all its views' blends.
-template <bool EXTRA, bool FEAT, int GROUP, bool DET, bool ROWS>
-__global__ __launch_bounds__(kThreads) void render_bwd_views_kernel(RenderBwdViews m) {
+template <bool EXTRA, bool FEAT, int GROUP, bool DET, bool ROWS, bool PIPE>
+__global__ __launch_bounds__(kThreads) GSR_BWD_WAVES(PIPE) void render_bwd_views_kernel(RenderBwdViews m) {
   const uint32_t b = blockIdx.x;
   int k = 0;
   while (k + 1 < m.V && b >= m.first[k + 1]) k++;  // workgroup-uniform
-  render_bwd_tile<EXTRA, FEAT, GROUP, DET, ROWS>(m.v[k], b - m.first[k]);
+  render_bwd_tile<EXTRA, FEAT, GROUP, DET, ROWS, PIPE>(m.v[k], b - m.first[k]);
+}
+
+// GSR_BWD_PIPE (default 1): the pipelined wave reduction of render_bwd_tile
+static bool bwd_pipe() {
+  static const bool on = [] {
+    const char* e = getenv("GSR_BWD_PIPE");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
 }
 
 // ================================================================================================
@@ -1309,11 +1363,13 @@ hipError_t launch_render_backward_views(const RenderBwdArgs* views, int V, hipSt
 #define GSR_BWDV(E, F)                                                                            \
   do {                                                                                           \
     if (a.partial && a.det)                                                                      \
-      hipLaunchKernelGGL((render_bwd_views_kernel<E, F, 4, true, true>), dim3(nblk), dim3(kThreads), 0, s, m); \
+      hipLaunchKernelGGL((render_bwd_views_kernel<E, F, 4, true, true, false>), dim3(nblk), dim3(kThreads), 0, s, m); \
     else if (a.partial)                                                                          \
-      hipLaunchKernelGGL((render_bwd_views_kernel<E, F, 4, false, true>), dim3(nblk), dim3(kThreads), 0, s, m); \
+      hipLaunchKernelGGL((render_bwd_views_kernel<E, F, 4, false, true, false>), dim3(nblk), dim3(kThreads), 0, s, m); \
+    else if (bwd_pipe())                                                                         \
+      hipLaunchKernelGGL((render_bwd_views_kernel<E, F, 4, false, false, true>), dim3(nblk), dim3(kThreads), 0, s, m); \
     else                                                                                         \
-      hipLaunchKernelGGL((render_bwd_views_kernel<E, F, 4, false, false>), dim3(nblk), dim3(kThreads), 0, s, m); \
+      hipLaunchKernelGGL((render_bwd_views_kernel<E, F, 4, false, false, false>), dim3(nblk), dim3(kThreads), 0, s, m); \
   } while (0)
   if (feat) GSR_BWDV(true, true);
   else if (extra) GSR_BWDV(true, false);
@@ -1345,13 +1401,15 @@ hipError_t launch_render_backward(const RenderBwdArgs& a, hipStream_t s) {
 #define GSR_BWD(E, F)                                                                             \
   do {                                                                                           \
     if (a.partial && a.det)                                                                      \
-      hipLaunchKernelGGL((render_bwd_kernel<E, F, 4, true, true>), dim3(ntiles), dim3(kThreads), 0, s, a); \
+      hipLaunchKernelGGL((render_bwd_kernel<E, F, 4, true, true, false>), dim3(ntiles), dim3(kThreads), 0, s, a); \
     else if (a.partial)                                                                          \
-      hipLaunchKernelGGL((render_bwd_kernel<E, F, 4, false, true>), dim3(ntiles), dim3(kThreads), 0, s, a); \
+      hipLaunchKernelGGL((render_bwd_kernel<E, F, 4, false, true, false>), dim3(ntiles), dim3(kThreads), 0, s, a); \
     else if (group == 1)                                                                         \
-      hipLaunchKernelGGL((render_bwd_kernel<E, F, 1, false, false>), dim3(ntiles), dim3(kThreads), 0, s, a); \
+      hipLaunchKernelGGL((render_bwd_kernel<E, F, 1, false, false, false>), dim3(ntiles), dim3(kThreads), 0, s, a); \
+    else if (bwd_pipe())                                                                         \
+      hipLaunchKernelGGL((render_bwd_kernel<E, F, 4, false, false, true>), dim3(ntiles), dim3(kThreads), 0, s, a); \
     else                                                                                         \
-      hipLaunchKernelGGL((render_bwd_kernel<E, F, 4, false, false>), dim3(ntiles), dim3(kThreads), 0, s, a); \
+      hipLaunchKernelGGL((render_bwd_kernel<E, F, 4, false, false, false>), dim3(ntiles), dim3(kThreads), 0, s, a); \
   } while (0)
   if (feat) GSR_BWD(true, true);
   else if (extra) GSR_BWD(true, false);

@@ -107,6 +107,8 @@ def run_f64_path(inp, cams, grads, progress=None, bound=True):
                 J = _raw_chain(o.backward_rows(unit), inp["op"], inp["sc"], qh, nq)
                 term = {k: np.abs(J[k]) * A.reshape((P,) + (1,) * (J[k].ndim - 1)) for k in J}
                 B = term if B is None else {k: B[k] + term[k] for k in term}
+                if progress and P >= 1_000_000:
+                    progress(f"f64 view {i + 1}: rounding scale of slot {slot} done")
         del o
         if progress:
             progress(f"f64 oracle view {i + 1}/{len(cams)} done")
