@@ -729,9 +729,56 @@ def _cpu_model():
     return platform.processor() or platform.machine()
 
 
+def torch_cpu_baseline(model, cam, dimg, ddep, dfeat, deg, g1, c1, threads):
+    """BASELINE.json's "PyTorch-CPU render() on the host cores": the rasterizer as PyTorch tensor
+    code (oracle/torch_cpu.py: preprocess, binning by torch.sort, per-tile blend, autograd
+    backward), float32, torch.set_num_threads(threads).  Config 1 forward only (median of 5 after
+    one warm-up) and one headline view forward + backward (one timed run after a forward-only
+    warm-up: ~15-30 s of CPU work).  kind "pytorch"."""
+    try:
+        from oracle import torch_cpu as TC
+    except Exception as exc:  # pragma: no cover - reported, not fatal
+        return {"value": None, "error": repr(exc)[:200]}
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        with torch.no_grad():
+            l1 = [t.detach().cpu().float() for t in (g1.xyz, g1.get_opacity(), g1.get_features(),
+                                                    g1.get_scaling(), g1.get_rotation(),
+                                                    g1.language_feature)]
+            cam1 = TC.camera_dict(c1)
+            ts = []
+            for i in range(6):
+                t0 = time.perf_counter()
+                TC.render(*l1, 0, cam1, torch.zeros(3))
+                if i:
+                    ts.append(time.perf_counter() - t0)
+            t1 = float(np.median(ts))
+            lh = [t.detach().cpu().float().clone() for t in (
+                model.get_xyz, model.get_opacity, model.get_features, model.get_scaling,
+                model.get_rotation, model.get_language_feature)]
+            camh = TC.camera_dict(cam)
+            up = tuple(t.detach().cpu().float() for t in (dimg, ddep, dfeat))
+            TC.render(*lh, deg, camh, torch.zeros(3))  # warm-up (forward)
+        lh = [t.requires_grad_(True) for t in lh]
+        t0 = time.perf_counter()
+        TC.render(*lh, deg, camh, torch.zeros(3), upstream=up)
+        th = time.perf_counter() - t0
+    finally:
+        torch.set_num_threads(prev)
+    return {"value": round(1.0 / th, 5), "unit": "views/s", "cores": threads, "kind": "pytorch",
+            "sample": (f"one headline view ({cam.image_width}x{cam.image_height}, "
+                       f"{lh[0].shape[0]} Gaussians, SH degree {deg}, fwd+bwd) through "
+                       f"oracle/torch_cpu.py on {threads} torch threads: one run after a "
+                       f"forward warm-up, {th:.1f} s"),
+            "config1_fwd_views_per_s": round(1.0 / t1, 3),
+            "config1": f"10k Gaussians, 400x400, forward only, SH degree 0: median {1000 * t1:.1f} ms"}
+
+
 def cpu_baseline(model, cams, dimg, ddep, dfeat, deg, threads=0):
     """The CPU restatement (oracle/: C, float32, the reference's arithmetic) on the host cores,
-    timed in this run (rank 0 at N = 1), 2 warm-ups then the median of 5 (BASELINE.md CPU plan):
+    timed in this run (rank 0 at N = 1), 2 warm-ups then the median of 5 (BASELINE.md CPU plan),
+    and beside it (`pytorch`) the PyTorch-CPU render() BASELINE.json names (torch_cpu_baseline):
       * config 1: 10k synthetic Gaussians, one 400x400 camera, forward only (SH degree 0 as
         render()'s default Python SH at active degree 0);
       * the headline workload: one full view of it, forward + backward.
@@ -791,7 +838,9 @@ def cpu_baseline(model, cams, dimg, ddep, dfeat, deg, threads=0):
     def fwd_bwd():
         OracleRaster(**kwh).backward(dimg_n, ddep_n, None, dfeat_n)
     th = median_time(fwd_bwd)
+    pyt = torch_cpu_baseline(model, cams[0], dimg, ddep, dfeat, deg, g1, c1, n)
     return {"value": round(1.0 / th, 4), "unit": "views/s", "cores": n, "kind": "port",
+            "pytorch": pyt,
             "sample": (f"one headline view ({cams[0].image_width}x{cams[0].image_height}, "
                        f"{kwh['means3D'].shape[0]} Gaussians, SH degree {deg}, fwd+bwd) on the C "
                        f"restatement with {n} threads: median of 5 after 2 warm-ups, "

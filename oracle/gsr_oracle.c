@@ -280,11 +280,13 @@ struct oracle_state {
     unsigned gx, gy;
     real scale_modifier, tan_fovx, tan_fovy, focal_x, focal_y;
     real bg[3], view[16], proj[16], campos[3];
+    float viewf[16]; /* the float32 view matrix (the depth-sort key, below) */
     /* inputs (borrowed: the caller keeps them alive between forward and backward) */
     const float *means3D, *colors_precomp, *opacities, *scales, *rotations, *cov3D_precomp, *sh,
         *sh_language, *lang_precomp, *confidence;
     /* geometry (GeometryState, rasterizer_impl.h:21-37) */
     real* depths;
+    float* depth_key; /* the reference's float32 view-space z: the depth-sort key */
     unsigned char* clamped; /* [P*3] */
     int* radii;
     real* means2D;       /* [P*2] */
@@ -508,6 +510,13 @@ static void preprocess_one(oracle_state* st, int idx) {
         st->rgb[3 * idx + 2] = c.z;
     }
     st->depths[idx] = p_view.z;
+    {   /* forward.cu:227 depths[idx] = p_view.z in float32 (auxiliary.h:58-64): the key bits the
+         * binning sorts by (rasterizer_impl.cu:95), so the float64 build orders every tile's list
+         * exactly as the float32 one -- near-equal depths would otherwise swap */
+        const float* m = st->viewf;
+        const float px = means3D[3 * idx], py = means3D[3 * idx + 1], pz = means3D[3 * idx + 2];
+        st->depth_key[idx] = m[2] * px + m[6] * py + m[10] * pz + m[14];
+    }
     st->radii[idx] = f2i_sat(my_radius);
     st->means2D[2 * idx] = pix_x;
     st->means2D[2 * idx + 1] = pix_y;
@@ -667,6 +676,7 @@ oracle_state* oracle_forward(int P, int M, const float* background, const float*
     st->focal_x = (real)W / (2.0f * tan_fovx);
     for (int k = 0; k < 3; k++) st->bg[k] = background[k];
     for (int k = 0; k < 16; k++) st->view[k] = viewmatrix[k];
+    memcpy(st->viewf, viewmatrix, sizeof(st->viewf));
     for (int k = 0; k < 16; k++) st->proj[k] = projmatrix[k];
     for (int k = 0; k < 3; k++) st->campos[k] = campos[k];
     st->means3D = means3D; st->colors_precomp = colors_precomp; st->opacities = opacities;
@@ -679,6 +689,7 @@ oracle_state* oracle_forward(int P, int M, const float* background, const float*
     const unsigned gx = st->gx, gy = st->gy;
 
     st->depths = (real*)xcalloc(P, sizeof(real));
+    st->depth_key = (float*)xcalloc(P, sizeof(float));
     st->clamped = (unsigned char*)xcalloc((size_t)P * 3, 1);
     st->radii = (int*)xcalloc(P, sizeof(int));
     st->means2D = (real*)xcalloc((size_t)P * 2, sizeof(real));
@@ -710,8 +721,7 @@ oracle_state* oracle_forward(int P, int M, const float* background, const float*
             getRect(st->means2D[2 * idx], st->means2D[2 * idx + 1], st->radii[idx], &rmin, &rmax,
                     gx, gy);
             uint32_t dbits;
-            const float dkey = (float)st->depths[idx]; /* the float32 depth bits of the key */
-            memcpy(&dbits, &dkey, 4);
+            memcpy(&dbits, &st->depth_key[idx], 4);
             for (unsigned y = rmin.y; y < rmax.y; y++)
                 for (unsigned x = rmin.x; x < rmax.x; x++) {
                     uint64_t key = (uint64_t)(y * gx + x);
@@ -1287,7 +1297,7 @@ int oracle_backward_rows(oracle_state* st, const real* rows, real* dL_dmeans2D, 
 
 void oracle_free(oracle_state* st) {
     if (!st) return;
-    free(st->depths); free(st->clamped); free(st->radii); free(st->means2D); free(st->cov3D);
+    free(st->depths); free(st->depth_key); free(st->clamped); free(st->radii); free(st->means2D); free(st->cov3D);
     free(st->conic_opacity); free(st->rgb); free(st->feat); free(st->tiles_touched);
     free(st->point_list); free(st->ranges); free(st->final_T); free(st->n_contrib); free(st->margin);
     free(st);

@@ -180,7 +180,19 @@ def decision_flips(a, b):
     their n_contrib differs, or their final T by more than rounding (a flipped 1/255 splat moves
     T by ~0.4 %, a flipped T < 1e-4 stop changes n_contrib)."""
     Ta, Tb = a["final_T"].astype(np.float64), b["final_T"].astype(np.float64)
-    return (a["n_contrib"] != b["n_contrib"]) | (np.abs(Ta - Tb) > 1e-4 * np.maximum(Tb, 1e-4))
+    flips = (a["n_contrib"] != b["n_contrib"]) | (np.abs(Ta - Tb) > 1e-4 * np.maximum(Tb, 1e-4))
+    # tiles whose instance lists differ (a radius rounded to another integer, a near-plane
+    # cull decided the other way): every pixel of the tile
+    ra, rb = a["ranges"].reshape(-1, 2), b["ranges"].reshape(-1, 2)
+    H, W = flips.shape
+    gx = (W + 15) // 16
+    for t in range(ra.shape[0]):
+        sa, ea = ra[t]
+        sb, eb = rb[t]
+        if ea - sa != eb - sb or not np.array_equal(a["point_list"][sa:ea], b["point_list"][sb:eb]):
+            ty, tx = divmod(t, gx)
+            flips[ty * 16:(ty + 1) * 16, tx * 16:(tx + 1) * 16] = True
+    return flips
 
 
 def flip_gaussians(b, flips, P):
