@@ -80,9 +80,11 @@ __device__ __forceinline__ void pre_model_in(const PreArgs& a, int idx, const fl
 // pm / ps / pl: this Gaussian's 3 floats of means3D / scales / sh_language.  in: its
 // view-independent inputs if already evaluated (multi-view kernel), else null (evaluated here,
 // after the near-plane test).
+// rec: the lane's 4 LDS record slots, part k at rec[k ^ sw] (rec_swizzle).
 __device__ __forceinline__ uint32_t preprocess_gaussian(const PreArgs& a, int idx, float4* rec,
-                                                        const float* pm, const float* ps,
-                                                        const float* pl, uint32_t& rect_tiles,
+                                                        uint32_t sw, const float* pm,
+                                                        const float* ps, const float* pl,
+                                                        uint32_t& rect_tiles,
                                                         const PreModelIn* in) {
 #pragma unroll
   for (int k = 0; k < 4; k++) rec[k] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -165,10 +167,10 @@ __device__ __forceinline__ uint32_t preprocess_gaussian(const PreArgs& a, int id
   }
   g.tiles_touched[idx] = count;
   g.dkey_a[idx] = __float_as_uint(depth);
-  rec[0] = make_float4(px, py, con_a, con_b);
-  rec[1] = make_float4(con_c, op, depth, cr);
-  rec[2] = make_float4(cg, cb, in->f0, in->f1);
-  rec[3] = make_float4(in->f2, (float)r, qc, 0.f);
+  rec[0 ^ sw] = make_float4(px, py, con_a, con_b);
+  rec[1 ^ sw] = make_float4(con_c, op, depth, cr);
+  rec[2 ^ sw] = make_float4(cg, cb, in->f0, in->f1);
+  rec[3 ^ sw] = make_float4(in->f2, (float)r, qc, 0.f);
   return count;
 }
 
@@ -194,7 +196,14 @@ __device__ __forceinline__ void stage_rows3(const float* __restrict__ g, int n, 
     for (int q = (int)threadIdx.x; q < nf; q += kThreads) s[q] = g[q];
   }
 }
-constexpr int kRecStride = 5;  // float4s per LDS record row (4 + 1 pad)
+// The workgroup's records in LDS, 4 float4 slots per lane, part k of lane l's record in slot
+// 4 l + (k ^ rec_swizzle(l)).  Lane stores (ds_write_b128, 8-lane groups over 32 banks): the
+// swizzle puts the 8 lanes of a group on 8 different 16-byte bank quads; the epilogue's linear
+// reads (ds_read_b128, 16-lane groups over 64 banks) cover 16 consecutive slots: conflict-free
+// both ways.  (Round 3's 80-byte padded rows made the reads ~3-way conflicted: 4.03 M conflict
+// cycles per 3-view launch against 1.38 M LDS instructions)
+constexpr int kRecStride = 4;
+__device__ __forceinline__ uint32_t rec_swizzle(uint32_t lane) { return (lane >> 1) & 3u; }
 // (__launch_bounds__(256, 6), 80 VGPRs with a 12-byte spill, measured equal to the unbounded 82)
 // The workgroup's outputs after its lanes' preprocess_gaussian: the records (from LDS), the
 // zeroed accumulator rows and the partial sums of the tile counts.
@@ -213,8 +222,8 @@ __device__ __forceinline__ void pre_epilogue(const PreArgs& a, int base, int n, 
   __syncthreads();
   {
     float4* out = a.g.rec + 4 * (size_t)base;
-    for (int q = (int)threadIdx.x; q < 4 * n; q += kThreads)
-      out[q] = s_rec[(q >> 2) * kRecStride + (q & 3)];
+    for (int q = (int)threadIdx.x; q < 4 * n; q += kThreads)  // slot q holds part k of record q / 4
+      out[(q & ~3) | ((q & 3) ^ (int)rec_swizzle((uint32_t)q >> 2))] = s_rec[q];
   }
   if (a.acc_zero) {  // the workgroup's 64-B gradient accumulator rows (zeroed before the backward)
     float4* z = reinterpret_cast<float4*>(a.g.acc + (size_t)base * kAccFloats);
@@ -261,7 +270,8 @@ __global__ __launch_bounds__(kThreads) void preprocess_kernel(PreArgs a) {
 #endif
   uint32_t rect = 0;
   const uint32_t count = idx < a.P ? preprocess_gaussian(a, idx, s_rec + threadIdx.x * kRecStride,
-                                                         pm, ps, pl, rect, nullptr) : 0u;
+                                                         rec_swizzle(threadIdx.x), pm, ps, pl,
+                                                         rect, nullptr) : 0u;
   pre_epilogue(a, base, n, count, rect, s_rec, s_sum, s_rect);
 }
 
@@ -301,8 +311,9 @@ __global__ __launch_bounds__(kThreads, GSR_PRE_VIEWS_MINBLK) void preprocess_vie
 #else
     const PreModelIn& iv = in;
 #endif
-    const uint32_t count = live ? preprocess_gaussian(a, idx, s_rec + threadIdx.x * kRecStride, pm,
-                                                      ps, pl, rect, &iv) : 0u;
+    const uint32_t count = live ? preprocess_gaussian(a, idx, s_rec + threadIdx.x * kRecStride,
+                                                      rec_swizzle(threadIdx.x), pm, ps, pl, rect,
+                                                      &iv) : 0u;
     pre_epilogue(a, base, n, count, rect, s_rec, s_sum, s_rect);
     __syncthreads();  // s_rec / s_sum are the next view's
   }

@@ -992,7 +992,11 @@ __device__ __forceinline__ uint32_t block_mask(float4 r0, float4 r1, float qc, u
 
 // Per-group compaction: group g's list holds, in batch order, the entries whose mask has bit
 // 4 wid + g.  Returns this lane's group's length; `nmax` gets the longest of the wave's four.
-__device__ __forceinline__ uint32_t build_group_lists(const uint16_t* s_mask, uint8_t (*list)[kThreads],
+// The four lists of a wave sit kListRow bytes apart: a 4-byte pad puts the four groups' list
+// reads (one ds_read_b32 per step, four addresses per wave) on four different banks instead of
+// one (256-byte rows: a 4-way conflict on every step).
+constexpr int kListRow = kThreads + 4;
+__device__ __forceinline__ uint32_t build_group_lists(const uint16_t* s_mask, uint8_t (*list)[kListRow],
                                                       uint32_t cnt, int wid, int lane, uint32_t grp,
                                                       uint32_t& nmax, uint32_t& ntot) {
   const uint64_t lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
@@ -1026,7 +1030,7 @@ __device__ __forceinline__ void render_fwd_blk_tile(const RenderArgs& a, uint32_
   __shared__ float4 s_r2[kThreads];
   __shared__ float s_f2[FEAT ? kThreads : 1];  // rec[3].x (feature 2) only
   __shared__ uint16_t s_mask[kThreads];
-  __shared__ uint8_t s_list[kThreads / 64][4][kThreads];
+  __shared__ uint8_t s_list[kThreads / 64][4][kListRow];
   __shared__ uint32_t s_max;
   const int lane = (int)(threadIdx.x & 63);
   const int wid = (int)(threadIdx.x >> 6);

@@ -333,3 +333,24 @@ def test_densify_data_parallel_replicas_stay_identical():
     b = ref.arrays()
     for k in a0:
         assert np.array_equal(a0[k], b[k].cpu().numpy()), k
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+def test_densify_and_prune_5m_config5():
+    """BASELINE config 5: densify_and_prune on a 5M-row model at iteration
+    2500 (clone + split + prune, past the proximity window; gaussian_model.py:591-608), the
+    gradient threshold at the statistics' 90th percentile as bench.py's training leg sets it, so
+    ~10 % of the rows clone or split: parameters, statistics and Adam state bit-exact against the
+    restatement of the reference."""
+    P = 5_000_000
+    m, ref = _pair(P, seed=21, big_rows=64)
+    g = (m.xyz_gradient_accum / m.denom).nan_to_num(0.0).reshape(-1)
+    thr = float(torch.quantile(g[g > 0][: 1 << 24], 0.9))
+    torch.manual_seed(5)
+    m.densify_and_prune(thr, MIN_OP, EXTENT, None, 2500, True)
+    torch.manual_seed(5)
+    ref.densify_and_prune(thr, MIN_OP, EXTENT, None, 2500)
+    _assert_same(m, ref)
+    n = m._xyz.shape[0]
+    assert n != P and n > 0.5 * P, n
