@@ -310,6 +310,27 @@ int gsr_rasterize_views_fused_backward(
     float* dL_dopacity_raw, float* dL_dscaling_raw, float* dL_drotation_raw,
     float* dL_dlanguage_feature, int accumulate, void* stream, int debug);
 
+/* Called by the sliced backward below after the per-Gaussian backward of rows [row_begin,
+ * row_end) has been enqueued on the call's stream (every leaf gradient of those rows is final
+ * once that work runs).  Runs on the calling thread, inside the call. */
+typedef void (*gsr_rows_fn)(void* ctx, int row_begin, int row_end);
+
+/* gsr_rasterize_views_fused_backward with the per-Gaussian backward issued in row slices of
+ * slice_rows (a multiple of 256; 0 = one slice) and on_rows(ctx, a, b) called after each slice
+ * (after the single launch when 0; for [0, P) when the merged launch is not available): a
+ * multi-GPU caller starts the slice's gradient all-reduce there while the next slice computes
+ * (gsr_amd.pipeline).  Results are identical to the unsliced call. */
+int gsr_rasterize_views_fused_backward_sliced(
+    int V, const gsr_view* views, int image_height, int image_width,
+    int P, int M, const float* background, const float* means3D,
+    const float* features_dc, const float* features_rest, const float* opacity_raw,
+    const float* scaling_raw, const float* rotation_raw, float scale_modifier,
+    int degree, const float* language_feature, const float* confidence, int include_feature,
+    float* dL_dmeans3D, float* dL_dfeatures_dc, float* dL_dfeatures_rest,
+    float* dL_dopacity_raw, float* dL_dscaling_raw, float* dL_drotation_raw,
+    float* dL_dlanguage_feature, int accumulate, void* stream, int debug, int slice_rows,
+    gsr_rows_fn on_rows, void* rows_ctx);
+
 /* Replaces _C.mark_visible -> markVisible (rasterize_points.cu:198-217) -> checkFrustum
  * (rasterizer_impl.cu:54-66): present[i] = view-space z > 0.2 (bool as uint8). */
 int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,

@@ -1641,7 +1641,26 @@ int gsr_rasterize_views_fused_backward(
     float* dL_dfeatures_rest, float* dL_dopacity_raw, float* dL_dscaling_raw,
     float* dL_drotation_raw, float* dL_dlanguage_feature, int accumulate, void* stream_ptr,
     int debug) {
+  return gsr_rasterize_views_fused_backward_sliced(
+      V, views, image_height, image_width, P, M, background, means3D, features_dc, features_rest,
+      opacity_raw, scaling_raw, rotation_raw, scale_modifier, degree, language_feature,
+      confidence, include_feature, dL_dmeans3D, dL_dfeatures_dc, dL_dfeatures_rest,
+      dL_dopacity_raw, dL_dscaling_raw, dL_drotation_raw, dL_dlanguage_feature, accumulate,
+      stream_ptr, debug, 0, nullptr, nullptr);
+}
+
+int gsr_rasterize_views_fused_backward_sliced(
+    int V, const gsr_view* views, int image_height, int image_width, int P, int M,
+    const float* background, const float* means3D, const float* features_dc,
+    const float* features_rest, const float* opacity_raw, const float* scaling_raw,
+    const float* rotation_raw, float scale_modifier, int degree, const float* language_feature,
+    const float* confidence, int include_feature, float* dL_dmeans3D, float* dL_dfeatures_dc,
+    float* dL_dfeatures_rest, float* dL_dopacity_raw, float* dL_dscaling_raw,
+    float* dL_drotation_raw, float* dL_dlanguage_feature, int accumulate, void* stream_ptr,
+    int debug, int slice_rows, gsr_rows_fn on_rows, void* rows_ctx) {
   g_err.clear();
+  if (slice_rows < 0 || (slice_rows % 256) != 0)
+    return fail(GSR_ERR_ARGUMENT, "slice_rows = %d: a multiple of 256 (0 = one slice)", slice_rows);
   if (V < 0 || V > kFwdSlots) return fail(GSR_ERR_ARGUMENT, "V = %d views: 0 .. %d supported", V, kFwdSlots);
   if (V > 0 && !views) return fail(GSR_ERR_ARGUMENT, "views missing");
   hipStream_t call_stream = (hipStream_t)stream_ptr;
@@ -1661,7 +1680,10 @@ int gsr_rasterize_views_fused_backward(
                            (v > 0 || accumulate) ? 1 : 0, w.dL_dcolor_sh, w.pre_jac))
       return rc;
   }
-  if (V == 0) return GSR_OK;
+  if (V == 0) {
+    if (on_rows && P > 0) on_rows(rows_ctx, 0, P);
+    return GSR_OK;
+  }
   // The backward blends of all views run on views[0].stream, merged into launches of up to
   // kMaxBwdViews views (`chunks` launches; one launch's tiles are its views' tiles, so no per-view
   // tail of idle CUs); the per-Gaussian parts read-modify-write the leaves' gradients and run in
@@ -1724,22 +1746,33 @@ int gsr_rasterize_views_fused_backward(
     for (int k = 0; k < n; k++)
       if (!calls[(size_t)(v0 + k)].done) bas[np++] = calls[(size_t)(v0 + k)].ba;
     hipError_t ve = hipErrorNotSupported;
+    // the last chunk's per-Gaussian backward finishes the leaves' gradients: in row slices, each
+    // handed to on_rows as soon as it is enqueued (gsr.h: a multi-GPU caller all-reduces the
+    // slice while the next one computes)
+    const bool last = v0 + per >= V;
+    const uint32_t step = (last && on_rows && slice_rows > 0) ? (uint32_t)slice_rows : (uint32_t)P;
     if (np > 1 && views_pre_merged() && !per_view_pre) {
       const int debug = debug_sync;
       hipStream_t stream = call_stream;
       PROF_BEGIN(PREPROCESS_BWD);
-      ve = launch_preprocess_backward_views(bas, np, call_stream);
+      for (uint32_t r0 = 0; r0 < (uint32_t)P; r0 += step) {
+        ve = launch_preprocess_backward_views(bas, np, call_stream, r0, r0 + step);
+        if (ve != hipSuccess) break;
+        if (last && on_rows && step < (uint32_t)P) on_rows(rows_ctx, (int)r0, (int)std::min(r0 + step, (uint32_t)P));
+      }
       if (ve != hipSuccess && ve != hipErrorNotSupported)
         return fail(GSR_ERR_HIP, "launch_preprocess_backward_views: %s", hipGetErrorString(ve));
       if (ve == hipSuccess) {
         PROF_END(PREPROCESS_BWD);
         if (debug) GSR_CHECK(hipStreamSynchronize(stream));
+        if (last && on_rows && step >= (uint32_t)P) on_rows(rows_ctx, 0, P);
       }
     }
     if (ve == hipErrorNotSupported) {
       (void)hipGetLastError();
       for (int k = 0; k < n; k++)
         if (int rc = bwd_pre(calls[(size_t)(v0 + k)], call_stream)) return rc;
+      if (last && on_rows) on_rows(rows_ctx, 0, P);
     }
   }
   return GSR_OK;

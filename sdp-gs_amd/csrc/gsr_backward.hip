@@ -533,8 +533,8 @@ __global__ __launch_bounds__(kThreads) void preprocess_bwd_kernel(BwdPreArgs a) 
 template <bool ACC>
 __global__ __launch_bounds__(kThreads, GSR_BWDV_MINBLK) void preprocess_bwd_views_kernel(BwdPreViews m) {
   const BwdPreArgs& a0 = m.v[0];
-  const size_t i = (size_t)blockIdx.x * kThreads + threadIdx.x;
-  if (i >= (size_t)a0.P) return;
+  const size_t i = (size_t)m.row0 + (size_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= (size_t)m.row1) return;
   RegSink sk;
   sk.assign = !ACC;
   if (ACC) {
@@ -668,7 +668,8 @@ hipError_t launch_sh_grad_flush(const ShFlushArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_preprocess_backward_views(const BwdPreArgs* views, int V, hipStream_t s) {
+hipError_t launch_preprocess_backward_views(const BwdPreArgs* views, int V, hipStream_t s,
+                                            uint32_t row0, uint32_t row1) {
   if (V <= 0) return hipSuccess;
   if (V > kMaxBwdViews) return hipErrorNotSupported;
   BwdPreViews m{};
@@ -685,8 +686,10 @@ hipError_t launch_preprocess_backward_views(const BwdPreArgs* views, int V, hipS
       return hipErrorNotSupported;
     m.v[k] = a;
   }
-  if (views[0].P == 0) return hipSuccess;
-  const dim3 grid((views[0].P + kThreads - 1) / kThreads);
+  m.row0 = row0;
+  m.row1 = row1 < (uint32_t)views[0].P ? row1 : (uint32_t)views[0].P;
+  if (m.row1 <= m.row0) return hipSuccess;
+  const dim3 grid((m.row1 - m.row0 + kThreads - 1) / kThreads);
   if (views[0].accumulate)
     hipLaunchKernelGGL(preprocess_bwd_views_kernel<true>, grid, dim3(kThreads), 0, s, m);
   else

@@ -349,8 +349,11 @@ hipError_t launch_preprocess_backward(const BwdPreArgs& a, hipStream_t s);
 struct BwdPreViews {
   BwdPreArgs v[8];
   int V;
+  uint32_t row0, row1;  // the Gaussian rows [row0, row1) of this launch
 };
-hipError_t launch_preprocess_backward_views(const BwdPreArgs* views, int V, hipStream_t s);
+// rows [row0, row1) of the per-Gaussian backward (row1 > P: up to P)
+hipError_t launch_preprocess_backward_views(const BwdPreArgs* views, int V, hipStream_t s,
+                                            uint32_t row0 = 0, uint32_t row1 = 0xffffffffu);
 constexpr int kShFlushMaxViews = 8;
 struct ShFlushArgs {
   int P, M, D, nviews, accumulate;

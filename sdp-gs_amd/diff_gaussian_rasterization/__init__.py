@@ -671,14 +671,27 @@ class _RasterizeViewsFused(torch.autograd.Function):
         if into_leaves:
             _order_leaf_grads(dev, cur)
         t_host = time.perf_counter()
-        with _lib.on_device(dev):
-            rc = L.gsr_rasterize_views_fused_backward(
-                V, views, H, W, P, M, _ptr(bg), _ptr(m3), _ptr(dc), _ptr(rest), _ptr(op),
+        args = (V, views, H, W, P, M, _ptr(bg), _ptr(m3), _ptr(dc), _ptr(rest), _ptr(op),
                 _ptr(sc), _ptr(rot), mt["scale_modifier"], mt["degree"], _ptr(lf), _ptr(conf),
                 int(mt["include_feature"]), _ptr(d_means3D), _ptr(d_dc), _ptr(d_rest),
                 _ptr(d_op), _ptr(d_sc), _ptr(d_rot), _ptr(d_lf), int(accumulate),
                 cur.cuda_stream, ctx.gsr_flags | _TEST_BWD_BITS[0])
+        slices = _ROW_SLICES.get(dev.index) if into_leaves else None
+        errors = []
+        with _lib.on_device(dev):
+            if slices is None:
+                rc = L.gsr_rasterize_views_fused_backward(*args)
+            else:
+                def on_rows(_ctx, a, b):  # the leaves' rows [a, b) are final once this runs
+                    try:
+                        slices.on_rows(a, b)
+                    except Exception as exc:  # noqa: BLE001 -- re-raised after the C call
+                        errors.append(exc)
+                cb = _lib.ROWS_FN(on_rows)
+                rc = L.gsr_rasterize_views_fused_backward_sliced(*args, slices.rows(P), cb, None)
         _lib.check(rc)
+        if errors:
+            raise errors[0]
         LAST_STATS["views_bwd_host_s"] = time.perf_counter() - t_host
         if into_leaves:
             prev = _LEAF_GRAD_EVENT.get(dev.index)
@@ -785,6 +798,42 @@ class ShPrecolor:
 
     def __exit__(self, *exc):
         _PRECOLOR.pop(self.device.index, None)
+        return False
+
+
+_ROW_SLICES = {}  # device index -> BackwardRowSlices
+
+
+class BackwardRowSlices:
+    """While installed (``with BackwardRowSlices(dev, on_rows, slices):``), a grad-into-leaves
+    backward of the multi-view call (rasterize_views_fused) runs its per-Gaussian part in
+    `slices` row ranges (include/gsr.h gsr_rasterize_views_fused_backward_sliced) and calls
+    on_rows(a, b) as soon as rows [a, b) of every leaf gradient it writes are final on the
+    current stream -- gsr_amd.pipeline starts those rows' all-reduce there, so the reduction of
+    one slice overlaps the next slice's compute.  `ran` tells whether a
+    backward used it."""
+
+    def __init__(self, device, on_rows, slices: int = 4):
+        self.device = torch.device(device)
+        self.on_rows = on_rows
+        self.slices = max(1, int(slices))
+        self.ran = False
+
+    def rows(self, P):
+        self.ran = True
+        if self.slices <= 1 or P <= 256:
+            return 0
+        per = -(-P // self.slices)
+        return -(-per // 256) * 256
+
+    def __enter__(self):
+        if self.device.index in _ROW_SLICES:
+            raise RuntimeError("backward row slices are already installed on this device")
+        _ROW_SLICES[self.device.index] = self
+        return self
+
+    def __exit__(self, *exc):
+        _ROW_SLICES.pop(self.device.index, None)
         return False
 
 

@@ -196,6 +196,9 @@ def load():
             _i, _p, _p, _i,              # degree, language_feature, confidence, include_feature
             _p, _p, _p, _p, _p, _p, _p,  # grads: means3D, dc, rest, op, scale, rot, lang
             _i, _p, _i]                  # accumulate, stream, debug
+        L.gsr_rasterize_views_fused_backward_sliced.restype = _i
+        L.gsr_rasterize_views_fused_backward_sliced.argtypes = list(
+            L.gsr_rasterize_views_fused_backward.argtypes) + [_i, ROWS_FN, _p]
         L.gsr_sh_precolor.restype = _i
         L.gsr_sh_precolor.argtypes = [_i, _i, _i, _p, _p, _p, _i, ctypes.POINTER(_p),
                                       ctypes.POINTER(_p), ctypes.POINTER(_p), ctypes.POINTER(_p), _p]
@@ -316,6 +319,10 @@ def load():
         L.gsr_test_host_wait_ms.argtypes = [_i]
         _lib = L
     return _lib
+
+
+# include/gsr.h gsr_rows_fn: (ctx, row_begin, row_end)
+ROWS_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int, ctypes.c_int)
 
 
 def check(rc: int):

@@ -193,6 +193,42 @@ class GradAllReducer:
         self._issue(lo, hi)
         self._done.add(i)
 
+    def reduce_row_slices_async(self, params: Iterable[torch.Tensor], a: int, b: int):
+        """Start the all-reduce of rows [a, b) of several parameters' gradients -- one span per
+        parameter, issued as ONE coalesced collective on RCCL (a row slice of the per-Gaussian
+        backward, diff_gaussian_rasterization.BackwardRowSlices), so a slice costs one
+        collective's latency, not one per parameter."""
+        if not self._active():
+            return
+        spans = []
+        for p in params:
+            i, lo, hi = self._range(p, a, b)
+            if hi <= lo:
+                continue
+            self._pack(i, lo, hi)
+            spans.append((lo, hi))
+            self._done.add(i)
+        if not spans:
+            return
+        if len(spans) > 1 and self._coalesce():
+            from torch.distributed.distributed_c10d import _coalescing_manager
+            group = self.group or dist.group.WORLD
+            with _coalescing_manager(group=group, device=self.flat.device, async_ops=True) as cm:
+                for lo, hi in spans:
+                    dist.all_reduce(self.flat[lo:hi], op=dist.ReduceOp.SUM, group=self.group)
+            self._works.append(cm)
+            return
+        for lo, hi in spans:
+            self._issue(lo, hi)
+
+    def _coalesce(self) -> bool:
+        """RCCL groups coalesced all-reduces into one launch; gloo issues them one by one."""
+        try:
+            from torch.distributed.distributed_c10d import _coalescing_manager  # noqa: F401
+        except ImportError:  # pragma: no cover - older torch
+            return False
+        return dist.get_backend(self.group) == "nccl" and self.flat.is_cuda
+
     def wait(self):
         """Finish the step's reduction: wait for the collectives (their results are ordered
         before later work on the current stream), average if asked, unpack non-view grads."""

@@ -40,7 +40,7 @@ class ViewPipeline:
     ``depth - 1`` side streams, joined back into the current stream at the end of run()."""
 
     def __init__(self, device: Optional[torch.device] = None, depth: int = 2,
-                 defer_sh: bool = True, precolor: bool = True):
+                 defer_sh: bool = True, precolor: bool = True, bwd_slices: int = 4):
         if depth < 1:
             raise ValueError("depth must be >= 1")
         self.device = torch.device(device) if device is not None else torch.device(
@@ -48,6 +48,9 @@ class ViewPipeline:
         self.depth = depth
         self.defer_sh = defer_sh
         self.precolor = precolor
+        # with a reducer: the multi-view backward's per-Gaussian part in this many row slices,
+        # each slice's non-SH gradient rows all-reduced as soon as it is written (run_views)
+        self.bwd_slices = bwd_slices
         self._pre_bufs = None  # the pre-pass's per-view buffers, reused step after step
         self.side = [torch.cuda.Stream(device=self.device) for _ in range(depth - 1)]
 
@@ -113,7 +116,7 @@ class ViewPipeline:
             out.append(fn(items, streams))
             return out
 
-        return self._step(items, issue, model, campos_of, reducer)[0]
+        return self._step(items, issue, model, campos_of, reducer, sliced=True)[0]
 
     def _check(self, reducer, model):
         if reducer is not None and self.defer_sh and model is None:
@@ -122,7 +125,7 @@ class ViewPipeline:
             raise ValueError("ViewPipeline.run: a reducer with defer_sh needs model= (the SH "
                              "leaves are reduced after the deferred flush)")
 
-    def _step(self, items, issue, model, campos_of, reducer):
+    def _step(self, items, issue, model, campos_of, reducer, sliced=False):
         import diff_gaussian_rasterization as dgr
         main = torch.cuda.current_stream(self.device)
         pre = contextlib.nullcontext()
@@ -150,13 +153,24 @@ class ViewPipeline:
                         reducer.reduce_rows_async(t, a, b)
         defer = (dgr.ShGradDeferral(self.device, on_rows=on_rows, chunk_rows=chunk)
                  if self.defer_sh else contextlib.nullcontext())
+        slices = contextlib.nullcontext()
+        if reducer is not None and sliced and self.bwd_slices > 1:
+            ids = {id(t) for t in sh_leaves}
+            rest = [p for p in reducer.current_params() if id(p) not in ids]
+            slices = dgr.BackwardRowSlices(
+                self.device, lambda a, b: reducer.reduce_row_slices_async(rest, a, b),
+                self.bwd_slices)
         with pre, defer:  # defer's exit: the SH gradients of all views, after the join
-            issue(out)
+            with slices:
+                issue(out)
             if reducer is not None:  # every view's backward is done: the non-SH grads are final
                 ids = {id(t) for t in sh_leaves}
                 # (with the step's fault snapshot: every forward of the step is done)
-                reducer.reduce_async([p for p in reducer.current_params() if id(p) not in ids],
-                                     guard=True)
+                if getattr(slices, "ran", False):  # already reduced slice by slice
+                    reducer.reduce_async([], guard=True)
+                else:
+                    reducer.reduce_async([p for p in reducer.current_params()
+                                          if id(p) not in ids], guard=True)
         if reducer is not None:
             if sh_leaves and not defer.views_flushed:
                 reducer.reduce_async(sh_leaves)  # no view produced deferred SH gradients

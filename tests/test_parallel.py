@@ -102,7 +102,7 @@ class _Model:
                        for p in self.params]
 
 
-def _overlapped_worker(rank, world, init, n_views, q):
+def _overlapped_worker(rank, world, init, n_views, q, sliced=False):
     """Two steps with a densification between them; the reducer is built once on the model.
     Step order as ViewPipeline.run(reducer=...): non-SH gradients reduced first, then the 'SH'
     parameter (params[1]) in row slices as they are 'flushed'."""
@@ -119,7 +119,13 @@ def _overlapped_worker(rank, world, init, n_views, q):
         for v in shard_views(n_views, rank, world):
             _view_loss(ps, v + step).backward()
         reducer.begin()
-        reducer.reduce_async([ps[0], ps[2]])
+        if sliced:  # the per-Gaussian backward's row slices (BackwardRowSlices), then the guard
+            n = ps[0].shape[0]
+            for a in range(0, n, 384):
+                reducer.reduce_row_slices_async([ps[0], ps[2]], a, min(n, a + 384))
+            reducer.reduce_async([], guard=True)
+        else:
+            reducer.reduce_async([ps[0], ps[2]])
         rows = ps[1].shape[0]
         for a in range(0, rows, 256):
             reducer.reduce_rows_async(ps[1], a, min(rows, a + 256))
@@ -131,14 +137,18 @@ def _overlapped_worker(rank, world, init, n_views, q):
     dist.destroy_process_group()
 
 
-def test_overlapped_allreduce_follows_densification():
+@pytest.mark.parametrize("sliced", [False, True])
+def test_overlapped_allreduce_follows_densification(sliced):
     """after densification replaces the parameters, the reducer rebuilds its flat
     buffer and the new .grad are the ones reduced; the sliced (overlapped) ordering gives the
-    single-process gradients."""
+    single-process gradients.  sliced: the non-SH gradients go out in row
+    slices of all their parameters at once (reduce_row_slices_async, as the per-Gaussian
+    backward's slices finish), the SH rows as flushed: still the single-process sums."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     init = _init_method()
-    procs = [ctx.Process(target=_overlapped_worker, args=(r, 2, init, 5, q)) for r in range(2)]
+    procs = [ctx.Process(target=_overlapped_worker, args=(r, 2, init, 5, q, sliced))
+             for r in range(2)]
     for p in procs:
         p.start()
     out = q.get(timeout=120)

@@ -35,8 +35,8 @@ def _scene(dev):
     return model, cams, grads
 
 
-def _step(model, cams, grads, views, reducer):
-    from gaussian_renderer import render
+def _step(model, cams, grads, views, reducer, multi=False):
+    from gaussian_renderer import render, render_views
     dimg, ddep, dfeat = grads
     bg = torch.zeros(3, device=dimg.device)
 
@@ -44,12 +44,22 @@ def _step(model, cams, grads, views, reducer):
         pkg = render(cam, model, _Pipe(), bg, _Opt())
         torch.autograd.backward([pkg["render"], pkg["depth"], pkg["feature"]], [dimg, ddep, dfeat])
 
+    def all_views(cs, strs):  # the multi-view call: its backward runs in row slices
+        pkgs = render_views(cs, model, _Pipe(), bg, _Opt(), streams=strs)
+        st = pkgs[0]["views"]
+        V = len(pkgs)
+        torch.autograd.backward([st["render"], st["depth"], st["feature"]],
+                                [g.expand(V, *g.shape) for g in (dimg, ddep, dfeat)])
+
     if reducer is not None:
         reducer.attach_grads()
     else:
         for p in model.parameters():
             p.grad = None
-    views.run(cams, one_view, model=model, reducer=reducer)
+    if multi:
+        views.run_views(cams, all_views, model=model, reducer=reducer)
+    else:
+        views.run(cams, one_view, model=model, reducer=reducer)
     torch.cuda.synchronize()
     return [p.grad.detach().clone() for p in model.parameters()]
 
@@ -72,8 +82,9 @@ def world1(request, tmp_path):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("bucket_bytes", [64 << 20, 256 << 10])
-def test_bucket_view_grads_equal_plain_step(world1, bucket_bytes):
+@pytest.mark.parametrize("bucket_bytes,multi", [(64 << 20, False), (256 << 10, False),
+                                                (64 << 20, True), (256 << 10, True)])
+def test_bucket_view_grads_equal_plain_step(world1, bucket_bytes, multi):
     import diff_gaussian_rasterization as dgr
     from gsr_amd.parallel import GradAllReducer
     from gsr_amd.pipeline import ViewPipeline
@@ -83,13 +94,13 @@ def test_bucket_view_grads_equal_plain_step(world1, bucket_bytes):
     try:
         model, cams, grads = _scene(dev)
         views = ViewPipeline(dev, depth=2, defer_sh=True, precolor=True)
-        ref = _step(model, cams, grads, views, None)
+        ref = _step(model, cams, grads, views, None, multi)
         reducer = GradAllReducer(model, bucket_bytes=bucket_bytes)
         # issue the collectives at world size 1 as well: gloo copies each slice to the host and
         # back, so a collective that ran before its slice was flushed would write stale zeros
         reducer._active = lambda: True
         for _ in range(2):  # the second step reuses the attached buffer (zeroed by attach_grads)
-            got = _step(model, cams, grads, views, reducer)
+            got = _step(model, cams, grads, views, reducer, multi)
             for p, g, r in zip(model.parameters(), got, ref):
                 assert g.shape == r.shape
                 # the backward's float atomics make two runs of a view differ in the last bits
@@ -101,6 +112,7 @@ def test_bucket_view_grads_equal_plain_step(world1, bucket_bytes):
             end = base + reducer.flat.numel() * 4
             assert all(base <= p.grad.data_ptr() < end for p in model.parameters())
         assert any(float(r.abs().max()) > 0 for r in ref)
+        assert float(reducer.skip_flag()) == 0.0  # the fault snapshot went through too
         if world1 == "nccl":
             assert dist.get_backend() == "nccl"
     finally:
