@@ -918,6 +918,280 @@ __global__ __launch_bounds__(kThreads) GSR_BWD_WAVES(PIPE) void render_bwd_views
   render_bwd_tile<EXTRA, FEAT, GROUP, DET, ROWS, PIPE>(m.v[k], b - m.first[k]);
 }
 
+// ================================================================================================
+// Backward with two pixels per lane (GSR_BWD_PIX2=1): 128-lane workgroups, wave
+// w owns the 8x16 column half w of the tile, lane l the pixels (8w + l % 8, l / 8) and the one 8
+// rows below.  Per list entry both pixels' recurrences run side by side (two independent chains
+// per lane) and their terms are added in-lane before ONE wave reduction, which thus serves 128
+// pixels instead of 64; a wave's list is the union of its two quadrants' lists.  Batches of 128
+// records (one per lane), 17 KB of LDS per workgroup.  Same per-pixel arithmetic as
+// render_bwd_tile, so the results agree with it up to the order of the float additions.
+// ================================================================================================
+constexpr int kThreads2 = 128;
+template <bool EXTRA, bool FEAT, int GROUP>
+__device__ __forceinline__ void render_bwd_tile2(const RenderBwdArgs& a, uint32_t blk) {
+  __shared__ float4 s_r0[kThreads2];
+  __shared__ float2 s_r1[kThreads2];
+  __shared__ float4 s_c0[kThreads2];
+  __shared__ float4 s_c1[FEAT ? kThreads2 : 1];
+  __shared__ uint32_t s_gid[kThreads2];
+  __shared__ float s_acc[kThreads2 * kAccPad];
+  __shared__ uint8_t s_mask[kThreads2];
+  __shared__ uint8_t s_list[kThreads2 / 64][kThreads2];
+
+  const int lane = (int)(threadIdx.x & 63);
+  const int wid = (int)(threadIdx.x >> 6);
+  const SwapOrient swap_orient = probe_swaps(lane);
+  const int red_slot = reduce16_slot(lane, swap_orient);
+  const bool red_lane = (lane & 3) == 0 && red_slot < kAccDet;
+  const uint32_t ntiles = a.gx * a.gy;
+  const uint32_t tile = sched_tile(blk, ntiles, a.sched, a.order);
+  const uint32_t tx = tile % a.gx, ty = tile / a.gx;
+  const uint32_t px = tx * kTile + (uint32_t)wid * 8u + (uint32_t)(lane & 7);
+  const uint32_t py0 = ty * kTile + (uint32_t)(lane >> 3), py1 = py0 + 8u;
+  const bool in0 = px < (uint32_t)a.W && py0 < (uint32_t)a.H;
+  const bool in1 = px < (uint32_t)a.W && py1 < (uint32_t)a.H;
+  const float pfx = (float)px, pfy0 = (float)py0, pfy1 = (float)py1;
+  const size_t pix0 = (size_t)py0 * a.W + px, pix1 = (size_t)py1 * a.W + px;
+  const size_t HW = (size_t)a.W * a.H;
+
+  const uint2 range = a.ranges[tile];
+  const uint32_t tile_last = a.tile_last[tile];
+  const float Tf0 = in0 ? a.final_T[pix0] : 0.0f, Tf1 = in1 ? a.final_T[pix1] : 0.0f;
+  float T0 = Tf0, T1 = Tf1;
+  const uint32_t lc0 = in0 ? a.n_contrib[pix0] : 0u, lc1 = in1 ? a.n_contrib[pix1] : 0u;
+  uint32_t wave_last = max(lc0, lc1);
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) wave_last = max(wave_last, (uint32_t)__shfl_xor((int)wave_last, d, 64));
+
+  // upstream gradients of both pixels as the packed pairs of render_bwd_tile
+  auto load_dp = [&](bool in, size_t pix, f2& A, f2& B, f2& C, f2& D) {
+    float d[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (in) {
+      d[0] = a.dL_dcolor[pix]; d[1] = a.dL_dcolor[HW + pix]; d[2] = a.dL_dcolor[2 * HW + pix];
+      if (EXTRA) {
+        d[3] = a.dL_ddepth ? a.dL_ddepth[pix] : 0.0f;
+        d[4] = a.dL_dalpha ? a.dL_dalpha[pix] : 0.0f;
+      }
+      if (FEAT) {
+        d[5] = a.dL_dfeature[pix]; d[6] = a.dL_dfeature[HW + pix]; d[7] = a.dL_dfeature[2 * HW + pix];
+      }
+    }
+    A = mk2(d[0], d[1]);
+    B = mk2(d[2], d[3]);
+    C = mk2(d[5], d[6]);
+    D = mk2(d[7], d[4]);
+  };
+  f2 dA0, dB0, dC0, dD0, dA1, dB1, dC1, dD1;
+  load_dp(in0, pix0, dA0, dB0, dC0, dD0);
+  load_dp(in1, pix1, dA1, dB1, dC1, dD1);
+  const float bgd0 = a.bg[0] * dA0.x + a.bg[1] * dA0.y + a.bg[2] * dB0.x;
+  const float bgd1 = a.bg[0] * dA1.x + a.bg[1] * dA1.y + a.bg[2] * dB1.x;
+  const bool has_bg = a.bg[0] != 0.0f || a.bg[1] != 0.0f || a.bg[2] != 0.0f;
+  asm volatile("" ::"v"(dA0.x), "v"(dA0.y), "v"(dB0.x), "v"(dB0.y), "v"(dC0.x), "v"(dC0.y),
+               "v"(dD0.x), "v"(dD0.y));
+  asm volatile("" ::"v"(dA1.x), "v"(dA1.y), "v"(dB1.x), "v"(dB1.y), "v"(dC1.x), "v"(dC1.y),
+               "v"(dD1.x), "v"(dD1.y));
+  float acc0 = 0.f, lcd0 = 0.f, la0 = 0.f, acc1 = 0.f, lcd1 = 0.f, la1 = 0.f;
+  const float ddelx_dx = (float)(0.5 * a.W);
+  const float ddely_dy = (float)(0.5 * a.H);
+  for (int k = (int)threadIdx.x; k < kThreads2 * kAccPad; k += kThreads2) s_acc[k] = 0.0f;
+
+  // one pixel's pair update: the recurrence and (u = G dL/dalpha, w = alpha T) of render_bwd_tile
+  auto pair = [&](bool contrib, float Gv, float av, float cdot, float Tf, float bgd, float& T,
+                  float& acc, float& lcd, float& la, float& uu, float& w) {
+    const float G = contrib ? Gv : 0.0f;
+    const float alpha = contrib ? av : 0.0f;
+    {
+      const float d = 1.f - alpha;
+      const float r = __builtin_amdgcn_rcpf(d);
+      const float q = T * r;
+      T = __builtin_fmaf(__builtin_fmaf(-q, d, T), r, q);
+    }
+    w = alpha * T;
+    const float acc_new = la * lcd + (1.f - la) * acc;
+    float dL_dalpha = cdot - acc_new;
+    acc = contrib ? acc_new : acc;
+    lcd = contrib ? cdot : lcd;
+    la = contrib ? alpha : la;
+    dL_dalpha *= T;
+    if (has_bg) dL_dalpha += (-Tf / (1.f - alpha)) * bgd;
+    uu = G * dL_dalpha;
+  };
+
+  for (uint32_t done_cnt = 0; done_cnt < tile_last; done_cnt += kThreads2) {
+    __syncthreads();
+    const uint32_t cnt = min((uint32_t)kThreads2, tile_last - done_cnt);
+    if (threadIdx.x < cnt) {
+      const uint32_t rel = tile_last - 1 - done_cnt - threadIdx.x;
+      const uint32_t gid = min(a.point_list[range.x + rel], a.P - 1u);
+      s_gid[threadIdx.x] = gid;
+      const float4* rec = a.rec + 4 * (size_t)gid;
+      const float4 q0 = rec[0], q1 = rec[1], q2 = rec[2], q3 = rec[3];
+      s_r0[threadIdx.x] = q0;
+      s_r1[threadIdx.x] = make_float2(q1.x, q1.y);
+      s_mask[threadIdx.x] = (uint8_t)wave_mask(q0, q1, q3.z, tx, ty);
+      s_c0[threadIdx.x] = make_float4(q1.w, q2.x, q2.y, q1.z);
+      if (FEAT) s_c1[threadIdx.x] = make_float4(q2.z, q2.w, q3.x, 1.0f);
+    }
+    __syncthreads();
+    uint32_t nlist = 0;
+    {  // the wave's list: entries reaching either of its quadrants (w top, w + 2 bottom)
+      const uint64_t lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
+#pragma unroll
+      for (int c = 0; c < kThreads2 / 64; c++) {
+        const uint32_t j = (uint32_t)(c * 64 + lane);
+        const uint32_t m = j < cnt ? (uint32_t)s_mask[j] : 0u;
+        const bool bit = ((m >> wid) | (m >> (wid + 2))) & 1u;
+        const uint64_t b = __ballot(bit);
+        if (bit) s_list[wid][nlist + (uint32_t)__popcll(b & lt)] = (uint8_t)j;
+        nlist += (uint32_t)__popcll(b);
+      }
+    }
+    for (uint32_t k0 = 0; k0 < nlist; k0 += GROUP) {
+      const uint32_t packed = GROUP == 4 ? *reinterpret_cast<const uint32_t*>(&s_list[wid][k0])
+                                         : GROUP == 2 ? (uint32_t)*reinterpret_cast<const uint16_t*>(&s_list[wid][k0])
+                                                      : (uint32_t)s_list[wid][k0];
+      {
+        const uint32_t ulast = min((uint32_t)GROUP - 1u, nlist - 1 - k0);
+        const uint32_t jl = (packed >> (8 * ulast)) & 0xffu;
+        if (tile_last - 1 - done_cnt - jl >= wave_last) continue;  // wave-uniform
+      }
+      float G0[GROUP], G1[GROUP], a0v[GROUP], a1v[GROUP], cd0[GROUP], cd1[GROUP], dxv[GROUP];
+      float dyv[GROUP], dy1v[GROUP];
+      bool c0v[GROUP], c1v[GROUP];
+      {
+        float4 r0v[GROUP], cc0[GROUP], cc1[GROUP];
+        float2 r1v[GROUP];
+#pragma unroll
+        for (int u = 0; u < GROUP; u++) {
+          const uint32_t j = (packed >> (8 * u)) & 0xffu;
+          r0v[u] = s_r0[j];
+          r1v[u] = s_r1[j];
+          cc0[u] = s_c0[j];
+          if (FEAT) cc1[u] = s_c1[j];
+        }
+        float tdist = 1.0f;
+        float pw0[GROUP], pw1[GROUP];
+#pragma unroll
+        for (int u = 0; u < GROUP; u++) {
+          const float4 r0 = r0v[u];
+          // each pixel's offsets exactly as the forward forms them (same power, same decisions)
+          const float dx = r0.x - pfx, dy = r0.y - pfy0, dy1 = r0.y - pfy1;
+          dxv[u] = dx;
+          dyv[u] = dy;
+          dy1v[u] = dy1;
+          pw0[u] = -0.5f * (r0.z * dx * dx + r1v[u].x * dy * dy) - r0.w * dx * dy;
+          pw1[u] = -0.5f * (r0.z * dx * dx + r1v[u].x * dy1 * dy1) - r0.w * dx * dy1;
+          G0[u] = __builtin_amdgcn_exp2f(pw0[u] * 1.44269504088896341f);
+          G1[u] = __builtin_amdgcn_exp2f(pw1[u] * 1.44269504088896341f);
+          const float e0 = fabsf(r1v[u].y * G0[u] - (1.0f / 255.0f));
+          const float e1 = fabsf(r1v[u].y * G1[u] - (1.0f / 255.0f));
+          tdist = fminf(tdist, fminf(e0, e1));
+          const float4 c0 = cc0[u];
+          f2 x0 = mk2(c0.x, c0.y) * dA0, x1 = mk2(c0.x, c0.y) * dA1;
+          x0 = fma2(mk2(c0.z, EXTRA ? c0.w : 0.f), dB0, x0);
+          x1 = fma2(mk2(c0.z, EXTRA ? c0.w : 0.f), dB1, x1);
+          if (FEAT) {
+            x0 = fma2(mk2(cc1[u].x, cc1[u].y), dC0, x0);
+            x1 = fma2(mk2(cc1[u].x, cc1[u].y), dC1, x1);
+          }
+          if (EXTRA) {
+            x0 = fma2(mk2(FEAT ? cc1[u].z : 0.f, 1.0f), dD0, x0);
+            x1 = fma2(mk2(FEAT ? cc1[u].z : 0.f, 1.0f), dD1, x1);
+          }
+          cd0[u] = x0.x + x0.y;
+          cd1[u] = x1.x + x1.y;
+        }
+        if (__ballot(tdist <= 2e-6f * (1.0f / 255.0f))) {
+#pragma unroll
+          for (int u = 0; u < GROUP; u++) {
+            if (fabsf(r1v[u].y * G0[u] - (1.0f / 255.0f)) <= 2e-6f * (1.0f / 255.0f)) G0[u] = splat_exp(pw0[u]);
+            if (fabsf(r1v[u].y * G1[u] - (1.0f / 255.0f)) <= 2e-6f * (1.0f / 255.0f)) G1[u] = splat_exp(pw1[u]);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < GROUP; u++) {
+          const uint32_t j = (packed >> (8 * u)) & 0xffu;
+          const uint32_t rel = tile_last - 1 - done_cnt - j;
+          a0v[u] = fminf(0.99f, r1v[u].y * G0[u]);
+          a1v[u] = fminf(0.99f, r1v[u].y * G1[u]);
+          const bool live = k0 + u < nlist;
+          c0v[u] = live && rel < lc0 && !(pw0[u] > 0.0f) && !(a0v[u] < 1.0f / 255.0f);
+          c1v[u] = live && rel < lc1 && !(pw1[u] > 0.0f) && !(a1v[u] < 1.0f / 255.0f);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < GROUP; u++) {
+        if (__ballot(c0v[u] || c1v[u]) == 0ull) continue;  // wave-uniform
+        const uint32_t j = (packed >> (8 * u)) & 0xffu;
+        float u0, w0, u1, w1;
+        pair(c0v[u], G0[u], a0v[u], cd0[u], Tf0, bgd0, T0, acc0, lcd0, la0, u0, w0);
+        pair(c1v[u], G1[u], a1v[u], cd1[u], Tf1, bgd1, T1, acc1, lcd1, la1, u1, w1);
+        const float dx = dxv[u], dy0 = dyv[u], dy1 = dy1v[u];
+        // both pixels' terms, added in-lane, then one reduction over the wave's 128 pixels
+        const float usum = u0 + u1;
+        const float ux = u0 * dx + u1 * dx;
+        f2 g[8];
+        g[0] = mk2(ux, u0 * dy0 + u1 * dy1);
+        g[1] = mk2(ux * dx, (u0 * dx) * dy0 + (u1 * dx) * dy1);
+        g[2] = mk2((u0 * dy0) * dy0 + (u1 * dy1) * dy1, usum);
+        g[3] = w0 * dA0 + w1 * dA1;
+        g[4] = w0 * dB0 + w1 * dB1;
+        g[5] = FEAT ? w0 * dC0 + w1 * dC1 : mk2(0.f, 0.f);
+        g[6] = mk2(FEAT ? w0 * dD0.x + w1 * dD1.x : 0.f, 0.f);
+        g[7] = mk2(dx, dy0);
+        const float sum = wave_reduce16_dpp(g, lane);
+        if (red_lane && sum != 0.0f) atomicAdd(&s_acc[j * kAccPad + red_slot], sum);
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x < cnt) {
+      const float4 r0 = s_r0[threadIdx.x];
+      const float2 r1 = s_r1[threadIdx.x];
+      float* row = s_acc + threadIdx.x * kAccPad;
+      const float sx = row[kAccMx], sy = row[kAccMy];
+      const float o = r1.y;
+      row[kAccMx] = -(o * (r0.z * sx + r0.w * sy)) * ddelx_dx;
+      row[kAccMy] = -(o * (r1.x * sy + r0.w * sx)) * ddely_dy;
+      row[kAccCa] = (-0.5f * o) * row[kAccCa];
+      row[kAccCb] = (-0.5f * o) * row[kAccCb];
+      row[kAccCc] = (-0.5f * o) * row[kAccCc];
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int it = 0; it < kThreads2 * kAccFloats / kThreads2; it++) {
+      const uint32_t jj = (uint32_t)it * (kThreads2 / kAccFloats) + (threadIdx.x >> 4);
+      const int k = (int)(threadIdx.x & 15);
+      if (jj < cnt) {
+        const float v = s_acc[jj * kAccPad + k];
+        if (v != 0.0f) {
+          atomicAdd(&a.acc[(size_t)s_gid[jj] * kAccFloats + k], v);
+          s_acc[jj * kAccPad + k] = 0.0f;
+        }
+      }
+    }
+  }
+}
+
+template <bool EXTRA, bool FEAT, int GROUP>
+__global__ __launch_bounds__(kThreads2) void render_bwd2_views_kernel(RenderBwdViews m) {
+  const uint32_t b = blockIdx.x;
+  int k = 0;
+  while (k + 1 < m.V && b >= m.first[k + 1]) k++;  // workgroup-uniform
+  render_bwd_tile2<EXTRA, FEAT, GROUP>(m.v[k], b - m.first[k]);
+}
+
+// GSR_BWD_PIX2 (default 0): the two-pixels-per-lane backward above; its list group size
+static int bwd_pix2() {
+  static const int g = [] {
+    const char* e = getenv("GSR_BWD_PIX2");
+    const int v = e ? atoi(e) : 0;
+    return (v == 1 || v == 2 || v == 4) ? v : 0;
+  }();
+  return g;
+}
+
 // GSR_BWD_PIPE (default 1): the pipelined wave reduction of render_bwd_tile
 static bool bwd_pipe() {
   static const bool on = [] {
@@ -1364,6 +1638,22 @@ hipError_t launch_render_backward_views(const RenderBwdArgs* views, int V, hipSt
   }
   const uint32_t nblk = m.first[V];
   if (nblk == 0) return hipSuccess;
+  if (bwd_pix2() && !a.partial && a.sched == 2) {  // the two-pixels-per-lane variant (A/B)
+#define GSR_BWD2(E, F)                                                                            \
+    do {                                                                                           \
+      if (bwd_pix2() == 4)                                                                         \
+        hipLaunchKernelGGL((render_bwd2_views_kernel<E, F, 4>), dim3(nblk), dim3(kThreads2), 0, s, m); \
+      else if (bwd_pix2() == 2)                                                                    \
+        hipLaunchKernelGGL((render_bwd2_views_kernel<E, F, 2>), dim3(nblk), dim3(kThreads2), 0, s, m); \
+      else                                                                                         \
+        hipLaunchKernelGGL((render_bwd2_views_kernel<E, F, 1>), dim3(nblk), dim3(kThreads2), 0, s, m); \
+    } while (0)
+    if (feat) GSR_BWD2(true, true);
+    else if (extra) GSR_BWD2(true, false);
+    else GSR_BWD2(false, false);
+#undef GSR_BWD2
+    return hipGetLastError();
+  }
 #define GSR_BWDV(E, F)                                                                            \
   do {                                                                                           \
     if (a.partial && a.det)                                                                      \
