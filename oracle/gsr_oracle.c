@@ -652,6 +652,16 @@ static void blend_fwd_rows(void* ctx, long lo, long hi, int chunk) {
         }
 }
 
+/* oracle_use_lists: the next oracle_forward on this thread takes these instance lists instead of
+ * binning itself (the float64 build run on the float32 build's lists, so that both blend the
+ * same instances in the same order even where a radius rounds to another integer). */
+static _Thread_local struct { const unsigned *point_list, *ranges; int R; } g_lists;
+void oracle_use_lists(const unsigned* point_list, int R, const unsigned* ranges) {
+    g_lists.point_list = point_list;
+    g_lists.R = R;
+    g_lists.ranges = ranges;
+}
+
 oracle_state* oracle_forward(int P, int M, const float* background, const float* means3D,
                              const float* colors_precomp, const float* opacities,
                              const float* scales, const float* rotations, float scale_modifier,
@@ -709,6 +719,18 @@ oracle_state* oracle_forward(int P, int M, const float* background, const float*
     if (radii_out) memcpy(radii_out, st->radii, sizeof(int) * (size_t)P);
 
     /* ---- scan + duplicateWithKeys + stable SortPairs, rasterizer_impl.cu:70-111, 277-308 ---- */
+    const unsigned ntiles = gx * gy;
+    if (g_lists.point_list) { /* oracle_use_lists: another evaluation's binning, as given */
+        const int R = g_lists.R;
+        st->R = R;
+        st->point_list = (unsigned*)xcalloc((size_t)R, sizeof(unsigned));
+        memcpy(st->point_list, g_lists.point_list, sizeof(unsigned) * (size_t)R);
+        st->ranges = (unsigned*)xcalloc((size_t)ntiles * 2, sizeof(unsigned));
+        memcpy(st->ranges, g_lists.ranges, sizeof(unsigned) * 2 * (size_t)ntiles);
+        if (num_rendered) *num_rendered = R;
+        goto blend;
+    }
+    {
     uint64_t R64 = 0;
     for (int i = 0; i < P; i++) R64 += st->tiles_touched[i];
     int R = (int)R64;
@@ -738,7 +760,6 @@ oracle_state* oracle_forward(int P, int M, const float* background, const float*
     st->point_list = (unsigned*)xcalloc((size_t)R, sizeof(unsigned));
     for (int i = 0; i < R; i++) st->point_list[i] = inst[i].val;
     /* identifyTileRanges, rasterizer_impl.cu:116-138 (ranges zeroed first, :310) */
-    const unsigned ntiles = gx * gy;
     st->ranges = (unsigned*)xcalloc((size_t)ntiles * 2, sizeof(unsigned));
     for (int i = 0; i < R; i++) {
         unsigned cur = (unsigned)(inst[i].key >> 32);
@@ -754,7 +775,9 @@ oracle_state* oracle_forward(int P, int M, const float* background, const float*
     }
     free(inst);
     if (num_rendered) *num_rendered = R;
+    }
 
+blend:
     /* ---- renderCUDA (fwd), forward.cu:261-374, extended to NCH channels ---- */
     st->final_T = (real*)xcalloc((size_t)W * H, sizeof(real));
     st->n_contrib = (unsigned*)xcalloc((size_t)W * H, sizeof(unsigned));

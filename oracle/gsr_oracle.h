@@ -120,6 +120,11 @@ int oracle_backward_rows(oracle_state* st, const oreal* rows, oreal* dL_dmeans2D
                          oreal* dL_drotations, oreal* dL_dsh_language,
                          oreal* dL_dlanguage_feature);
 
+/* The next oracle_forward on the calling thread uses these instance lists (point_list [R],
+ * ranges [tiles*2], as oracle_get_point_list / _ranges return them) instead of binning; NULL
+ * point_list = bin normally again.  Test diagnostic: the float64 build on the float32 lists. */
+void oracle_use_lists(const unsigned* point_list, int R, const unsigned* ranges);
+
 void oracle_free(oracle_state* st);
 
 int oracle_mark_visible(int P, const float* means3D, const float* viewmatrix,

@@ -53,6 +53,8 @@ def lib(variant: str = "f32"):
         L.oracle_backward_rows.argtypes = [_p] * 12
         L.oracle_free.restype = None
         L.oracle_free.argtypes = [_p]
+        L.oracle_use_lists.restype = None
+        L.oracle_use_lists.argtypes = [_p, _i, _p]
         L.oracle_mark_visible.restype = _i
         L.oracle_mark_visible.argtypes = [_i, _p, _p, _p, _p]
         L.oracle_splat_exp.restype = None
@@ -98,13 +100,14 @@ def _ptr(a):
 class OracleRaster:
     """One forward (+ optional backward) of the restated rasterizer on host arrays.  variant:
     "f32" (the checker), "f64" (the same restatement in float64: images and gradients come back
-    as float64) or "expf" (float32 with libm's expf as the blend exp)."""
+    as float64) or "expf" (float32 with libm's expf as the blend exp).  lists=(point_list, ranges)
+    skips the binning and blends those instance lists (another raster's point_list() / ranges())."""
 
     def __init__(self, *, variant="f32", means3D, opacities, viewmatrix, projmatrix, campos, tanfovx, tanfovy,
                  image_height, image_width, bg, scale_modifier=1.0, sh_degree=0, shs=None,
                  colors_precomp=None, scales=None, rotations=None, cov3D_precomp=None,
                  shs_language=None, language_feature_precomp=None, confidence=None,
-                 include_feature=True, prefiltered=False):
+                 include_feature=True, prefiltered=False, lists=None):
         L = lib(variant)
         self.variant = variant
         self._L = L
@@ -136,7 +139,14 @@ class OracleRaster:
         self.feature = np.zeros((3, H, W), od)
         self.radii = np.zeros((P,), np.int32)
         nr = _i(0)
-        self._st = L.oracle_forward(
+        if lists is not None:
+            k["pl"] = np.ascontiguousarray(lists[0], np.uint32)
+            k["rg"] = np.ascontiguousarray(lists[1], np.uint32)
+            if k["rg"].size != 2 * ((W + 15) // 16) * ((H + 15) // 16):
+                raise ValueError("lists: ranges must hold two entries per tile")
+            L.oracle_use_lists(_ptr(k["pl"]), int(k["pl"].size), _ptr(k["rg"]))
+        try:
+            self._st = L.oracle_forward(
             P, M, _ptr(k["bg"]), _ptr(k["means3D"]), _ptr(k["colors"]), _ptr(k["opac"]),
             _ptr(k["scales"]), _ptr(k["rot"]), float(scale_modifier), _ptr(k["cov"]),
             _ptr(k["view"]), _ptr(k["proj"]), float(tanfovx), float(tanfovy), H, W,
@@ -144,6 +154,9 @@ class OracleRaster:
             _ptr(k["shl"]), _ptr(k["lfp"]), _ptr(k["conf"]), int(bool(include_feature)),
             _ptr(self.color), _ptr(self.depth), _ptr(self.alpha), _ptr(self.feature),
             _ptr(self.radii), ctypes.byref(nr))
+        finally:
+            if lists is not None:
+                L.oracle_use_lists(None, 0, None)
         if not self._st:
             raise RuntimeError("oracle_forward rejected its arguments")
         self.num_rendered = int(nr.value)

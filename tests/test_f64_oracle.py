@@ -72,6 +72,13 @@ def test_f32_oracle_within_rounding_scale_of_f64():
     # negative control: the colour terms off by 1e-4 (the image's upstream gradient scaled)
     gd = (grads[0] * (1.0 + 1e-4), grads[1], grads[2])
     _, g64d, _ = run_f64_path(inp, cams, gd, bound=False)
+    # the float64 build can blend the float32 build's lists: same lists back, same images
+    lists = [(v["point_list"], v["ranges"]) for v in vo]
+    v64l, _, _ = run_f64_path(inp, cams, grads, bound=False, lists=lists)
+    for a, b in zip(v64l, v64):
+        assert np.array_equal(a["point_list"], b["point_list"])
+        assert np.array_equal(a["ranges"], b["ranges"])
+        assert np.array_equal(a["render"], b["render"])
     st = rounding_stats(go["_features_dc"], go["_features_dc"], g64d["_features_dc"],
                         B["_features_dc"], exclude=hit, C=8.0)
     assert st["f32_fail"] > 0.05 * st["n_big"], st

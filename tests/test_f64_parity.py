@@ -71,7 +71,8 @@ def test_gradients_within_float32_rounding_of_f64(case):
     print(f"[{case}] f32 oracle done", flush=True)
     inp = oracle_inputs(m, act)
     del m
-    v64, g64, B = run_f64_path(inp, cams, grads,
+    lists = [(v["point_list"], v["ranges"]) for v in vo]  # f64 blends the f32 binning's lists
+    v64, g64, B = run_f64_path(inp, cams, grads, lists=lists,
                                progress=lambda s: print(f"[{case}] {s}", flush=True))
     # Gaussians behind a pixel whose blend decisions differ (GPU vs f32, f32 vs f64) see a
     # different set of terms: left out of the entry-wise statistics (counted)
@@ -83,6 +84,7 @@ def test_gradients_within_float32_rounding_of_f64(case):
         f64flip = decision_flips(d, b)  # f32 vs f64: decisions (images differ by rounding ~1e-5)
         nflip64 += int(f64flip.sum())
         hit |= flip_gaussians(b, off | f64flip, P)
+        hit |= d["radii"] != b["radii"]  # a radius rounded to another integer in float64
         assert np.array_equal(a["radii"], b["radii"]), case
     rec = {"case": case, "gaussians_excluded": int(hit.sum()), "f64_decision_flips": nflip64,
            "C": C_BOUND, "grads": {}}
@@ -104,7 +106,7 @@ def test_gradients_within_float32_rounding_of_f64(case):
         # negative control: a 1e-4 systematic error in the colour terms (the image's upstream
         # gradient scaled) is caught by the same bound
         gd = (grads[0] * (1.0 + 1e-4), grads[1], grads[2])
-        _, g64d, _ = run_f64_path(inp, cams, gd, bound=False)
+        _, g64d, _ = run_f64_path(inp, cams, gd, bound=False, lists=lists)
         st = rounding_stats(gg["_features_dc"], go["_features_dc"], g64d["_features_dc"],
                             B["_features_dc"], exclude=hit, C=C_BOUND)
         assert st["gpu_fail"] > 0.05 * st["n_big"], st
