@@ -463,6 +463,60 @@ __device__ __forceinline__ int reduce16_slot(int lane, SwapOrient o) {
   return b5 * 8 + b4 * 4 + ((lane >> 3) & 1) * 2 + ((lane >> 2) & 1);
 }
 
+// Joint halving butterfly of FOUR entries' 16 values (GSR_BWD_PIPE=2): 64 values per lane, one
+// fully reduced value per lane on exit -- entry e = 2 b5' + b4' (the probed swap orientation, as
+// reduce16_slot), slot k = lane & 15.  permlane32_swap pairs entries (0, 2) and (1, 3),
+// permlane16_swap then (0|2, 1|3); the rest is the 16-lane row's four halving DPP stages (l^15,
+// l^7, l^2, l^1: linearly independent over the low lane bits, so every lane of the row is summed
+// once).  Same instruction count per entry as wave_reduce16_dpp, four times the independent work
+// per stage, and one LDS add per lane for the four entries.
+__device__ __forceinline__ float wave_reduce_joint4(f2 (&v)[4][8], int lane) {
+  f2 r0[8], r1[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    r0[i] = swap32_add(v[0][i], v[2][i]);
+    r1[i] = swap32_add(v[1][i], v[3][i]);
+  }
+  f2 s[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) s[i] = swap16_add(r0[i], r1[i]);
+  f2 w[4];
+  {
+    const bool hi = lane & 8;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const f2 send = hi ? s[i] : s[i + 4];
+      const f2 keep = hi ? s[i + 4] : s[i];
+      w[i] = keep + mk2(dpp<0x140>(send.x), dpp<0x140>(send.y));  // row_mirror
+    }
+  }
+  f2 x[2];
+  {
+    const bool hi = lane & 4;
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+      const f2 send = hi ? w[i] : w[i + 2];
+      const f2 keep = hi ? w[i + 2] : w[i];
+      x[i] = keep + mk2(dpp<0x141>(send.x), dpp<0x141>(send.y));  // row_half_mirror
+    }
+  }
+  f2 y;
+  {
+    const bool hi = lane & 2;
+    const f2 send = hi ? x[0] : x[1];
+    const f2 keep = hi ? x[1] : x[0];
+    y = keep + mk2(dpp<0x4E>(send.x), dpp<0x4E>(send.y));  // quad_perm [2,3,0,1]
+  }
+  const bool hi = lane & 1;
+  const float send = hi ? y.x : y.y;
+  const float keep = hi ? y.y : y.x;
+  return keep + dpp<0xB1>(send);  // quad_perm [1,0,3,2]
+}
+
+__device__ __forceinline__ int joint4_entry(int lane, SwapOrient o) {
+  return (((lane >> 5) & 1) ^ (int)o.flip32) * 2 + (((lane >> 4) & 1) ^ (int)o.flip16);
+}
+
 // Deterministic variant (DET, gsr.h debug bit 1): no float atomics.  Every wave stores its
 // butterfly sums into its OWN accumulator rows (each batch entry is in a wave's list at most
 // once), the four waves' rows are added in wave order, and each (splat, tile) row is stored to
@@ -477,7 +531,7 @@ constexpr int kAccDet = 13;
 // -- and the backward preprocess sums each Gaussian's rows.  DET implies ROWS.
 // One tile of the backward blend: workgroup `blk` of the view described by `a` (render_bwd_kernel:
 // one view per launch; render_bwd_views_kernel: the tiles of several views in one launch).
-// 4 waves per SIMD (128 VGPRs): the pipelined variant holds one pending entry more
+// 4 waves per SIMD (128 VGPRs): the pipelined variants hold pending entries
 #define GSR_BWD_WAVES(PIPE) __attribute__((amdgpu_waves_per_eu((PIPE) ? 4 : 1)))
 // PIPE (GSR_BWD_PIPE, round 4): the wave reduction of a contributing entry is issued together
 // with the next contributing entry's recurrence, in one basic block -- the two are independent
@@ -486,10 +540,14 @@ constexpr int kAccDet = 13;
 // instead of serialising behind it.  The last entry of a batch is reduced before the batch's
 // barrier.  Same values, same LDS adds: results equal to the unpipelined kernel up to the order
 // of the LDS float adds (as between waves already).
-template <bool EXTRA, bool FEAT, int GROUP, bool DET, bool ROWS, bool PIPE>
+// PIPE == 2 (GSR_BWD_PIPE=2, round 4): the group's contributing entries keep their (u, w, d) and
+// the group ends in ONE joint reduction of its four entries (wave_reduce_joint4; entries without
+// a contributing lane are zeros) -- the butterfly's dependent stages carry four entries' work.
+template <bool EXTRA, bool FEAT, int GROUP, bool DET, bool ROWS, int PIPE>
 __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t blk) {
   static_assert(!DET || ROWS, "the deterministic backward stores per-instance rows");
   static_assert(!(PIPE && DET), "the pipelined reduction is a default-mode kernel");
+  static_assert(PIPE != 2 || GROUP == 4, "the joint reduction takes a group of four entries");
   // the batch's records in LDS, regrouped so that the colour dot product's packed FMAs read
   // register pairs straight from the loads: s_r0 = {x, y, conic.a, conic.b}, s_r1 = {conic.c,
   // opacity}, s_c0 = {r, g, b, depth}, s_c1 = {f0, f1, f2, 1} (alpha channel)
@@ -514,6 +572,7 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
   // the lanes that hold a reduced gradient value (one of the four per value, value < kAccDet)
   const int red_slot = reduce16_slot(lane, swap_orient);
   const bool red_lane = (lane & 3) == 0 && red_slot < kAccDet;
+  const int j4_shift = 8 * joint4_entry(lane, swap_orient);  // PIPE == 2: this lane's entry's byte
   const uint32_t ntiles = a.gx * a.gy;
   const uint32_t tile = sched_tile(blk, ntiles, a.sched, a.order);
   const uint32_t tx = tile % a.gx, ty = tile / a.gx;
@@ -730,6 +789,16 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
                 !(av[u] < 1.0f / 255.0f);
       }
     }
+    // PIPE == 2: the group's entries for the joint reduction (zeros unless contributing)
+    float q_uu[GROUP], q_w[GROUP];
+    f2 q_d[GROUP];
+    bool q_any = false;
+#pragma unroll
+    for (int u = 0; u < GROUP; u++) {
+      q_uu[u] = 0.0f;
+      q_w[u] = 0.0f;
+      q_d[u] = mk2(0.f, 0.f);
+    }
 #pragma unroll
     for (int u = 0; u < GROUP; u++) {
       const bool contrib = cv[u];
@@ -790,7 +859,14 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
       //   dL/dconic.{x,y,w} = -1/2 o sum u {dx dx, dx dy, dy dy},   dL/dopacity = sum u
       // The per-splat constants (a, b, c, o) are applied once per (splat, tile) at the flush.
       const float uu = G * dL_dalpha;
-      if (PIPE) {
+      if (PIPE == 2) {
+        q_uu[u] = uu;
+        q_w[u] = dchannel_dcolor;
+        q_d[u] = dxy;
+        q_any = true;
+        continue;
+      }
+      if (PIPE == 1) {
         // the previous contributing entry's reduction, beside this entry's recurrence
         f2 g[8];
         pair_terms(p_uu, p_w, slot_dxy(p_j), g);
@@ -818,8 +894,17 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
       }
 #endif
     }
+    if constexpr (PIPE == 2) if (q_any) {  // wave-uniform
+      f2 g[4][8];
+#pragma unroll
+      for (int u = 0; u < 4; u++) pair_terms(q_uu[u], q_w[u], q_d[u], g[u]);
+      const float sum = wave_reduce_joint4(g, lane);
+      const int k = lane & 15;
+      if (k < kAccDet && sum != 0.0f)
+        atomicAdd(&s_acc[((packed >> j4_shift) & 0xffu) * kAccPad + k], sum);
     }
-    if (PIPE) {  // the batch's last contributing entry
+    }
+    if (PIPE == 1) {  // the batch's last contributing entry
       f2 g[8];
       pair_terms(p_uu, p_w, slot_dxy(p_j), g);
       reduce_add(g, p_j);
@@ -901,7 +986,7 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
   }
 }
 
-template <bool EXTRA, bool FEAT, int GROUP, bool DET, bool ROWS, bool PIPE>
+template <bool EXTRA, bool FEAT, int GROUP, bool DET, bool ROWS, int PIPE>
 __global__ __launch_bounds__(kThreads) GSR_BWD_WAVES(PIPE) void render_bwd_kernel(RenderBwdArgs a) {
   render_bwd_tile<EXTRA, FEAT, GROUP, DET, ROWS, PIPE>(a, blockIdx.x);
 }
@@ -910,7 +995,7 @@ __global__ __launch_bounds__(kThreads) GSR_BWD_WAVES(PIPE) void render_bwd_kerne
 // with first[k] <= b < first[k + 1] (view-major; inside a view the forward's heaviest-first tile
 // order), so the views' launches do not each end in a tail of idle CUs, and one launch's duration
 // is the time of all its views' blends.
-template <bool EXTRA, bool FEAT, int GROUP, bool DET, bool ROWS, bool PIPE>
+template <bool EXTRA, bool FEAT, int GROUP, bool DET, bool ROWS, int PIPE>
 __global__ __launch_bounds__(kThreads) GSR_BWD_WAVES(PIPE) void render_bwd_views_kernel(RenderBwdViews m) {
   const uint32_t b = blockIdx.x;
   int k = 0;
@@ -1192,13 +1277,15 @@ static int bwd_pix2() {
   return g;
 }
 
-// GSR_BWD_PIPE (default 1): the pipelined wave reduction of render_bwd_tile
-static bool bwd_pipe() {
-  static const bool on = [] {
+// GSR_BWD_PIPE (default 1): the pipelined wave reduction of render_bwd_tile (1), the joint
+// reduction of a group's four entries (2), or neither (0)
+static int bwd_pipe() {
+  static const int mode = [] {
     const char* e = getenv("GSR_BWD_PIPE");
-    return !(e && atoi(e) == 0);
+    const int v = e ? atoi(e) : 1;
+    return (v == 0 || v == 2) ? v : 1;
   }();
-  return on;
+  return mode;
 }
 
 // ================================================================================================
@@ -1657,13 +1744,15 @@ hipError_t launch_render_backward_views(const RenderBwdArgs* views, int V, hipSt
 #define GSR_BWDV(E, F)                                                                            \
   do {                                                                                           \
     if (a.partial && a.det)                                                                      \
-      hipLaunchKernelGGL((render_bwd_views_kernel<E, F, 4, true, true, false>), dim3(nblk), dim3(kThreads), 0, s, m); \
+      hipLaunchKernelGGL((render_bwd_views_kernel<E, F, 4, true, true, 0>), dim3(nblk), dim3(kThreads), 0, s, m); \
     else if (a.partial)                                                                          \
-      hipLaunchKernelGGL((render_bwd_views_kernel<E, F, 4, false, true, false>), dim3(nblk), dim3(kThreads), 0, s, m); \
-    else if (bwd_pipe())                                                                         \
-      hipLaunchKernelGGL((render_bwd_views_kernel<E, F, 4, false, false, true>), dim3(nblk), dim3(kThreads), 0, s, m); \
+      hipLaunchKernelGGL((render_bwd_views_kernel<E, F, 4, false, true, 0>), dim3(nblk), dim3(kThreads), 0, s, m); \
+    else if (bwd_pipe() == 2)                                                                    \
+      hipLaunchKernelGGL((render_bwd_views_kernel<E, F, 4, false, false, 2>), dim3(nblk), dim3(kThreads), 0, s, m); \
+    else if (bwd_pipe() == 1)                                                                    \
+      hipLaunchKernelGGL((render_bwd_views_kernel<E, F, 4, false, false, 1>), dim3(nblk), dim3(kThreads), 0, s, m); \
     else                                                                                         \
-      hipLaunchKernelGGL((render_bwd_views_kernel<E, F, 4, false, false, false>), dim3(nblk), dim3(kThreads), 0, s, m); \
+      hipLaunchKernelGGL((render_bwd_views_kernel<E, F, 4, false, false, 0>), dim3(nblk), dim3(kThreads), 0, s, m); \
   } while (0)
   if (feat) GSR_BWDV(true, true);
   else if (extra) GSR_BWDV(true, false);
@@ -1695,15 +1784,17 @@ hipError_t launch_render_backward(const RenderBwdArgs& a, hipStream_t s) {
 #define GSR_BWD(E, F)                                                                             \
   do {                                                                                           \
     if (a.partial && a.det)                                                                      \
-      hipLaunchKernelGGL((render_bwd_kernel<E, F, 4, true, true, false>), dim3(ntiles), dim3(kThreads), 0, s, a); \
+      hipLaunchKernelGGL((render_bwd_kernel<E, F, 4, true, true, 0>), dim3(ntiles), dim3(kThreads), 0, s, a); \
     else if (a.partial)                                                                          \
-      hipLaunchKernelGGL((render_bwd_kernel<E, F, 4, false, true, false>), dim3(ntiles), dim3(kThreads), 0, s, a); \
+      hipLaunchKernelGGL((render_bwd_kernel<E, F, 4, false, true, 0>), dim3(ntiles), dim3(kThreads), 0, s, a); \
     else if (group == 1)                                                                         \
-      hipLaunchKernelGGL((render_bwd_kernel<E, F, 1, false, false, false>), dim3(ntiles), dim3(kThreads), 0, s, a); \
-    else if (bwd_pipe())                                                                         \
-      hipLaunchKernelGGL((render_bwd_kernel<E, F, 4, false, false, true>), dim3(ntiles), dim3(kThreads), 0, s, a); \
+      hipLaunchKernelGGL((render_bwd_kernel<E, F, 1, false, false, 0>), dim3(ntiles), dim3(kThreads), 0, s, a); \
+    else if (bwd_pipe() == 2)                                                                    \
+      hipLaunchKernelGGL((render_bwd_kernel<E, F, 4, false, false, 2>), dim3(ntiles), dim3(kThreads), 0, s, a); \
+    else if (bwd_pipe() == 1)                                                                    \
+      hipLaunchKernelGGL((render_bwd_kernel<E, F, 4, false, false, 1>), dim3(ntiles), dim3(kThreads), 0, s, a); \
     else                                                                                         \
-      hipLaunchKernelGGL((render_bwd_kernel<E, F, 4, false, false, false>), dim3(ntiles), dim3(kThreads), 0, s, a); \
+      hipLaunchKernelGGL((render_bwd_kernel<E, F, 4, false, false, 0>), dim3(ntiles), dim3(kThreads), 0, s, a); \
   } while (0)
   if (feat) GSR_BWD(true, true);
   else if (extra) GSR_BWD(true, false);
