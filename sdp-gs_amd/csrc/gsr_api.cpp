@@ -37,6 +37,7 @@ GeomState carve_geom(char* base, size_t P) {
   g.clamped = c.take<uint8_t>(P);
   g.radii = c.take<int32_t>(P);
   g.rec = c.take<float4>(4 * P);
+  g.drec = c.take<float4>(2 * P);
   g.tiles_touched = c.take<uint32_t>(P);
   g.offsets = c.take<uint32_t>(P);
   g.acc = c.take<float>((size_t)kAccFloats * P);
@@ -558,10 +559,12 @@ static int fwd_begin(const FwdModel& m, FwdCam& c) {
 
   bool in_b = false;
   PROF_BEGIN(DEPTH_SORT);
-  // the last pass writes each Gaussian's tile count in place of its sorted key
+  // the last pass writes each Gaussian's tile count in place of its sorted key (and, GSR_DUP_DREC,
+  // its binning record in depth order for the duplication)
   GSR_CHECK(radix_sort_pairs(g.dkey_a, g.dval_a, g.dkey_b, g.dval_b, (size_t)P, 32,
                              g.sort, &in_b, stream, /*sentinel_anywhere=*/true,
-                             /*precleared=*/true, /*key_payload=*/g.tiles_touched));
+                             /*precleared=*/true, /*key_payload=*/g.tiles_touched,
+                             dup_drec() ? g.rec : nullptr, dup_drec() ? g.drec : nullptr));
   PROF_END(DEPTH_SORT);
   c.depth_in_b = in_b;
   const uint32_t* counts_sorted = in_b ? g.dkey_b : g.dkey_a;
@@ -648,7 +651,8 @@ static int fwd_bin(const FwdModel& m, FwdCam& c) {
   GSR_CHECK(launch_duplicate(P, order, g.offsets, c.radii_ptr, g.rec, c.gx, c.gy, b.tkey_a, b.tval_a,
                              (uint32_t)R, SideClear{b.sort.aux, sort_clear_bytes(b.sort, R, tbits)},
                              SideClear{im.ranges, sizeof(uint2) * ntiles}, stream,
-                             m.rows ? b.egid : nullptr, m.rows ? g.ebeg : nullptr));
+                             m.rows ? b.egid : nullptr, m.rows ? g.ebeg : nullptr,
+                             dup_drec() ? g.drec : nullptr));
   PROF_END(DUPLICATE);
   bool t_in_b = false;
   PROF_BEGIN(TILE_SORT);
@@ -1310,7 +1314,8 @@ int views_forward_batched(const FwdModel& m, std::vector<FwdCam>& cams, gsr_view
       }
       sums[l] = SumSpec{g.pre_parts, g.pre_parts + pre_blocks, pre_blocks, g.flags + 1, c.host_dev,
                         m.prefiltered ? g.flags : nullptr};
-      ds[l] = SortSpec{g.dkey_a, g.dval_a, g.dkey_b, g.dval_b, (size_t)P, g.sort, g.tiles_touched};
+      ds[l] = SortSpec{g.dkey_a, g.dval_a, g.dkey_b, g.dval_b, (size_t)P, g.sort, g.tiles_touched,
+                       dup_drec() ? g.rec : nullptr, dup_drec() ? g.drec : nullptr};
       G.live.push_back(v);
     }
     const int nl = (int)G.live.size();
@@ -1389,7 +1394,8 @@ int views_forward_batched(const FwdModel& m, std::vector<FwdCam>& cams, gsr_view
                          b.tkey_a, b.tval_a, R,
                          SideClear{b.sort.aux, sort_clear_bytes(b.sort, R, tbits)},
                          SideClear{c.im.ranges, sizeof(uint2) * ntiles},
-                         m.rows ? b.egid : nullptr, m.rows ? g.ebeg : nullptr};
+                         m.rows ? b.egid : nullptr, m.rows ? g.ebeg : nullptr,
+                         dup_drec() ? g.drec : nullptr};
         ts[l] = SortSpec{b.tkey_a, b.tval_a, b.tkey_b, b.tval_b, (size_t)R, b.sort, nullptr};
       }
       PROF_BEGIN(DUPLICATE);

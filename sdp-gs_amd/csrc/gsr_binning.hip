@@ -45,7 +45,7 @@ __device__ __forceinline__ void duplicate_body_lds(int P, const uint32_t* __rest
                                                    SideClear clear0, SideClear clear1,
                                                    uint32_t* __restrict__ egid,
                                                    uint32_t* __restrict__ ebeg, uint32_t blk,
-                                                   uint32_t nblk) {
+                                                   uint32_t nblk, const float4* __restrict__ drec) {
   constexpr int kWin = GSR_DUP_WIN;  // instances per wave window
   __shared__ uint32_t s_key[kThreads / 64][kWin];
   __shared__ uint32_t s_val[kThreads / 64][kWin];
@@ -67,14 +67,29 @@ __device__ __forceinline__ void duplicate_body_lds(int P, const uint32_t* __rest
   uint32_t gid = 0, y = 0, y1 = 0, x0 = 0, x1 = 0, x = 0, xe = 0;
   SplatCut cut{};
   if (off < end) {
-    gid = min(order[s], (uint32_t)P - 1u);
-    const float4 r0 = rec[4 * (size_t)gid];
-    const float4 r1 = rec[4 * (size_t)gid + 1];
-    const float4 r3 = rec[4 * (size_t)gid + 3];
+    float4 r0;
+    float qc, rad;
+    float cc;
+    if (drec) {  // the depth sort's binning record of this position: no gather
+      r0 = drec[2 * (size_t)s];
+      const float4 b = drec[2 * (size_t)s + 1];  // {conic.c, q_cut, radius, id}
+      gid = min(__float_as_uint(b.w), (uint32_t)P - 1u);
+      cc = b.x;
+      qc = b.y;
+      rad = b.z;
+    } else {
+      gid = min(order[s], (uint32_t)P - 1u);
+      r0 = rec[4 * (size_t)gid];
+      const float4 r1 = rec[4 * (size_t)gid + 1];
+      const float4 r3 = rec[4 * (size_t)gid + 3];
+      cc = r1.x;
+      qc = r3.z;
+      rad = r3.y;
+    }
     if (egid) ebeg[gid] = off;
     uint32_t y0;
-    tile_rect(r0.x, r0.y, (int)r3.y, gx, gy, x0, y0, x1, y1);
-    cut = make_cut(r0.x, r0.y, r0.z, r0.w, r1.x, r3.z);
+    tile_rect(r0.x, r0.y, (int)rad, gx, gy, x0, y0, x1, y1);
+    cut = make_cut(r0.x, r0.y, r0.z, r0.w, cc, qc);
     y = y0;
     if (y < y1) cut_row_range(cut, y, x0, x1, x, xe);
     else off = end;
@@ -119,10 +134,10 @@ __device__ __forceinline__ void duplicate_body(int P, const uint32_t* __restrict
                                                SideClear clear0, SideClear clear1,
                                                uint32_t* __restrict__ egid,
                                                uint32_t* __restrict__ ebeg, uint32_t blk,
-                                               uint32_t nblk) {
-  if (GSR_DUP_LDS) {
+                                               uint32_t nblk, const float4* __restrict__ drec) {
+  if (GSR_DUP_LDS || drec) {
     duplicate_body_lds(P, order, offsets, rec, gx, gy, tkey, tval, R, clear0, clear1, egid, ebeg,
-                       blk, nblk);
+                       blk, nblk, drec);
     return;
   }
   const int s = (int)(blk * kThreads + threadIdx.x);
@@ -172,9 +187,10 @@ __global__ __launch_bounds__(kThreads) void duplicate_kernel(int P,
                                                              uint32_t R, SideClear clear0,
                                                              SideClear clear1,
                                                              uint32_t* __restrict__ egid,
-                                                             uint32_t* __restrict__ ebeg) {
+                                                             uint32_t* __restrict__ ebeg,
+                                                             const float4* __restrict__ drec) {
   duplicate_body(P, order, offsets, rec, gx, gy, tkey, tval, R, clear0, clear1, egid, ebeg,
-                 blockIdx.x, gridDim.x);
+                 blockIdx.x, gridDim.x, drec);
 }
 
 // Instances per lane of the ranges kernel: consecutive keys, one 16-B load when aligned (one
@@ -269,7 +285,8 @@ __global__ __launch_bounds__(kThreads) void duplicate_views_kernel(DupViews m) {
   const int k = batch_view(m.first, m.V, blockIdx.x);
   const DupSpec& j = m.j[k];
   duplicate_body(j.P, j.order, j.offsets, j.rec, j.gx, j.gy, j.tkey, j.tval, j.R, j.clear0,
-                 j.clear1, j.egid, j.ebeg, blockIdx.x - m.first[k], m.first[k + 1] - m.first[k]);
+                 j.clear1, j.egid, j.ebeg, blockIdx.x - m.first[k], m.first[k + 1] - m.first[k],
+                 j.drec);
 }
 
 __global__ __launch_bounds__(kThreads) void tile_ranges_views_kernel(RangesViews m) {
@@ -300,11 +317,21 @@ hipError_t launch_det_gather(size_t R, const uint32_t* einst, const uint32_t* eg
 hipError_t launch_duplicate(int P, const uint32_t* order, const uint32_t* offsets,
                             const int32_t* radii, const float4* rec, uint32_t gx, uint32_t gy,
                             uint32_t* tkey, uint32_t* tval, uint32_t R, SideClear clear0,
-                            SideClear clear1, hipStream_t s, uint32_t* egid, uint32_t* ebeg) {
+                            SideClear clear1, hipStream_t s, uint32_t* egid, uint32_t* ebeg,
+                            const float4* drec) {
   if (P == 0) return hipSuccess;
   hipLaunchKernelGGL(duplicate_kernel, dim3((P + kThreads - 1) / kThreads), dim3(kThreads), 0, s,
-                     P, order, offsets, rec, gx, gy, tkey, tval, R, clear0, clear1, egid, ebeg);
+                     P, order, offsets, rec, gx, gy, tkey, tval, R, clear0, clear1, egid, ebeg,
+                     drec);
   return hipGetLastError();
+}
+
+bool dup_drec() {
+  static const bool on = [] {
+    const char* e = getenv("GSR_DUP_DREC");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
 }
 
 hipError_t launch_duplicate_views(const DupSpec* v, int V, hipStream_t s) {

@@ -9,8 +9,10 @@
 //   rec[4g+0] = {x_px, y_px, conic.a, conic.b}
 //   rec[4g+1] = {conic.c, opacity*confidence, depth, r}
 //   rec[4g+2] = {g, b, f0, f1}
-//   rec[4g+3] = {f2, radius, q_cut, 0}   (radius as float: exact; q_cut: the culling threshold of
-//                                        gsr_device.h, computed once here for the binning and blends)
+//   rec[4g+3] = {f2, radius, q_cut, count} (radius as float: exact; q_cut: the culling threshold of
+//                                        gsr_device.h, computed once here for the binning and blends;
+//                                        count: the exact tile count, as bits -- the depth sort's
+//                                        last pass gathers it with the binning fields)
 // so the blend reads one contiguous record per instance instead of five scattered arrays.
 #include "gsr_device.h"
 #include "gsr_internal.h"
@@ -170,7 +172,7 @@ __device__ __forceinline__ uint32_t preprocess_gaussian(const PreArgs& a, int id
   rec[0 ^ sw] = make_float4(px, py, con_a, con_b);
   rec[1 ^ sw] = make_float4(con_c, op, depth, cr);
   rec[2 ^ sw] = make_float4(cg, cb, in->f0, in->f1);
-  rec[3 ^ sw] = make_float4(in->f2, (float)r, qc, 0.f);
+  rec[3 ^ sw] = make_float4(in->f2, (float)r, qc, __uint_as_float(count));
   return count;
 }
 

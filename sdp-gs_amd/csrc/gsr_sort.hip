@@ -327,8 +327,24 @@ __device__ __forceinline__ void onesweep_body(
     int bits, const uint32_t* __restrict__ totals, const uint32_t* __restrict__ nsent_sh,
     uint32_t* __restrict__ ticket, uint64_t* __restrict__ status, uint32_t* __restrict__ err,
     uint32_t* __restrict__ kout, uint32_t* __restrict__ vout, const uint32_t* __restrict__ kpay,
-    uint32_t blk, uint32_t nblk) {
+    const float4* __restrict__ rpay, float4* __restrict__ rout, uint32_t blk, uint32_t nblk) {
   constexpr int kSortWaves = NT / 64, kSortThreads = NT;
+  // one sorted element out at position o: its value, and its key -- or (last pass) the payload
+  // gathered by its value: kpay[v], or from the splat record rpay[4 v ..] the binning record
+  // rout[2 o ..] = {x, y, conic.a, conic.b}, {conic.c, q_cut, radius, v} with the tile count
+  // (rec[3].w) as the key, so the duplication reads its Gaussians in depth order without a gather
+  auto emit = [&](uint32_t o, uint32_t v, uint32_t k) {
+    if (rpay) {
+      const float4* r = rpay + 4 * (size_t)min(v, (uint32_t)n - 1u);
+      const float4 r0 = r[0], r1 = r[1], r3 = r[3];
+      kout[o] = __float_as_uint(r3.w);
+      rout[2 * (size_t)o] = r0;
+      rout[2 * (size_t)o + 1] = make_float4(r1.x, r3.z, r3.y, __uint_as_float(v));
+    } else {
+      kout[o] = kpay ? kpay[min(v, (uint32_t)n - 1u)] : k;
+    }
+    vout[o] = v;
+  };
   constexpr int kKeysPerThread = kSortTile / NT, kKeysPerWave = kKeysPerThread * 64;
   static_assert(NT >= 256 && kSortTile % NT == 0, "one-sweep tile shape");
   __shared__ uint32_t s_k[kSortTile];
@@ -376,11 +392,7 @@ __device__ __forceinline__ void onesweep_body(
     if (ndig <= 1u) {
       const size_t b0 = (size_t)blk * kSortTile;
       const size_t e0 = min(n, b0 + (size_t)kSortTile);
-      for (size_t i = b0 + (size_t)t; i < e0; i += NT) {
-        const uint32_t v = vin[i];
-        kout[i] = kpay ? kpay[min(v, (uint32_t)n - 1u)] : kin[i];
-        vout[i] = v;
-      }
+      for (size_t i = b0 + (size_t)t; i < e0; i += NT) emit((uint32_t)i, vin[i], kin[i]);
       return;
     }
   }
@@ -548,11 +560,7 @@ __device__ __forceinline__ void onesweep_body(
   for (uint32_t i = (uint32_t)t; i < nvalid; i += kSortThreads) {
     const uint32_t k = s_k[i];
     const uint32_t o = s_gofs[(k >> shift) & mask] + i;
-    if (o < n) {  // only a timed-out look-back (error word raised) can produce o >= n
-      const uint32_t v = s_v[i];
-      kout[o] = kpay ? kpay[min(v, (uint32_t)n - 1u)] : k;
-      vout[o] = v;
-    }
+    if (o < n) emit(o, s_v[i], k);  // only a timed-out look-back (error word raised) can produce o >= n
   }
 #if GSR_SORT_TRACE
   SORT_TRACE(5)
@@ -571,9 +579,10 @@ __global__ __launch_bounds__(NT, NT == 1024 ? 8 : (NT == 512 ? 6 : 1)) void radi
     const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin, size_t n, int shift,
     int bits, const uint32_t* __restrict__ totals, const uint32_t* __restrict__ nsent_sh,
     uint32_t* __restrict__ ticket, uint64_t* __restrict__ status, uint32_t* __restrict__ err,
-    uint32_t* __restrict__ kout, uint32_t* __restrict__ vout, const uint32_t* __restrict__ kpay) {
+    uint32_t* __restrict__ kout, uint32_t* __restrict__ vout, const uint32_t* __restrict__ kpay,
+    const float4* __restrict__ rpay, float4* __restrict__ rout) {
   onesweep_body<NT>(kin, vin, n, shift, bits, totals, nsent_sh, ticket, status, err, kout, vout,
-                    kpay, blockIdx.x, gridDim.x);
+                    kpay, rpay, rout, blockIdx.x, gridDim.x);
 }
 
 // ---- several independent sorts / scans / sums per launch (the multi-view forward's batched
@@ -587,6 +596,8 @@ struct SortPassJob {
   uint32_t* kout;
   uint32_t* vout;
   const uint32_t* kpay;  // last pass: payload gathered in place of the key
+  const float4* rpay;    // last pass: splat records -> binning records rout (see onesweep_body)
+  float4* rout;
   uint32_t* aux;         // totals, sentinel counts, tickets, error word (kSortAux*)
   uint64_t* status;      // this pass's look-back words
   uint32_t n;
@@ -618,7 +629,7 @@ __global__ __launch_bounds__(NT, NT == 1024 ? 8 : (NT == 512 ? 6 : 1)) void radi
   const SortPassJob& j = m.j[k];
   onesweep_body<NT>(j.kin, j.vin, j.n, shift, bits, j.aux + kSortAuxTotals + 256 * pass,
                     sentinel ? j.aux + kSortAuxSent : nullptr, j.aux + kSortAuxTickets + 8 * pass,
-                    j.status, j.aux + kSortAuxErr, j.kout, j.vout, j.kpay,
+                    j.status, j.aux + kSortAuxErr, j.kout, j.vout, j.kpay, j.rpay, j.rout,
                     blockIdx.x - m.first[k], m.first[k + 1] - m.first[k]);
 }
 
@@ -935,7 +946,8 @@ uint32_t* sort_timeouts_word() {
 hipError_t radix_sort_pairs(uint32_t* ka, uint32_t* va, uint32_t* kb, uint32_t* vb, size_t n,
                             int bits, SortScratch scratch, bool* result_in_b, hipStream_t s,
                             bool sentinel_anywhere, bool precleared,
-                            const uint32_t* key_payload) {
+                            const uint32_t* key_payload, const float4* rec_payload,
+                            float4* rec_out) {
   *result_in_b = false;
   if (n == 0 || bits <= 0) return hipSuccess;
   if (bits > 32 || n > 0xffffffffull) return hipErrorInvalidValue;
@@ -965,7 +977,8 @@ hipError_t radix_sort_pairs(uint32_t* ka, uint32_t* va, uint32_t* kb, uint32_t* 
                      scratch.aux + kSortAuxTickets + 8 * p,                                      \
                      scratch.status + (size_t)p * sort_pass_words(n), \
                      scratch.aux + kSortAuxErr, kout, vout,                                      \
-                     p == passes - 1 ? key_payload : nullptr)
+                     p == passes - 1 ? key_payload : nullptr,                                    \
+                     p == passes - 1 ? rec_payload : nullptr, rec_out)
     if (nt == 1024) GSR_ONESWEEP(1024);
     else if (nt == 512) GSR_ONESWEEP(512);
     else GSR_ONESWEEP(256);
@@ -1015,6 +1028,8 @@ hipError_t radix_sort_pairs_views(const SortSpec* v, int V, int bits, bool* resu
       j.kout = b_in ? w.ka : w.kb;
       j.vout = b_in ? w.va : w.vb;
       j.kpay = p == passes - 1 ? w.key_payload : nullptr;
+      j.rpay = p == passes - 1 ? w.rec_payload : nullptr;
+      j.rout = w.rec_out;
       j.aux = w.scratch.aux;
       j.status = w.scratch.status + (size_t)p * sort_pass_words(w.n);
       j.n = (uint32_t)w.n;
