@@ -329,7 +329,7 @@ hipError_t launch_duplicate(int P, const uint32_t* order, const uint32_t* offset
 bool dup_drec() {
   static const bool on = [] {
     const char* e = getenv("GSR_DUP_DREC");
-    return !(e && atoi(e) == 0);
+    return e && atoi(e) == 1;
   }();
   return on;
 }

@@ -386,8 +386,10 @@ hipError_t launch_duplicate(int P, const uint32_t* order, const uint32_t* offset
                             uint32_t* tkey, uint32_t* tval, uint32_t R, SideClear clear0,
                             SideClear clear1, hipStream_t s, uint32_t* egid = nullptr,
                             uint32_t* ebeg = nullptr, const float4* drec = nullptr);
-// whether the forward hands the duplication depth-ordered binning records (env GSR_DUP_DREC,
-// default 1; 0 = the duplication gathers the splat records by id)
+// whether the forward hands the duplication depth-ordered binning records (env GSR_DUP_DREC=1;
+// default 0 = the duplication gathers the splat records by id).  Round 4, alternating runs:
+// duplicate 0.094 -> 0.074 ms per 3 views, but the depth sort 0.131 -> 0.177 (its last pass then
+// gathers 48 B and writes 32 B more per Gaussian): 2.88-2.91 vs 2.93-2.96 ms per step -- off
 bool dup_drec();
 // ranges_cleared: the ranges are already zero (duplicate's side clear): no memset launch.
 // Also writes the call's status word from the depth / tile sorts' error words (either may be null).

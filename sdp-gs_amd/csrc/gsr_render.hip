@@ -1277,13 +1277,13 @@ static int bwd_pix2() {
   return g;
 }
 
-// GSR_BWD_PIPE (default 1): the pipelined wave reduction of render_bwd_tile (1), the joint
+// GSR_BWD_PIPE (default 0): the pipelined wave reduction of render_bwd_tile (1), the joint
 // reduction of a group's four entries (2), or neither (0)
 static int bwd_pipe() {
   static const int mode = [] {
     const char* e = getenv("GSR_BWD_PIPE");
-    const int v = e ? atoi(e) : 1;
-    return (v == 0 || v == 2) ? v : 1;
+    const int v = e ? atoi(e) : 0;
+    return (v == 1 || v == 2) ? v : 0;
   }();
   return mode;
 }
