@@ -1384,7 +1384,13 @@ __device__ __forceinline__ uint32_t build_group_lists(const uint16_t* s_mask, ui
 #ifndef GSR_FWD_BLK_WAVES
 #define GSR_FWD_BLK_WAVES 1
 #endif
-template <bool FEAT>
+// FAST (GSR_FWD_FAST, round 4; bits): 1 = G by the hardware exp2 with splat_exp wherever op * G
+// lies within 2e-6 (relative) of 1/255 -- the alpha >= 1/255 decision stays the oracle's exactly,
+// G differs from splat_exp's by < 1e-6 relative (the T < 1e-4 stop can then flip only at pixels
+// within ~1e-6 of it, which the parity tests' threshold margin covers); the backward evaluates the
+// same instruction sequence (GSR_BWD_FAST_EXP), so its alpha is the forward's bit for bit.
+// 2 = the channel sums by fused multiply-adds (output-only arithmetic, no decision depends on it).
+template <bool FEAT, int FAST>
 __device__ __forceinline__ void render_fwd_blk_tile(const RenderArgs& a, uint32_t blk) {
   __shared__ float4 s_r0[kThreads];
   __shared__ float4 s_r1[kThreads];
@@ -1481,7 +1487,13 @@ __device__ __forceinline__ void render_fwd_blk_tile(const RenderArgs& a, uint32_
         // entries past the group's list end get power = +1 and are skipped
         pw[u] = (k + u < nl) ? power : 1.0f;
 #if !GSR_FWD_TEST_FIRST
-        al[u] = fminf(0.99f, r1v[u].y * splat_exp(pw[u]));
+        if (FAST & 1) {
+          float G = __builtin_amdgcn_exp2f(pw[u] * 1.44269504088896341f);
+          if (fabsf(r1v[u].y * G - (1.0f / 255.0f)) <= 2e-6f * (1.0f / 255.0f)) G = splat_exp(pw[u]);
+          al[u] = fminf(0.99f, r1v[u].y * G);
+        } else {
+          al[u] = fminf(0.99f, r1v[u].y * splat_exp(pw[u]));
+        }
 #endif
       }
 #if GSR_FWD_TEST_FIRST
@@ -1509,15 +1521,28 @@ __device__ __forceinline__ void render_fwd_blk_tile(const RenderArgs& a, uint32_
           continue;
         }
         const float wgt = alpha * T;
-        C[0] += r1v[u].w * wgt;
-        C[1] += r2v[u].x * wgt;
-        C[2] += r2v[u].y * wgt;
-        C[3] += r1v[u].z * wgt;
-        C[4] += wgt;
-        if (FEAT) {
-          C[5 % NC] += r2v[u].z * wgt;
-          C[6 % NC] += r2v[u].w * wgt;
-          C[7 % NC] += f2v[u] * wgt;
+        if (FAST & 2) {
+          C[0] = __builtin_fmaf(r1v[u].w, wgt, C[0]);
+          C[1] = __builtin_fmaf(r2v[u].x, wgt, C[1]);
+          C[2] = __builtin_fmaf(r2v[u].y, wgt, C[2]);
+          C[3] = __builtin_fmaf(r1v[u].z, wgt, C[3]);
+          C[4] += wgt;
+          if (FEAT) {
+            C[5 % NC] = __builtin_fmaf(r2v[u].z, wgt, C[5 % NC]);
+            C[6 % NC] = __builtin_fmaf(r2v[u].w, wgt, C[6 % NC]);
+            C[7 % NC] = __builtin_fmaf(f2v[u], wgt, C[7 % NC]);
+          }
+        } else {
+          C[0] += r1v[u].w * wgt;
+          C[1] += r2v[u].x * wgt;
+          C[2] += r2v[u].y * wgt;
+          C[3] += r1v[u].z * wgt;
+          C[4] += wgt;
+          if (FEAT) {
+            C[5 % NC] += r2v[u].z * wgt;
+            C[6 % NC] += r2v[u].w * wgt;
+            C[7 % NC] += f2v[u] * wgt;
+          }
         }
         T = test_T;
         last_contributor = rel0 + jj[u] + 1;
@@ -1551,20 +1576,20 @@ __device__ __forceinline__ void render_fwd_blk_tile(const RenderArgs& a, uint32_
   }
 }
 
-template <bool FEAT>
+template <bool FEAT, int FAST>
 __global__ __launch_bounds__(kThreads, GSR_FWD_BLK_WAVES) void render_fwd_blk_kernel(RenderArgs a) {
-  render_fwd_blk_tile<FEAT>(a, blockIdx.x);
+  render_fwd_blk_tile<FEAT, FAST>(a, blockIdx.x);
 }
 
 // The forward blends of several views in ONE launch (view-major workgroups, as
 // render_bwd_views_kernel): no per-view tail of idle CUs.
-template <bool FEAT>
+template <bool FEAT, int FAST>
 __global__ __launch_bounds__(kThreads, GSR_FWD_BLK_WAVES) void render_fwd_blk_views_kernel(
     RenderFwdViews m) {
   const uint32_t b = blockIdx.x;
   int k = 0;
   while (k + 1 < m.V && b >= m.first[k + 1]) k++;  // workgroup-uniform
-  render_fwd_blk_tile<FEAT>(m.v[k], b - m.first[k]);
+  render_fwd_blk_tile<FEAT, FAST>(m.v[k], b - m.first[k]);
 }
 
 __global__ void expf_pair_kernel(const float* __restrict__ x, float* __restrict__ ref,
@@ -1621,6 +1646,16 @@ hipError_t launch_expf_pair(const float* x, float* ref, float* fast, size_t n, h
 }
 
 // GSR_BLOCK_LISTS=0 selects the quadrant-list kernels (one list per wave) for A/B runs
+// GSR_FWD_FAST (bits, default 0): render_fwd_blk_tile's hardware-exp2 alpha test (1) and fused
+// channel sums (2)
+static int fwd_fast() {
+  static const int v = [] {
+    const char* e = getenv("GSR_FWD_FAST");
+    return e ? (atoi(e) & 3) : 0;
+  }();
+  return v;
+}
+
 static bool block_lists() {
   static const bool on = [] {
     const char* e = getenv("GSR_BLOCK_LISTS");
@@ -1678,10 +1713,18 @@ hipError_t launch_render_forward_views(const RenderArgs* views, int V, hipStream
     m.first[k + 1] = m.first[k] + views[k].gx * views[k].gy;
   }
   if (m.first[V] == 0) return hipSuccess;
-  if (feat)
-    hipLaunchKernelGGL(render_fwd_blk_views_kernel<true>, dim3(m.first[V]), dim3(kThreads), 0, s, m);
-  else
-    hipLaunchKernelGGL(render_fwd_blk_views_kernel<false>, dim3(m.first[V]), dim3(kThreads), 0, s, m);
+#define GSR_FWDV(F)                                                                               \
+  do {                                                                                           \
+    switch (fwd_fast()) {                                                                        \
+      case 1: hipLaunchKernelGGL((render_fwd_blk_views_kernel<F, 1>), dim3(m.first[V]), dim3(kThreads), 0, s, m); break; \
+      case 2: hipLaunchKernelGGL((render_fwd_blk_views_kernel<F, 2>), dim3(m.first[V]), dim3(kThreads), 0, s, m); break; \
+      case 3: hipLaunchKernelGGL((render_fwd_blk_views_kernel<F, 3>), dim3(m.first[V]), dim3(kThreads), 0, s, m); break; \
+      default: hipLaunchKernelGGL((render_fwd_blk_views_kernel<F, 0>), dim3(m.first[V]), dim3(kThreads), 0, s, m); \
+    }                                                                                            \
+  } while (0)
+  if (feat) GSR_FWDV(true);
+  else GSR_FWDV(false);
+#undef GSR_FWDV
   return hipGetLastError();
 }
 
@@ -1692,10 +1735,18 @@ hipError_t launch_render_forward(const RenderArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(tile_schedule_kernel, dim3(1), dim3(kSchedThreads), 0, s, a.ranges,
                        (const uint32_t*)nullptr, ntiles, a.order);
   if (block_lists()) {
-    if (a.include_feature)
-      hipLaunchKernelGGL(render_fwd_blk_kernel<true>, dim3(ntiles), dim3(kThreads), 0, s, a);
-    else
-      hipLaunchKernelGGL(render_fwd_blk_kernel<false>, dim3(ntiles), dim3(kThreads), 0, s, a);
+#define GSR_FWD1(F)                                                                               \
+  do {                                                                                           \
+    switch (fwd_fast()) {                                                                        \
+      case 1: hipLaunchKernelGGL((render_fwd_blk_kernel<F, 1>), dim3(ntiles), dim3(kThreads), 0, s, a); break; \
+      case 2: hipLaunchKernelGGL((render_fwd_blk_kernel<F, 2>), dim3(ntiles), dim3(kThreads), 0, s, a); break; \
+      case 3: hipLaunchKernelGGL((render_fwd_blk_kernel<F, 3>), dim3(ntiles), dim3(kThreads), 0, s, a); break; \
+      default: hipLaunchKernelGGL((render_fwd_blk_kernel<F, 0>), dim3(ntiles), dim3(kThreads), 0, s, a); \
+    }                                                                                            \
+  } while (0)
+    if (a.include_feature) GSR_FWD1(true);
+    else GSR_FWD1(false);
+#undef GSR_FWD1
   } else if (a.include_feature)
     hipLaunchKernelGGL(render_fwd_kernel<true>, dim3(ntiles), dim3(kThreads), 0, s, a);
   else
