@@ -1384,13 +1384,15 @@ __device__ __forceinline__ uint32_t build_group_lists(const uint16_t* s_mask, ui
 #ifndef GSR_FWD_BLK_WAVES
 #define GSR_FWD_BLK_WAVES 1
 #endif
-// FAST (GSR_FWD_FAST, round 4; bits): 1 = G by the hardware exp2 with splat_exp wherever op * G
-// lies within 2e-6 (relative) of 1/255 -- the alpha >= 1/255 decision stays the oracle's exactly,
-// G differs from splat_exp's by < 1e-6 relative (the T < 1e-4 stop can then flip only at pixels
-// within ~1e-6 of it, which the parity tests' threshold margin covers); the backward evaluates the
-// same instruction sequence (GSR_BWD_FAST_EXP), so its alpha is the forward's bit for bit.
-// 2 = the channel sums by fused multiply-adds (output-only arithmetic, no decision depends on it).
-template <bool FEAT, int FAST>
+// FAST (GSR_FWD_FAST, default 1; round 4): G by the hardware exp2 (v_exp_f32, 3 instructions
+// instead of the 17 of splat_exp) with splat_exp wherever op * G lies within 2e-6 (relative) of
+// 1/255 -- the alpha >= 1/255 decision stays the oracle's exactly, G differs from splat_exp's by
+// < 1e-6 relative (so the T < 1e-4 stop can flip only at pixels within ~1e-6 of it, inside the
+// parity tests' threshold margin); the backward evaluates the same instruction sequence
+// (GSR_BWD_FAST_EXP), so its alpha is the forward's bit for bit.  render_fwd 0.294 / 0.299 ->
+// 0.279 / 0.284 ms per 3-view launch (profiles/r04_fwd_fast_ab.txt).  Fused multiply-adds for
+// the channel sums (output-only arithmetic) measured slower, 0.313 ms, and were dropped.
+template <bool FEAT, bool FAST>
 __device__ __forceinline__ void render_fwd_blk_tile(const RenderArgs& a, uint32_t blk) {
   __shared__ float4 s_r0[kThreads];
   __shared__ float4 s_r1[kThreads];
@@ -1487,7 +1489,7 @@ __device__ __forceinline__ void render_fwd_blk_tile(const RenderArgs& a, uint32_
         // entries past the group's list end get power = +1 and are skipped
         pw[u] = (k + u < nl) ? power : 1.0f;
 #if !GSR_FWD_TEST_FIRST
-        if (FAST & 1) {
+        if (FAST) {
           float G = __builtin_amdgcn_exp2f(pw[u] * 1.44269504088896341f);
           if (fabsf(r1v[u].y * G - (1.0f / 255.0f)) <= 2e-6f * (1.0f / 255.0f)) G = splat_exp(pw[u]);
           al[u] = fminf(0.99f, r1v[u].y * G);
@@ -1521,28 +1523,15 @@ __device__ __forceinline__ void render_fwd_blk_tile(const RenderArgs& a, uint32_
           continue;
         }
         const float wgt = alpha * T;
-        if (FAST & 2) {
-          C[0] = __builtin_fmaf(r1v[u].w, wgt, C[0]);
-          C[1] = __builtin_fmaf(r2v[u].x, wgt, C[1]);
-          C[2] = __builtin_fmaf(r2v[u].y, wgt, C[2]);
-          C[3] = __builtin_fmaf(r1v[u].z, wgt, C[3]);
-          C[4] += wgt;
-          if (FEAT) {
-            C[5 % NC] = __builtin_fmaf(r2v[u].z, wgt, C[5 % NC]);
-            C[6 % NC] = __builtin_fmaf(r2v[u].w, wgt, C[6 % NC]);
-            C[7 % NC] = __builtin_fmaf(f2v[u], wgt, C[7 % NC]);
-          }
-        } else {
-          C[0] += r1v[u].w * wgt;
-          C[1] += r2v[u].x * wgt;
-          C[2] += r2v[u].y * wgt;
-          C[3] += r1v[u].z * wgt;
-          C[4] += wgt;
-          if (FEAT) {
-            C[5 % NC] += r2v[u].z * wgt;
-            C[6 % NC] += r2v[u].w * wgt;
-            C[7 % NC] += f2v[u] * wgt;
-          }
+        C[0] += r1v[u].w * wgt;
+        C[1] += r2v[u].x * wgt;
+        C[2] += r2v[u].y * wgt;
+        C[3] += r1v[u].z * wgt;
+        C[4] += wgt;
+        if (FEAT) {
+          C[5 % NC] += r2v[u].z * wgt;
+          C[6 % NC] += r2v[u].w * wgt;
+          C[7 % NC] += f2v[u] * wgt;
         }
         T = test_T;
         last_contributor = rel0 + jj[u] + 1;
@@ -1576,14 +1565,14 @@ __device__ __forceinline__ void render_fwd_blk_tile(const RenderArgs& a, uint32_
   }
 }
 
-template <bool FEAT, int FAST>
+template <bool FEAT, bool FAST>
 __global__ __launch_bounds__(kThreads, GSR_FWD_BLK_WAVES) void render_fwd_blk_kernel(RenderArgs a) {
   render_fwd_blk_tile<FEAT, FAST>(a, blockIdx.x);
 }
 
 // The forward blends of several views in ONE launch (view-major workgroups, as
 // render_bwd_views_kernel): no per-view tail of idle CUs.
-template <bool FEAT, int FAST>
+template <bool FEAT, bool FAST>
 __global__ __launch_bounds__(kThreads, GSR_FWD_BLK_WAVES) void render_fwd_blk_views_kernel(
     RenderFwdViews m) {
   const uint32_t b = blockIdx.x;
@@ -1646,12 +1635,11 @@ hipError_t launch_expf_pair(const float* x, float* ref, float* fast, size_t n, h
 }
 
 // GSR_BLOCK_LISTS=0 selects the quadrant-list kernels (one list per wave) for A/B runs
-// GSR_FWD_FAST (bits, default 0): render_fwd_blk_tile's hardware-exp2 alpha test (1) and fused
-// channel sums (2)
-static int fwd_fast() {
-  static const int v = [] {
+// GSR_FWD_FAST (default 1): render_fwd_blk_tile's hardware-exp2 alpha test; 0 = splat_exp
+static bool fwd_fast() {
+  static const bool v = [] {
     const char* e = getenv("GSR_FWD_FAST");
-    return e ? (atoi(e) & 3) : 0;
+    return !(e && atoi(e) == 0);
   }();
   return v;
 }
@@ -1715,12 +1703,10 @@ hipError_t launch_render_forward_views(const RenderArgs* views, int V, hipStream
   if (m.first[V] == 0) return hipSuccess;
 #define GSR_FWDV(F)                                                                               \
   do {                                                                                           \
-    switch (fwd_fast()) {                                                                        \
-      case 1: hipLaunchKernelGGL((render_fwd_blk_views_kernel<F, 1>), dim3(m.first[V]), dim3(kThreads), 0, s, m); break; \
-      case 2: hipLaunchKernelGGL((render_fwd_blk_views_kernel<F, 2>), dim3(m.first[V]), dim3(kThreads), 0, s, m); break; \
-      case 3: hipLaunchKernelGGL((render_fwd_blk_views_kernel<F, 3>), dim3(m.first[V]), dim3(kThreads), 0, s, m); break; \
-      default: hipLaunchKernelGGL((render_fwd_blk_views_kernel<F, 0>), dim3(m.first[V]), dim3(kThreads), 0, s, m); \
-    }                                                                                            \
+    if (fwd_fast())                                                                              \
+      hipLaunchKernelGGL((render_fwd_blk_views_kernel<F, true>), dim3(m.first[V]), dim3(kThreads), 0, s, m); \
+    else                                                                                         \
+      hipLaunchKernelGGL((render_fwd_blk_views_kernel<F, false>), dim3(m.first[V]), dim3(kThreads), 0, s, m); \
   } while (0)
   if (feat) GSR_FWDV(true);
   else GSR_FWDV(false);
@@ -1737,12 +1723,10 @@ hipError_t launch_render_forward(const RenderArgs& a, hipStream_t s) {
   if (block_lists()) {
 #define GSR_FWD1(F)                                                                               \
   do {                                                                                           \
-    switch (fwd_fast()) {                                                                        \
-      case 1: hipLaunchKernelGGL((render_fwd_blk_kernel<F, 1>), dim3(ntiles), dim3(kThreads), 0, s, a); break; \
-      case 2: hipLaunchKernelGGL((render_fwd_blk_kernel<F, 2>), dim3(ntiles), dim3(kThreads), 0, s, a); break; \
-      case 3: hipLaunchKernelGGL((render_fwd_blk_kernel<F, 3>), dim3(ntiles), dim3(kThreads), 0, s, a); break; \
-      default: hipLaunchKernelGGL((render_fwd_blk_kernel<F, 0>), dim3(ntiles), dim3(kThreads), 0, s, a); \
-    }                                                                                            \
+    if (fwd_fast())                                                                              \
+      hipLaunchKernelGGL((render_fwd_blk_kernel<F, true>), dim3(ntiles), dim3(kThreads), 0, s, a); \
+    else                                                                                         \
+      hipLaunchKernelGGL((render_fwd_blk_kernel<F, false>), dim3(ntiles), dim3(kThreads), 0, s, a); \
   } while (0)
     if (a.include_feature) GSR_FWD1(true);
     else GSR_FWD1(false);
