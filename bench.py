@@ -288,7 +288,7 @@ def main():
         # gradients are flushed in row slices, each slice reduced as soon as it is written)
         if not args.per_view and not args.autograd_grads:
             views_.run_views(my_cams, lambda cams, strs: all_views(cams, strs, record),
-                             model=model, reducer=reducer)
+                             model=model, reducer=reducer, chunks=args.view_chunks)
         elif args.lag > 0:
             views_.run(my_cams, view_forward, model=model, reducer=reducer,
                        bwd=lambda pkg: view_backward(pkg, record), lag=args.lag)
@@ -296,25 +296,21 @@ def main():
             views_.run(my_cams, lambda cam: one_view(cam, record), model=model, reducer=reducer)
 
     def all_views(cams, strs, record):
-        """The step's views in `--view-chunks` multi-view calls: a chunk's forward of all its
-        views, then the backward of the fixed upstream gradients seeded on its stacked [V,...]
-        outputs, so the next chunk's binning (latency-bound, on the binning streams) runs beside
-        this chunk's backward blend (on the backward stream)."""
-        n = max(1, min(args.view_chunks, len(cams)))
-        bounds = [round(i * len(cams) / n) for i in range(n + 1)]
-        for a, b in zip(bounds[:-1], bounds[1:]):
-            pkgs = render_views(cams[a:b], model, pipe, bg, opt, streams=strs)
-            st = pkgs[0]["views"]
-            V = len(pkgs)
-            torch.autograd.backward(
-                [st["render"], st["depth"], st["feature"]],
-                [dimg.expand(V, *dimg.shape), ddep.expand(V, *ddep.shape),
-                 dfeat.expand(V, *dfeat.shape)])
-            if record:
-                for (nr, ni), pkg in zip(dgr.LAST_STATS["view_counts"], pkgs):
-                    stats["R"].append(ni)
-                    stats["R_ref"].append(nr)
-                    stats["Pv"].append(int(pkg["visibility_filter"].sum()))
+        """One multi-view call (a chunk of the step's views with --view-chunks, issued by
+        ViewPipeline.run_views on its own streams): the forward of all its views, then the
+        backward of the fixed upstream gradients seeded on its stacked [V,...] outputs."""
+        pkgs = render_views(cams, model, pipe, bg, opt, streams=strs)
+        st = pkgs[0]["views"]
+        V = len(pkgs)
+        torch.autograd.backward(
+            [st["render"], st["depth"], st["feature"]],
+            [dimg.expand(V, *dimg.shape), ddep.expand(V, *ddep.shape),
+             dfeat.expand(V, *dfeat.shape)])
+        if record:
+            for (nr, ni), pkg in zip(dgr.LAST_STATS["view_counts"], pkgs):
+                stats["R"].append(ni)
+                stats["R_ref"].append(nr)
+                stats["Pv"].append(int(pkg["visibility_filter"].sum()))
 
     def view_forward(cam):
         pkg = render(cam, model, pipe, bg, opt)

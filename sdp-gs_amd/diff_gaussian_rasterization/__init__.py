@@ -677,6 +677,8 @@ class _RasterizeViewsFused(torch.autograd.Function):
                 _ptr(d_op), _ptr(d_sc), _ptr(d_rot), _ptr(d_lf), int(accumulate),
                 cur.cuda_stream, ctx.gsr_flags | _TEST_BWD_BITS[0])
         slices = _ROW_SLICES.get(dev.index) if into_leaves else None
+        if slices is not None and not slices.active:
+            slices = None  # an earlier chunk of a chunked step (ViewPipeline.run_views)
         errors = []
         with _lib.on_device(dev):
             if slices is None:
@@ -818,6 +820,7 @@ class BackwardRowSlices:
         self.on_rows = on_rows
         self.slices = max(1, int(slices))
         self.ran = False
+        self.active = True  # False: backwards pass it by (an earlier chunk of a chunked step)
 
     def rows(self, P):
         self.ran = True

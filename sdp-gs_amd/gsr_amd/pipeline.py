@@ -53,6 +53,7 @@ class ViewPipeline:
         self.bwd_slices = bwd_slices
         self._pre_bufs = None  # the pre-pass's per-view buffers, reused step after step
         self.side = [torch.cuda.Stream(device=self.device) for _ in range(depth - 1)]
+        self._slices = None  # the step's BackwardRowSlices while run_views issues
 
     def run(self, items: Iterable[T], fn: Callable[[T], R], model=None,
             campos_of: Callable[[T], torch.Tensor] = lambda cam: cam.camera_center,
@@ -101,22 +102,47 @@ class ViewPipeline:
 
     def run_views(self, items: Iterable[T], fn: Callable[[List[T], List[torch.cuda.Stream]], R],
                   model=None, campos_of: Callable[[T], torch.Tensor] = lambda cam: cam.camera_center,
-                  reducer=None) -> R:
+                  reducer=None, chunks: int = 1):
         """The step's views in ONE multi-view call: fn(items, streams) renders all of them at once
         (gaussian_renderer.render_views(items, ..., streams=streams): one host call issues every
         view's forward, autograd one call for every backward) and runs their backward; the views
         are spread over this pipeline's streams inside the library, which joins them back into the
         current stream.  Pre-pass, deferred SH gradients and the overlapped all-reduce as run().
-        Returns fn's result."""
+        Returns fn's result.
+
+        chunks > 1: the views in that many consecutive chunks, one multi-view call each, chunk c
+        issued with streams (2c, 2c + 1) mod depth of [current] + side as its call and binning
+        streams -- so chunk c + 1's forward (latency-bound binning) runs beside chunk c's backward
+        blend instead of queueing behind it on one stream, and its buffers come from its own
+        stream's allocator pool (never memory that an earlier chunk's backward still reads).  The
+        grad-into-leaves backwards are ordered by diff_gaussian_rasterization; the row-sliced
+        all-reduce (reducer) runs on the last chunk's per-Gaussian backward only.  Returns the
+        list of fn's results."""
         self._check(reducer, model)
         items = list(items)
-        streams = [torch.cuda.current_stream(self.device)] + self.side
+        main = torch.cuda.current_stream(self.device)
+        streams = [main] + self.side
+        n = max(1, min(int(chunks), len(items)))
 
         def issue(out):
-            out.append(fn(items, streams))
+            if n == 1:
+                out.append(fn(items, streams))
+                return out
+            bounds = [round(i * len(items) / n) for i in range(n + 1)]
+            for c, (a, b) in enumerate(zip(bounds[:-1], bounds[1:])):
+                cs = [streams[(2 * c) % self.depth], streams[(2 * c + 1) % self.depth]]
+                if cs[1] is cs[0]:
+                    cs = cs[:1]
+                if self._slices is not None:  # the leaves' rows are final after the last chunk only
+                    self._slices.active = c == n - 1
+                with _lib.on_stream(cs[0]):
+                    out.append(fn(items[a:b], cs))
+            for s in self.side:
+                main.wait_stream(s)
             return out
 
-        return self._step(items, issue, model, campos_of, reducer, sliced=True)[0]
+        out = self._step(items, issue, model, campos_of, reducer, sliced=True)
+        return out[0] if n == 1 else out
 
     def _check(self, reducer, model):
         if reducer is not None and self.defer_sh and model is None:
@@ -160,9 +186,13 @@ class ViewPipeline:
             slices = dgr.BackwardRowSlices(
                 self.device, lambda a, b: reducer.reduce_row_slices_async(rest, a, b),
                 self.bwd_slices)
+            self._slices = slices
         with pre, defer:  # defer's exit: the SH gradients of all views, after the join
-            with slices:
-                issue(out)
+            try:
+                with slices:
+                    issue(out)
+            finally:
+                self._slices = None
             if reducer is not None:  # every view's backward is done: the non-SH grads are final
                 ids = {id(t) for t in sh_leaves}
                 # (with the step's fault snapshot: every forward of the step is done)

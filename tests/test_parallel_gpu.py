@@ -35,7 +35,7 @@ def _scene(dev):
     return model, cams, grads
 
 
-def _step(model, cams, grads, views, reducer, multi=False):
+def _step(model, cams, grads, views, reducer, multi=False, chunks=1):
     from gaussian_renderer import render, render_views
     dimg, ddep, dfeat = grads
     bg = torch.zeros(3, device=dimg.device)
@@ -57,7 +57,7 @@ def _step(model, cams, grads, views, reducer, multi=False):
         for p in model.parameters():
             p.grad = None
     if multi:
-        views.run_views(cams, all_views, model=model, reducer=reducer)
+        views.run_views(cams, all_views, model=model, reducer=reducer, chunks=chunks)
     else:
         views.run(cams, one_view, model=model, reducer=reducer)
     torch.cuda.synchronize()
@@ -82,9 +82,12 @@ def world1(request, tmp_path):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("bucket_bytes,multi", [(64 << 20, False), (256 << 10, False),
-                                                (64 << 20, True), (256 << 10, True)])
-def test_bucket_view_grads_equal_plain_step(world1, bucket_bytes, multi):
+@pytest.mark.parametrize("bucket_bytes,multi,chunks", [(64 << 20, False, 1), (256 << 10, False, 1),
+                                                       (64 << 20, True, 1), (256 << 10, True, 1),
+                                                       (256 << 10, True, 2)])
+def test_bucket_view_grads_equal_plain_step(world1, bucket_bytes, multi, chunks):
+    """chunks = 2: the step's views in two multi-view calls on their own streams (run_views
+    chunks=; the row-sliced all-reduce on the last chunk only), against the one-call step."""
     import diff_gaussian_rasterization as dgr
     from gsr_amd.parallel import GradAllReducer
     from gsr_amd.pipeline import ViewPipeline
@@ -93,14 +96,14 @@ def test_bucket_view_grads_equal_plain_step(world1, bucket_bytes, multi):
     dgr.grad_into_leaves(True)
     try:
         model, cams, grads = _scene(dev)
-        views = ViewPipeline(dev, depth=2, defer_sh=True, precolor=True)
+        views = ViewPipeline(dev, depth=2 * chunks, defer_sh=True, precolor=True)
         ref = _step(model, cams, grads, views, None, multi)
         reducer = GradAllReducer(model, bucket_bytes=bucket_bytes)
         # issue the collectives at world size 1 as well: gloo copies each slice to the host and
         # back, so a collective that ran before its slice was flushed would write stale zeros
         reducer._active = lambda: True
         for _ in range(2):  # the second step reuses the attached buffer (zeroed by attach_grads)
-            got = _step(model, cams, grads, views, reducer, multi)
+            got = _step(model, cams, grads, views, reducer, multi, chunks)
             for p, g, r in zip(model.parameters(), got, ref):
                 assert g.shape == r.shape
                 # the backward's float atomics make two runs of a view differ in the last bits
