@@ -195,17 +195,27 @@ def decision_flips(a, b):
     return flips
 
 
-def flip_gaussians(b, flips, P):
-    """Gaussians in the tile lists of the flipped pixels: their gradients see the flip."""
+def flip_gaussians(b, flips, P, ncs=None):
+    """Gaussians whose gradients see the flipped pixels: with ncs (the n_contrib maps of the
+    evaluations compared) the pixel's contributors in either of them -- list positions
+    [0, max n_contrib) of its tile -- else every Gaussian of the pixel's tile list."""
     hit = np.zeros(P, bool)
     if not flips.any():
         return hit
     H, W = flips.shape
     gx = (W + 15) // 16
     ys, xs = np.nonzero(flips)
-    for t in np.unique((ys // 16) * gx + xs // 16):
+    if ncs is None:
+        for t in np.unique((ys // 16) * gx + xs // 16):
+            s, e = b["ranges"][t]
+            hit[b["point_list"][s:e]] = True
+        return hit
+    lim = np.max([np.asarray(n).reshape(H, W)[ys, xs] for n in ncs], axis=0)
+    tiles = (ys // 16) * gx + xs // 16
+    for t in np.unique(tiles):
         s, e = b["ranges"][t]
-        hit[b["point_list"][s:e]] = True
+        L = int(lim[tiles == t].max())
+        hit[b["point_list"][s:min(e, s + L)]] = True
     return hit
 
 
