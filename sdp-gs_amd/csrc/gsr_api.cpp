@@ -1169,11 +1169,11 @@ bool pre_views() {
 struct HostTrace {
   bool on;
   std::chrono::steady_clock::time_point t0;
-  char buf[512];
+  char buf[2048];
   int n = 0;
   HostTrace() : on(getenv("GSR_HOST_TRACE") != nullptr), t0(std::chrono::steady_clock::now()) {}
   void mark(const char* what, int g) {
-    if (!on || n > 440) return;
+    if (!on || n > 1980) return;
     const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
     n += snprintf(buf + n, sizeof(buf) - (size_t)n, " %s%d=%.0f", what, g, us);
   }
@@ -1383,10 +1383,12 @@ int views_forward_batched(const FwdModel& m, std::vector<FwdCam>& cams, gsr_view
         char* base = (char*)c0.alloc(c0.alloc_ctx, off[nl] ? off[nl] : 256, GSR_BUF_BINNING);
         if (!base) return fail(GSR_ERR_ALLOC, "binning buffer allocation of %zu bytes failed", off[nl]);
         for (int l = 0; l < nl; l++) cams[(size_t)G.live[(size_t)l]].given_b = base + off[l];
+        ht.mark("A", gi);
       }
       for (int l = 0; l < nl; l++) {
         FwdCam& c = cams[(size_t)G.live[(size_t)l]];
         if (int rc = fwd_bin_alloc(m, c)) return rc;  // (debug: checks the depth sort)
+        ht.mark("b", l);
         const GeomState& g = c.g;
         const BinState& b = c.b;
         const uint32_t R = (uint32_t)c.num_instances;
@@ -1406,6 +1408,7 @@ int views_forward_batched(const FwdModel& m, std::vector<FwdCam>& cams, gsr_view
       PROF_BEGIN(TILE_SORT);
       GSR_CHECK(radix_sort_pairs_views(ts, nl, tbits, &t_in_b, stream, false, /*precleared=*/true));
       PROF_END(TILE_SORT);
+      ht.mark("t", gi);
       RangesSpec rs[kMaxBatchViews];
       for (int l = 0; l < nl; l++) {
         FwdCam& c = cams[(size_t)G.live[(size_t)l]];
@@ -1462,6 +1465,7 @@ int views_forward_batched(const FwdModel& m, std::vector<FwdCam>& cams, gsr_view
       FwdCam& c = cams[(size_t)v];
       if (c.done) c.num_rendered = c.num_instances = 0;
       if (int rc = fwd_blended(m, c, rstream)) return rc;
+      ht.mark("B", k);
       gsr_view& out = views[v];
       out.geom_buffer = c.gbase; out.binning_buffer = c.bbase; out.image_buffer = c.ibase;
       out.num_rendered = c.num_rendered; out.num_instances = c.num_instances;
