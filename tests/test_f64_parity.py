@@ -113,4 +113,4 @@ def test_gradients_within_float32_rounding_of_f64(case):
         _, g64d, _ = run_f64_path(inp, cams, gd, bound=False, lists=lists)
         st = rounding_stats(gg["_features_dc"], go["_features_dc"], g64d["_features_dc"],
                             B["_features_dc"], exclude=hit, C=C_BOUND)
-        assert st["gpu_fail"] > 0.05 * st["n_big"], st
+        assert st["gpu_fail"] >= max(20, 0.01 * st["n_big"]), st
