@@ -576,7 +576,7 @@ static int fwd_begin(const FwdModel& m, FwdCam& c) {
 
 // The read-back's values (already landed in c.host) -> the argument checks of
 // rasterizer_impl.cu:281-283 and the binning buffer, carved for the reference's count.
-static int fwd_bin_alloc(const FwdModel& m, FwdCam& c) {
+static int fwd_bin_alloc(const FwdModel& m, FwdCam& c, bool tag_by_dup = false) {
   const int debug = m.debug;
   hipStream_t stream = c.stream;
   const GeomState& g = c.g;
@@ -598,7 +598,9 @@ static int fwd_bin_alloc(const FwdModel& m, FwdCam& c) {
   c.b = carve_bin(c.bbase, R_ref, m.rows);  // capacity R_ref, the first R entries used
   // the layout this forward binned with, for a backward that only holds the buffer (the `_C`
   // signature: GSR_DEBUG_LAYOUT_FROM_BUFFER)
-  GSR_CHECK(hipMemsetD32Async((hipDeviceptr_t)c.b.tag, (int)bin_layout_tag(m.det, m.rows), 1, stream));
+  // (tag_by_dup: the duplicate kernel writes it, no fill launch of its own)
+  if (!tag_by_dup)
+    GSR_CHECK(hipMemsetD32Async((hipDeviceptr_t)c.b.tag, (int)bin_layout_tag(m.det, m.rows), 1, stream));
   c.num_rendered = (int)R_ref;
   c.num_instances = (int)R;
   return GSR_OK;
@@ -1257,6 +1259,7 @@ int views_forward_batched(const FwdModel& m, std::vector<FwdCam>& cams, gsr_view
     hipEvent_t ready = nullptr;
     std::vector<int> live;  // views with P > 0
     bool depth_in_b = false;
+    RenderArgs ras[kMaxBatchViews];  // the binned views' blend arguments (phase 2a -> 2b)
   };
   std::vector<Group> grp((size_t)ng);
   const int P = m.P;
@@ -1352,10 +1355,10 @@ int views_forward_batched(const FwdModel& m, std::vector<FwdCam>& cams, gsr_view
     PROF_END(SCAN);
     return GSR_OK;
   };
-  // phase 2 of a group: its read-back, then its binning and blend
-  auto phase2 = [&](int gi) -> int {
+  // phase 2a of a group: its read-back, then its binning (the blend's arguments left in G.ras)
+  auto phase2a = [&](int gi) -> int {
     Group& G = grp[(size_t)gi];
-    RenderArgs ras[kMaxBatchViews];
+    RenderArgs* ras = G.ras;
     hipStream_t stream = G.st;
     const int nl = (int)G.live.size();
     if (nl > 0) {
@@ -1387,7 +1390,7 @@ int views_forward_batched(const FwdModel& m, std::vector<FwdCam>& cams, gsr_view
       }
       for (int l = 0; l < nl; l++) {
         FwdCam& c = cams[(size_t)G.live[(size_t)l]];
-        if (int rc = fwd_bin_alloc(m, c)) return rc;  // (debug: checks the depth sort)
+        if (int rc = fwd_bin_alloc(m, c, /*tag_by_dup=*/true)) return rc;  // (debug: checks the depth sort)
         ht.mark("b", l);
         const GeomState& g = c.g;
         const BinState& b = c.b;
@@ -1397,7 +1400,7 @@ int views_forward_batched(const FwdModel& m, std::vector<FwdCam>& cams, gsr_view
                          SideClear{b.sort.aux, sort_clear_bytes(b.sort, R, tbits)},
                          SideClear{c.im.ranges, sizeof(uint2) * ntiles},
                          m.rows ? b.egid : nullptr, m.rows ? g.ebeg : nullptr,
-                         dup_drec() ? g.drec : nullptr};
+                         dup_drec() ? g.drec : nullptr, b.tag, bin_layout_tag(m.det, m.rows)};
         ts[l] = SortSpec{b.tkey_a, b.tval_a, b.tkey_b, b.tval_b, (size_t)R, b.sort, nullptr};
       }
       PROF_BEGIN(DUPLICATE);
@@ -1438,6 +1441,15 @@ int views_forward_batched(const FwdModel& m, std::vector<FwdCam>& cams, gsr_view
       GSR_CHECK(launch_render_schedule_views(ras, nl, stream));
       PROF_END(RANGES);
     }
+    return GSR_OK;
+  };
+  // phase 2b of a group: its blend (after every group's binning has been issued, so a group's
+  // latency-bound binning never queues for CUs behind another group's full-chip blend)
+  auto phase2b = [&](int gi) -> int {
+    Group& G = grp[(size_t)gi];
+    const RenderArgs* ras = G.ras;
+    hipStream_t stream = G.st;
+    const int nl = (int)G.live.size();
     // the group's stream joins the call's stream here; with GSR_VIEWS_RENDER_CALL the blend then
     // runs on the call's stream (the blends in group order there, the backward right behind
     // the last), else on the group's stream before the join
@@ -1485,11 +1497,22 @@ int views_forward_batched(const FwdModel& m, std::vector<FwdCam>& cams, gsr_view
     if (int rc = phase1(gi)) return rc;
     ht.mark("p", gi);
   }
+  // GSR_VIEWS_BIN_FIRST (default 1): every group's binning, then the blends; 0 = per group
+  // binning + blend (round 3's order)
+  static const bool bin_first = [] {
+    const char* e = getenv("GSR_VIEWS_BIN_FIRST");
+    return !(e && atoi(e) == 0);
+  }();
   for (int gi = 0; gi < ng; gi++) {
-    if (int rc = phase2(gi)) return rc;
+    if (int rc = phase2a(gi)) return rc;
+    if (!bin_first)
+      if (int rc = phase2b(gi)) return rc;
     if (gi + lead < ng)
       if (int rc = phase1(gi + lead)) return rc;
   }
+  if (bin_first)
+    for (int gi = 0; gi < ng; gi++)
+      if (int rc = phase2b(gi)) return rc;
   ht.mark("end", 0);
   g_last_instances = cams[(size_t)V - 1].num_instances;
   return GSR_OK;

@@ -284,6 +284,7 @@ __device__ __forceinline__ int batch_view(const uint32_t* first, int V, uint32_t
 __global__ __launch_bounds__(kThreads) void duplicate_views_kernel(DupViews m) {
   const int k = batch_view(m.first, m.V, blockIdx.x);
   const DupSpec& j = m.j[k];
+  if (j.tag && blockIdx.x == m.first[k] && threadIdx.x == 0) *j.tag = j.tag_val;
   duplicate_body(j.P, j.order, j.offsets, j.rec, j.gx, j.gy, j.tkey, j.tval, j.R, j.clear0,
                  j.clear1, j.egid, j.ebeg, blockIdx.x - m.first[k], m.first[k + 1] - m.first[k],
                  j.drec);

@@ -413,6 +413,8 @@ struct DupSpec {
   uint32_t* egid;
   uint32_t* ebeg;
   const float4* drec = nullptr;
+  uint32_t* tag = nullptr;  // written with tag_val by the launch (the binning buffer's layout tag)
+  uint32_t tag_val = 0;
 };
 hipError_t launch_duplicate_views(const DupSpec* v, int V, hipStream_t s);
 struct RangesSpec {
