@@ -219,7 +219,9 @@ int gsr_rasterize_gaussians_fused_backward_deferred(
  * rows writes per view the fused forward's colour clamp(SH(dir) + 0.5) (forward.cu:20-71), its
  * clamp bits [P] (u8) and the colour's direction Jacobian dRGB/d(dir_x, dir_y, dir_z)
  * (backward.cu:56-131), colour and Jacobian PLANAR: color[c * P + i] ([3][P]) and
- * jac[(3 * r + c) * P + i] = d colour_c / d dir_r ([9][P]).  campos / color / clamped / jac: HOST arrays of nviews DEVICE pointers. */
+ * jac[(3 * r + c) * P + i] = d colour_c / d dir_r ([9][P]).  campos / color / clamped / jac: HOST arrays of nviews DEVICE pointers.
+ * Either part may be skipped: color and clamped both NULL (the Jacobian only), or jac NULL (the
+ * colour only) -- the forward needs the colour before it starts, the Jacobian only its backward. */
 int gsr_sh_precolor(int P, int M, int degree, const float* means3D, const float* features_dc,
                     const float* features_rest, int nviews, const float* const* campos,
                     float* const* color, uint8_t* const* clamped, float* const* jac, void* stream);

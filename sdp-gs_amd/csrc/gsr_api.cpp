@@ -1822,18 +1822,26 @@ int gsr_sh_precolor(int P, int M, int degree, const float* means3D, const float*
   if (P == 0 || nviews == 0) return GSR_OK;
   if (M < 1 || M > 16 || degree < 0 || degree > 3 || (degree + 1) * (degree + 1) > M)
     return fail(GSR_ERR_ARGUMENT, "invalid sh degree %d for M = %d", degree, M);
-  if (!means3D || !features_dc || (M > 1 && !features_rest) || !campos || !color || !clamped || !jac)
+  if (!means3D || !features_dc || (M > 1 && !features_rest) || !campos)
     return fail(GSR_ERR_ARGUMENT, "null pointer");
+  // either part may be left out: color + clamped both NULL (the Jacobian only) or jac NULL (the
+  // colour only), e.g. the colour ahead of the forward and the Jacobian on another stream
+  const bool want_col = color || clamped, want_jac = jac != nullptr;
+  if ((color == nullptr) != (clamped == nullptr) || !(want_col || want_jac))
+    return fail(GSR_ERR_ARGUMENT, "color and clamped go together, and one part is needed");
   for (int v0 = 0; v0 < nviews; v0 += kShFlushMaxViewsFwd) {
     PrecolorArgs a{};
     a.P = P; a.M = M; a.D = degree; a.means3D = means3D; a.sh_dc = features_dc;
     a.sh_rest = features_rest;
     a.nviews = nviews - v0 < kShFlushMaxViewsFwd ? nviews - v0 : kShFlushMaxViewsFwd;
     for (int v = 0; v < a.nviews; v++) {
-      if (!campos[v0 + v] || !color[v0 + v] || !clamped[v0 + v] || !jac[v0 + v])
+      if (!campos[v0 + v] || (want_col && (!color[v0 + v] || !clamped[v0 + v])) ||
+          (want_jac && !jac[v0 + v]))
         return fail(GSR_ERR_ARGUMENT, "null view pointer");
-      a.campos[v] = campos[v0 + v]; a.color[v] = color[v0 + v];
-      a.clamp[v] = clamped[v0 + v]; a.jac[v] = jac[v0 + v];
+      a.campos[v] = campos[v0 + v];
+      a.color[v] = want_col ? color[v0 + v] : nullptr;
+      a.clamp[v] = want_col ? clamped[v0 + v] : nullptr;
+      a.jac[v] = want_jac ? jac[v0 + v] : nullptr;
     }
     PROF_BEGIN(SH_PRECOLOR);
     GSR_CHECK(launch_sh_precolor(a, stream));

@@ -335,6 +335,7 @@ constexpr int kPcThreads = GSR_SH_THREADS;
 // view: sh_to_rgb (forward.cu:20-71, the forward's own function) -> colour [3][P] + clamp bits,
 // and sh_dir_jacobian (backward.cu:56-131) -> dRGB/ddir [9][P].  The rows go through LDS
 // (gsr_stage.h) so the global reads are coalesced 16-byte vectors.
+template <bool COL, bool JAC>
 __global__ __launch_bounds__(kPcThreads) void sh_precolor_kernel(PrecolorArgs a) {
   __shared__ float4 s_sh4[kPcThreads * kShMaxFloats / 4];
   __shared__ uint8_t s_live[kPcThreads];
@@ -355,10 +356,12 @@ __global__ __launch_bounds__(kPcThreads) void sh_precolor_kernel(PrecolorArgs a)
   const float* r1 = s_sh + p1.lds + t * p1.w;
   const int used = (a.D + 1) * (a.D + 1);
   V3 c[16];
-  c[0] = v3(r0[0], r0[1], r0[2]);
+  if (JAC) {
+    c[0] = v3(r0[0], r0[1], r0[2]);
 #pragma unroll
-  for (int k = 1; k < 16; k++)
-    c[k] = (k < used && k < a.M) ? v3(r1[3 * k - 3], r1[3 * k - 2], r1[3 * k - 1]) : v3(0, 0, 0);
+    for (int k = 1; k < 16; k++)
+      c[k] = (k < used && k < a.M) ? v3(r1[3 * k - 3], r1[3 * k - 2], r1[3 * k - 1]) : v3(0, 0, 0);
+  }
   const V3 p_orig = v3(a.means3D[3 * i], a.means3D[3 * i + 1], a.means3D[3 * i + 2]);
   for (int v = 0; v < a.nviews; v++) {
     const float* cp = a.campos[v];
@@ -366,14 +369,17 @@ __global__ __launch_bounds__(kPcThreads) void sh_precolor_kernel(PrecolorArgs a)
     // forward: gsr_preprocess_kernel's direction and colour
     const float len = sqrtf(dot3(dir_orig, dir_orig));
     const V3 dir = v3(dir_orig.x / len, dir_orig.y / len, dir_orig.z / len);
-    uint8_t cl;
-    const V3 col = sh_to_rgb(r0, r1, a.D, dir, cl);
     // planar outputs ([3][P] colour, [9][P] Jacobian): every store instruction of the wave is
     // one contiguous 256-byte run, and so is every load of the consuming preprocesses
     const size_t P = (size_t)a.P;
-    float* co = a.color[v] + i;
-    stream_st(co, col.x); stream_st(co + P, col.y); stream_st(co + 2 * P, col.z);
-    stream_st(a.clamp[v] + i, cl);
+    if (COL) {
+      uint8_t cl;
+      const V3 col = sh_to_rgb(r0, r1, a.D, dir, cl);
+      float* co = a.color[v] + i;
+      stream_st(co, col.x); stream_st(co + P, col.y); stream_st(co + 2 * P, col.z);
+      stream_st(a.clamp[v] + i, cl);
+    }
+    if (!JAC) continue;
     // backward: sh_backward's Jacobian at the same normalised direction
     V3 jx, jy, jz;
     sh_dir_jacobian(c, a.D, dir, jx, jy, jz);
@@ -428,8 +434,13 @@ hipError_t launch_preprocess_views(const PreArgs* views, int V, hipStream_t s) {
 
 hipError_t launch_sh_precolor(const PrecolorArgs& a, hipStream_t s) {
   if (a.P == 0 || a.nviews <= 0) return hipSuccess;
-  hipLaunchKernelGGL(sh_precolor_kernel, dim3((a.P + kPcThreads - 1) / kPcThreads), dim3(kPcThreads), 0,
-                     s, a);
+  const dim3 grid((a.P + kPcThreads - 1) / kPcThreads);
+  if (a.color[0] && a.jac[0])
+    hipLaunchKernelGGL((sh_precolor_kernel<true, true>), grid, dim3(kPcThreads), 0, s, a);
+  else if (a.color[0])
+    hipLaunchKernelGGL((sh_precolor_kernel<true, false>), grid, dim3(kPcThreads), 0, s, a);
+  else
+    hipLaunchKernelGGL((sh_precolor_kernel<false, true>), grid, dim3(kPcThreads), 0, s, a);
   return hipGetLastError();
 }
 

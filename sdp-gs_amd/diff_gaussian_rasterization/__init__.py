@@ -318,6 +318,7 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
         ctx.gsr_flags = _debug_flags(rs.debug)
         ctx.num_rendered = num_rendered
         ctx.pre_jac = None if pre is None else pre[2]
+        ctx.jac_event = None if pre is None else _jac_ready(dev)
         # grad-into-leaves mode: only when every differentiable input is itself the float32
         # contiguous leaf (then the kernel's pointer IS the parameter's storage)
         leaves = (means3D, features_dc, features_rest, opacity_raw, scaling_raw, rotation_raw,
@@ -415,6 +416,8 @@ class _RasterizeGaussiansFused(torch.autograd.Function):
         stream = cur.cuda_stream
         if into_leaves:
             _order_leaf_grads(dev, cur)
+        if d_rgb is not None and ctx.pre_jac is not None and ctx.jac_event is not None:
+            cur.wait_event(ctx.jac_event)  # the Jacobian came from the pre-pass's side stream
         with _lib.on_device(dev):
             rc = L.gsr_rasterize_gaussians_fused_backward_deferred(
                 P, M, ctx.num_rendered, _ptr(bg), _ptr(m3), _ptr(radii), _ptr(dc), _ptr(rest),
@@ -567,6 +570,7 @@ class _RasterizeViewsFused(torch.autograd.Function):
         ctx.gsr_flags = flags
         ctx.cams = cams
         ctx.pre_jacs = [None if p is None else p[2] for p in pres]
+        ctx.jac_event = _jac_ready(dev) if any(p is not None for p in pres) else None
         leaves = (means3D, features_dc, features_rest, opacity_raw, scaling_raw, rotation_raw,
                   language_feature)
         used = (m3, dc, rest, op, sc, rot, lf)
@@ -670,6 +674,8 @@ class _RasterizeViewsFused(torch.autograd.Function):
         cur = torch.cuda.current_stream(dev)
         if into_leaves:
             _order_leaf_grads(dev, cur)
+        if d_rgb is not None and ctx.jac_event is not None:
+            cur.wait_event(ctx.jac_event)  # the Jacobians came from the pre-pass's side stream
         t_host = time.perf_counter()
         args = (V, views, H, W, P, M, _ptr(bg), _ptr(m3), _ptr(dc), _ptr(rest), _ptr(op),
                 _ptr(sc), _ptr(rot), mt["scale_modifier"], mt["degree"], _ptr(lf), _ptr(conf),
@@ -743,6 +749,13 @@ def _precolor_lookup(dev, campos, m3, dc, rest, degree, M):
     return pc.lookup(campos, m3, dc, rest, degree, M)
 
 
+def _jac_ready(dev):
+    """The active pre-pass's Jacobian-done event (None: written on the pre-pass's own stream
+    ahead of everything, nothing to wait for); a backward reading pre_jac waits for it."""
+    pc = _PRECOLOR.get(dev.index)
+    return None if pc is None else pc.jac_event
+
+
 class ShPrecolor:
     """Multi-view colour pre-pass of one step on one device (include/gsr.h gsr_sh_precolor).
     One pass over the SH rows computes, for every camera of the step, the fused forward's colour
@@ -751,10 +764,16 @@ class ShPrecolor:
     reading the 192-byte SH rows again, and -- under ShGradDeferral -- so do their backwards.
     Outputs are identical (the same device functions, gsr_sh.h)."""
 
-    def __init__(self, means3D, features_dc, features_rest, degree, campos_list, buffers=None):
+    def __init__(self, means3D, features_dc, features_rest, degree, campos_list, buffers=None,
+                 jac_stream=None):
         """buffers: optional list of (colour [3,P], clamp [P] u8, Jacobian [9,P]) per camera to
         reuse (written on the current stream, so every earlier reader must be ordered before it).
-        Colour and Jacobian are planar (include/gsr.h gsr_sh_precolor)."""
+        Colour and Jacobian are planar (include/gsr.h gsr_sh_precolor).
+
+        jac_stream: the Jacobians (needed by the backward only) are computed there, after the
+        current stream's work so far, while the colours (needed before the forward) are computed
+        on the current stream -- the step's forward starts after the colour part alone; the
+        backwards that read a Jacobian wait for `jac_event`."""
         self.device = means3D.device
         self.keys = (means3D.data_ptr(), features_dc.data_ptr(),
                      features_rest.data_ptr() if features_rest is not None else 0, int(degree))
@@ -771,15 +790,33 @@ class ShPrecolor:
                      torch.empty((P,), dtype=torch.uint8, device=self.device),
                      torch.empty((9, P), **fopts)) for _ in cams]
         self.buffers = bufs
+        self.jac_event = None
         n = len(cams)
         if n and P:
             arr = lambda xs: (_lib.ctypes.c_void_p * n)(*[x.data_ptr() for x in xs])  # noqa: E731
+            m3c = means3D.contiguous()
+            L = _lib.load()
+            head = (P, self.M, int(degree), _ptr(m3c), _ptr(features_dc), _ptr(features_rest), n,
+                    arr(cams))
+            cols = (arr([b[0] for b in bufs]), arr([b[1] for b in bufs]))
+            jacs = arr([b[2] for b in bufs])
             with _lib.on_device(self.device):
-                rc = _lib.load().gsr_sh_precolor(
-                    P, self.M, int(degree), _ptr(means3D.contiguous()), _ptr(features_dc),
-                    _ptr(features_rest), n, arr(cams), arr([b[0] for b in bufs]),
-                    arr([b[1] for b in bufs]), arr([b[2] for b in bufs]),
-                    _lib.raw_stream(self.device))
+                if jac_stream is None:
+                    rc = L.gsr_sh_precolor(*head, *cols, jacs, _lib.raw_stream(self.device))
+                else:
+                    rc = L.gsr_sh_precolor(*head, *cols, None, _lib.raw_stream(self.device))
+                    if rc == 0:
+                        # after the current stream's work so far: the previous step's readers
+                        # of these buffers, and the inputs
+                        jac_stream.wait_stream(torch.cuda.current_stream(self.device))
+                        rc = L.gsr_sh_precolor(*head, None, None, jacs, jac_stream.cuda_stream)
+                        self.jac_event = torch.cuda.Event()
+                        self.jac_event.record(jac_stream)
+                        for b in bufs:
+                            b[2].record_stream(jac_stream)
+                        m3c.record_stream(jac_stream)
+                        for c in cams:
+                            c.record_stream(jac_stream)
             _lib.check(rc)
         for c, b in zip(cams, bufs):
             self.views[c.data_ptr()] = b
