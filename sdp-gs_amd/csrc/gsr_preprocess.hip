@@ -209,9 +209,10 @@ __device__ __forceinline__ uint32_t rec_swizzle(uint32_t lane) { return (lane >>
 // (__launch_bounds__(256, 6), 80 VGPRs with a 12-byte spill, measured equal to the unbounded 82)
 // The workgroup's outputs after its lanes' preprocess_gaussian: the records (from LDS), the
 // zeroed accumulator rows and the partial sums of the tile counts.
-__device__ __forceinline__ void pre_epilogue(const PreArgs& a, int base, int n, uint32_t count,
-                                             uint32_t rect, const float4* s_rec,
-                                             uint32_t* s_sum, uint32_t* s_rect) {
+__device__ __forceinline__ void pre_epilogue_blk(const PreArgs& a, int base, int n, uint32_t count,
+                                                 uint32_t rect, const float4* s_rec,
+                                                 uint32_t* s_sum, uint32_t* s_rect, uint32_t blk,
+                                                 uint32_t nblk) {
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) {
     count += (uint32_t)__shfl_xor((int)count, d, 64);
@@ -239,9 +240,14 @@ __device__ __forceinline__ void pre_epilogue(const PreArgs& a, int base, int n, 
       t += s_sum[w];
       tr += s_rect[w];
     }
-    a.parts[blockIdx.x] = t;
-    a.parts[gridDim.x + blockIdx.x] = tr;
+    a.parts[blk] = t;
+    a.parts[nblk + blk] = tr;
   }
+}
+__device__ __forceinline__ void pre_epilogue(const PreArgs& a, int base, int n, uint32_t count,
+                                             uint32_t rect, const float4* s_rec,
+                                             uint32_t* s_sum, uint32_t* s_rect) {
+  pre_epilogue_blk(a, base, n, count, rect, s_rec, s_sum, s_rect, blockIdx.x, gridDim.x);
 }
 
 // (__launch_bounds__(256, 6), 80 VGPRs with a 12-byte spill, measured equal to the unbounded 82)
@@ -319,6 +325,31 @@ __global__ __launch_bounds__(kThreads, GSR_PRE_VIEWS_MINBLK) void preprocess_vie
     pre_epilogue(a, base, n, count, rect, s_rec, s_sum, s_rect);
     __syncthreads();  // s_rec / s_sum are the next view's
   }
+}
+
+// The same views in one launch with one view per workgroup instead of all of them per lane
+// (GSR_PRE_VIEWS_SPLIT=1, round 4): workgroup b runs preprocess_kernel's body for view b % V over
+// Gaussian block b / V -- the view-independent part and the model rows once per view again (the
+// V workgroups of a block are dispatched together, so the re-reads are cache hits), but every
+// lane's chain is one view long and the launch has V times the workgroups.
+__global__ __launch_bounds__(kThreads) void preprocess_views_split_kernel(PreViews m) {
+  __shared__ float4 s_rec[kThreads * kRecStride];
+  __shared__ uint32_t s_sum[kThreads / 64], s_rect[kThreads / 64];
+  const uint32_t k = blockIdx.x % (uint32_t)m.V, blk = blockIdx.x / (uint32_t)m.V;
+  const PreArgs& a = m.v[k];
+  const uint32_t nblk = gridDim.x / (uint32_t)m.V;
+  const int base = (int)(blk * kThreads);
+  const int idx = base + (int)threadIdx.x;
+  const int n = min(kThreads, a.P - base);
+  side_clear(a.clear.p, a.clear.bytes, (size_t)idx, (size_t)nblk * kThreads);
+  const float* pm = a.means3D + 3 * (size_t)idx;
+  const float* ps = a.scales + 3 * (size_t)idx;
+  const float* pl = a.sh_language + 3 * (size_t)idx;
+  uint32_t rect = 0;
+  const uint32_t count = idx < a.P ? preprocess_gaussian(a, idx, s_rec + threadIdx.x * kRecStride,
+                                                         rec_swizzle(threadIdx.x), pm, ps, pl,
+                                                         rect, nullptr) : 0u;
+  pre_epilogue_blk(a, base, n, count, rect, s_rec, s_sum, s_rect, blk, nblk);
 }
 
 // Workgroup size of the SH-row kernels (colour pre-pass here, SH flush in gsr_backward.hip):
@@ -427,8 +458,15 @@ hipError_t launch_preprocess_views(const PreArgs* views, int V, hipStream_t s) {
       return hipErrorInvalidValue;
     m.v[k] = a;
   }
-  hipLaunchKernelGGL(preprocess_views_kernel, dim3((a0.P + kThreads - 1) / kThreads),
-                     dim3(kThreads), 0, s, m);
+  static const bool split = [] {
+    const char* e = getenv("GSR_PRE_VIEWS_SPLIT");
+    return e && atoi(e) == 1;
+  }();
+  const uint32_t nblk = (uint32_t)((a0.P + kThreads - 1) / kThreads);
+  if (split)
+    hipLaunchKernelGGL(preprocess_views_split_kernel, dim3(nblk * (uint32_t)V), dim3(kThreads), 0, s, m);
+  else
+    hipLaunchKernelGGL(preprocess_views_kernel, dim3(nblk), dim3(kThreads), 0, s, m);
   return hipGetLastError();
 }
 
