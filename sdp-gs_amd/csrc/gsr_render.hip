@@ -1301,13 +1301,26 @@ static int bwd_pipe() {
 // 57 per wave while the 16-bit masks and four lists per batch cost more than that saved.
 // ================================================================================================
 
-// lane -> pixel: quadrant (w & 1, w >> 1); block g = (lane >> 1) & 3 at (g & 1, g >> 1) inside
-// it; inside the block x = bit0 + 2 bit3, y = bit4 + 2 bit5 of the lane
+// lane -> pixel: quadrant (w & 1, w >> 1); block g = blk_group(lane) at (g & 1, g >> 1) inside
+// it.  GSR_FWD_GROUP_ROWS (default 1, round 4): block g is lanes 16 g .. 16 g + 15 (x = lane & 3,
+// y = (lane >> 2) & 3), i.e. exactly one of ds_read_b128's 16-lane groups, so a group's record
+// reads are one address (a broadcast) and never conflict across the four blocks' records (round 3
+// 's map, g = lane bits 1-2 with x = bit0 + 2 bit3, y = bit4 + 2 bit5, put all four blocks in
+// every 16-lane group: a 2-way bank conflict whenever two of the four records share an index mod
+// 16).  Per pixel the blend is unchanged: outputs bit-identical either way.
+#ifndef GSR_FWD_GROUP_ROWS
+#define GSR_FWD_GROUP_ROWS 1
+#endif
+__device__ __forceinline__ uint32_t blk_group(uint32_t l) {
+  return GSR_FWD_GROUP_ROWS ? (l >> 4) : ((l >> 1) & 3u);
+}
 __device__ __forceinline__ void pixel_of_blk(uint32_t tx, uint32_t ty, uint32_t t, uint32_t& px,
                                              uint32_t& py) {
-  const uint32_t w = t >> 6, l = t & 63u, g = (l >> 1) & 3u;
-  px = tx * kTile + (w & 1u) * 8u + (g & 1u) * 4u + ((l & 1u) | ((l >> 2) & 2u));
-  py = ty * kTile + (w >> 1) * 8u + (g >> 1) * 4u + ((l >> 4) & 3u);
+  const uint32_t w = t >> 6, l = t & 63u, g = blk_group(l);
+  const uint32_t bx = GSR_FWD_GROUP_ROWS ? (l & 3u) : ((l & 1u) | ((l >> 2) & 2u));
+  const uint32_t by = GSR_FWD_GROUP_ROWS ? ((l >> 2) & 3u) : ((l >> 4) & 3u);
+  px = tx * kTile + (w & 1u) * 8u + (g & 1u) * 4u + bx;
+  py = ty * kTile + (w >> 1) * 8u + (g >> 1) * 4u + by;
 }
 
 // Which of the 16 4x4 blocks a splat can reach: bit 4w + g for block g of quadrant w.  The exact
@@ -1403,7 +1416,7 @@ __device__ __forceinline__ void render_fwd_blk_tile(const RenderArgs& a, uint32_
   __shared__ uint32_t s_max;
   const int lane = (int)(threadIdx.x & 63);
   const int wid = (int)(threadIdx.x >> 6);
-  const uint32_t grp = ((uint32_t)lane >> 1) & 3u;
+  const uint32_t grp = blk_group((uint32_t)lane);
 
   const uint32_t ntiles = a.gx * a.gy;
   side_clear(a.clear.p, a.clear.bytes, (size_t)blk * kThreads + threadIdx.x, (size_t)ntiles * kThreads);
