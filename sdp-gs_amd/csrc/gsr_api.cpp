@@ -1497,11 +1497,14 @@ int views_forward_batched(const FwdModel& m, std::vector<FwdCam>& cams, gsr_view
     if (int rc = phase1(gi)) return rc;
     ht.mark("p", gi);
   }
-  // GSR_VIEWS_BIN_FIRST (default 1): every group's binning, then the blends; 0 = per group
-  // binning + blend (round 3's order)
+  // GSR_VIEWS_BIN_FIRST=1: every group's binning, then the blends; default 0 = per group binning
+  // + blend.  Round 4 (profiles/r04_pipeline_ab.txt): 2090 / 2107 views/s with it against 2096 /
+  // 2117 without -- the later group's binning then overlaps the earlier group's blend (a full-chip
+  // launch) instead of running beside the other latency-bound binning, which hides as much
+  // latency as it saves queueing
   static const bool bin_first = [] {
     const char* e = getenv("GSR_VIEWS_BIN_FIRST");
-    return !(e && atoi(e) == 0);
+    return e && atoi(e) == 1;
   }();
   for (int gi = 0; gi < ng; gi++) {
     if (int rc = phase2a(gi)) return rc;

@@ -157,10 +157,12 @@ class ViewPipeline:
         main = torch.cuda.current_stream(self.device)
         pre = contextlib.nullcontext()
         if self.precolor and model is not None and items:
-            # the colour Jacobians (backward only) on the last side stream, which the one-call
-            # multi-view step leaves free (GSR_PRECOLOR_SPLIT=0: one kernel ahead of the forward)
+            # GSR_PRECOLOR_SPLIT=1: the colour Jacobians (backward only) on the last side stream,
+            # which the one-call multi-view step leaves free; default one kernel ahead of the
+            # forward (round 4: 2090 / 2107 views/s split against 2116 / 2111 not split,
+            # profiles/r04_pipeline_ab.txt -- the forward's head is latency-bound, not the pass)
             js = (self.side[-1] if jac_side and len(self.side) >= 2
-                  and os.environ.get("GSR_PRECOLOR_SPLIT", "1") != "0" else None)
+                  and os.environ.get("GSR_PRECOLOR_SPLIT", "0") == "1" else None)
             pre = dgr.ShPrecolor(model._xyz, model._features_dc, model._features_rest,
                                  model.active_sh_degree, [campos_of(it) for it in items],
                                  buffers=self._pre_bufs, jac_stream=js)
