@@ -88,8 +88,10 @@ __device__ __forceinline__ uint32_t preprocess_gaussian(const PreArgs& a, int id
                                                         const float* ps, const float* pl,
                                                         uint32_t& rect_tiles,
                                                         const PreModelIn* in) {
+  // zeros in the same swizzled slots as the record (k -> k ^ sw): unswizzled, the 8 lanes of a
+  // ds_write_b128 group hit 2 slots four ways each (profiles/pmc_r04.json: 4.5 M conflict cycles)
 #pragma unroll
-  for (int k = 0; k < 4; k++) rec[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int k = 0; k < 4; k++) rec[k ^ sw] = make_float4(0.f, 0.f, 0.f, 0.f);
   rect_tiles = 0;
   const V3 p_orig = in ? in->p_orig : v3(pm[0], pm[1], pm[2]);
   const V3 p_view = xform_point43(p_orig, a.view);
