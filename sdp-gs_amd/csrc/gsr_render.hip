@@ -1392,6 +1392,12 @@ __device__ __forceinline__ uint32_t build_group_lists(const uint16_t* s_mask, ui
   return grp == 0 ? n[0] : grp == 1 ? n[1] : grp == 2 ? n[2] : n[3];
 }
 
+// GSR_FWD_LAZY=1: the block-list forward reads a group's channel values (colour, depth,
+// feature) after its four alpha tests instead of with the geometry, so they are not live in
+// VGPRs through the tests (more waves per SIMD)
+#ifndef GSR_FWD_LAZY
+#define GSR_FWD_LAZY 0
+#endif
 // waves per SIMD the block-list forward is compiled for (VGPR budget 512 / n); 5 measured
 // slower (96 VGPRs with 16 spilled: 0.116 -> 0.122 ms), so the default lets it take 118
 #ifndef GSR_FWD_BLK_WAVES
@@ -1495,8 +1501,10 @@ __device__ __forceinline__ void render_fwd_blk_tile(const RenderArgs& a, uint32_
         jj[u] = (packed >> (8 * u)) & 0xffu;
         const float4 r0 = s_r0[jj[u]];
         r1v[u] = s_r1[jj[u]];
-        r2v[u] = s_r2[jj[u]];
-        f2v[u] = FEAT ? s_f2[jj[u]] : 0.0f;
+        if (!GSR_FWD_LAZY) {
+          r2v[u] = s_r2[jj[u]];
+          f2v[u] = FEAT ? s_f2[jj[u]] : 0.0f;
+        }
         const float dx = r0.x - pfx, dy = r0.y - pfy;
         const float power = -0.5f * (r0.z * dx * dx + r1v[u].x * dy * dy) - r0.w * dx * dy;
         // entries past the group's list end get power = +1 and are skipped
@@ -1523,6 +1531,17 @@ __device__ __forceinline__ void render_fwd_blk_tile(const RenderArgs& a, uint32_
       // `done` branches below and serialises the exps
       asm volatile("" ::"v"(al[0]), "v"(al[1]), "v"(al[2]), "v"(al[3]), "v"(pw[0]), "v"(pw[1]),
                    "v"(pw[2]), "v"(pw[3]));
+#endif
+#if GSR_FWD_LAZY
+      // the channel values of the four entries are read only now: no LDS access crosses this
+      // point, so they are not live (and held in VGPRs) through the alpha tests above
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        r1v[u] = s_r1[jj[u]];
+        r2v[u] = s_r2[jj[u]];
+        f2v[u] = FEAT ? s_f2[jj[u]] : 0.0f;
+      }
 #endif
 #pragma unroll
       for (int u = 0; u < 4; u++) {
