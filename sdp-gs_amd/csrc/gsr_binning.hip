@@ -64,8 +64,19 @@ __device__ __forceinline__ void duplicate_body_lds(int P, const uint32_t* __rest
   // last valid lane's end
   const uint32_t obase = (uint32_t)__shfl((int)off, 0, 64);
   const uint32_t oend = (uint32_t)__shfl((int)end, min(P - 1 - sw0, 63), 64);
-  uint32_t gid = 0, y = 0, y1 = 0, x0 = 0, x1 = 0, x = 0, xe = 0;
+  uint32_t gid = 0, y = 0, y0 = 0, y1 = 0, x0 = 0, x1 = 0, x = 0, xe = 0;
+  uint32_t rows = kNoRowPack;  // the preprocess's packed per-row ranges (rec[3].w)
   SplatCut cut{};
+  // the kept tiles of row y: from the packed ranges, else the cut itself (cut_row_range)
+  auto row_range = [&](uint32_t yy) {
+    if (rows != kNoRowPack) {
+      const uint32_t b = (rows >> (8 * (yy - y0))) & 0xffu;
+      x = x0 + (b & 15u);
+      xe = x + (b >> 4);
+    } else {
+      cut_row_range(cut, yy, x0, x1, x, xe);
+    }
+  };
   if (off < end) {
     float4 r0;
     float qc, rad;
@@ -85,13 +96,13 @@ __device__ __forceinline__ void duplicate_body_lds(int P, const uint32_t* __rest
       cc = r1.x;
       qc = r3.z;
       rad = r3.y;
+      rows = __float_as_uint(r3.w);
     }
     if (egid) ebeg[gid] = off;
-    uint32_t y0;
     tile_rect(r0.x, r0.y, (int)rad, gx, gy, x0, y0, x1, y1);
-    cut = make_cut(r0.x, r0.y, r0.z, r0.w, cc, qc);
+    if (rows == kNoRowPack) cut = make_cut(r0.x, r0.y, r0.z, r0.w, cc, qc);
     y = y0;
-    if (y < y1) cut_row_range(cut, y, x0, x1, x, xe);
+    if (y < y1) row_range(y);
     else off = end;
   }
   for (uint32_t wbeg = obase; wbeg < oend; wbeg += kWin) {
@@ -103,7 +114,7 @@ __device__ __forceinline__ void duplicate_body_lds(int P, const uint32_t* __rest
           off = end;
           break;
         }
-        cut_row_range(cut, y, x0, x1, x, xe);
+        row_range(y);
         continue;
       }
       s_key[wid][off - wbeg] = y * gx + x;

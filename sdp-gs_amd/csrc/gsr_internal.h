@@ -239,6 +239,8 @@ BinState carve_bin(char* base, size_t R, bool rows = false);
 // false = float atomics into one accumulator row per Gaussian.  The deterministic backward always
 // uses rows.  Fixed for the process, so a forward's layout is the one its backward expects.
 bool bwd_rows_mode();
+// rec[3].w of a splat record whose per-row tile ranges did not fit the packing (gsr_preprocess.hip)
+constexpr uint32_t kNoRowPack = 0xffffffffu;
 constexpr uint32_t kBinLayoutMagic = 0x47535200u;  // "GSR\0"
 inline uint32_t bin_layout_tag(bool det, bool rows) {
   return kBinLayoutMagic | (det ? 2u : 0u) | (rows ? 1u : 0u);

@@ -9,10 +9,10 @@
 //   rec[4g+0] = {x_px, y_px, conic.a, conic.b}
 //   rec[4g+1] = {conic.c, opacity*confidence, depth, r}
 //   rec[4g+2] = {g, b, f0, f1}
-//   rec[4g+3] = {f2, radius, q_cut, count} (radius as float: exact; q_cut: the culling threshold of
+//   rec[4g+3] = {f2, radius, q_cut, rows} (radius as float: exact; q_cut: the culling threshold of
 //                                        gsr_device.h, computed once here for the binning and blends;
-//                                        count: the exact tile count, as bits -- the depth sort's
-//                                        last pass gathers it with the binning fields)
+//                                        rows: the kept tile range of each row, packed (kNoRowPack:
+//                                        not packed), so the duplication does not re-run the cut)
 // so the blend reads one contiguous record per instance instead of five scattered arrays.
 #include "gsr_device.h"
 #include "gsr_internal.h"
@@ -158,8 +158,14 @@ __device__ __forceinline__ uint32_t preprocess_gaussian(const PreArgs& a, int id
   // in which no pixel can reach alpha >= 1/255 are dropped here (no output bit changes)
   const float qc = splat_q_cut(con_a, con_b, con_c, op);
   uint32_t count = 0;
+  // the kept per-row ranges, packed for the duplication when the rectangle has at most 4 rows
+  // of at most 15 tiles (row r: bits 8r..8r+3 = first tile - x0, bits 8r+4..8r+7 = its length)
+  const bool pack = (y1 - y0) <= 4u && (x1 - x0) <= 15u;
+  uint32_t packed = pack ? 0u : kNoRowPack;
   if (qc == -1.0f) {
     count = (y1 - y0) * (x1 - x0);
+    if (pack)
+      for (uint32_t r = 0; r < y1 - y0; r++) packed |= ((x1 - x0) << 4) << (8 * r);
   } else if (qc >= 0.0f) {
     // per tile row, the kept tiles form one range (cut_row_range): found from both ends
     const SplatCut cut = make_cut(px, py, con_a, con_b, con_c, qc);
@@ -167,6 +173,7 @@ __device__ __forceinline__ uint32_t preprocess_gaussian(const PreArgs& a, int id
       uint32_t ra, rb;
       cut_row_range(cut, ty, x0, x1, ra, rb);
       count += rb - ra;
+      if (pack) packed |= ((ra - x0) | ((rb - ra) << 4)) << (8 * (ty - y0));
     }
   }
   g.tiles_touched[idx] = count;
@@ -174,7 +181,7 @@ __device__ __forceinline__ uint32_t preprocess_gaussian(const PreArgs& a, int id
   rec[0 ^ sw] = make_float4(px, py, con_a, con_b);
   rec[1 ^ sw] = make_float4(con_c, op, depth, cr);
   rec[2 ^ sw] = make_float4(cg, cb, in->f0, in->f1);
-  rec[3 ^ sw] = make_float4(in->f2, (float)r, qc, __uint_as_float(count));
+  rec[3 ^ sw] = make_float4(in->f2, (float)r, qc, __uint_as_float(packed));
   return count;
 }
 

@@ -337,7 +337,7 @@ __device__ __forceinline__ void onesweep_body(
     if (rpay) {
       const float4* r = rpay + 4 * (size_t)min(v, (uint32_t)n - 1u);
       const float4 r0 = r[0], r1 = r[1], r3 = r[3];
-      kout[o] = __float_as_uint(r3.w);
+      kout[o] = kpay ? kpay[min(v, (uint32_t)n - 1u)] : __float_as_uint(r3.w);
       rout[2 * (size_t)o] = r0;
       rout[2 * (size_t)o + 1] = make_float4(r1.x, r3.z, r3.y, __uint_as_float(v));
     } else {
