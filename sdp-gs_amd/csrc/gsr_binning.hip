@@ -14,6 +14,12 @@
 #include "gsr_device.h"
 #include "gsr_internal.h"
 
+// 1: the duplication takes each Gaussian's kept tile range per row from the preprocess's packed
+// rec[3].w (rectangles of at most 4 rows x 15 tiles) instead of re-running cut_row_range
+#ifndef GSR_DUP_ROWPACK
+#define GSR_DUP_ROWPACK 1
+#endif
+
 namespace gsr {
 namespace {
 
@@ -96,7 +102,7 @@ __device__ __forceinline__ void duplicate_body_lds(int P, const uint32_t* __rest
       cc = r1.x;
       qc = r3.z;
       rad = r3.y;
-      rows = __float_as_uint(r3.w);
+      if (GSR_DUP_ROWPACK) rows = __float_as_uint(r3.w);
     }
     if (egid) ebeg[gid] = off;
     tile_rect(r0.x, r0.y, (int)rad, gx, gy, x0, y0, x1, y1);
