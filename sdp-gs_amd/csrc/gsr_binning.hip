@@ -97,12 +97,12 @@ __device__ __forceinline__ void duplicate_body_lds(int P, const uint32_t* __rest
     } else {
       gid = min(order[s], (uint32_t)P - 1u);
       r0 = rec[4 * (size_t)gid];
-      const float4 r1 = rec[4 * (size_t)gid + 1];
       const float4 r3 = rec[4 * (size_t)gid + 3];
-      cc = r1.x;
       qc = r3.z;
       rad = r3.y;
       if (GSR_DUP_ROWPACK) rows = __float_as_uint(r3.w);
+      // conic.c only for the cut itself (rows not packed)
+      cc = rows == kNoRowPack ? rec[4 * (size_t)gid + 1].x : 0.0f;
     }
     if (egid) ebeg[gid] = off;
     tile_rect(r0.x, r0.y, (int)rad, gx, gy, x0, y0, x1, y1);
