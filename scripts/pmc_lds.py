@@ -9,7 +9,7 @@ import sys
 
 def klass(name):
     """the kernel's own name, without namespaces and template arguments"""
-    base = name.split("(")[0].split("<")[0]
+    base = name.replace("(anonymous namespace)::", "").split("(")[0].split("<")[0]
     return base.rsplit("::", 1)[-1][:40]
 
 acc = collections.defaultdict(lambda: collections.defaultdict(float))
