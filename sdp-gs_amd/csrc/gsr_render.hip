@@ -1400,7 +1400,7 @@ __device__ __forceinline__ uint32_t build_group_lists(const uint16_t* s_mask, ui
 #endif
 // waves per SIMD the block-list forward is compiled for (VGPR budget 512 / n).  Round 2: 5
 // measured slower (96 VGPRs with 16 spilled: 0.116 -> 0.122 ms per view).  Round 4, with the
-// hardware-exp2 alpha test and the block-to-lane map: 5 (96 VGPRs, 16 spilled) 0.262 / 0.263
+// hardware-exp2 alpha test and the block-to-lane map: 5 (96 VGPRs, 4 spilled) 0.262 / 0.263
 // against 0.275 / 0.276 ms per 3-view launch at the default 104 VGPRs (4 waves); the lazy
 // channel reads at 5 / 6 waves 0.271 / 0.265 (profiles/r04_fwd_occ_ab.txt) -- 5, no lazy reads
 #ifndef GSR_FWD_BLK_WAVES
