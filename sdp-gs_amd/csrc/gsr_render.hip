@@ -122,7 +122,21 @@ __global__ __launch_bounds__(kSchedThreads) void tile_schedule_views_kernel(Sche
 // backward colour dot product: 1 = formed in the group's test phase for every entry (the colour
 // registers die early), 0 = where the compiler places it
 #ifndef GSR_BWD_CDOT_EARLY
-#define GSR_BWD_CDOT_EARLY 0
+#define GSR_BWD_CDOT_EARLY 1
+#endif
+// backward LDS accumulator rows: 1 = 13 floats (the gradient values; the flush supplies the row's
+// three zero slots), 0 = 17 (16 + 1 pad).  13 is odd as well, so the column accesses stay
+// conflict-free, and the workgroup's LDS drops 34.3 -> 30.2 KB (5 workgroups per CU instead of 4)
+#ifndef GSR_BWD_ACC13
+#define GSR_BWD_ACC13 1
+#endif
+// backward minimum waves per SIMD requested from the register allocator (amdgpu_waves_per_eu; the
+// default-mode kernels).  5 with the 13-float rows and the colour dot product in the test phase:
+// 96 VGPRs, 12 spilled (all outside the entry loop), 5 workgroups per CU -- render_bwd 1.012 /
+// 1.011 -> 0.998 / 0.995 ms per 6-view launch (profiles/r04_bwd_occ_ab.txt); 5 without the early
+// dot product spills 23 and is slower (1.017 / 1.020)
+#ifndef GSR_BWD_MIN_WAVES
+#define GSR_BWD_MIN_WAVES 5
 #endif
 // backward transmittance recovery T / (1 - alpha): 0 = IEEE division, 1 = rcp + Newton step
 #ifndef GSR_BWD_FAST_DIV
@@ -532,7 +546,8 @@ constexpr int kAccDet = 13;
 // One tile of the backward blend: workgroup `blk` of the view described by `a` (render_bwd_kernel:
 // one view per launch; render_bwd_views_kernel: the tiles of several views in one launch).
 // 4 waves per SIMD (128 VGPRs): the pipelined variants hold pending entries
-#define GSR_BWD_WAVES(PIPE) __attribute__((amdgpu_waves_per_eu((PIPE) ? 4 : 1)))
+#define GSR_BWD_WAVES(PIPE, DET) \
+  __attribute__((amdgpu_waves_per_eu((PIPE) ? 4 : ((DET) ? 1 : GSR_BWD_MIN_WAVES))))
 // PIPE (GSR_BWD_PIPE, round 4): the wave reduction of a contributing entry is issued together
 // with the next contributing entry's recurrence, in one basic block -- the two are independent
 // (the reduction needs only the entry's u = G dL/dalpha, w = alpha T and (dx, dy)), so the
@@ -558,10 +573,11 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
   // double-buffered under GSR_BWD_FLUSH_LATE: the flush of batch k reads its ids after batch k + 1
   // has been staged
   __shared__ uint32_t s_gid[GSR_BWD_FLUSH_LATE ? 2 : 1][kThreads];
-  // accumulator rows padded to an odd stride (17 floats): the per-splat moments pass (lane t ->
-  // row t) and the zero-fill are bank-conflict-free; the butterfly's adds (16 lanes -> 16 slots of
-  // one row) and the flush (4 rows x 16 slots per wave) stay conflict-free as well
-  constexpr int kRow = DET ? kAccDet : kAccPad;
+  // accumulator rows of an odd stride (13 floats, the gradient values; 17 without
+  // GSR_BWD_ACC13): the per-splat moments pass (lane t -> row t) and the zero-fill are
+  // bank-conflict-free; the butterfly's adds (one row's slots) and the flush (4 rows x 16 slots
+  // per wave, slots >= 13 supplied as zeros) stay conflict-free as well
+  constexpr int kRow = (DET || GSR_BWD_ACC13) ? kAccDet : kAccPad;
   __shared__ float s_acc[(DET ? 4 : 1) * kThreads * kRow];
   __shared__ uint8_t s_mask[kThreads];
   __shared__ uint8_t s_list[kThreads / 64][kThreads];
@@ -664,7 +680,7 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
   };
   auto reduce_add = [&](f2 (&g)[8], uint32_t j) {
     const float sum = wave_reduce16_dpp(g, lane);
-    if (red_lane && sum != 0.0f) atomicAdd(&s_acc[j * kAccPad + red_slot], sum);
+    if (red_lane && sum != 0.0f) atomicAdd(&s_acc[j * kRow + red_slot], sum);
   };
   const float ddelx_dx = (float)(0.5 * a.W);
   const float ddely_dy = (float)(0.5 * a.H);
@@ -884,13 +900,13 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
       // diagnostic build only (wrong gradients): no wave reduction, one lane-local LDS add
       {
         f2 t = g[0] + g[1] + g[2] + g[3] + g[4] + g[5] + g[6];
-        if (lane == 0 && t.x + t.y != 0.0f) atomicAdd(&s_acc[j * kAccPad], t.x + t.y);
+        if (lane == 0 && t.x + t.y != 0.0f) atomicAdd(&s_acc[j * kRow], t.x + t.y);
       }
 #else
       const float sum = wave_reduce16_dpp(g, lane);
       if (red_lane) {
         if (DET) s_acc[(wid * kThreads + j) * kRow + red_slot] = sum;
-        else if (sum != 0.0f) atomicAdd(&s_acc[j * kAccPad + red_slot], sum);
+        else if (sum != 0.0f) atomicAdd(&s_acc[j * kRow + red_slot], sum);
       }
 #endif
     }
@@ -901,7 +917,7 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
       const float sum = wave_reduce_joint4(g, lane);
       const int k = lane & 15;
       if (k < kAccDet && sum != 0.0f)
-        atomicAdd(&s_acc[((packed >> j4_shift) & 0xffu) * kAccPad + k], sum);
+        atomicAdd(&s_acc[((packed >> j4_shift) & 0xffu) * kRow + k], sum);
     }
     }
     if (PIPE == 1) {  // the batch's last contributing entry
@@ -960,11 +976,12 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
             for (int w = 0; w < 4; w++) s_acc[(w * kThreads + jj) * kRow + k] = 0.0f;
         } else if (ROWS) {  // every slot stored (16 lanes = one 64-B row), then re-zeroed
           const uint32_t q = range.x + tile_last - 1 - done_cnt - jj;
-          const float v = s_acc[jj * kAccPad + k];
+          const bool held = kRow > kAccDet || k < kAccDet;
+          const float v = held ? s_acc[jj * kRow + k] : 0.0f;
           a.partial[(size_t)min(a.einst[q], a.nrows - 1u) * kAccFloats + k] = v;
-          s_acc[jj * kAccPad + k] = 0.0f;
+          if (held) s_acc[jj * kRow + k] = 0.0f;
         } else {
-          const float v = s_acc[jj * kAccPad + k];
+          const float v = (kRow > kAccDet || k < kAccDet) ? s_acc[jj * kRow + k] : 0.0f;
           if (v != 0.0f) {
 #if GSR_BWD_DIAG == 2
             // diagnostic build only (wrong gradients): the flush's traffic as plain stores
@@ -972,7 +989,7 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
 #else
             atomicAdd(&a.acc[(size_t)s_gid[buf][jj] * kAccFloats + k], v);
 #endif
-            s_acc[jj * kAccPad + k] = 0.0f;
+            s_acc[jj * kRow + k] = 0.0f;
           }
         }
       }
@@ -987,7 +1004,7 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
 }
 
 template <bool EXTRA, bool FEAT, int GROUP, bool DET, bool ROWS, int PIPE>
-__global__ __launch_bounds__(kThreads) GSR_BWD_WAVES(PIPE) void render_bwd_kernel(RenderBwdArgs a) {
+__global__ __launch_bounds__(kThreads) GSR_BWD_WAVES(PIPE, DET) void render_bwd_kernel(RenderBwdArgs a) {
   render_bwd_tile<EXTRA, FEAT, GROUP, DET, ROWS, PIPE>(a, blockIdx.x);
 }
 
@@ -996,7 +1013,7 @@ __global__ __launch_bounds__(kThreads) GSR_BWD_WAVES(PIPE) void render_bwd_kerne
 // order), so the views' launches do not each end in a tail of idle CUs, and one launch's duration
 // is the time of all its views' blends.
 template <bool EXTRA, bool FEAT, int GROUP, bool DET, bool ROWS, int PIPE>
-__global__ __launch_bounds__(kThreads) GSR_BWD_WAVES(PIPE) void render_bwd_views_kernel(RenderBwdViews m) {
+__global__ __launch_bounds__(kThreads) GSR_BWD_WAVES(PIPE, DET) void render_bwd_views_kernel(RenderBwdViews m) {
   const uint32_t b = blockIdx.x;
   int k = 0;
   while (k + 1 < m.V && b >= m.first[k + 1]) k++;  // workgroup-uniform
