@@ -656,53 +656,11 @@ __global__ __launch_bounds__(kShThreads) void sh_flush_kernel(ShFlushArgs a) {
   stage<kShThreads, false, ACC>(p1, base, n, s_live, s_sh);
 }
 
-// Store-mode flush without LDS staging (GSR_SH_FLUSH_DIRECT=1, A/B): each thread stores its own
-// row with per-lane (strided) stores and leaves the line merging to L2; no 48-KB LDS buffer, so
-// occupancy is set by the registers alone.
-__global__ __launch_bounds__(kShThreads) void sh_flush_direct_kernel(ShFlushArgs a) {
-  const size_t i = (size_t)blockIdx.x * kShThreads + threadIdx.x;
-  if (i >= (size_t)a.P) return;
-  const V3 mean = v3(a.means3D[3 * i], a.means3D[3 * i + 1], a.means3D[3 * i + 2]);
-  V3 g[16];
-  const int used = (a.D + 1) * (a.D + 1);
-  for (int v = 0; v < a.nviews; v++) {
-    const float* cp = a.campos[v];
-    float b[16];
-    sh_basis(mean - v3(cp[0], cp[1], cp[2]), a.D, b);  // gsr_sh.h
-    const float* d = a.dRGB[v] + i;  // planar [3][rgb_stride]
-    const V3 dRGB = v3(d[0], d[a.rgb_stride], d[2 * a.rgb_stride]);
-#pragma unroll
-    for (int k = 0; k < 16; k++) g[k] = v == 0 ? b[k] * dRGB : g[k] + b[k] * dRGB;
-  }
-  float* r0 = a.dL_dsh_dc + 3 * i;
-  __builtin_nontemporal_store(g[0].x, r0);
-  __builtin_nontemporal_store(g[0].y, r0 + 1);
-  __builtin_nontemporal_store(g[0].z, r0 + 2);
-  float* r1 = a.dL_dsh_rest + i * (size_t)((a.M - 1) * 3);
-#pragma unroll
-  for (int k = 1; k < 16; k++) {
-    if (k < a.M) {
-      const V3 v = k < used ? g[k] : v3(0, 0, 0);
-      __builtin_nontemporal_store(v.x, r1 + 3 * k - 3);
-      __builtin_nontemporal_store(v.y, r1 + 3 * k - 2);
-      __builtin_nontemporal_store(v.z, r1 + 3 * k - 1);
-    }
-  }
-}
-
 }  // namespace
 
 hipError_t launch_sh_grad_flush(const ShFlushArgs& a, hipStream_t s) {
   if (a.P == 0 || a.nviews <= 0) return hipSuccess;
   const dim3 grid((a.P + kShThreads - 1) / kShThreads);
-  static const bool direct = [] {
-    const char* e = getenv("GSR_SH_FLUSH_DIRECT");
-    return e && atoi(e) == 1;
-  }();
-  if (direct && !a.accumulate) {
-    hipLaunchKernelGGL(sh_flush_direct_kernel, grid, dim3(kShThreads), 0, s, a);
-    return hipGetLastError();
-  }
   if (a.accumulate)
     hipLaunchKernelGGL(sh_flush_kernel<true>, grid, dim3(kShThreads), 0, s, a);
   else
