@@ -275,12 +275,15 @@ def main():
             stats["R_ref"].append(dgr.LAST_STATS["num_rendered"])
             stats["Pv"].append(int(pkg["visibility_filter"].sum()))
 
-    def step(record=False, vp=None):
+    def step(record=False, vp=None, collective=True):
+        """One step of this rank's views; collective=False leaves the gradient all-reduce out
+        (the instrumented step that picks the dominant kernel: no collective in its brackets)."""
         views_ = vp or views
         my_cams = step_cams(step_no[0])
         step_no[0] += 1
-        if reducer is not None:
-            reducer.attach_grads()  # grads accumulate straight into the all-reduce buckets
+        red = reducer if collective else None
+        if red is not None:
+            red.attach_grads()  # grads accumulate straight into the all-reduce buckets
         else:
             for p in model.parameters():
                 p.grad = None
@@ -288,12 +291,12 @@ def main():
         # gradients are flushed in row slices, each slice reduced as soon as it is written)
         if not args.per_view and not args.autograd_grads:
             views_.run_views(my_cams, lambda cams, strs: all_views(cams, strs, record),
-                             model=model, reducer=reducer, chunks=args.view_chunks)
+                             model=model, reducer=red, chunks=args.view_chunks)
         elif args.lag > 0:
-            views_.run(my_cams, view_forward, model=model, reducer=reducer,
+            views_.run(my_cams, view_forward, model=model, reducer=red,
                        bwd=lambda pkg: view_backward(pkg, record), lag=args.lag)
         else:
-            views_.run(my_cams, lambda cam: one_view(cam, record), model=model, reducer=reducer)
+            views_.run(my_cams, lambda cam: one_view(cam, record), model=model, reducer=red)
 
     def all_views(cams, strs, record):
         """One multi-view call (a chunk of the step's views with --view-chunks, issued by
@@ -343,11 +346,12 @@ def main():
         # the per-stage table and the choice of the dominant kernel come from one instrumented step
         # issued on ONE stream: with the views' work spread over several streams an event pair
         # also spans the other streams' kernels, so a latency-bound stage that waits beside a
-        # full-chip launch would look dominant
+        # full-chip launch would look dominant; and without the gradient all-reduce, so that at
+        # N > 1 no stage's bracket spans a collective
         serial = ViewPipeline(dev, depth=1, defer_sh=defer_sh, precolor=not args.no_precolor)
         timer.reset()
         timer.enable(True)
-        step(vp=serial)
+        step(vp=serial, collective=False)
         timer.enable(False)
         all_stages = timer.collect()
         busy = {n: ms for n, (ms, c) in all_stages.items() if c}
@@ -395,9 +399,8 @@ def main():
     HW = W * H
     kernels = {}
     # the batched multi-view forward zeroes the accumulator rows in its blend (gsr_api.cpp
-    # blend_zeroes_acc; GSR_VIEWS_BATCHED / GSR_BLEND_ZEROES_ACC = 0 turn it off)
-    acc_in_blend = (not args.per_view and os.environ.get("GSR_VIEWS_BATCHED", "1") != "0"
-                    and os.environ.get("GSR_BLEND_ZEROES_ACC", "1") != "0")
+    # views_forward_batched)
+    acc_in_blend = not args.per_view
     for name, (ms, calls) in stages.items():
         if calls == 0:
             continue
@@ -501,9 +504,11 @@ def main():
                                  if args.per_view or args.autograd_grads else
                                  "multi-view call (gsr_rasterize_views_fused, one host call per "
                                  "step for the forwards and one for the backwards)"),
-                       "hw_queue_budget": (f"{views.depth} view streams + 1 RCCL stream <= "
-                                           f"GPU_MAX_HW_QUEUES={hw_queues}") if world > 1 else
+                       "hw_queue_budget": (f"{views.depth} view streams + 1 collective stream "
+                                           f"({_backend_name()}) <= GPU_MAX_HW_QUEUES="
+                                           f"{hw_queues}") if world > 1 else
                                           f"{views.depth} view streams (no collectives)",
+                       "collective_backend": _backend_name() if world > 1 else None,
                        "camera_pool": pool,
                        "sh_grads": "deferred (one flush per step)" if defer_sh else "per view",
                        "sh_colour": "per view" if args.no_precolor else "multi-view pre-pass",
@@ -715,6 +720,12 @@ def extra_legs(args, model, step_cams, pool, n_views, views, reducer, timed_regi
     return out
 
 
+def _backend_name():
+    """The process group's backend as run: torch's "nccl" is RCCL on ROCm."""
+    b = dist.get_backend()
+    return "rccl" if b == "nccl" else b
+
+
 def _cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -725,18 +736,23 @@ def _cpu_model():
     return platform.processor() or platform.machine()
 
 
-def torch_cpu_baseline(model, cam, dimg, ddep, dfeat, deg, g1, c1, threads):
+def torch_cpu_baseline(model, cam, dimg, ddep, dfeat, deg, g1, c1, threads, budget_s=120.0):
     """BASELINE.json's "PyTorch-CPU render() on the host cores": the rasterizer as PyTorch tensor
     code (oracle/torch_cpu.py: preprocess, binning by torch.sort, per-tile blend, autograd
-    backward), float32, torch.set_num_threads(threads).  Config 1 forward only (median of 5 after
-    one warm-up) and one headline view forward + backward (one timed run after a forward-only
-    warm-up: ~15-30 s of CPU work).  kind "pytorch"."""
+    backward), float32, torch.set_num_threads(threads), timed by BASELINE.md's protocol -- 2
+    warm-ups, then the median of 5:
+      * config 1: 10k synthetic Gaussians, one 400x400 camera, forward only (render()'s default
+        Python SH at active degree 0);
+      * the headline workload: one full view of it, forward + backward.
+    SURVEY.md 8(d)'s time rule: a run whose first warm-up takes longer than budget_s / 7 gets
+    fewer timed repetitions (logged in `protocol`), so that the bench stays within minutes."""
     try:
         from oracle import torch_cpu as TC
     except Exception as exc:  # pragma: no cover - reported, not fatal
         return {"value": None, "error": repr(exc)[:200]}
     prev = torch.get_num_threads()
     torch.set_num_threads(threads)
+    notes = []
     try:
         with torch.no_grad():
             l1 = [t.detach().cpu().float() for t in (g1.xyz, g1.get_opacity(), g1.get_features(),
@@ -744,42 +760,51 @@ def torch_cpu_baseline(model, cam, dimg, ddep, dfeat, deg, g1, c1, threads):
                                                     g1.language_feature)]
             cam1 = TC.camera_dict(c1)
             ts = []
-            for i in range(6):
+            for i in range(7):
                 t0 = time.perf_counter()
                 TC.render(*l1, 0, cam1, torch.zeros(3))
-                if i:
+                if i >= 2:
                     ts.append(time.perf_counter() - t0)
             t1 = float(np.median(ts))
-            lh = [t.detach().cpu().float().clone() for t in (
+            lh0 = [t.detach().cpu().float().clone() for t in (
                 model.get_xyz, model.get_opacity, model.get_features, model.get_scaling,
                 model.get_rotation, model.get_language_feature)]
             camh = TC.camera_dict(cam)
             up = tuple(t.detach().cpu().float() for t in (dimg, ddep, dfeat))
-            TC.render(*lh, deg, camh, torch.zeros(3))  # warm-up (forward)
-        lh = [t.requires_grad_(True) for t in lh]
-        t0 = time.perf_counter()
-        TC.render(*lh, deg, camh, torch.zeros(3), upstream=up)
-        th = time.perf_counter() - t0
+
+        def fwd_bwd():
+            lh = [t.clone().requires_grad_(True) for t in lh0]
+            t0 = time.perf_counter()
+            TC.render(*lh, deg, camh, torch.zeros(3), upstream=up)
+            return time.perf_counter() - t0
+        warm = [fwd_bwd()]
+        reps = 5
+        if warm[0] * 7 > budget_s:
+            reps = max(1, int(budget_s // warm[0]) - 1)
+            notes.append(f"first warm-up {warm[0]:.1f} s: {reps} timed run(s) instead of 5 "
+                         f"(bench time budget {budget_s:.0f} s, SURVEY.md 8(d))")
+        else:
+            warm.append(fwd_bwd())
+        th = float(np.median([fwd_bwd() for _ in range(reps)]))
     finally:
         torch.set_num_threads(prev)
     return {"value": round(1.0 / th, 5), "unit": "views/s", "cores": threads, "kind": "pytorch",
             "sample": (f"one headline view ({cam.image_width}x{cam.image_height}, "
-                       f"{lh[0].shape[0]} Gaussians, SH degree {deg}, fwd+bwd) through "
-                       f"oracle/torch_cpu.py on {threads} torch threads: one run after a "
-                       f"forward warm-up, {th:.1f} s"),
+                       f"{lh0[0].shape[0]} Gaussians, SH degree {deg}, fwd+bwd) through "
+                       f"oracle/torch_cpu.py (PyTorch-CPU render()) on {threads} torch threads: "
+                       f"median of {reps} after {len(warm)} warm-up(s), {th:.2f} s per view"),
+            "protocol": notes or ["2 warm-ups, median of 5 (BASELINE.md)"],
             "config1_fwd_views_per_s": round(1.0 / t1, 3),
-            "config1": f"10k Gaussians, 400x400, forward only, SH degree 0: median {1000 * t1:.1f} ms"}
+            "config1": f"10k Gaussians, 400x400, forward only, SH degree 0: median of 5 after 2 "
+                       f"warm-ups, {1000 * t1:.1f} ms"}
 
 
 def cpu_baseline(model, cams, dimg, ddep, dfeat, deg, threads=0):
-    """The CPU restatement (oracle/: C, float32, the reference's arithmetic) on the host cores,
-    timed in this run (rank 0 at N = 1), 2 warm-ups then the median of 5 (BASELINE.md CPU plan),
-    and beside it (`pytorch`) the PyTorch-CPU render() BASELINE.json names (torch_cpu_baseline):
-      * config 1: 10k synthetic Gaussians, one 400x400 camera, forward only (SH degree 0 as
-        render()'s default Python SH at active degree 0);
-      * the headline workload: one full view of it, forward + backward.
-    Threads: OMP_NUM_THREADS (the box's CPU share) or all cores; the oracle splits its loops into
-    fixed chunks, one per thread (oracle/gsr_oracle.c)."""
+    """The CPU baseline BASELINE.json names -- PyTorch-CPU render() on the host cores, timed in
+    this run (rank 0 at N = 1; torch_cpu_baseline) -- and beside it (`port`) the C restatement of
+    the reference's arithmetic (oracle/gsr_oracle.c, float32) on the same samples.
+    Threads: OMP_NUM_THREADS (the box's CPU share) or all cores; the C port splits its loops into
+    fixed chunks, one per thread."""
     try:
         from oracle.oracle import OracleRaster, build, set_threads
         build()
@@ -834,18 +859,17 @@ def cpu_baseline(model, cams, dimg, ddep, dfeat, deg, threads=0):
     def fwd_bwd():
         OracleRaster(**kwh).backward(dimg_n, ddep_n, None, dfeat_n)
     th = median_time(fwd_bwd)
-    pyt = torch_cpu_baseline(model, cams[0], dimg, ddep, dfeat, deg, g1, c1, n)
-    return {"value": round(1.0 / th, 4), "unit": "views/s", "cores": n, "kind": "port",
-            "pytorch": pyt,
+    port = {"value": round(1.0 / th, 4), "unit": "views/s", "cores": n, "kind": "port",
             "sample": (f"one headline view ({cams[0].image_width}x{cams[0].image_height}, "
                        f"{kwh['means3D'].shape[0]} Gaussians, SH degree {deg}, fwd+bwd) on the C "
                        f"restatement with {n} threads: median of 5 after 2 warm-ups, "
                        f"{1000 * th:.0f} ms"),
             "config1_fwd_views_per_s": round(1.0 / t1, 3),
             "config1": (f"10k Gaussians, 400x400, forward only, SH degree 0: median "
-                        f"{1000 * t1:.1f} ms"),
-            "cpu": _cpu_model(), "os_cpu_count": os.cpu_count(),
-            "threads": n}
+                        f"{1000 * t1:.1f} ms")}
+    out = torch_cpu_baseline(model, cams[0], dimg, ddep, dfeat, deg, g1, c1, n)
+    out.update({"port": port, "cpu": _cpu_model(), "os_cpu_count": os.cpu_count(), "threads": n})
+    return out
 
 
 if __name__ == "__main__":

@@ -37,7 +37,6 @@ GeomState carve_geom(char* base, size_t P) {
   g.clamped = c.take<uint8_t>(P);
   g.radii = c.take<int32_t>(P);
   g.rec = c.take<float4>(4 * P);
-  g.drec = c.take<float4>(2 * P);
   g.tiles_touched = c.take<uint32_t>(P);
   g.offsets = c.take<uint32_t>(P);
   g.acc = c.take<float>((size_t)kAccFloats * P);
@@ -48,14 +47,6 @@ GeomState carve_geom(char* base, size_t P) {
   g.pre_parts = c.take<uint32_t>(2 * ((P + 255) / 256) + 1);
   g.bytes = c.size();
   return g;
-}
-
-bool bwd_rows_mode() {
-  static const bool rows = [] {
-    const char* e = getenv("GSR_BWD_ROWS");
-    return e ? atoi(e) != 0 : false;
-  }();
-  return rows;
 }
 
 BinState carve_bin(char* base, size_t R, bool rows) {
@@ -367,7 +358,7 @@ const char* gsr_last_error(void) { return g_err.c_str(); }
 
 size_t gsr_geom_buffer_bytes(int P) { return carve_geom(nullptr, (size_t)(P > 0 ? P : 0)).bytes; }
 size_t gsr_binning_buffer_bytes(int R) {
-  return carve_bin(nullptr, (size_t)(R > 0 ? R : 0), bwd_rows_mode()).bytes;
+  return carve_bin(nullptr, (size_t)(R > 0 ? R : 0), false).bytes;
 }
 size_t gsr_binning_buffer_bytes_det(int R) {
   return carve_bin(nullptr, (size_t)(R > 0 ? R : 0), true).bytes;
@@ -559,12 +550,10 @@ static int fwd_begin(const FwdModel& m, FwdCam& c) {
 
   bool in_b = false;
   PROF_BEGIN(DEPTH_SORT);
-  // the last pass writes each Gaussian's tile count in place of its sorted key (and, GSR_DUP_DREC,
-  // its binning record in depth order for the duplication)
+  // the last pass writes each Gaussian's tile count in place of its sorted key
   GSR_CHECK(radix_sort_pairs(g.dkey_a, g.dval_a, g.dkey_b, g.dval_b, (size_t)P, 32,
                              g.sort, &in_b, stream, /*sentinel_anywhere=*/true,
-                             /*precleared=*/true, /*key_payload=*/g.tiles_touched,
-                             dup_drec() ? g.rec : nullptr, dup_drec() ? g.drec : nullptr));
+                             /*precleared=*/true, /*key_payload=*/g.tiles_touched));
   PROF_END(DEPTH_SORT);
   c.depth_in_b = in_b;
   const uint32_t* counts_sorted = in_b ? g.dkey_b : g.dkey_a;
@@ -653,8 +642,7 @@ static int fwd_bin(const FwdModel& m, FwdCam& c) {
   GSR_CHECK(launch_duplicate(P, order, g.offsets, c.radii_ptr, g.rec, c.gx, c.gy, b.tkey_a, b.tval_a,
                              (uint32_t)R, SideClear{b.sort.aux, sort_clear_bytes(b.sort, R, tbits)},
                              SideClear{im.ranges, sizeof(uint2) * ntiles}, stream,
-                             m.rows ? b.egid : nullptr, m.rows ? g.ebeg : nullptr,
-                             dup_drec() ? g.drec : nullptr));
+                             m.rows ? b.egid : nullptr, m.rows ? g.ebeg : nullptr));
   PROF_END(DUPLICATE);
   bool t_in_b = false;
   PROF_BEGIN(TILE_SORT);
@@ -748,7 +736,7 @@ static int forward_impl(int P, int M, const float* background, const float* mean
   g_err.clear();
   FwdModel m;
   m.det = (debug & GSR_DEBUG_DETERMINISTIC) != 0;  // gsr.h: debug bit 1
-  m.rows = m.det || bwd_rows_mode();  // per-instance gradient rows (binning layout)
+  m.rows = m.det;  // per-instance gradient rows (binning layout)
   m.debug = debug & 1;
   m.P = P; m.M = M; m.background = background; m.means3D = means3D;
   m.colors_precomp = colors_precomp; m.opacities = opacities; m.scales = scales;
@@ -863,7 +851,7 @@ static int bwd_setup(
     const float* opacity_raw, float* dL_dsh_rest, int accumulate, float* dRGB_sh,
     const float* pre_jac) {
   const bool det = (debug & GSR_DEBUG_DETERMINISTIC) != 0;  // must match the forward's flags
-  const bool rows = det || bwd_rows_mode();
+  const bool rows = det;
   debug &= 1;
   call.debug = debug;
   if (fused && P != 0) {
@@ -1011,7 +999,7 @@ static int backward_impl(
       GSR_CHECK(hipMemcpyAsync(&tag, hb.tag, sizeof(tag), hipMemcpyDeviceToHost, stream));
       GSR_CHECK(hipStreamSynchronize(stream));
       const bool det = (tag & 2u) != 0;
-      if ((tag & ~3u) != kBinLayoutMagic || ((tag & 1u) != 0) != (det || bwd_rows_mode()))
+      if ((tag & ~3u) != kBinLayoutMagic || ((tag & 1u) != 0) != det)
         return fail(GSR_ERR_ARGUMENT, "binningBuffer does not come from a libgsr forward of this "
                                       "process (layout tag 0x%08x)", tag);
       debug = (debug & ~GSR_DEBUG_DETERMINISTIC) | (det ? GSR_DEBUG_DETERMINISTIC : 0);
@@ -1102,14 +1090,6 @@ int gsr_rasterize_gaussians_fused_backward_deferred(
 
 // ---- multi-view calls --------------------------------------------------------------------------
 namespace {
-// GSR_VIEWS_PRE_MERGED=0: one per-Gaussian backward launch per view in multi-view calls
-bool views_pre_merged() {
-  static const bool on = [] {
-    const char* e = getenv("GSR_VIEWS_PRE_MERGED");
-    return !(e && atoi(e) == 0);
-  }();
-  return on;
-}
 // per host thread: events joining the views' streams with the call's stream
 hipEvent_t join_event(int i) {
   constexpr int kMaxDev = 64;
@@ -1120,69 +1100,6 @@ hipEvent_t join_event(int i) {
     ev[dev][i] = nullptr;
   return ev[dev][i];
 }
-
-// The batched path zeroes the backward accumulator rows in the forward blend's grid (default)
-// instead of the preprocess's (GSR_BLEND_ZEROES_ACC=0)
-bool blend_zeroes_acc() {
-  static const bool on = [] {
-    const char* e = getenv("GSR_BLEND_ZEROES_ACC");
-    return e ? atoi(e) != 0 : true;
-  }();
-  return on;
-}
-
-// The batched forward's scan: reduce-then-scan, three launches (default), or one look-back launch
-// (GSR_SCAN_LB=1; measured 0.5-1.4 % slower per step, profiles/r03_scan_lookback_ab.txt)
-bool scan_lookback() {
-  static const bool on = [] {
-    const char* e = getenv("GSR_SCAN_LB");
-    return e ? atoi(e) != 0 : false;
-  }();
-  return on;
-}
-
-bool render_on_call() {
-  static const bool on = [] {
-    const char* e = getenv("GSR_VIEWS_RENDER_CALL");
-    return e ? atoi(e) != 0 : false;
-  }();
-  return on;
-}
-
-int g0_on_call() {
-  static const int mode = [] {
-    const char* e = getenv("GSR_VIEWS_G0_CALL");
-    return e ? atoi(e) : 1;
-  }();
-  return mode;
-}
-
-// The batched path's preprocess: one multi-view launch (default) or one launch per view
-// (GSR_PRE_VIEWS=0).
-bool pre_views() {
-  static const bool on = [] {
-    const char* e = getenv("GSR_PRE_VIEWS");
-    return e ? atoi(e) != 0 : true;
-  }();
-  return on;
-}
-
-// GSR_HOST_TRACE=1: host timestamps of the batched forward's phases, printed per call (stderr)
-struct HostTrace {
-  bool on;
-  std::chrono::steady_clock::time_point t0;
-  char buf[2048];
-  int n = 0;
-  HostTrace() : on(getenv("GSR_HOST_TRACE") != nullptr), t0(std::chrono::steady_clock::now()) {}
-  void mark(const char* what, int g) {
-    if (!on || n > 1980) return;
-    const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
-    n += snprintf(buf + n, sizeof(buf) - (size_t)n, " %s%d=%.0f", what, g, us);
-  }
-  ~HostTrace() {
-    if (on) fprintf(stderr, "[gsr host]%s\n", buf);
-  }
-};
 
 // Coherent, device-mapped pinned words (4 per view) that the batched sums store each view's
 // read-back into: no copy launch, one event per group.
@@ -1213,16 +1130,20 @@ int check_sort_err(const uint32_t* err, hipStream_t stream, const char* what) {
   return GSR_OK;
 }
 
-// Batched binning (GSR_VIEWS_BATCHED, default 1).  The views are split into `ng` groups, group g
-// on the g-th distinct view stream; inside a group every stage after the per-view preprocess is
-// ONE launch for all the group's views -- the instance-count sums (which also store the read-back
-// into pinned words), each depth-sort pass, the scan, the duplication, each tile-sort pass, the
-// ranges, the schedules and the blend.  A view's binning alone is a chain of ~14 small launches
-// whose latency, not HBM, sets its time (0.20 ms per view at 1 stream); batched, each launch is as
-// wide as the group.  Every kernel sees exactly its one-view arguments (own totals, tickets,
-// look-back words), so the results are bit-identical to the per-view path.  The host waits once
-// per group, for its read-back, while the group's depth sort and scan run; group g's blend then
-// overlaps group g + 1's binning on the other stream.
+// Batched binning.  The views are split into `ng` groups, group g on the g-th distinct view
+// stream (group 0 on the call's stream, so its preprocess follows the caller's last kernel -- the
+// colour pre-pass -- on the same queue without a cross-stream wait); inside a group every stage
+// after the preprocess is ONE launch for all the group's views -- the preprocesses, the
+// instance-count sums (which also store the read-back into pinned words), each depth-sort pass,
+// the scan, the duplication, each tile-sort pass, the ranges, the schedules and the blend.  A
+// view's binning alone is a chain of ~14 small launches whose latency, not HBM, sets its time
+// (0.20 ms per view at 1 stream); batched, each launch is as wide as the group.  Every kernel sees
+// exactly its one-view arguments (own totals, tickets, look-back words), so the results are
+// bit-identical to the per-view path.  The host waits once per group, for its read-back, while the
+// group's depth sort and scan run; group g's blend then overlaps group g + 1's binning on the other
+// stream.  Each group's first phase is queued before the first wait.  The views' backward
+// accumulator rows are zeroed by the forward blend's grid (a VALU-bound kernel) instead of the
+// memory-bound preprocess's.
 int views_forward_batched(const FwdModel& m, std::vector<FwdCam>& cams, gsr_view* views,
                           hipStream_t call_stream, int ng) {
   const int V = (int)cams.size();
@@ -1236,23 +1157,6 @@ int views_forward_batched(const FwdModel& m, std::vector<FwdCam>& cams, gsr_view
   int per = (V + ng - 1) / ng;
   if (per > kMaxBatchViews) per = kMaxBatchViews;
   ng = (V + per - 1) / per;
-  // group boundaries: equal groups, or a first group of GSR_VIEWS_FWD_FIRST views and the rest
-  // split evenly (a smaller first group's blend starts earlier, beside the others' binning)
-  std::vector<int> gstart((size_t)ng + 1, 0);
-  {
-    static const int first_env = [] {
-      const char* e = getenv("GSR_VIEWS_FWD_FIRST");
-      return e ? atoi(e) : 0;
-    }();
-    if (first_env > 0 && first_env < V && ng > 1 && first_env <= kMaxBatchViews &&
-        (V - first_env + ng - 2) / (ng - 1) <= kMaxBatchViews) {
-      gstart[1] = first_env;
-      for (int gi = 2; gi <= ng; gi++)
-        gstart[(size_t)gi] = first_env + (int)((long long)(V - first_env) * (gi - 1) / (ng - 1));
-    } else {
-      for (int gi = 1; gi <= ng; gi++) gstart[(size_t)gi] = gi * per < V ? gi * per : V;
-    }
-  }
   struct Group {
     int v0 = 0, n = 0;
     hipStream_t st = nullptr;
@@ -1277,21 +1181,12 @@ int views_forward_batched(const FwdModel& m, std::vector<FwdCam>& cams, gsr_view
       cams[(size_t)v].given_i = cams[(size_t)v].given_g + gb;
     }
   }
-  // phase 1 of a group: preprocess per view, then one launch per stage for the group
-  HostTrace ht;
+  // phase 1 of a group: the views' preprocesses in one launch, then one launch per stage
   auto phase1 = [&](int gi) -> int {
     Group& G = grp[(size_t)gi];
-    G.v0 = gstart[(size_t)gi];
-    G.n = gstart[(size_t)gi + 1] - G.v0;
-    // group 0 on the call's stream (GSR_VIEWS_G0_CALL, default 1): its preprocess follows the
-    // caller's last kernel (the colour pre-pass) on the same queue, without a cross-stream wait
-    // (GSR_VIEWS_G0_CALL=2: the LAST group there instead -- the backward then follows it directly)
-    {
-      const int mode = g0_on_call();
-      const int cg = mode == 2 ? ng - 1 : (mode == 1 ? 0 : -1);  // the group on the call's stream
-      G.st = gi == cg ? call_stream
-                      : distinct[(size_t)(gi - (cg >= 0 && gi > cg ? 1 : 0)) % distinct.size()];
-    }
+    G.v0 = (int)((long long)gi * per);
+    G.n = std::min(per, V - G.v0);
+    G.st = gi == 0 ? call_stream : distinct[(size_t)(gi - 1) % distinct.size()];
     G.ready = readback_event(gi);
     if (!G.ready) return fail(GSR_ERR_HIP, "event creation failed");
     hipStream_t stream = G.st;
@@ -1311,24 +1206,19 @@ int views_forward_batched(const FwdModel& m, std::vector<FwdCam>& cams, gsr_view
       const GeomState& g = c.g;
       const int l = (int)G.live.size();
       pas[l] = c.pa;
-      if (blend_zeroes_acc() && pas[l].acc_zero) {
+      if (pas[l].acc_zero) {
         pas[l].acc_zero = 0;  // the view's forward blend zeroes the accumulator rows instead
         c.acc_clear = SideClear{g.acc, (size_t)P * kAccFloats * sizeof(float)};
       }
       sums[l] = SumSpec{g.pre_parts, g.pre_parts + pre_blocks, pre_blocks, g.flags + 1, c.host_dev,
                         m.prefiltered ? g.flags : nullptr};
-      ds[l] = SortSpec{g.dkey_a, g.dval_a, g.dkey_b, g.dval_b, (size_t)P, g.sort, g.tiles_touched,
-                       dup_drec() ? g.rec : nullptr, dup_drec() ? g.drec : nullptr};
+      ds[l] = SortSpec{g.dkey_a, g.dval_a, g.dkey_b, g.dval_b, (size_t)P, g.sort, g.tiles_touched};
       G.live.push_back(v);
     }
     const int nl = (int)G.live.size();
     if (nl == 0) return GSR_OK;
     PROF_BEGIN(PREPROCESS);
-    if (pre_views()) {
-      GSR_CHECK(launch_preprocess_views(pas, nl, stream));
-    } else {
-      for (int l = 0; l < nl; l++) GSR_CHECK(launch_preprocess(pas[l], stream));
-    }
+    GSR_CHECK(launch_preprocess_views(pas, nl, stream));
     PROF_END(PREPROCESS);
     GSR_CHECK(sum_u32_parts_views(sums, nl, stream));
     GSR_CHECK(hipEventRecord(G.ready, stream));
@@ -1337,21 +1227,14 @@ int views_forward_batched(const FwdModel& m, std::vector<FwdCam>& cams, gsr_view
                                      /*precleared=*/true));
     PROF_END(DEPTH_SORT);
     ScanSpec sc[kMaxBatchViews];
-    ScanLbSpec sl[kMaxBatchViews];
     for (int l = 0; l < nl; l++) {
       FwdCam& c = cams[(size_t)G.live[(size_t)l]];
       c.depth_in_b = G.depth_in_b;
       const uint32_t* counts = G.depth_in_b ? c.g.dkey_b : c.g.dkey_a;
       sc[l] = ScanSpec{counts, c.g.offsets, (size_t)P, c.g.scan_parts};
-      sl[l] = ScanLbSpec{counts, c.g.offsets, (size_t)P, c.g.scan_status,
-                         c.g.sort.aux + kSortAuxErr};
     }
     PROF_BEGIN(SCAN);
-    if (scan_lookback()) {
-      GSR_CHECK(scan_u32_lookback_views(sl, nl, stream));
-    } else {
-      GSR_CHECK(scan_u32_views(sc, nl, true, stream));
-    }
+    GSR_CHECK(scan_u32_views(sc, nl, true, stream));
     PROF_END(SCAN);
     return GSR_OK;
   };
@@ -1361,172 +1244,119 @@ int views_forward_batched(const FwdModel& m, std::vector<FwdCam>& cams, gsr_view
     RenderArgs* ras = G.ras;
     hipStream_t stream = G.st;
     const int nl = (int)G.live.size();
-    if (nl > 0) {
-      {
-        const auto t0 = std::chrono::steady_clock::now();
-        ht.mark("w", gi);
-        GSR_CHECK(hipEventSynchronize(G.ready));
-        ht.mark("r", gi);
-        g_wait_ns.fetch_add((long long)std::chrono::duration_cast<std::chrono::nanoseconds>(
-                                std::chrono::steady_clock::now() - t0).count(),
-                            std::memory_order_relaxed);
-      }
-      DupSpec dup[kMaxBatchViews];
-      SortSpec ts[kMaxBatchViews];
-      const uint32_t ntiles = cams[(size_t)G.live[0]].gx * cams[(size_t)G.live[0]].gy;
-      const int tbits = tile_bits(ntiles);
-      {  // the group's binning buffers in one allocation callback (sizes from the read-back)
-        size_t off[kMaxBatchViews + 1] = {0};
-        for (int l = 0; l < nl; l++) {
-          const uint32_t R_ref = cams[(size_t)G.live[(size_t)l]].host[2];
-          const size_t bb = R_ref <= 0x7fffffffu ? carve_bin(nullptr, R_ref, m.rows).bytes : 0;
-          off[l + 1] = off[l] + bb;  // (an invalid count is reported by fwd_bin_alloc)
-        }
-        FwdCam& c0 = cams[(size_t)G.live[0]];
-        char* base = (char*)c0.alloc(c0.alloc_ctx, off[nl] ? off[nl] : 256, GSR_BUF_BINNING);
-        if (!base) return fail(GSR_ERR_ALLOC, "binning buffer allocation of %zu bytes failed", off[nl]);
-        for (int l = 0; l < nl; l++) cams[(size_t)G.live[(size_t)l]].given_b = base + off[l];
-        ht.mark("A", gi);
-      }
-      for (int l = 0; l < nl; l++) {
-        FwdCam& c = cams[(size_t)G.live[(size_t)l]];
-        if (int rc = fwd_bin_alloc(m, c, /*tag_by_dup=*/true)) return rc;  // (debug: checks the depth sort)
-        ht.mark("b", l);
-        const GeomState& g = c.g;
-        const BinState& b = c.b;
-        const uint32_t R = (uint32_t)c.num_instances;
-        dup[l] = DupSpec{P, G.depth_in_b ? g.dval_b : g.dval_a, g.offsets, g.rec, c.gx, c.gy,
-                         b.tkey_a, b.tval_a, R,
-                         SideClear{b.sort.aux, sort_clear_bytes(b.sort, R, tbits)},
-                         SideClear{c.im.ranges, sizeof(uint2) * ntiles},
-                         m.rows ? b.egid : nullptr, m.rows ? g.ebeg : nullptr,
-                         dup_drec() ? g.drec : nullptr, b.tag, bin_layout_tag(m.det, m.rows)};
-        ts[l] = SortSpec{b.tkey_a, b.tval_a, b.tkey_b, b.tval_b, (size_t)R, b.sort, nullptr};
-      }
-      PROF_BEGIN(DUPLICATE);
-      ht.mark("a", gi);
-      GSR_CHECK(launch_duplicate_views(dup, nl, stream));
-      PROF_END(DUPLICATE);
-      bool t_in_b = false;
-      PROF_BEGIN(TILE_SORT);
-      GSR_CHECK(radix_sort_pairs_views(ts, nl, tbits, &t_in_b, stream, false, /*precleared=*/true));
-      PROF_END(TILE_SORT);
-      ht.mark("t", gi);
-      RangesSpec rs[kMaxBatchViews];
-      for (int l = 0; l < nl; l++) {
-        FwdCam& c = cams[(size_t)G.live[(size_t)l]];
-        const BinState& b = c.b;
-        const uint32_t R = (uint32_t)c.num_instances;
-        if (debug)
-          if (int rc = check_sort_err(b.sort.aux + kSortAuxErr, stream, "tile sort")) return rc;
-        const uint32_t* tiles_sorted = t_in_b ? b.tkey_b : b.tkey_a;
-        const uint32_t* point_list = t_in_b ? b.tval_b : b.tval_a;
-        if (m.rows) {
-          uint32_t* pl = t_in_b ? b.tval_a : b.tval_b;
-          GSR_CHECK(launch_det_gather(R, point_list, b.egid, pl, stream));
-          point_list = pl;
-        }
-        int mail_slot = -1;
-        uint32_t* host_status = mail_post(c.ibase, &mail_slot);
-        rs[l] = RangesSpec{R, tiles_sorted, c.im.ranges, ntiles, c.g.sort.aux + kSortAuxErr,
-                           b.sort.aux + kSortAuxErr, c.im.status, host_status,
-                           forward_faults_word()};
-        fwd_render_args(m, c, point_list, host_status);
-        c.ra.clear = c.acc_clear;
-        c.mail_slot = mail_slot;
-        ras[l] = c.ra;
-      }
-      PROF_BEGIN(RANGES);
-      GSR_CHECK(launch_tile_ranges_views(rs, nl, stream));
-      GSR_CHECK(launch_render_schedule_views(ras, nl, stream));
-      PROF_END(RANGES);
+    if (nl == 0) return GSR_OK;
+    {
+      const auto t0 = std::chrono::steady_clock::now();
+      GSR_CHECK(hipEventSynchronize(G.ready));
+      g_wait_ns.fetch_add((long long)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                              std::chrono::steady_clock::now() - t0).count(),
+                          std::memory_order_relaxed);
     }
+    DupSpec dup[kMaxBatchViews];
+    SortSpec ts[kMaxBatchViews];
+    const uint32_t ntiles = cams[(size_t)G.live[0]].gx * cams[(size_t)G.live[0]].gy;
+    const int tbits = tile_bits(ntiles);
+    {  // the group's binning buffers in one allocation callback (sizes from the read-back)
+      size_t off[kMaxBatchViews + 1] = {0};
+      for (int l = 0; l < nl; l++) {
+        const uint32_t R_ref = cams[(size_t)G.live[(size_t)l]].host[2];
+        const size_t bb = R_ref <= 0x7fffffffu ? carve_bin(nullptr, R_ref, m.rows).bytes : 0;
+        off[l + 1] = off[l] + bb;  // (an invalid count is reported by fwd_bin_alloc)
+      }
+      FwdCam& c0 = cams[(size_t)G.live[0]];
+      char* base = (char*)c0.alloc(c0.alloc_ctx, off[nl] ? off[nl] : 256, GSR_BUF_BINNING);
+      if (!base) return fail(GSR_ERR_ALLOC, "binning buffer allocation of %zu bytes failed", off[nl]);
+      for (int l = 0; l < nl; l++) cams[(size_t)G.live[(size_t)l]].given_b = base + off[l];
+    }
+    for (int l = 0; l < nl; l++) {
+      FwdCam& c = cams[(size_t)G.live[(size_t)l]];
+      if (int rc = fwd_bin_alloc(m, c, /*tag_by_dup=*/true)) return rc;  // (debug: checks the depth sort)
+      const GeomState& g = c.g;
+      const BinState& b = c.b;
+      const uint32_t R = (uint32_t)c.num_instances;
+      dup[l] = DupSpec{P, G.depth_in_b ? g.dval_b : g.dval_a, g.offsets, g.rec, c.gx, c.gy,
+                       b.tkey_a, b.tval_a, R,
+                       SideClear{b.sort.aux, sort_clear_bytes(b.sort, R, tbits)},
+                       SideClear{c.im.ranges, sizeof(uint2) * ntiles},
+                       m.rows ? b.egid : nullptr, m.rows ? g.ebeg : nullptr, b.tag,
+                       bin_layout_tag(m.det, m.rows)};
+      ts[l] = SortSpec{b.tkey_a, b.tval_a, b.tkey_b, b.tval_b, (size_t)R, b.sort, nullptr};
+    }
+    PROF_BEGIN(DUPLICATE);
+    GSR_CHECK(launch_duplicate_views(dup, nl, stream));
+    PROF_END(DUPLICATE);
+    bool t_in_b = false;
+    PROF_BEGIN(TILE_SORT);
+    GSR_CHECK(radix_sort_pairs_views(ts, nl, tbits, &t_in_b, stream, false, /*precleared=*/true));
+    PROF_END(TILE_SORT);
+    RangesSpec rs[kMaxBatchViews];
+    for (int l = 0; l < nl; l++) {
+      FwdCam& c = cams[(size_t)G.live[(size_t)l]];
+      const BinState& b = c.b;
+      const uint32_t R = (uint32_t)c.num_instances;
+      if (debug)
+        if (int rc = check_sort_err(b.sort.aux + kSortAuxErr, stream, "tile sort")) return rc;
+      const uint32_t* tiles_sorted = t_in_b ? b.tkey_b : b.tkey_a;
+      const uint32_t* point_list = t_in_b ? b.tval_b : b.tval_a;
+      if (m.rows) {
+        uint32_t* pl = t_in_b ? b.tval_a : b.tval_b;
+        GSR_CHECK(launch_det_gather(R, point_list, b.egid, pl, stream));
+        point_list = pl;
+      }
+      int mail_slot = -1;
+      uint32_t* host_status = mail_post(c.ibase, &mail_slot);
+      rs[l] = RangesSpec{R, tiles_sorted, c.im.ranges, ntiles, c.g.sort.aux + kSortAuxErr,
+                         b.sort.aux + kSortAuxErr, c.im.status, host_status,
+                         forward_faults_word()};
+      fwd_render_args(m, c, point_list, host_status);
+      c.ra.clear = c.acc_clear;
+      c.mail_slot = mail_slot;
+      ras[l] = c.ra;
+    }
+    PROF_BEGIN(RANGES);
+    GSR_CHECK(launch_tile_ranges_views(rs, nl, stream));
+    GSR_CHECK(launch_render_schedule_views(ras, nl, stream));
+    PROF_END(RANGES);
     return GSR_OK;
   };
-  // phase 2b of a group: its blend (after every group's binning has been issued, so a group's
-  // latency-bound binning never queues for CUs behind another group's full-chip blend)
+  // phase 2b of a group: its blend on the group's stream, which then joins the call's stream
   auto phase2b = [&](int gi) -> int {
     Group& G = grp[(size_t)gi];
-    const RenderArgs* ras = G.ras;
-    hipStream_t stream = G.st;
     const int nl = (int)G.live.size();
-    // the group's stream joins the call's stream here; with GSR_VIEWS_RENDER_CALL the blend then
-    // runs on the call's stream (the blends in group order there, the backward right behind
-    // the last), else on the group's stream before the join
-    const bool on_call = render_on_call() && G.st != call_stream;
-    auto join = [&]() -> int {
-      if (G.st == call_stream) return GSR_OK;
-      hipEvent_t e = join_event(gi);
-      if (!e || hipEventRecord(e, G.st) != hipSuccess ||
-          hipStreamWaitEvent(call_stream, e, 0) != hipSuccess)
-        return fail(GSR_ERR_HIP, "joining group %d's stream failed", gi);
-      return GSR_OK;
-    };
-    if (on_call)
-      if (int rc = join()) return rc;
-    hipStream_t rstream = on_call ? call_stream : stream;
+    hipStream_t stream = G.st;
     if (nl > 0) {
-      hipStream_t stream = rstream;
       PROF_BEGIN(RENDER_FWD);
-      GSR_CHECK(launch_render_forward_views(ras, nl, stream));
-      ht.mark("f", gi);
+      GSR_CHECK(launch_render_forward_views(G.ras, nl, stream));
       PROF_END(RENDER_FWD);
     }
     for (int k = 0; k < G.n; k++) {
       const int v = G.v0 + k;
       FwdCam& c = cams[(size_t)v];
       if (c.done) c.num_rendered = c.num_instances = 0;
-      if (int rc = fwd_blended(m, c, rstream)) return rc;
-      ht.mark("B", k);
+      if (int rc = fwd_blended(m, c, stream)) return rc;
       gsr_view& out = views[v];
       out.geom_buffer = c.gbase; out.binning_buffer = c.bbase; out.image_buffer = c.ibase;
       out.num_rendered = c.num_rendered; out.num_instances = c.num_instances;
     }
-    if (!on_call)
-      if (int rc = join()) return rc;
+    if (G.st != call_stream) {
+      hipEvent_t e = join_event(gi);
+      if (!e || hipEventRecord(e, G.st) != hipSuccess ||
+          hipStreamWaitEvent(call_stream, e, 0) != hipSuccess)
+        return fail(GSR_ERR_HIP, "joining group %d's stream failed", gi);
+    }
     return GSR_OK;
   };
-  // `lead` groups' first phases are queued ahead of the first wait; each later group's right
-  // after the phase 2 of the group `lead` before it (GSR_VIEWS_LEAD, default all groups at once)
-  static const int lead_env = [] {
-    const char* e = getenv("GSR_VIEWS_LEAD");
-    return e ? atoi(e) : 0;
-  }();
-  const int lead = (lead_env < 1 || lead_env > ng) ? ng : lead_env;
-  for (int gi = 0; gi < lead; gi++) {
+  // Round 4 (profiles/r04_pipeline_ab.txt): every group's binning before the blends measured
+  // slower than binning + blend per group -- the later group's binning then overlaps the earlier
+  // group's blend (a full-chip launch) instead of running beside the other latency-bound binning
+  for (int gi = 0; gi < ng; gi++)
     if (int rc = phase1(gi)) return rc;
-    ht.mark("p", gi);
-  }
-  // GSR_VIEWS_BIN_FIRST=1: every group's binning, then the blends; default 0 = per group binning
-  // + blend.  Round 4 (profiles/r04_pipeline_ab.txt): 2090 / 2107 views/s with it against 2096 /
-  // 2117 without -- the later group's binning then overlaps the earlier group's blend (a full-chip
-  // launch) instead of running beside the other latency-bound binning, which hides as much
-  // latency as it saves queueing
-  static const bool bin_first = [] {
-    const char* e = getenv("GSR_VIEWS_BIN_FIRST");
-    return e && atoi(e) == 1;
-  }();
   for (int gi = 0; gi < ng; gi++) {
     if (int rc = phase2a(gi)) return rc;
-    if (!bin_first)
-      if (int rc = phase2b(gi)) return rc;
-    if (gi + lead < ng)
-      if (int rc = phase1(gi + lead)) return rc;
+    if (int rc = phase2b(gi)) return rc;
   }
-  if (bin_first)
-    for (int gi = 0; gi < ng; gi++)
-      if (int rc = phase2b(gi)) return rc;
-  ht.mark("end", 0);
   g_last_instances = cams[(size_t)V - 1].num_instances;
   return GSR_OK;
-}
-
-bool views_batched() {
-  static const bool on = [] {
-    const char* e = getenv("GSR_VIEWS_BATCHED");
-    return e ? atoi(e) != 0 : true;
-  }();
-  return on;
 }
 }  // namespace
 
@@ -1545,7 +1375,7 @@ int gsr_rasterize_views_fused(int V, gsr_view* views, int image_height, int imag
     return fail(GSR_ERR_ARGUMENT, "image size must be positive (got %dx%d)", image_width, image_height);
   FwdModel m;
   m.det = (debug & GSR_DEBUG_DETERMINISTIC) != 0;
-  m.rows = m.det || bwd_rows_mode();
+  m.rows = m.det;
   m.debug = debug & 1;
   m.P = P; m.M = M; m.background = background; m.means3D = means3D;
   m.opacities = opacity_raw; m.scales = scaling_raw; m.rotations = rotation_raw;
@@ -1565,8 +1395,6 @@ int gsr_rasterize_views_fused(int V, gsr_view* views, int image_height, int imag
     c.out_feature = in.out_feature; c.radii = in.radii;
     c.alloc = alloc; c.alloc_ctx = in.alloc_ctx;
     c.stream = in.stream ? (hipStream_t)in.stream : call_stream;
-    c.host = pinned_slot(v);
-    c.ready = readback_event(v);
   }
   // the views' streams start after the call's stream (inputs prepared there)
   hipEvent_t start = join_event(kFwdSlots);
@@ -1576,96 +1404,9 @@ int gsr_rasterize_views_fused(int V, gsr_view* views, int image_height, int imag
     if (cams[(size_t)v].stream != call_stream &&
         hipStreamWaitEvent(cams[(size_t)v].stream, start, 0) != hipSuccess)
       return fail(GSR_ERR_HIP, "stream wait failed");
-  // Software-pipelined, readiness-driven issue.  Each view stream holds one view in flight: its
-  // first phase (preprocess .. scan, read-back) is queued, and when the host sees that view's
-  // read-back complete -- whichever stream's comes first -- it issues the view's binning and then
-  // the first phase of the next view assigned to that stream, so per stream the order stays
-  // begin(a), bin(a), begin(b), bin(b), ... and no stream idles behind the host waiting for
-  // another stream's view.  The blends of a group of consecutive views (`groups` groups;
-  // GSR_VIEWS_FWD_GROUPS) run merged into one launch on the call's stream once the group's
-  // binning has been issued, in group order.
-  static const int groups_env = [] {
-    const char* e = getenv("GSR_VIEWS_FWD_GROUPS");
-    return e ? atoi(e) : 2;
-  }();
-  (void)inflight;  // one view in flight per distinct view stream
-  const int ng = groups_env < 1 ? 1 : groups_env;
-  if (views_batched()) return views_forward_batched(m, cams, views, call_stream, ng);
-  int per = (V + ng - 1) / ng;
-  if (per < 1) per = 1;
-  if (per > kMaxFwdViews) per = kMaxFwdViews;
-  std::vector<int> state((size_t)V, 0);  // 0 = not begun, 1 = first phase queued, 2 = binned
-  auto begin_next_on = [&](hipStream_t st) -> int {
-    for (int u = 0; u < V; u++)
-      if (state[(size_t)u] == 0 && cams[(size_t)u].stream == st) {
-        for (int w = 0; w < u; w++)  // one view in flight per stream
-          if (state[(size_t)w] == 1 && cams[(size_t)w].stream == st) return GSR_OK;
-        if (int rc = fwd_begin(m, cams[(size_t)u])) return rc;
-        state[(size_t)u] = 1;
-        return GSR_OK;
-      }
-    return GSR_OK;
-  };
-  for (int v = 0; v < V; v++)
-    if (int rc = begin_next_on(cams[(size_t)v].stream)) return rc;
-  int binned = 0, next_group = 0;
-  while (binned < V || next_group * per < V) {
-    bool progressed = false;
-    for (int v = 0; v < V; v++) {
-      if (state[(size_t)v] != 1) continue;
-      FwdCam& c = cams[(size_t)v];
-      if (!c.done) {
-        const hipError_t q = hipEventQuery(c.ready);
-        if (q == hipErrorNotReady) continue;
-        if (q != hipSuccess) return fail(GSR_ERR_HIP, "hipEventQuery: %s", hipGetErrorString(q));
-      }
-      if (int rc = fwd_bin(m, c)) return rc;
-      if (!c.done) {
-        const int debug = m.debug;
-        hipStream_t stream = c.stream;
-        GSR_CHECK(launch_render_schedule(c.ra, stream));
-      }
-      state[(size_t)v] = 2;
-      binned++;
-      progressed = true;
-      gsr_view& out = views[v];
-      out.geom_buffer = c.gbase; out.binning_buffer = c.bbase; out.image_buffer = c.ibase;
-      out.num_rendered = c.num_rendered; out.num_instances = c.num_instances;
-      if (c.stream != call_stream) {
-        hipEvent_t e = join_event(v);
-        if (!e || hipEventRecord(e, c.stream) != hipSuccess ||
-            hipStreamWaitEvent(call_stream, e, 0) != hipSuccess)
-          return fail(GSR_ERR_HIP, "joining view %d's stream failed", v);
-      }
-      if (int rc = begin_next_on(c.stream)) return rc;
-    }
-    // merged blends of the groups whose views are all binned, in group order
-    while (next_group * per < V) {
-      const int v0 = next_group * per;
-      const int n = V - v0 < per ? V - v0 : per;
-      bool ready = true;
-      for (int k = 0; k < n; k++) ready = ready && state[(size_t)(v0 + k)] == 2;
-      if (!ready) break;
-      RenderArgs ras[kMaxFwdViews];
-      int nb = 0;
-      for (int k = 0; k < n; k++)
-        if (!cams[(size_t)(v0 + k)].done) ras[nb++] = cams[(size_t)(v0 + k)].ra;
-      if (nb > 0) {
-        const int debug = m.debug;
-        hipStream_t stream = call_stream;
-        PROF_BEGIN(RENDER_FWD);
-        GSR_CHECK(launch_render_forward_views(ras, nb, call_stream));
-        PROF_END(RENDER_FWD);
-      }
-      for (int k = 0; k < n; k++)
-        if (int rc = fwd_blended(m, cams[(size_t)(v0 + k)], call_stream)) return rc;
-      next_group++;
-      progressed = true;
-    }
-    if (!progressed) std::this_thread::yield();  // every view in flight still computes
-  }
-  if (V > 0) g_last_instances = cams[(size_t)V - 1].num_instances;
-  return GSR_OK;
+  (void)inflight;  // one group in flight per distinct view stream
+  // two groups: group 1's binning overlaps group 0's blend
+  return views_forward_batched(m, cams, views, call_stream, 2);
 }
 
 int gsr_rasterize_views_fused_backward(
@@ -1720,25 +1461,14 @@ int gsr_rasterize_views_fused_backward_sliced(
     if (on_rows && P > 0) on_rows(rows_ctx, 0, P);
     return GSR_OK;
   }
-  // The backward blends of all views run on views[0].stream, merged into launches of up to
-  // kMaxBwdViews views (`chunks` launches; one launch's tiles are its views' tiles, so no per-view
-  // tail of idle CUs); the per-Gaussian parts read-modify-write the leaves' gradients and run in
-  // view order on the call's stream, each after the launch holding its view.
-  static const int chunks_env = [] {
-    const char* e = getenv("GSR_VIEWS_BWD_CHUNKS");
-    return e ? atoi(e) : 1;
-  }();
-  int per = (V + (chunks_env > 0 ? chunks_env : 1) - 1) / (chunks_env > 0 ? chunks_env : 1);
-  if (per > kMaxBwdViews) per = kMaxBwdViews;
-  // one chunk: the blend runs on the call's stream too (nothing to overlap it with, and no
-  // cross-stream hops before and after it); several: on views[0].stream, beside the previous
-  // chunk's per-Gaussian backward
-  static const bool side_env = [] {  // GSR_VIEWS_BWD_SIDE=1: the side stream even for one chunk
-    const char* e = getenv("GSR_VIEWS_BWD_SIDE");
-    return e && atoi(e) != 0;
-  }();
-  hipStream_t bs = (views[0].stream && (per < V || side_env)) ? (hipStream_t)views[0].stream
-                                                              : call_stream;
+  // The backward blends of all views run merged into launches of up to kMaxBwdViews views (one
+  // launch's tiles are its views' tiles, so no per-view tail of idle CUs); the per-Gaussian parts
+  // read-modify-write the leaves' gradients and run in view order on the call's stream, each
+  // after the launch holding its view.  One launch: the blend runs on the call's stream too
+  // (nothing to overlap it with); several: on views[0].stream, beside the previous launch's
+  // per-Gaussian backward.
+  const int per = V < kMaxBwdViews ? V : kMaxBwdViews;
+  hipStream_t bs = (views[0].stream && per < V) ? (hipStream_t)views[0].stream : call_stream;
   hipEvent_t start = join_event(kFwdSlots);  // the upstream gradients were produced on the call's stream
   if (bs != call_stream) {
     if (!start || hipEventRecord(start, call_stream) != hipSuccess)
@@ -1787,7 +1517,7 @@ int gsr_rasterize_views_fused_backward_sliced(
     // slice while the next one computes)
     const bool last = v0 + per >= V;
     const uint32_t step = (last && on_rows && slice_rows > 0) ? (uint32_t)slice_rows : (uint32_t)P;
-    if (np > 1 && views_pre_merged() && !per_view_pre) {
+    if (np > 1 && !per_view_pre) {
       const int debug = debug_sync;
       hipStream_t stream = call_stream;
       PROF_BEGIN(PREPROCESS_BWD);
@@ -2016,7 +1746,7 @@ int gsr_test_binning_lists(const void* binning_buffer, const void* image_buffer,
       image_width <= 0 || !image_buffer || !ranges_out ||
       (n_instances && (!binning_buffer || !point_list_out)))
     return fail(GSR_ERR_ARGUMENT, "invalid arguments");
-  const bool rows = (flags & GSR_DEBUG_DETERMINISTIC) != 0 || bwd_rows_mode();
+  const bool rows = (flags & GSR_DEBUG_DETERMINISTIC) != 0;
   const uint32_t gx = (uint32_t)((image_width + kTile - 1) / kTile);
   const uint32_t gy = (uint32_t)((image_height + kTile - 1) / kTile);
   const ImgState im = carve_img((char*)image_buffer, (size_t)image_width, (size_t)image_height);

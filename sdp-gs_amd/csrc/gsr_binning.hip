@@ -14,24 +14,11 @@
 #include "gsr_device.h"
 #include "gsr_internal.h"
 
-// 1: the duplication takes each Gaussian's kept tile range per row from the preprocess's packed
-// rec[3].w (rectangles of at most 4 rows x 15 tiles) instead of re-running cut_row_range
-#ifndef GSR_DUP_ROWPACK
-#define GSR_DUP_ROWPACK 1
-#endif
-
 namespace gsr {
 namespace {
 
 constexpr int kThreads = 256;
 
-// 1 (default): the LDS-staged duplication below; 0: each lane stores at its own offsets
-#ifndef GSR_DUP_LDS
-#define GSR_DUP_LDS 1
-#endif
-#ifndef GSR_DUP_WIN
-#define GSR_DUP_WIN 256
-#endif
 // wave-scope ordering of LDS stores before other lanes' loads of the same wave
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -39,11 +26,16 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Staged variant: a wave's 64 depth-consecutive Gaussians own one contiguous range of instances;
-// every lane enumerates its tiles (same order) into a per-wave LDS window, then the wave copies
-// the window out with coalesced stores (the direct variant stores each lane's ids at its own
-// offsets: 64 scattered lines per store instruction).
-__device__ __forceinline__ void duplicate_body_lds(int P, const uint32_t* __restrict__ order,
+// One lane per depth-sorted Gaussian, enumerating its kept tiles row-major over its tile
+// rectangle (the reference's emission order inside one Gaussian, rasterizer_impl.cu:98-109).  A
+// wave's 64 depth-consecutive Gaussians own one contiguous range of instances: every lane writes
+// its tile ids into a per-wave LDS window, then the wave copies the window out with coalesced
+// stores (each lane storing at its own offsets puts 64 scattered lines in every store
+// instruction).  Each Gaussian's kept range per tile row comes from the preprocess's packed
+// rec[3].w (rectangles of at most 4 rows x 15 tiles), else from cut_row_range itself.
+// (body shared by the one-view kernel and the several-views kernel: blk / nblk = this
+// workgroup's index and the workgroup count of its view)
+__device__ __forceinline__ void duplicate_body(int P, const uint32_t* __restrict__ order,
                                                    const uint32_t* __restrict__ offsets,
                                                    const float4* __restrict__ rec, uint32_t gx,
                                                    uint32_t gy, uint32_t* __restrict__ tkey,
@@ -51,8 +43,8 @@ __device__ __forceinline__ void duplicate_body_lds(int P, const uint32_t* __rest
                                                    SideClear clear0, SideClear clear1,
                                                    uint32_t* __restrict__ egid,
                                                    uint32_t* __restrict__ ebeg, uint32_t blk,
-                                                   uint32_t nblk, const float4* __restrict__ drec) {
-  constexpr int kWin = GSR_DUP_WIN;  // instances per wave window
+                                                   uint32_t nblk) {
+  constexpr int kWin = 256;  // instances per wave window
   __shared__ uint32_t s_key[kThreads / 64][kWin];
   __shared__ uint32_t s_val[kThreads / 64][kWin];
   __shared__ uint32_t s_eg[kThreads / 64][kWin];
@@ -87,23 +79,14 @@ __device__ __forceinline__ void duplicate_body_lds(int P, const uint32_t* __rest
     float4 r0;
     float qc, rad;
     float cc;
-    if (drec) {  // the depth sort's binning record of this position: no gather
-      r0 = drec[2 * (size_t)s];
-      const float4 b = drec[2 * (size_t)s + 1];  // {conic.c, q_cut, radius, id}
-      gid = min(__float_as_uint(b.w), (uint32_t)P - 1u);
-      cc = b.x;
-      qc = b.y;
-      rad = b.z;
-    } else {
-      gid = min(order[s], (uint32_t)P - 1u);
-      r0 = rec[4 * (size_t)gid];
-      const float4 r3 = rec[4 * (size_t)gid + 3];
-      qc = r3.z;
-      rad = r3.y;
-      if (GSR_DUP_ROWPACK) rows = __float_as_uint(r3.w);
-      // conic.c only for the cut itself (rows not packed)
-      cc = rows == kNoRowPack ? rec[4 * (size_t)gid + 1].x : 0.0f;
-    }
+    gid = min(order[s], (uint32_t)P - 1u);  // in range unless a sort gave up (reported)
+    r0 = rec[4 * (size_t)gid];
+    const float4 r3 = rec[4 * (size_t)gid + 3];  // {f2, radius, q_cut, rows}
+    qc = r3.z;
+    rad = r3.y;
+    rows = __float_as_uint(r3.w);
+    // conic.c only for the cut itself (rows not packed)
+    cc = rows == kNoRowPack ? rec[4 * (size_t)gid + 1].x : 0.0f;
     if (egid) ebeg[gid] = off;
     tile_rect(r0.x, r0.y, (int)rad, gx, gy, x0, y0, x1, y1);
     if (rows == kNoRowPack) cut = make_cut(r0.x, r0.y, r0.z, r0.w, cc, qc);
@@ -139,61 +122,6 @@ __device__ __forceinline__ void duplicate_body_lds(int P, const uint32_t* __rest
   }
 }
 
-// One lane per depth-sorted Gaussian; the lane writes its tile ids row-major over its tile
-// rectangle (the reference's emission order inside one Gaussian, rasterizer_impl.cu:98-109).
-// (body shared by the one-view kernel and the several-views kernel: blk / nblk = this
-// workgroup's index and the workgroup count of its view)
-__device__ __forceinline__ void duplicate_body(int P, const uint32_t* __restrict__ order,
-                                               const uint32_t* __restrict__ offsets,
-                                               const float4* __restrict__ rec, uint32_t gx,
-                                               uint32_t gy, uint32_t* __restrict__ tkey,
-                                               uint32_t* __restrict__ tval, uint32_t R,
-                                               SideClear clear0, SideClear clear1,
-                                               uint32_t* __restrict__ egid,
-                                               uint32_t* __restrict__ ebeg, uint32_t blk,
-                                               uint32_t nblk, const float4* __restrict__ drec) {
-  if (GSR_DUP_LDS || drec) {
-    duplicate_body_lds(P, order, offsets, rec, gx, gy, tkey, tval, R, clear0, clear1, egid, ebeg,
-                       blk, nblk, drec);
-    return;
-  }
-  const int s = (int)(blk * kThreads + threadIdx.x);
-  const size_t nth = (size_t)nblk * kThreads;
-  side_clear(clear0.p, clear0.bytes, (size_t)s, nth);
-  side_clear(clear1.p, clear1.bytes, (size_t)s, nth);
-  if (s >= P) return;
-  // coalesced reads first: culled / tile-less Gaussians (count 0) never touch the random gather
-  uint32_t off = (s == 0) ? 0u : offsets[s - 1];
-  const uint32_t end = min(offsets[s], R);
-  if (off == end) return;
-  const uint32_t gid = min(order[s], (uint32_t)P - 1u);  // in range unless a sort gave up (reported)
-  // the radius travels in the record (rec[3].y, exact as float): the gather stays inside the
-  // Gaussian's 64-byte record line
-  const float4 r0 = rec[4 * (size_t)gid];
-  const float4 r1 = rec[4 * (size_t)gid + 1];
-  const float4 r3 = rec[4 * (size_t)gid + 3];  // {f2, radius, q_cut, -}
-  const int r = (int)r3.y;
-  if (egid) ebeg[gid] = off;  // rows layout: the Gaussian's rows start at its first instance
-  uint32_t x0, y0, x1, y1;
-  tile_rect(r0.x, r0.y, r, gx, gy, x0, y0, x1, y1);
-  // exactly the per-row tile ranges the preprocess counted (cut_row_range, gsr_device.h)
-  const SplatCut cut = make_cut(r0.x, r0.y, r0.z, r0.w, r1.x, r3.z);
-  for (uint32_t y = y0; y < y1 && off < end; y++) {
-    uint32_t a, b;
-    cut_row_range(cut, y, x0, x1, a, b);
-    for (uint32_t x = a; x < b && off < end; x++) {
-      tkey[off] = y * gx + x;
-      if (egid) {  // rows layout: sort the emission index, keep its Gaussian aside
-        tval[off] = off;
-        egid[off] = gid;
-      } else {
-        tval[off] = gid;
-      }
-      off++;
-    }
-  }
-}
-
 __global__ __launch_bounds__(kThreads) void duplicate_kernel(int P,
                                                              const uint32_t* __restrict__ order,
                                                              const uint32_t* __restrict__ offsets,
@@ -204,19 +132,14 @@ __global__ __launch_bounds__(kThreads) void duplicate_kernel(int P,
                                                              uint32_t R, SideClear clear0,
                                                              SideClear clear1,
                                                              uint32_t* __restrict__ egid,
-                                                             uint32_t* __restrict__ ebeg,
-                                                             const float4* __restrict__ drec) {
+                                                             uint32_t* __restrict__ ebeg) {
   duplicate_body(P, order, offsets, rec, gx, gy, tkey, tval, R, clear0, clear1, egid, ebeg,
-                 blockIdx.x, gridDim.x, drec);
+                 blockIdx.x, gridDim.x);
 }
 
 // Instances per lane of the ranges kernel: consecutive keys, one 16-B load when aligned (one
 // key per lane made the launch ~4x more workgroups than its 4-byte loads can keep busy).
-#ifndef GSR_RANGES_KPT
-#define GSR_RANGES_KPT 4
-#endif
-constexpr int kRangesKPT = GSR_RANGES_KPT;
-static_assert(kRangesKPT == 1 || kRangesKPT == 4, "ranges keys per lane");
+constexpr int kRangesKPT = 4;
 
 __device__ __forceinline__ void tile_ranges_body(size_t R, const uint32_t* __restrict__ tiles,
                                                  uint2* __restrict__ ranges, uint32_t ntiles,
@@ -303,8 +226,7 @@ __global__ __launch_bounds__(kThreads) void duplicate_views_kernel(DupViews m) {
   const DupSpec& j = m.j[k];
   if (j.tag && blockIdx.x == m.first[k] && threadIdx.x == 0) *j.tag = j.tag_val;
   duplicate_body(j.P, j.order, j.offsets, j.rec, j.gx, j.gy, j.tkey, j.tval, j.R, j.clear0,
-                 j.clear1, j.egid, j.ebeg, blockIdx.x - m.first[k], m.first[k + 1] - m.first[k],
-                 j.drec);
+                 j.clear1, j.egid, j.ebeg, blockIdx.x - m.first[k], m.first[k + 1] - m.first[k]);
 }
 
 __global__ __launch_bounds__(kThreads) void tile_ranges_views_kernel(RangesViews m) {
@@ -335,21 +257,11 @@ hipError_t launch_det_gather(size_t R, const uint32_t* einst, const uint32_t* eg
 hipError_t launch_duplicate(int P, const uint32_t* order, const uint32_t* offsets,
                             const int32_t* radii, const float4* rec, uint32_t gx, uint32_t gy,
                             uint32_t* tkey, uint32_t* tval, uint32_t R, SideClear clear0,
-                            SideClear clear1, hipStream_t s, uint32_t* egid, uint32_t* ebeg,
-                            const float4* drec) {
+                            SideClear clear1, hipStream_t s, uint32_t* egid, uint32_t* ebeg) {
   if (P == 0) return hipSuccess;
   hipLaunchKernelGGL(duplicate_kernel, dim3((P + kThreads - 1) / kThreads), dim3(kThreads), 0, s,
-                     P, order, offsets, rec, gx, gy, tkey, tval, R, clear0, clear1, egid, ebeg,
-                     drec);
+                     P, order, offsets, rec, gx, gy, tkey, tval, R, clear0, clear1, egid, ebeg);
   return hipGetLastError();
-}
-
-bool dup_drec() {
-  static const bool on = [] {
-    const char* e = getenv("GSR_DUP_DREC");
-    return e && atoi(e) == 1;
-  }();
-  return on;
 }
 
 hipError_t launch_duplicate_views(const DupSpec* v, int V, hipStream_t s) {

@@ -125,16 +125,10 @@ hipError_t reduce_u32(const uint32_t* in, size_t n, uint32_t* parts, uint32_t* o
 // key_payload: when set, the LAST pass writes key_payload[value] instead of the sorted key (the
 // keys themselves are not needed afterwards): the depth sort hands the scan its tile counts
 // already in depth order, one gather inside the sort instead of two in the scan.
-// rec_payload / rec_out (round 4): the last pass instead gathers each value's splat record (4
-// float4 per Gaussian, preprocess layout) and writes the tile count rec[3].w as the key and the
-// binning record {x, y, conic.a, conic.b}, {conic.c, q_cut, radius, id} to rec_out[2 o .. 2 o + 1]
-// at the element's sorted position o -- the duplication then reads its Gaussians' records in depth
-// order, coalesced, instead of gathering them by id.
 hipError_t radix_sort_pairs(uint32_t* ka, uint32_t* va, uint32_t* kb, uint32_t* vb, size_t n,
                             int bits, SortScratch scratch, bool* result_in_b, hipStream_t s,
                             bool sentinel_anywhere = false, bool precleared = false,
-                            const uint32_t* key_payload = nullptr,
-                            const float4* rec_payload = nullptr, float4* rec_out = nullptr);
+                            const uint32_t* key_payload = nullptr);
 // Several independent sorts / scans / sums, one launch per stage for all of them (the multi-view
 // forward's batched binning, gsr_api.cpp): a view's workgroups are a contiguous block range of
 // the launch, and inside it everything is the one-view kernel's (own totals, tickets, look-back
@@ -146,8 +140,6 @@ struct SortSpec {
   size_t n;
   SortScratch scratch;
   const uint32_t* key_payload;
-  const float4* rec_payload = nullptr;  // see radix_sort_pairs
-  float4* rec_out = nullptr;
 };
 hipError_t radix_sort_pairs_views(const SortSpec* v, int V, int bits, bool* result_in_b,
                                   hipStream_t s, bool sentinel_anywhere, bool precleared);
@@ -198,10 +190,9 @@ struct GeomState {
   uint8_t* clamped;         // [P] bit c set <=> SH colour channel c clamped (forward.cu:67-69)
   int32_t* radii;           // [P] internal radii (used when the caller passes none)
   float4* rec;              // [P*4] splat record for the blend
-  float4* drec;             // [P*2] binning records in depth order (the depth sort's last pass)
   uint32_t* tiles_touched;  // [P]
   uint32_t* offsets;        // [P] inclusive scan of tiles_touched in depth order
-  float* acc;               // [P*16] backward accumulators (atomic mode only, see bwd_rows_mode)
+  float* acc;               // [P*16] backward accumulators (atomic mode; not the deterministic backward)
   uint32_t* ebeg;           // [P] per Gaussian id: its first emission index (rows mode, DET)
   uint32_t* flags;          // [4]  [0]: prefiltered violation
   SortScratch sort;         // depth-sort scratch
@@ -224,21 +215,14 @@ struct BinState {
   uint32_t* tkey_b;
   uint32_t* tval_b;
   SortScratch sort;  // tile-sort scratch
-  // rows layout (bwd_rows_mode() or the deterministic backward, gsr.h debug bit 1): the tile
-  // sort carries each instance's emission index e (depth order, Gaussian-major) instead of its
-  // Gaussian id, and the backward blend stores one gradient row per instance instead of float
-  // atomics
+  // rows layout (the deterministic backward, gsr.h debug bit 1): the tile sort carries each
+  // instance's emission index e (depth order, Gaussian-major) instead of its Gaussian id, and the
+  // backward blend stores one gradient row per instance instead of float atomics
   uint32_t* egid;    // [R] Gaussian id of emission index e
   float* partial;    // [R][kAccFloats] the blend backward's gradient row of each instance, by e
   size_t bytes;
 };
 BinState carve_bin(char* base, size_t R, bool rows = false);
-// Backward gradient path (process-wide, env GSR_BWD_ROWS, default 0): true = the backward blend
-// stores one 64-B gradient row per (splat, tile) instance (plain coalesced stores, no global float
-// atomics) and the backward preprocess sums each Gaussian's rows (contiguous in emission order);
-// false = float atomics into one accumulator row per Gaussian.  The deterministic backward always
-// uses rows.  Fixed for the process, so a forward's layout is the one its backward expects.
-bool bwd_rows_mode();
 // rec[3].w of a splat record whose per-row tile ranges did not fit the packing (gsr_preprocess.hip)
 constexpr uint32_t kNoRowPack = 0xffffffffu;
 constexpr uint32_t kBinLayoutMagic = 0x47535200u;  // "GSR\0"
@@ -381,18 +365,11 @@ hipError_t launch_sh_grad_flush(const ShFlushArgs& a, hipStream_t s);
 // R bounds the writes (offsets of a complete depth order never exceed it).
 // egid != nullptr (rows layout): tval gets emission indices, egid[e] the Gaussian id and
 // ebeg[gid] the Gaussian's first emission index.
-// drec != nullptr: the Gaussians' binning records in depth order (radix_sort_pairs rec_out) are
-// read instead of order[] and the records gathered from rec.
 hipError_t launch_duplicate(int P, const uint32_t* order, const uint32_t* offsets,
                             const int32_t* radii, const float4* rec, uint32_t gx, uint32_t gy,
                             uint32_t* tkey, uint32_t* tval, uint32_t R, SideClear clear0,
                             SideClear clear1, hipStream_t s, uint32_t* egid = nullptr,
-                            uint32_t* ebeg = nullptr, const float4* drec = nullptr);
-// whether the forward hands the duplication depth-ordered binning records (env GSR_DUP_DREC=1;
-// default 0 = the duplication gathers the splat records by id).  Round 4, alternating runs:
-// duplicate 0.094 -> 0.074 ms per 3 views, but the depth sort 0.131 -> 0.177 (its last pass then
-// gathers 48 B and writes 32 B more per Gaussian): 2.88-2.91 vs 2.93-2.96 ms per step -- off
-bool dup_drec();
+                            uint32_t* ebeg = nullptr);
 // ranges_cleared: the ranges are already zero (duplicate's side clear): no memset launch.
 // Also writes the call's status word from the depth / tile sorts' error words (either may be null).
 // A failed call also or-s its status into `fault` (forward_faults_word(), may be null).
@@ -414,7 +391,6 @@ struct DupSpec {
   SideClear clear0, clear1;
   uint32_t* egid;
   uint32_t* ebeg;
-  const float4* drec = nullptr;
   uint32_t* tag = nullptr;  // written with tag_val by the launch (the binning buffer's layout tag)
   uint32_t tag_val = 0;
 };

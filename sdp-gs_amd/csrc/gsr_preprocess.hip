@@ -192,21 +192,6 @@ __device__ __forceinline__ uint32_t preprocess_gaussian(const PreArgs& a, int id
 // transposed through LDS at an 80-byte row stride) instead of 16-byte pieces at a 64-byte lane
 // stride.  Each workgroup also writes the sum of its tile counts (a.parts), so R = sum of the
 // partials needs one more small launch instead of a separate pass over tiles_touched.
-#ifndef GSR_PRE_STAGE
-#define GSR_PRE_STAGE 0
-#endif
-// n rows of 3 floats from g (row 0 at a 3-KB-aligned offset of the array) into LDS s
-__device__ __forceinline__ void stage_rows3(const float* __restrict__ g, int n, float* s) {
-  const int nf = 3 * n;
-  if ((reinterpret_cast<uintptr_t>(g) & 15u) == 0) {
-    const int n4 = nf >> 2;
-    const float4* g4 = reinterpret_cast<const float4*>(g);
-    for (int q = (int)threadIdx.x; q < n4; q += kThreads) reinterpret_cast<float4*>(s)[q] = g4[q];
-    for (int q = 4 * n4 + (int)threadIdx.x; q < nf; q += kThreads) s[q] = g[q];
-  } else {
-    for (int q = (int)threadIdx.x; q < nf; q += kThreads) s[q] = g[q];
-  }
-}
 // The workgroup's records in LDS, 4 float4 slots per lane, part k of lane l's record in slot
 // 4 l + (k ^ rec_swizzle(l)).  Lane stores (ds_write_b128, 8-lane groups over 32 banks): the
 // swizzle puts the 8 lanes of a group on 8 different 16-byte bank quads; the epilogue's linear
@@ -267,24 +252,9 @@ __global__ __launch_bounds__(kThreads) void preprocess_kernel(PreArgs a) {
   const int idx = base + (int)threadIdx.x;
   const int n = min(kThreads, a.P - base);
   side_clear(a.clear.p, a.clear.bytes, (size_t)idx, (size_t)gridDim.x * kThreads);
-#if GSR_PRE_STAGE
-  // the [P,3] inputs (12-byte rows) enter as the workgroup's contiguous 3-KB segments in 16-byte
-  // loads instead of three 4-byte loads at a 12-byte lane stride; lane reads at a 3-dword LDS
-  // stride are bank-conflict free
-  __shared__ float s_m[3 * kThreads], s_s[3 * kThreads], s_l[3 * kThreads];
-  stage_rows3(a.means3D + 3 * (size_t)base, n, s_m);
-  const bool use_s = !a.cov3D_precomp, use_l = a.include_feature && !a.lang_precomp && a.sh_language;
-  if (use_s) stage_rows3(a.scales + 3 * (size_t)base, n, s_s);
-  if (use_l) stage_rows3(a.sh_language + 3 * (size_t)base, n, s_l);
-  __syncthreads();
-  const float* pm = s_m + 3 * threadIdx.x;
-  const float* ps = s_s + 3 * threadIdx.x;
-  const float* pl = s_l + 3 * threadIdx.x;
-#else
   const float* pm = a.means3D + 3 * (size_t)idx;
   const float* ps = a.scales + 3 * (size_t)idx;
   const float* pl = a.sh_language + 3 * (size_t)idx;
-#endif
   uint32_t rect = 0;
   const uint32_t count = idx < a.P ? preprocess_gaussian(a, idx, s_rec + threadIdx.x * kRecStride,
                                                          rec_swizzle(threadIdx.x), pm, ps, pl,
@@ -334,31 +304,6 @@ __global__ __launch_bounds__(kThreads, GSR_PRE_VIEWS_MINBLK) void preprocess_vie
     pre_epilogue(a, base, n, count, rect, s_rec, s_sum, s_rect);
     __syncthreads();  // s_rec / s_sum are the next view's
   }
-}
-
-// The same views in one launch with one view per workgroup instead of all of them per lane
-// (GSR_PRE_VIEWS_SPLIT=1, round 4): workgroup b runs preprocess_kernel's body for view b % V over
-// Gaussian block b / V -- the view-independent part and the model rows once per view again (the
-// V workgroups of a block are dispatched together, so the re-reads are cache hits), but every
-// lane's chain is one view long and the launch has V times the workgroups.
-__global__ __launch_bounds__(kThreads) void preprocess_views_split_kernel(PreViews m) {
-  __shared__ float4 s_rec[kThreads * kRecStride];
-  __shared__ uint32_t s_sum[kThreads / 64], s_rect[kThreads / 64];
-  const uint32_t k = blockIdx.x % (uint32_t)m.V, blk = blockIdx.x / (uint32_t)m.V;
-  const PreArgs& a = m.v[k];
-  const uint32_t nblk = gridDim.x / (uint32_t)m.V;
-  const int base = (int)(blk * kThreads);
-  const int idx = base + (int)threadIdx.x;
-  const int n = min(kThreads, a.P - base);
-  side_clear(a.clear.p, a.clear.bytes, (size_t)idx, (size_t)nblk * kThreads);
-  const float* pm = a.means3D + 3 * (size_t)idx;
-  const float* ps = a.scales + 3 * (size_t)idx;
-  const float* pl = a.sh_language + 3 * (size_t)idx;
-  uint32_t rect = 0;
-  const uint32_t count = idx < a.P ? preprocess_gaussian(a, idx, s_rec + threadIdx.x * kRecStride,
-                                                         rec_swizzle(threadIdx.x), pm, ps, pl,
-                                                         rect, nullptr) : 0u;
-  pre_epilogue_blk(a, base, n, count, rect, s_rec, s_sum, s_rect, blk, nblk);
 }
 
 // Workgroup size of the SH-row kernels (colour pre-pass here, SH flush in gsr_backward.hip):
@@ -467,15 +412,8 @@ hipError_t launch_preprocess_views(const PreArgs* views, int V, hipStream_t s) {
       return hipErrorInvalidValue;
     m.v[k] = a;
   }
-  static const bool split = [] {
-    const char* e = getenv("GSR_PRE_VIEWS_SPLIT");
-    return e && atoi(e) == 1;
-  }();
   const uint32_t nblk = (uint32_t)((a0.P + kThreads - 1) / kThreads);
-  if (split)
-    hipLaunchKernelGGL(preprocess_views_split_kernel, dim3(nblk * (uint32_t)V), dim3(kThreads), 0, s, m);
-  else
-    hipLaunchKernelGGL(preprocess_views_kernel, dim3(nblk), dim3(kThreads), 0, s, m);
+  hipLaunchKernelGGL(preprocess_views_kernel, dim3(nblk), dim3(kThreads), 0, s, m);
   return hipGetLastError();
 }
 

@@ -103,11 +103,8 @@ __global__ __launch_bounds__(1024) void scan_parts_kernel(uint32_t* __restrict__
   scan_parts_body(parts, n);
 }
 
-// GSR_SCAN_VEC: a lane's kScanItems consecutive counts as 16-byte loads and stores when the
-// arrays are aligned (workgroup-uniform test); else one 4-byte access per item
-#ifndef GSR_SCAN_VEC
-#define GSR_SCAN_VEC 1
-#endif
+// A lane's kScanItems consecutive counts as 16-byte loads and stores when the arrays are aligned
+// (workgroup-uniform test); else one 4-byte access per item
 template <bool GATHER, bool INCLUSIVE>
 __device__ __forceinline__ void scan_final_body(const uint32_t* __restrict__ in,
                                                 const uint32_t* __restrict__ gather, size_t n,
@@ -116,7 +113,7 @@ __device__ __forceinline__ void scan_final_body(const uint32_t* __restrict__ in,
   static_assert(kScanItems % 4 == 0, "vector scan items");
   __shared__ uint32_t lds[kThreads / 64];
   const size_t base = (size_t)blk * kScanTile + (size_t)threadIdx.x * kScanItems;
-  const bool vec = GSR_SCAN_VEC && !GATHER && base + kScanItems <= n &&
+  const bool vec = !GATHER && base + kScanItems <= n &&
                    (((uintptr_t)in | (uintptr_t)out) & 15u) == 0;
   uint32_t v[kScanItems];
   uint32_t s = 0;
@@ -206,48 +203,28 @@ __device__ uint32_t g_force_lookback_timeout;
 // step reads it and leaves the parameters and moments untouched while it is non-zero, so NaN
 // gradients of a failed call never reach them (the reference __trap()s, auxiliary.h:156-160).
 __device__ uint32_t g_forward_faults;
-#ifndef GSR_SORT_TRACE
-#define GSR_SORT_TRACE 0
-#endif
-#if GSR_SORT_TRACE
-// per-partition phase timestamps (100 MHz wall clock) of the last one-sweep pass:
-// [part][0..5] = start, ranked, scanned, looked back, reordered, stored; [part][6] = hw id
-__device__ uint64_t g_sort_trace[16384][8];
-#endif
 namespace {
 constexpr int kSpinLimit = 1 << 18;
 // One-sweep workgroup size: NT lanes share a partition of kSortTile keys.  More lanes keep the
 // ranking chain short (kSortTile / NT keys per lane) and hide its LDS latency with other waves
 // (256 lanes = one wave per SIMD, every latency exposed: 7.5 us of ranking per pass); but 1024-lane
 // workgroups (48 KB LDS, 16 waves) fit only 2 per CU, so with more than 2 x 256 partitions the
-// late ones wait for a slot.  GSR_SORT_THREADS = 0 picks 1024 when every partition is resident
-// at once and 512 otherwise; 256 / 512 / 1024 force one shape.
-#ifndef GSR_SORT_THREADS
-#define GSR_SORT_THREADS 0
-#endif
+// late ones wait for a slot.  1024 lanes when every partition is resident at once, else 512.
 constexpr uint32_t kResident1024 = 2 * 256;  // 1024-lane partitions resident at once (256 CUs)
 
-// Digit totals of every pass from the unsorted keys.  Its own tile (GSR_TOTALS_KPT keys per
-// thread) and a bounded grid striding over tiles: short per-workgroup chains for latency, and at
-// most GSR_TOTALS_GROUPS global atomics per counter at the end.
-#ifndef GSR_TOTALS_KPT
-#define GSR_TOTALS_KPT 8
-#endif
-#ifndef GSR_TOTALS_GROUPS
-#define GSR_TOTALS_GROUPS 1024
-#endif
-constexpr int kTotKPT = GSR_TOTALS_KPT;
+// Digit totals of every pass from the unsorted keys.  Its own tile (kTotKPT keys per thread) and a
+// bounded grid striding over tiles: short per-workgroup chains for latency, and at most
+// kTotGroups global atomics per counter at the end.
+constexpr int kTotKPT = 8;
+constexpr size_t kTotGroups = 1024;
 constexpr int kTotTile = kThreads * kTotKPT;
 
 // Digit width of a sort over `bits` key bits: the passes (ceil(bits / 8)) split the bits evenly
 // (12-bit tile ids: 6 + 6 instead of 8 + 4) -- fewer, longer runs per bucket in the scatter of the
 // first pass.  Any split gives the same stable order.
-#ifndef GSR_SORT_EVEN
-#define GSR_SORT_EVEN 1
-#endif
 __host__ __device__ __forceinline__ int sort_digit_width(int bits) {
   const int passes = (bits + 7) / 8;
-  return GSR_SORT_EVEN ? (bits + passes - 1) / passes : 8;
+  return (bits + passes - 1) / passes;
 }
 
 // (body shared by the one-sort kernel and the several-sorts kernel: blk / nblk = this
@@ -327,22 +304,12 @@ __device__ __forceinline__ void onesweep_body(
     int bits, const uint32_t* __restrict__ totals, const uint32_t* __restrict__ nsent_sh,
     uint32_t* __restrict__ ticket, uint64_t* __restrict__ status, uint32_t* __restrict__ err,
     uint32_t* __restrict__ kout, uint32_t* __restrict__ vout, const uint32_t* __restrict__ kpay,
-    const float4* __restrict__ rpay, float4* __restrict__ rout, uint32_t blk, uint32_t nblk) {
+    uint32_t blk, uint32_t nblk) {
   constexpr int kSortWaves = NT / 64, kSortThreads = NT;
   // one sorted element out at position o: its value, and its key -- or (last pass) the payload
-  // gathered by its value: kpay[v], or from the splat record rpay[4 v ..] the binning record
-  // rout[2 o ..] = {x, y, conic.a, conic.b}, {conic.c, q_cut, radius, v} with the tile count
-  // (rec[3].w) as the key, so the duplication reads its Gaussians in depth order without a gather
+  // gathered by its value, kpay[v]
   auto emit = [&](uint32_t o, uint32_t v, uint32_t k) {
-    if (rpay) {
-      const float4* r = rpay + 4 * (size_t)min(v, (uint32_t)n - 1u);
-      const float4 r0 = r[0], r1 = r[1], r3 = r[3];
-      kout[o] = kpay ? kpay[min(v, (uint32_t)n - 1u)] : __float_as_uint(r3.w);
-      rout[2 * (size_t)o] = r0;
-      rout[2 * (size_t)o + 1] = make_float4(r1.x, r3.z, r3.y, __uint_as_float(v));
-    } else {
-      kout[o] = kpay ? kpay[min(v, (uint32_t)n - 1u)] : k;
-    }
+    kout[o] = kpay ? kpay[min(v, (uint32_t)n - 1u)] : k;
     vout[o] = v;
   };
   constexpr int kKeysPerThread = kSortTile / NT, kKeysPerWave = kKeysPerThread * 64;
@@ -355,21 +322,10 @@ __device__ __forceinline__ void onesweep_body(
   __shared__ uint32_t s_part;
   const int t = (int)threadIdx.x, lane = t & 63, wid = t >> 6;
   const uint32_t mask = (1u << bits) - 1u;
-#if GSR_SORT_TRACE
-  uint64_t tr[6];
-#define SORT_TRACE(k) \
-  if (t == 0) tr[k] = wall_clock64();
-#else
-#define SORT_TRACE(k)
-#endif
-  SORT_TRACE(0)
   // thread t < 2^bits <-> digit t: this pass's digit total, summed over the partial copies (a
   // narrower last digit -- 4 bits for 3024 tiles -- publishes and looks back 16 words per
   // partition instead of 256)
-#ifndef GSR_SORT_NARROW
-#define GSR_SORT_NARROW 1
-#endif
-  const bool dig = t < (GSR_SORT_NARROW ? (1 << bits) : 256);
+  const bool dig = t < (1 << bits);
   const int dt = dig ? t : 0;
   uint32_t dtotal = 0;
   if (dig) {
@@ -432,7 +388,6 @@ __device__ __forceinline__ void onesweep_body(
     if (valid && (__ffsll((long long)peers) - 1) == lane) s_cnt[wid][d] = before + (uint32_t)__popcll(peers);
   }
   __syncthreads();
-  SORT_TRACE(1)
   // (the lanes t >= 256 join the workgroup scans with zeros)
   uint32_t h = 0;
   if (dig)
@@ -473,7 +428,6 @@ __device__ __forceinline__ void onesweep_body(
       s_v[pos] = val[r];
     }
   }
-  SORT_TRACE(2)
   uint32_t excl = 0;
   if (dig && part > 0) {
     // Two-level windowed look-back.  (A) the predecessors inside this partition's own
@@ -553,25 +507,13 @@ __device__ __forceinline__ void onesweep_body(
     status_store(my, kStIncl | (uint64_t)(excl + h));
   }
   if (dig) s_gofs[t] = dbase + excl - lstart;
-  SORT_TRACE(3)
   __syncthreads();
-  SORT_TRACE(4)
   const uint32_t nvalid = (uint32_t)min((size_t)kSortTile, n - base);
   for (uint32_t i = (uint32_t)t; i < nvalid; i += kSortThreads) {
     const uint32_t k = s_k[i];
     const uint32_t o = s_gofs[(k >> shift) & mask] + i;
     if (o < n) emit(o, s_v[i], k);  // only a timed-out look-back (error word raised) can produce o >= n
   }
-#if GSR_SORT_TRACE
-  SORT_TRACE(5)
-  if (t == 0 && part < 16384) {
-    for (int k = 0; k < 6; k++) g_sort_trace[part][k] = tr[k];
-    uint32_t hw;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(hw));
-    g_sort_trace[part][6] = hw;
-  }
-#endif
-#undef SORT_TRACE
 }
 
 template <int NT>
@@ -579,10 +521,9 @@ __global__ __launch_bounds__(NT, NT == 1024 ? 8 : (NT == 512 ? 6 : 1)) void radi
     const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin, size_t n, int shift,
     int bits, const uint32_t* __restrict__ totals, const uint32_t* __restrict__ nsent_sh,
     uint32_t* __restrict__ ticket, uint64_t* __restrict__ status, uint32_t* __restrict__ err,
-    uint32_t* __restrict__ kout, uint32_t* __restrict__ vout, const uint32_t* __restrict__ kpay,
-    const float4* __restrict__ rpay, float4* __restrict__ rout) {
+    uint32_t* __restrict__ kout, uint32_t* __restrict__ vout, const uint32_t* __restrict__ kpay) {
   onesweep_body<NT>(kin, vin, n, shift, bits, totals, nsent_sh, ticket, status, err, kout, vout,
-                    kpay, rpay, rout, blockIdx.x, gridDim.x);
+                    kpay, blockIdx.x, gridDim.x);
 }
 
 // ---- several independent sorts / scans / sums per launch (the multi-view forward's batched
@@ -596,8 +537,6 @@ struct SortPassJob {
   uint32_t* kout;
   uint32_t* vout;
   const uint32_t* kpay;  // last pass: payload gathered in place of the key
-  const float4* rpay;    // last pass: splat records -> binning records rout (see onesweep_body)
-  float4* rout;
   uint32_t* aux;         // totals, sentinel counts, tickets, error word (kSortAux*)
   uint64_t* status;      // this pass's look-back words
   uint32_t n;
@@ -629,7 +568,7 @@ __global__ __launch_bounds__(NT, NT == 1024 ? 8 : (NT == 512 ? 6 : 1)) void radi
   const SortPassJob& j = m.j[k];
   onesweep_body<NT>(j.kin, j.vin, j.n, shift, bits, j.aux + kSortAuxTotals + 256 * pass,
                     sentinel ? j.aux + kSortAuxSent : nullptr, j.aux + kSortAuxTickets + 8 * pass,
-                    j.status, j.aux + kSortAuxErr, j.kout, j.vout, j.kpay, j.rpay, j.rout,
+                    j.status, j.aux + kSortAuxErr, j.kout, j.vout, j.kpay,
                     blockIdx.x - m.first[k], m.first[k + 1] - m.first[k]);
 }
 
@@ -899,13 +838,6 @@ hipError_t scan_u32(const uint32_t* in, const uint32_t* gather, uint32_t* out, s
   return hipGetLastError();
 }
 
-#if GSR_SORT_TRACE
-extern "C" int gsr_test_sort_trace(uint64_t* out, int parts) {
-  if (parts > 16384) parts = 16384;
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sort_trace), (size_t)parts * 8 * sizeof(uint64_t))
-             == hipSuccess ? 0 : 2;
-}
-#endif
 
 extern "C" int gsr_test_force_sort_timeout(int on) {
   const uint32_t v = on ? 1u : 0u;
@@ -946,8 +878,7 @@ uint32_t* sort_timeouts_word() {
 hipError_t radix_sort_pairs(uint32_t* ka, uint32_t* va, uint32_t* kb, uint32_t* vb, size_t n,
                             int bits, SortScratch scratch, bool* result_in_b, hipStream_t s,
                             bool sentinel_anywhere, bool precleared,
-                            const uint32_t* key_payload, const float4* rec_payload,
-                            float4* rec_out) {
+                            const uint32_t* key_payload) {
   *result_in_b = false;
   if (n == 0 || bits <= 0) return hipSuccess;
   if (bits > 32 || n > 0xffffffffull) return hipErrorInvalidValue;
@@ -960,7 +891,7 @@ hipError_t radix_sort_pairs(uint32_t* ka, uint32_t* va, uint32_t* kb, uint32_t* 
   }
   const size_t tot_tiles = (n + kTotTile - 1) / kTotTile;
   hipLaunchKernelGGL(radix_totals_kernel,
-                     dim3((unsigned)(tot_tiles < GSR_TOTALS_GROUPS ? tot_tiles : GSR_TOTALS_GROUPS)),
+                     dim3((unsigned)(tot_tiles < kTotGroups ? tot_tiles : kTotGroups)),
                      dim3(kThreads), 0, s, ka, n, bits, scratch.aux + kSortAuxTotals,
                      scratch.aux + kSortAuxSent, sentinel_anywhere ? 1 : 0);
   uint32_t *kin = ka, *vin = va, *kout = kb, *vout = vb;
@@ -969,7 +900,7 @@ hipError_t radix_sort_pairs(uint32_t* ka, uint32_t* va, uint32_t* kb, uint32_t* 
     const int dw = sort_digit_width(bits);
     const int shift = dw * p;
     const int dbits = (bits - shift) < dw ? (bits - shift) : dw;
-    const int nt = GSR_SORT_THREADS ? GSR_SORT_THREADS : (nb <= kResident1024 ? 1024 : 512);
+    const int nt = nb <= kResident1024 ? 1024 : 512;
 #define GSR_ONESWEEP(NT)                                                                          \
   hipLaunchKernelGGL(radix_onesweep_kernel<NT>, dim3(nb), dim3(NT), 0, s, kin, vin, n, shift,    \
                      dbits, scratch.aux + kSortAuxTotals + 256 * p,                              \
@@ -977,11 +908,9 @@ hipError_t radix_sort_pairs(uint32_t* ka, uint32_t* va, uint32_t* kb, uint32_t* 
                      scratch.aux + kSortAuxTickets + 8 * p,                                      \
                      scratch.status + (size_t)p * sort_pass_words(n), \
                      scratch.aux + kSortAuxErr, kout, vout,                                      \
-                     p == passes - 1 ? key_payload : nullptr,                                    \
-                     p == passes - 1 ? rec_payload : nullptr, rec_out)
+                     p == passes - 1 ? key_payload : nullptr)
     if (nt == 1024) GSR_ONESWEEP(1024);
-    else if (nt == 512) GSR_ONESWEEP(512);
-    else GSR_ONESWEEP(256);
+    else GSR_ONESWEEP(512);
 #undef GSR_ONESWEEP
     uint32_t* t;
     t = kin; kin = kout; kout = t;
@@ -1013,7 +942,7 @@ hipError_t radix_sort_pairs_views(const SortSpec* v, int V, int bits, bool* resu
       if (e != hipSuccess) return e;
     }
     const size_t tt = (n + kTotTile - 1) / kTotTile;
-    tfirst[k + 1] = tfirst[k] + (uint32_t)(tt < GSR_TOTALS_GROUPS ? tt : GSR_TOTALS_GROUPS);
+    tfirst[k + 1] = tfirst[k] + (uint32_t)(tt < kTotGroups ? tt : kTotGroups);
     ofirst[k + 1] = ofirst[k] + (uint32_t)sort_blocks(n);
   }
   if (ofirst[V] == 0) return hipSuccess;
@@ -1028,8 +957,6 @@ hipError_t radix_sort_pairs_views(const SortSpec* v, int V, int bits, bool* resu
       j.kout = b_in ? w.ka : w.kb;
       j.vout = b_in ? w.va : w.vb;
       j.kpay = p == passes - 1 ? w.key_payload : nullptr;
-      j.rpay = p == passes - 1 ? w.rec_payload : nullptr;
-      j.rout = w.rec_out;
       j.aux = w.scratch.aux;
       j.status = w.scratch.status + (size_t)p * sort_pass_words(w.n);
       j.n = (uint32_t)w.n;
@@ -1039,7 +966,7 @@ hipError_t radix_sort_pairs_views(const SortSpec* v, int V, int bits, bool* resu
   hipLaunchKernelGGL(radix_totals_views_kernel, dim3(tfirst[V]), dim3(kThreads), 0, s, m, bits,
                      sentinel_anywhere ? 1 : 0);
   const uint32_t nb = ofirst[V];
-  const int nt = GSR_SORT_THREADS ? GSR_SORT_THREADS : (nb <= kResident1024 ? 1024 : 512);
+  const int nt = nb <= kResident1024 ? 1024 : 512;
   for (int p = 0; p < passes; p++) {
     fill(p, ofirst);
     const int dw = sort_digit_width(bits);
@@ -1048,11 +975,8 @@ hipError_t radix_sort_pairs_views(const SortSpec* v, int V, int bits, bool* resu
     if (nt == 1024)
       hipLaunchKernelGGL(radix_onesweep_views_kernel<1024>, dim3(nb), dim3(1024), 0, s, m, p, shift, dbits,
                          sentinel_anywhere ? 1 : 0);
-    else if (nt == 512)
-      hipLaunchKernelGGL(radix_onesweep_views_kernel<512>, dim3(nb), dim3(512), 0, s, m, p, shift, dbits,
-                         sentinel_anywhere ? 1 : 0);
     else
-      hipLaunchKernelGGL(radix_onesweep_views_kernel<256>, dim3(nb), dim3(256), 0, s, m, p, shift, dbits,
+      hipLaunchKernelGGL(radix_onesweep_views_kernel<512>, dim3(nb), dim3(512), 0, s, m, p, shift, dbits,
                          sentinel_anywhere ? 1 : 0);
   }
   *result_in_b = (passes & 1) != 0;

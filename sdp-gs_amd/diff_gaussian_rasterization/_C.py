@@ -98,9 +98,21 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     g = geomBuffer if geomBuffer.numel() else None
     b = binningBuffer if binningBuffer.numel() else None
     i = imageBuffer if imageBuffer.numel() else None
-    # the forward's layout travels in its binning buffer (a tag word the forward writes; include/
-    # gsr.h GSR_DEBUG_LAYOUT_FROM_BUFFER): no table of live forwards, no global mode
-    flags = int(bool(debug)) | 4
+    # The forward's layout: the buffer's size tells it when only the default layout fits (no
+    # device read); a buffer large enough for the deterministic layout too is tagged by its
+    # forward (include/gsr.h GSR_DEBUG_LAYOUT_FROM_BUFFER: one 4-byte read).  A buffer too small
+    # for R instances (R larger than its forward's num_rendered) raises instead of letting the
+    # kernels read past it.
+    flags = int(bool(debug))
+    if int(R) > 0:
+        L = _lib.load()
+        need, need_det = int(L.gsr_binning_buffer_bytes(int(R))), int(L.gsr_binning_buffer_bytes_det(int(R)))
+        have = 0 if b is None else b.numel() * b.element_size()
+        if have < need:
+            raise RuntimeError(f"binningBuffer holds {have} bytes, {need} needed for R = {int(R)} "
+                               "instances: not the buffer of a forward with this num_rendered")
+        if have >= need_det:
+            flags |= 4
     with torch.cuda.device(dev):
         rc = _lib.load().gsr_rasterize_gaussians_backward(
             P, M, int(R), _p(bg), _p(m3), _p(rad), _p(col), _p(sc), _p(rot), float(scale_modifier),

@@ -860,6 +860,13 @@ class BackwardRowSlices:
         self.active = True  # False: backwards pass it by (an earlier chunk of a chunked step)
 
     def rows(self, P):
+        # the slices' all-reduce treats the rows as final: a second sliced backward in the same
+        # scope would add gradients the other ranks never receive
+        if self.ran:
+            raise RuntimeError("BackwardRowSlices: a second grad-into-leaves multi-view backward in "
+                               "one slicing scope; its rows were already all-reduced (issue one "
+                               "multi-view backward per step, or deactivate the scope for the "
+                               "earlier ones)")
         self.ran = True
         if self.slices <= 1 or P <= 256:
             return 0

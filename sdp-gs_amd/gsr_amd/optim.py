@@ -35,7 +35,8 @@ class FusedAdam(torch.optim.Adam):
             raise ValueError("FusedAdam implements Adam without amsgrad / maximize")
         super().__init__(params, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay,
                          amsgrad=False, foreach=False)
-        self._mailbox = {}     # device -> pinned int32 [1]: 1 = the last launch skipped the step
+        self._mailbox = {}     # device -> pinned int32 [1]: 1 = the step's launches skipped it
+        self._guard = {}       # device -> float32 [1] device slot: the step's one fault snapshot
         self._pending = None   # (events, mailboxes, stepped states, fault-reset count)
         self.skipped_steps = 0
 
@@ -109,7 +110,19 @@ class FusedAdam(torch.optim.Adam):
             box[0] = 0
             if skip is not None and (skip.device != dev or skip.dtype != torch.float32):
                 raise ValueError("FusedAdam.step: skip must be a float32 tensor on the parameters' device")
-            skip_ptr = None if skip is None else skip.data_ptr()
+            if skip is None:
+                # ONE snapshot of the device's fault word for every launch of the step (chunks of
+                # MAX_TENSORS, (betas, eps) batches): a fault published between two launches
+                # cannot leave some tensors updated and others not
+                slot = self._guard.get(dev)
+                if slot is None:
+                    slot = torch.zeros(1, dtype=torch.float32, device=dev)
+                    self._guard[dev] = slot
+                with _lib.on_device(dev):
+                    _lib.step_guard(slot)
+                skip_ptr = slot.data_ptr()
+            else:
+                skip_ptr = skip.data_ptr()
             for c in range(0, len(items), MAX_TENSORS):
                 chunk = items[c:c + MAX_TENSORS]
                 n = len(chunk)

@@ -25,7 +25,6 @@ ShPrecolor, gsr_sh_precolor); the views' forward and backward preprocesses then 
 from __future__ import annotations
 
 import contextlib
-import os
 from typing import Callable, Iterable, List, Optional, TypeVar
 
 import torch
@@ -99,7 +98,7 @@ class ViewPipeline:
                 main.wait_stream(s)
             return out
 
-        return self._step(items, issue, model, campos_of, reducer, jac_side=False)
+        return self._step(items, issue, model, campos_of, reducer)
 
     def run_views(self, items: Iterable[T], fn: Callable[[List[T], List[torch.cuda.Stream]], R],
                   model=None, campos_of: Callable[[T], torch.Tensor] = lambda cam: cam.camera_center,
@@ -152,20 +151,17 @@ class ViewPipeline:
             raise ValueError("ViewPipeline.run: a reducer with defer_sh needs model= (the SH "
                              "leaves are reduced after the deferred flush)")
 
-    def _step(self, items, issue, model, campos_of, reducer, sliced=False, jac_side=True):
+    def _step(self, items, issue, model, campos_of, reducer, sliced=False):
         import diff_gaussian_rasterization as dgr
         main = torch.cuda.current_stream(self.device)
         pre = contextlib.nullcontext()
         if self.precolor and model is not None and items:
-            # GSR_PRECOLOR_SPLIT=1: the colour Jacobians (backward only) on the last side stream,
-            # which the one-call multi-view step leaves free; default one kernel ahead of the
-            # forward (round 4: 2090 / 2107 views/s split against 2116 / 2111 not split,
-            # profiles/r04_pipeline_ab.txt -- the forward's head is latency-bound, not the pass)
-            js = (self.side[-1] if jac_side and len(self.side) >= 2
-                  and os.environ.get("GSR_PRECOLOR_SPLIT", "0") == "1" else None)
+            # one kernel ahead of the forward: colours and Jacobians of every view (round 4: the
+            # Jacobians split onto a side stream measured slower, profiles/r04_pipeline_ab.txt --
+            # the forward's head is latency-bound, not the pass)
             pre = dgr.ShPrecolor(model._xyz, model._features_dc, model._features_rest,
                                  model.active_sh_degree, [campos_of(it) for it in items],
-                                 buffers=self._pre_bufs, jac_stream=js)
+                                 buffers=self._pre_bufs)
             # reuse next step: its pre-pass is issued on this stream after this step's join
             self._pre_bufs = pre.buffers
         for s in self.side:

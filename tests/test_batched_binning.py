@@ -1,5 +1,4 @@
-"""The multi-view call's batched forward (gsr_api.cpp views_forward_batched, the default
-GSR_VIEWS_BATCHED=1): the views' preprocesses in one multi-view launch, then one launch per
+"""The multi-view call's batched forward (gsr_api.cpp views_forward_batched): the views' preprocesses in one multi-view launch, then one launch per
 binning stage for a group of views (instance-count sums with the pinned read-back, depth-sort
 passes, scan, duplication, tile-sort passes, ranges, schedules, blend).  The forward has no float
 atomics, so every view's images, radii and instance counts must be bitwise those of the

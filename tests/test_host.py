@@ -103,10 +103,23 @@ def test_view_pipeline_reducer_with_deferral_needs_the_model():
 
 
 def test_C_shim_asks_for_the_layout_from_the_buffer():
-    """the `_C` shim's backward passes GSR_DEBUG_LAYOUT_FROM_BUFFER, so the library
-    reads the forward's layout from the tag word in its binning buffer -- no size inference, no
-    global mode (the GPU side: tests/test_deterministic.py)."""
+    """the `_C` shim's backward checks the binning buffer's size against R (a
+    buffer too small raises) and passes GSR_DEBUG_LAYOUT_FROM_BUFFER only when the size cannot
+    tell the layouts apart, so the library then reads the forward's layout from the tag word --
+    no global mode (the GPU side: tests/test_deterministic.py)."""
     import inspect
     from diff_gaussian_rasterization import _C
     src = inspect.getsource(_C.rasterize_gaussians_backward)
-    assert "| 4" in src and "deterministic" not in src.split("flags =")[1].split("\n")[0]
+    assert "flags |= 4" in src and "gsr_binning_buffer_bytes_det" in src
+    assert "if have < need:" in src
+
+
+def test_row_slices_one_backward_per_scope():
+    """a second sliced multi-view backward in one BackwardRowSlices scope would add
+    gradients whose rows were already all-reduced -- it raises instead of corrupting them."""
+    import diff_gaussian_rasterization as dgr
+    seen = []
+    sl = dgr.BackwardRowSlices("cpu", lambda a, b: seen.append((a, b)), slices=4)
+    assert sl.rows(4096) == 1024
+    with pytest.raises(RuntimeError, match="second"):
+        sl.rows(4096)
