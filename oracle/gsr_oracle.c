@@ -303,6 +303,13 @@ struct oracle_state {
     real* final_T;
     unsigned* n_contrib;
     real* margin; /* [H*W] test-side diagnostic, see oracle_get_margin */
+    /* decision lock (oracle_use_decisions): per pixel, another evaluation's blend decisions --
+     * its n_contrib and, over list positions [0, n_contrib), the bitset of the splats it blended
+     * (lock_offs[pix] = the pixel's first 32-bit word) -- replace this build's own alpha >= 1/255,
+     * power <= 0 and T < 1e-4 tests in the blends.  NULL = no lock. */
+    unsigned* lock_nc;
+    uint64_t* lock_offs;
+    unsigned* lock_words;
 };
 
 /* forward.cu:20-71 computeColorFromSH */
@@ -617,20 +624,26 @@ static void blend_fwd_rows(void* ctx, long lo, long hi, int chunk) {
             unsigned contributor = 0, last_contributor = 0;
             real C[NCH] = {0};
             real margin = 1.0f;
+            const size_t lpix = (size_t)py * W + px;
+            const unsigned lock_nc = st->lock_nc ? st->lock_nc[lpix] : 0;
+            const unsigned* lock_w = st->lock_nc ? st->lock_words + st->lock_offs[lpix] : NULL;
             for (unsigned k = rs; k < re; k++) {
                 contributor++;
+                if (lock_w && contributor > lock_nc) break; /* the locked evaluation stopped here */
                 const unsigned g = st->point_list[k];
                 const real dx = st->means2D[2 * g] - pfx, dy = st->means2D[2 * g + 1] - pfy;
                 const real* co = st->conic_opacity + 4 * (size_t)g;
                 real power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
+                const unsigned q = contributor - 1;
+                const int lock_take = lock_w ? (int)((lock_w[q >> 5] >> (q & 31)) & 1u) : -1;
                 if (fabs(power) < 1e-6f) margin = 0.0f;
-                if (power > 0.0f) continue;
+                if (lock_take == 0 || (lock_take < 0 && power > 0.0f)) continue;
                 real alpha = fminf_cuda(0.99f, co[3] * blend_exp(power));
                 margin = fmin(margin, fabs(alpha * 255.0f - 1.0f));
-                if (alpha < 1.0f / 255.0f) continue;
+                if (lock_take < 0 && alpha < 1.0f / 255.0f) continue;
                 real test_T = T * (1 - alpha);
                 margin = fmin(margin, fabs(test_T * 1e4f - 1.0f));
-                if (test_T < 0.0001f) break; /* done: nothing later changes this pixel */
+                if (lock_take < 0 && test_T < 0.0001f) break; /* done: nothing later changes this pixel */
                 real v[NCH];
                 v[0] = feat_ptr[3 * g]; v[1] = feat_ptr[3 * g + 1]; v[2] = feat_ptr[3 * g + 2];
                 v[3] = st->depths[g]; v[4] = 1.0f;
@@ -660,6 +673,52 @@ void oracle_use_lists(const unsigned* point_list, int R, const unsigned* ranges)
     g_lists.point_list = point_list;
     g_lists.R = R;
     g_lists.ranges = ranges;
+}
+
+/* oracle_use_decisions: the next oracle_forward on this thread blends with another evaluation's
+ * per-pixel decisions (oracle_accept_bits of a float32 run) instead of its own threshold tests --
+ * the float64 build then sums exactly the terms float32 summed, so every remaining difference is
+ * rounding (tests/f64_ref.py).  The arrays are copied into the state. */
+static _Thread_local struct { const unsigned *nc, *words; const uint64_t* offs; } g_lock;
+void oracle_use_decisions(const unsigned* n_contrib, const uint64_t* word_offsets,
+                          const unsigned* words) {
+    g_lock.nc = n_contrib;
+    g_lock.offs = word_offsets;
+    g_lock.words = words;
+}
+
+/* The blend decisions of a forward: per pixel the 32-bit word offset of its bitset (offs[H*W+1],
+ * a prefix sum of ceil(n_contrib / 32)) and, when words != NULL, the bitset of the list positions
+ * [0, n_contrib) it blended (power <= 0 and alpha >= 1/255, recomputed with the forward's own
+ * arithmetic).  Returns the number of words. */
+long oracle_accept_bits(const oracle_state* st, uint64_t* offs, unsigned* words) {
+    const int W = st->W, H = st->H;
+    const size_t HW = (size_t)W * H;
+    uint64_t o = 0;
+    for (size_t pix = 0; pix < HW; pix++) {
+        offs[pix] = o;
+        o += (st->n_contrib[pix] + 31u) / 32u;
+    }
+    offs[HW] = o;
+    if (!words) return (long)o;
+    memset(words, 0, sizeof(unsigned) * (size_t)o);
+    for (int py = 0; py < H; py++)
+        for (int px = 0; px < W; px++) {
+            const size_t pix = (size_t)py * W + px;
+            const unsigned tile = (unsigned)(py / BLOCK_Y) * st->gx + (unsigned)(px / BLOCK_X);
+            const unsigned rs = st->ranges[2 * tile], nc = st->n_contrib[pix];
+            const real pfx = (real)px, pfy = (real)py;
+            for (unsigned q = 0; q < nc; q++) {
+                const unsigned g = st->point_list[rs + q];
+                const real dx = st->means2D[2 * g] - pfx, dy = st->means2D[2 * g + 1] - pfy;
+                const real* co = st->conic_opacity + 4 * (size_t)g;
+                const real power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
+                if (power > 0.0f) continue;
+                if (fminf_cuda(0.99f, co[3] * blend_exp(power)) < 1.0f / 255.0f) continue;
+                words[offs[pix] + (q >> 5)] |= 1u << (q & 31);
+            }
+        }
+    return (long)o;
 }
 
 oracle_state* oracle_forward(int P, int M, const float* background, const float* means3D,
@@ -778,6 +837,16 @@ oracle_state* oracle_forward(int P, int M, const float* background, const float*
     }
 
 blend:
+    if (g_lock.nc) { /* oracle_use_decisions: copied, so the lock outlives the caller's arrays */
+        const size_t HW = (size_t)W * H;
+        const uint64_t nw = g_lock.offs[HW];
+        st->lock_nc = (unsigned*)xcalloc(HW, sizeof(unsigned));
+        st->lock_offs = (uint64_t*)xcalloc(HW + 1, sizeof(uint64_t));
+        st->lock_words = (unsigned*)xcalloc((size_t)nw, sizeof(unsigned));
+        memcpy(st->lock_nc, g_lock.nc, sizeof(unsigned) * HW);
+        memcpy(st->lock_offs, g_lock.offs, sizeof(uint64_t) * (HW + 1));
+        memcpy(st->lock_words, g_lock.words, sizeof(unsigned) * (size_t)nw);
+    }
     /* ---- renderCUDA (fwd), forward.cu:261-374, extended to NCH channels ---- */
     st->final_T = (real*)xcalloc((size_t)W * H, sizeof(real));
     st->n_contrib = (unsigned*)xcalloc((size_t)W * H, sizeof(unsigned));
@@ -1057,6 +1126,7 @@ static void blend_bwd_rows(void* ctx, long lo, long hi, int chunk) {
             dL_dpixel[4] = c->da ? c->da[pix] : 0.0f;
             for (int i = 0; i < 3; i++) dL_dpixel[5 + i] = c->df ? c->df[i * HW + pix] : 0.0f;
             real last_alpha = 0;
+            const unsigned* lock_w = st->lock_nc ? st->lock_words + st->lock_offs[pix] : NULL;
             /* mass mode: the float32 chain length of T at each splat -- the forward's product over
              * the pixel's contributors, then one division per splat replayed -- weights the terms
              * (T, and with it every term, carries ~ one rounding per link of that chain) */
@@ -1064,6 +1134,10 @@ static void blend_bwd_rows(void* ctx, long lo, long hi, int chunk) {
             if (c->mass) {
                 unsigned pos = 0;
                 for (unsigned k = rs; k < re && pos < last_contributor; k++, pos++) {
+                    if (lock_w) {
+                        chain += (real)((lock_w[pos >> 5] >> (pos & 31)) & 1u);
+                        continue;
+                    }
                     const unsigned g = st->point_list[k];
                     const real dx = st->means2D[2 * g] - pfx, dy = st->means2D[2 * g + 1] - pfy;
                     const real* co = st->conic_opacity + 4 * (size_t)g;
@@ -1076,14 +1150,17 @@ static void blend_bwd_rows(void* ctx, long lo, long hi, int chunk) {
             for (unsigned k = re; k-- > rs;) {
                 contributor--;
                 if (contributor >= last_contributor) continue;
+                const int lock_take =
+                    lock_w ? (int)((lock_w[contributor >> 5] >> (contributor & 31)) & 1u) : -1;
+                if (lock_take == 0) continue;
                 const unsigned g = st->point_list[k];
                 const real dx = st->means2D[2 * g] - pfx, dy = st->means2D[2 * g + 1] - pfy;
                 const real* co = st->conic_opacity + 4 * (size_t)g;
                 const real power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
-                if (power > 0.0f) continue;
+                if (lock_take < 0 && power > 0.0f) continue;
                 const real G = blend_exp(power);
                 const real alpha = fminf_cuda(0.99f, co[3] * G);
-                if (alpha < 1.0f / 255.0f) continue;
+                if (lock_take < 0 && alpha < 1.0f / 255.0f) continue;
                 T = T / (1.f - alpha);
                 const real dchannel_dcolor = alpha * T;
                 real dL_dalpha = 0.0f;
@@ -1323,6 +1400,7 @@ void oracle_free(oracle_state* st) {
     free(st->depths); free(st->depth_key); free(st->clamped); free(st->radii); free(st->means2D); free(st->cov3D);
     free(st->conic_opacity); free(st->rgb); free(st->feat); free(st->tiles_touched);
     free(st->point_list); free(st->ranges); free(st->final_T); free(st->n_contrib); free(st->margin);
+    free(st->lock_nc); free(st->lock_offs); free(st->lock_words);
     free(st);
 }
 

@@ -124,6 +124,13 @@ int oracle_backward_rows(oracle_state* st, const oreal* rows, oreal* dL_dmeans2D
  * ranges [tiles*2], as oracle_get_point_list / _ranges return them) instead of binning; NULL
  * point_list = bin normally again.  Test diagnostic: the float64 build on the float32 lists. */
 void oracle_use_lists(const unsigned* point_list, int R, const unsigned* ranges);
+/* The next oracle_forward on this thread blends with these per-pixel decisions (another
+ * evaluation's oracle_accept_bits) instead of its own threshold tests (float64 parity). */
+void oracle_use_decisions(const unsigned* n_contrib, const uint64_t* word_offsets,
+                          const unsigned* words);
+/* Per pixel: word offsets (H*W + 1) of the bitsets of the list positions the forward blended;
+ * with words != NULL also the bitsets.  Returns the number of 32-bit words. */
+long oracle_accept_bits(const oracle_state* st, uint64_t* offs, unsigned* words);
 
 void oracle_free(oracle_state* st);
 

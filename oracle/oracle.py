@@ -55,6 +55,10 @@ def lib(variant: str = "f32"):
         L.oracle_free.argtypes = [_p]
         L.oracle_use_lists.restype = None
         L.oracle_use_lists.argtypes = [_p, _i, _p]
+        L.oracle_use_decisions.restype = None
+        L.oracle_use_decisions.argtypes = [_p, _p, _p]
+        L.oracle_accept_bits.restype = ctypes.c_long
+        L.oracle_accept_bits.argtypes = [_p, _p, _p]
         L.oracle_mark_visible.restype = _i
         L.oracle_mark_visible.argtypes = [_i, _p, _p, _p, _p]
         L.oracle_splat_exp.restype = None
@@ -101,13 +105,15 @@ class OracleRaster:
     """One forward (+ optional backward) of the restated rasterizer on host arrays.  variant:
     "f32" (the checker), "f64" (the same restatement in float64: images and gradients come back
     as float64) or "expf" (float32 with libm's expf as the blend exp).  lists=(point_list, ranges)
-    skips the binning and blends those instance lists (another raster's point_list() / ranges())."""
+    skips the binning and blends those instance lists (another raster's point_list() / ranges());
+    decisions=(n_contrib, offsets, words) blends with another raster's per-pixel decisions
+    (its accept_bits()) instead of this one's own threshold tests."""
 
     def __init__(self, *, variant="f32", means3D, opacities, viewmatrix, projmatrix, campos, tanfovx, tanfovy,
                  image_height, image_width, bg, scale_modifier=1.0, sh_degree=0, shs=None,
                  colors_precomp=None, scales=None, rotations=None, cov3D_precomp=None,
                  shs_language=None, language_feature_precomp=None, confidence=None,
-                 include_feature=True, prefiltered=False, lists=None):
+                 include_feature=True, prefiltered=False, lists=None, decisions=None):
         L = lib(variant)
         self.variant = variant
         self._L = L
@@ -145,6 +151,14 @@ class OracleRaster:
             if k["rg"].size != 2 * ((W + 15) // 16) * ((H + 15) // 16):
                 raise ValueError("lists: ranges must hold two entries per tile")
             L.oracle_use_lists(_ptr(k["pl"]), int(k["pl"].size), _ptr(k["rg"]))
+        if decisions is not None:
+            k["dnc"] = np.ascontiguousarray(decisions[0], np.uint32).reshape(-1)
+            k["doffs"] = np.ascontiguousarray(decisions[1], np.uint64).reshape(-1)
+            k["dwords"] = np.ascontiguousarray(decisions[2], np.uint32).reshape(-1)
+            if k["dnc"].size != H * W or k["doffs"].size != H * W + 1 or \
+                    k["dwords"].size < int(k["doffs"][-1]):
+                raise ValueError("decisions: (n_contrib [H*W], offsets [H*W+1], words) expected")
+            L.oracle_use_decisions(_ptr(k["dnc"]), _ptr(k["doffs"]), _ptr(k["dwords"]))
         try:
             self._st = L.oracle_forward(
             P, M, _ptr(k["bg"]), _ptr(k["means3D"]), _ptr(k["colors"]), _ptr(k["opac"]),
@@ -157,6 +171,8 @@ class OracleRaster:
         finally:
             if lists is not None:
                 L.oracle_use_lists(None, 0, None)
+            if decisions is not None:
+                L.oracle_use_decisions(None, None, None)
         if not self._st:
             raise RuntimeError("oracle_forward rejected its arguments")
         self.num_rendered = int(nr.value)
@@ -195,6 +211,16 @@ class OracleRaster:
 
     def n_contrib(self):
         return self._get("n_contrib", (self.H, self.W), np.uint32)
+
+    def accept_bits(self):
+        """The forward's blend decisions: (n_contrib [H*W], word offsets [H*W + 1], bitset words)
+        -- per pixel, bit q set iff list position q < n_contrib was blended (the `decisions=` of
+        another raster)."""
+        offs = np.zeros(self.H * self.W + 1, np.uint64)
+        n = int(self._L.oracle_accept_bits(self._st, _ptr(offs), None))
+        words = np.zeros(max(n, 1), np.uint32)
+        self._L.oracle_accept_bits(self._st, _ptr(offs), _ptr(words))
+        return self.n_contrib().reshape(-1), offs, words
 
     def margin(self):
         """Per pixel: the smallest relative distance of any blend decision from its threshold

@@ -68,8 +68,8 @@ def oracle_inputs(m, act):
         q=m._rotation.detach().cpu().numpy().astype(np.float64), deg=m.active_sh_degree)
 
 
-def _raster(inp, cam, variant, lists=None):
-    return OracleRaster(lists=lists,
+def _raster(inp, cam, variant, lists=None, decisions=None):
+    return OracleRaster(lists=lists, decisions=decisions,
         variant=variant, means3D=inp["xyz"], opacities=inp["op"],
         viewmatrix=cam.world_view_transform.cpu().numpy(),
         projmatrix=cam.full_proj_transform.cpu().numpy(), campos=cam.camera_center.cpu().numpy(),
@@ -79,20 +79,24 @@ def _raster(inp, cam, variant, lists=None):
         shs_language=inp["lang"], include_feature=True)
 
 
-def run_f64_path(inp, cams, grads, progress=None, bound=True, lists=None):
+def run_f64_path(inp, cams, grads, progress=None, bound=True, lists=None, decisions=None):
     """The float64 oracle on the views of the benchmarked path: per-view images / radii / margin /
     lists, the raw-leaf gradients summed over the views, and (bound) the per-entry rounding scale
     B (float64 arrays shaped like the leaves).  lists: per view (point_list, ranges) to blend
     instead of the float64 binning -- the float32 run's, so that a radius that rounds to another
-    integer in float64 does not add or drop a Gaussian from whole tiles (its remaining
-    differences are then the per-pixel threshold flips that decision_flips reports)."""
+    integer in float64 does not add or drop a Gaussian from whole tiles.  decisions: per view the
+    float32 run's blend decisions (OracleRaster.accept_bits: n_contrib and, per pixel, which list
+    positions it blended) in place of float64's own alpha >= 1/255, power <= 0 and T < 1e-4
+    tests -- float64 then sums exactly the terms float32 summed, so every
+    remaining difference is rounding."""
     dimg, ddep, dfeat = (g.detach().cpu().numpy() for g in grads)
     q = inp["q"]
     nq = np.maximum(np.linalg.norm(q, axis=1, keepdims=True), 1e-12)
     qh = q / nq
     views, acc, B = [], None, None
     for i, cam in enumerate(cams):
-        o = _raster(inp, cam, "f64", None if lists is None else lists[i])
+        o = _raster(inp, cam, "f64", None if lists is None else lists[i],
+                    None if decisions is None else decisions[i])
         P = o.P
         rows = o.blend_rows(dimg, ddep, None, dfeat)
         raw = _raw_chain(o.backward_rows(rows), inp["op"], inp["sc"], qh, nq)

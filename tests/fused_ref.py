@@ -138,7 +138,9 @@ def run_oracle_path(m, cams, grads, act, progress=None):
         views.append(dict(render=orc.color, depth=orc.depth, alpha=orc.alpha,
                           feature=orc.feature, radii=orc.radii, means2D=og["means2D"],
                           margin=orc.margin(), ranges=orc.ranges(), point_list=orc.point_list(),
-                          n_contrib=orc.n_contrib(), final_T=orc.final_T()))
+                          n_contrib=orc.n_contrib(), final_T=orc.final_T(),
+                          xy=orc.means2D(), conic_opacity=orc.conic_opacity(),
+                          decisions=orc.accept_bits()))
         g = {k: og[k].astype(np.float64)
              for k in ("means3D", "sh", "opacity", "scales", "rotations", "sh_language")}
         gq = g["rotations"]
@@ -216,6 +218,35 @@ def flip_gaussians(b, flips, P, ncs=None):
         s, e = b["ranges"][t]
         L = int(lim[tiles == t].max())
         hit[b["point_list"][s:min(e, s + L)]] = True
+    return hit
+
+
+def pixel_contributors(b, flips, P, thr=0.99 / 255.0, extra=2):
+    """Gaussians that can contribute to the flipped pixels in either of two evaluations whose
+    decisions differ by rounding: per pixel, the tile-list entries with float32 alpha within 1 %
+    of the 1/255 threshold or above it (power <= 0) before the float32 run's n_contrib, plus the
+    first `extra` such entries after it (a T < 1e-4 stop decided one entry later).  The blend
+    test follows forward.cu:337-357 (the oracle's alpha, its pixel centre convention)."""
+    hit = np.zeros(P, bool)
+    if not flips.any():
+        return hit
+    H, W = flips.shape
+    gx = (W + 15) // 16
+    nc = np.asarray(b["n_contrib"]).reshape(H, W)
+    xy, co = b["xy"].astype(np.float64), b["conic_opacity"].astype(np.float64)
+    for y, x in zip(*np.nonzero(flips)):
+        s, e = b["ranges"][(y // 16) * gx + x // 16]
+        ids = b["point_list"][s:e].astype(np.int64)
+        dx, dy = xy[ids, 0] - x, xy[ids, 1] - y
+        a, bb, c, o = co[ids].T
+        power = -0.5 * (a * dx * dx + c * dy * dy) - bb * dx * dy
+        alpha = np.minimum(0.99, o * np.exp(np.minimum(power, 0.0)))
+        cand = (power <= 1e-6) & (alpha >= thr)
+        pos = np.arange(ids.size)
+        n = int(nc[y, x])
+        late = np.nonzero(cand & (pos >= n))[0][:extra]
+        hit[ids[cand & (pos < n)]] = True
+        hit[ids[late]] = True
     return hit
 
 
