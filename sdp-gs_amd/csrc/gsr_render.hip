@@ -209,7 +209,7 @@ constexpr int kAccRow = 13;          // LDS accumulator row: the 13 gradient val
 constexpr int kUwStride = 130;
 // per-wave table of the pixels' upstream gradients: 8 rows of 8 pixels x 8 floats
 // {r, g, b, depth}, {f0, f1, f2, 0}; rows padded by 4 dwords so the rows read in one phase-2 step
-// fall on different banks
+// fall on different banks (ds_read_b128: row s at bank 4 s + 8 t, conflict-free)
 constexpr int kDpRow = 68;
 
 template <bool EXTRA, bool FEAT, bool DET>
@@ -228,7 +228,6 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
   __shared__ uint8_t s_list[kThreads / 64][kBatch];
   __shared__ __attribute__((aligned(16))) float s_uw[kThreads / 64][kSlots * kUwStride];
   __shared__ __attribute__((aligned(16))) float s_dp[kThreads / 64][8 * kDpRow];
-  __shared__ uint8_t s_slot[kThreads / 64][kSlots];
 
   const int lane = (int)(threadIdx.x & 63);
   const int wid = (int)(threadIdx.x >> 6);
@@ -311,20 +310,26 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
 
   for (int k = (int)threadIdx.x; k < (DET ? 4 : 1) * kBatch * kAccRow; k += kThreads) s_acc[k] = 0.0f;
 
-  // Phase 2 over the first `ns` slots (wave-uniform, 1..kSlots)
-  auto phase2 = [&](uint32_t ns) {
+  // Phase 2 over the first `ns` slots (wave-uniform, 1..kSlots).  slotv: lane l holds the batch
+  // index of slot l & 7 (set in phase 1, no LDS round trip).
+  auto phase2 = [&](uint32_t ns, uint32_t slotv) {
     const int j = lane & 7;
-    const uint32_t bj = s_slot[wid][j] & (uint32_t)(kBatch - 1);  // stale for j >= ns: kept in range
+    const uint32_t bj = slotv & (uint32_t)(kBatch - 1);  // stale for j >= ns: kept in range
     const float4 r0 = s_r0[bj];
     const float dy = r0.y - pfy_row;
     const float* uw = &s_uw[wid][j * kUwStride + (lane >> 3) * 16];
     const float* dp = &s_dp[wid][(lane >> 3) * kDpRow];
     float su = 0.f, sux = 0.f, suxx = 0.f;
-    f2 cA = mk2(0.f, 0.f), cB = mk2(0.f, 0.f), cC = mk2(0.f, 0.f);
-    float cF2 = 0.f;
+    f2 cA = mk2(0.f, 0.f), cB = mk2(0.f, 0.f), cC = mk2(0.f, 0.f), cD = mk2(0.f, 0.f);
 #pragma unroll
     for (int t = 0; t < 8; t++) {
-      const f2 p = *reinterpret_cast<const f2*>(uw + 2 * t);  // (u, w) of pixel (t, row)
+      // one ds_read_b64 per pixel (2 LDS cycles, conflict-free at kUwStride): the opaque offset
+      // keeps the backend from pairing two of them into a ds_read2_b64 (8 cycles)
+      uint32_t off = (uint32_t)(2 * t);
+      asm volatile("" : "+v"(off));
+      const f2 p = *reinterpret_cast<const f2*>(uw + off);  // (u, w) of pixel (t, row)
+      // both halves of the pixel's table entry as ds_read_b128 (4 cycles each; a 12-byte read
+      // of the second half would be a ds_read_b96, 8 cycles)
       const float4 d0 = *reinterpret_cast<const float4*>(dp + 8 * t);
       const float dx = r0.x - (float)(qx0 + (uint32_t)t);
       su += p.x;
@@ -336,7 +341,7 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
       if (FEAT) {
         const float4 d1 = *reinterpret_cast<const float4*>(dp + 8 * t + 4);
         cC = fma2(mk2(p.y, p.y), mk2(d1.x, d1.y), cC);
-        cF2 = __builtin_fmaf(p.y, d1.z, cF2);
+        cD = fma2(mk2(p.y, p.y), mk2(d1.z, d1.w), cD);  // d1.w = 0
       }
     }
     // the 16 slots of the row as 8 pairs (slot order of kAcc*): (sum u dx, sum u dy),
@@ -348,7 +353,7 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
     v[3] = cA;
     v[4] = cB;
     v[5] = cC;
-    v[6] = mk2(cF2, 0.f);
+    v[6] = cD;
     v[7] = mk2(0.f, 0.f);
     // halving butterfly over the 8 rows: lane bit 5 (permlane32_swap), bit 4 (permlane16_swap),
     // bit 3 (DPP row_ror:8 swaps the halves of a 16-lane row)
@@ -399,7 +404,8 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
     }
     __syncthreads();
     const uint32_t nlist = build_wave_list<kBatch>(s_mask, s_list[wid], cnt, wid, lane);
-    uint32_t ns = 0;  // phase-2 slots in use (wave-uniform)
+    uint32_t ns = 0;     // phase-2 slots in use (wave-uniform)
+    uint32_t slotv = 0;  // lane l: batch index of phase-2 slot l & 7
     // Four list entries per group: the per-pair test (power, G, alpha) of all four is evaluated
     // first (independent work), then the entries are replayed in list order.
     for (uint32_t k0 = 0; k0 < nlist; k0 += 4) {
@@ -505,14 +511,15 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
         const float uu = G * dL_dalpha;
         // park (u, w) in the next phase-2 slot
         *reinterpret_cast<f2*>(&s_uw[wid][ns * kUwStride + 2 * lane]) = mk2(uu, wgt);
-        if (lane == 0) s_slot[wid][ns] = (uint8_t)j;
-        if (++ns == (uint32_t)kSlots) {
-          phase2(ns);
+        slotv = ((uint32_t)(lane & 7) == ns) ? j : slotv;
+        ns = (uint32_t)__builtin_amdgcn_readfirstlane((int)(ns + 1));
+        if (ns == (uint32_t)kSlots) {
+          phase2(ns, slotv);
           ns = 0;
         }
       }
     }
-    if (ns) phase2(ns);
+    if (ns) phase2(ns, slotv);
     __syncthreads();
     // moments -> the reference's dL/dmean2D (NDC-scaled) and dL/dconic, once per (splat, tile)
     if (threadIdx.x < cnt) {

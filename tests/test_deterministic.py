@@ -156,8 +156,12 @@ def test_C_backward_takes_the_layout_from_the_binning_buffer():
         c = bwd(f_std, dpix)  # mode on now: the buffer says atomics
         for x, y in zip(a, c):
             assert float((x - y).abs().max()) <= 1e-5 * float(y.abs().max()) + 1e-30
-        junk = torch.zeros_like(f_std[4])
+        # a buffer large enough for either layout is identified by its tag: junk is refused
+        junk = torch.zeros_like(f_det[4])
         with pytest.raises(_lib.GsrError, match="binningBuffer"):
             bwd(f_std, dpix, binning=junk)
+        # a buffer too small for R instances is refused on the host (no device read)
+        with pytest.raises(RuntimeError, match="binningBuffer"):
+            bwd(f_std, dpix, binning=f_std[4][: f_std[4].numel() // 2])
     finally:
         dgr.deterministic(prev)
