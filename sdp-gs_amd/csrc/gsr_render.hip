@@ -455,7 +455,9 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
           f2 c2 = mk2(c0.x, c0.y) * dpA;
           c2 = fma2(mk2(c0.z, NC > 3 ? c0.w : 0.f), dpB, c2);
           if (FEAT) c2 = fma2(mk2(c1v[u].x, c1v[u].y), dpC, c2);
-          if (NC > 3) c2 = fma2(mk2(FEAT ? c1v[u].z : 0.f, 1.0f), dpD, c2);
+          // (FEAT: c1.w holds the alpha channel's 1, read so that the record is one ds_read_b128
+          // rather than a ds_read_b96 at twice the LDS cycles)
+          if (NC > 3) c2 = fma2(FEAT ? mk2(c1v[u].z, c1v[u].w) : mk2(0.f, 1.0f), dpD, c2);
           cdv[u] = c2.x + c2.y;
           // keep the dot product here (the compiler would sink it into the contributing branch
           // and hold the colours live across the test phase)
