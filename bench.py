@@ -68,7 +68,8 @@ class Opt:
 
 
 def algorithmic_bytes(stage, P, Pv, R, T, HW, D=3, C=8, tile_passes=2, acc=True, defer_sh=False,
-                      precolor=False, views=6, launch_views=1, acc_in_blend=False):
+                      precolor=False, views=6, launch_views=1, acc_in_blend=False,
+                      sh_in_bwd=False):
     """Bytes each stage must move per launch.
     P Gaussians, Pv visible, R instances, T tiles, HW pixels, C blended channels (rgb, depth,
     alpha, feature x3), acc: the backward adds into existing gradients (read + write),
@@ -78,9 +79,10 @@ def algorithmic_bytes(stage, P, Pv, R, T, HW, D=3, C=8, tile_passes=2, acc=True,
     scale by it, except that the multi-view preprocess and per-Gaussian backward read the model
     rows (and read-modify-write the leaf gradients) once per launch.  acc_in_blend: the 64-B
     backward accumulator rows are zeroed by the forward blend's grid (the batched multi-view
-    forward) instead of the preprocess's."""
+    forward) instead of the preprocess's.  sh_in_bwd: the multi-view per-Gaussian backward forms
+    the SH gradients itself (no per-view dL/dRGB plane, no flush; include/gsr.h gsr_view)."""
     if stage in ("preprocess", "preprocess_bwd") and launch_views > 1:
-        per, once = _model_split(stage, P, Pv, D, acc, defer_sh, precolor)
+        per, once = _model_split(stage, P, Pv, D, acc, defer_sh, precolor, sh_in_bwd)
         b = launch_views * per + once
     else:
         b = launch_views * _stage_bytes(stage, P, Pv, R, T, HW, D, C, tile_passes, acc, defer_sh,
@@ -90,7 +92,7 @@ def algorithmic_bytes(stage, P, Pv, R, T, HW, D=3, C=8, tile_passes=2, acc=True,
     return b
 
 
-def _model_split(stage, P, Pv, D, acc, defer_sh, precolor):
+def _model_split(stage, P, Pv, D, acc, defer_sh, precolor, sh_in_bwd=False):
     """(per-view bytes, once-per-launch bytes) of the multi-view preprocess / backward launch."""
     sh = 12 * (D + 1) ** 2
     sh_fwd = 13 if precolor else sh
@@ -102,10 +104,12 @@ def _model_split(stage, P, Pv, D, acc, defer_sh, precolor):
     # once: means, scale, rotation, opacity, language in; the leaf gradients (means3D, opacity,
     # scale, rotation, language; SH deferred or not) read-modify-written (acc) or stored once;
     # per view: accumulator row, colour Jacobian + clamp, radii, screen-space gradient out,
-    # deferred dL/dRGB out
+    # deferred dL/dRGB out (sh_in_bwd: none -- the SH gradient rows, every row, are written once)
     leaf = 12 + 4 + 12 + 16 + 12 + (0 if defer_sh else sh)
     once = Pv * (12 + 12 + 16 + 4 + 12) + ((2 * Pv) if acc else P) * leaf
-    per = Pv * (64 + sh_bwd + 1) + P * 4 + P * 12 + (P * 12 if defer_sh else 0)
+    if sh_in_bwd:
+        once += (2 * P if acc else P) * sh
+    per = Pv * (64 + sh_bwd + 1) + P * 4 + P * 12 + (P * 12 if defer_sh and not sh_in_bwd else 0)
     return per, once
 
 
@@ -401,6 +405,12 @@ def main():
     # the batched multi-view forward zeroes the accumulator rows in its blend (gsr_api.cpp
     # views_forward_batched)
     acc_in_blend = not args.per_view
+    # deferred SH gradients formed by the multi-view backward itself (ViewPipeline.run_views with
+    # the colour pre-pass and at most 8 views per call: no flush launch)
+    chunk_views = -(-args.views_per_gpu // max(1, args.view_chunks))
+    sh_in_bwd = (defer_sh and multi and not args.no_precolor and chunk_views <= 8)
+    if stages and sh_in_bwd != (stages.get("sh_flush", (0.0, 0))[1] == 0):
+        print("bench: SH-gradient mode and the measured stages disagree", file=sys.stderr)
     for name, (ms, calls) in stages.items():
         if calls == 0:
             continue
@@ -412,7 +422,8 @@ def main():
             vpl = max(1, int(round(len(my_cams) * stage_steps.get(name, 1) / calls)))
         b = algorithmic_bytes(name, P, Pv, R, T, HW, D=deg, acc=not args.autograd_grads,
                               defer_sh=defer_sh, precolor=not args.no_precolor,
-                              views=len(my_cams), launch_views=vpl, acc_in_blend=acc_in_blend)
+                              views=len(my_cams), launch_views=vpl, acc_in_blend=acc_in_blend,
+                              sh_in_bwd=sh_in_bwd)
         k = {"avg_ms": round(avg_ms, 4), "calls": int(calls), "bytes": int(b),
              "views_per_launch": vpl, "gbs": round(b / (avg_ms * 1e-3) / 1e9, 1)}
         if name in ("render_fwd", "render_bwd"):
@@ -510,7 +521,8 @@ def main():
                                           f"{views.depth} view streams (no collectives)",
                        "collective_backend": _backend_name() if world > 1 else None,
                        "camera_pool": pool,
-                       "sh_grads": "deferred (one flush per step)" if defer_sh else "per view",
+                       "sh_grads": ("formed in the multi-view backward" if sh_in_bwd else
+                                    "deferred (one flush per step)") if defer_sh else "per view",
                        "sh_colour": "per view" if args.no_precolor else "multi-view pre-pass",
                        # num_rendered: the reference's count (boundary return value, full
                        # 3-sigma rectangles); instances: those binned after the exact tile cull

@@ -274,7 +274,9 @@ typedef struct gsr_view {
   /* backward: upstream gradients (depth / alpha / feature may be NULL), the screen-space
    * gradient dL_dmeans2D[P,3] (always stored), and -- deferred SH gradients -- the planar
    * dL/dRGB [3][P] this view stores (NULL: the SH gradients are added directly) with the
-   * pre-pass Jacobian pre_jac (optional, needs dL_dcolor_sh) */
+   * pre-pass Jacobian pre_jac (optional).  pre_jac without dL_dcolor_sh, in every view of a
+   * call of at most 8 views: the call's single per-Gaussian launch forms the SH gradients itself
+   * from the views' dL/dRGB (the deferred path's flush fused: same values, no [3][P] planes) */
   const float* dL_dout_color; const float* dL_dout_depth; const float* dL_dout_alpha;
   const float* dL_dout_feature;
   float* dL_dmeans2D; float* dL_dcolor_sh; const float* pre_jac;
@@ -301,7 +303,8 @@ int gsr_rasterize_views_fused(
  * raw leaves' gradients exactly as
  * consecutive gsr_rasterize_gaussians_fused_backward[_deferred] calls with accumulate = 1 for
  * every view after the first (the first uses `accumulate`).  With views[v].dL_dcolor_sh set the
- * SH gradients are deferred (dL_dfeatures_dc / _rest may be NULL). */
+ * SH gradients are deferred (dL_dfeatures_dc / _rest may be NULL); with pre_jac and no
+ * dL_dcolor_sh they are formed in the per-Gaussian launch (gsr_view). */
 int gsr_rasterize_views_fused_backward(
     int V, const gsr_view* views, int image_height, int image_width,
     int P, int M, const float* background, const float* means3D,

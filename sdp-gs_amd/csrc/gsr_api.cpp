@@ -849,7 +849,7 @@ static int bwd_setup(
     float* dL_dscales, float* dL_drotations, float* dL_dsh_language, float* dL_dlanguage_feature,
     int debug, int fused, const float* sh_dc, const float* sh_rest,
     const float* opacity_raw, float* dL_dsh_rest, int accumulate, float* dRGB_sh,
-    const float* pre_jac) {
+    const float* pre_jac, bool sh_in_views = false) {
   const bool det = (debug & GSR_DEBUG_DETERMINISTIC) != 0;  // must match the forward's flags
   const bool rows = det;
   debug &= 1;
@@ -862,7 +862,9 @@ static int bwd_setup(
   } else if (dRGB_sh) {
     return fail(GSR_ERR_ARGUMENT, "deferred SH gradients are a fused-path mode");
   }
-  if (pre_jac && !dRGB_sh)
+  // pre_jac without dL_dcolor_sh: the multi-view call forms the SH gradients in its per-Gaussian
+  // launch (gsr.h gsr_view.pre_jac); a single-view call needs the deferred dL/dRGB plane
+  if (pre_jac && !dRGB_sh && !sh_in_views)
     return fail(GSR_ERR_ARGUMENT, "pre_jac needs the deferred SH gradients (dL_dcolor_sh)");
   const int W = image_width, H = image_height;
   if (P < 0 || R < 0 || W <= 0 || H <= 0) return fail(GSR_ERR_ARGUMENT, "invalid sizes");
@@ -1454,9 +1456,18 @@ int gsr_rasterize_views_fused_backward_sliced(
                            dL_dopacity_raw, dL_dmeans3D, nullptr, dL_dfeatures_dc,
                            dL_dscaling_raw, dL_drotation_raw, dL_dlanguage_feature, nullptr,
                            debug, 1, features_dc, features_rest, opacity_raw, dL_dfeatures_rest,
-                           (v > 0 || accumulate) ? 1 : 0, w.dL_dcolor_sh, w.pre_jac))
+                           (v > 0 || accumulate) ? 1 : 0, w.dL_dcolor_sh, w.pre_jac,
+                           /*sh_in_views=*/true))
       return rc;
   }
+  // SH gradients formed by the per-Gaussian launch itself (every view with pre_jac and without
+  // dL_dcolor_sh): all views in one launch, no per-view fallback
+  int sh_in = 0;
+  for (int v = 0; v < V; v++) sh_in += (views[v].pre_jac && !views[v].dL_dcolor_sh) ? 1 : 0;
+  if (sh_in != 0 && (sh_in != V || V > kMaxBwdViews || (debug & GSR_DEBUG_TEST_PER_VIEW_PRE)))
+    return fail(GSR_ERR_ARGUMENT, "SH gradients formed in the multi-view backward (pre_jac without "
+                                  "dL_dcolor_sh) need it in every view and at most %d views",
+                kMaxBwdViews);
   if (V == 0) {
     if (on_rows && P > 0) on_rows(rows_ctx, 0, P);
     return GSR_OK;
@@ -1534,6 +1545,9 @@ int gsr_rasterize_views_fused_backward_sliced(
         if (last && on_rows && step >= (uint32_t)P) on_rows(rows_ctx, 0, P);
       }
     }
+    if (ve == hipErrorNotSupported && sh_in)
+      return fail(GSR_ERR_ARGUMENT, "SH gradients formed in the multi-view backward: this "
+                                    "configuration has no multi-view per-Gaussian launch");
     if (ve == hipErrorNotSupported) {
       (void)hipGetLastError();
       for (int k = 0; k < n; k++)

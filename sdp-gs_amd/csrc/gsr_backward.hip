@@ -158,6 +158,7 @@ struct MemSink {
   const BwdPreArgs& a;
   size_t i;
   __device__ void colors(V3 v) { if (a.dL_dcolors) st3<ACC>(a.dL_dcolors, i, v); }
+  __device__ void rgb(V3) {}
   __device__ void opacity(float v) { st<ACC>(a.dL_dopacity + i, v); }
   __device__ void cov3D(const float* d) {
     if (a.dL_dcov3D)
@@ -183,10 +184,20 @@ struct RegSink {
   float op;
   V3 m3, sc, lf, shl;
   float4 rot;
+  // the view's clamp-masked dL/dRGB, when the launch forms the SH gradients itself: this
+  // Gaussian's slot of the view's LDS plane (stride kThreads per channel), else null
+  float* rgb_lds;
   __device__ static V3 add3(bool as, V3 acc, V3 v) {
     return as ? v : v3(acc.x + v.x, acc.y + v.y, acc.z + v.z);
   }
   __device__ void colors(V3) {}
+  __device__ void rgb(V3 v) {
+    if (rgb_lds) {
+      rgb_lds[0] = v.x;
+      rgb_lds[kThreads] = v.y;
+      rgb_lds[2 * kThreads] = v.z;
+    }
+  }
   __device__ void opacity(float v) { op = assign ? v : op + v; }
   __device__ void cov3D(const float*) {}
   __device__ void scales(V3 v) { sc = add3(assign, sc, v); }
@@ -357,8 +368,9 @@ __device__ __forceinline__ void gaussian_bwd(const BwdPreArgs& a, size_t i, floa
     dRGB.y *= (cl & 2) ? 0 : 1;
     dRGB.z *= (cl & 4) ? 0 : 1;
     const V3 dir_orig = mean - v3(a.campos[0], a.campos[1], a.campos[2]);
-    if (a.dRGB_out && a.pre_jac) {  // deferred, Jacobian from the multi-view pre-pass
-      put3p(a.dRGB_out, (size_t)a.P, i, dRGB);
+    if (a.pre_jac) {  // Jacobian from the multi-view pre-pass; dL/dRGB deferred or to the sink
+      if (a.dRGB_out) put3p(a.dRGB_out, (size_t)a.P, i, dRGB);
+      sk.rgb(dRGB);
       const float* j = a.pre_jac + i;  // planar [9][P]
       const size_t P = (size_t)a.P;
       auto jl = [&](size_t o) { return GSR_BWD_NT ? __builtin_nontemporal_load(j + o) : j[o]; };
@@ -526,15 +538,11 @@ __global__ __launch_bounds__(kThreads) void preprocess_bwd_kernel(BwdPreArgs a) 
 #ifndef GSR_BWDV_MINBLK
 #define GSR_BWDV_MINBLK 1
 #endif
-// 1: each view's gradient row and radius are loaded one view ahead (registers)
-#ifndef GSR_BWDV_PREFETCH
-#define GSR_BWDV_PREFETCH 1
-#endif
+// One Gaussian's views (the body of preprocess_bwd_views_kernel).  rgb: its slot of view 0's
+// LDS dL/dRGB plane when the launch forms the SH gradients itself (planes kThreads * 3 apart).
 template <bool ACC>
-__global__ __launch_bounds__(kThreads, GSR_BWDV_MINBLK) void preprocess_bwd_views_kernel(BwdPreViews m) {
+__device__ __forceinline__ void views_body(const BwdPreViews& m, size_t i, float* rgb) {
   const BwdPreArgs& a0 = m.v[0];
-  const size_t i = (size_t)m.row0 + (size_t)blockIdx.x * kThreads + threadIdx.x;
-  if (i >= (size_t)m.row1) return;
   RegSink sk;
   sk.assign = !ACC;
   if (ACC) {
@@ -559,38 +567,36 @@ __global__ __launch_bounds__(kThreads, GSR_BWDV_MINBLK) void preprocess_bwd_view
   BwdModel md;
   bwd_model(a0, i, md);
   float4 cur[4], nxt[4];
-  int rcur = 0, rnxt = 0;
-  if (GSR_BWDV_PREFETCH) {
-    rcur = a0.radii[i];
-    grad_row(a0, i, cur[0], cur[1], cur[2], cur[3]);
-  }
+  int rcur = a0.radii[i], rnxt = 0;
+  grad_row(a0, i, cur[0], cur[1], cur[2], cur[3]);
 #pragma unroll 1
   for (int v = 0; v < m.V; v++) {
     const BwdPreArgs& a = m.v[v];
-    if (!GSR_BWDV_PREFETCH) {
-      rcur = a.radii[i];
-    } else if (v + 1 < m.V) {
+    if (v + 1 < m.V) {
       const BwdPreArgs& an = m.v[v + 1];
       rnxt = an.radii[i];
       grad_row(an, i, nxt[0], nxt[1], nxt[2], nxt[3]);
     }
+    sk.rgb_lds = rgb ? rgb + v * 3 * kThreads : nullptr;
     if (a.status && *a.status) {  // this view's forward failed (view-uniform): NaN gradients
       const float nan = __builtin_nanf("");
       const V3 n3 = v3(nan, nan, nan);
       put3(a.dL_dmeans2D, i, n3);
-      put3p(a.dRGB_out, (size_t)a.P, i, n3);
+      if (a.dRGB_out) put3p(a.dRGB_out, (size_t)a.P, i, n3);
+      sk.rgb(n3);
       sk.opacity(nan); sk.means3D(n3); sk.scales(n3); sk.rotation(make_float4(nan, nan, nan, nan));
       sk.lang_feature(n3); sk.sh_language(n3);
       sk.assign = false;
       touched = true;
     } else if (rcur > 0) {
       const BwdModel mv = opaque(md);
-      gaussian_bwd<true>(a, i, nullptr, nullptr, sk, &mv, GSR_BWDV_PREFETCH ? cur : nullptr);
+      gaussian_bwd<true>(a, i, nullptr, nullptr, sk, &mv, cur);
       sk.assign = false;
       touched = true;
     } else {
       put3(a.dL_dmeans2D, i, v3(0, 0, 0));
-      put3p(a.dRGB_out, (size_t)a.P, i, v3(0, 0, 0));
+      if (a.dRGB_out) put3p(a.dRGB_out, (size_t)a.P, i, v3(0, 0, 0));
+      sk.rgb(v3(0, 0, 0));
       if (v == 0) sk.assign = false;  // store mode: the zeros of the culled first view
     }
 #pragma unroll
@@ -604,6 +610,63 @@ __global__ __launch_bounds__(kThreads, GSR_BWDV_MINBLK) void preprocess_bwd_view
   if (a0.dL_drotations) reinterpret_cast<float4*>(a0.dL_drotations)[i] = sk.rot;
   if (a0.dL_dsh_language) put3(a0.dL_dsh_language, i, sk.shl);
   if (a0.dL_dlanguage_feature) put3(a0.dL_dlanguage_feature, i, sk.lf);
+}
+
+// SH = true: the launch holds every view of the step and forms the SH gradients itself --
+//   dL/dsh_k = sum over the views v, in order, of basis_k(normalize(mean - campos_v)) * dL/dRGB_v
+// (backward.cu:20-139, the same operations as sh_flush_kernel), each view's dL/dRGB kept in LDS
+// instead of a [3][P] plane stored here and read back by a flush launch; the rows go out
+// through the LDS staging planes (stored, or added under ACC).
+template <bool ACC, bool SH>
+__global__ __launch_bounds__(kThreads, GSR_BWDV_MINBLK) void preprocess_bwd_views_kernel(BwdPreViews m) {
+  const uint32_t base = m.row0 + blockIdx.x * (uint32_t)kThreads;
+  const int t = (int)threadIdx.x;
+  const size_t i = (size_t)base + t;
+  const bool valid = i < (size_t)m.row1;
+  if (!SH) {
+    if (valid) views_body<ACC>(m, i, nullptr);
+    return;
+  }
+  // the views' dL/dRGB planes ([V][3][kThreads] floats), then the same LDS as staging planes
+  __shared__ float4 s_sh4[SH ? kThreads * kShMaxFloats / 4 : 1];
+  __shared__ uint8_t s_live[kThreads];
+  float* s_sh = reinterpret_cast<float*>(s_sh4);
+  const BwdPreArgs& a0 = m.v[0];
+  const int n = (int)min((uint32_t)kThreads, m.row1 - base);
+  s_live[t] = t < n;
+  if (valid) views_body<ACC>(m, i, s_sh + t);
+  V3 g[16];
+  const int used = (a0.D + 1) * (a0.D + 1);
+  if (valid) {
+    const V3 mean = v3(a0.means3D[3 * i], a0.means3D[3 * i + 1], a0.means3D[3 * i + 2]);
+    for (int v = 0; v < m.V; v++) {
+      const float* cp = m.v[v].campos;
+      float b[16];
+      sh_basis(mean - v3(cp[0], cp[1], cp[2]), a0.D, b);  // gsr_sh.h
+      const float* d = s_sh + v * 3 * kThreads + t;
+      const V3 dRGB = v3(d[0], d[kThreads], d[2 * kThreads]);
+#pragma unroll
+      for (int k = 0; k < 16; k++) g[k] = v == 0 ? b[k] * dRGB : g[k] + b[k] * dRGB;
+    }
+  }
+  __syncthreads();  // every dL/dRGB plane read: the LDS becomes the staging planes
+  const ShPlane p0{nullptr, a0.dL_dsh, 3, 0};
+  const ShPlane p1{nullptr, a0.dL_dsh_rest, (a0.M - 1) * 3, kThreads * 3};
+  if (valid) {
+    float* r0 = s_sh + p0.lds + t * p0.w;
+    float* r1 = s_sh + p1.lds + t * p1.w;
+    r0[0] = g[0].x; r0[1] = g[0].y; r0[2] = g[0].z;
+#pragma unroll
+    for (int k = 1; k < 16; k++) {  // static indices: g stays in registers
+      if (k < a0.M) {
+        const V3 v = k < used ? g[k] : v3(0, 0, 0);
+        r1[3 * k - 3] = v.x; r1[3 * k - 2] = v.y; r1[3 * k - 1] = v.z;
+      }
+    }
+  }
+  __syncthreads();
+  stage<kThreads, false, ACC>(p0, (int)base, n, s_live, s_sh);
+  stage<kThreads, false, ACC>(p1, (int)base, n, s_live, s_sh);
 }
 
 // Deferred SH gradients of a multi-view step: per Gaussian, for each view v in order,
@@ -674,15 +737,21 @@ hipError_t launch_preprocess_backward_views(const BwdPreArgs* views, int V, hipS
   if (V > kMaxBwdViews) return hipErrorNotSupported;
   BwdPreViews m{};
   m.V = V;
+  // SH gradients formed in the launch (pre-pass Jacobian, no deferred dL/dRGB plane, the SH
+  // gradient planes given) or deferred to the step's flush (dL/dRGB planes)
+  const bool sh = views[0].dRGB_out == nullptr;
   for (int k = 0; k < V; k++) {
     const BwdPreArgs& a = views[k];
-    // the multi-view kernel covers the fused, deferred-SH, pre-pass configuration of one model
-    if (!a.fused || !a.dRGB_out || !a.pre_jac || a.cov3D || a.colors_precomp || a.dL_dcolors ||
-        a.dL_dcov3D || a.use_rows || a.P != views[0].P || a.means3D != views[0].means3D ||
+    // the multi-view kernel covers the fused, pre-pass configuration of one model
+    if (!a.fused || !a.pre_jac || a.cov3D || a.colors_precomp || a.dL_dcolors ||
+        a.dL_dcov3D || a.P != views[0].P || a.means3D != views[0].means3D ||
         a.dL_dmeans3D != views[0].dL_dmeans3D || a.dL_dopacity != views[0].dL_dopacity ||
         a.dL_dscales != views[0].dL_dscales || a.dL_drotations != views[0].dL_drotations ||
         a.dL_dsh_language != views[0].dL_dsh_language ||
-        a.dL_dlanguage_feature != views[0].dL_dlanguage_feature || (k > 0 && !a.accumulate))
+        a.dL_dlanguage_feature != views[0].dL_dlanguage_feature || (k > 0 && !a.accumulate) ||
+        (a.dRGB_out == nullptr) != sh ||
+        (sh && (!a.dL_dsh || a.dL_dsh != views[0].dL_dsh || a.dL_dsh_rest != views[0].dL_dsh_rest ||
+                (a.M > 1 && !a.dL_dsh_rest) || a.M != views[0].M || a.D != views[0].D)))
       return hipErrorNotSupported;
     m.v[k] = a;
   }
@@ -690,10 +759,13 @@ hipError_t launch_preprocess_backward_views(const BwdPreArgs* views, int V, hipS
   m.row1 = row1 < (uint32_t)views[0].P ? row1 : (uint32_t)views[0].P;
   if (m.row1 <= m.row0) return hipSuccess;
   const dim3 grid((m.row1 - m.row0 + kThreads - 1) / kThreads);
-  if (views[0].accumulate)
-    hipLaunchKernelGGL(preprocess_bwd_views_kernel<true>, grid, dim3(kThreads), 0, s, m);
-  else
-    hipLaunchKernelGGL(preprocess_bwd_views_kernel<false>, grid, dim3(kThreads), 0, s, m);
+  if (views[0].accumulate) {
+    if (sh) hipLaunchKernelGGL((preprocess_bwd_views_kernel<true, true>), grid, dim3(kThreads), 0, s, m);
+    else hipLaunchKernelGGL((preprocess_bwd_views_kernel<true, false>), grid, dim3(kThreads), 0, s, m);
+  } else {
+    if (sh) hipLaunchKernelGGL((preprocess_bwd_views_kernel<false, true>), grid, dim3(kThreads), 0, s, m);
+    else hipLaunchKernelGGL((preprocess_bwd_views_kernel<false, false>), grid, dim3(kThreads), 0, s, m);
+  }
   return hipGetLastError();
 }
 

@@ -618,6 +618,12 @@ class _RasterizeViewsFused(torch.autograd.Function):
         views[0].stream = ctx.streams[-1].cuda_stream if len(ctx.streams) > 1 else None
         into_leaves = ctx.leaves is not None
         defer = _SH_DEFER.get(dev.index) if into_leaves else None
+        # the SH gradients formed in this call's per-Gaussian launch (ShGradDeferral.fuse_views)
+        fuse_sh = (defer is not None and defer.fuse_views and not defer.views and V <= 8
+                   and all(j is not None for j in ctx.pre_jacs))
+        if fuse_sh:
+            defer.fused = True
+            defer = None
         d_means2D = torch.empty((V, P, 3), **fopts)
         d_rgb = torch.empty((V, 3, P), **fopts) if defer is not None else None
         for v in range(V):
@@ -639,7 +645,7 @@ class _RasterizeViewsFused(torch.autograd.Function):
                 w.pre_jac = _ptr(ctx.pre_jacs[v])
             else:
                 w.dL_dcolor_sh = None
-                w.pre_jac = None
+                w.pre_jac = _ptr(ctx.pre_jacs[v]) if fuse_sh else None
         s_dc, s_rest, s_op, s_sc, s_rot = mt["shapes"]
         accumulate = into_leaves
         if into_leaves:
@@ -674,7 +680,7 @@ class _RasterizeViewsFused(torch.autograd.Function):
         cur = torch.cuda.current_stream(dev)
         if into_leaves:
             _order_leaf_grads(dev, cur)
-        if d_rgb is not None and ctx.jac_event is not None:
+        if (d_rgb is not None or fuse_sh) and ctx.jac_event is not None:
             cur.wait_event(ctx.jac_event)  # the Jacobians came from the pre-pass's side stream
         t_host = time.perf_counter()
         args = (V, views, H, W, P, M, _ptr(bg), _ptr(m3), _ptr(dc), _ptr(rest), _ptr(op),
@@ -893,15 +899,23 @@ class ShGradDeferral:
     the reference's own per-view SH backward (backward.cu:20-139) summed in view order.  The
     .grad of the SH leaves is only complete after flush() (the context's exit flushes)."""
 
-    def __init__(self, device, on_rows=None, chunk_rows: int = 0):
+    def __init__(self, device, on_rows=None, chunk_rows: int = 0, fuse_views: bool = False):
         """on_rows(a, b): called after the flush of Gaussian rows [a, b) has been issued on the
         current stream (gsr_amd.parallel.GradAllReducer starts that slice's all-reduce there);
-        chunk_rows > 0 splits the flush into row ranges of that size (multiple of 256)."""
+        chunk_rows > 0 splits the flush into row ranges of that size (multiple of 256).
+
+        fuse_views: a multi-view backward of at most 8 views with the colour pre-pass forms the
+        SH gradients in its own per-Gaussian launch instead of deferring them (include/gsr.h
+        gsr_view.pre_jac: the flush fused, same values) -- for callers whose multi-view call holds
+        the whole step (gsr_amd.pipeline.ViewPipeline.run_views).  `fused` then says so: those
+        SH gradients are final when that backward's rows are."""
         self.device = torch.device(device)
         self.views = []
         self.leaves = None
         self.on_rows = on_rows
         self.chunk_rows = int(chunk_rows)
+        self.fuse_views = bool(fuse_views)
+        self.fused = False  # a multi-view backward wrote the SH gradients itself
         self.views_flushed = False  # a flush wrote SH gradients (the on_rows hooks ran)
 
     def __enter__(self):

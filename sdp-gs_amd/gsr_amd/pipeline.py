@@ -180,14 +180,23 @@ class ViewPipeline:
                 def on_rows(a, b):
                     for t in sh_leaves:
                         reducer.reduce_rows_async(t, a, b)
-        defer = (dgr.ShGradDeferral(self.device, on_rows=on_rows, chunk_rows=chunk)
+        # run_views: a multi-view call holding the step's views forms the SH gradients in its
+        # per-Gaussian launch (ShGradDeferral.fuse_views); run(): one flush at the end
+        defer = (dgr.ShGradDeferral(self.device, on_rows=on_rows, chunk_rows=chunk,
+                                    fuse_views=sliced)
                  if self.defer_sh else contextlib.nullcontext())
+
+        def fused():  # the SH rows were written with the others (final with the backward's rows)
+            return getattr(defer, "fused", False)
+
         slices = contextlib.nullcontext()
         if reducer is not None and sliced and self.bwd_slices > 1:
             ids = {id(t) for t in sh_leaves}
             rest = [p for p in reducer.current_params() if id(p) not in ids]
             slices = dgr.BackwardRowSlices(
-                self.device, lambda a, b: reducer.reduce_row_slices_async(rest, a, b),
+                self.device,
+                lambda a, b: reducer.reduce_row_slices_async(
+                    rest + (list(sh_leaves) if fused() else []), a, b),
                 self.bwd_slices)
             self._slices = slices
         with pre, defer:  # defer's exit: the SH gradients of all views, after the join
@@ -197,7 +206,7 @@ class ViewPipeline:
             finally:
                 self._slices = None
             if reducer is not None:  # every view's backward is done: the non-SH grads are final
-                ids = {id(t) for t in sh_leaves}
+                ids = set() if fused() else {id(t) for t in sh_leaves}
                 # (with the step's fault snapshot: every forward of the step is done)
                 if getattr(slices, "ran", False):  # already reduced slice by slice
                     reducer.reduce_async([], guard=True)
@@ -205,7 +214,7 @@ class ViewPipeline:
                     reducer.reduce_async([p for p in reducer.current_params()
                                           if id(p) not in ids], guard=True)
         if reducer is not None:
-            if sh_leaves and not defer.views_flushed:
+            if sh_leaves and not defer.views_flushed and not fused():
                 reducer.reduce_async(sh_leaves)  # no view produced deferred SH gradients
             reducer.wait()
         return out
