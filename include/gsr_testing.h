@@ -28,6 +28,10 @@ int gsr_test_force_sort_timeout(int on);
 
 int gsr_test_radix_sort_pairs_sentinel(uint32_t* keys, uint32_t* vals, size_t n, int bits,
                                        void* scratch, void* stream);
+/* The planned sort (the depth sort's): passes whose digit is constant over the (non-sentinel)
+ * keys do not run; same result as gsr_test_radix_sort_pairs[_sentinel]. */
+int gsr_test_radix_sort_pairs_planned(uint32_t* keys, uint32_t* vals, size_t n, int bits,
+                                      int sentinel_anywhere, void* scratch, void* stream);
 /* Scratch bytes needed by gsr_test_scan for n elements. */
 size_t gsr_test_scan_scratch_bytes(size_t n);
 /* out = inclusive (or exclusive) prefix sum of in (device pointers). */

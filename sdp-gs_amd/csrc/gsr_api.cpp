@@ -34,6 +34,8 @@ GeomState carve_geom(char* base, size_t P) {
   g.dval_a = c.take<uint32_t>(P);
   g.dkey_b = c.take<uint32_t>(P);
   g.dval_b = c.take<uint32_t>(P);
+  g.dkey_c = c.take<uint32_t>(P);
+  g.dval_c = c.take<uint32_t>(P);
   g.clamped = c.take<uint8_t>(P);
   g.radii = c.take<int32_t>(P);
   g.rec = c.take<float4>(4 * P);
@@ -551,9 +553,11 @@ static int fwd_begin(const FwdModel& m, FwdCam& c) {
   bool in_b = false;
   PROF_BEGIN(DEPTH_SORT);
   // the last pass writes each Gaussian's tile count in place of its sorted key
+  // (planned: the passes of constant digits -- typically the exponent byte -- do not run)
   GSR_CHECK(radix_sort_pairs(g.dkey_a, g.dval_a, g.dkey_b, g.dval_b, (size_t)P, 32,
                              g.sort, &in_b, stream, /*sentinel_anywhere=*/true,
-                             /*precleared=*/true, /*key_payload=*/g.tiles_touched));
+                             /*precleared=*/true, /*key_payload=*/g.tiles_touched, g.dkey_c,
+                             g.dval_c));
   PROF_END(DEPTH_SORT);
   c.depth_in_b = in_b;
   const uint32_t* counts_sorted = in_b ? g.dkey_b : g.dkey_a;
@@ -1214,7 +1218,8 @@ int views_forward_batched(const FwdModel& m, std::vector<FwdCam>& cams, gsr_view
       }
       sums[l] = SumSpec{g.pre_parts, g.pre_parts + pre_blocks, pre_blocks, g.flags + 1, c.host_dev,
                         m.prefiltered ? g.flags : nullptr};
-      ds[l] = SortSpec{g.dkey_a, g.dval_a, g.dkey_b, g.dval_b, (size_t)P, g.sort, g.tiles_touched};
+      ds[l] = SortSpec{g.dkey_a, g.dval_a, g.dkey_b, g.dval_b, (size_t)P, g.sort, g.tiles_touched,
+                       g.dkey_c, g.dval_c};
       G.live.push_back(v);
     }
     const int nl = (int)G.live.size();
@@ -1632,13 +1637,18 @@ int gsr_sh_grad_flush(int P, int M, int degree, const float* means3D, int nviews
 
 // ---- test hooks (include/gsr_testing.h) -----------------------------------------------------------
 static size_t sort_scratch_layout(char* base, size_t n, uint32_t** kb, uint32_t** vb,
-                                  SortScratch* sc) {
+                                  SortScratch* sc, uint32_t** kc = nullptr,
+                                  uint32_t** vc = nullptr) {
   Carver c(base);
   uint32_t* a = c.take<uint32_t>(n);
   uint32_t* b = c.take<uint32_t>(n);
+  uint32_t* a2 = c.take<uint32_t>(n);  // the planned sort's third pair
+  uint32_t* b2 = c.take<uint32_t>(n);
   SortScratch s = take_sort_scratch(c, n);
   if (kb) *kb = a;
   if (vb) *vb = b;
+  if (kc) *kc = a2;
+  if (vc) *vc = b2;
   if (sc) *sc = s;
   return c.size();
 }
@@ -1648,7 +1658,7 @@ size_t gsr_test_sort_scratch_bytes(size_t n) {
 }
 
 static int test_radix_sort(uint32_t* keys, uint32_t* vals, size_t n, int bits, void* scratch,
-                           void* stream_ptr, bool sentinel_anywhere);
+                           void* stream_ptr, bool sentinel_anywhere, bool planned = false);
 
 int gsr_test_radix_sort_pairs(uint32_t* keys, uint32_t* vals, size_t n, int bits, void* scratch,
                               void* stream_ptr) {
@@ -1660,19 +1670,25 @@ int gsr_test_radix_sort_pairs_sentinel(uint32_t* keys, uint32_t* vals, size_t n,
   return test_radix_sort(keys, vals, n, bits, scratch, stream_ptr, true);
 }
 
+int gsr_test_radix_sort_pairs_planned(uint32_t* keys, uint32_t* vals, size_t n, int bits,
+                                      int sentinel_anywhere, void* scratch, void* stream_ptr) {
+  return test_radix_sort(keys, vals, n, bits, scratch, stream_ptr, sentinel_anywhere != 0, true);
+}
+
 static int test_radix_sort(uint32_t* keys, uint32_t* vals, size_t n, int bits, void* scratch,
-                           void* stream_ptr, bool sentinel_anywhere) {
+                           void* stream_ptr, bool sentinel_anywhere, bool planned) {
   g_err.clear();
   hipStream_t stream = (hipStream_t)stream_ptr;
   const int debug = 0;
   if (n == 0) return GSR_OK;
   if (!keys || !vals || !scratch || bits < 0 || bits > 32) return fail(GSR_ERR_ARGUMENT, "bad args");
   if (n > 0xffffffffull) return fail(GSR_ERR_TOO_LARGE, "n too large");
-  uint32_t *kb, *vb;
+  uint32_t *kb, *vb, *kc, *vc;
   SortScratch sc;
-  sort_scratch_layout((char*)scratch, n, &kb, &vb, &sc);
+  sort_scratch_layout((char*)scratch, n, &kb, &vb, &sc, &kc, &vc);
   bool in_b = false;
-  GSR_CHECK(radix_sort_pairs(keys, vals, kb, vb, n, bits, sc, &in_b, stream, sentinel_anywhere));
+  GSR_CHECK(radix_sort_pairs(keys, vals, kb, vb, n, bits, sc, &in_b, stream, sentinel_anywhere,
+                             false, nullptr, planned ? kc : nullptr, planned ? vc : nullptr));
   uint32_t* host = pinned_slot(0);
   if (!host) return fail(GSR_ERR_HIP, "pinned host allocation failed");
   GSR_CHECK(hipMemcpyAsync(host + 2, sc.aux + kSortAuxErr, 4, hipMemcpyDeviceToHost, stream));

@@ -75,7 +75,10 @@ constexpr int kSortTotShards = 16;
 constexpr size_t kSortAuxTotals = 0,
                  kSortAuxSent = kSortAuxTotals + (size_t)kSortTotShards * kSortMaxPasses * 256,
                  kSortAuxTickets = kSortAuxSent + kSortTotShards,
-                 kSortAuxErr = kSortAuxTickets + 8 * kSortMaxPasses, kSortAuxLen = kSortAuxErr + 4;
+                 kSortAuxErr = kSortAuxTickets + 8 * kSortMaxPasses,
+                 // planned sorts (a third buffer pair): the plan -- bit p set for each pass
+                 // that runs (gsr_sort.hip sort_plan_kernel)
+                 kSortAuxPlan = kSortAuxErr + 4, kSortAuxLen = kSortAuxPlan + 4;
 // Key whose position in the sorted output does not matter (culled Gaussians: no tiles): it is
 // left out of the count of digits present, so a pass whose digit is constant over every other key
 // is a plain copy (see radix_onesweep_kernel).
@@ -125,10 +128,16 @@ hipError_t reduce_u32(const uint32_t* in, size_t n, uint32_t* parts, uint32_t* o
 // key_payload: when set, the LAST pass writes key_payload[value] instead of the sorted key (the
 // keys themselves are not needed afterwards): the depth sort hands the scan its tile counts
 // already in depth order, one gather inside the sort instead of two in the scan.
+// kc, vc (optional, a third buffer pair): a PLANNED sort -- the digit-totals launch marks every
+// pass whose digit is the same for every (non-sentinel) key, those passes do not run at all (not
+// even as a copy), and the passes that do run ping-pong between (kc, vc) and (kb, vb) so that the
+// last one writes (kb, vb): the result is always in (kb, vb), (ka, va) is only read.  Same
+// result as the unplanned sort, bit for bit (a constant digit's stable pass is the identity).
 hipError_t radix_sort_pairs(uint32_t* ka, uint32_t* va, uint32_t* kb, uint32_t* vb, size_t n,
                             int bits, SortScratch scratch, bool* result_in_b, hipStream_t s,
                             bool sentinel_anywhere = false, bool precleared = false,
-                            const uint32_t* key_payload = nullptr);
+                            const uint32_t* key_payload = nullptr, uint32_t* kc = nullptr,
+                            uint32_t* vc = nullptr);
 // Several independent sorts / scans / sums, one launch per stage for all of them (the multi-view
 // forward's batched binning, gsr_api.cpp): a view's workgroups are a contiguous block range of
 // the launch, and inside it everything is the one-view kernel's (own totals, tickets, look-back
@@ -140,6 +149,7 @@ struct SortSpec {
   size_t n;
   SortScratch scratch;
   const uint32_t* key_payload;
+  uint32_t *kc = nullptr, *vc = nullptr;  // planned sort (radix_sort_pairs): all views or none
 };
 hipError_t radix_sort_pairs_views(const SortSpec* v, int V, int bits, bool* result_in_b,
                                   hipStream_t s, bool sentinel_anywhere, bool precleared);
@@ -185,8 +195,10 @@ uint32_t* forward_faults_word();
 struct GeomState {
   uint32_t* dkey_a;         // [P] depth-sort keys (float bits of z; 0xffffffff if culled)
   uint32_t* dval_a;         // [P] Gaussian ids, depth-sorted after the sort (see depth_sorted())
-  uint32_t* dkey_b;
+  uint32_t* dkey_b;          // the planned depth sort's result (radix_sort_pairs kb, vb)
   uint32_t* dval_b;
+  uint32_t* dkey_c;          // its third buffer pair
+  uint32_t* dval_c;
   uint8_t* clamped;         // [P] bit c set <=> SH colour channel c clamped (forward.cu:67-69)
   int32_t* radii;           // [P] internal radii (used when the caller passes none)
   float4* rec;              // [P*4] splat record for the blend

@@ -283,12 +283,79 @@ __device__ __forceinline__ void radix_totals_body(const uint32_t* __restrict__ k
   if (threadIdx.x == 0 && nsent) atomicAdd(&nsent_out[shard], nsent);
 }
 
+// Planned sort (radix_sort_pairs kc): one workgroup per sort, after the totals launch, writes the
+// plan -- bit p set for each pass whose digit is not the same for every non-sentinel key (the
+// passes that run); none: the last pass runs (a copy that places the result and gathers the
+// payload).  (A separate launch: a last-workgroup plan inside the totals launch needs an
+// agent-scope release fence per workgroup, an L2 write-back each.)
+__device__ __forceinline__ void sort_plan_body(const uint32_t* __restrict__ aux, int bits,
+                                               int skip_sentinel, uint32_t* __restrict__ plan_out) {
+  __shared__ uint32_t s_n[kSortMaxPasses][kThreads / 64];
+  const int passes = (bits + 7) / 8;
+  const int dw = sort_digit_width(bits);
+  uint32_t sent = 0;
+  if (skip_sentinel) {
+#pragma unroll
+    for (int sh = 0; sh < kSortTotShards; sh++) sent += aux[kSortAuxSent + sh];
+  }
+  for (int p = 0; p < passes; p++) {
+    const int dbits = (bits - dw * p) < dw ? (bits - dw * p) : dw;
+    const uint32_t dig = threadIdx.x;  // kThreads = 256 digits
+    uint32_t c = 0;
+    if (dig < (1u << dbits)) {
+#pragma unroll
+      for (int sh = 0; sh < kSortTotShards; sh++)
+        c += aux[kSortAuxTotals + (size_t)sh * kSortMaxPasses * 256 + p * 256 + dig];
+      // sentinel keys (every digit at its maximum) do not count
+      if (dig == (1u << dbits) - 1u) c -= sent;
+    }
+    const uint64_t b = __ballot(c != 0u);
+    if ((threadIdx.x & 63) == 0) s_n[p][threadIdx.x >> 6] = (uint32_t)__popcll(b);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t plan = 0;
+    for (int p = 0; p < passes; p++)
+      if (s_n[p][0] + s_n[p][1] + s_n[p][2] + s_n[p][3] > 1u) plan |= 1u << p;
+    if (plan == 0) plan = 1u << (passes - 1);
+    plan_out[0] = plan;
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void sort_plan_kernel(uint32_t* __restrict__ aux, int bits,
+                                                             int skip_sentinel) {
+  sort_plan_body(aux, bits, skip_sentinel, aux + kSortAuxPlan);
+}
+
 __global__ __launch_bounds__(kThreads) void radix_totals_kernel(const uint32_t* __restrict__ keys,
                                                                 size_t n, int bits,
                                                                 uint32_t* __restrict__ totals,
                                                                 uint32_t* __restrict__ nsent_out,
                                                                 int skip_sentinel) {
   radix_totals_body(keys, n, bits, totals, nsent_out, skip_sentinel, blockIdx.x, gridDim.x);
+}
+
+// The buffers of pass `pass` of a planned sort (radix_sort_pairs kc): the passes that run (plan
+// bits) read (ka, va) first and alternate so that the last one writes (kb, vb).  False: this pass
+// does not run.
+struct PassBufs {
+  const uint32_t *kin, *vin;
+  uint32_t *kout, *vout;
+  bool last;
+};
+__device__ __forceinline__ bool planned_pass(uint32_t plan, int pass, const uint32_t* ka,
+                                             const uint32_t* va, uint32_t* kb, uint32_t* vb,
+                                             uint32_t* kc, uint32_t* vc, PassBufs& o) {
+  if (!((plan >> pass) & 1u)) return false;
+  const int k = __popc(plan), j = __popc(plan & ((1u << pass) - 1u));
+  // run j writes B when (k - 1 - j) is even, else C; it reads what run j - 1 wrote (A for j = 0)
+  const bool out_b = ((k - 1 - j) & 1) == 0;
+  o.kout = out_b ? kb : kc;
+  o.vout = out_b ? vb : vc;
+  o.kin = j == 0 ? ka : (out_b ? kc : kb);
+  o.vin = j == 0 ? va : (out_b ? vc : vb);
+  o.last = j == k - 1;
+  return true;
 }
 
 __device__ __forceinline__ uint64_t status_load(const uint64_t* p) {
@@ -526,6 +593,20 @@ __global__ __launch_bounds__(NT, NT == 1024 ? 8 : (NT == 512 ? 6 : 1)) void radi
                     kpay, blockIdx.x, gridDim.x);
 }
 
+// a pass of a planned sort: (kin, vin) = A, (kout, vout) = B, (kc, vc) = C; plan = kSortAuxPlan
+template <int NT>
+__global__ __launch_bounds__(NT, NT == 1024 ? 8 : (NT == 512 ? 6 : 1)) void radix_planned_kernel(
+    const uint32_t* __restrict__ ka, const uint32_t* __restrict__ va, size_t n, int pass,
+    int shift, int bits, const uint32_t* __restrict__ totals, const uint32_t* __restrict__ nsent_sh,
+    uint32_t* __restrict__ ticket, uint64_t* __restrict__ status, uint32_t* __restrict__ err,
+    uint32_t* __restrict__ kb, uint32_t* __restrict__ vb, uint32_t* __restrict__ kc,
+    uint32_t* __restrict__ vc, const uint32_t* __restrict__ kpay, const uint32_t* plan) {
+  PassBufs o;
+  if (!planned_pass(*plan, pass, ka, va, kb, vb, kc, vc, o)) return;  // grid-uniform
+  onesweep_body<NT>(o.kin, o.vin, n, shift, bits, totals, nsent_sh, ticket, status, err, o.kout,
+                    o.vout, o.last ? kpay : nullptr, blockIdx.x, gridDim.x);
+}
+
 // ---- several independent sorts / scans / sums per launch (the multi-view forward's batched
 // binning).  Workgroup b belongs to view k with first[k] <= b < first[k + 1] (workgroup-uniform);
 // inside a view everything is exactly the one-view kernel: its own digit totals, tickets and
@@ -536,6 +617,7 @@ struct SortPassJob {
   const uint32_t* vin;
   uint32_t* kout;
   uint32_t* vout;
+  uint32_t *kc, *vc;     // planned sort: (kin, vin) = A, (kout, vout) = B, this = C (else null)
   const uint32_t* kpay;  // last pass: payload gathered in place of the key
   uint32_t* aux;         // totals, sentinel counts, tickets, error word (kSortAux*)
   uint64_t* status;      // this pass's look-back words
@@ -561,14 +643,26 @@ __global__ __launch_bounds__(kThreads) void radix_totals_views_kernel(SortPassVi
                     blockIdx.x - m.first[k], m.first[k + 1] - m.first[k]);
 }
 
+// one workgroup per view (planned sorts)
+__global__ __launch_bounds__(kThreads) void sort_plan_views_kernel(SortPassViews m, int bits,
+                                                                   int skip_sentinel) {
+  const SortPassJob& j = m.j[blockIdx.x];
+  if (j.n == 0) return;
+  sort_plan_body(j.aux, bits, skip_sentinel, j.aux + kSortAuxPlan);
+}
+
 template <int NT>
 __global__ __launch_bounds__(NT, NT == 1024 ? 8 : (NT == 512 ? 6 : 1)) void radix_onesweep_views_kernel(
     SortPassViews m, int pass, int shift, int bits, int sentinel) {
   const int k = batch_view(m.first, m.V, blockIdx.x);
   const SortPassJob& j = m.j[k];
-  onesweep_body<NT>(j.kin, j.vin, j.n, shift, bits, j.aux + kSortAuxTotals + 256 * pass,
+  PassBufs o{j.kin, j.vin, j.kout, j.vout, true};
+  if (j.kc) {  // planned (workgroup-uniform per view: the view's own plan)
+    if (!planned_pass(j.aux[kSortAuxPlan], pass, j.kin, j.vin, j.kout, j.vout, j.kc, j.vc, o)) return;
+  }
+  onesweep_body<NT>(o.kin, o.vin, j.n, shift, bits, j.aux + kSortAuxTotals + 256 * pass,
                     sentinel ? j.aux + kSortAuxSent : nullptr, j.aux + kSortAuxTickets + 8 * pass,
-                    j.status, j.aux + kSortAuxErr, j.kout, j.vout, j.kpay,
+                    j.status, j.aux + kSortAuxErr, o.kout, o.vout, o.last ? j.kpay : nullptr,
                     blockIdx.x - m.first[k], m.first[k + 1] - m.first[k]);
 }
 
@@ -878,8 +972,9 @@ uint32_t* sort_timeouts_word() {
 hipError_t radix_sort_pairs(uint32_t* ka, uint32_t* va, uint32_t* kb, uint32_t* vb, size_t n,
                             int bits, SortScratch scratch, bool* result_in_b, hipStream_t s,
                             bool sentinel_anywhere, bool precleared,
-                            const uint32_t* key_payload) {
+                            const uint32_t* key_payload, uint32_t* kc, uint32_t* vc) {
   *result_in_b = false;
+  if (kc && !vc) return hipErrorInvalidValue;
   if (n == 0 || bits <= 0) return hipSuccess;
   if (bits > 32 || n > 0xffffffffull) return hipErrorInvalidValue;
   const int passes = sort_passes(bits);
@@ -894,6 +989,9 @@ hipError_t radix_sort_pairs(uint32_t* ka, uint32_t* va, uint32_t* kb, uint32_t* 
                      dim3((unsigned)(tot_tiles < kTotGroups ? tot_tiles : kTotGroups)),
                      dim3(kThreads), 0, s, ka, n, bits, scratch.aux + kSortAuxTotals,
                      scratch.aux + kSortAuxSent, sentinel_anywhere ? 1 : 0);
+  if (kc)
+    hipLaunchKernelGGL(sort_plan_kernel, dim3(1), dim3(kThreads), 0, s, scratch.aux, bits,
+                       sentinel_anywhere ? 1 : 0);
   uint32_t *kin = ka, *vin = va, *kout = kb, *vout = vb;
   bool in_b = false;
   for (int p = 0; p < passes; p++) {
@@ -901,6 +999,19 @@ hipError_t radix_sort_pairs(uint32_t* ka, uint32_t* va, uint32_t* kb, uint32_t* 
     const int shift = dw * p;
     const int dbits = (bits - shift) < dw ? (bits - shift) : dw;
     const int nt = nb <= kResident1024 ? 1024 : 512;
+    if (kc) {  // planned: the pass itself reads the plan and picks its buffers
+#define GSR_PLANNED(NT)                                                                           \
+  hipLaunchKernelGGL(radix_planned_kernel<NT>, dim3(nb), dim3(NT), 0, s, ka, va, n, p, shift,    \
+                     dbits, scratch.aux + kSortAuxTotals + 256 * p,                              \
+                     sentinel_anywhere ? scratch.aux + kSortAuxSent : nullptr,                   \
+                     scratch.aux + kSortAuxTickets + 8 * p,                                      \
+                     scratch.status + (size_t)p * sort_pass_words(n), scratch.aux + kSortAuxErr, \
+                     kb, vb, kc, vc, key_payload, scratch.aux + kSortAuxPlan)
+      if (nt == 1024) GSR_PLANNED(1024);
+      else GSR_PLANNED(512);
+#undef GSR_PLANNED
+      continue;
+    }
 #define GSR_ONESWEEP(NT)                                                                          \
   hipLaunchKernelGGL(radix_onesweep_kernel<NT>, dim3(nb), dim3(NT), 0, s, kin, vin, n, shift,    \
                      dbits, scratch.aux + kSortAuxTotals + 256 * p,                              \
@@ -917,7 +1028,7 @@ hipError_t radix_sort_pairs(uint32_t* ka, uint32_t* va, uint32_t* kb, uint32_t* 
     t = vin; vin = vout; vout = t;
     in_b = !in_b;
   }
-  *result_in_b = in_b;
+  *result_in_b = kc ? true : in_b;
   return hipGetLastError();
 }
 
@@ -933,10 +1044,12 @@ hipError_t radix_sort_pairs_views(const SortSpec* v, int V, int bits, bool* resu
   const int passes = sort_passes(bits);
   SortPassViews m{};
   m.V = V;
+  const bool planned = v[0].kc != nullptr;
   uint32_t tfirst[kMaxBatchViews + 1] = {0}, ofirst[kMaxBatchViews + 1] = {0};
   for (int k = 0; k < V; k++) {
     const size_t n = v[k].n;
     if (n > 0xffffffffull) return hipErrorInvalidValue;
+    if ((v[k].kc != nullptr) != planned || (v[k].kc && !v[k].vc)) return hipErrorInvalidValue;
     if (!precleared && n) {
       hipError_t e = hipMemsetAsync(v[k].scratch.aux, 0, sort_clear_bytes(v[k].scratch, n, bits), s);
       if (e != hipSuccess) return e;
@@ -948,15 +1061,18 @@ hipError_t radix_sort_pairs_views(const SortSpec* v, int V, int bits, bool* resu
   if (ofirst[V] == 0) return hipSuccess;
   auto fill = [&](int p, const uint32_t* first) {
     for (int k = 0; k <= V; k++) m.first[k] = first[k];
-    const bool b_in = (p & 1) != 0;  // pass p reads the pair written by pass p - 1
+    // pass p reads the pair written by pass p - 1; planned: (A, B, C), each pass picks its own
+    const bool b_in = !planned && (p & 1) != 0;
     for (int k = 0; k < V; k++) {
       const SortSpec& w = v[k];
       SortPassJob& j = m.j[k];
       j.kin = b_in ? w.kb : w.ka;
       j.vin = b_in ? w.vb : w.va;
-      j.kout = b_in ? w.ka : w.kb;
-      j.vout = b_in ? w.va : w.vb;
-      j.kpay = p == passes - 1 ? w.key_payload : nullptr;
+      j.kout = (b_in && !planned) ? w.ka : w.kb;
+      j.vout = (b_in && !planned) ? w.va : w.vb;
+      j.kc = w.kc;
+      j.vc = w.vc;
+      j.kpay = (planned || p == passes - 1) ? w.key_payload : nullptr;
       j.aux = w.scratch.aux;
       j.status = w.scratch.status + (size_t)p * sort_pass_words(w.n);
       j.n = (uint32_t)w.n;
@@ -965,6 +1081,9 @@ hipError_t radix_sort_pairs_views(const SortSpec* v, int V, int bits, bool* resu
   fill(0, tfirst);
   hipLaunchKernelGGL(radix_totals_views_kernel, dim3(tfirst[V]), dim3(kThreads), 0, s, m, bits,
                      sentinel_anywhere ? 1 : 0);
+  if (planned)
+    hipLaunchKernelGGL(sort_plan_views_kernel, dim3(V), dim3(kThreads), 0, s, m, bits,
+                       sentinel_anywhere ? 1 : 0);
   const uint32_t nb = ofirst[V];
   const int nt = nb <= kResident1024 ? 1024 : 512;
   for (int p = 0; p < passes; p++) {
@@ -979,7 +1098,7 @@ hipError_t radix_sort_pairs_views(const SortSpec* v, int V, int bits, bool* resu
       hipLaunchKernelGGL(radix_onesweep_views_kernel<512>, dim3(nb), dim3(512), 0, s, m, p, shift, dbits,
                          sentinel_anywhere ? 1 : 0);
   }
-  *result_in_b = (passes & 1) != 0;
+  *result_in_b = planned || (passes & 1) != 0;
   return hipGetLastError();
 }
 

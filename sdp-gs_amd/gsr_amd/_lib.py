@@ -290,6 +290,8 @@ def load():
         L.gsr_test_radix_sort_pairs.argtypes = [_p, _p, _sz, _i, _p, _p]
         L.gsr_test_radix_sort_pairs_sentinel.restype = _i
         L.gsr_test_radix_sort_pairs_sentinel.argtypes = [_p, _p, _sz, _i, _p, _p]
+        L.gsr_test_radix_sort_pairs_planned.restype = _i
+        L.gsr_test_radix_sort_pairs_planned.argtypes = [_p, _p, _sz, _i, _i, _p, _p]
         L.gsr_test_scan_scratch_bytes.restype = _sz
         L.gsr_test_scan_scratch_bytes.argtypes = [_sz]
         L.gsr_test_scan.restype = _i

@@ -71,6 +71,20 @@ class FusedAdam(torch.optim.Adam):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        h = self.begin_rows(skip=skip)
+        self.step_rows(h, 0, None)
+        self.end_rows(h)
+        return loss
+
+    # -- the step in row slices (multi-GPU: Adam on the rows whose all-reduce is done while the
+    # next slice's collective runs, gsr_amd.trainer.train_step_views) ---------------------------
+    @torch.no_grad()
+    def begin_rows(self, *, skip=None):
+        """Start a step applied in row ranges: the step counts advance once here and the
+        (betas, eps) batches are fixed; step_rows(h, a, b) then updates rows [a, b) of every
+        parameter (dim 0), end_rows(h) finishes.  The row ranges must cover every row exactly
+        once; the result is bitwise the one of step() (the update is elementwise)."""
+        self._resolve_pending()
         batches = {}
         for group in self.param_groups:
             beta1, beta2 = group["betas"]
@@ -99,10 +113,10 @@ class FusedAdam(torch.optim.Adam):
                 batches.setdefault(key, []).append(
                     (p, g, m, v, float(group["lr"]), float(group["weight_decay"]),
                      float(state["step"])))
-        L = _lib.load()
-        events, boxes, states = [], [], [self.state[it[0]] for its in batches.values() for it in its]
-        for (dev, beta1, beta2, eps), items in batches.items():
-            stream = _lib.raw_stream(dev)
+        skips = {}
+        for (dev, _, _, _) in batches:
+            if dev in skips:
+                continue
             box = self._mailbox.get(dev)
             if box is None:
                 box = torch.zeros(1, dtype=torch.int32, pin_memory=True)
@@ -112,36 +126,59 @@ class FusedAdam(torch.optim.Adam):
                 raise ValueError("FusedAdam.step: skip must be a float32 tensor on the parameters' device")
             if skip is None:
                 # ONE snapshot of the device's fault word for every launch of the step (chunks of
-                # MAX_TENSORS, (betas, eps) batches): a fault published between two launches
-                # cannot leave some tensors updated and others not
+                # MAX_TENSORS, (betas, eps) batches, row slices): a fault published between two
+                # launches cannot leave some rows updated and others not
                 slot = self._guard.get(dev)
                 if slot is None:
                     slot = torch.zeros(1, dtype=torch.float32, device=dev)
                     self._guard[dev] = slot
                 with _lib.on_device(dev):
                     _lib.step_guard(slot)
-                skip_ptr = slot.data_ptr()
+                skips[dev] = (slot.data_ptr(), box)
             else:
-                skip_ptr = skip.data_ptr()
-            for c in range(0, len(items), MAX_TENSORS):
-                chunk = items[c:c + MAX_TENSORS]
+                skips[dev] = (skip.data_ptr(), box)
+        states = [self.state[it[0]] for its in batches.values() for it in its]
+        return {"batches": batches, "skips": skips, "states": states}
+
+    @torch.no_grad()
+    def step_rows(self, h, a: int, b):
+        """Rows [a, b) of every parameter of the step begun by begin_rows (b None: to the end).
+        Issued on the current stream of each parameter's device."""
+        L = _lib.load()
+        for (dev, beta1, beta2, eps), items in h["batches"].items():
+            stream = _lib.raw_stream(dev)
+            skip_ptr, box = h["skips"][dev]
+            sel = []
+            for it in items:
+                rows = it[0].shape[0] if it[0].dim() else 1
+                row = it[0].numel() // max(1, rows)
+                lo, hi = a, rows if b is None else min(b, rows)
+                if hi > lo:
+                    sel.append((it, lo * row * 4, (hi - lo) * row))
+            for c in range(0, len(sel), MAX_TENSORS):
+                chunk = sel[c:c + MAX_TENSORS]
                 n = len(chunk)
-                ptrs = [(ctypes.c_void_p * n)(*[it[k].data_ptr() for it in chunk]) for k in range(4)]
-                numel = (ctypes.c_int64 * n)(*[it[0].numel() for it in chunk])
-                lr = (ctypes.c_double * n)(*[it[4] for it in chunk])
-                wd = (ctypes.c_double * n)(*[it[5] for it in chunk])
-                steps = (ctypes.c_double * n)(*[it[6] for it in chunk])
+                ptrs = [(ctypes.c_void_p * n)(*[s[0][k].data_ptr() + s[1] for s in chunk])
+                        for k in range(4)]
+                numel = (ctypes.c_int64 * n)(*[s[2] for s in chunk])
+                lr = (ctypes.c_double * n)(*[s[0][4] for s in chunk])
+                wd = (ctypes.c_double * n)(*[s[0][5] for s in chunk])
+                steps = (ctypes.c_double * n)(*[s[0][6] for s in chunk])
                 with _lib.on_device(dev):
                     rc = L.gsr_adam_step_guarded(n, ptrs[0], ptrs[1], ptrs[2], ptrs[3], numel, lr,
                                                  wd, steps, beta1, beta2, eps, skip_ptr,
                                                  box.data_ptr(), stream)
                 if rc != 0:
                     raise RuntimeError(f"gsr_adam_step failed with status {rc}")
+
+    def end_rows(self, h):
+        """Finish a step begun by begin_rows: its skip decision is read back by the next step."""
+        events, boxes = [], []
+        for dev, (_, box) in h["skips"].items():
             with _lib.on_device(dev):
                 ev = torch.cuda.Event()
                 ev.record(torch.cuda.current_stream(dev))
             events.append(ev)
             boxes.append(box)
         if events:
-            self._pending = (events, boxes, states, _lib.fault_resets())
-        return loss
+            self._pending = (events, boxes, h["states"], _lib.fault_resets())

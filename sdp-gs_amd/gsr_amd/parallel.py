@@ -101,11 +101,34 @@ class GradAllReducer:
     def attach_grads(self):
         """Zero the flat buffer and make every parameter's .grad a view into it (gradient as
         bucket view): the backward then accumulates straight into the all-reduce buffer and the
-        reduction needs no pack / unpack copies.  Call instead of zero_grad()."""
-        self._sync_layout()
-        self.flat.zero_()
+        reduction needs no pack / unpack copies.  Call instead of zero_grad().  After a step whose
+        row slices were zeroed behind the optimizer (zero_rows over every row, the next step's
+        prologue done slice by slice) only the guard slot is cleared."""
+        changed = self._sync_layout()
+        if changed or not getattr(self, "_prezeroed", False):
+            self.flat.zero_()
+        else:
+            self.guard.zero_()
+        self._prezeroed = False
+        self._zeroed_rows = 0
         for p, off in zip(self.params, self.offsets):
             p.grad = self.flat[off:off + p.numel()].view_as(p)
+
+    def zero_rows(self, a: int, b: int):
+        """Zero rows [a, b) of every parameter's slot in the flat buffer (on the current stream,
+        after the optimizer read them): the next step's gradient zeroing, one slice at a time.
+        Once the slices cover every row, the next attach_grads() skips its full-buffer fill."""
+        views = []
+        for i, p in enumerate(self.params):
+            _, lo, hi = self._range(p, a, b)
+            if hi > lo:
+                views.append(self.flat[lo:hi])
+        if views:
+            torch._foreach_zero_(views)
+        rows = self.params[0].shape[0] if self.params else 0
+        self._zeroed_rows = getattr(self, "_zeroed_rows", 0) + max(0, min(b, rows) - a)
+        same_rows = all(p.shape[0] == rows for p in self.params)
+        self._prezeroed = same_rows and self._zeroed_rows >= rows
 
     def _attached(self, p, off):
         g = p.grad
@@ -145,6 +168,8 @@ class GradAllReducer:
         """Start of a step's reduction: re-read the parameters (after a densification)."""
         self._sync_layout()
         self._works = []
+        self._slice_works = []  # (a, b, works) of reduce_row_slices_async, in issue order
+        self._guard_works = []
         self._done = set()
         self._guarded = False
 
@@ -165,6 +190,7 @@ class GradAllReducer:
         if not self._active():
             return
         spans = []
+        n0 = len(self._works)
         if guard:
             self._write_guard()
             spans.append((self.numel, self.numel + 1))
@@ -183,6 +209,8 @@ class GradAllReducer:
                 merged.append((lo, hi))
         for lo, hi in merged:
             self._issue(lo, hi)
+        if guard:
+            self._guard_works = self._works[n0:]
 
     def reduce_rows_async(self, p: torch.Tensor, a: int, b: int):
         """Start the all-reduce of rows [a, b) of p's gradient."""
@@ -210,6 +238,7 @@ class GradAllReducer:
             self._done.add(i)
         if not spans:
             return
+        n0 = len(self._works)
         if len(spans) > 1 and self._coalesce():
             from torch.distributed.distributed_c10d import _coalescing_manager
             group = self.group or dist.group.WORLD
@@ -217,9 +246,29 @@ class GradAllReducer:
                 for lo, hi in spans:
                     dist.all_reduce(self.flat[lo:hi], op=dist.ReduceOp.SUM, group=self.group)
             self._works.append(cm)
-            return
-        for lo, hi in spans:
-            self._issue(lo, hi)
+        else:
+            for lo, hi in spans:
+                self._issue(lo, hi)
+        self._slice_works.append((a, b, self._works[n0:]))
+
+    def each_reduced_slice(self, fn):
+        """For each row slice reduced by reduce_row_slices_async, in issue order: make the
+        current stream wait for that slice's collectives, then call fn(a, b) -- work issued there
+        (the optimizer on those rows) overlaps the next slices' collectives.  No-op at world
+        size 1 (fn is not called: the caller runs its unsliced path).  Returns whether it ran."""
+        if not self._active() or not self._slice_works:
+            return False
+        if self.average:
+            raise RuntimeError("each_reduced_slice: averaging reducers are not sliced")
+        if not getattr(self, "_guarded", False):
+            raise RuntimeError("each_reduced_slice: reduce the step's guard before its slices")
+        for w in self._guard_works:  # the skip decision first (every slice's optimizer reads it)
+            w.wait()
+        for a, b, works in self._slice_works:
+            for w in works:
+                w.wait()
+            fn(a, b)
+        return True
 
     def _coalesce(self) -> bool:
         """RCCL groups coalesced all-reduces into one launch; gloo issues them one by one."""

@@ -102,7 +102,7 @@ class ViewPipeline:
 
     def run_views(self, items: Iterable[T], fn: Callable[[List[T], List[torch.cuda.Stream]], R],
                   model=None, campos_of: Callable[[T], torch.Tensor] = lambda cam: cam.camera_center,
-                  reducer=None, chunks: int = 1):
+                  reducer=None, chunks: int = 1, after_slice: Optional[Callable] = None):
         """The step's views in ONE multi-view call: fn(items, streams) renders all of them at once
         (gaussian_renderer.render_views(items, ..., streams=streams): one host call issues every
         view's forward, autograd one call for every backward) and runs their backward; the views
@@ -117,7 +117,14 @@ class ViewPipeline:
         stream's allocator pool (never memory that an earlier chunk's backward still reads).  The
         grad-into-leaves backwards are ordered by diff_gaussian_rasterization; the row-sliced
         all-reduce (reducer) runs on the last chunk's per-Gaussian backward only.  Returns the
-        list of fn's results."""
+        list of fn's results.
+
+        after_slice(a, b) (with a reducer): called on the current stream for each row slice of
+        the per-Gaussian backward once every gradient of rows [a, b) -- SH included -- is reduced,
+        in row order, while the later slices' collectives are still running (the optimizer on
+        those rows: gsr_amd.trainer.train_step_views).  self.rows_done says whether it ran for
+        every row; when it did not (world size 1, no row slices, SH gradients deferred to a
+        flush) the caller runs its unsliced path."""
         self._check(reducer, model)
         items = list(items)
         main = torch.cuda.current_stream(self.device)
@@ -141,7 +148,8 @@ class ViewPipeline:
                 main.wait_stream(s)
             return out
 
-        out = self._step(items, issue, model, campos_of, reducer, sliced=True)
+        out = self._step(items, issue, model, campos_of, reducer, sliced=True,
+                         after_slice=after_slice)
         return out[0] if n == 1 else out
 
     def _check(self, reducer, model):
@@ -151,9 +159,10 @@ class ViewPipeline:
             raise ValueError("ViewPipeline.run: a reducer with defer_sh needs model= (the SH "
                              "leaves are reduced after the deferred flush)")
 
-    def _step(self, items, issue, model, campos_of, reducer, sliced=False):
+    def _step(self, items, issue, model, campos_of, reducer, sliced=False, after_slice=None):
         import diff_gaussian_rasterization as dgr
         main = torch.cuda.current_stream(self.device)
+        self.rows_done = False
         pre = contextlib.nullcontext()
         if self.precolor and model is not None and items:
             # one kernel ahead of the forward: colours and Jacobians of every view (round 4: the
@@ -190,14 +199,20 @@ class ViewPipeline:
             return getattr(defer, "fused", False)
 
         slices = contextlib.nullcontext()
+        guarded = [False]
         if reducer is not None and sliced and self.bwd_slices > 1:
             ids = {id(t) for t in sh_leaves}
             rest = [p for p in reducer.current_params() if id(p) not in ids]
-            slices = dgr.BackwardRowSlices(
-                self.device,
-                lambda a, b: reducer.reduce_row_slices_async(
-                    rest + (list(sh_leaves) if fused() else []), a, b),
-                self.bwd_slices)
+
+            def on_slice(a, b):
+                if not guarded[0]:
+                    # the step's fault snapshot ahead of the first slice: every forward of the
+                    # step is ordered before the backward, and the optimizer slices need the
+                    # reduced skip decision before their rows' collectives are done
+                    reducer.reduce_async([], guard=True)
+                    guarded[0] = True
+                reducer.reduce_row_slices_async(rest + (list(sh_leaves) if fused() else []), a, b)
+            slices = dgr.BackwardRowSlices(self.device, on_slice, self.bwd_slices)
             self._slices = slices
         with pre, defer:  # defer's exit: the SH gradients of all views, after the join
             try:
@@ -209,12 +224,16 @@ class ViewPipeline:
                 ids = set() if fused() else {id(t) for t in sh_leaves}
                 # (with the step's fault snapshot: every forward of the step is done)
                 if getattr(slices, "ran", False):  # already reduced slice by slice
-                    reducer.reduce_async([], guard=True)
+                    if not guarded[0]:
+                        reducer.reduce_async([], guard=True)
                 else:
                     reducer.reduce_async([p for p in reducer.current_params()
                                           if id(p) not in ids], guard=True)
         if reducer is not None:
             if sh_leaves and not defer.views_flushed and not fused():
                 reducer.reduce_async(sh_leaves)  # no view produced deferred SH gradients
+            if (after_slice is not None and getattr(slices, "ran", False)
+                    and (fused() or not sh_leaves)):
+                self.rows_done = reducer.each_reduced_slice(after_slice)
             reducer.wait()
         return out

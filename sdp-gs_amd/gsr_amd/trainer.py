@@ -168,8 +168,30 @@ def train_step_views(model, cams: Sequence, gt_images: Sequence[torch.Tensor],
                                                              pkg["radii"],
                                                              pkg["visibility_filter"])
             return [loss.detach() for loss in losses]
-        losses = pipeline.run_views(cams, all_views, model=model, reducer=reducer)
+        # Multi-GPU: the optimizer step in row slices, each as soon as its rows' all-reduce is
+        # done (overlapping the next slice's collective), followed by the next step's gradient
+        # zeroing of those rows -- unless this iteration densifies (the step then follows the
+        # densification, as in train.py:223-231)
+        from .optim import FusedAdam
+        opt = model.optimizer
+        h = None
+        if (reducer is not None and isinstance(opt, FusedAdam) and reducer._active()
+                and not reducer.average and not _densify_due(iteration, args)):
+            reducer.begin()  # the step's layout (also re-read by run_views)
+            h = opt.begin_rows(skip=reducer.guard)
+
+            def after_slice(a, b):
+                opt.step_rows(h, a, b)
+                reducer.zero_rows(a, b)
+        losses = pipeline.run_views(cams, all_views, model=model, reducer=reducer,
+                                    after_slice=None if h is None else after_slice)
         with torch.no_grad():
+            if h is not None:
+                if not pipeline.rows_done:  # no sliced reduction ran: the whole step now
+                    opt.step_rows(h, 0, None)
+                opt.end_rows(h)
+                _guard_step()
+                return losses
             if _densify_due(iteration, args):
                 allreduce_densification_stats(model.xyz_gradient_accum, model.denom,
                                                model.max_radii2D)

@@ -295,6 +295,63 @@ def test_radix_sort_sentinel_copy_pass(n, frac_culled):
     np.testing.assert_array_equal(gv[keep], order)
 
 
+@pytest.mark.parametrize("n,kind,frac_culled", [
+    (1_000_000, "narrow", 0.2),   # constant top byte: 3 of 4 passes run
+    (1_000_000, "wide", 0.0),     # every pass runs
+    (70_001, "const", 0.3),       # one distinct real key: only the last pass runs (a copy)
+    (4097, "narrow", 1.0),        # every key a sentinel
+    (2_000_003, "mid", 0.1)])     # constant second byte too: passes 0 and 3 skipped?
+def test_radix_sort_planned(n, kind, frac_culled):
+    """The depth sort's planned form (gsr_sort.hip radix_planned_kernel): passes whose digit is
+    constant over the non-sentinel keys do not run, the rest alternate so that the result lands
+    in the fixed output pair -- the same keys and values as the unplanned sort, bit for bit, and
+    the non-sentinel keys in stable sorted order."""
+    from gsr_amd import _lib
+    L = _lib.load()
+    rng = np.random.default_rng(n + len(kind))
+    if kind == "narrow":
+        keys = rng.uniform(3.0, 5.0, size=n).astype(np.float32).view(np.uint32) + 0
+    elif kind == "wide":
+        keys = rng.lognormal(1.0, 2.0, size=n).astype(np.float32).view(np.uint32) + 0
+    elif kind == "const":
+        keys = np.full(n, 0x40400000, np.uint32)
+    else:  # two middle bytes constant, low and high bytes varying
+        keys = (rng.integers(0, 256, size=n, dtype=np.uint32) |
+                (rng.integers(0, 64, size=n, dtype=np.uint32) << 24) | 0x00ABCD00).astype(np.uint32)
+    keys[: n // 5] = keys[0]
+    culled = rng.random(n) < frac_culled
+    keys[culled] = 0xFFFFFFFF
+    vals = np.arange(n, dtype=np.uint32)
+    scratch = torch.empty(int(L.gsr_test_sort_scratch_bytes(n)), dtype=torch.uint8, device="cuda")
+    out = []
+    for planned in (False, True):
+        k = torch.tensor(keys.view(np.int32), device="cuda")
+        v = torch.tensor(vals.view(np.int32), device="cuda")
+        st = torch.cuda.current_stream().cuda_stream
+        if planned:
+            rc = L.gsr_test_radix_sort_pairs_planned(k.data_ptr(), v.data_ptr(), n, 32, 1,
+                                                     scratch.data_ptr(), st)
+        else:
+            rc = L.gsr_test_radix_sort_pairs_sentinel(k.data_ptr(), v.data_ptr(), n, 32,
+                                                      scratch.data_ptr(), st)
+        _lib.check(rc)
+        out.append((k.cpu().numpy().view(np.uint32), v.cpu().numpy().view(np.uint32)))
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    np.testing.assert_array_equal(out[0][1], out[1][1])
+    gv = out[1][1]
+    keep = ~culled[gv]
+    order = np.argsort(keys, kind="stable")
+    np.testing.assert_array_equal(gv[keep], order[~culled[order]])
+    # without sentinels the planned sort is a full stable sort too
+    if frac_culled == 0.0:
+        k = torch.tensor(keys.view(np.int32), device="cuda")
+        v = torch.tensor(vals.view(np.int32), device="cuda")
+        _lib.check(L.gsr_test_radix_sort_pairs_planned(k.data_ptr(), v.data_ptr(), n, 32, 0,
+                                                       scratch.data_ptr(),
+                                                       torch.cuda.current_stream().cuda_stream))
+        np.testing.assert_array_equal(v.cpu().numpy().view(np.uint32), order)
+
+
 @pytest.mark.parametrize("n", [1, 2047, 2049, 5_000_001])
 def test_scan(n):
     from gsr_amd import _lib

@@ -120,3 +120,55 @@ def test_bucket_view_grads_equal_plain_step(world1, bucket_bytes, multi, chunks)
             assert dist.get_backend() == "nccl"
     finally:
         dgr.grad_into_leaves(prev)
+
+
+def test_sliced_adam_equals_serial_step(world1):
+    """the multi-GPU training step with the optimizer in row slices (FusedAdam
+    on rows [a, b) as soon as that slice's all-reduce is done, overlapping the next slice's
+    collective, then the next step's gradient zeroing of those rows) gives bitwise the
+    parameters, moments and step counts of the serial step (all-reduce, wait, one Adam step) --
+    over three iterations, the middle one a densification (which takes the serial order: densify,
+    then Adam).  Deterministic backward, so the two runs' gradients are bitwise equal."""
+    import diff_gaussian_rasterization as dgr
+    from gsr_amd import trainer
+    from gsr_amd.model import SplatModel
+    from gsr_amd.parallel import GradAllReducer
+    from gsr_amd.pipeline import ViewPipeline
+    from gsr_amd.synthetic import make_cameras, make_gaussians, training_targets
+    dev = torch.device("cuda", 0)
+    cams = [c.to(dev) for c in make_cameras(4, 320, 240, seed=5)]
+    gts, monos = training_targets(len(cams), 240, 320, seed=2, device=dev)
+    bg = torch.zeros(3, device=dev)
+    prev_leaves, prev_det = dgr.grad_into_leaves(), dgr.deterministic()
+    dgr.grad_into_leaves(True)
+    dgr.deterministic(True)
+    runs = []
+    try:
+        for slices in (1, 4):  # 1: no row slices -> the serial step
+            model = SplatModel(make_gaussians(20_000, sh_degree=3, seed=3), device=dev)
+            args = trainer.OptArgs()
+            trainer.make_trainable(model, args)
+            reducer = GradAllReducer(model, bucket_bytes=256 << 10)
+            reducer._active = lambda: True  # issue the collectives at world size 1 too
+            views = ViewPipeline(dev, depth=2, defer_sh=True, precolor=True, bwd_slices=slices)
+            gen = torch.Generator(device=dev).manual_seed(0)
+            sliced = []
+            for it in (599, 600, 601):  # 600: densification due (interval 100)
+                trainer.train_step_views(model, cams, gts, monos, bg, args, it, 2.78, views,
+                                         reducer=reducer, generator=gen, multi=True)
+                sliced.append(views.rows_done)
+            torch.cuda.synchronize()
+            state = [(p.detach().clone(), model.optimizer.state[p]["exp_avg"].clone(),
+                      model.optimizer.state[p]["exp_avg_sq"].clone(),
+                      float(model.optimizer.state[p]["step"]))
+                     for p in model.parameters()]
+            runs.append((state, sliced, model._xyz.shape[0]))
+    finally:
+        dgr.grad_into_leaves(prev_leaves)
+        dgr.deterministic(prev_det)
+    (ser, ser_sliced, n0), (got, got_sliced, n1) = runs
+    assert ser_sliced == [False, False, False]
+    assert got_sliced == [True, False, True]  # the densification iteration runs serially
+    assert n0 == n1
+    for (p, m, v, st), (q, m2, v2, st2) in zip(ser, got):
+        assert torch.equal(p, q) and torch.equal(m, m2) and torch.equal(v, v2) and st == st2
