@@ -321,28 +321,43 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
     const float* dp = &s_dp[wid][(lane >> 3) * kDpRow];
     float su = 0.f, sux = 0.f, suxx = 0.f;
     f2 cA = mk2(0.f, 0.f), cB = mk2(0.f, 0.f), cC = mk2(0.f, 0.f), cD = mk2(0.f, 0.f);
+    // The row's reads in batches of two pixels, each batch's reads issued together before its
+    // arithmetic (sched_barrier: the backend otherwise interleaves them one pixel at a time, one
+    // LDS round trip per pixel).  Batches of 4 need 142 VGPRs: 3 waves per SIMD, 1.086 ms against
+    // 0.947 (profiles/r05_bwd_ab.txt)
+    constexpr int kB = 2;
 #pragma unroll
-    for (int t = 0; t < 8; t++) {
-      // one ds_read_b64 per pixel (2 LDS cycles, conflict-free at kUwStride): the opaque offset
-      // keeps the backend from pairing two of them into a ds_read2_b64 (8 cycles)
-      uint32_t off = (uint32_t)(2 * t);
-      asm volatile("" : "+v"(off));
-      const f2 p = *reinterpret_cast<const f2*>(uw + off);  // (u, w) of pixel (t, row)
-      // both halves of the pixel's table entry as ds_read_b128 (4 cycles each; a 12-byte read
-      // of the second half would be a ds_read_b96, 8 cycles)
-      const float4 d0 = *reinterpret_cast<const float4*>(dp + 8 * t);
-      const float dx = r0.x - (float)(qx0 + (uint32_t)t);
-      su += p.x;
-      const float ux = p.x * dx;
-      sux += ux;
-      suxx = __builtin_fmaf(ux, dx, suxx);
-      cA = fma2(mk2(p.y, p.y), mk2(d0.x, d0.y), cA);
-      cB = fma2(mk2(p.y, p.y), mk2(d0.z, NC > 3 ? d0.w : 0.f), cB);
-      if (FEAT) {
-        const float4 d1 = *reinterpret_cast<const float4*>(dp + 8 * t + 4);
-        cC = fma2(mk2(p.y, p.y), mk2(d1.x, d1.y), cC);
-        cD = fma2(mk2(p.y, p.y), mk2(d1.z, d1.w), cD);  // d1.w = 0
+    for (int t0 = 0; t0 < 8; t0 += kB) {
+      f2 p[kB];
+      float4 d0[kB], d1[kB];
+#pragma unroll
+      for (int t = 0; t < kB; t++) {
+        // one ds_read_b64 per pixel (2 LDS cycles, conflict-free at kUwStride): the opaque
+        // offset keeps the backend from pairing two of them into a ds_read2_b64 (8 cycles)
+        uint32_t off = (uint32_t)(2 * (t0 + t));
+        asm volatile("" : "+v"(off));
+        p[t] = *reinterpret_cast<const f2*>(uw + off);  // (u, w) of pixel (t0 + t, row)
+        // both halves of the pixel's table entry as ds_read_b128 (4 cycles each; a 12-byte
+        // read of the second half would be a ds_read_b96, 8 cycles)
+        d0[t] = *reinterpret_cast<const float4*>(dp + 8 * (t0 + t));
+        if (FEAT) d1[t] = *reinterpret_cast<const float4*>(dp + 8 * (t0 + t) + 4);
       }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int t = 0; t < kB; t++) {
+        const float dx = r0.x - (float)(qx0 + (uint32_t)(t0 + t));
+        su += p[t].x;
+        const float ux = p[t].x * dx;
+        sux += ux;
+        suxx = __builtin_fmaf(ux, dx, suxx);
+        cA = fma2(mk2(p[t].y, p[t].y), mk2(d0[t].x, d0[t].y), cA);
+        cB = fma2(mk2(p[t].y, p[t].y), mk2(d0[t].z, NC > 3 ? d0[t].w : 0.f), cB);
+        if (FEAT) {
+          cC = fma2(mk2(p[t].y, p[t].y), mk2(d1[t].x, d1[t].y), cC);
+          cD = fma2(mk2(p[t].y, p[t].y), mk2(d1[t].z, d1[t].w), cD);  // d1.w = 0
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
     }
     // the 16 slots of the row as 8 pairs (slot order of kAcc*): (sum u dx, sum u dy),
     // (sum u dx dx, sum u dx dy), (sum u dy dy, sum u), (r, g), (b, depth), (f0, f1), (f2, -), -
