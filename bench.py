@@ -67,9 +67,22 @@ class Opt:
     include_feature = True
 
 
+def depth_sort_passes(xyz, cam, radii):
+    """Passes the planned depth sort runs for this view (gsr_sort.hip sort_plan_body): the 8-bit
+    digits of the visible Gaussians' depth keys (float bits of the view-space z) that are not
+    the same for every key; at least one."""
+    W = cam.world_view_transform
+    z = (xyz.detach() @ W[:3, 2] + W[3, 2]).float()
+    keys = z[radii > 0].contiguous().view(torch.int32).cpu().numpy().view(np.uint32)
+    if keys.size == 0:
+        return 1
+    n = sum(1 for p in range(4) if np.unique((keys >> (8 * p)) & 0xFF).size > 1)
+    return max(1, n)
+
+
 def algorithmic_bytes(stage, P, Pv, R, T, HW, D=3, C=8, tile_passes=2, acc=True, defer_sh=False,
                       precolor=False, views=6, launch_views=1, acc_in_blend=False,
-                      sh_in_bwd=False):
+                      sh_in_bwd=False, depth_passes=4):
     """Bytes each stage must move per launch.
     P Gaussians, Pv visible, R instances, T tiles, HW pixels, C blended channels (rgb, depth,
     alpha, feature x3), acc: the backward adds into existing gradients (read + write),
@@ -86,7 +99,7 @@ def algorithmic_bytes(stage, P, Pv, R, T, HW, D=3, C=8, tile_passes=2, acc=True,
         b = launch_views * per + once
     else:
         b = launch_views * _stage_bytes(stage, P, Pv, R, T, HW, D, C, tile_passes, acc, defer_sh,
-                                        precolor, views)
+                                        precolor, views, depth_passes)
     if acc_in_blend and stage in ("preprocess", "render_fwd"):
         b += launch_views * P * 64 * (1 if stage == "render_fwd" else -1)
     return b
@@ -113,7 +126,8 @@ def _model_split(stage, P, Pv, D, acc, defer_sh, precolor, sh_in_bwd=False):
     return per, once
 
 
-def _stage_bytes(stage, P, Pv, R, T, HW, D, C, tile_passes, acc, defer_sh, precolor, views):
+def _stage_bytes(stage, P, Pv, R, T, HW, D, C, tile_passes, acc, defer_sh, precolor, views,
+                 depth_passes=4):
     sh = 12 * (D + 1) ** 2
     sh_fwd = 13 if precolor else sh
     sh_bwd = 36 if (precolor and defer_sh) else sh
@@ -122,8 +136,9 @@ def _stage_bytes(stage, P, Pv, R, T, HW, D, C, tile_passes, acc, defer_sh, preco
         # means (all); scale, rot, opacity, SH, language (visible); radii/tiles/key/value (all);
         # 64-B splat record + clamp bits (visible), the 64-B gradient accumulator row it zeroes (all)
         "preprocess": P * 12 + Pv * (12 + 16 + 4 + sh_fwd + 12) + P * 16 + Pv * (64 + 1) + P * 64,
-        # one-sweep: digit totals read the keys once, each 8-bit pass reads and writes key+value
-        "depth_sort": P * 4 + 4 * P * 16,
+        # one-sweep: digit totals read the keys once, each 8-bit pass that runs (the planned
+        # sort skips constant digits) reads and writes key+value, the last gathers the tile count
+        "depth_sort": P * 4 + depth_passes * P * 16 + P * 4,
         "scan": P * 12,
         # offsets (all), order + 48-B record gather (non-empty), R (tile, id) pairs
         "duplicate": P * 8 + Pv * (4 + 48) + R * 8,
@@ -268,6 +283,7 @@ def main():
     defer_sh = not args.no_defer_sh and not args.autograd_grads
     views = ViewPipeline(dev, depth=streams, defer_sh=defer_sh, precolor=not args.no_precolor)
     stats["R_ref"] = []
+    stats["depth_passes"] = []
     step_no = [0]
 
     def one_view(cam, record):
@@ -314,10 +330,11 @@ def main():
             [dimg.expand(V, *dimg.shape), ddep.expand(V, *ddep.shape),
              dfeat.expand(V, *dfeat.shape)])
         if record:
-            for (nr, ni), pkg in zip(dgr.LAST_STATS["view_counts"], pkgs):
+            for (nr, ni), pkg, cam in zip(dgr.LAST_STATS["view_counts"], pkgs, cams):
                 stats["R"].append(ni)
                 stats["R_ref"].append(nr)
                 stats["Pv"].append(int(pkg["visibility_filter"].sum()))
+                stats["depth_passes"].append(depth_sort_passes(model._xyz, cam, pkg["radii"]))
 
     def view_forward(cam):
         pkg = render(cam, model, pipe, bg, opt)
@@ -399,6 +416,7 @@ def main():
     R = float(np.mean(stats["R"]))
     R_ref = float(np.mean(stats["R_ref"]))
     Pv = float(np.mean(stats["Pv"]))
+    depth_passes = float(np.mean(stats["depth_passes"])) if stats["depth_passes"] else 4.0
     T = ((W + 15) // 16) * ((H + 15) // 16)
     HW = W * H
     kernels = {}
@@ -423,7 +441,7 @@ def main():
         b = algorithmic_bytes(name, P, Pv, R, T, HW, D=deg, acc=not args.autograd_grads,
                               defer_sh=defer_sh, precolor=not args.no_precolor,
                               views=len(my_cams), launch_views=vpl, acc_in_blend=acc_in_blend,
-                              sh_in_bwd=sh_in_bwd)
+                              sh_in_bwd=sh_in_bwd, depth_passes=depth_passes)
         k = {"avg_ms": round(avg_ms, 4), "calls": int(calls), "bytes": int(b),
              "views_per_launch": vpl, "gbs": round(b / (avg_ms * 1e-3) / 1e9, 1)}
         if name in ("render_fwd", "render_bwd"):
@@ -527,7 +545,8 @@ def main():
                        # num_rendered: the reference's count (boundary return value, full
                        # 3-sigma rectangles); instances: those binned after the exact tile cull
                        "num_rendered_mean": int(R_ref), "instances_mean": int(R),
-                       "visible_mean": int(Pv), "tiles": T},
+                       "visible_mean": int(Pv), "tiles": T,
+                       "depth_sort_passes_mean": round(depth_passes, 2)},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "kernels": kernels,
@@ -655,9 +674,11 @@ def extra_legs(args, model, step_cams, pool, n_views, views, reducer, timed_regi
 
     def train_step():
         cams = next_cams()
+        # (N > 1: the next step's colour pre-pass is issued slice by slice behind the optimizer)
         trainer.train_step_views(model, cams, [gts[c.uid] for c in cams],
                                  [monos[c.uid] for c in cams], bg, targs, it[0], extent, views,
-                                 reducer=reducer, multi=multi_issue)
+                                 reducer=reducer, multi=multi_issue,
+                                 next_cams=step_cams(k_step[0]))
         it[0] += 1
     for _ in range(args.warmup):
         train_step()

@@ -225,6 +225,13 @@ int gsr_rasterize_gaussians_fused_backward_deferred(
 int gsr_sh_precolor(int P, int M, int degree, const float* means3D, const float* features_dc,
                     const float* features_rest, int nviews, const float* const* campos,
                     float* const* color, uint8_t* const* clamped, float* const* jac, void* stream);
+/* gsr_sh_precolor for the Gaussian rows [row0, row1) only (outputs stay planes of P): the next
+ * step's pre-pass issued slice by slice behind the optimizer's row slices (a multi-GPU step,
+ * gsr_amd.trainer.train_step_views).  Rows outside the range are not touched. */
+int gsr_sh_precolor_rows(int P, int row0, int row1, int M, int degree, const float* means3D,
+                         const float* features_dc, const float* features_rest, int nviews,
+                         const float* const* campos, float* const* color,
+                         uint8_t* const* clamped, float* const* jac, void* stream);
 
 /* gsr_rasterize_gaussians_fused with the SH colour and clamp bits of this view taken from
  * gsr_sh_precolor (identical outputs; the SH rows are not read). */

@@ -1567,11 +1567,21 @@ int gsr_sh_precolor(int P, int M, int degree, const float* means3D, const float*
                     const float* features_rest, int nviews, const float* const* campos,
                     float* const* color, uint8_t* const* clamped, float* const* jac,
                     void* stream_ptr) {
+  return gsr_sh_precolor_rows(P, 0, P, M, degree, means3D, features_dc, features_rest, nviews,
+                              campos, color, clamped, jac, stream_ptr);
+}
+
+int gsr_sh_precolor_rows(int P, int row0, int row1, int M, int degree, const float* means3D,
+                         const float* features_dc, const float* features_rest, int nviews,
+                         const float* const* campos, float* const* color,
+                         uint8_t* const* clamped, float* const* jac, void* stream_ptr) {
   g_err.clear();
   hipStream_t stream = (hipStream_t)stream_ptr;
   const int debug = 0;
   if (P < 0 || nviews < 0) return fail(GSR_ERR_ARGUMENT, "invalid sizes");
-  if (P == 0 || nviews == 0) return GSR_OK;
+  if (row0 < 0 || row1 < row0 || row1 > P)
+    return fail(GSR_ERR_ARGUMENT, "rows [%d, %d) outside [0, %d)", row0, row1, P);
+  if (P == 0 || nviews == 0 || row1 == row0) return GSR_OK;
   if (M < 1 || M > 16 || degree < 0 || degree > 3 || (degree + 1) * (degree + 1) > M)
     return fail(GSR_ERR_ARGUMENT, "invalid sh degree %d for M = %d", degree, M);
   if (!means3D || !features_dc || (M > 1 && !features_rest) || !campos)
@@ -1584,6 +1594,7 @@ int gsr_sh_precolor(int P, int M, int degree, const float* means3D, const float*
   for (int v0 = 0; v0 < nviews; v0 += kShFlushMaxViewsFwd) {
     PrecolorArgs a{};
     a.P = P; a.M = M; a.D = degree; a.means3D = means3D; a.sh_dc = features_dc;
+    a.row0 = (uint32_t)row0; a.row1 = (uint32_t)row1;
     a.sh_rest = features_rest;
     a.nviews = nviews - v0 < kShFlushMaxViewsFwd ? nviews - v0 : kShFlushMaxViewsFwd;
     for (int v = 0; v < a.nviews; v++) {

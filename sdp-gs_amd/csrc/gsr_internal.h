@@ -298,6 +298,7 @@ static_assert(sizeof(PreViews) <= 4096, "kernel argument size");
 hipError_t launch_preprocess_views(const PreArgs* views, int V, hipStream_t s);
 struct PrecolorArgs {
   int P, M, D, nviews;
+  uint32_t row0, row1;  // the Gaussian rows [row0, row1) of this launch (outputs: planes of P)
   const float *means3D, *sh_dc, *sh_rest;
   const float* campos[kShFlushMaxViewsFwd];
   float* color[kShFlushMaxViewsFwd];     // [3][P] (planar)

@@ -325,8 +325,8 @@ __global__ __launch_bounds__(kPcThreads) void sh_precolor_kernel(PrecolorArgs a)
   __shared__ float4 s_sh4[kPcThreads * kShMaxFloats / 4];
   __shared__ uint8_t s_live[kPcThreads];
   float* s_sh = reinterpret_cast<float*>(s_sh4);
-  const int base = (int)(blockIdx.x * kPcThreads);
-  const int n = min(kPcThreads, a.P - base);
+  const int base = (int)(a.row0 + blockIdx.x * kPcThreads);
+  const int n = min(kPcThreads, (int)a.row1 - base);
   const int t = (int)threadIdx.x;
   const size_t i = (size_t)base + t;
   s_live[t] = t < n;
@@ -418,8 +418,9 @@ hipError_t launch_preprocess_views(const PreArgs* views, int V, hipStream_t s) {
 }
 
 hipError_t launch_sh_precolor(const PrecolorArgs& a, hipStream_t s) {
-  if (a.P == 0 || a.nviews <= 0) return hipSuccess;
-  const dim3 grid((a.P + kPcThreads - 1) / kPcThreads);
+  if (a.P == 0 || a.nviews <= 0 || a.row1 <= a.row0) return hipSuccess;
+  if (a.row1 > (uint32_t)a.P) return hipErrorInvalidValue;
+  const dim3 grid((a.row1 - a.row0 + kPcThreads - 1) / kPcThreads);
   if (a.color[0] && a.jac[0])
     hipLaunchKernelGGL((sh_precolor_kernel<true, true>), grid, dim3(kPcThreads), 0, s, a);
   else if (a.color[0])

@@ -771,19 +771,19 @@ class ShPrecolor:
     Outputs are identical (the same device functions, gsr_sh.h)."""
 
     def __init__(self, means3D, features_dc, features_rest, degree, campos_list, buffers=None,
-                 jac_stream=None):
+                 rows: bool = False):
         """buffers: optional list of (colour [3,P], clamp [P] u8, Jacobian [9,P]) per camera to
         reuse (written on the current stream, so every earlier reader must be ordered before it).
         Colour and Jacobian are planar (include/gsr.h gsr_sh_precolor).
 
-        jac_stream: the Jacobians (needed by the backward only) are computed there, after the
-        current stream's work so far, while the colours (needed before the forward) are computed
-        on the current stream -- the step's forward starts after the colour part alone; the
-        backwards that read a Jacobian wait for `jac_event`."""
+        rows: nothing is computed here; compute_rows(a, b) fills rows [a, b) (the next step's
+        pre-pass issued slice by slice behind the optimizer, gsr_amd.trainer), and `complete`
+        says when every row has been filled."""
         self.device = means3D.device
         self.keys = (means3D.data_ptr(), features_dc.data_ptr(),
                      features_rest.data_ptr() if features_rest is not None else 0, int(degree))
         P = int(means3D.shape[0])
+        self.P = P
         self.M = 1 + (features_rest.numel() // (3 * P) if features_rest is not None and P else 0)
         fopts = dict(dtype=torch.float32, device=self.device)
         self.views = {}
@@ -798,35 +798,35 @@ class ShPrecolor:
         self.buffers = bufs
         self.jac_event = None
         n = len(cams)
+        self._m3c = means3D.contiguous()
+        self._args = None
+        self._done_rows = 0
         if n and P:
             arr = lambda xs: (_lib.ctypes.c_void_p * n)(*[x.data_ptr() for x in xs])  # noqa: E731
-            m3c = means3D.contiguous()
-            L = _lib.load()
-            head = (P, self.M, int(degree), _ptr(m3c), _ptr(features_dc), _ptr(features_rest), n,
-                    arr(cams))
-            cols = (arr([b[0] for b in bufs]), arr([b[1] for b in bufs]))
-            jacs = arr([b[2] for b in bufs])
-            with _lib.on_device(self.device):
-                if jac_stream is None:
-                    rc = L.gsr_sh_precolor(*head, *cols, jacs, _lib.raw_stream(self.device))
-                else:
-                    rc = L.gsr_sh_precolor(*head, *cols, None, _lib.raw_stream(self.device))
-                    if rc == 0:
-                        # after the current stream's work so far: the previous step's readers
-                        # of these buffers, and the inputs
-                        jac_stream.wait_stream(torch.cuda.current_stream(self.device))
-                        rc = L.gsr_sh_precolor(*head, None, None, jacs, jac_stream.cuda_stream)
-                        self.jac_event = torch.cuda.Event()
-                        self.jac_event.record(jac_stream)
-                        for b in bufs:
-                            b[2].record_stream(jac_stream)
-                        m3c.record_stream(jac_stream)
-                        for c in cams:
-                            c.record_stream(jac_stream)
-            _lib.check(rc)
+            self._args = ((self.M, int(degree), _ptr(self._m3c), _ptr(features_dc),
+                           _ptr(features_rest), n, arr(cams)),
+                          (arr([b[0] for b in bufs]), arr([b[1] for b in bufs]),
+                           arr([b[2] for b in bufs])))
+            if not rows:
+                self.compute_rows(0, P)
         for c, b in zip(cams, bufs):
             self.views[c.data_ptr()] = b
         self._campos = cams  # keep the keyed tensors alive
+
+    @property
+    def complete(self) -> bool:
+        return self._args is None or self._done_rows >= self.P
+
+    def compute_rows(self, a: int, b: int):
+        """The pre-pass of rows [a, b) of every camera, on the current stream."""
+        if self._args is None or b <= a:
+            return
+        head, outs = self._args
+        with _lib.on_device(self.device):
+            rc = _lib.load().gsr_sh_precolor_rows(self.P, int(a), int(min(b, self.P)), *head,
+                                                  *outs, _lib.raw_stream(self.device))
+        _lib.check(rc)
+        self._done_rows += max(0, min(b, self.P) - a)
 
     def lookup(self, campos, m3, dc, rest, degree, M):
         keys = (m3.data_ptr(), dc.data_ptr(), rest.data_ptr() if rest is not None else 0,

@@ -202,6 +202,8 @@ def load():
         L.gsr_sh_precolor.restype = _i
         L.gsr_sh_precolor.argtypes = [_i, _i, _i, _p, _p, _p, _i, ctypes.POINTER(_p),
                                       ctypes.POINTER(_p), ctypes.POINTER(_p), ctypes.POINTER(_p), _p]
+        L.gsr_sh_precolor_rows.restype = _i
+        L.gsr_sh_precolor_rows.argtypes = [_i, _i, _i] + list(L.gsr_sh_precolor.argtypes[1:])
         L.gsr_sh_grad_flush.restype = _i
         L.gsr_sh_grad_flush.argtypes = [_i, _i, _i, _p, _i, ctypes.POINTER(_p),
                                         ctypes.POINTER(_p), ctypes.c_int64, _p, _p, _i, _p]

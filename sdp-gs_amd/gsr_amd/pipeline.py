@@ -54,6 +54,8 @@ class ViewPipeline:
         self._pre_bufs = None  # the pre-pass's per-view buffers, reused step after step
         self.side = [torch.cuda.Stream(device=self.device) for _ in range(depth - 1)]
         self._slices = None  # the step's BackwardRowSlices while run_views issues
+        self._prepared = None  # (campos ptrs, ShPrecolor) of the next step, filled slice by slice
+        self.rows_done = False
 
     def run(self, items: Iterable[T], fn: Callable[[T], R], model=None,
             campos_of: Callable[[T], torch.Tensor] = lambda cam: cam.camera_center,
@@ -152,6 +154,22 @@ class ViewPipeline:
                          after_slice=after_slice)
         return out[0] if n == 1 else out
 
+    def prepare_next(self, model, items, campos_of=lambda cam: cam.camera_center):
+        """The next step's colour pre-pass (SH colour, clamp bits, colour Jacobian of `items`'
+        cameras), to be filled row slice by row slice: returns fill(a, b), which issues rows
+        [a, b) on the current stream -- after the optimizer updated those rows.  The next run() /
+        run_views() over the same cameras uses it when every row was filled and the model's
+        tensors are the same (no densification in between); otherwise it computes its own.
+        Issue every fill after this step's forwards and backwards (the buffers are this step's)."""
+        import diff_gaussian_rasterization as dgr
+        if not (self.precolor and items):
+            return lambda a, b: None
+        campos = [campos_of(it) for it in items]
+        pre = dgr.ShPrecolor(model._xyz, model._features_dc, model._features_rest,
+                             model.active_sh_degree, campos, buffers=self._pre_bufs, rows=True)
+        self._prepared = ([c.data_ptr() for c in campos], pre)
+        return pre.compute_rows
+
     def _check(self, reducer, model):
         if reducer is not None and self.defer_sh and model is None:
             # the early all-reduce must leave out the SH leaves, whose deferred gradients are only
@@ -164,13 +182,20 @@ class ViewPipeline:
         main = torch.cuda.current_stream(self.device)
         self.rows_done = False
         pre = contextlib.nullcontext()
+        prepared, self._prepared = self._prepared, None
         if self.precolor and model is not None and items:
-            # one kernel ahead of the forward: colours and Jacobians of every view (round 4: the
-            # Jacobians split onto a side stream measured slower, profiles/r04_pipeline_ab.txt --
-            # the forward's head is latency-bound, not the pass)
-            pre = dgr.ShPrecolor(model._xyz, model._features_dc, model._features_rest,
-                                 model.active_sh_degree, [campos_of(it) for it in items],
-                                 buffers=self._pre_bufs)
+            campos = [campos_of(it) for it in items]
+            if (prepared is not None and prepared[1].complete
+                    and prepared[0] == [c.data_ptr() for c in campos]
+                    and prepared[1].lookup(campos[0], model._xyz, model._features_dc,
+                                           model._features_rest, model.active_sh_degree,
+                                           prepared[1].M) is not None):
+                # filled slice by slice behind the previous step's optimizer (prepare_next)
+                pre = prepared[1]
+            else:
+                # one kernel ahead of the forward: colours and Jacobians of every view
+                pre = dgr.ShPrecolor(model._xyz, model._features_dc, model._features_rest,
+                                     model.active_sh_degree, campos, buffers=self._pre_bufs)
             # reuse next step: its pre-pass is issued on this stream after this step's join
             self._pre_bufs = pre.buffers
         for s in self.side:

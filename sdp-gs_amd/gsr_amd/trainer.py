@@ -123,14 +123,19 @@ def train_iteration(model, cam, gt_image, depth_mono, bg, args: OptArgs, iterati
 def train_step_views(model, cams: Sequence, gt_images: Sequence[torch.Tensor],
                      depth_monos: Sequence[Optional[torch.Tensor]], bg, args: OptArgs,
                      iteration: int, extent: float, pipeline, reducer=None, pipe=None,
-                     generator=None, multi: bool = True) -> List[torch.Tensor]:
+                     generator=None, multi: bool = True,
+                     next_cams: Optional[Sequence] = None) -> List[torch.Tensor]:
     """The batched iteration: every camera's render + loss + backward + statistics (gradients
     summed over the views), the gradient all-reduce across ranks (reducer, overlapped with the
     step's tail), densification when due (statistics summed / maxed across ranks first,
     identical generator on every rank), one optimizer step.  multi: all views in one multi-view
     call (gaussian_renderer.render_views: one host call for the forwards, one for the backwards;
     the per-view losses are back-propagated together); else view by view on the pipeline's
-    streams (render() per view, lagged)."""
+    streams (render() per view, lagged).
+
+    Multi-GPU (reducer, multi): the optimizer runs in row slices behind the sliced all-reduce,
+    each slice followed by the next step's prologue for those rows -- the gradient zeroing and,
+    given next_cams (the next step's cameras), its colour pre-pass."""
     from gaussian_renderer import render, render_views
     from .parallel import allreduce_densification_stats
     pipe = pipe or _Pipe()
@@ -179,10 +184,16 @@ def train_step_views(model, cams: Sequence, gt_images: Sequence[torch.Tensor],
                 and not reducer.average and not _densify_due(iteration, args)):
             reducer.begin()  # the step's layout (also re-read by run_views)
             h = opt.begin_rows(skip=reducer.guard)
+            fill = None
 
             def after_slice(a, b):
+                nonlocal fill
                 opt.step_rows(h, a, b)
                 reducer.zero_rows(a, b)
+                if next_cams is not None:
+                    if fill is None:  # this step's forwards and backwards are issued by now
+                        fill = pipeline.prepare_next(model, list(next_cams))
+                    fill(a, b)
         losses = pipeline.run_views(cams, all_views, model=model, reducer=reducer,
                                     after_slice=None if h is None else after_slice)
         with torch.no_grad():

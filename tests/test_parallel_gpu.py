@@ -125,7 +125,8 @@ def test_bucket_view_grads_equal_plain_step(world1, bucket_bytes, multi, chunks)
 def test_sliced_adam_equals_serial_step(world1):
     """the multi-GPU training step with the optimizer in row slices (FusedAdam
     on rows [a, b) as soon as that slice's all-reduce is done, overlapping the next slice's
-    collective, then the next step's gradient zeroing of those rows) gives bitwise the
+    collective, then the next step's prologue for those rows: its gradient zeroing and its colour
+    pre-pass, used by the next step) gives bitwise the
     parameters, moments and step counts of the serial step (all-reduce, wait, one Adam step) --
     over three iterations, the middle one a densification (which takes the serial order: densify,
     then Adam).  Deterministic backward, so the two runs' gradients are bitwise equal."""
@@ -155,8 +156,11 @@ def test_sliced_adam_equals_serial_step(world1):
             sliced = []
             for it in (599, 600, 601):  # 600: densification due (interval 100)
                 trainer.train_step_views(model, cams, gts, monos, bg, args, it, 2.78, views,
-                                         reducer=reducer, generator=gen, multi=True)
-                sliced.append(views.rows_done)
+                                         reducer=reducer, generator=gen, multi=True,
+                                         next_cams=cams)
+                # the next step's colour pre-pass, filled slice by slice behind the optimizer
+                prep = views._prepared
+                sliced.append((views.rows_done, prep is not None and prep[1].complete))
             torch.cuda.synchronize()
             state = [(p.detach().clone(), model.optimizer.state[p]["exp_avg"].clone(),
                       model.optimizer.state[p]["exp_avg_sq"].clone(),
@@ -167,8 +171,9 @@ def test_sliced_adam_equals_serial_step(world1):
         dgr.grad_into_leaves(prev_leaves)
         dgr.deterministic(prev_det)
     (ser, ser_sliced, n0), (got, got_sliced, n1) = runs
-    assert ser_sliced == [False, False, False]
-    assert got_sliced == [True, False, True]  # the densification iteration runs serially
+    assert ser_sliced == [(False, False)] * 3
+    # the densification iteration runs serially (no sliced optimizer, no prepared pre-pass)
+    assert got_sliced == [(True, True), (False, False), (True, True)]
     assert n0 == n1
     for (p, m, v, st), (q, m2, v2, st2) in zip(ser, got):
         assert torch.equal(p, q) and torch.equal(m, m2) and torch.equal(v, v2) and st == st2
