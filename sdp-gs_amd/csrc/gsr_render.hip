@@ -201,8 +201,10 @@ __device__ __forceinline__ f2 swap16_add(f2 p, f2 q) {
 // Per contributing (wave, entry): ~40 VALU in phase 1 and ~12 in phase 2, against ~105 for the
 // per-entry 64-lane butterfly this replaces.
 // ================================================================================================
-constexpr int kBatch = 128;          // splat records staged per batch (threads 0..127 stage)
-constexpr int kSlots = 8;            // phase-2 width: splats summed per pass
+constexpr int kBatch = 64;           // splat records staged per batch (wave 0 stages)
+// phase-2 width: splats summed per pass (phase-2 lanes j = l & 7; slot 7 unused, so that the
+// wave-private accumulator rows fit the LDS of 4 workgroups per CU)
+constexpr int kSlots = 7;
 constexpr int kAccRow = 13;          // LDS accumulator row: the 13 gradient values (odd: conflict-free)
 // phase-2 slot stride in dwords: 64 (u, w) pairs + 2 pad dwords, so the eight slots of a phase-2
 // read start on banks 2j (ds_read_b64: 32 lanes x 2 banks, all distinct)
@@ -222,8 +224,9 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
   __shared__ float4 s_c0[kBatch];
   __shared__ float4 s_c1[FEAT ? kBatch : 1];
   __shared__ uint32_t s_gid[kBatch];
-  // per batch entry: its 13 gradient values (DET: one row per wave, summed in wave order)
-  __shared__ float s_acc[(DET ? 4 : 1) * kBatch * kAccRow];
+  // per batch entry and wave: its 13 gradient values, stored (not added: LDS float atomics cost
+  // ~1 cycle per lane, profiles/r05_bwd_ab.txt) and summed over the waves in wave order
+  __shared__ float s_acc[4 * kBatch * kAccRow];
   __shared__ uint8_t s_mask[kBatch];
   __shared__ uint8_t s_list[kThreads / 64][kBatch];
   __shared__ __attribute__((aligned(16))) float s_uw[kThreads / 64][kSlots * kUwStride];
@@ -308,7 +311,7 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
   const uint32_t qx0 = tx * kTile + (uint32_t)(wid & 1) * 8u;
   const float pfy_row = (float)(ty * kTile + (uint32_t)(wid >> 1) * 8u + (uint32_t)(lane >> 3));
 
-  for (int k = (int)threadIdx.x; k < (DET ? 4 : 1) * kBatch * kAccRow; k += kThreads) s_acc[k] = 0.0f;
+  for (int k = (int)threadIdx.x; k < 4 * kBatch * kAccRow; k += kThreads) s_acc[k] = 0.0f;
 
   // Phase 2 over the first `ns` slots (wave-uniform, 1..kSlots).  slotv: lane l holds the batch
   // index of slot l & 7 (set in phase 1, no LDS round trip).
@@ -386,17 +389,12 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
     // pair index held: b3 + 2 b4' + 4 b5' (b4', b5' corrected by the probed swap orientation)
     const int pr = ((lane >> 3) & 1) + 2 * (((lane >> 4) & 1) ^ (int)swap_orient.flip16) +
                    4 * (((lane >> 5) & 1) ^ (int)swap_orient.flip32);
+    // a batch entry is in a wave's list at most once: its row of this wave is written once
     if ((uint32_t)j < ns) {
       const int k0 = 2 * pr;
-      if (DET) {
-        float* row = &s_acc[(wid * kBatch + bj) * kAccRow];
-        if (k0 < kAccRow) row[k0] = w.x;
-        if (k0 + 1 < kAccRow) row[k0 + 1] = w.y;
-      } else {
-        float* row = &s_acc[bj * kAccRow];
-        if (k0 < kAccRow && w.x != 0.0f) atomicAdd(&row[k0], w.x);
-        if (k0 + 1 < kAccRow && w.y != 0.0f) atomicAdd(&row[k0 + 1], w.y);
-      }
+      float* row = &s_acc[(wid * kBatch + bj) * kAccRow];
+      if (k0 < kAccRow) row[k0] = w.x;
+      if (k0 + 1 < kAccRow) row[k0 + 1] = w.y;
     }
   };
 
@@ -543,12 +541,11 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
       const float4 r0 = s_r0[threadIdx.x];
       const float2 r1 = s_r1[threadIdx.x];
       float* row = s_acc + threadIdx.x * kAccRow;
-      if (DET) {  // the four waves' rows, added in wave order, into wave 0's row
+      // the four waves' rows, added in wave order, into wave 0's row
 #pragma unroll
-        for (int k = 0; k < kAccRow; k++)
-          row[k] = ((row[k] + row[kBatch * kAccRow + k]) + row[2 * kBatch * kAccRow + k]) +
-                   row[3 * kBatch * kAccRow + k];
-      }
+      for (int k = 0; k < kAccRow; k++)
+        row[k] = ((row[k] + row[kBatch * kAccRow + k]) + row[2 * kBatch * kAccRow + k]) +
+                 row[3 * kBatch * kAccRow + k];
       const float sx = row[kAccMx], sy = row[kAccMy];
       const float o = r1.y;
       row[kAccMx] = -(o * (r0.z * sx + r0.w * sy)) * ddelx_dx;
@@ -559,7 +556,7 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
     }
     __syncthreads();
     // flush: lane l of wave-instruction `it` handles splat (it*16 + tid/16), slot tid%16
-#pragma unroll 4
+#pragma unroll 1
     for (int it = 0; it < kBatch * kAccFloats / kThreads; it++) {
       const uint32_t jj = (uint32_t)it * (kThreads / kAccFloats) + (threadIdx.x >> 4);
       const int k = (int)(threadIdx.x & 15);
@@ -574,10 +571,10 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
             for (int w = 0; w < 4; w++) s_acc[(w * kBatch + jj) * kAccRow + k] = 0.0f;
         } else {
           const float v = held ? s_acc[jj * kAccRow + k] : 0.0f;
-          if (v != 0.0f) {
-            atomicAdd(&a.acc[(size_t)s_gid[jj] * kAccFloats + k], v);
-            s_acc[jj * kAccRow + k] = 0.0f;
-          }
+          if (v != 0.0f) atomicAdd(&a.acc[(size_t)s_gid[jj] * kAccFloats + k], v);
+          if (held)
+#pragma unroll
+            for (int w = 0; w < 4; w++) s_acc[(w * kBatch + jj) * kAccRow + k] = 0.0f;
         }
       }
     }
