@@ -223,7 +223,7 @@ def main():
                          "consecutive chunks, each forward + backward)")
     ap.add_argument("--no-precolor", action="store_true",
                     help="each view evaluates its SH colour itself instead of the step's pre-pass")
-    ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_r04.json"))
+    ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_r05.json"))
     ap.add_argument("--no-extra-legs", action="store_true",
                     help="skip the train-step, reference-cadence and reference-API legs")
     ap.add_argument("--cpu-threads", type=int, default=0,
@@ -476,6 +476,10 @@ def main():
             if v is not None and pmc.get("workload") == args.workload:
                 # SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES: the blend kernels are VALU/latency-bound
                 roofline["valu_active_per_wave_cycle_pmc"] = v
+            lanes = pk.get("valu_exec_lane_frac")
+            if lanes is not None and pmc.get("workload") == args.workload:
+                # SQ_THREAD_CYCLES_VALU / (64 SQ_ACTIVE_INST_VALU): lanes enabled per VALU cycle
+                roofline["valu_exec_lane_frac_pmc"] = lanes
             n_valu = pk.get("counters", {}).get("SQ_INSTS_VALU")
             if n_valu and pmc.get("workload") == args.workload:
                 # VALU issue roofline: CDNA4's SIMDs are 32 lanes wide, so a SIMD issues one wave64
@@ -488,10 +492,9 @@ def main():
         if dom == "render_bwd":
             # the flush's float atomics: at most one per (instance, gradient value) -- 13 values x
             # 4 B per binned instance -- against the ~1.3 TB/s chip-wide rate of memory-side float
-            # atomics (MI355X_MICROARCH.md "Global float atomics"); an upper bound (rows of
-            # instances behind a tile's last contributor and zero values are not flushed).  A
-            # plain-store build of the same flush ran equally fast, so they are not
-            # what bounds the kernel
+            # atomics (MI355X_MICROARCH.md "Global float atomics"); an upper bound per (splat,
+            # tile) (rows of instances behind a tile's last contributor and zero values are not
+            # flushed; each wave flushes its own sums, up to 4 per (splat, tile))
             ab = 13 * 4 * R * kd["views_per_launch"]
             roofline["atomic_bytes_upper"] = int(ab)
             roofline["atomic_frac_upper"] = round(ab / (kd["avg_ms"] * 1e-3) / 1.3e12, 4)
