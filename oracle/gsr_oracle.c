@@ -310,11 +310,15 @@ struct oracle_state {
     unsigned* lock_nc;
     uint64_t* lock_offs;
     unsigned* lock_words;
+    /* colour-clamp lock (oracle_use_clamp): another evaluation's SH colour clamp bits [P*3]
+     * replace this build's own result < 0 tests (forward.cu:67-69; the backward's dL/dRGB mask,
+     * backward.cu:390-391).  NULL = no lock. */
+    unsigned char* clamp_lock;
 };
 
 /* forward.cu:20-71 computeColorFromSH */
 static v3 color_from_sh(int idx, int deg, int max_coeffs, const float* means, const real* campos,
-                        const float* shs, unsigned char* clamped) {
+                        const float* shs, unsigned char* clamped, const unsigned char* lock) {
     v3 pos = v3_mk(means[3 * idx], means[3 * idx + 1], means[3 * idx + 2]);
     v3 dir = v3_sub(pos, v3_mk(campos[0], campos[1], campos[2]));
     real len = sqrt(v3_dot(dir, dir));
@@ -351,6 +355,13 @@ static v3 color_from_sh(int idx, int deg, int max_coeffs, const float* means, co
     clamped[3 * idx + 0] = result.x < 0;
     clamped[3 * idx + 1] = result.y < 0;
     clamped[3 * idx + 2] = result.z < 0;
+    if (lock) { /* oracle_use_clamp: the other evaluation's decisions, colour and mask alike */
+        clamped[3 * idx + 0] = lock[3 * idx + 0];
+        clamped[3 * idx + 1] = lock[3 * idx + 1];
+        clamped[3 * idx + 2] = lock[3 * idx + 2];
+        return v3_mk(clamped[3 * idx + 0] ? 0 : result.x, clamped[3 * idx + 1] ? 0 : result.y,
+                     clamped[3 * idx + 2] ? 0 : result.z);
+    }
     return v3_mk(fmaxf_cuda(result.x, 0.0f), fmaxf_cuda(result.y, 0.0f), fmaxf_cuda(result.z, 0.0f));
 }
 
@@ -511,7 +522,8 @@ static void preprocess_one(oracle_state* st, int idx) {
     getRect(pix_x, pix_y, f2i_sat(my_radius), &rmin, &rmax, st->gx, st->gy);
     if ((rmax.x - rmin.x) * (rmax.y - rmin.y) == 0) return;
     if (!st->colors_precomp) {
-        v3 c = color_from_sh(idx, st->D, st->M, means3D, st->campos, st->sh, st->clamped);
+        v3 c = color_from_sh(idx, st->D, st->M, means3D, st->campos, st->sh, st->clamped,
+                             st->clamp_lock);
         st->rgb[3 * idx + 0] = c.x;
         st->rgb[3 * idx + 1] = c.y;
         st->rgb[3 * idx + 2] = c.z;
@@ -687,6 +699,23 @@ void oracle_use_decisions(const unsigned* n_contrib, const uint64_t* word_offset
     g_lock.words = words;
 }
 
+/* oracle_use_clamp: the next oracle_forward on this thread takes another evaluation's SH colour
+ * clamp bits (oracle_get_clamped, [P*3]) instead of its own result < 0 tests (copied). */
+static _Thread_local const unsigned char* g_clamp;
+void oracle_use_clamp(const unsigned char* clamped) { g_clamp = clamped; }
+
+/* oracle_use_geometry: the next oracle_forward on this thread blends with another evaluation's
+ * projected splats -- screen means [P*2] and conic + opacity [P*4] (oracle_get_means2D /
+ * oracle_get_conic_opacity, float32) -- instead of its own preprocess's (float64 parity: the
+ * float32 pixel coordinates carry ~1e-4 px of rounding at x ~ 1500, which the Gaussian's falloff
+ * turns into ~1e-4 relative changes of G at the splat's edge; with the float32 geometry the
+ * float64 blend sums exactly the float32 terms).  The arrays are read during that call. */
+static _Thread_local struct { const float *means2D, *conic_opacity; } g_geom;
+void oracle_use_geometry(const float* means2D, const float* conic_opacity) {
+    g_geom.means2D = means2D;
+    g_geom.conic_opacity = conic_opacity;
+}
+
 /* The blend decisions of a forward: per pixel the 32-bit word offset of its bitset (offs[H*W+1],
  * a prefix sum of ceil(n_contrib / 32)) and, when words != NULL, the bitset of the list positions
  * [0, n_contrib) it blended (power <= 0 and alpha >= 1/255, recomputed with the forward's own
@@ -760,6 +789,11 @@ oracle_state* oracle_forward(int P, int M, const float* background, const float*
     st->depths = (real*)xcalloc(P, sizeof(real));
     st->depth_key = (float*)xcalloc(P, sizeof(float));
     st->clamped = (unsigned char*)xcalloc((size_t)P * 3, 1);
+    if (g_clamp) { /* oracle_use_clamp: copied, applied by the preprocess below */
+        st->clamp_lock = (unsigned char*)xcalloc((size_t)P * 3, 1);
+        memcpy(st->clamp_lock, g_clamp, (size_t)P * 3);
+        g_clamp = NULL;
+    }
     st->radii = (int*)xcalloc(P, sizeof(int));
     st->means2D = (real*)xcalloc((size_t)P * 2, sizeof(real));
     st->cov3D = (real*)xcalloc((size_t)P * 6, sizeof(real));
@@ -776,6 +810,12 @@ oracle_state* oracle_forward(int P, int M, const float* background, const float*
         for (size_t i = 0; i < (size_t)P * 6; i++) st->cov3D[i] = cov3D_precomp[i];
     par_for(P, preprocess_range, st);
     if (radii_out) memcpy(radii_out, st->radii, sizeof(int) * (size_t)P);
+    if (g_geom.means2D) { /* oracle_use_geometry: another evaluation's projected splats */
+        for (size_t i = 0; i < (size_t)P * 2; i++) st->means2D[i] = g_geom.means2D[i];
+        for (size_t i = 0; i < (size_t)P * 4; i++) st->conic_opacity[i] = g_geom.conic_opacity[i];
+        g_geom.means2D = NULL;
+        g_geom.conic_opacity = NULL;
+    }
 
     /* ---- scan + duplicateWithKeys + stable SortPairs, rasterizer_impl.cu:70-111, 277-308 ---- */
     const unsigned ntiles = gx * gy;
@@ -1400,7 +1440,7 @@ void oracle_free(oracle_state* st) {
     free(st->depths); free(st->depth_key); free(st->clamped); free(st->radii); free(st->means2D); free(st->cov3D);
     free(st->conic_opacity); free(st->rgb); free(st->feat); free(st->tiles_touched);
     free(st->point_list); free(st->ranges); free(st->final_T); free(st->n_contrib); free(st->margin);
-    free(st->lock_nc); free(st->lock_offs); free(st->lock_words);
+    free(st->lock_nc); free(st->lock_offs); free(st->lock_words); free(st->clamp_lock);
     free(st);
 }
 
@@ -1445,4 +1485,5 @@ int oracle_get_conic_opacity(const oracle_state* st, float* out) { to_float(out,
 int oracle_get_depths(const oracle_state* st, float* out) { to_float(out, st->depths, (size_t)st->P); return 0; }
 int oracle_get_rgb(const oracle_state* st, float* out) { to_float(out, st->rgb, 3 * (size_t)st->P); return 0; }
 int oracle_get_tiles_touched(const oracle_state* st, unsigned* out) { memcpy(out, st->tiles_touched, sizeof(unsigned) * (size_t)st->P); return 0; }
+int oracle_get_clamped(const oracle_state* st, unsigned char* out) { memcpy(out, st->clamped, 3 * (size_t)st->P); return 0; }
 int oracle_get_cov3D(const oracle_state* st, float* out) { to_float(out, st->cov3D, 6 * (size_t)st->P); return 0; }

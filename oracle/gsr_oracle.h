@@ -131,6 +131,13 @@ void oracle_use_decisions(const unsigned* n_contrib, const uint64_t* word_offset
 /* Per pixel: word offsets (H*W + 1) of the bitsets of the list positions the forward blended;
  * with words != NULL also the bitsets.  Returns the number of 32-bit words. */
 long oracle_accept_bits(const oracle_state* st, uint64_t* offs, unsigned* words);
+/* The next oracle_forward on this thread takes another evaluation's SH colour clamp bits [P*3]
+ * (oracle_get_clamped) instead of its own result < 0 tests (float64 parity). */
+void oracle_use_clamp(const unsigned char* clamped);
+/* The next oracle_forward on this thread blends with another evaluation's screen means [P*2]
+ * and conic + opacity [P*4] instead of its own preprocess's (float64 parity). */
+void oracle_use_geometry(const float* means2D, const float* conic_opacity);
+int oracle_get_clamped(const oracle_state* st, unsigned char* out);
 
 void oracle_free(oracle_state* st);
 

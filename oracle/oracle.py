@@ -57,6 +57,12 @@ def lib(variant: str = "f32"):
         L.oracle_use_lists.argtypes = [_p, _i, _p]
         L.oracle_use_decisions.restype = None
         L.oracle_use_decisions.argtypes = [_p, _p, _p]
+        L.oracle_use_geometry.restype = None
+        L.oracle_use_geometry.argtypes = [_p, _p]
+        L.oracle_use_clamp.restype = None
+        L.oracle_use_clamp.argtypes = [_p]
+        L.oracle_get_clamped.restype = _i
+        L.oracle_get_clamped.argtypes = [_p, _p]
         L.oracle_accept_bits.restype = ctypes.c_long
         L.oracle_accept_bits.argtypes = [_p, _p, _p]
         L.oracle_mark_visible.restype = _i
@@ -107,13 +113,16 @@ class OracleRaster:
     as float64) or "expf" (float32 with libm's expf as the blend exp).  lists=(point_list, ranges)
     skips the binning and blends those instance lists (another raster's point_list() / ranges());
     decisions=(n_contrib, offsets, words) blends with another raster's per-pixel decisions
-    (its accept_bits()) instead of this one's own threshold tests."""
+    (its accept_bits()) instead of this one's own threshold tests; clamp= [P,3] u8 takes another
+    raster's SH colour clamp bits (its clamped()) instead of this one's result < 0 tests;
+    geometry=(means2D [P,2], conic_opacity [P,4]) blends another raster's projected splats."""
 
     def __init__(self, *, variant="f32", means3D, opacities, viewmatrix, projmatrix, campos, tanfovx, tanfovy,
                  image_height, image_width, bg, scale_modifier=1.0, sh_degree=0, shs=None,
                  colors_precomp=None, scales=None, rotations=None, cov3D_precomp=None,
                  shs_language=None, language_feature_precomp=None, confidence=None,
-                 include_feature=True, prefiltered=False, lists=None, decisions=None):
+                 include_feature=True, prefiltered=False, lists=None, decisions=None,
+                 clamp=None, geometry=None):
         L = lib(variant)
         self.variant = variant
         self._L = L
@@ -159,6 +168,17 @@ class OracleRaster:
                     k["dwords"].size < int(k["doffs"][-1]):
                 raise ValueError("decisions: (n_contrib [H*W], offsets [H*W+1], words) expected")
             L.oracle_use_decisions(_ptr(k["dnc"]), _ptr(k["doffs"]), _ptr(k["dwords"]))
+        if clamp is not None:
+            k["clamp"] = np.ascontiguousarray(clamp, np.uint8).reshape(-1)
+            if k["clamp"].size != 3 * P:
+                raise ValueError("clamp: [P, 3] clamp bits expected")
+            L.oracle_use_clamp(_ptr(k["clamp"]))
+        if geometry is not None:
+            k["gm"] = np.ascontiguousarray(geometry[0], np.float32).reshape(-1)
+            k["gc"] = np.ascontiguousarray(geometry[1], np.float32).reshape(-1)
+            if k["gm"].size != 2 * P or k["gc"].size != 4 * P:
+                raise ValueError("geometry: (means2D [P,2], conic_opacity [P,4]) expected")
+            L.oracle_use_geometry(_ptr(k["gm"]), _ptr(k["gc"]))
         try:
             self._st = L.oracle_forward(
             P, M, _ptr(k["bg"]), _ptr(k["means3D"]), _ptr(k["colors"]), _ptr(k["opac"]),
@@ -173,6 +193,10 @@ class OracleRaster:
                 L.oracle_use_lists(None, 0, None)
             if decisions is not None:
                 L.oracle_use_decisions(None, None, None)
+            if clamp is not None:
+                L.oracle_use_clamp(None)
+            if geometry is not None:
+                L.oracle_use_geometry(None, None)
         if not self._st:
             raise RuntimeError("oracle_forward rejected its arguments")
         self.num_rendered = int(nr.value)
@@ -221,6 +245,13 @@ class OracleRaster:
         words = np.zeros(max(n, 1), np.uint32)
         self._L.oracle_accept_bits(self._st, _ptr(offs), _ptr(words))
         return self.n_contrib().reshape(-1), offs, words
+
+    def clamped(self):
+        """The SH colour clamp bits [P, 3] (forward.cu:67-69: channel clamped at 0, its dL/dRGB
+        masked in the backward) -- the `clamp=` of another raster."""
+        out = np.zeros((self.P, 3), np.uint8)
+        self._L.oracle_get_clamped(self._st, _ptr(out))
+        return out
 
     def margin(self):
         """Per pixel: the smallest relative distance of any blend decision from its threshold

@@ -201,10 +201,14 @@ __device__ __forceinline__ f2 swap16_add(f2 p, f2 q) {
 // Per contributing (wave, entry): ~40 VALU in phase 1 and ~12 in phase 2, against ~105 for the
 // per-entry 64-lane butterfly this replaces.
 // ================================================================================================
-constexpr int kBatch = 64;           // splat records staged per batch (wave 0 stages)
-// phase-2 width: splats summed per pass (phase-2 lanes j = l & 7; slot 7 unused, so that the
-// wave-private accumulator rows fit the LDS of 4 workgroups per CU)
-constexpr int kSlots = 7;
+// Batch (records staged per batch) and phase-2 width (slots summed per pass; phase-2 lanes
+// j = l & 7): the default backward flushes each wave's sums straight to the accumulator rows
+// (128 records, 8 slots); the deterministic one keeps wave-private LDS rows for the ordered
+// per-instance store (64 records and 7 slots so that they fit 4 workgroups per CU)
+template <bool DET> struct BwdShape {
+  static constexpr int kBatch = DET ? 64 : 128;
+  static constexpr int kSlots = DET ? 7 : 8;
+};
 constexpr int kAccRow = 13;          // LDS accumulator row: the 13 gradient values (odd: conflict-free)
 // phase-2 slot stride in dwords: 64 (u, w) pairs + 2 pad dwords, so the eight slots of a phase-2
 // read start on banks 2j (ds_read_b64: 32 lanes x 2 banks, all distinct)
@@ -217,6 +221,7 @@ constexpr int kDpRow = 68;
 template <bool EXTRA, bool FEAT, bool DET>
 __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t blk) {
   constexpr bool ROWS = DET;  // the deterministic backward stores per-instance rows
+  constexpr int kBatch = BwdShape<DET>::kBatch, kSlots = BwdShape<DET>::kSlots;
   // the batch's records, regrouped for the test phase: s_r0 = {x, y, conic.a, conic.b},
   // s_r1 = {conic.c, opacity}, s_c0 = {r, g, b, depth}, s_c1 = {f0, f1, f2, 1} (alpha channel)
   __shared__ float4 s_r0[kBatch];
@@ -224,9 +229,10 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
   __shared__ float4 s_c0[kBatch];
   __shared__ float4 s_c1[FEAT ? kBatch : 1];
   __shared__ uint32_t s_gid[kBatch];
-  // per batch entry and wave: its 13 gradient values, stored (not added: LDS float atomics cost
-  // ~1 cycle per lane, profiles/r05_bwd_ab.txt) and summed over the waves in wave order
-  __shared__ float s_acc[4 * kBatch * kAccRow];
+  // DET: per batch entry and wave its 13 gradient values, stored and summed over the waves in
+  // wave order (the default backward flushes from phase 2 and needs none: LDS float atomics cost
+  // ~1 cycle per active lane, profiles/r05_bwd_ab.txt)
+  __shared__ float s_acc[DET ? 4 * kBatch * kAccRow : 1];
   __shared__ uint8_t s_mask[kBatch];
   __shared__ uint8_t s_list[kThreads / 64][kBatch];
   __shared__ __attribute__((aligned(16))) float s_uw[kThreads / 64][kSlots * kUwStride];
@@ -311,7 +317,8 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
   const uint32_t qx0 = tx * kTile + (uint32_t)(wid & 1) * 8u;
   const float pfy_row = (float)(ty * kTile + (uint32_t)(wid >> 1) * 8u + (uint32_t)(lane >> 3));
 
-  for (int k = (int)threadIdx.x; k < 4 * kBatch * kAccRow; k += kThreads) s_acc[k] = 0.0f;
+  if (DET)
+    for (int k = (int)threadIdx.x; k < 4 * kBatch * kAccRow; k += kThreads) s_acc[k] = 0.0f;
 
   // Phase 2 over the first `ns` slots (wave-uniform, 1..kSlots).  slotv: lane l holds the batch
   // index of slot l & 7 (set in phase 1, no LDS round trip).
@@ -389,12 +396,33 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
     // pair index held: b3 + 2 b4' + 4 b5' (b4', b5' corrected by the probed swap orientation)
     const int pr = ((lane >> 3) & 1) + 2 * (((lane >> 4) & 1) ^ (int)swap_orient.flip16) +
                    4 * (((lane >> 5) & 1) ^ (int)swap_orient.flip32);
-    // a batch entry is in a wave's list at most once: its row of this wave is written once
     if ((uint32_t)j < ns) {
       const int k0 = 2 * pr;
-      float* row = &s_acc[(wid * kBatch + bj) * kAccRow];
-      if (k0 < kAccRow) row[k0] = w.x;
-      if (k0 + 1 < kAccRow) row[k0 + 1] = w.y;
+      if (DET) {
+        // a batch entry is in a wave's list at most once: its row of this wave is written once
+        float* row = &s_acc[(wid * kBatch + bj) * kAccRow];
+        if (k0 < kAccRow) row[k0] = w.x;
+        if (k0 + 1 < kAccRow) row[k0 + 1] = w.y;
+      } else if (k0 < kAccRow) {
+        // this wave's sums of the splat -> the reference's dL/dmean2D (NDC-scaled), dL/dconic
+        // (linear in the moments, so per-wave partial sums convert exactly up to rounding),
+        // then one global float atomic per value into the splat's accumulator row
+        f2 g = w;
+        const float o = s_r1[bj].y;
+        if (pr == 0) {
+          const float cc = s_r1[bj].x;
+          g.x = -(o * (r0.z * w.x + r0.w * w.y)) * ddelx_dx;
+          g.y = -(o * (cc * w.y + r0.w * w.x)) * ddely_dy;
+        } else if (pr == 1) {
+          g.x = (-0.5f * o) * w.x;
+          g.y = (-0.5f * o) * w.y;
+        } else if (pr == 2) {
+          g.x = (-0.5f * o) * w.x;
+        }
+        float* acc = a.acc + (size_t)s_gid[bj] * kAccFloats + k0;
+        if (g.x != 0.0f) atomicAdd(acc, g.x);
+        if (k0 + 1 < kAccRow && g.y != 0.0f) atomicAdd(acc + 1, g.y);
+      }
     }
   };
 
@@ -535,6 +563,7 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
       }
     }
     if (ns) phase2(ns, slotv);
+    if (!DET) continue;  // flushed from phase 2; the next batch's first barrier protects the records
     __syncthreads();
     // moments -> the reference's dL/dmean2D (NDC-scaled) and dL/dconic, once per (splat, tile)
     if (threadIdx.x < cnt) {

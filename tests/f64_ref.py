@@ -68,8 +68,8 @@ def oracle_inputs(m, act):
         q=m._rotation.detach().cpu().numpy().astype(np.float64), deg=m.active_sh_degree)
 
 
-def _raster(inp, cam, variant, lists=None, decisions=None):
-    return OracleRaster(lists=lists, decisions=decisions,
+def _raster(inp, cam, variant, lists=None, decisions=None, clamp=None, geometry=None):
+    return OracleRaster(lists=lists, decisions=decisions, clamp=clamp, geometry=geometry,
         variant=variant, means3D=inp["xyz"], opacities=inp["op"],
         viewmatrix=cam.world_view_transform.cpu().numpy(),
         projmatrix=cam.full_proj_transform.cpu().numpy(), campos=cam.camera_center.cpu().numpy(),
@@ -79,7 +79,8 @@ def _raster(inp, cam, variant, lists=None, decisions=None):
         shs_language=inp["lang"], include_feature=True)
 
 
-def run_f64_path(inp, cams, grads, progress=None, bound=True, lists=None, decisions=None):
+def run_f64_path(inp, cams, grads, progress=None, bound=True, lists=None, decisions=None,
+                 clamps=None, geometry=None):
     """The float64 oracle on the views of the benchmarked path: per-view images / radii / margin /
     lists, the raw-leaf gradients summed over the views, and (bound) the per-entry rounding scale
     B (float64 arrays shaped like the leaves).  lists: per view (point_list, ranges) to blend
@@ -88,7 +89,14 @@ def run_f64_path(inp, cams, grads, progress=None, bound=True, lists=None, decisi
     float32 run's blend decisions (OracleRaster.accept_bits: n_contrib and, per pixel, which list
     positions it blended) in place of float64's own alpha >= 1/255, power <= 0 and T < 1e-4
     tests -- float64 then sums exactly the terms float32 summed, so every
-    remaining difference is rounding."""
+    remaining difference is rounding.  clamps: per view the float32 run's SH colour clamp bits
+    (OracleRaster.clamped) in place of float64's own result < 0 tests: the per-Gaussian decision
+    that masks a channel's dL/dRGB (backward.cu:390-391), locked the same way.  geometry: per
+    view the float32 run's projected splats (screen means, conic + opacity): the float32 pixel
+    coordinate carries up to half an ulp (6e-5 px at x ~ 1500), which the Gaussian's falloff turns
+    into ~1e-4 relative changes of G at a splat's edge -- a float32 preprocess effect the blend's
+    rounding scale does not model; with it locked the float64 blend sums exactly the float32
+    terms and the bound covers the blend and backward arithmetic."""
     dimg, ddep, dfeat = (g.detach().cpu().numpy() for g in grads)
     q = inp["q"]
     nq = np.maximum(np.linalg.norm(q, axis=1, keepdims=True), 1e-12)
@@ -96,7 +104,9 @@ def run_f64_path(inp, cams, grads, progress=None, bound=True, lists=None, decisi
     views, acc, B = [], None, None
     for i, cam in enumerate(cams):
         o = _raster(inp, cam, "f64", None if lists is None else lists[i],
-                    None if decisions is None else decisions[i])
+                    None if decisions is None else decisions[i],
+                    None if clamps is None else clamps[i],
+                    None if geometry is None else geometry[i])
         P = o.P
         rows = o.blend_rows(dimg, ddep, None, dfeat)
         raw = _raw_chain(o.backward_rows(rows), inp["op"], inp["sc"], qh, nq)

@@ -140,7 +140,7 @@ def run_oracle_path(m, cams, grads, act, progress=None):
                           margin=orc.margin(), ranges=orc.ranges(), point_list=orc.point_list(),
                           n_contrib=orc.n_contrib(), final_T=orc.final_T(),
                           xy=orc.means2D(), conic_opacity=orc.conic_opacity(),
-                          decisions=orc.accept_bits()))
+                          decisions=orc.accept_bits(), clamped=orc.clamped()))
         g = {k: og[k].astype(np.float64)
              for k in ("means3D", "sh", "opacity", "scales", "rotations", "sh_language")}
         gq = g["rotations"]

@@ -113,7 +113,10 @@ def test_decision_lock():
     dec = a.accept_bits()
     assert int(dec[1][-1]) == int(np.sum((a.n_contrib().astype(np.int64) + 31) // 32))
     lists = (a.point_list(), a.ranges())
-    b = O.OracleRaster(variant="f32", lists=lists, decisions=dec, **kw)
+    cl = a.clamped()
+    assert cl.shape == (kw["means3D"].shape[0], 3) and cl.any()  # some SH colours clamp
+    b = O.OracleRaster(variant="f32", lists=lists, decisions=dec, clamp=cl, **kw)
+    assert np.array_equal(b.clamped(), cl)
     for k in ("color", "depth", "alpha", "feature"):
         assert np.array_equal(getattr(a, k), getattr(b, k)), k
     assert np.array_equal(a.n_contrib(), b.n_contrib())
@@ -122,8 +125,9 @@ def test_decision_lock():
     for k in ga:
         assert ga[k] is None or np.array_equal(ga[k], gb[k]), k
     # float64 under the float32 decisions: the same decisions, values within rounding
-    c = O.OracleRaster(variant="f64", lists=lists, decisions=dec, **kw)
+    c = O.OracleRaster(variant="f64", lists=lists, decisions=dec, clamp=cl, **kw)
     assert np.array_equal(a.n_contrib(), c.n_contrib())
+    assert np.array_equal(c.clamped(), cl)  # the clamp decisions are float32's
     assert float(np.abs(c.final_T() - a.final_T()).max()) <= 1e-5
     assert float(np.abs(c.color - a.color).max()) <= 1e-5
     # unlocked float64 does flip a few threshold-marginal pixels on this scene (what the lock

@@ -13,8 +13,12 @@ propagated through the per-Gaussian backward with |J| (f64_ref.py explains it).
 
 Decision-locked: the float64 evaluation blends the float32 oracle's instance
 lists AND its per-pixel decisions (n_contrib and which list positions passed alpha >= 1/255 /
-power <= 0, OracleRaster.accept_bits), so it sums exactly the terms float32 summed and no pixel
-is excluded for a float32-vs-float64 threshold flip.  What is still left out of the entry-wise
+power <= 0, OracleRaster.accept_bits), the per-Gaussian SH colour clamp decisions that mask
+dL/dRGB (OracleRaster.clamped) and the projected splats the blend evaluates (screen means, conic +
+opacity: their float32 rounding, up to 6e-5 px at x ~ 1500, moves G by ~1e-4 relative at a
+splat's edge at 1920x1080 -- a preprocess effect the blend's rounding scale B does not model), so
+it sums exactly the terms float32 summed and no pixel is excluded for a float32-vs-float64
+threshold flip.  What is still left out of the entry-wise
 statistics, counted separately and capped at max(50, 1e-4 P) together: Gaussians behind a
 GPU-vs-float32 image flip (the Gaussians that can reach the flipped pixels,
 fused_ref.pixel_contributors) and Gaussians whose visibility (radius > 0)
@@ -83,7 +87,10 @@ def test_gradients_within_float32_rounding_of_f64(case):
     # f64 blends the f32 binning's lists with the f32 blend's per-pixel decisions
     lists = [(v["point_list"], v["ranges"]) for v in vo]
     decisions = [v.pop("decisions") for v in vo]
-    v64, g64, B = run_f64_path(inp, cams, grads, lists=lists, decisions=decisions,
+    clamps = [v.pop("clamped") for v in vo]  # the SH colour clamp decisions, locked too
+    geometry = [(v["xy"], v["conic_opacity"]) for v in vo]  # and the projected splats
+    v64, g64, B = run_f64_path(inp, cams, grads, lists=lists, decisions=decisions, clamps=clamps,
+                               geometry=geometry,
                                progress=lambda s: print(f"[{case}] {s}", flush=True))
     P = vo[0]["radii"].shape[0]
     hit_gpu = np.zeros(P, bool)
@@ -123,7 +130,8 @@ def test_gradients_within_float32_rounding_of_f64(case):
         # negative control: a 1e-4 systematic error in the colour terms (the image's upstream
         # gradient scaled) is caught by the same bound
         gd = (grads[0] * (1.0 + 1e-4), grads[1], grads[2])
-        _, g64d, _ = run_f64_path(inp, cams, gd, bound=False, lists=lists, decisions=decisions)
+        _, g64d, _ = run_f64_path(inp, cams, gd, bound=False, lists=lists, decisions=decisions,
+                                  clamps=clamps, geometry=geometry)
         st = rounding_stats(gg["_features_dc"], go["_features_dc"], g64d["_features_dc"],
                             B["_features_dc"], exclude=hit, C=C_BOUND)
         assert st["gpu_fail"] >= max(20, 0.01 * st["n_big"]), st
