@@ -51,6 +51,8 @@ class GradAllReducer:
     step everywhere -- a failed rank's NaN gradients are in every rank's summed gradients.
     """
 
+    _ALIGN = 64  # floats (256 B) between parameter slots of the flat buffer
+
     def __init__(self, params, bucket_bytes: int = 64 << 20, group=None, average: bool = False):
         self._source = params
         self.group = group
@@ -81,16 +83,20 @@ class GradAllReducer:
         self._sig = sig
         self.params = params
         dev = params[0].device
-        self.numel = sum(p.numel() for p in params)
-        self.flat = torch.zeros(self.numel + 1, dtype=torch.float32, device=dev)
-        self.guard = self.flat[self.numel:]  # the step's fault snapshot (see the class docstring)
-        per = max(1, self.bucket_bytes // 4)
-        self.buckets = [(s, min(s + per, self.numel)) for s in range(0, self.numel, per)]
+        # Every parameter's slot starts on a _ALIGN-float boundary: the kernels writing gradients
+        # into it take float4 rows (rotations, SH planes) and refuse unaligned pointers, and the
+        # row counts change under densification.  The gaps stay zero on every rank, so reducing
+        # them with their neighbours is harmless.
         self.offsets = []
         off = 0
         for p in params:
             self.offsets.append(off)
-            off += p.numel()
+            off += -(-p.numel() // self._ALIGN) * self._ALIGN
+        self.numel = off
+        self.flat = torch.zeros(self.numel + 1, dtype=torch.float32, device=dev)
+        self.guard = self.flat[self.numel:]  # the step's fault snapshot (see the class docstring)
+        per = max(1, self.bucket_bytes // 4)
+        self.buckets = [(s, min(s + per, self.numel)) for s in range(0, self.numel, per)]
         self._index = {id(p): i for i, p in enumerate(params)}
         return True
 
@@ -203,7 +209,7 @@ class GradAllReducer:
         spans.sort()
         merged = []
         for lo, hi in spans:  # adjacent tensors of the flat buffer go out as one collective
-            if merged and merged[-1][1] == lo:
+            if merged and lo - merged[-1][1] < self._ALIGN:  # only alignment padding between
                 merged[-1] = (merged[-1][0], hi)
             else:
                 merged.append((lo, hi))

@@ -115,7 +115,7 @@ def _overlapped_worker(rank, world, init, n_views, q, sliced=False):
             model.densify()
         reducer.attach_grads()  # re-reads the (new) parameters
         ps = model.parameters()
-        assert reducer.numel == sum(p.numel() for p in ps)
+        assert reducer.numel == sum(-(-p.numel() // 64) * 64 for p in ps)
         for v in shard_views(n_views, rank, world):
             _view_loss(ps, v + step).backward()
         reducer.begin()
@@ -229,3 +229,29 @@ def test_fault_guard_rides_the_allreduce():
         for gs in (g0, g1):  # the gradient sums are unaffected by the extra slot
             for g, r in zip(gs, ref):
                 torch.testing.assert_close(torch.from_numpy(g), r.grad, rtol=1e-5, atol=1e-6)
+
+
+def test_flat_buffer_slots_stay_aligned_under_row_changes():
+    """Every parameter's gradient slot starts on a 256-byte boundary, also for row counts that are
+    not multiples of 4 (densification): the multi-view backward writes float4 rows (rotations,
+    SH planes) into these slots and refuses unaligned pointers."""
+    rows = [1000]
+    params = {}
+
+    def current():
+        n = rows[0]
+        if params.get("n") != n:
+            params["n"] = n
+            params["t"] = [torch.zeros(n, 3), torch.zeros(n, 45), torch.zeros(n, 1),
+                           torch.zeros(n, 3), torch.zeros(n, 4)]
+        return params["t"]
+
+    reducer = GradAllReducer(current)
+    for n in (1000, 1018987, 7):
+        rows[0] = n
+        reducer.attach_grads()
+        assert all(o % 64 == 0 for o in reducer.offsets)
+        assert all(p.grad.data_ptr() % 256 == reducer.flat.data_ptr() % 256 for p in current())
+        assert reducer.guard.data_ptr() >= current()[-1].grad.data_ptr() + 4 * n * 4
+        reducer.zero_rows(0, n)
+        assert reducer._prezeroed

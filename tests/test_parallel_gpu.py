@@ -29,7 +29,7 @@ class _Opt:
 def _scene(dev):
     from gsr_amd.model import SplatModel
     from gsr_amd.synthetic import make_cameras, make_gaussians, upstream_grads
-    model = SplatModel(make_gaussians(20_000, sh_degree=3, seed=3), device=dev)
+    model = SplatModel(make_gaussians(20_001, sh_degree=3, seed=3), device=dev)
     cams = [c.to(dev) for c in make_cameras(4, 320, 240, seed=5)]
     grads = upstream_grads(240, 320, seed=7, device=dev)
     return model, cams, grads
@@ -146,7 +146,7 @@ def test_sliced_adam_equals_serial_step(world1):
     runs = []
     try:
         for slices in (1, 4):  # 1: no row slices -> the serial step
-            model = SplatModel(make_gaussians(20_000, sh_degree=3, seed=3), device=dev)
+            model = SplatModel(make_gaussians(20_001, sh_degree=3, seed=3), device=dev)
             args = trainer.OptArgs()
             trainer.make_trainable(model, args)
             reducer = GradAllReducer(model, bucket_bytes=256 << 10)
