@@ -114,17 +114,39 @@ __device__ __forceinline__ uint32_t wave_mask(float4 r0, float4 r1, float qc, ui
   return m;
 }
 
-// Per-wave compaction of the batch: the wave's list holds, in batch order, the entries whose
-// mask has this wave's bit.  Returns the list length (wave-uniform).
+// The backward's finer form: bit 2 w + h for half h (pixel rows 4 h .. 4 h + 3) of quadrant w.
+__device__ __forceinline__ uint32_t half_mask(float4 r0, float4 r1, float qc, uint32_t tx,
+                                              uint32_t ty) {
+  if (qc == -1.0f) return 0xffu;
+  if (qc == -2.0f) return 0u;
+  const SplatCut cut = make_cut(r0.x, r0.y, r0.z, r0.w, r1.x, qc);
+  uint32_t m = 0;
+#pragma unroll
+  for (int w = 0; w < 4; w++) {
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const float x0 = (float)(tx * kTile + (w & 1) * 8), x1 = x0 + 7.0f;
+      const float y0 = (float)(ty * kTile + (w >> 1) * 8 + h * 4), y1 = y0 + 3.0f;
+      m |= cut_touches_rect(cut, x0, x1, y0, y1) ? (1u << (2 * w + h)) : 0u;
+    }
+  }
+  return m;
+}
+
+// Per-wave compaction of the batch: the list holds, in batch order, the entries whose mask has
+// bit `bit` and whose list position base - j lies before `lim` (the largest n_contrib of the
+// pixels the list serves: entries behind it contribute nowhere).  Returns the list length
+// (wave-uniform).
 template <int N>
 __device__ __forceinline__ uint32_t build_wave_list(const uint8_t* s_mask, uint8_t* list,
-                                                    uint32_t cnt, int wid, int lane) {
+                                                    uint32_t cnt, int bit_idx, int lane,
+                                                    uint32_t base = 0u, uint32_t lim = ~0u) {
   const uint64_t lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
   uint32_t n = 0;
 #pragma unroll
   for (int c = 0; c < N / 64; c++) {
     const uint32_t j = (uint32_t)(c * 64 + lane);
-    const bool bit = j < cnt && ((s_mask[j] >> wid) & 1u);
+    const bool bit = j < cnt && ((s_mask[j] >> bit_idx) & 1u) && base - j < lim;
     const uint64_t b = __ballot(bit);
     if (bit) list[n + (uint32_t)__popcll(b & lt)] = (uint8_t)j;
     n += (uint32_t)__popcll(b);
@@ -144,6 +166,14 @@ template <int CTRL>
 __device__ __forceinline__ float dpp(float x) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xf, 0xf, true));
 }
+template <int CTRL>
+__device__ __forceinline__ uint32_t dppu(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xf, 0xf, true);
+}
+// DPP controls: quad_perm (lane i of each quad takes lane p_i), row_half_mirror (lane i of each
+// 8-lane half row takes lane 7 - i), row_ror:8
+constexpr int kDppQuadXor1 = 0xB1, kDppQuadXor2 = 0x4E, kDppHalfMirror = 0x141;
+constexpr int kDppQuadBcast0 = 0x00, kDppQuadBcast1 = 0x55, kDppQuadBcast2 = 0xAA, kDppQuadBcast3 = 0xFF;
 
 // Orientation of gfx950's v_permlane32_swap / v_permlane16_swap (which half of the pair keeps
 // the first operand), probed once per kernel so the value->lane map below does not rest on an
@@ -201,6 +231,9 @@ __device__ __forceinline__ f2 swap16_add(f2 p, f2 q) {
 // Per contributing (wave, entry): ~40 VALU in phase 1 and ~12 in phase 2, against ~105 for the
 // per-entry 64-lane butterfly this replaces.
 // ================================================================================================
+#ifndef GSR_BWD_HALF
+#define GSR_BWD_HALF 1
+#endif
 // Batch (records staged per batch) and phase-2 width (slots summed per pass; phase-2 lanes
 // j = l & 7): the default backward flushes each wave's sums straight to the accumulator rows
 // (128 records, 8 slots); the deterministic one keeps wave-private LDS rows for the ordered
@@ -221,9 +254,14 @@ constexpr int kDpRow = 68;
 template <bool EXTRA, bool FEAT, bool DET>
 __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t blk) {
   constexpr bool ROWS = DET;  // the deterministic backward stores per-instance rows
+  // HALF: the two halves of a quadrant (pixel rows 0-3 = lanes 0-31, rows 4-7 = lanes 32-63) walk
+  // their own lists, so one phase-1 step replays a splat for each half; the deterministic
+  // backward keeps one list per quadrant (its per-(wave, entry) rows)
+  constexpr bool HALF = !DET && GSR_BWD_HALF;
   constexpr int kBatch = BwdShape<DET>::kBatch, kSlots = BwdShape<DET>::kSlots;
-  // the batch's records, regrouped for the test phase: s_r0 = {x, y, conic.a, conic.b},
-  // s_r1 = {conic.c, opacity}, s_c0 = {r, g, b, depth}, s_c1 = {f0, f1, f2, 1} (alpha channel)
+  // the batch's records, regrouped for the test phase: s_r0 = {x, y, conic.a, conic.c} (the
+  // packed pairs of the power), s_r1 = {conic.b, opacity}, s_c0 = {r, g, b, depth},
+  // s_c1 = {f0, f1, f2, 1} (alpha channel)
   __shared__ float4 s_r0[kBatch];
   __shared__ float2 s_r1[kBatch];
   __shared__ float4 s_c0[kBatch];
@@ -234,12 +272,13 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
   // ~1 cycle per active lane, profiles/r05_bwd_ab.txt)
   __shared__ float s_acc[DET ? 4 * kBatch * kAccRow : 1];
   __shared__ uint8_t s_mask[kBatch];
-  __shared__ uint8_t s_list[kThreads / 64][kBatch];
+  __shared__ uint8_t s_list[kThreads / 64][HALF ? 2 : 1][kBatch];
   __shared__ __attribute__((aligned(16))) float s_uw[kThreads / 64][kSlots * kUwStride];
   __shared__ __attribute__((aligned(16))) float s_dp[kThreads / 64][8 * kDpRow];
 
   const int lane = (int)(threadIdx.x & 63);
   const int wid = (int)(threadIdx.x >> 6);
+  const int half = HALF ? (lane >> 5) : 0;
   const SwapOrient swap_orient = probe_swaps(lane);
   const uint32_t ntiles = a.gx * a.gy;
   const uint32_t tile = sched_tile(blk, ntiles, a.sched, a.order);
@@ -259,9 +298,11 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
   const float T_final = inside ? a.final_T[pix] : 0.0f;
   float T = T_final;
   const uint32_t last_contributor = inside ? a.n_contrib[pix] : 0u;
+  // the largest n_contrib of the wave (HALF: of the lane's half)
   uint32_t wave_last = last_contributor;
 #pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) wave_last = max(wave_last, (uint32_t)__shfl_xor((int)wave_last, d, 64));
+  for (int d = HALF ? 16 : 32; d >= 1; d >>= 1)
+    wave_last = max(wave_last, (uint32_t)__shfl_xor((int)wave_last, d, 64));
 
   constexpr int NC = FEAT ? 8 : (EXTRA ? 5 : 3);
   float dpix[NC];
@@ -380,6 +421,68 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
     v[5] = cC;
     v[6] = cD;
     v[7] = mk2(0.f, 0.f);
+    if (HALF) {
+      // rows 0-3 and 4-7 (lane bit 5) are different splats: halving butterfly over the 4 rows of
+      // each half, lane bit 4 (permlane16_swap), bit 3 (DPP row_ror:8); each lane is left with the
+      // two pairs 2 m, 2 m + 1 of its slot and half, m = b3 + 2 b4' -- the 4 consecutive values
+      // 4 m .. 4 m + 3 of the gradient row
+#pragma unroll
+      for (int i = 0; i < 4; i++) v[i] = swap16_add(v[i], v[i + 4]);
+      f2 w2[2];
+      const bool hi = lane & 8;
+#pragma unroll
+      for (int i = 0; i < 2; i++) {
+        const f2 send = hi ? v[i] : v[i + 2];
+        const f2 keep = hi ? v[i + 2] : v[i];
+        w2[i] = keep + mk2(dpp<0x128>(send.x), dpp<0x128>(send.y));  // row_ror:8
+      }
+      const int m = ((lane >> 3) & 1) + 2 * (((lane >> 4) & 1) ^ (int)swap_orient.flip16);
+      // this wave-half's sums of the splat -> the reference's dL/dmean2D (NDC-scaled) and
+      // dL/dconic (linear in the moments: partial sums convert exactly up to rounding)
+      float g[4];
+      {
+        const float2 r1 = s_r1[bj];
+        const float o = r1.y, nho = -0.5f * o;
+        const f2 p0 = w2[0], p1 = w2[1];
+        const bool m0 = m == 0;
+        g[0] = m0 ? -(o * (r0.z * p0.x + r1.x * p0.y)) * ddelx_dx : (m == 1 ? nho * p0.x : p0.x);
+        g[1] = m0 ? -(o * (r0.w * p0.y + r1.x * p0.x)) * ddely_dy : p0.y;
+        g[2] = m0 ? nho * p1.x : p1.x;
+        g[3] = m0 ? nho * p1.y : p1.y;
+      }
+      // one global float atomic per value into the splat's accumulator row.  Float atomics cost
+      // per 64-B line a wave-instruction touches, so the values are first transposed inside each
+      // quad (lanes q = slot bits 0-1): lane q's register k (slot q, value 4 m + k) moves to lane
+      // k's register q, and atomic instruction r then covers 4 whole rows (slots 4 b + r of both
+      // halves) instead of values of 16 rows
+      uint32_t gid = ((uint32_t)j < ns && slotv < (uint32_t)kBatch) ? s_gid[bj] : 0xffffffffu;
+      const int q = lane & 3;
+#pragma unroll
+      for (int i = 0; i < 2; i++) {  // lane bit 1 <-> register bit 1
+        const bool b1 = q & 2;
+        const float recv = dpp<kDppQuadXor2>(b1 ? g[i] : g[i + 2]);
+        g[i] = b1 ? recv : g[i];
+        g[i + 2] = b1 ? g[i + 2] : recv;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; i += 2) {  // lane bit 0 <-> register bit 0
+        const bool b0 = q & 1;
+        const float recv = dpp<kDppQuadXor1>(b0 ? g[i] : g[i + 1]);
+        g[i] = b0 ? recv : g[i];
+        g[i + 1] = b0 ? g[i + 1] : recv;
+      }
+      const int k = 4 * m + q;  // the value every register of this lane now holds
+      // register r's row: slot r of the quad (DPP quad broadcast of lane r's id)
+      const uint32_t gr[4] = {dppu<kDppQuadBcast0>(gid), dppu<kDppQuadBcast1>(gid),
+                              dppu<kDppQuadBcast2>(gid), dppu<kDppQuadBcast3>(gid)};
+      if (k < kAccRow) {
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+          if (gr[r] != 0xffffffffu && g[r] != 0.0f)
+            atomicAdd(a.acc + (size_t)gr[r] * kAccFloats + k, g[r]);
+      }
+      return;
+    }
     // halving butterfly over the 8 rows: lane bit 5 (permlane32_swap), bit 4 (permlane16_swap),
     // bit 3 (DPP row_ror:8 swaps the halves of a 16-lane row)
 #pragma unroll
@@ -396,32 +499,36 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
     // pair index held: b3 + 2 b4' + 4 b5' (b4', b5' corrected by the probed swap orientation)
     const int pr = ((lane >> 3) & 1) + 2 * (((lane >> 4) & 1) ^ (int)swap_orient.flip16) +
                    4 * (((lane >> 5) & 1) ^ (int)swap_orient.flip32);
-    if ((uint32_t)j < ns) {
-      const int k0 = 2 * pr;
-      if (DET) {
+    if (DET) {
+      if ((uint32_t)j < ns) {
         // a batch entry is in a wave's list at most once: its row of this wave is written once
+        const int k0 = 2 * pr;
         float* row = &s_acc[(wid * kBatch + bj) * kAccRow];
         if (k0 < kAccRow) row[k0] = w.x;
         if (k0 + 1 < kAccRow) row[k0 + 1] = w.y;
-      } else if (k0 < kAccRow) {
-        // this wave's sums of the splat -> the reference's dL/dmean2D (NDC-scaled), dL/dconic
-        // (linear in the moments, so per-wave partial sums convert exactly up to rounding),
-        // then one global float atomic per value into the splat's accumulator row
-        f2 g = w;
-        const float o = s_r1[bj].y;
-        if (pr == 0) {
-          const float cc = s_r1[bj].x;
-          g.x = -(o * (r0.z * w.x + r0.w * w.y)) * ddelx_dx;
-          g.y = -(o * (cc * w.y + r0.w * w.x)) * ddely_dy;
-        } else if (pr == 1) {
-          g.x = (-0.5f * o) * w.x;
-          g.y = (-0.5f * o) * w.y;
-        } else if (pr == 2) {
-          g.x = (-0.5f * o) * w.x;
-        }
-        float* acc = a.acc + (size_t)s_gid[bj] * kAccFloats + k0;
-        if (g.x != 0.0f) atomicAdd(acc, g.x);
-        if (k0 + 1 < kAccRow && g.y != 0.0f) atomicAdd(acc + 1, g.y);
+      }
+    } else {
+      // this wave's sums of the splat -> the reference's dL/dmean2D (NDC-scaled), dL/dconic
+      // (linear in the moments, so per-wave partial sums convert exactly up to rounding), then
+      // one global float atomic per value into the splat's accumulator row
+      const float2 r1 = s_r1[bj];
+      const float o = r1.y, nho = -0.5f * o;
+      f2 g;
+      g.x = pr == 0 ? -(o * (r0.z * w.x + r1.x * w.y)) * ddelx_dx : (pr <= 2 ? nho * w.x : w.x);
+      g.y = pr == 0 ? -(o * (r0.w * w.y + r1.x * w.x)) * ddely_dy : (pr == 1 ? nho * w.y : w.y);
+      // float atomics cost per 64-B line a wave-instruction touches: slots j and 7 - j swap one
+      // value (DPP row_half_mirror), so each of the two atomic instructions covers 4 whole rows
+      // (slots 0-3 / 4-7) instead of one value pair of all 8
+      const uint32_t gid = (uint32_t)j < ns ? s_gid[bj] : 0xffffffffu;
+      const bool lo = j < 4;
+      const float recv = dpp<kDppHalfMirror>(lo ? g.y : g.x);
+      const uint32_t gp = dppu<kDppHalfMirror>(gid);
+      const int k = 2 * pr + (lo ? 0 : 1);
+      const float ax = lo ? g.x : recv, ay = lo ? recv : g.y;
+      const uint32_t ga = lo ? gid : gp, gb = lo ? gp : gid;
+      if (k < kAccRow) {
+        if (ga != 0xffffffffu && ax != 0.0f) atomicAdd(a.acc + (size_t)ga * kAccFloats + k, ax);
+        if (gb != 0xffffffffu && ay != 0.0f) atomicAdd(a.acc + (size_t)gb * kAccFloats + k, ay);
       }
     }
   };
@@ -437,27 +544,39 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
       s_gid[threadIdx.x] = gid;
       const float4* rec = a.rec + 4 * (size_t)gid;
       const float4 q0 = rec[0], q1 = rec[1], q2 = rec[2], q3 = rec[3];
-      s_r0[threadIdx.x] = q0;
-      s_r1[threadIdx.x] = make_float2(q1.x, q1.y);
-      s_mask[threadIdx.x] = (uint8_t)wave_mask(q0, q1, q3.z, tx, ty);
+      s_r0[threadIdx.x] = make_float4(q0.x, q0.y, q0.z, q1.x);
+      s_r1[threadIdx.x] = make_float2(q0.w, q1.y);
+      s_mask[threadIdx.x] = (uint8_t)(HALF ? half_mask(q0, q1, q3.z, tx, ty)
+                                           : wave_mask(q0, q1, q3.z, tx, ty));
       s_c0[threadIdx.x] = make_float4(q1.w, q2.x, q2.y, q1.z);
       if (FEAT) s_c1[threadIdx.x] = make_float4(q2.z, q2.w, q3.x, 1.0f);
     }
     __syncthreads();
-    const uint32_t nlist = build_wave_list<kBatch>(s_mask, s_list[wid], cnt, wid, lane);
+    // nlist: the wave's step count; nmine: the length of the lane's own list (HALF: its half's)
+    // (entries behind the list's pixels' last contributor are left out)
+    uint32_t nlist, nmine;
+    const uint32_t base = tile_last - 1 - done_cnt;
+    if (HALF) {
+      const uint32_t n0 = build_wave_list<kBatch>(s_mask, s_list[wid][0], cnt, 2 * wid, lane, base,
+                                                  (uint32_t)__builtin_amdgcn_readlane((int)wave_last, 0));
+      const uint32_t n1 = build_wave_list<kBatch>(s_mask, s_list[wid][HALF ? 1 : 0], cnt,
+                                                  2 * wid + 1, lane, base,
+                                                  (uint32_t)__builtin_amdgcn_readlane((int)wave_last, 32));
+      nmine = half ? n1 : n0;
+      nlist = max(n0, n1);
+    } else {
+      nlist = build_wave_list<kBatch>(s_mask, s_list[wid][0], cnt, wid, lane, base,
+                                      (uint32_t)__builtin_amdgcn_readfirstlane((int)wave_last));
+      nmine = nlist;
+    }
     uint32_t ns = 0;     // phase-2 slots in use (wave-uniform)
-    uint32_t slotv = 0;  // lane l: batch index of phase-2 slot l & 7
+    // lane l: batch index of phase-2 slot l & 7 (HALF: of the lane's half; >= kBatch when that
+    // half had no contributing pixel at that step)
+    uint32_t slotv = 0;
     // Four list entries per group: the per-pair test (power, G, alpha) of all four is evaluated
     // first (independent work), then the entries are replayed in list order.
     for (uint32_t k0 = 0; k0 < nlist; k0 += 4) {
-      const uint32_t packed = *reinterpret_cast<const uint32_t*>(&s_list[wid][k0]);
-      {
-        // list order is back to front: if even the group's front-most entry lies behind every
-        // pixel's last contributor in this wave, nothing in the group can contribute
-        const uint32_t ulast = min(3u, nlist - 1 - k0);
-        const uint32_t jl = (packed >> (8 * ulast)) & 0xffu;
-        if (tile_last - 1 - done_cnt - jl >= wave_last) continue;  // wave-uniform
-      }
+      const uint32_t packed = *reinterpret_cast<const uint32_t*>(&s_list[wid][half][k0]);
       // Every LDS read of the group's entries is issued here, before any arithmetic; the colours
       // are consumed at once by the colour dot product, so the replay below reads no records.
       float Gv[4], av[4], cdv[4];
@@ -467,7 +586,8 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
         float2 r1v[4];
 #pragma unroll
         for (int u = 0; u < 4; u++) {
-          const uint32_t j = (packed >> (8 * u)) & 0xffu;
+          // (entries past the list's end hold stale bytes: kept inside the batch)
+          const uint32_t j = (packed >> (8 * u)) & (uint32_t)(kBatch - 1);
           r0v[u] = s_r0[j];
           r1v[u] = s_r1[j];
           c0v[u] = s_c0[j];
@@ -477,9 +597,11 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
         float tdist = 1.0f;  // min over the group of |op * G - 1/255| (the exact-path test)
 #pragma unroll
         for (int u = 0; u < 4; u++) {
+          // the reference's -0.5 (ca dx dx + cc dy dy) - cb dx dy, the pairs as packed products
+          // (same operations, same order)
           const float4 r0 = r0v[u];
           const float dx = r0.x - pfx, dy = r0.y - pfy;
-          pw[u] = -0.5f * (r0.z * dx * dx + r1v[u].x * dy * dy) - r0.w * dx * dy;
+          pw[u] = -0.5f * (r0.z * dx * dx + r0.w * dy * dy) - r1v[u].x * dx * dy;
           // The backward needs the forward's alpha >= 1/255 DECISION exactly, its G only to
           // gradient precision: G by the hardware exp2 (v_exp_f32, ~1 ulp; 3 instructions
           // instead of the 17 of splat_exp), and splat_exp -- the forward's and the oracle's
@@ -513,10 +635,10 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
         }
 #pragma unroll
         for (int u = 0; u < 4; u++) {
-          const uint32_t j = (packed >> (8 * u)) & 0xffu;
+          const uint32_t j = (packed >> (8 * u)) & (uint32_t)(kBatch - 1);
           const uint32_t rel = tile_last - 1 - done_cnt - j;
           av[u] = fminf(0.99f, r1v[u].y * Gv[u]);
-          cv[u] = (k0 + u < nlist) && rel < last_contributor && !(pw[u] > 0.0f) &&
+          cv[u] = (k0 + u < nmine) && rel < last_contributor && !(pw[u] > 0.0f) &&
                   !(av[u] < 1.0f / 255.0f);
         }
       }
@@ -524,8 +646,9 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
       for (int u = 0; u < 4; u++) {
         const bool contrib = cv[u];
         // wave-uniform skip of entries without a contributing lane
-        if (__ballot(contrib) == 0ull) continue;
-        const uint32_t j = (packed >> (8 * u)) & 0xffu;
+        const uint64_t bal = __ballot(contrib);
+        if (bal == 0ull) continue;
+        const uint32_t j = (packed >> (8 * u)) & (uint32_t)(kBatch - 1);
         // Branch-free: a lane whose pixel does not take this splat runs the same arithmetic with
         // G = alpha = 0, which makes u and w exactly zero and T / (1 - 0) == T; its recurrence
         // state is kept by selects.  Contributing lanes compute exactly the operations of the
@@ -554,7 +677,12 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
         const float uu = G * dL_dalpha;
         // park (u, w) in the next phase-2 slot
         *reinterpret_cast<f2*>(&s_uw[wid][ns * kUwStride + 2 * lane]) = mk2(uu, wgt);
-        slotv = ((uint32_t)(lane & 7) == ns) ? j : slotv;
+        if (HALF) {
+          const bool hv = (half ? (bal >> 32) : (bal & 0xffffffffull)) != 0ull;
+          slotv = ((uint32_t)(lane & 7) == ns) ? (hv ? j : 0xffffffffu) : slotv;
+        } else {
+          slotv = ((uint32_t)(lane & 7) == ns) ? j : slotv;
+        }
         ns = (uint32_t)__builtin_amdgcn_readfirstlane((int)(ns + 1));
         if (ns == (uint32_t)kSlots) {
           phase2(ns, slotv);
@@ -577,8 +705,8 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
                  row[3 * kBatch * kAccRow + k];
       const float sx = row[kAccMx], sy = row[kAccMy];
       const float o = r1.y;
-      row[kAccMx] = -(o * (r0.z * sx + r0.w * sy)) * ddelx_dx;
-      row[kAccMy] = -(o * (r1.x * sy + r0.w * sx)) * ddely_dy;
+      row[kAccMx] = -(o * (r0.z * sx + r1.x * sy)) * ddelx_dx;
+      row[kAccMy] = -(o * (r0.w * sy + r1.x * sx)) * ddely_dy;
       row[kAccCa] = (-0.5f * o) * row[kAccCa];
       row[kAccCb] = (-0.5f * o) * row[kAccCb];
       row[kAccCc] = (-0.5f * o) * row[kAccCc];

@@ -446,4 +446,6 @@ def test_backward_twice_through_one_forward():
     first = torch.autograd.grad(loss, [inp["means3D"], inp["opacities"]], retain_graph=True)
     second = torch.autograd.grad(loss, [inp["means3D"], inp["opacities"]])
     for a, b in zip(first, second):
-        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-7)
+        # float atomics: two backwards differ in the last bits (as the reference's); a stale or
+        # doubled accumulator would differ by whole gradients
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6 * float(b.abs().max()))
