@@ -12,13 +12,21 @@
 //    in its pixels (the conservative test the binning uses);
 //  * forward: each wave's 64 lanes are four 16-lane groups owning 4x4 pixel blocks, each walking
 //    its own compacted list (block lists);
-//  * backward (two phases per wave): phase 1 replays the tile back to front
-//    with lanes = pixels (the reference's per-pixel recurrence, backward.cu:482-534) and parks each
-//    contributing splat's per-pixel pair (u = G dL/dalpha, w = alpha T) in LDS; phase 2 switches
-//    to lanes = (splat, pixel row) and sums the 13 gradient values over the pixels in registers,
-//    eight splats at a time, before one LDS add per value and a 64-B row of global float atomics
-//    per (splat, tile) -- instead of a 64-lane reduction per splat, or the reference's 9 atomics
-//    per contributing (splat, pixel) pair.
+//  * backward (two phases per wave): the two halves of a wave's quadrant walk
+//    their own lists; phase 1 replays the tile back to front with lanes = pixels (the reference's
+//    per-pixel recurrence, backward.cu:482-534) and parks each contributing splat's per-pixel
+//    pair (u = G dL/dalpha, w = alpha T) in LDS; phase 2 switches to lanes = (splat, pixel row),
+//    sums the 13 gradient values over the pixels in registers, eight slots at a time, and flushes
+//    them as global float atomics, each wave-instruction covering 4 whole accumulator rows --
+//    instead of a 64-lane reduction per splat, or the reference's 9 atomics per contributing
+//    (splat, pixel) pair.
+//
+// Two translation units: GSR_RENDER_PART 1 = the backward (this file, built with the SLP
+// vectorizer), 2 = the forward, schedule and activation kernels (gsr_render_fwd.hip, built
+// without it: its scalar code runs 6 % faster unpaired, profiles/r05_slp_ab.txt); 0 = both.
+#ifndef GSR_RENDER_PART
+#define GSR_RENDER_PART 0
+#endif
 #include "gsr_device.h"
 #include "gsr_internal.h"
 
@@ -114,15 +122,18 @@ __device__ __forceinline__ uint32_t wave_mask(float4 r0, float4 r1, float qc, ui
   return m;
 }
 
-// The backward's finer form: bit 2 w + h for half h (pixel rows 4 h .. 4 h + 3) of quadrant w.
+// The backward's finer form: bit 2 w + h for half h (pixel rows 4 h .. 4 h + 3) of quadrant w,
+// for the quadrants w0 .. w0 + NW - 1.
+template <int NW = 4>
 __device__ __forceinline__ uint32_t half_mask(float4 r0, float4 r1, float qc, uint32_t tx,
-                                              uint32_t ty) {
+                                              uint32_t ty, int w0 = 0) {
   if (qc == -1.0f) return 0xffu;
   if (qc == -2.0f) return 0u;
   const SplatCut cut = make_cut(r0.x, r0.y, r0.z, r0.w, r1.x, qc);
   uint32_t m = 0;
 #pragma unroll
-  for (int w = 0; w < 4; w++) {
+  for (int wi = 0; wi < NW; wi++) {
+    const int w = w0 + wi;
 #pragma unroll
     for (int h = 0; h < 2; h++) {
       const float x0 = (float)(tx * kTile + (w & 1) * 8), x1 = x0 + 7.0f;
@@ -206,6 +217,7 @@ __device__ __forceinline__ f2 swap16_add(f2 p, f2 q) {
          mk2(__uint_as_float(rx[1]), __uint_as_float(ry[1]));
 }
 
+#if GSR_RENDER_PART != 2
 // ================================================================================================
 // Backward blend.
 //
@@ -272,6 +284,8 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
   // ~1 cycle per active lane, profiles/r05_bwd_ab.txt)
   __shared__ float s_acc[DET ? 4 * kBatch * kAccRow : 1];
   __shared__ uint8_t s_mask[kBatch];
+  // HALF: the mask bits of quadrants 2 and 3, computed by the workgroup's upper half
+  __shared__ uint8_t s_mask23[HALF ? kBatch : 1];
   __shared__ uint8_t s_list[kThreads / 64][HALF ? 2 : 1][kBatch];
   __shared__ __attribute__((aligned(16))) float s_uw[kThreads / 64][kSlots * kUwStride];
   __shared__ __attribute__((aligned(16))) float s_dp[kThreads / 64][8 * kDpRow];
@@ -534,22 +548,38 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
   };
 
   // rel = position inside the tile's list; every pixel only uses rel < its n_contrib <= tile_last
+  // staging lanes: sj = the batch slot this thread stages (HALF: both halves of the workgroup
+  // take the batch's records, the lower half staging them and the quadrant-0/1 mask bits, the
+  // upper half the quadrant-2/3 bits); its list entry is loaded one batch ahead
+  static_assert(!HALF || kThreads == 2 * kBatch, "HALF staging: two threads per record");
+  const uint32_t sj = HALF ? (threadIdx.x & (uint32_t)(kBatch - 1)) : threadIdx.x;
+  const bool upper = HALF && threadIdx.x >= (uint32_t)kBatch;  // wave-uniform
+  uint32_t pid_next = sj < min((uint32_t)kBatch, tile_last) ? a.point_list[range.x + tile_last - 1 - sj] : 0u;
   for (uint32_t done_cnt = 0; done_cnt < tile_last; done_cnt += kBatch) {
     __syncthreads();
     const uint32_t cnt = min((uint32_t)kBatch, tile_last - done_cnt);
     // stage the batch starting at list position done_cnt (back to front)
-    if (threadIdx.x < cnt) {
-      const uint32_t rel = tile_last - 1 - done_cnt - threadIdx.x;
-      const uint32_t gid = min(a.point_list[range.x + rel], a.P - 1u);
-      s_gid[threadIdx.x] = gid;
+    if (sj < cnt) {
+      const uint32_t gid = min(pid_next, a.P - 1u);
       const float4* rec = a.rec + 4 * (size_t)gid;
-      const float4 q0 = rec[0], q1 = rec[1], q2 = rec[2], q3 = rec[3];
-      s_r0[threadIdx.x] = make_float4(q0.x, q0.y, q0.z, q1.x);
-      s_r1[threadIdx.x] = make_float2(q0.w, q1.y);
-      s_mask[threadIdx.x] = (uint8_t)(HALF ? half_mask(q0, q1, q3.z, tx, ty)
-                                           : wave_mask(q0, q1, q3.z, tx, ty));
-      s_c0[threadIdx.x] = make_float4(q1.w, q2.x, q2.y, q1.z);
-      if (FEAT) s_c1[threadIdx.x] = make_float4(q2.z, q2.w, q3.x, 1.0f);
+      if (!upper) {
+        s_gid[sj] = gid;
+        const float4 q0 = rec[0], q1 = rec[1], q2 = rec[2], q3 = rec[3];
+        s_r0[sj] = make_float4(q0.x, q0.y, q0.z, q1.x);
+        s_r1[sj] = make_float2(q0.w, q1.y);
+        s_mask[sj] = (uint8_t)(HALF ? half_mask<2>(q0, q1, q3.z, tx, ty, 0)
+                                    : wave_mask(q0, q1, q3.z, tx, ty));
+        s_c0[sj] = make_float4(q1.w, q2.x, q2.y, q1.z);
+        if (FEAT) s_c1[sj] = make_float4(q2.z, q2.w, q3.x, 1.0f);
+      } else {
+        const float4 q0 = rec[0], q1 = rec[1], q3 = rec[3];
+        s_mask23[sj] = (uint8_t)half_mask<2>(q0, q1, q3.z, tx, ty, 2);
+      }
+    }
+    {  // the next batch's list entries, in flight while this batch is replayed
+      const uint32_t nd = done_cnt + kBatch;
+      if (sj < min((uint32_t)kBatch, tile_last - min(nd, tile_last)))
+        pid_next = a.point_list[range.x + tile_last - 1 - nd - sj];
     }
     __syncthreads();
     // nlist: the wave's step count; nmine: the length of the lane's own list (HALF: its half's)
@@ -557,9 +587,10 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
     uint32_t nlist, nmine;
     const uint32_t base = tile_last - 1 - done_cnt;
     if (HALF) {
-      const uint32_t n0 = build_wave_list<kBatch>(s_mask, s_list[wid][0], cnt, 2 * wid, lane, base,
+      const uint8_t* msk = wid < 2 ? s_mask : s_mask23;
+      const uint32_t n0 = build_wave_list<kBatch>(msk, s_list[wid][0], cnt, 2 * wid, lane, base,
                                                   (uint32_t)__builtin_amdgcn_readlane((int)wave_last, 0));
-      const uint32_t n1 = build_wave_list<kBatch>(s_mask, s_list[wid][HALF ? 1 : 0], cnt,
+      const uint32_t n1 = build_wave_list<kBatch>(msk, s_list[wid][HALF ? 1 : 0], cnt,
                                                   2 * wid + 1, lane, base,
                                                   (uint32_t)__builtin_amdgcn_readlane((int)wave_last, 32));
       nmine = half ? n1 : n0;
@@ -767,6 +798,8 @@ __global__ __launch_bounds__(kThreads) GSR_BWD_WAVES(DET) void render_bwd_views_
   render_bwd_tile<EXTRA, FEAT, DET>(m.v[k], b - m.first[k]);
 }
 
+#endif  // GSR_RENDER_PART != 2
+#if GSR_RENDER_PART != 1
 // ================================================================================================
 // Forward with block lists: each wave's 64 lanes are four 16-lane groups, group g = lanes
 // 16 g .. 16 g + 15 owning a 4x4 pixel block of the wave's 8x8 quadrant (x = lane & 3,
@@ -1058,8 +1091,10 @@ __global__ void activations_kernel(const float* __restrict__ op_raw, const float
   rot[i] = normalize_quat(rot_raw[i]);
 }
 
+#endif  // GSR_RENDER_PART != 1
 }  // namespace
 
+#if GSR_RENDER_PART != 1
 hipError_t launch_activations(const float* op_raw, const float* sc_raw, const float* rot_raw,
                               size_t P, float* op, float* sc, float* rot, hipStream_t s) {
   if (P == 0) return hipSuccess;
@@ -1132,6 +1167,8 @@ hipError_t launch_render_forward(const RenderArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+#endif  // GSR_RENDER_PART != 1
+#if GSR_RENDER_PART != 2
 hipError_t launch_render_backward_views(const RenderBwdArgs* views, int V, hipStream_t s) {
   if (V <= 0) return hipSuccess;
   if (V > kMaxBwdViews) return hipErrorInvalidValue;
@@ -1188,4 +1225,5 @@ hipError_t launch_render_backward(const RenderBwdArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+#endif  // GSR_RENDER_PART != 2
 }  // namespace gsr
