@@ -709,8 +709,14 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
         // park (u, w) in the next phase-2 slot
         *reinterpret_cast<f2*>(&s_uw[wid][ns * kUwStride + 2 * lane]) = mk2(uu, wgt);
         if (HALF) {
-          const bool hv = (half ? (bal >> 32) : (bal & 0xffffffffull)) != 0ull;
-          slotv = ((uint32_t)(lane & 7) == ns) ? (hv ? j : 0xffffffffu) : slotv;
+          // the lanes of a half with a contributing pixel, as a scalar lane mask, selects the
+          // entry or "no slot" in one v_cndmask (the per-lane form costs ~5 VALU per step)
+          constexpr uint64_t kLo = 0x00000000ffffffffull;
+          const uint64_t hm = (((uint32_t)bal != 0u) ? kLo : 0ull) |
+                              (((uint32_t)(bal >> 32) != 0u) ? ~kLo : 0ull);
+          uint32_t jv;
+          asm("v_cndmask_b32_e64 %0, -1, %1, %2" : "=v"(jv) : "v"(j), "s"(hm));
+          slotv = ((uint32_t)(lane & 7) == ns) ? jv : slotv;
         } else {
           slotv = ((uint32_t)(lane & 7) == ns) ? j : slotv;
         }
