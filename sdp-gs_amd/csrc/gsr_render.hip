@@ -949,12 +949,15 @@ __device__ __forceinline__ void render_fwd_blk_tile(const RenderArgs& a, uint32_
 #pragma unroll
   for (int c = 0; c < NC; c++) C[c] = 0.0f;
 
+  // this lane's list entry of the next batch, loaded one batch ahead
+  uint32_t pid_next = range.x + threadIdx.x < range.y ? a.point_list[range.x + threadIdx.x] : 0u;
   for (uint32_t base = range.x; base < range.y; base += kThreads) {
     // forward.cu:309-311: stop when every pixel of the tile is saturated
     if (__syncthreads_count(done) == kThreads) break;
     const uint32_t i = base + threadIdx.x;
     if (i < range.y) {
-      const uint32_t pid = a.point_list[i];
+      const uint32_t pid = pid_next;
+      if (i + kThreads < range.y) pid_next = a.point_list[i + kThreads];
       if (pid >= a.P) {  // memory-safe clamp, reported to this call's status check
         atomicOr(a.status, kStatusClamp);
         if (a.host_status) *a.host_status = kStatusClamp;  // sort bits are 0 on this path
