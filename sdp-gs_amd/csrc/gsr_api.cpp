@@ -1102,7 +1102,10 @@ hipEvent_t join_event(int i) {
   thread_local hipEvent_t ev[kMaxDev][kFwdSlots + 1] = {};
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return nullptr;
-  if (!ev[dev][i] && hipEventCreateWithFlags(&ev[dev][i], hipEventDisableTiming) != hipSuccess)
+  // stream-to-stream ordering only: a device-scope release, no system fence (no host reads)
+  if (!ev[dev][i] &&
+      hipEventCreateWithFlags(&ev[dev][i], hipEventDisableTiming | hipEventDisableSystemFence) !=
+          hipSuccess)
     ev[dev][i] = nullptr;
   return ev[dev][i];
 }
@@ -1326,7 +1329,12 @@ int views_forward_batched(const FwdModel& m, std::vector<FwdCam>& cams, gsr_view
     PROF_END(RANGES);
     return GSR_OK;
   };
-  // phase 2b of a group: its blend on the group's stream, which then joins the call's stream
+  // phase 2b of a group: its blend on the group's stream, which then joins the call's stream.
+  // The join comes right after the blend and before the views' mailbox events: those carry a
+  // system-scope release (the host reads the status words), each a drain and L2 write-back that
+  // would otherwise sit between the blend and the backward waiting on it.  Round 5
+  // (profiles/r05_stream_gaps.txt): blending every group on the call's stream instead measured
+  // slower (the groups' blends no longer overlap, and the mailbox events then sit in-stream).
   auto phase2b = [&](int gi) -> int {
     Group& G = grp[(size_t)gi];
     const int nl = (int)G.live.size();
@@ -1336,6 +1344,12 @@ int views_forward_batched(const FwdModel& m, std::vector<FwdCam>& cams, gsr_view
       GSR_CHECK(launch_render_forward_views(G.ras, nl, stream));
       PROF_END(RENDER_FWD);
     }
+    if (G.st != call_stream) {
+      hipEvent_t e = join_event(gi);
+      if (!e || hipEventRecord(e, G.st) != hipSuccess ||
+          hipStreamWaitEvent(call_stream, e, 0) != hipSuccess)
+        return fail(GSR_ERR_HIP, "joining group %d's stream failed", gi);
+    }
     for (int k = 0; k < G.n; k++) {
       const int v = G.v0 + k;
       FwdCam& c = cams[(size_t)v];
@@ -1344,12 +1358,6 @@ int views_forward_batched(const FwdModel& m, std::vector<FwdCam>& cams, gsr_view
       gsr_view& out = views[v];
       out.geom_buffer = c.gbase; out.binning_buffer = c.bbase; out.image_buffer = c.ibase;
       out.num_rendered = c.num_rendered; out.num_instances = c.num_instances;
-    }
-    if (G.st != call_stream) {
-      hipEvent_t e = join_event(gi);
-      if (!e || hipEventRecord(e, G.st) != hipSuccess ||
-          hipStreamWaitEvent(call_stream, e, 0) != hipSuccess)
-        return fail(GSR_ERR_HIP, "joining group %d's stream failed", gi);
     }
     return GSR_OK;
   };
@@ -1407,10 +1415,13 @@ int gsr_rasterize_views_fused(int V, gsr_view* views, int image_height, int imag
   hipEvent_t start = join_event(kFwdSlots);
   if (!start || hipEventRecord(start, call_stream) != hipSuccess)
     return fail(GSR_ERR_HIP, "event record on the call's stream failed");
-  for (int v = 0; v < V; v++)
-    if (cams[(size_t)v].stream != call_stream &&
-        hipStreamWaitEvent(cams[(size_t)v].stream, start, 0) != hipSuccess)
+  for (int v = 0; v < V; v++) {  // once per distinct stream
+    hipStream_t s = cams[(size_t)v].stream;
+    bool seen = s == call_stream;
+    for (int u = 0; u < v && !seen; u++) seen = cams[(size_t)u].stream == s;
+    if (!seen && hipStreamWaitEvent(s, start, 0) != hipSuccess)
       return fail(GSR_ERR_HIP, "stream wait failed");
+  }
   (void)inflight;  // one group in flight per distinct view stream
   // two groups: group 1's binning overlaps group 0's blend
   return views_forward_batched(m, cams, views, call_stream, 2);

@@ -150,8 +150,9 @@ class ViewPipeline:
                 main.wait_stream(s)
             return out
 
+        # one call: the library orders its streams after the current one itself
         out = self._step(items, issue, model, campos_of, reducer, sliced=True,
-                         after_slice=after_slice)
+                         after_slice=after_slice, join_side=n > 1)
         return out[0] if n == 1 else out
 
     def prepare_next(self, model, items, campos_of=lambda cam: cam.camera_center):
@@ -177,7 +178,8 @@ class ViewPipeline:
             raise ValueError("ViewPipeline.run: a reducer with defer_sh needs model= (the SH "
                              "leaves are reduced after the deferred flush)")
 
-    def _step(self, items, issue, model, campos_of, reducer, sliced=False, after_slice=None):
+    def _step(self, items, issue, model, campos_of, reducer, sliced=False, after_slice=None,
+              join_side=True):
         import diff_gaussian_rasterization as dgr
         main = torch.cuda.current_stream(self.device)
         self.rows_done = False
@@ -198,8 +200,13 @@ class ViewPipeline:
                                      model.active_sh_degree, campos, buffers=self._pre_bufs)
             # reuse next step: its pre-pass is issued on this stream after this step's join
             self._pre_bufs = pre.buffers
-        for s in self.side:
-            s.wait_stream(main)  # inputs prepared on the main stream (zeroed grads, pre-pass)
+        if join_side and self.side:
+            # inputs prepared on the main stream (zeroed grads, pre-pass): one event for all sides
+            # (each event record after a kernel costs the GPU a few us before the next launch)
+            ev = torch.cuda.Event()
+            ev.record(main)
+            for s in self.side:
+                s.wait_event(ev)
         out = []
         sh_leaves = ()
         on_rows, chunk = None, 0
