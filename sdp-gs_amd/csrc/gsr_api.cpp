@@ -1266,6 +1266,15 @@ int views_forward_batched(const FwdModel& m, std::vector<FwdCam>& cams, gsr_view
     SortSpec ts[kMaxBatchViews];
     const uint32_t ntiles = cams[(size_t)G.live[0]].gx * cams[(size_t)G.live[0]].gy;
     const int tbits = tile_bits(ntiles);
+    // Keys-only tile sort when tile id and Gaussian id fit one 32-bit key (tile << pack | gid:
+    // 12 + 20 bits at 1008x756 and P <= 2^20): the duplication writes 4 B per instance instead of
+    // 8, every pass but the last moves 4 B instead of 8 each way, and the last pass writes the
+    // same (tile, gid) pairs the pair sort does -- a stable sort on the tile bits keeps each
+    // tile's depth order, so the result is bit-identical.  The deterministic rows path sorts
+    // instance indices (egid) and keeps the pair sort.
+    const uint32_t pack = (!m.rows && tbits <= 16 && (uint64_t)P <= (1ull << (32 - tbits)))
+                              ? (uint32_t)(32 - tbits)
+                              : 0u;
     {  // the group's binning buffers in one allocation callback (sizes from the read-back)
       size_t off[kMaxBatchViews + 1] = {0};
       for (int l = 0; l < nl; l++) {
@@ -1289,8 +1298,9 @@ int views_forward_batched(const FwdModel& m, std::vector<FwdCam>& cams, gsr_view
                        SideClear{b.sort.aux, sort_clear_bytes(b.sort, R, tbits)},
                        SideClear{c.im.ranges, sizeof(uint2) * ntiles},
                        m.rows ? b.egid : nullptr, m.rows ? g.ebeg : nullptr, b.tag,
-                       bin_layout_tag(m.det, m.rows)};
+                       bin_layout_tag(m.det, m.rows), pack};
       ts[l] = SortSpec{b.tkey_a, b.tval_a, b.tkey_b, b.tval_b, (size_t)R, b.sort, nullptr};
+      ts[l].lo = (int)pack;
     }
     PROF_BEGIN(DUPLICATE);
     GSR_CHECK(launch_duplicate_views(dup, nl, stream));

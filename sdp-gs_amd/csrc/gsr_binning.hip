@@ -43,7 +43,7 @@ __device__ __forceinline__ void duplicate_body(int P, const uint32_t* __restrict
                                                    SideClear clear0, SideClear clear1,
                                                    uint32_t* __restrict__ egid,
                                                    uint32_t* __restrict__ ebeg, uint32_t blk,
-                                                   uint32_t nblk) {
+                                                   uint32_t nblk, uint32_t pack = 0) {
   constexpr int kWin = 256;  // instances per wave window
   __shared__ uint32_t s_key[kThreads / 64][kWin];
   __shared__ uint32_t s_val[kThreads / 64][kWin];
@@ -106,8 +106,8 @@ __device__ __forceinline__ void duplicate_body(int P, const uint32_t* __restrict
         row_range(y);
         continue;
       }
-      s_key[wid][off - wbeg] = y * gx + x;
-      s_val[wid][off - wbeg] = egid ? off : gid;
+      s_key[wid][off - wbeg] = pack ? (((y * gx + x) << pack) | gid) : y * gx + x;
+      if (!pack) s_val[wid][off - wbeg] = egid ? off : gid;
       if (egid) s_eg[wid][off - wbeg] = gid;
       x++;
       off++;
@@ -115,7 +115,7 @@ __device__ __forceinline__ void duplicate_body(int P, const uint32_t* __restrict
     wave_sync();
     for (uint32_t i = (uint32_t)lane; i < wend - wbeg; i += 64) {
       tkey[wbeg + i] = s_key[wid][i];
-      tval[wbeg + i] = s_val[wid][i];
+      if (!pack) tval[wbeg + i] = s_val[wid][i];
       if (egid) egid[wbeg + i] = s_eg[wid][i];
     }
     wave_sync();
@@ -226,7 +226,8 @@ __global__ __launch_bounds__(kThreads) void duplicate_views_kernel(DupViews m) {
   const DupSpec& j = m.j[k];
   if (j.tag && blockIdx.x == m.first[k] && threadIdx.x == 0) *j.tag = j.tag_val;
   duplicate_body(j.P, j.order, j.offsets, j.rec, j.gx, j.gy, j.tkey, j.tval, j.R, j.clear0,
-                 j.clear1, j.egid, j.ebeg, blockIdx.x - m.first[k], m.first[k + 1] - m.first[k]);
+                 j.clear1, j.egid, j.ebeg, blockIdx.x - m.first[k], m.first[k + 1] - m.first[k],
+                 j.pack);
 }
 
 __global__ __launch_bounds__(kThreads) void tile_ranges_views_kernel(RangesViews m) {
@@ -271,6 +272,10 @@ hipError_t launch_duplicate_views(const DupSpec* v, int V, hipStream_t s) {
   m.V = V;
   m.first[0] = 0;
   for (int k = 0; k < V; k++) {
+    const DupSpec& d = v[k];
+    if (d.pack && (d.egid || d.pack >= 32u || (uint64_t)d.P > (1ull << d.pack) ||
+                   (uint64_t)d.gx * d.gy > (1ull << (32u - d.pack))))
+      return hipErrorInvalidValue;  // tile << pack | gid must fit 32 bits
     m.j[k] = v[k];
     m.first[k + 1] = m.first[k] + (uint32_t)((v[k].P + kThreads - 1) / kThreads);
   }

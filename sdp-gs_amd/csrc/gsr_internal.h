@@ -150,6 +150,10 @@ struct SortSpec {
   SortScratch scratch;
   const uint32_t* key_payload;
   uint32_t *kc = nullptr, *vc = nullptr;  // planned sort (radix_sort_pairs): all views or none
+  // keys-only packed sort (lo > 0; all views or none, va / vb only receive the last pass's
+  // values): the keys carry the sort key in bits [lo, lo + bits) and the value in bits [0, lo);
+  // the result pair is (key >> lo, key & (2^lo - 1)) in the buffers the pair sort would use
+  int lo = 0;
 };
 hipError_t radix_sort_pairs_views(const SortSpec* v, int V, int bits, bool* result_in_b,
                                   hipStream_t s, bool sentinel_anywhere, bool precleared);
@@ -406,6 +410,9 @@ struct DupSpec {
   uint32_t* ebeg;
   uint32_t* tag = nullptr;  // written with tag_val by the launch (the binning buffer's layout tag)
   uint32_t tag_val = 0;
+  // > 0: packed keys tile << pack | gid into tkey for the keys-only tile sort (tval not written;
+  // needs gid < 2^pack, no egid)
+  uint32_t pack = 0;
 };
 hipError_t launch_duplicate_views(const DupSpec* v, int V, hipStream_t s);
 struct RangesSpec {

@@ -232,7 +232,8 @@ __host__ __device__ __forceinline__ int sort_digit_width(int bits) {
 __device__ __forceinline__ void radix_totals_body(const uint32_t* __restrict__ keys, size_t n,
                                                   int bits, uint32_t* __restrict__ totals,
                                                   uint32_t* __restrict__ nsent_out,
-                                                  int skip_sentinel, uint32_t blk, uint32_t nblk) {
+                                                  int skip_sentinel, uint32_t blk, uint32_t nblk,
+                                                  int lo = 0) {
   __shared__ uint32_t cnt[kSortMaxPasses][256];
   __shared__ uint32_t nsent;  // sentinel keys of this workgroup (all digits 0xff)
 #pragma unroll
@@ -260,7 +261,7 @@ __device__ __forceinline__ void radix_totals_body(const uint32_t* __restrict__ k
         if (sm && (threadIdx.x & 63) == 0) atomicAdd(&nsent, (uint32_t)__popcll(sm));
       }
       for (int p = 0; p < passes; p++) {
-        const uint32_t d = (key[r] >> (dw * p)) & dmask;
+        const uint32_t d = (key[r] >> (lo + dw * p)) & dmask;
         // typical depth keys share their top byte across a wave: one LDS add instead of 64
         // serialised same-address atomics
         const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
@@ -371,13 +372,21 @@ __device__ __forceinline__ void onesweep_body(
     int bits, const uint32_t* __restrict__ totals, const uint32_t* __restrict__ nsent_sh,
     uint32_t* __restrict__ ticket, uint64_t* __restrict__ status, uint32_t* __restrict__ err,
     uint32_t* __restrict__ kout, uint32_t* __restrict__ vout, const uint32_t* __restrict__ kpay,
-    uint32_t blk, uint32_t nblk) {
+    uint32_t blk, uint32_t nblk, uint32_t ulo = 0) {
   constexpr int kSortWaves = NT / 64, kSortThreads = NT;
-  // one sorted element out at position o: its value, and its key -- or (last pass) the payload
+  // Keys-only sort (vin null, grid-uniform): packed keys whose low bits carry the value; the
+  // last pass (ulo > 0) writes them out as the pair (key >> ulo, key & (2^ulo - 1)), earlier
+  // passes the packed key alone (vout null).
+  // One sorted element out at position o: its value, and its key -- or (last pass) the payload
   // gathered by its value, kpay[v]
   auto emit = [&](uint32_t o, uint32_t v, uint32_t k) {
+    if (ulo) {
+      kout[o] = k >> ulo;
+      vout[o] = k & ((1u << ulo) - 1u);
+      return;
+    }
     kout[o] = kpay ? kpay[min(v, (uint32_t)n - 1u)] : k;
-    vout[o] = v;
+    if (vout) vout[o] = v;
   };
   constexpr int kKeysPerThread = kSortTile / NT, kKeysPerWave = kKeysPerThread * 64;
   static_assert(NT >= 256 && kSortTile % NT == 0, "one-sweep tile shape");
@@ -415,7 +424,7 @@ __device__ __forceinline__ void onesweep_body(
     if (ndig <= 1u) {
       const size_t b0 = (size_t)blk * kSortTile;
       const size_t e0 = min(n, b0 + (size_t)kSortTile);
-      for (size_t i = b0 + (size_t)t; i < e0; i += NT) emit((uint32_t)i, vin[i], kin[i]);
+      for (size_t i = b0 + (size_t)t; i < e0; i += NT) emit((uint32_t)i, vin ? vin[i] : 0u, kin[i]);
       return;
     }
   }
@@ -440,7 +449,7 @@ __device__ __forceinline__ void onesweep_body(
   for (int r = 0; r < kKeysPerThread; r++) {
     const size_t i = wbase + (size_t)r * 64 + lane;
     key[r] = i < n ? kin[i] : 0u;
-    val[r] = i < n ? vin[i] : 0u;
+    val[r] = (vin && i < n) ? vin[i] : 0u;
   }
   // stable rank inside the wave's 1024 consecutive keys
   const uint64_t lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
@@ -492,7 +501,7 @@ __device__ __forceinline__ void onesweep_body(
       const uint32_t d = (key[r] >> shift) & mask;
       const uint32_t pos = s_cnt[wid][d] + rk[r];
       s_k[pos] = key[r];
-      s_v[pos] = val[r];
+      if (vin) s_v[pos] = val[r];
     }
   }
   uint32_t excl = 0;
@@ -579,7 +588,7 @@ __device__ __forceinline__ void onesweep_body(
   for (uint32_t i = (uint32_t)t; i < nvalid; i += kSortThreads) {
     const uint32_t k = s_k[i];
     const uint32_t o = s_gofs[(k >> shift) & mask] + i;
-    if (o < n) emit(o, s_v[i], k);  // only a timed-out look-back (error word raised) can produce o >= n
+    if (o < n) emit(o, vin ? s_v[i] : 0u, k);  // only a timed-out look-back (error word raised) can produce o >= n
   }
 }
 
@@ -622,6 +631,7 @@ struct SortPassJob {
   uint32_t* aux;         // totals, sentinel counts, tickets, error word (kSortAux*)
   uint64_t* status;      // this pass's look-back words
   uint32_t n;
+  uint32_t ulo;          // keys-only sort, last pass: the value bits to unpack (else 0)
 };
 struct SortPassViews {
   SortPassJob j[kMaxBatchViews];
@@ -636,11 +646,11 @@ __device__ __forceinline__ int batch_view(const uint32_t* first, int V, uint32_t
 }
 
 __global__ __launch_bounds__(kThreads) void radix_totals_views_kernel(SortPassViews m, int bits,
-                                                                      int skip_sentinel) {
+                                                                      int skip_sentinel, int lo) {
   const int k = batch_view(m.first, m.V, blockIdx.x);
   const SortPassJob& j = m.j[k];
   radix_totals_body(j.kin, j.n, bits, j.aux + kSortAuxTotals, j.aux + kSortAuxSent, skip_sentinel,
-                    blockIdx.x - m.first[k], m.first[k + 1] - m.first[k]);
+                    blockIdx.x - m.first[k], m.first[k + 1] - m.first[k], lo);
 }
 
 // one workgroup per view (planned sorts)
@@ -663,7 +673,7 @@ __global__ __launch_bounds__(NT, NT == 1024 ? 8 : (NT == 512 ? 6 : 1)) void radi
   onesweep_body<NT>(o.kin, o.vin, j.n, shift, bits, j.aux + kSortAuxTotals + 256 * pass,
                     sentinel ? j.aux + kSortAuxSent : nullptr, j.aux + kSortAuxTickets + 8 * pass,
                     j.status, j.aux + kSortAuxErr, o.kout, o.vout, o.last ? j.kpay : nullptr,
-                    blockIdx.x - m.first[k], m.first[k + 1] - m.first[k]);
+                    blockIdx.x - m.first[k], m.first[k + 1] - m.first[k], j.ulo);
 }
 
 struct ScanJob {
@@ -1045,6 +1055,11 @@ hipError_t radix_sort_pairs_views(const SortSpec* v, int V, int bits, bool* resu
   SortPassViews m{};
   m.V = V;
   const bool planned = v[0].kc != nullptr;
+  // keys-only packed sort (SortSpec::lo): every view or none, not planned, no payload gather
+  const int lo = v[0].lo;
+  if (lo < 0 || lo + bits > 32 || (lo && planned)) return hipErrorInvalidValue;
+  for (int k = 0; k < V; k++)
+    if (v[k].lo != lo || (lo && v[k].key_payload)) return hipErrorInvalidValue;
   uint32_t tfirst[kMaxBatchViews + 1] = {0}, ofirst[kMaxBatchViews + 1] = {0};
   for (int k = 0; k < V; k++) {
     const size_t n = v[k].n;
@@ -1066,10 +1081,12 @@ hipError_t radix_sort_pairs_views(const SortSpec* v, int V, int bits, bool* resu
     for (int k = 0; k < V; k++) {
       const SortSpec& w = v[k];
       SortPassJob& j = m.j[k];
+      const bool last = p == passes - 1;
       j.kin = b_in ? w.kb : w.ka;
-      j.vin = b_in ? w.vb : w.va;
+      j.vin = lo ? nullptr : (b_in ? w.vb : w.va);
       j.kout = (b_in && !planned) ? w.ka : w.kb;
-      j.vout = (b_in && !planned) ? w.va : w.vb;
+      j.vout = (lo && !last) ? nullptr : ((b_in && !planned) ? w.va : w.vb);
+      j.ulo = (lo && last) ? (uint32_t)lo : 0u;
       j.kc = w.kc;
       j.vc = w.vc;
       j.kpay = (planned || p == passes - 1) ? w.key_payload : nullptr;
@@ -1080,7 +1097,7 @@ hipError_t radix_sort_pairs_views(const SortSpec* v, int V, int bits, bool* resu
   };
   fill(0, tfirst);
   hipLaunchKernelGGL(radix_totals_views_kernel, dim3(tfirst[V]), dim3(kThreads), 0, s, m, bits,
-                     sentinel_anywhere ? 1 : 0);
+                     sentinel_anywhere ? 1 : 0, lo);
   if (planned)
     hipLaunchKernelGGL(sort_plan_views_kernel, dim3(V), dim3(kThreads), 0, s, m, bits,
                        sentinel_anywhere ? 1 : 0);
@@ -1092,11 +1109,11 @@ hipError_t radix_sort_pairs_views(const SortSpec* v, int V, int bits, bool* resu
     const int shift = dw * p;
     const int dbits = (bits - shift) < dw ? (bits - shift) : dw;
     if (nt == 1024)
-      hipLaunchKernelGGL(radix_onesweep_views_kernel<1024>, dim3(nb), dim3(1024), 0, s, m, p, shift, dbits,
-                         sentinel_anywhere ? 1 : 0);
+      hipLaunchKernelGGL(radix_onesweep_views_kernel<1024>, dim3(nb), dim3(1024), 0, s, m, p,
+                         lo + shift, dbits, sentinel_anywhere ? 1 : 0);
     else
-      hipLaunchKernelGGL(radix_onesweep_views_kernel<512>, dim3(nb), dim3(512), 0, s, m, p, shift, dbits,
-                         sentinel_anywhere ? 1 : 0);
+      hipLaunchKernelGGL(radix_onesweep_views_kernel<512>, dim3(nb), dim3(512), 0, s, m, p,
+                         lo + shift, dbits, sentinel_anywhere ? 1 : 0);
   }
   *result_in_b = planned || (passes & 1) != 0;
   return hipGetLastError();
