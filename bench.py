@@ -20,6 +20,7 @@ over RCCL.  GSR_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs.
 from __future__ import annotations
 
 import argparse
+import copy
 import json
 import math
 import os
@@ -132,6 +133,11 @@ def _stage_bytes(stage, P, Pv, R, T, HW, D, C, tile_passes, acc, defer_sh, preco
     sh_fwd = 13 if precolor else sh
     sh_bwd = 36 if (precolor and defer_sh) else sh
     grads = 12 + 12 + 4 + 12 + 16 + 12 + (0 if defer_sh else sh)  # means2D/3D, op, scale, rot, lang, SH
+    # keys-only tile sort (gsr_api.cpp phase 2a): tile << (32 - tile bits) | gid in one key when
+    # the ids fit -- 4-B instances from the duplication, 4 B each way per pass but the last,
+    # which reads 4 and writes the 8-B (tile, gid) pair
+    tbits = max(0, (T - 1).bit_length())
+    packed = 0 < tbits <= 16 and P <= (1 << (32 - tbits))
     return {
         # means (all); scale, rot, opacity, SH, language (visible); radii/tiles/key/value (all);
         # 64-B splat record + clamp bits (visible), the 64-B gradient accumulator row it zeroes (all)
@@ -140,9 +146,10 @@ def _stage_bytes(stage, P, Pv, R, T, HW, D, C, tile_passes, acc, defer_sh, preco
         # sort skips constant digits) reads and writes key+value, the last gathers the tile count
         "depth_sort": P * 4 + depth_passes * P * 16 + P * 4,
         "scan": P * 12,
-        # offsets (all), order + 48-B record gather (non-empty), R (tile, id) pairs
-        "duplicate": P * 8 + Pv * (4 + 48) + R * 8,
-        "tile_sort": R * 4 + tile_passes * R * 16,
+        # offsets (all), order + 48-B record gather (non-empty), R (tile, id) pairs / packed keys
+        "duplicate": P * 8 + Pv * (4 + 48) + R * (4 if packed else 8),
+        "tile_sort": (R * 4 + (tile_passes - 1) * R * 8 + R * 12) if packed
+                     else R * 4 + tile_passes * R * 16,
         "ranges": R * 4 + T * 8,
         # point_list + 64-B record per instance, ranges/tile_last, C outputs + final_T + n_contrib
         "render_fwd": R * (4 + 64) + T * 12 + HW * (4 * C + 8),
@@ -501,16 +508,23 @@ def main():
         except (OSError, ValueError):
             pass
 
-    # the CPU baseline samples the headline model before the training legs change it
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_baseline_views > 0:
-        cpu = cpu_baseline(model, cams_all[: args.cpu_baseline_views], dimg, ddep, dfeat, deg,
-                           args.cpu_threads)
+    # The CPU baseline samples the headline model (a copy taken before the training legs change
+    # it) and runs after the legs: its host thread pools (OpenMP / torch intra-op, 16 threads)
+    # must not compete with the legs' host-issued GPU work -- twice a leg measured at a third /
+    # half of its rate when the baseline ran first.
+    want_cpu = rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_baseline_views > 0
+    snap = copy.deepcopy(model) if (want_cpu and not args.no_extra_legs) else model
 
     legs = {}
     if not args.no_extra_legs:
         legs = extra_legs(args, model, step_cams, pool, n_views, views, reducer, timed_region,
                           rank, world, dev, (P, W, H, deg), (dimg, ddep, dfeat), bg)
+
+    cpu = None
+    if want_cpu:
+        cpu = cpu_baseline(snap, cams_all[: args.cpu_baseline_views], dimg, ddep, dfeat, deg,
+                           args.cpu_threads)
+    del snap
 
     if rank == 0:
         line = {

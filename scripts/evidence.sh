@@ -20,7 +20,7 @@ fi
 timeout -k 10 600 python bench.py > $OUT/b_$TAG.json 2> $OUT/b_$TAG.err || { tail -5 $OUT/b_$TAG.err; exit 3; }
 python3 -c "import json;d=json.load(open('$OUT/b_$TAG.json'));print('bench', d['value'], d['roofline'])"
 rm -rf $OUT/prof_$TAG
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run -- python3 bench.py --no-cpu-baseline > $OUT/b_prof_$TAG.json 2> $OUT/b_prof_$TAG.err || exit 4
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run -- python3 bench.py --no-cpu-baseline --no-extra-legs > $OUT/b_prof_$TAG.json 2> $OUT/b_prof_$TAG.err || exit 4
 find $OUT/prof_$TAG -name "*kernel_stats.csv"
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke_$TAG.log 2>&1; rc=$?
 echo "smoke rc=$rc"; tail -2 $OUT/smoke_$TAG.log; [ $rc -eq 0 ] || exit $rc
