@@ -535,6 +535,9 @@ __global__ __launch_bounds__(kThreads) void preprocess_bwd_kernel(BwdPreArgs a) 
 // gaussian_bwd, their gradients summed in registers (RegSink: the same additions, in the same
 // order, as one launch per view) and written once -- the parameters and the leaves' gradients
 // cross HBM once per step instead of once per view.  View 0's `accumulate` decides store / add.
+// waves per SIMD the views kernel is compiled for: 1 = the compiler's choice (143 VGPRs, 3 waves).
+// Forcing 4 (128 VGPRs) spills 10 registers and measured 8 % slower, 4 without the per-view row
+// prefetch 17 % slower (profiles/r05_pbwd_occupancy_ab.txt)
 #ifndef GSR_BWDV_MINBLK
 #define GSR_BWDV_MINBLK 1
 #endif
@@ -627,8 +630,12 @@ __global__ __launch_bounds__(kThreads, GSR_BWDV_MINBLK) void preprocess_bwd_view
     if (valid) views_body<ACC>(m, i, nullptr);
     return;
   }
-  // the views' dL/dRGB planes ([V][3][kThreads] floats), then the same LDS as staging planes
-  __shared__ float4 s_sh4[SH ? kThreads * kShMaxFloats / 4 : 1];
+  // the views' dL/dRGB planes ([V][3][kThreads] floats, V <= kMaxBwdViews), then the same LDS as
+  // the staging planes of half the workgroup's rows at a time (24 KB instead of 48: the LDS no
+  // longer caps the launch at 3 workgroups per CU)
+  constexpr int kHalf = kThreads / 2;
+  static_assert(kMaxBwdViews * 3 * kThreads == kHalf * kShMaxFloats, "LDS: planes = half staging");
+  __shared__ float4 s_sh4[SH ? kHalf * kShMaxFloats / 4 : 1];
   __shared__ uint8_t s_live[kThreads];
   float* s_sh = reinterpret_cast<float*>(s_sh4);
   const BwdPreArgs& a0 = m.v[0];
@@ -649,24 +656,33 @@ __global__ __launch_bounds__(kThreads, GSR_BWDV_MINBLK) void preprocess_bwd_view
       for (int k = 0; k < 16; k++) g[k] = v == 0 ? b[k] * dRGB : g[k] + b[k] * dRGB;
     }
   }
-  __syncthreads();  // every dL/dRGB plane read: the LDS becomes the staging planes
   const ShPlane p0{nullptr, a0.dL_dsh, 3, 0};
-  const ShPlane p1{nullptr, a0.dL_dsh_rest, (a0.M - 1) * 3, kThreads * 3};
-  if (valid) {
-    float* r0 = s_sh + p0.lds + t * p0.w;
-    float* r1 = s_sh + p1.lds + t * p1.w;
-    r0[0] = g[0].x; r0[1] = g[0].y; r0[2] = g[0].z;
+  const ShPlane p1{nullptr, a0.dL_dsh_rest, (a0.M - 1) * 3, kHalf * 3};
+#pragma unroll 1
+  for (int h = 0; h < 2; h++) {
+    // h = 0: every dL/dRGB plane read, the LDS becomes the staging planes; h = 1: the first
+    // half's rows are out
+    __syncthreads();
+    const int r = t - h * kHalf;
+    if (valid && r >= 0 && r < kHalf) {
+      float* r0 = s_sh + p0.lds + r * p0.w;
+      float* r1 = s_sh + p1.lds + r * p1.w;
+      r0[0] = g[0].x; r0[1] = g[0].y; r0[2] = g[0].z;
 #pragma unroll
-    for (int k = 1; k < 16; k++) {  // static indices: g stays in registers
-      if (k < a0.M) {
-        const V3 v = k < used ? g[k] : v3(0, 0, 0);
-        r1[3 * k - 3] = v.x; r1[3 * k - 2] = v.y; r1[3 * k - 1] = v.z;
+      for (int k = 1; k < 16; k++) {  // static indices: g stays in registers
+        if (k < a0.M) {
+          const V3 v = k < used ? g[k] : v3(0, 0, 0);
+          r1[3 * k - 3] = v.x; r1[3 * k - 2] = v.y; r1[3 * k - 1] = v.z;
+        }
       }
     }
+    __syncthreads();
+    const int hn = min(kHalf, n - h * kHalf);  // workgroup-uniform
+    if (hn > 0) {
+      stage<kThreads, false, ACC>(p0, (int)base + h * kHalf, hn, s_live + h * kHalf, s_sh);
+      stage<kThreads, false, ACC>(p1, (int)base + h * kHalf, hn, s_live + h * kHalf, s_sh);
+    }
   }
-  __syncthreads();
-  stage<kThreads, false, ACC>(p0, (int)base, n, s_live, s_sh);
-  stage<kThreads, false, ACC>(p1, (int)base, n, s_live, s_sh);
 }
 
 // Deferred SH gradients of a multi-view step: per Gaussian, for each view v in order,
