@@ -320,9 +320,13 @@ constexpr int kPcThreads = GSR_SH_THREADS;
 // view: sh_to_rgb (forward.cu:20-71, the forward's own function) -> colour [3][P] + clamp bits,
 // and sh_dir_jacobian (backward.cu:56-131) -> dRGB/ddir [9][P].  The rows go through LDS
 // (gsr_stage.h) so the global reads are coalesced 16-byte vectors.
+// The rows are staged half a workgroup at a time (24 KB of LDS instead of 48, so the LDS no longer
+// caps the launch at 3 workgroups per CU) and copied into registers, the colour and the Jacobian
+// then read the registers.
 template <bool COL, bool JAC>
 __global__ __launch_bounds__(kPcThreads) void sh_precolor_kernel(PrecolorArgs a) {
-  __shared__ float4 s_sh4[kPcThreads * kShMaxFloats / 4];
+  constexpr int kHalf = kPcThreads / 2;
+  __shared__ float4 s_sh4[kHalf * kShMaxFloats / 4];
   __shared__ uint8_t s_live[kPcThreads];
   float* s_sh = reinterpret_cast<float*>(s_sh4);
   const int base = (int)(a.row0 + blockIdx.x * kPcThreads);
@@ -331,22 +335,29 @@ __global__ __launch_bounds__(kPcThreads) void sh_precolor_kernel(PrecolorArgs a)
   const size_t i = (size_t)base + t;
   s_live[t] = t < n;
   const ShPlane p0{a.sh_dc, nullptr, 3, 0};
-  const ShPlane p1{a.sh_rest, nullptr, (a.M - 1) * 3, kPcThreads * 3};
-  __syncthreads();
-  stage<kPcThreads, true, false>(p0, base, n, s_live, s_sh);
-  stage<kPcThreads, true, false>(p1, base, n, s_live, s_sh);
-  __syncthreads();
-  if (t >= n) return;
-  const float* r0 = s_sh + p0.lds + t * p0.w;
-  const float* r1 = s_sh + p1.lds + t * p1.w;
+  const ShPlane p1{a.sh_rest, nullptr, (a.M - 1) * 3, kHalf * 3};
   const int used = (a.D + 1) * (a.D + 1);
   V3 c[16];
-  if (JAC) {
-    c[0] = v3(r0[0], r0[1], r0[2]);
+#pragma unroll 1
+  for (int h = 0; h < 2; h++) {
+    const int hn = min(kHalf, n - h * kHalf);  // workgroup-uniform
+    __syncthreads();  // (h = 1: the first half's rows are in registers)
+    if (hn > 0) {
+      stage<kPcThreads, true, false>(p0, base + h * kHalf, hn, s_live + h * kHalf, s_sh);
+      stage<kPcThreads, true, false>(p1, base + h * kHalf, hn, s_live + h * kHalf, s_sh);
+    }
+    __syncthreads();
+    const int r = t - h * kHalf;
+    if (r >= 0 && r < hn) {
+      const float* r0 = s_sh + p0.lds + r * p0.w;
+      const float* r1 = s_sh + p1.lds + r * p1.w;
+      c[0] = v3(r0[0], r0[1], r0[2]);
 #pragma unroll
-    for (int k = 1; k < 16; k++)
-      c[k] = (k < used && k < a.M) ? v3(r1[3 * k - 3], r1[3 * k - 2], r1[3 * k - 1]) : v3(0, 0, 0);
+      for (int k = 1; k < 16; k++)
+        c[k] = (k < used && k < a.M) ? v3(r1[3 * k - 3], r1[3 * k - 2], r1[3 * k - 1]) : v3(0, 0, 0);
+    }
   }
+  if (t >= n) return;
   const V3 p_orig = v3(a.means3D[3 * i], a.means3D[3 * i + 1], a.means3D[3 * i + 2]);
   for (int v = 0; v < a.nviews; v++) {
     const float* cp = a.campos[v];
@@ -359,7 +370,7 @@ __global__ __launch_bounds__(kPcThreads) void sh_precolor_kernel(PrecolorArgs a)
     const size_t P = (size_t)a.P;
     if (COL) {
       uint8_t cl;
-      const V3 col = sh_to_rgb(r0, r1, a.D, dir, cl);
+      const V3 col = sh_to_rgb_at([&](int k) { return c[k]; }, a.D, dir, cl);
       float* co = a.color[v] + i;
       stream_st(co, col.x); stream_st(co + P, col.y); stream_st(co + 2 * P, col.z);
       stream_st(a.clamp[v] + i, cl);

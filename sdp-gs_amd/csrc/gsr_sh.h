@@ -10,10 +10,9 @@ namespace gsr {
 // forward.cu:20-71 (float32, same evaluation order as the CPU restatement)
 // s0: coefficient 0 of this Gaussian, s1: its coefficients 1.. (contiguous); for the reference's
 // [P,M,3] layout s1 = s0 + 3, for the fused split layout s0 = features_dc, s1 = features_rest.
-__device__ __forceinline__ V3 sh_to_rgb(const float* __restrict__ s0, const float* __restrict__ s1,
-                                        int deg, V3 dir, uint8_t& clamped) {
-#define SH(k) ((k) == 0 ? v3(s0[0], s0[1], s0[2]) \
-                        : v3(s1[3 * ((k) - 1)], s1[3 * ((k) - 1) + 1], s1[3 * ((k) - 1) + 2]))
+// (coefficient k of the row from SH(k): LDS rows or registers, the same operations either way)
+template <class ShAt>
+__device__ __forceinline__ V3 sh_to_rgb_at(ShAt SH, int deg, V3 dir, uint8_t& clamped) {
   V3 result = SH_C0 * SH(0);
   if (deg > 0) {
     const float x = dir.x, y = dir.y, z = dir.z;
@@ -37,10 +36,18 @@ __device__ __forceinline__ V3 sh_to_rgb(const float* __restrict__ s0, const floa
       }
     }
   }
-#undef SH
   result = v3(result.x + 0.5f, result.y + 0.5f, result.z + 0.5f);
   clamped = (uint8_t)((result.x < 0) | ((result.y < 0) << 1) | ((result.z < 0) << 2));
   return v3(fmaxf(result.x, 0.0f), fmaxf(result.y, 0.0f), fmaxf(result.z, 0.0f));
+}
+__device__ __forceinline__ V3 sh_to_rgb(const float* __restrict__ s0, const float* __restrict__ s1,
+                                        int deg, V3 dir, uint8_t& clamped) {
+  return sh_to_rgb_at(
+      [&](int k) {
+        return k == 0 ? v3(s0[0], s0[1], s0[2])
+                      : v3(s1[3 * (k - 1)], s1[3 * (k - 1) + 1], s1[3 * (k - 1) + 2]);
+      },
+      deg, dir, clamped);
 }
 
 // dRGB/dsh_k for a normalised direction (backward.cu:36-76): the SH gradient of a view is
