@@ -138,13 +138,16 @@ def _stage_bytes(stage, P, Pv, R, T, HW, D, C, tile_passes, acc, defer_sh, preco
     # which reads 4 and writes the 8-B (tile, gid) pair
     tbits = max(0, (T - 1).bit_length())
     packed = 0 < tbits <= 16 and P <= (1 << (32 - tbits))
+    # the depth sort's values carry the tile counts when id and count fit 32 bits (no gather)
+    vsplit = P <= (1 << (32 - max(1, T.bit_length())))
     return {
         # means (all); scale, rot, opacity, SH, language (visible); radii/tiles/key/value (all);
         # 64-B splat record + clamp bits (visible), the 64-B gradient accumulator row it zeroes (all)
         "preprocess": P * 12 + Pv * (12 + 16 + 4 + sh_fwd + 12) + P * 16 + Pv * (64 + 1) + P * 64,
         # one-sweep: digit totals read the keys once, each 8-bit pass that runs (the planned
-        # sort skips constant digits) reads and writes key+value, the last gathers the tile count
-        "depth_sort": P * 4 + depth_passes * P * 16 + P * 4,
+        # sort skips constant digits) reads and writes key+value; the last gathers the tile count
+        # unless the values carry it
+        "depth_sort": P * 4 + depth_passes * P * 16 + (0 if vsplit else P * 4),
         "scan": P * 12,
         # offsets (all), order + 48-B record gather (non-empty), R (tile, id) pairs / packed keys
         "duplicate": P * 8 + Pv * (4 + 48) + R * (4 if packed else 8),

@@ -154,6 +154,9 @@ struct SortSpec {
   // values): the keys carry the sort key in bits [lo, lo + bits) and the value in bits [0, lo);
   // the result pair is (key >> lo, key & (2^lo - 1)) in the buffers the pair sort would use
   int lo = 0;
+  // > 0: the values carry a payload in bits [vsplit, 32); the last pass writes (value >> vsplit)
+  // in place of the key and value & (2^vsplit - 1) as the value (no key_payload gather)
+  int vsplit = 0;
 };
 hipError_t radix_sort_pairs_views(const SortSpec* v, int V, int bits, bool* result_in_b,
                                   hipStream_t s, bool sentinel_anywhere, bool precleared);
@@ -290,6 +293,9 @@ struct PreArgs {
   // clamp bits come precomputed (gsr_sh_precolor) instead of being evaluated from the SH rows
   const float* pre_color;
   const uint8_t* pre_clamp;
+  // > 0: the depth sort's value is id | (exact tile count << vpack) (the sort's last pass splits it,
+  // SortSpec::vsplit, instead of gathering the counts by id)
+  uint32_t vpack = 0;
 };
 hipError_t launch_preprocess(const PreArgs& a, hipStream_t s);
 // Several views of one model in one launch (every view's PreArgs share the model fields): per

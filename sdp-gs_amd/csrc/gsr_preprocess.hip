@@ -178,6 +178,7 @@ __device__ __forceinline__ uint32_t preprocess_gaussian(const PreArgs& a, int id
   }
   g.tiles_touched[idx] = count;
   g.dkey_a[idx] = __float_as_uint(depth);
+  if (a.vpack) g.dval_a[idx] = (uint32_t)idx | (count << a.vpack);
   rec[0 ^ sw] = make_float4(px, py, con_a, con_b);
   rec[1 ^ sw] = make_float4(con_c, op, depth, cr);
   rec[2 ^ sw] = make_float4(cg, cb, in->f0, in->f1);

@@ -372,14 +372,20 @@ __device__ __forceinline__ void onesweep_body(
     int bits, const uint32_t* __restrict__ totals, const uint32_t* __restrict__ nsent_sh,
     uint32_t* __restrict__ ticket, uint64_t* __restrict__ status, uint32_t* __restrict__ err,
     uint32_t* __restrict__ kout, uint32_t* __restrict__ vout, const uint32_t* __restrict__ kpay,
-    uint32_t blk, uint32_t nblk, uint32_t ulo = 0) {
+    uint32_t blk, uint32_t nblk, uint32_t ulo = 0, uint32_t vsplit = 0) {
   constexpr int kSortWaves = NT / 64, kSortThreads = NT;
   // Keys-only sort (vin null, grid-uniform): packed keys whose low bits carry the value; the
   // last pass (ulo > 0) writes them out as the pair (key >> ulo, key & (2^ulo - 1)), earlier
   // passes the packed key alone (vout null).
   // One sorted element out at position o: its value, and its key -- or (last pass) the payload
   // gathered by its value, kpay[v]
+  // (vsplit: the values carry the payload in their high bits -- the last pass splits them)
   auto emit = [&](uint32_t o, uint32_t v, uint32_t k) {
+    if (vsplit) {
+      kout[o] = v >> vsplit;
+      vout[o] = v & ((1u << vsplit) - 1u);
+      return;
+    }
     if (ulo) {
       kout[o] = k >> ulo;
       vout[o] = k & ((1u << ulo) - 1u);
@@ -632,6 +638,7 @@ struct SortPassJob {
   uint64_t* status;      // this pass's look-back words
   uint32_t n;
   uint32_t ulo;          // keys-only sort, last pass: the value bits to unpack (else 0)
+  uint32_t vsplit;       // last pass: split the values at this bit (else 0; SortSpec::vsplit)
 };
 struct SortPassViews {
   SortPassJob j[kMaxBatchViews];
@@ -673,7 +680,8 @@ __global__ __launch_bounds__(NT, NT == 1024 ? 8 : (NT == 512 ? 6 : 1)) void radi
   onesweep_body<NT>(o.kin, o.vin, j.n, shift, bits, j.aux + kSortAuxTotals + 256 * pass,
                     sentinel ? j.aux + kSortAuxSent : nullptr, j.aux + kSortAuxTickets + 8 * pass,
                     j.status, j.aux + kSortAuxErr, o.kout, o.vout, o.last ? j.kpay : nullptr,
-                    blockIdx.x - m.first[k], m.first[k + 1] - m.first[k], j.ulo);
+                    blockIdx.x - m.first[k], m.first[k + 1] - m.first[k], j.ulo,
+                    o.last ? j.vsplit : 0u);
 }
 
 struct ScanJob {
@@ -1059,7 +1067,9 @@ hipError_t radix_sort_pairs_views(const SortSpec* v, int V, int bits, bool* resu
   const int lo = v[0].lo;
   if (lo < 0 || lo + bits > 32 || (lo && planned)) return hipErrorInvalidValue;
   for (int k = 0; k < V; k++)
-    if (v[k].lo != lo || (lo && v[k].key_payload)) return hipErrorInvalidValue;
+    if (v[k].lo != lo || (lo && v[k].key_payload) || v[k].vsplit < 0 || v[k].vsplit >= 32 ||
+        (v[k].vsplit && (v[k].key_payload || lo)))
+      return hipErrorInvalidValue;
   uint32_t tfirst[kMaxBatchViews + 1] = {0}, ofirst[kMaxBatchViews + 1] = {0};
   for (int k = 0; k < V; k++) {
     const size_t n = v[k].n;
@@ -1090,6 +1100,7 @@ hipError_t radix_sort_pairs_views(const SortSpec* v, int V, int bits, bool* resu
       j.kc = w.kc;
       j.vc = w.vc;
       j.kpay = (planned || p == passes - 1) ? w.key_payload : nullptr;
+      j.vsplit = (planned || p == passes - 1) ? (uint32_t)w.vsplit : 0u;
       j.aux = w.scratch.aux;
       j.status = w.scratch.status + (size_t)p * sort_pass_words(w.n);
       j.n = (uint32_t)w.n;
