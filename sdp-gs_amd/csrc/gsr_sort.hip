@@ -104,8 +104,10 @@ __global__ __launch_bounds__(1024) void scan_parts_kernel(uint32_t* __restrict__
 }
 
 // A lane's kScanItems consecutive counts as 16-byte loads and stores when the arrays are aligned
-// (workgroup-uniform test); else one 4-byte access per item
-template <bool GATHER, bool INCLUSIVE>
+// (workgroup-uniform test); else one 4-byte access per item.  RAW: parts holds the workgroups'
+// plain sums (no scan_parts launch) and each workgroup adds up its predecessors' itself -- integer
+// sums, so the same result; one launch fewer in the binning chain.
+template <bool GATHER, bool INCLUSIVE, bool RAW = false>
 __device__ __forceinline__ void scan_final_body(const uint32_t* __restrict__ in,
                                                 const uint32_t* __restrict__ gather, size_t n,
                                                 const uint32_t* __restrict__ parts,
@@ -135,8 +137,17 @@ __device__ __forceinline__ void scan_final_body(const uint32_t* __restrict__ in,
   }
 #pragma unroll
   for (int k = 0; k < kScanItems; k++) s += v[k];
+  uint32_t base_pre;
+  if (RAW) {
+    __shared__ uint32_t lds_p[kThreads / 64];
+    uint32_t ps = 0;
+    for (uint32_t q = threadIdx.x; q < blk; q += kThreads) ps += parts[q];
+    block_excl_scan<kThreads / 64>(ps, lds_p, base_pre);  // base_pre = the workgroup's total
+  } else {
+    base_pre = parts[blk];
+  }
   uint32_t total;
-  uint32_t pre = block_excl_scan<kThreads / 64>(s, lds, total) + parts[blk];
+  uint32_t pre = block_excl_scan<kThreads / 64>(s, lds, total) + base_pre;
   uint32_t o[kScanItems];
 #pragma unroll
   for (int k = 0; k < kScanItems; k++) {
@@ -702,16 +713,12 @@ __global__ __launch_bounds__(kThreads) void scan_reduce_views_kernel(ScanViews m
   scan_reduce_body<false>(j.in, nullptr, j.n, j.parts, blockIdx.x - m.first[k]);
 }
 
-__global__ __launch_bounds__(1024) void scan_parts_views_kernel(ScanViews m) {
-  const ScanJob& j = m.j[blockIdx.x];  // one workgroup per view
-  scan_parts_body(j.parts, (int)(m.first[blockIdx.x + 1] - m.first[blockIdx.x]));
-}
-
 template <bool INCLUSIVE>
 __global__ __launch_bounds__(kThreads) void scan_final_views_kernel(ScanViews m) {
   const int k = batch_view(m.first, m.V, blockIdx.x);
   const ScanJob& j = m.j[k];
-  scan_final_body<false, INCLUSIVE>(j.in, nullptr, j.n, j.parts, j.out, blockIdx.x - m.first[k]);
+  scan_final_body<false, INCLUSIVE, true>(j.in, nullptr, j.n, j.parts, j.out,
+                                          blockIdx.x - m.first[k]);
 }
 
 // One workgroup: *out = sum of the n partials (n <= kScanMaxParts).
@@ -906,7 +913,6 @@ hipError_t scan_u32_views(const ScanSpec* v, int V, bool inclusive, hipStream_t 
   if (m.first[V] == 0) return hipSuccess;
   const dim3 grid(m.first[V]);
   hipLaunchKernelGGL(scan_reduce_views_kernel, grid, dim3(kThreads), 0, s, m);
-  hipLaunchKernelGGL(scan_parts_views_kernel, dim3((unsigned)V), dim3(1024), 0, s, m);
   if (inclusive) hipLaunchKernelGGL(scan_final_views_kernel<true>, grid, dim3(kThreads), 0, s, m);
   else hipLaunchKernelGGL(scan_final_views_kernel<false>, grid, dim3(kThreads), 0, s, m);
   return hipGetLastError();
