@@ -24,6 +24,40 @@ def _away_camera(W, H, like):
     return make_camera(R, -R.T @ c, like.FoVx, like.FoVy, W, H, uid=99, device="cuda")
 
 
+def _batched_vs_single(m, cams):
+    import diff_gaussian_rasterization as dgr
+    from gaussian_renderer import render, render_views
+    bg = torch.zeros(3, device="cuda")
+    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(2)]
+    pkgs = render_views(cams, m, Pipe(), bg, Opt(), streams=streams)
+    counts = list(dgr.LAST_STATS["view_counts"])
+    multi = [{k: p[k].detach().clone() for k in IMAGES + ("radii",)} for p in pkgs]
+    del pkgs
+    torch.cuda.synchronize()
+    assert len(counts) == len(cams)
+    for v, cam in enumerate(cams):
+        one = render(cam, m, Pipe(), bg, Opt())
+        torch.cuda.synchronize()
+        assert counts[v] == (dgr.LAST_STATS["num_rendered"], dgr.LAST_STATS["num_instances"]), v
+        for k in IMAGES + ("radii",):
+            assert torch.equal(multi[v][k], one[k].detach()), (v, k)
+    return counts
+
+
+def test_batched_forward_wide_ids_equals_single_view():
+    """Ids too wide to share a 32-bit word with a tile id or a tile count (2048x2048: 16384 tiles,
+    300k Gaussians > 2^18 and 2^17): the batched forward falls back to the pair tile sort and the
+    gathered depth-sort payload (gsr_api.cpp phase 1 / 2a), still bitwise the single-view call."""
+    W = H = 2048
+    tiles = (W // 16) * (H // 16)
+    P = 300_000
+    assert P > 1 << (32 - (tiles - 1).bit_length()) and P > 1 << (32 - tiles.bit_length())
+    m = SplatModel(make_gaussians(P, sh_degree=3, seed=7), device="cuda")
+    cams = [c.to("cuda") for c in make_cameras(2, W, H, seed=7)]
+    counts = _batched_vs_single(m, cams)
+    assert all(c[1] > 0 for c in counts)
+
+
 @pytest.mark.parametrize("nviews,distance", [(1, 4.0), (7, 4.0), (10, 4.0), (5, 1.6)])
 def test_batched_forward_equals_single_view(nviews, distance):
     """(distance 4: every binned depth in [2, 8), one top byte -- the batched depth sort leaves its
