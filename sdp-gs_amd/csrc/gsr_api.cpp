@@ -1239,11 +1239,11 @@ int views_forward_batched(const FwdModel& m, std::vector<FwdCam>& cams, gsr_view
     PROF_BEGIN(PREPROCESS);
     GSR_CHECK(launch_preprocess_views(pas, nl, stream));
     PROF_END(PREPROCESS);
-    GSR_CHECK(sum_u32_parts_views(sums, nl, stream));
-    GSR_CHECK(hipEventRecord(G.ready, stream));
+    // the read-back sums ride in the depth sort's digit-totals launch (one launch fewer in the
+    // chain); the read-back event follows that launch
     PROF_BEGIN(DEPTH_SORT);
     GSR_CHECK(radix_sort_pairs_views(ds, nl, 32, &G.depth_in_b, stream, /*sentinel_anywhere=*/true,
-                                     /*precleared=*/true));
+                                     /*precleared=*/true, sums, G.ready));
     PROF_END(DEPTH_SORT);
     ScanSpec sc[kMaxBatchViews];
     for (int l = 0; l < nl; l++) {

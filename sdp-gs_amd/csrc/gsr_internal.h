@@ -158,8 +158,12 @@ struct SortSpec {
   // in place of the key and value & (2^vsplit - 1) as the value (no key_payload gather)
   int vsplit = 0;
 };
+// sums (one per view, optional): the views' read-back sums formed inside the digit-totals launch
+// (sum_u32_parts_views folded in); after_totals (optional): recorded right after that launch
+struct SumSpec;
 hipError_t radix_sort_pairs_views(const SortSpec* v, int V, int bits, bool* result_in_b,
-                                  hipStream_t s, bool sentinel_anywhere, bool precleared);
+                                  hipStream_t s, bool sentinel_anywhere, bool precleared,
+                                  const SumSpec* sums = nullptr, hipEvent_t after_totals = nullptr);
 struct ScanSpec {
   const uint32_t* in;
   uint32_t* out;

@@ -663,10 +663,50 @@ __device__ __forceinline__ int batch_view(const uint32_t* first, int V, uint32_t
   return k;
 }
 
+struct SumJob {
+  const uint32_t* parts;
+  const uint32_t* parts2;
+  uint32_t* out;
+  uint32_t* host;
+  const uint32_t* flag0;
+  int n;
+};
+struct SumViews {
+  SumJob j[kMaxBatchViews];
+  int V;
+};
+// one view's read-back sums (exact and full-rectangle instance counts, sticky flag) by one
+// workgroup of NT lanes
+template <int NT>
+__device__ __forceinline__ void sum_job_body(const SumJob& j) {
+  __shared__ uint32_t lds[NT / 64], lds2[NT / 64];
+  uint32_t s = 0, s2 = 0;
+  for (int i = (int)threadIdx.x; i < j.n; i += NT) {
+    s += j.parts[i];
+    s2 += j.parts2[i];
+  }
+  uint32_t total, total2;
+  block_excl_scan<NT / 64>(s, lds, total);
+  block_excl_scan<NT / 64>(s2, lds2, total2);
+  if (threadIdx.x == 0) {
+    j.out[0] = total;
+    j.out[1] = total2;
+    if (j.host) {
+      j.host[0] = j.flag0 ? *j.flag0 : 0u;
+      j.host[1] = total;
+      j.host[2] = total2;
+    }
+  }
+}
+
+// sm.V > 0: each view's first workgroup also forms that view's read-back sums (the launch that
+// would otherwise do it alone, one workgroup per view, is folded in here)
 __global__ __launch_bounds__(kThreads) void radix_totals_views_kernel(SortPassViews m, int bits,
-                                                                      int skip_sentinel, int lo) {
+                                                                      int skip_sentinel, int lo,
+                                                                      SumViews sm) {
   const int k = batch_view(m.first, m.V, blockIdx.x);
   const SortPassJob& j = m.j[k];
+  if (sm.V && blockIdx.x == m.first[k]) sum_job_body<kThreads>(sm.j[k]);
   radix_totals_body(j.kin, j.n, bits, j.aux + kSortAuxTotals, j.aux + kSortAuxSent, skip_sentinel,
                     blockIdx.x - m.first[k], m.first[k + 1] - m.first[k], lo);
 }
@@ -834,38 +874,8 @@ __global__ __launch_bounds__(kThreads) void scan_lookback_views_kernel(ScanLbVie
 
 // One workgroup per view: out = {sum parts, sum parts2}; host (device-mapped pinned words, may be
 // null) = {*flag0, the two sums}: the views' read-back is these stores plus one event, no copy.
-struct SumJob {
-  const uint32_t* parts;
-  const uint32_t* parts2;
-  uint32_t* out;
-  uint32_t* host;
-  const uint32_t* flag0;
-  int n;
-};
-struct SumViews {
-  SumJob j[kMaxBatchViews];
-  int V;
-};
 __global__ __launch_bounds__(1024) void sum_parts_views_kernel(SumViews m) {
-  __shared__ uint32_t lds[16], lds2[16];
-  const SumJob& j = m.j[blockIdx.x];
-  uint32_t s = 0, s2 = 0;
-  for (int i = (int)threadIdx.x; i < j.n; i += 1024) {
-    s += j.parts[i];
-    s2 += j.parts2[i];
-  }
-  uint32_t total, total2;
-  block_excl_scan<16>(s, lds, total);
-  block_excl_scan<16>(s2, lds2, total2);
-  if (threadIdx.x == 0) {
-    j.out[0] = total;
-    j.out[1] = total2;
-    if (j.host) {
-      j.host[0] = j.flag0 ? *j.flag0 : 0u;
-      j.host[1] = total;
-      j.host[2] = total2;
-    }
-  }
+  sum_job_body<1024>(m.j[blockIdx.x]);
 }
 }  // namespace
 
@@ -1061,7 +1071,8 @@ hipError_t radix_sort_pairs(uint32_t* ka, uint32_t* va, uint32_t* kb, uint32_t* 
 namespace gsr {
 
 hipError_t radix_sort_pairs_views(const SortSpec* v, int V, int bits, bool* result_in_b,
-                                  hipStream_t s, bool sentinel_anywhere, bool precleared) {
+                                  hipStream_t s, bool sentinel_anywhere, bool precleared,
+                                  const SumSpec* sums, hipEvent_t after_totals) {
   *result_in_b = false;
   if (V <= 0 || bits <= 0) return hipSuccess;
   if (V > kMaxBatchViews || bits > 32) return hipErrorInvalidValue;
@@ -1113,8 +1124,21 @@ hipError_t radix_sort_pairs_views(const SortSpec* v, int V, int bits, bool* resu
     }
   };
   fill(0, tfirst);
+  SumViews sm{};
+  if (sums) {  // one per view, in the views' order
+    sm.V = V;
+    for (int k = 0; k < V; k++) {
+      if (sums[k].n > 0x7fffffffull || !sums[k].parts2) return hipErrorInvalidValue;
+      sm.j[k] = SumJob{sums[k].parts, sums[k].parts2, sums[k].out, sums[k].host, sums[k].flag0,
+                       (int)sums[k].n};
+    }
+  }
   hipLaunchKernelGGL(radix_totals_views_kernel, dim3(tfirst[V]), dim3(kThreads), 0, s, m, bits,
-                     sentinel_anywhere ? 1 : 0, lo);
+                     sentinel_anywhere ? 1 : 0, lo, sm);
+  if (after_totals) {
+    const hipError_t e = hipEventRecord(after_totals, s);
+    if (e != hipSuccess) return e;
+  }
   if (planned)
     hipLaunchKernelGGL(sort_plan_views_kernel, dim3(V), dim3(kThreads), 0, s, m, bits,
                        sentinel_anywhere ? 1 : 0);
