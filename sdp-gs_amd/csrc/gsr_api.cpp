@@ -1563,7 +1563,9 @@ int gsr_rasterize_views_fused_backward_sliced(
     // slice while the next one computes)
     const bool last = v0 + per >= V;
     const uint32_t step = (last && on_rows && slice_rows > 0) ? (uint32_t)slice_rows : (uint32_t)P;
-    if (np > 1 && !per_view_pre) {
+    // one view takes the multi-view launch too when it forms the SH gradients (no per-view
+    // kernel does); np == 0 (P == 0, every call done) falls through to the no-op per-view path
+    if ((np > 1 || (np == 1 && sh_in)) && !per_view_pre) {
       const int debug = debug_sync;
       hipStream_t stream = call_stream;
       PROF_BEGIN(PREPROCESS_BWD);
@@ -1580,7 +1582,7 @@ int gsr_rasterize_views_fused_backward_sliced(
         if (last && on_rows && step >= (uint32_t)P) on_rows(rows_ctx, 0, P);
       }
     }
-    if (ve == hipErrorNotSupported && sh_in)
+    if (ve == hipErrorNotSupported && sh_in && np > 0)
       return fail(GSR_ERR_ARGUMENT, "SH gradients formed in the multi-view backward: this "
                                     "configuration has no multi-view per-Gaussian launch");
     if (ve == hipErrorNotSupported) {

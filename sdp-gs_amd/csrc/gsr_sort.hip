@@ -753,12 +753,22 @@ __global__ __launch_bounds__(kThreads) void scan_reduce_views_kernel(ScanViews m
   scan_reduce_body<false>(j.in, nullptr, j.n, j.parts, blockIdx.x - m.first[k]);
 }
 
-template <bool INCLUSIVE>
+// RAW (each workgroup sums its predecessors' plain partials itself) reads O(parts^2) words in
+// total, so it is taken only up to kScanRawMaxParts partitions per view; above, one workgroup per
+// view scans the partials first (scan_parts_views_kernel) and the final pass reads its prefix.
+constexpr uint32_t kScanRawMaxParts = 1024;
+
+__global__ __launch_bounds__(1024) void scan_parts_views_kernel(ScanViews m) {
+  const int k = (int)blockIdx.x;
+  scan_parts_body(m.j[k].parts, (int)(m.first[k + 1] - m.first[k]));
+}
+
+template <bool INCLUSIVE, bool RAW>
 __global__ __launch_bounds__(kThreads) void scan_final_views_kernel(ScanViews m) {
   const int k = batch_view(m.first, m.V, blockIdx.x);
   const ScanJob& j = m.j[k];
-  scan_final_body<false, INCLUSIVE, true>(j.in, nullptr, j.n, j.parts, j.out,
-                                          blockIdx.x - m.first[k]);
+  scan_final_body<false, INCLUSIVE, RAW>(j.in, nullptr, j.n, j.parts, j.out,
+                                         blockIdx.x - m.first[k]);
 }
 
 // One workgroup: *out = sum of the n partials (n <= kScanMaxParts).
@@ -914,17 +924,26 @@ hipError_t scan_u32_views(const ScanSpec* v, int V, bool inclusive, hipStream_t 
   ScanViews m{};
   m.V = V;
   m.first[0] = 0;
+  size_t np_max = 0;
   for (int k = 0; k < V; k++) {
     const size_t np = scan_parts(v[k].n);
     if (np > (size_t)kScanMaxParts || v[k].n > 0xffffffffull) return hipErrorInvalidValue;
     m.j[k] = ScanJob{v[k].in, v[k].out, v[k].parts, (uint32_t)v[k].n};
     m.first[k + 1] = m.first[k] + (uint32_t)np;
+    np_max = np > np_max ? np : np_max;
   }
   if (m.first[V] == 0) return hipSuccess;
   const dim3 grid(m.first[V]);
+  const bool raw = np_max <= kScanRawMaxParts;
   hipLaunchKernelGGL(scan_reduce_views_kernel, grid, dim3(kThreads), 0, s, m);
-  if (inclusive) hipLaunchKernelGGL(scan_final_views_kernel<true>, grid, dim3(kThreads), 0, s, m);
-  else hipLaunchKernelGGL(scan_final_views_kernel<false>, grid, dim3(kThreads), 0, s, m);
+  if (!raw) hipLaunchKernelGGL(scan_parts_views_kernel, dim3(V), dim3(1024), 0, s, m);
+  if (raw) {
+    if (inclusive) hipLaunchKernelGGL((scan_final_views_kernel<true, true>), grid, dim3(kThreads), 0, s, m);
+    else hipLaunchKernelGGL((scan_final_views_kernel<false, true>), grid, dim3(kThreads), 0, s, m);
+  } else {
+    if (inclusive) hipLaunchKernelGGL((scan_final_views_kernel<true, false>), grid, dim3(kThreads), 0, s, m);
+    else hipLaunchKernelGGL((scan_final_views_kernel<false, false>), grid, dim3(kThreads), 0, s, m);
+  }
   return hipGetLastError();
 }
 

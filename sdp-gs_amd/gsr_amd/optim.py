@@ -138,13 +138,25 @@ class FusedAdam(torch.optim.Adam):
             else:
                 skips[dev] = (skip.data_ptr(), box)
         states = [self.state[it[0]] for its in batches.values() for it in its]
-        return {"batches": batches, "skips": skips, "states": states}
+        return {"batches": batches, "skips": skips, "states": states, "issued": False}
+
+    def abort_rows(self, h):
+        """Give back the step counts begin_rows advanced when the step is abandoned before any
+        step_rows launch was issued (a forward or backward between them raised): the next step's
+        bias corrections then see the counts of the updates actually applied.  Once a
+        slice was issued the rows it updated used the advanced counts, so they are kept."""
+        if h is None or h["issued"]:
+            return
+        for st in h["states"]:
+            st["step"] -= 1
+        h["issued"] = True  # idempotent
 
     @torch.no_grad()
     def step_rows(self, h, a: int, b):
         """Rows [a, b) of every parameter of the step begun by begin_rows (b None: to the end).
         Issued on the current stream of each parameter's device."""
         L = _lib.load()
+        h["issued"] = True
         for (dev, beta1, beta2, eps), items in h["batches"].items():
             stream = _lib.raw_stream(dev)
             skip_ptr, box = h["skips"][dev]

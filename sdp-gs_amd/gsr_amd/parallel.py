@@ -268,6 +268,12 @@ class GradAllReducer:
             raise RuntimeError("each_reduced_slice: averaging reducers are not sliced")
         if not getattr(self, "_guarded", False):
             raise RuntimeError("each_reduced_slice: reduce the step's guard before its slices")
+        # fn reads the reduced rows through p.grad: every gradient must be a view of the flat
+        # buffer (a detached .grad would give fn the local, unreduced values)
+        for p, off in zip(self.params, self.offsets):
+            if not self._attached(p, off):
+                raise RuntimeError("each_reduced_slice: a parameter's .grad is not a view of the "
+                                   "flat all-reduce buffer (call attach_grads() before the backward)")
         for w in self._guard_works:  # the skip decision first (every slice's optimizer reads it)
             w.wait()
         for a, b, works in self._slice_works:

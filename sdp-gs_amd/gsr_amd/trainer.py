@@ -194,8 +194,13 @@ def train_step_views(model, cams: Sequence, gt_images: Sequence[torch.Tensor],
                     if fill is None:  # this step's forwards and backwards are issued by now
                         fill = pipeline.prepare_next(model, list(next_cams))
                     fill(a, b)
-        losses = pipeline.run_views(cams, all_views, model=model, reducer=reducer,
-                                    after_slice=None if h is None else after_slice)
+        try:
+            losses = pipeline.run_views(cams, all_views, model=model, reducer=reducer,
+                                        after_slice=None if h is None else after_slice)
+        except BaseException:
+            if h is not None:  # no Adam update ran: the step counts go back
+                opt.abort_rows(h)
+            raise
         with torch.no_grad():
             if h is not None:
                 if not pipeline.rows_done:  # no sliced reduction ran: the whole step now

@@ -45,6 +45,10 @@ CASES = {
                                         deg=3, multi=True),
     "small_deg1_1stream_multi": dict(P=20_000, W=200, H=150, views=3, streams=1, seed=9,
                                      deg=1, multi=True),
+    # one view through the multi-view call: its SH gradients still come from the multi-view
+    # per-Gaussian launch (V == 1 used to reach a 'no multi-view launch' error)
+    "small_1view_1stream_multi": dict(P=20_000, W=200, H=150, views=1, streams=1, seed=10,
+                                      deg=3, multi=True),
     "cfg3_1m_1008x756_multi": dict(P=1_000_000, W=1008, H=756, views=3, streams=3, seed=0,
                                    deg=3, multi=True),
     "cfg5_5m_1920x1080_multi": dict(P=5_000_000, W=1920, H=1080, views=2, streams=2, seed=0,
@@ -126,3 +130,18 @@ def test_multi_view_call_equals_per_view_path(streams):
             assert (a[k] == b[k]).all(), k
     for n in LEAVES:
         assert (ga[n] == gb[n]).all(), n
+
+
+@pytest.mark.parametrize("views", [1, 2])
+def test_multi_view_call_empty_model(views):
+    """P == 0 through the multi-view call: empty outputs, no error (the per-Gaussian stage has
+    nothing to launch)."""
+    m = SplatModel(make_gaussians(0, sh_degree=3, seed=3), device="cuda")
+    cams = [x.to("cuda") for x in make_cameras(views, 64, 48, seed=3)]
+    grads = upstream_grads(48, 64, seed=1, device="cuda")
+    vg, gg = run_bench_path(m, cams, grads, streams=1, multi=True)
+    for v in vg:
+        assert v["radii"].size == 0
+        assert not v["alpha"].any()
+    for n in LEAVES:
+        assert gg[n].size == 0
