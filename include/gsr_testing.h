@@ -52,6 +52,14 @@ int gsr_test_binning_lists(const void* binning_buffer, const void* image_buffer,
                            int image_height, int image_width, int debug, int n_instances,
                            uint32_t* point_list_out, uint32_t* ranges_out, void* stream);
 
+/* The splat records a forward's preprocess left in its geometry buffer (geom_buffer: device; P as
+ * the forward was called; rec_out: host, [P][16] floats): per Gaussian {x_px, y_px, conic.a,
+ * conic.b}, {conic.c, opacity * confidence, depth, red}, {green, blue, f0, f1}, {f2, radius,
+ * q_cut, packed rows} (gsr_preprocess.hip).  Lets tests/ compare the preprocess outputs
+ * (preprocessCUDA, forward.cu:155-256: means2D, conic_opacity, depths, rgb) entry by entry with
+ * the float64 oracle. */
+int gsr_test_splat_records(const void* geom_buffer, int P, float* rec_out, void* stream);
+
 /* The fused path's GaussianModel activations as its kernels evaluate them (device pointers):
  * opacity = sigmoid(opacity_raw) [P], scaling = exp(scaling_raw) [P,3],
  * rotation = normalize(rotation_raw) [P,4] (16-byte aligned).  Lets the tests feed the CPU oracle

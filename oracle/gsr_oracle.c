@@ -1486,4 +1486,18 @@ int oracle_get_depths(const oracle_state* st, float* out) { to_float(out, st->de
 int oracle_get_rgb(const oracle_state* st, float* out) { to_float(out, st->rgb, 3 * (size_t)st->P); return 0; }
 int oracle_get_tiles_touched(const oracle_state* st, unsigned* out) { memcpy(out, st->tiles_touched, sizeof(unsigned) * (size_t)st->P); return 0; }
 int oracle_get_clamped(const oracle_state* st, unsigned char* out) { memcpy(out, st->clamped, 3 * (size_t)st->P); return 0; }
+/* The preprocess outputs at the build's own precision, [P][13] doubles in the GPU splat record's
+ * order (gsr_preprocess.hip): x_px, y_px, conic a, b, c, opacity, depth, r, g, b, f0, f1, f2
+ * (tests/test_pre_f64_parity.py; the float getters above round the float64 build to float). */
+int oracle_get_preprocess_f64(const oracle_state* st, double* out) {
+    for (long i = 0; i < st->P; i++) {
+        double* o = out + 13 * i;
+        o[0] = st->means2D[2 * i]; o[1] = st->means2D[2 * i + 1];
+        for (int k = 0; k < 4; k++) o[2 + k] = st->conic_opacity[4 * i + k];
+        o[6] = st->depths[i];
+        for (int k = 0; k < 3; k++) o[7 + k] = st->rgb[3 * i + k];
+        for (int k = 0; k < 3; k++) o[10 + k] = st->feat[3 * i + k];
+    }
+    return 0;
+}
 int oracle_get_cov3D(const oracle_state* st, float* out) { to_float(out, st->cov3D, 6 * (size_t)st->P); return 0; }

@@ -162,6 +162,8 @@ int oracle_get_depths(const oracle_state* st, float* out);          /* [P] */
 int oracle_get_rgb(const oracle_state* st, float* out);             /* [P*3] */
 int oracle_get_tiles_touched(const oracle_state* st, unsigned* out);/* [P] */
 int oracle_get_cov3D(const oracle_state* st, float* out);           /* [P*6] */
+/* [P][13] doubles: x_px, y_px, conic a b c, opacity, depth, rgb, feature (the build's precision) */
+int oracle_get_preprocess_f64(const oracle_state* st, double* out);
 
 /* The blend's exp(power): the deterministic single-precision exp shared with the HIP kernels. */
 void oracle_splat_exp(long n, const float* x, float* out);

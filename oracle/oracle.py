@@ -80,7 +80,7 @@ def lib(variant: str = "f32"):
         L.oracle_dist_knn3.restype = None
         L.oracle_dist_knn3.argtypes = [ctypes.c_int64, _p, _p, _p]
         for name in ("point_list", "ranges", "final_T", "n_contrib", "margin", "means2D", "conic_opacity",
-                     "depths", "rgb", "tiles_touched", "cov3D"):
+                     "depths", "rgb", "tiles_touched", "cov3D", "preprocess_f64"):
             fn = getattr(L, "oracle_get_" + name)
             fn.restype = _i
             fn.argtypes = [_p, _p]
@@ -277,6 +277,11 @@ class OracleRaster:
 
     def cov3D(self):
         return self._get("cov3D", (self.P, 6), np.float32)
+
+    def preprocess_f64(self):
+        """[P, 13] float64 at the build's own precision, in the GPU splat record's order: x_px,
+        y_px, conic a, b, c, opacity, depth, r, g, b, f0, f1, f2 (culled rows: zeros)."""
+        return self._get("preprocess_f64", (self.P, 13), np.float64)
 
     # ---- backward --------------------------------------------------------------------------
     def backward(self, dL_dcolor, dL_ddepth=None, dL_dalpha=None, dL_dfeature=None):

@@ -2,7 +2,7 @@
 have a contributing pixel, for pixel groups of several shapes -- the quadrant a backward wave owns
 (8x8), its halves (8x4), its 4x4 blocks.  Test-side tool (uses oracle/), not part of the product.
 
-  python scripts/blend_stats.py [--views 2] [--gaussians 1000000]
+  python scripts/blend_stats.py [--views 2] [--gaussians 1000000] [--width 1008 --height 756]
 """
 import argparse
 import math
@@ -39,10 +39,12 @@ def main():
     ap.add_argument("--views", type=int, default=2)
     ap.add_argument("--gaussians", type=int, default=1_000_000)
     ap.add_argument("--threads", type=int, default=8)
+    ap.add_argument("--width", type=int, default=1008)
+    ap.add_argument("--height", type=int, default=756)
     args = ap.parse_args()
     build()
     set_threads(args.threads)
-    H, W = 756, 1008
+    H, W = args.height, args.width
     model = SplatModel(make_gaussians(args.gaussians, sh_degree=3, seed=0), device="cpu")
     cams = make_cameras(12, W, H, seed=0)
     with torch.no_grad():

@@ -1838,6 +1838,19 @@ int gsr_test_binning_lists(const void* binning_buffer, const void* image_buffer,
   return GSR_OK;
 }
 
+int gsr_test_splat_records(const void* geom_buffer, int P, float* rec_out, void* stream_ptr) {
+  g_err.clear();
+  hipStream_t stream = (hipStream_t)stream_ptr;
+  const int debug = 0;
+  if (P < 0 || (P > 0 && (!geom_buffer || !rec_out))) return fail(GSR_ERR_ARGUMENT, "invalid arguments");
+  if (P == 0) return GSR_OK;
+  const GeomState g = carve_geom((char*)geom_buffer, (size_t)P);
+  GSR_CHECK(hipMemcpyAsync(rec_out, g.rec, sizeof(float) * kRecFloats * (size_t)P,
+                           hipMemcpyDeviceToHost, stream));
+  GSR_CHECK(hipStreamSynchronize(stream));
+  return GSR_OK;
+}
+
 void gsr_profile_enable(int stage_mask) { prof().mask.store((uint32_t)stage_mask); }
 
 int gsr_profile_collect(double* ms, long long* calls) {

@@ -308,7 +308,9 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
   // NaN-poisons every gradient; nothing is read from them here (grid-uniform)
   if (a.status && (*a.status & (kStatusDepthSort | kStatusTileSort))) return;
   const uint2 range = a.ranges[tile];
-  const uint32_t tile_last = a.tile_last[tile];
+  // every loop trip count of this kernel is bounded by the tile's list: the
+  // forward's largest n_contrib cannot exceed it, the min() makes that hold for any buffer
+  const uint32_t tile_last = min(a.tile_last[tile], range.y - min(range.x, range.y));
   const float T_final = inside ? a.final_T[pix] : 0.0f;
   float T = T_final;
   const uint32_t last_contributor = inside ? a.n_contrib[pix] : 0u;

@@ -541,6 +541,13 @@ __device__ __forceinline__ void onesweep_body(
         done = true;
         return;
       }
+      // fail fast: once any partition of this sort gave up, the others stop waiting too (a
+      // predecessor that never publishes would otherwise cost every later partition its own
+      // full spin bound in turn -- minutes of apparent hang instead of one bound)
+      if ((spins & 63) == 0 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+        done = true;
+        return;
+      }
       __builtin_amdgcn_s_sleep(1);
     };
     if (g_force_lookback_timeout) {  // test hook only: the bounded spin's give-up path
@@ -865,6 +872,9 @@ __global__ __launch_bounds__(kThreads) void scan_lookback_views_kernel(ScanLbVie
         }
         break;
       }
+      // fail fast once another partition gave up (see the sort's spin)
+      if ((spins & 63) == 0 && __hip_atomic_load(job.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        break;
       __builtin_amdgcn_s_sleep(1);
     }
     if (lane == 0) {

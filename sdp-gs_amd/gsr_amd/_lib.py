@@ -303,6 +303,8 @@ def load():
         L.gsr_test_force_sort_timeout.restype = _i
         L.gsr_test_force_sort_timeout.argtypes = [_i]
         L.gsr_test_binning_lists.restype = _i
+        L.gsr_test_splat_records.restype = _i
+        L.gsr_test_splat_records.argtypes = [_p, _i, _p, _p]
         L.gsr_test_binning_lists.argtypes = [_p, _p, _i, _i, _i, _i, _i, _p, _p, _p]
         L.gsr_test_activations.restype = _i
         L.gsr_test_activations.argtypes = [_p, _p, _p, _sz, _p, _p, _p, _p]

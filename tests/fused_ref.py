@@ -59,13 +59,15 @@ def kernel_activations(m):
     return op, sc, rot
 
 
-def run_bench_path(m, cams, grads, streams=3, defer_sh=True, precolor=True, lag=1, multi=False):
+def run_bench_path(m, cams, grads, streams=3, defer_sh=True, precolor=True, lag=1, multi=False,
+                   capture=None):
     """bench.py's step on `cams`: render + backward of the fixed upstream grads (image, depth,
     feature), grad-into-leaves, views over `streams` HIP streams.  multi: every view in one
     multi-view call (gaussian_renderer.render_views, ViewPipeline.run_views -- bench.py's default
     issue); else per view render() with view i's backward issued after view i + lag's forward
     (bench.py --per-view --lag, default 1; 0 = together).  Returns (per-view numpy dicts of the
-    images, radii and screen-space gradient, leaf grads float64)."""
+    images, radii and screen-space gradient, leaf grads float64).  capture (multi only): called
+    with the render_views packages after the forward, before the backward."""
     import diff_gaussian_rasterization as dgr
     from gaussian_renderer import render, render_views
     from gsr_amd.pipeline import ViewPipeline
@@ -88,6 +90,8 @@ def run_bench_path(m, cams, grads, streams=3, defer_sh=True, precolor=True, lag=
 
         def all_views(cs, strs):
             pkgs = render_views(cs, m, Pipe(), bg, Opt(), streams=strs)
+            if capture is not None:
+                capture(pkgs)
             st = pkgs[0]["views"]
             V = len(pkgs)
             torch.autograd.backward([st["render"], st["depth"], st["feature"]],
@@ -109,7 +113,10 @@ def run_bench_path(m, cams, grads, streams=3, defer_sh=True, precolor=True, lag=
     finally:
         dgr.grad_into_leaves(prev)
     views = [{k: v.cpu().numpy() for k, v in o.items()} for o in outs]
-    leaf_grads = {n: getattr(m, n).grad.detach().cpu().numpy().astype(np.float64) for n in LEAVES}
+    leaf_grads = {n: (getattr(m, n).grad.detach().cpu().numpy().astype(np.float64)
+                      if getattr(m, n).grad is not None else
+                      np.zeros(tuple(getattr(m, n).shape)))  # P == 0: no gradient written
+                  for n in LEAVES}
     return views, leaf_grads
 
 
@@ -267,7 +274,7 @@ def grad_stats(got, ref, exclude=None):
             "n": int(ref.size), "n_big": int(big.sum())}
 
 
-def compare(tag, vg, vo, gg, go, stats_path=None):
+def compare(tag, vg, vo, gg, go, stats_path=None, leaves=LEAVES):
     """Per-view images, radii, screen-space gradients and the summed raw-leaf gradients; returns
     the statistics (also appended to stats_path as one JSON line)."""
     st = {"case": tag, "views": [], "grads": {}}
@@ -292,10 +299,28 @@ def compare(tag, vg, vo, gg, go, stats_path=None):
         v["gaussians_behind_flips"] = int(hit.sum())
         v["means2D"] = grad_stats(a["means2D"][:, :2], b["means2D"][:, :2], hit)
         st["views"].append(v)
-    for n in LEAVES:
+    for n in leaves:
         st["grads"][n] = grad_stats(gg[n], go[n], hit_all)
     if stats_path:
         os.makedirs(os.path.dirname(stats_path), exist_ok=True)
         with open(stats_path, "a") as fh:
             fh.write(json.dumps(st) + "\n")
     return st
+
+
+def splat_records(pkgs):
+    """Per view of a render_views call: the splat records its preprocess wrote ([P, 16] float32,
+    gsr_testing.h gsr_test_splat_records), read from the views' geometry buffers, which the
+    autograd node of the stacked outputs keeps for the backward."""
+    from gsr_amd import _lib
+    L = _lib.load()
+    node = pkgs[0]["views"]["render"].grad_fn
+    P = int(pkgs[0]["radii"].shape[0])
+    torch.cuda.synchronize()
+    out = []
+    for view in node.views:  # the gsr_view structs: each view's carve of the call's scratch
+        rec = np.zeros((P, 16), np.float32)
+        _lib.check(L.gsr_test_splat_records(view.geom_buffer, P, rec.ctypes.data,
+                                            torch.cuda.current_stream().cuda_stream))
+        out.append(rec)
+    return out

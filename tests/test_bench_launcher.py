@@ -10,6 +10,8 @@ import subprocess
 import sys
 import textwrap
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
@@ -58,3 +60,29 @@ def test_bench_gpus2_without_gpu_exits_nonzero():
                        env=env, capture_output=True, text=True, timeout=300)
     assert p.returncode != 0
     assert '"metric"' not in p.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_dist2_roofline_bracket_is_collective_free():
+    """at N > 1 the dominant kernel's bracket is timed in a reducer-free
+    region, so its average launch time stays that of N = 1 (round 5's 2-rank rehearsal read
+    render_bwd at 25.6 ms, 33x its N = 1 time, because the bracket spanned the all-reduce).  Two
+    gloo ranks share this box's one GPU (so some slowdown from sharing the card is expected, not
+    a collective); the line also reports the step time the all-reduce adds
+    (collective_exposed_ms).  The ranks are child processes of bench.py's launcher."""
+    def run(n):
+        env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+        env["GSR_DIST_BACKEND"] = "gloo"
+        p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n),
+                            "--steps", "5", "--warmup", "2", "--workload", "tiny_20k_320x240",
+                            "--no-cpu-baseline", "--no-extra-legs"],
+                           env=env, capture_output=True, text=True, timeout=500)
+        assert p.returncode == 0, p.stderr[-2000:]
+        return json.loads([ln for ln in p.stdout.splitlines() if '"metric"' in ln][-1])
+    one, two = run(1), run(2)
+    assert one["collective_exposed_ms"] is None
+    assert two["collective_exposed_ms"] is not None
+    r1, r2 = one["roofline"], two["roofline"]
+    assert r1["kernel"] == r2["kernel"], (r1, r2)
+    assert r2["avg_ms"] <= 2.0 * r1["avg_ms"], (r1, r2)

@@ -5,7 +5,7 @@ flags through the fused multi-view call) is compared entry by entry with the flo
 oracle (tests/f64_ref.py): every raw-leaf gradient entry at >= 1 % of its tensor's maximum must
 satisfy
 
-    |gpu - f64| <= max(1e-5 |f64|, C u B)        u = 2^-24, C = 8
+    |gpu - f64| <= C u B        u = 2^-24, C = 1 (no relative floor, since round 6)
 
 where B is the entry's float32 rounding scale: the sum over its per-pixel terms of |term| times
 the length of the float32 chain that term went through (T's recovery over the pixel's list),
@@ -24,10 +24,14 @@ GPU-vs-float32 image flip (the Gaussians that can reach the flipped pixels,
 fused_ref.pixel_contributors) and Gaussians whose visibility (radius > 0)
 differs between float32 and float64 (the per-Gaussian backward's gate).  The float32
 oracle -- the reference's own arithmetic, restated -- is held to the same bound (it is the
-calibration: its worst ratio |f32 - f64| / (u B) is ~1.6 at these sizes), so passing says the
-GPU is as accurate as the reference's float32 arithmetic, entry by entry.  A negative control
-shows the bound catches a 1e-4 systematic error in the colour terms.  The scale-relative 1e-5 check
-stays in tests/test_fused_parity.py.  Statistics: gpurun_out/f64_stats.jsonl.
+calibration: its worst ratio |f32 - f64| / (u B) is <= 0.14 at these sizes, the GPU's <= 0.34 in
+round 5, profiles/r05_f64_stats.jsonl; since round 6 C = 1 and the 1e-5
+relative floor is gone -- every entry is held to its rounding scale alone), so passing says
+the GPU is as accurate as the reference's float32 arithmetic, entry by entry.  Negative controls
+show the bound catches a 1e-5 systematic error in the colour terms and a 1e-5 error in the conic
+the blend evaluates (f64_ref.controls_1e5).  The preprocess's own float32 outputs are checked
+entry by entry, unlocked, in tests/test_pre_f64_parity.py.  The scale-relative 1e-5 check stays in
+tests/test_fused_parity.py.  Statistics: gpurun_out/f64_stats.jsonl.
 
 VERDICT r3 also proposed |gpu - f64| <= max(2 |f32 - f64|, 1e-5 |f64|); it is reported
 (`gpu_within_2x_f32`) but not asserted: two float32 evaluations with different (equally valid)
@@ -41,7 +45,7 @@ import numpy as np
 import pytest
 import torch
 
-from f64_ref import oracle_inputs, rounding_stats, run_f64_path
+from f64_ref import controls_1e5, oracle_inputs, rounding_stats, run_f64_path
 from fused_ref import LEAVES, flipped_pixels, pixel_contributors, kernel_activations, \
     run_bench_path, run_oracle_path
 from gsr_amd.model import SplatModel
@@ -50,7 +54,7 @@ from oracle.oracle import set_threads
 
 pytestmark = pytest.mark.gpu
 
-C_BOUND = 8.0
+C_BOUND = 1.0
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 STATS = os.path.join(ROOT, "gpurun_out", "f64_stats.jsonl")
 
@@ -110,7 +114,7 @@ def test_gradients_within_float32_rounding_of_f64(case):
            "excluded_visibility_f32_vs_f64": int(hit_vis.sum()),
            "f64_decision_flips": nflip64, "decision_locked": True, "C": C_BOUND, "grads": {}}
     for n in LEAVES:
-        st = rounding_stats(gg[n], go[n], g64[n], B[n], exclude=hit, C=C_BOUND)
+        st = rounding_stats(gg[n], go[n], g64[n], B[n], exclude=hit, C=C_BOUND, rel=0.0)
         rec["grads"][n] = st
     os.makedirs(os.path.dirname(STATS), exist_ok=True)
     with open(STATS, "a") as fh:
@@ -126,12 +130,20 @@ def test_gradients_within_float32_rounding_of_f64(case):
         # ... and so does every GPU entry
         assert st["gpu_fail"] == 0, (case, n, st)
 
-    if case == "small_6views_multi":
-        # negative control: a 1e-4 systematic error in the colour terms (the image's upstream
-        # gradient scaled) is caught by the same bound
-        gd = (grads[0] * (1.0 + 1e-4), grads[1], grads[2])
-        _, g64d, _ = run_f64_path(inp, cams, gd, bound=False, lists=lists, decisions=decisions,
-                                  clamps=clamps, geometry=geometry)
-        st = rounding_stats(gg["_features_dc"], go["_features_dc"], g64d["_features_dc"],
-                            B["_features_dc"], exclude=hit, C=C_BOUND)
-        assert st["gpu_fail"] >= max(20, 0.01 * st["n_big"]), st
+    # negative controls: a 1e-5 error in the colour terms, and a 1e-5 error
+    # in the conic the float64 blend evaluates, each caught on >= 1 % of some leaf's entries
+    # (the two extra float64 evaluations run at the small and config-2 sizes)
+    if c["P"] > 100_000:
+        return
+    ctl = controls_1e5(inp, cams, grads, geometry, dict(lists=lists, decisions=decisions,
+                                                         clamps=clamps))
+    rec["controls"] = {}
+    for name, g64c in ctl.items():
+        fr = {}
+        for n in LEAVES:
+            st = rounding_stats(gg[n], go[n], g64c[n], B[n], exclude=hit, C=C_BOUND, rel=0.0)
+            fr[n] = st["gpu_fail"] / max(1, st["n_big"])
+        rec["controls"][name] = fr
+        assert max(fr.values()) >= 0.01, (case, name, fr)
+    with open(STATS.replace(".jsonl", "_controls.jsonl"), "a") as fh:
+        fh.write(json.dumps({"case": case, "controls": rec["controls"]}) + "\n")

@@ -177,3 +177,98 @@ def test_sliced_adam_equals_serial_step(world1):
     assert n0 == n1
     for (p, m, v, st), (q, m2, v2, st2) in zip(ser, got):
         assert torch.equal(p, q) and torch.equal(m, m2) and torch.equal(v, v2) and st == st2
+
+
+@pytest.mark.timeout(900)
+def test_config4_48_cameras_as_8_shards_world1(tmp_path):
+    """BASELINE config 4's workload -- 1M Gaussians, a 48-camera pool at
+    1008x756, 6 views per GPU over 8 GPUs with an RCCL gradient all-reduce -- at world size 1:
+    the pool as 8 sequential 6-view shards through ViewPipeline.run_views (one multi-view call
+    each, the row-sliced backward), RCCL initialised and the collectives forced on.  Deterministic
+    backward: every shard's gradients are bitwise the plain single-process shard's (no reducer);
+    their sum (what 8 ranks' all-reduce adds up) equals the 48 views rendered in ONE process call
+    within 1e-6 of each leaf's largest entry (the summation order of shards vs 8-view backward
+    launches differs); sampled views' images and radii match the CPU oracle (radii exact, images
+    within 1e-5 away from oracle-marked threshold pixels).  Hardware scaling stays the driver's
+    8-GPU SCALE run."""
+    import numpy as np
+
+    import diff_gaussian_rasterization as dgr
+    from fused_ref import IMAGES, compare, kernel_activations, run_oracle_path
+    from gaussian_renderer import render_views
+    from gsr_amd.model import SplatModel
+    from gsr_amd.parallel import GradAllReducer
+    from gsr_amd.pipeline import ViewPipeline
+    from gsr_amd.synthetic import make_cameras, make_gaussians, upstream_grads
+    from oracle.oracle import set_threads
+    dev = torch.device("cuda", 0)
+    init = "file://" + os.path.join(str(tmp_path), "pg")
+    dist.init_process_group("nccl", init_method=init, rank=0, world_size=1, device_id=dev)
+    prev_leaves, prev_det = dgr.grad_into_leaves(), dgr.deterministic()
+    dgr.grad_into_leaves(True)
+    dgr.deterministic(True)
+    try:
+        model = SplatModel(make_gaussians(1_000_000, sh_degree=3, seed=0), device=dev)
+        cams = [c.to(dev) for c in make_cameras(48, 1008, 756, seed=0)]
+        dimg, ddep, dfeat = upstream_grads(756, 1008, seed=1, device=dev)
+        bg = torch.zeros(3, device=dev)
+        shards = [cams[6 * r:6 * r + 6] for r in range(8)]
+        sample = {0: None, 47: None}  # view index -> its images and radii
+        views = ViewPipeline(dev, depth=2, defer_sh=True, precolor=True)
+
+        def step(cs, reducer, keep=None):
+            def all_views(items, strs):
+                pkgs = render_views(items, model, _Pipe(), bg, _Opt(), streams=strs)
+                st = pkgs[0]["views"]
+                V = len(pkgs)
+                torch.autograd.backward([st["render"], st["depth"], st["feature"]],
+                                        [g.expand(V, *g.shape) for g in (dimg, ddep, dfeat)])
+                if keep is not None:
+                    for i, pkg in enumerate(pkgs):
+                        k = keep + i
+                        if k in sample:
+                            sample[k] = {n: pkg[n].detach().cpu().numpy()
+                                         for n in IMAGES + ("radii",)}
+            if reducer is not None:
+                reducer.attach_grads()
+            else:
+                for p in model.parameters():
+                    p.grad = None
+            views.run_views(cs, all_views, model=model, reducer=reducer)
+            if reducer is not None:
+                reducer.wait()
+            torch.cuda.synchronize()
+            return [p.grad.detach().clone() for p in model.parameters()]
+
+        plain = [step(s, None) for s in shards]
+        reducer = GradAllReducer(model)
+        reducer._active = lambda: True  # issue the RCCL collectives at world size 1 too
+        for r, s in enumerate(shards):
+            got = step(s, reducer, keep=6 * r)
+            for g, w in zip(got, plain[r]):
+                assert torch.equal(g, w), r
+        assert dist.get_backend() == "nccl"
+        total = [torch.stack([plain[r][k] for r in range(8)]).sum(0) for k in range(len(plain[0]))]
+        del plain
+        one = step(cams, None)  # the 48 views in one process call
+        for t, o in zip(total, one):
+            scale = float(o.abs().max())
+            assert scale > 0
+            assert float((t - o).abs().max()) <= 1e-6 * scale
+        # sampled views against the CPU oracle
+        n = int(os.environ.get("OMP_NUM_THREADS") or 0) or (os.cpu_count() or 1)
+        set_threads(min(n, 32))
+        act = kernel_activations(model)
+        idx = sorted(sample)
+        vo, _ = run_oracle_path(model, [cams[i] for i in idx], (dimg, ddep, dfeat), act)
+        vg = [dict(sample[i], means2D=np.zeros((1_000_000, 3), np.float32)) for i in idx]
+        st = compare("cfg4_world1", vg, vo, {}, {}, leaves=())
+        for i, v in zip(idx, st["views"]):
+            assert v["radii_equal"], i
+            assert v["pixels_off"] == v["pixels_flipped"], (i, v)
+            for k in IMAGES:
+                assert v[k + "_unflipped"] <= 1e-5, (i, k, v)
+    finally:
+        dgr.grad_into_leaves(prev_leaves)
+        dgr.deterministic(prev_det)
+        dist.destroy_process_group()
