@@ -380,6 +380,9 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
   // Phase 2 over the first `ns` slots (wave-uniform, 1..kSlots).  slotv: lane l holds the batch
   // index of slot l & 7 (set in phase 1, no LDS round trip).
   auto phase2 = [&](uint32_t ns, uint32_t slotv) {
+#if GSR_ABL_NOPHASE2
+    if (HALF) { asm volatile("" ::"v"(slotv), "s"(ns)); return; }
+#endif
     const int j = lane & 7;
     const uint32_t bj = slotv & (uint32_t)(kBatch - 1);  // stale for j >= ns: kept in range
     const float4 r0 = s_r0[bj];
@@ -494,8 +497,13 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
       if (k < kAccRow) {
 #pragma unroll
         for (int r = 0; r < 4; r++)
-          if (gr[r] != 0xffffffffu && g[r] != 0.0f)
+          if (gr[r] != 0xffffffffu && g[r] != 0.0f) {
+#if GSR_ABL_NOATOMIC
+            asm volatile("" ::"v"(g[r]), "v"(gr[r]));
+#else
             atomicAdd(a.acc + (size_t)gr[r] * kAccFloats + k, g[r]);
+#endif
+          }
       }
       return;
     }
