@@ -172,56 +172,70 @@ static float splat_log(float x) { /* gsr_device.h splat_log: Cephes logf, explic
 void oracle_splat_log(long n, const float* x, float* out) {
     for (long i = 0; i < n; i++) out[i] = splat_log(x[i]);
 }
-typedef struct { float mx, my, ca, cb, cc, qc, kx, ky; } splat_cut;
+typedef struct { float mx, my, ica, cb, det, caQ, hx, hy, dyl, slack; int mode; } band_cut;
 static float cut_q(float ca, float cb, float cc, float op) { /* gsr_device.h splat_q_cut */
     if (!(op >= 1.0f / 255.0f)) return -2.0f;
     if (!(ca > 0.0f && cc > 0.0f && ca * cc - cb * cb > 0.0f)) return -1.0f;
     return 2.0f * splat_log(255.0f * op);
 }
-static splat_cut make_cut(float mx, float my, float ca, float cb, float cc, float qc) {
-    splat_cut s = {mx, my, ca, cb, cc, qc, 0.0f, 0.0f};
-    if (qc >= 0.0f) {
-        s.kx = -cb / cc;
-        s.ky = -cb / ca;
-    }
+/* gsr_device.h make_band_cut / band_extent / band_row_range: the binning's cut, the tiles of each
+ * tile row that the x-extent of the margin-widened cut ellipse in that row's 16-pixel band meets
+ * (float, the same operations in the same order as the kernels) */
+static band_cut make_band_cut(float mx, float my, float ca, float cb, float cc, float qc) {
+    band_cut s;
+    memset(&s, 0, sizeof s);
+    s.mx = mx; s.my = my;
+    if (qc == -2.0f) { s.mode = 0; return s; }
+    s.mode = 1;
+    if (qc < 0.0f) return s;
+    const float det = ca * cc - cb * cb;
+    if (!(det > 0.0f)) return s;
+    const float h2x = cc / det, h2y = ca / det;
+    const float ta = ca * h2x + cc * h2y + 2.0f * fabsf(cb) * sqrtf(h2x * h2y);
+    if (!(1e-4f * ta < 0.5f)) return s;
+    const float Q = (qc + 2e-2f) / (1.0f - 1e-4f * ta) * 1.001f;
+    s.mode = 2;
+    s.ica = 1.0f / ca;
+    s.cb = cb;
+    s.det = det;
+    s.caQ = ca * Q;
+    s.hx = sqrtf(Q * h2x) * 1.001f + 1e-3f;
+    s.hy = sqrtf(Q * h2y) * 1.001f + 1e-3f;
+    s.dyl = cb * (s.hx / cc);
+    s.slack = 2e-3f + 4e-6f * fabsf(mx) + 1e-4f * s.hx;
     return s;
 }
-static int cut_touches_rect(const splat_cut* s, float x0, float x1, float y0, float y1) {
-    if (s->qc == -2.0f) return 0;
-    if (s->qc < 0.0f) return 1;
-    const float dx0 = x0 - s->mx, dx1 = x1 - s->mx, dy0 = y0 - s->my, dy1 = y1 - s->my;
-    if (dx0 <= 0.0f && dx1 >= 0.0f && dy0 <= 0.0f && dy1 >= 0.0f) return 1;
-    float qmin = 3.0e38f, tabs = 0.0f;
-    for (int e = 0; e < 4; e++) {
-        float dx, dy;
-        if (e < 2) {
-            dx = (e == 0) ? dx0 : dx1;
-            dy = fminf(fmaxf(s->kx * dx, dy0), dy1);
-        } else {
-            dy = (e == 2) ? dy0 : dy1;
-            dx = fminf(fmaxf(s->ky * dy, dx0), dx1);
-        }
-        const float t1 = s->ca * dx * dx, t2 = s->cc * dy * dy, t3 = 2.0f * s->cb * dx * dy;
-        const float q = t1 + t2 + t3;
-        if (q < qmin) { qmin = q; tabs = t1 + t2 + fabsf(t3); }
-    }
-    return qmin <= s->qc + 2e-2f + 1e-4f * tabs;
+static int band_extent(const band_cut* s, float y0, float y1, float* pxl, float* pxr) {
+    const float lo = fmaxf(y0 - s->my, -s->hy), hi = fminf(y1 - s->my, s->hy);
+    if (lo > hi) return 0;
+    const float rl = sqrtf(fmaxf(s->caQ - s->det * lo * lo, 0.0f));
+    const float rh = sqrtf(fmaxf(s->caQ - s->det * hi * hi, 0.0f));
+    const float cl = -s->cb * lo, ch = -s->cb * hi;
+    float xl = fminf(cl - rl, ch - rh) * s->ica;
+    float xr = fmaxf(cl + rl, ch + rh) * s->ica;
+    if (s->dyl >= lo && s->dyl <= hi) xl = -s->hx;
+    if (-s->dyl >= lo && -s->dyl <= hi) xr = s->hx;
+    *pxl = xl - s->slack;
+    *pxr = xr + s->slack;
+    return 1;
 }
-static void cut_row_range(const splat_cut* s, unsigned ty, unsigned x0, unsigned x1, unsigned* pa,
-                          unsigned* pb) {
-    if (s->qc < 0.0f) {
+static void band_row_range(const band_cut* s, unsigned ty, unsigned x0, unsigned x1, unsigned* pa,
+                           unsigned* pb) {
+    if (s->mode != 2) {
         *pa = x0;
-        *pb = s->qc == -2.0f ? x0 : x1;
+        *pb = s->mode == 0 ? x0 : x1;
         return;
     }
-    const float y0 = (float)(ty * BLOCK_Y), y1 = (float)(ty * BLOCK_Y + BLOCK_Y - 1);
-    unsigned a = x0, b = x1;
-    while (a < x1 && !cut_touches_rect(s, (float)(a * BLOCK_X), (float)(a * BLOCK_X + BLOCK_X - 1), y0, y1))
-        a++;
-    while (b > a + 1 &&
-           !cut_touches_rect(s, (float)((b - 1) * BLOCK_X), (float)((b - 1) * BLOCK_X + BLOCK_X - 1), y0, y1))
-        b--;
-    if (a == x1) b = x1;
+    const float y0 = (float)(ty * BLOCK_Y);
+    float xl, xr;
+    if (!band_extent(s, y0, y0 + (float)(BLOCK_Y - 1), &xl, &xr)) {
+        *pa = *pb = x1;
+        return;
+    }
+    const float fa = fminf(fmaxf(ceilf((s->mx + xl - (float)(BLOCK_X - 1)) * (1.0f / BLOCK_X)), (float)x0), (float)x1);
+    const float fb = fminf(fmaxf(floorf((s->mx + xr) * (1.0f / BLOCK_X)) + 1.0f, (float)x0), (float)x1);
+    unsigned a = (unsigned)fa, b = (unsigned)fb;
+    if (a >= b) a = b = x1;
     *pa = a;
     *pb = b;
 }
@@ -1461,9 +1475,9 @@ int oracle_cut_lists(const oracle_state* st, unsigned* point_list_out, unsigned*
             const float mx = (float)st->means2D[2 * (size_t)g], my = (float)st->means2D[2 * (size_t)g + 1];
             u2 rmin, rmax;
             getRect(mx, my, st->radii[g], &rmin, &rmax, st->gx, st->gy);
-            const splat_cut c = make_cut(mx, my, co[0], co[1], co[2], cut_q(co[0], co[1], co[2], co[3]));
+            const band_cut c = make_band_cut(mx, my, co[0], co[1], co[2], cut_q(co[0], co[1], co[2], co[3]));
             unsigned a, b;
-            cut_row_range(&c, ty, rmin.x, rmax.x, &a, &b);
+            band_row_range(&c, ty, rmin.x, rmax.x, &a, &b);
             if (tx >= a && tx < b) point_list_out[n++] = g;
         }
         ranges_out[2 * t] = n > start ? start : 0;

@@ -99,8 +99,13 @@ def main():
     half = ((py % 16) // 8) * 4 + ((px % 16) // 8) * 2 + (py % 8) // 4  # quadrant * 2 + half
     key = np.unique((tile.astype(np.int64) * 8 + half) * (1 << 20) + ppos)
     contrib = np.bincount(key >> 20, minlength=gx * gy * 8).reshape(gx * gy, 8)
+    # the forward's per-block bounding box of the cut ellipse (gsr_render.hip block_mask):
+    # half-extents sqrt(qc c / det), sqrt(qc a / det), without its small margins
+    det = a * c - b * b
+    hx = np.sqrt(np.maximum(qc, 0) * c / det)
+    hy = np.sqrt(np.maximum(qc, 0) * a / det)
     res = {}
-    for name in ("rect", "pixel"):
+    for name in ("rect", "pixel", "quad&bbox"):
         cnt = np.zeros((gx * gy, 8), np.int64)
         for h in range(8):
             q, hh = h // 2, h % 2
@@ -111,10 +116,15 @@ def main():
                                               (q % 2) * 8:(q % 2) * 8 + 8].max(axis=(1, 3)).reshape(-1)
             within = pos < hm[tile_of]
             if name == "rect":
-                m = box_min(a, b, c, x0 - mx, x0 + 7 - mx, y0 - my, y0 + 3 - my)
+                keep = box_min(a, b, c, x0 - mx, x0 + 7 - mx, y0 - my, y0 + 3 - my) <= qc
+            elif name == "pixel":
+                keep = pixel_min(a, b, c, mx, my, x0, y0) <= qc
             else:
-                m = pixel_min(a, b, c, mx, my, x0, y0)
-            keep = within & (m <= qc)
+                qy0 = ty * 16 + (q // 2) * 8
+                quad = box_min(a, b, c, x0 - mx, x0 + 7 - mx, qy0 - my, qy0 + 7 - my) <= qc
+                bbox = (x0 <= mx + hx) & (x0 + 7 >= mx - hx) & (y0 <= my + hy) & (y0 + 3 >= my - hy)
+                keep = quad & bbox
+            keep = within & keep
             cnt[:, h] = np.bincount(tile_of[keep], minlength=gx * gy)
         res[name] = cnt
     waves = gx * gy * 4

@@ -32,7 +32,7 @@ __device__ __forceinline__ void wave_sync() {
 // its tile ids into a per-wave LDS window, then the wave copies the window out with coalesced
 // stores (each lane storing at its own offsets puts 64 scattered lines in every store
 // instruction).  Each Gaussian's kept range per tile row comes from the preprocess's packed
-// rec[3].w (rectangles of at most 4 rows x 15 tiles), else from cut_row_range itself.
+// rec[3].w (rectangles of at most 4 rows x 15 tiles), else from band_row_range itself.
 // (body shared by the one-view kernel and the several-views kernel: blk / nblk = this
 // workgroup's index and the workgroup count of its view)
 __device__ __forceinline__ void duplicate_body(int P, const uint32_t* __restrict__ order,
@@ -64,15 +64,15 @@ __device__ __forceinline__ void duplicate_body(int P, const uint32_t* __restrict
   const uint32_t oend = (uint32_t)__shfl((int)end, min(P - 1 - sw0, 63), 64);
   uint32_t gid = 0, y = 0, y0 = 0, y1 = 0, x0 = 0, x1 = 0, x = 0, xe = 0;
   uint32_t rows = kNoRowPack;  // the preprocess's packed per-row ranges (rec[3].w)
-  SplatCut cut{};
-  // the kept tiles of row y: from the packed ranges, else the cut itself (cut_row_range)
+  BandCut cut{};
+  // the kept tiles of row y: from the packed ranges, else the cut itself (band_row_range)
   auto row_range = [&](uint32_t yy) {
     if (rows != kNoRowPack) {
       const uint32_t b = (rows >> (8 * (yy - y0))) & 0xffu;
       x = x0 + (b & 15u);
       xe = x + (b >> 4);
     } else {
-      cut_row_range(cut, yy, x0, x1, x, xe);
+      band_row_range(cut, yy, x0, x1, x, xe);
     }
   };
   if (off < end) {
@@ -89,7 +89,7 @@ __device__ __forceinline__ void duplicate_body(int P, const uint32_t* __restrict
     cc = rows == kNoRowPack ? rec[4 * (size_t)gid + 1].x : 0.0f;
     if (egid) ebeg[gid] = off;
     tile_rect(r0.x, r0.y, (int)rad, gx, gy, x0, y0, x1, y1);
-    if (rows == kNoRowPack) cut = make_cut(r0.x, r0.y, r0.z, r0.w, cc, qc);
+    if (rows == kNoRowPack) cut = make_band_cut(r0.x, r0.y, r0.z, r0.w, cc, qc);
     y = y0;
     if (y < y1) row_range(y);
     else off = end;

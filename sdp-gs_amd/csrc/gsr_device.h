@@ -210,7 +210,7 @@ __device__ __forceinline__ float sigmoid_f(float x) { return 1.0f / (1.0f + expf
 // m in [sqrt(1/2), sqrt(2)), a degree-8 polynomial in m - 1 and the split ln 2 -- every step an
 // explicit IEEE operation, as splat_exp.  The CPU restatement evaluates the same sequence, so
 // the tests can pin the kept tile instances bit for bit;
-// its error (~1 ulp) is irrelevant next to the 2e-2 margin of cut_touches_rect.
+// its error (~1 ulp) is irrelevant next to the 2e-2 margin of the band cut below.
 __device__ __forceinline__ float splat_log(float x) {
   int e;
   float m = __builtin_frexpf(x, &e);  // x = m 2^e, m in [0.5, 1)
@@ -252,73 +252,87 @@ __device__ __forceinline__ float splat_q_cut(float ca, float cb, float cc, float
   return 2.0f * splat_log(255.0f * op);
 }
 
-// Per-splat constants of the rectangle test: centre, conic, q_cut and the two ratios -cb/cc,
-// -cb/ca of the edge minimisers (computed once per splat, not per rectangle edge).
-struct SplatCut {
-  float mx, my, ca, cb, cc, qc, kx, ky;  // kx = -cb / cc (dy* per dx), ky = -cb / ca (dx* per dy)
+// ---- band form of the cut: the binning's tile ranges and the blends' per-wave list masks --------
+// Every consumer asks the same question of a splat: which cells of a grid of pixel rectangles can
+// it reach with alpha >= 1/255 -- the binning per tile (16 x 16), the forward per 4x4 block, the
+// backward per 8x4 wave half.  The cells come in bands of pixel rows, so the x-extent of the
+// ellipse q <= Q inside each band is found once (two square roots) and every cell of the band is
+// an interval overlap.  Q widens q_cut by the margin 2e-2 + 1e-4 |terms| (|terms| <= Q ta on the
+// ellipse), far above the float error of the blend's own evaluation (dx = mx - px carries up to
+// ulp(2048) = 2.4e-4 px, i.e. |dq| <= 2 sqrt(ca q) 2.4e-4 < 3e-3 for q <= 11, ca <= 1/0.3), and
+// the extents get a pixel slack for their own float evaluation: a superset of the cells where any
+// pixel centre can reach alpha >= 1/255.  The blends' lists only decide which work is done, never
+// an output bit; the binning's ranges are restated by the oracle operation for operation and every
+// dropped instance is checked against the reference's own test (tests/test_index_parity.py).
+struct BandCut {
+  float mx, my, ica, cb, det, caQ, hx, hy, dyl, slack;
+  int mode;  // 0: none reachable (q_cut -2), 1: every group (not positive definite / degenerate), 2: test
 };
-__device__ __forceinline__ SplatCut make_cut(float mx, float my, float ca, float cb, float cc,
-                                             float qc) {
-  SplatCut s{mx, my, ca, cb, cc, qc, 0.0f, 0.0f};
-  if (qc >= 0.0f) {  // positive definite: ca, cc > 0
-    s.kx = -cb / cc;
-    s.ky = -cb / ca;
-  }
+__device__ __forceinline__ BandCut make_band_cut(float mx, float my, float ca, float cb, float cc,
+                                                 float qc) {
+  BandCut s{};
+  s.mx = mx; s.my = my;
+  if (qc == -2.0f) { s.mode = 0; return s; }
+  s.mode = 1;
+  if (qc < 0.0f) return s;
+  const float det = ca * cc - cb * cb;
+  if (!(det > 0.0f)) return s;
+  const float h2x = cc / det, h2y = ca / det;  // (half-extent)^2 per unit Q
+  const float ta = ca * h2x + cc * h2y + 2.0f * fabsf(cb) * sqrtf(h2x * h2y);
+  if (!(1e-4f * ta < 0.5f)) return s;
+  const float Q = (qc + 2e-2f) / (1.0f - 1e-4f * ta) * 1.001f;
+  s.mode = 2;
+  s.ica = 1.0f / ca;
+  s.cb = cb;
+  s.det = det;
+  s.caQ = ca * Q;
+  s.hx = sqrtf(Q * h2x) * 1.001f + 1e-3f;
+  s.hy = sqrtf(Q * h2y) * 1.001f + 1e-3f;
+  s.dyl = cb * (s.hx / cc);  // dy of the leftmost point (the rightmost one is at -dyl)
+  s.slack = 2e-3f + 4e-6f * fabsf(mx) + 1e-4f * s.hx;
   return s;
 }
-
-// True unless q > q_cut (plus a safety margin) on the whole rectangle of pixel centres
-// [x0, x1] x [y0, y1].  The minimum of the positive-definite form over a rectangle is 0 when the
-// centre is inside, else it lies on an edge; each edge is a clamped 1-D quadratic minimisation
-// (the minimiser's float rounding only moves the evaluated point along the edge, raising q by a
-// second-order amount far inside the margin).
-__device__ __forceinline__ bool cut_touches_rect(const SplatCut& s, float x0, float x1, float y0,
-                                                 float y1) {
-  if (s.qc == -2.0f) return false;
-  if (s.qc < 0.0f) return true;
-  const float dx0 = x0 - s.mx, dx1 = x1 - s.mx, dy0 = y0 - s.my, dy1 = y1 - s.my;
-  if (dx0 <= 0.0f && dx1 >= 0.0f && dy0 <= 0.0f && dy1 >= 0.0f) return true;
-  float qmin = 3.0e38f, tabs = 0.0f;
-#pragma unroll
-  for (int e = 0; e < 4; e++) {
-    float dx, dy;
-    if (e < 2) {
-      dx = (e == 0) ? dx0 : dx1;
-      dy = fminf(fmaxf(s.kx * dx, dy0), dy1);
-    } else {
-      dy = (e == 2) ? dy0 : dy1;
-      dx = fminf(fmaxf(s.ky * dy, dx0), dx1);
-    }
-    const float t1 = s.ca * dx * dx, t2 = s.cc * dy * dy, t3 = 2.0f * s.cb * dx * dy;
-    const float q = t1 + t2 + t3;
-    if (q < qmin) { qmin = q; tabs = t1 + t2 + fabsf(t3); }
-  }
-  // margin >> the float error of the blend's own evaluation: dx = mx - px carries up to
-  // ulp(2048) = 2.4e-4 px, i.e. |dq| <= 2 sqrt(ca q) * 2.4e-4 < 3e-3 for q <= 11, ca <= 1/0.3
-  return qmin <= s.qc + 2e-2f + 1e-4f * tabs;
+// The ellipse's x-extent [xl, xr] (relative to mx, slack included) over the pixel-centre rows
+// [y0, y1]; false when it misses the band.
+__device__ __forceinline__ bool band_extent(const BandCut& s, float y0, float y1, float& xl,
+                                            float& xr) {
+  const float lo = fmaxf(y0 - s.my, -s.hy), hi = fminf(y1 - s.my, s.hy);
+  if (lo > hi) return false;
+  // x-roots of the line dy: (-cb dy -+ sqrt(ca Q - det dy^2)) / ca
+  const float rl = sqrtf(fmaxf(s.caQ - s.det * lo * lo, 0.0f));
+  const float rh = sqrtf(fmaxf(s.caQ - s.det * hi * hi, 0.0f));
+  const float cl = -s.cb * lo, ch = -s.cb * hi;
+  xl = fminf(cl - rl, ch - rh) * s.ica;
+  xr = fmaxf(cl + rl, ch + rh) * s.ica;
+  if (s.dyl >= lo && s.dyl <= hi) xl = -s.hx;   // the leftmost point lies in the band
+  if (-s.dyl >= lo && -s.dyl <= hi) xr = s.hx;  // the rightmost point lies in the band
+  xl -= s.slack;
+  xr += s.slack;
+  return true;
 }
 
-// Tiles of tile row ty, among [x0, x1), kept by the binning: the contiguous range [a, b) from the
-// first to the last tile passing cut_touches_rect.  In exact arithmetic the passing tiles of a
-// row ARE contiguous (they meet the projection of the convex region q <= cut onto the row band),
-// so the range only adds tiles that rounding could have split off -- a conservative superset.
-// The preprocess counts and the duplication emits exactly these ranges.
-__device__ __forceinline__ void cut_row_range(const SplatCut& s, uint32_t ty, uint32_t x0,
-                                              uint32_t x1, uint32_t& a, uint32_t& b) {
-  if (s.qc < 0.0f) {
+// The binning's cut (the preprocess counts, the duplication emits): per tile row of the splat's
+// rectangle [x0, x1), the tiles [a, b) the ellipse's x-extent in the row's 16-pixel band meets --
+// one contiguous range by construction, O(1) per row.  Empty rows give a = b = x1.
+__device__ __forceinline__ void band_row_range(const BandCut& s, uint32_t ty, uint32_t x0,
+                                               uint32_t x1, uint32_t& a, uint32_t& b) {
+  if (s.mode != 2) {
     a = x0;
-    b = s.qc == -2.0f ? x0 : x1;
+    b = s.mode == 0 ? x0 : x1;
     return;
   }
-  const float y0 = (float)(ty * kTile), y1 = (float)(ty * kTile + kTile - 1);
-  a = x0;
-  while (a < x1 && !cut_touches_rect(s, (float)(a * kTile), (float)(a * kTile + kTile - 1), y0, y1))
-    a++;
-  b = x1;
-  while (b > a + 1 &&
-         !cut_touches_rect(s, (float)((b - 1) * kTile), (float)((b - 1) * kTile + kTile - 1), y0, y1))
-    b--;
-  if (a == x1) b = x1;
+  const float y0 = (float)(ty * kTile);
+  float xl, xr;
+  if (!band_extent(s, y0, y0 + (float)(kTile - 1), xl, xr)) {
+    a = b = x1;
+    return;
+  }
+  // tile t (pixel columns 16 t .. 16 t + 15) is met iff 16 t <= mx + xr and 16 t + 15 >= mx + xl
+  const float fa = fminf(fmaxf(ceilf((s.mx + xl - (float)(kTile - 1)) * (1.0f / kTile)), (float)x0), (float)x1);
+  const float fb = fminf(fmaxf(floorf((s.mx + xr) * (1.0f / kTile)) + 1.0f, (float)x0), (float)x1);
+  a = (uint32_t)fa;
+  b = (uint32_t)fb;
+  if (a >= b) a = b = x1;
 }
 
 // auxiliary.h:58-77 (the 4x4 matrices are row-major tensors read as column-major)

@@ -167,11 +167,11 @@ __device__ __forceinline__ uint32_t preprocess_gaussian(const PreArgs& a, int id
     if (pack)
       for (uint32_t r = 0; r < y1 - y0; r++) packed |= ((x1 - x0) << 4) << (8 * r);
   } else if (qc >= 0.0f) {
-    // per tile row, the kept tiles form one range (cut_row_range): found from both ends
-    const SplatCut cut = make_cut(px, py, con_a, con_b, con_c, qc);
+    // per tile row, the kept tiles form one range (band_row_range)
+    const BandCut cut = make_band_cut(px, py, con_a, con_b, con_c, qc);
     for (uint32_t ty = y0; ty < y1; ty++) {
       uint32_t ra, rb;
-      cut_row_range(cut, ty, x0, x1, ra, rb);
+      band_row_range(cut, ty, x0, x1, ra, rb);
       count += rb - ra;
       if (pack) packed |= ((ra - x0) | ((rb - ra) << 4)) << (8 * (ty - y0));
     }

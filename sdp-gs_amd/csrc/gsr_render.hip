@@ -104,41 +104,53 @@ __device__ __forceinline__ void pixel_of(uint32_t tx, uint32_t ty, uint32_t t, u
   py = ty * kTile + (w >> 1) * 8u + (l >> 3);
 }
 
-// Which of the 4 quadrants a splat can reach: bit w set unless the conservative test of
-// gsr_device.h proves alpha < 1/255 on all 64 pixels of quadrant w.
+// Which of the 4 quadrants a splat can reach: bit w set unless the band form of the cut
+// (gsr_device.h BandCut) proves alpha < 1/255 on all 64 pixels of quadrant w (the quadrants'
+// 8-row bands, each quadrant an interval overlap).
 __device__ __forceinline__ uint32_t wave_mask(float4 r0, float4 r1, float qc, uint32_t tx,
                                               uint32_t ty) {
-  // qc: the record's q_cut (rec[3].z, computed once by the preprocess)
-  if (qc == -1.0f) return 0xfu;
-  if (qc == -2.0f) return 0u;
-  const SplatCut cut = make_cut(r0.x, r0.y, r0.z, r0.w, r1.x, qc);
+  const BandCut s = make_band_cut(r0.x, r0.y, r0.z, r0.w, r1.x, qc);
+  if (s.mode == 0) return 0u;
+  if (s.mode == 1) return 0xfu;
+  const float xa = (float)(tx * kTile) - s.mx;
   uint32_t m = 0;
 #pragma unroll
-  for (int w = 0; w < 4; w++) {
-    const float x0 = (float)(tx * kTile + (w & 1) * 8), x1 = x0 + 7.0f;
-    const float y0 = (float)(ty * kTile + (w >> 1) * 8), y1 = y0 + 7.0f;
-    m |= cut_touches_rect(cut, x0, x1, y0, y1) ? (1u << w) : 0u;
+  for (int h = 0; h < 2; h++) {
+    const float y0 = (float)(ty * kTile + 8u * (uint32_t)h);
+    float xl, xr;
+    if (!band_extent(s, y0, y0 + 7.0f, xl, xr)) continue;
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+      const float x0 = xa + 8.0f * (float)c;
+      m |= (xl <= x0 + 7.0f && xr >= x0) ? (1u << (2 * h + c)) : 0u;
+    }
   }
   return m;
 }
 
-// The backward's finer form: bit 2 w + h for half h (pixel rows 4 h .. 4 h + 3) of quadrant w,
-// for the quadrants w0 .. w0 + NW - 1.
-template <int NW = 4>
-__device__ __forceinline__ uint32_t half_mask(float4 r0, float4 r1, float qc, uint32_t tx,
-                                              uint32_t ty, int w0 = 0) {
-  if (qc == -1.0f) return 0xffu;
-  if (qc == -2.0f) return 0u;
-  const SplatCut cut = make_cut(r0.x, r0.y, r0.z, r0.w, r1.x, qc);
+// The backward's finer form: bit 2 w + h for half h (pixel rows 4 h .. 4 h + 3) of quadrant w, for
+// the quadrants w0, w0 + 1 (one row of quadrants: two 4-row bands of the tile); the ellipse's
+// x-extent in each band is found once and each (quadrant, half) is an interval overlap.
+__device__ __forceinline__ uint32_t half_mask_bands(float4 r0, float4 r1, float qc, uint32_t tx,
+                                                    uint32_t ty, int w0) {
+  const BandCut s = make_band_cut(r0.x, r0.y, r0.z, r0.w, r1.x, qc);
+  if (s.mode == 0) return 0u;
+  if (s.mode == 1) return 0xffu;
+  // the band rows and column starts are re-derived here for each batch: the backend would hoist
+  // them out of the batch loop and spill them (the backward runs at its 128-VGPR cap)
+  asm volatile("" : "+v"(tx), "+v"(ty));
+  const float xa = (float)(tx * kTile) - s.mx;  // the tile's first pixel column, relative
   uint32_t m = 0;
 #pragma unroll
-  for (int wi = 0; wi < NW; wi++) {
-    const int w = w0 + wi;
+  for (int h = 0; h < 2; h++) {
+    const float y0 = (float)(ty * kTile + (uint32_t)(w0 >> 1) * 8u + (uint32_t)h * 4u);
+    float xl, xr;
+    if (!band_extent(s, y0, y0 + 3.0f, xl, xr)) continue;
 #pragma unroll
-    for (int h = 0; h < 2; h++) {
-      const float x0 = (float)(tx * kTile + (w & 1) * 8), x1 = x0 + 7.0f;
-      const float y0 = (float)(ty * kTile + (w >> 1) * 8 + h * 4), y1 = y0 + 3.0f;
-      m |= cut_touches_rect(cut, x0, x1, y0, y1) ? (1u << (2 * w + h)) : 0u;
+    for (int wi = 0; wi < 2; wi++) {
+      const int w = w0 + wi;
+      const float x0 = xa + (float)((w & 1) * 8);
+      m |= (xl <= x0 + 7.0f && xr >= x0) ? (1u << (2 * w + h)) : 0u;
     }
   }
   return m;
@@ -569,7 +581,11 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
     __syncthreads();
     const uint32_t cnt = min((uint32_t)kBatch, tile_last - done_cnt);
     // stage the batch starting at list position done_cnt (back to front)
+#if GSR_ABL_NOSTAGE
+    if (sj < cnt && done_cnt == 0) {
+#else
     if (sj < cnt) {
+#endif
       const uint32_t gid = min(pid_next, a.P - 1u);
       const float4* rec = a.rec + 4 * (size_t)gid;
       if (!upper) {
@@ -577,13 +593,13 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
         const float4 q0 = rec[0], q1 = rec[1], q2 = rec[2], q3 = rec[3];
         s_r0[sj] = make_float4(q0.x, q0.y, q0.z, q1.x);
         s_r1[sj] = make_float2(q0.w, q1.y);
-        s_mask[sj] = (uint8_t)(HALF ? half_mask<2>(q0, q1, q3.z, tx, ty, 0)
+        s_mask[sj] = (uint8_t)(HALF ? half_mask_bands(q0, q1, q3.z, tx, ty, 0)
                                     : wave_mask(q0, q1, q3.z, tx, ty));
         s_c0[sj] = make_float4(q1.w, q2.x, q2.y, q1.z);
         if (FEAT) s_c1[sj] = make_float4(q2.z, q2.w, q3.x, 1.0f);
       } else {
         const float4 q0 = rec[0], q1 = rec[1], q3 = rec[3];
-        s_mask23[sj] = (uint8_t)half_mask<2>(q0, q1, q3.z, tx, ty, 2);
+        s_mask23[sj] = (uint8_t)half_mask_bands(q0, q1, q3.z, tx, ty, 2);
       }
     }
     {  // the next batch's list entries, in flight while this batch is replayed
@@ -831,45 +847,31 @@ __device__ __forceinline__ void pixel_of_blk(uint32_t tx, uint32_t ty, uint32_t 
   py = ty * kTile + (w >> 1) * 8u + (g >> 1) * 4u + ((l >> 2) & 3u);
 }
 
-// Which of the 16 4x4 blocks a splat can reach: bit 4w + g for block g of quadrant w.  The exact
-// quadrant test (wave_mask) ANDed with the blocks met by the axis-aligned bounding box of the
-// splat's cut ellipse q <= c, where c widens q_cut by cut_touches_rect's own margin
-// (2e-2 + 1e-4 |terms|, with |terms| <= c * ta on the ellipse) -- a superset of the blocks where
-// any pixel can reach alpha >= 1/255, like the quadrant test.
+// Which of the 16 4x4 blocks a splat can reach: bit 4w + g for block g of quadrant w (tile column
+// 2 (w & 1) + (g & 1), row 2 (w >> 1) + (g >> 1)).  Band form of the cut (gsr_device.h BandCut):
+// the x-extent of the margin-widened ellipse in each of the tile's four 4-row bands, each block an
+// interval overlap -- exact per block, where the quadrant test AND the ellipse's bounding box kept
+// every block of a quadrant that the box met (and cost four rectangle tests).
 __device__ __forceinline__ uint32_t block_mask(float4 r0, float4 r1, float qc, uint32_t tx,
                                                uint32_t ty) {
-  const uint32_t qm = wave_mask(r0, r1, qc, tx, ty);
-  uint32_t m = 0;
-#pragma unroll
-  for (int w = 0; w < 4; w++) m |= ((qm >> w) & 1u) ? (0xfu << (4 * w)) : 0u;
-  if (qc < 0.0f || m == 0) return m;
-  const float ca = r0.z, cb = r0.w, cc = r1.x;
-  const float det = ca * cc - cb * cb;
-  if (!(det > 0.0f)) return m;
-  const float h2x = cc / det, h2y = ca / det;  // (half-extent)^2 per unit c
-  const float ta = ca * h2x + cc * h2y + 2.0f * fabsf(cb) * sqrtf(h2x * h2y);
-  if (!(1e-4f * ta < 0.5f)) return m;
-  const float c = (qc + 2e-2f) / (1.0f - 1e-4f * ta) * 1.001f;
-  const float hx = sqrtf(c * h2x) * 1.001f + 1e-3f, hy = sqrtf(c * h2y) * 1.001f + 1e-3f;
-  // 4-pixel columns / rows of the tile met by [mx - hx, mx + hx] x [my - hy, my + hy]
-  const float bx0 = (float)(tx * kTile), by0 = (float)(ty * kTile);
-  uint32_t cols = 0, rows = 0;
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    const float x0 = bx0 + 4.0f * i, y0 = by0 + 4.0f * i;
-    cols |= (x0 <= r0.x + hx && x0 + 3.0f >= r0.x - hx) ? (1u << i) : 0u;
-    rows |= (y0 <= r0.y + hy && y0 + 3.0f >= r0.y - hy) ? (1u << i) : 0u;
-  }
-  // block g of quadrant w covers tile column 2 (w & 1) + (g & 1), row 2 (w >> 1) + (g >> 1)
+  const BandCut s = make_band_cut(r0.x, r0.y, r0.z, r0.w, r1.x, qc);
+  if (s.mode == 0) return 0u;
+  if (s.mode == 1) return 0xffffu;
+  const float xa = (float)(tx * kTile) - s.mx;  // the tile's first pixel column, relative
   uint32_t bb = 0;
 #pragma unroll
-  for (int w = 0; w < 4; w++)
+  for (int cy = 0; cy < 4; cy++) {
+    const float y0 = (float)(ty * kTile + 4u * (uint32_t)cy);
+    float xl, xr;
+    if (!band_extent(s, y0, y0 + 3.0f, xl, xr)) continue;
 #pragma unroll
-    for (int g = 0; g < 4; g++) {
-      const int cx = 2 * (w & 1) + (g & 1), cy = 2 * (w >> 1) + (g >> 1);
-      bb |= (((cols >> cx) & (rows >> cy)) & 1u) << (4 * w + g);
+    for (int cx = 0; cx < 4; cx++) {
+      const float x0 = xa + 4.0f * (float)cx;
+      const int w = 2 * (cy >> 1) + (cx >> 1), g = 2 * (cy & 1) + (cx & 1);
+      bb |= (xl <= x0 + 3.0f && xr >= x0) ? (1u << (4 * w + g)) : 0u;
     }
-  return m & bb;
+  }
+  return bb;
 }
 
 // Per-group compaction: group g's list holds, in batch order, the entries whose mask has bit
