@@ -283,6 +283,9 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
   // backward keeps one list per quadrant (its per-(wave, entry) rows)
   constexpr bool HALF = !DET && GSR_BWD_HALF;
   constexpr int kBatch = BwdShape<DET>::kBatch, kSlots = BwdShape<DET>::kSlots;
+  // list entries per test-phase group: 2 in the default backward (106 VGPRs instead of 126 for 4,
+  // which pays for phase 2's four-pixel read batches), 4 in the deterministic one
+  constexpr int kGrp = DET ? 4 : 2;
   // the batch's records, regrouped for the test phase: s_r0 = {x, y, conic.a, conic.c} (the
   // packed pairs of the power), s_r1 = {conic.b, opacity}, s_c0 = {r, g, b, depth},
   // s_c1 = {f0, f1, f2, 1} (alpha channel)
@@ -392,9 +395,6 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
   // Phase 2 over the first `ns` slots (wave-uniform, 1..kSlots).  slotv: lane l holds the batch
   // index of slot l & 7 (set in phase 1, no LDS round trip).
   auto phase2 = [&](uint32_t ns, uint32_t slotv) {
-#if GSR_ABL_NOPHASE2
-    if (HALF) { asm volatile("" ::"v"(slotv), "s"(ns)); return; }
-#endif
     const int j = lane & 7;
     const uint32_t bj = slotv & (uint32_t)(kBatch - 1);  // stale for j >= ns: kept in range
     const float4 r0 = s_r0[bj];
@@ -403,11 +403,13 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
     const float* dp = &s_dp[wid][(lane >> 3) * kDpRow];
     float su = 0.f, sux = 0.f, suxx = 0.f;
     f2 cA = mk2(0.f, 0.f), cB = mk2(0.f, 0.f), cC = mk2(0.f, 0.f), cD = mk2(0.f, 0.f);
-    // The row's reads in batches of two pixels, each batch's reads issued together before its
-    // arithmetic (sched_barrier: the backend otherwise interleaves them one pixel at a time, one
-    // LDS round trip per pixel).  Batches of 4 need 142 VGPRs: 3 waves per SIMD, 1.086 ms against
-    // 0.947 (profiles/r05_bwd_ab.txt)
-    constexpr int kB = 2;
+    // The row's reads in batches of four pixels (two in the deterministic backward), each
+    // batch's reads issued together before its arithmetic (sched_barrier: the backend otherwise
+    // interleaves them one pixel at a time, one LDS round trip per pixel).  Batches of 4 fit the
+    // 128-VGPR budget since the test phase groups 2 entries instead of 4 (round 6: 125 VGPRs,
+    // render_bwd -1.3 %, profiles/r06_bwd_ablation.txt; with 4-entry groups they needed 142 VGPRs,
+    // 3 waves per SIMD, profiles/r05_bwd_ab.txt)
+    constexpr int kB = DET ? 2 : 4;
 #pragma unroll
     for (int t0 = 0; t0 < 8; t0 += kB) {
       f2 p[kB];
@@ -510,11 +512,7 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
 #pragma unroll
         for (int r = 0; r < 4; r++)
           if (gr[r] != 0xffffffffu && g[r] != 0.0f) {
-#if GSR_ABL_NOATOMIC
-            asm volatile("" ::"v"(g[r]), "v"(gr[r]));
-#else
             atomicAdd(a.acc + (size_t)gr[r] * kAccFloats + k, g[r]);
-#endif
           }
       }
       return;
@@ -581,11 +579,7 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
     __syncthreads();
     const uint32_t cnt = min((uint32_t)kBatch, tile_last - done_cnt);
     // stage the batch starting at list position done_cnt (back to front)
-#if GSR_ABL_NOSTAGE
-    if (sj < cnt && done_cnt == 0) {
-#else
     if (sj < cnt) {
-#endif
       const uint32_t gid = min(pid_next, a.P - 1u);
       const float4* rec = a.rec + 4 * (size_t)gid;
       if (!upper) {
@@ -632,17 +626,18 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
     uint32_t slotv = 0;
     // Four list entries per group: the per-pair test (power, G, alpha) of all four is evaluated
     // first (independent work), then the entries are replayed in list order.
-    for (uint32_t k0 = 0; k0 < nlist; k0 += 4) {
-      const uint32_t packed = *reinterpret_cast<const uint32_t*>(&s_list[wid][half][k0]);
+    for (uint32_t k0 = 0; k0 < nlist; k0 += kGrp) {
+      const uint32_t packed = kGrp == 4 ? *reinterpret_cast<const uint32_t*>(&s_list[wid][half][k0])
+                                        : (uint32_t)*reinterpret_cast<const uint16_t*>(&s_list[wid][half][k0]);
       // Every LDS read of the group's entries is issued here, before any arithmetic; the colours
       // are consumed at once by the colour dot product, so the replay below reads no records.
-      float Gv[4], av[4], cdv[4];
-      bool cv[4];
+      float Gv[kGrp], av[kGrp], cdv[kGrp];
+      bool cv[kGrp];
       {
-        float4 r0v[4], c0v[4], c1v[4];
-        float2 r1v[4];
+        float4 r0v[kGrp], c0v[kGrp], c1v[kGrp];
+        float2 r1v[kGrp];
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < kGrp; u++) {
           // (entries past the list's end hold stale bytes: kept inside the batch)
           const uint32_t j = (packed >> (8 * u)) & (uint32_t)(kBatch - 1);
           r0v[u] = s_r0[j];
@@ -650,10 +645,10 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
           c0v[u] = s_c0[j];
           if (FEAT) c1v[u] = s_c1[j];
         }
-        float pw[4];
+        float pw[kGrp];
         float tdist = 1.0f;  // min over the group of |op * G - 1/255| (the exact-path test)
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < kGrp; u++) {
           // the reference's -0.5 (ca dx dx + cc dy dy) - cb dx dy, the pairs as packed products
           // (same operations, same order)
           const float4 r0 = r0v[u];
@@ -685,13 +680,13 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
         }
         if (__ballot(tdist <= 2e-6f * (1.0f / 255.0f))) {
 #pragma unroll
-          for (int u = 0; u < 4; u++) {
+          for (int u = 0; u < kGrp; u++) {
             if (fabsf(r1v[u].y * Gv[u] - (1.0f / 255.0f)) <= 2e-6f * (1.0f / 255.0f))
               Gv[u] = splat_exp(pw[u]);
           }
         }
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < kGrp; u++) {
           const uint32_t j = (packed >> (8 * u)) & (uint32_t)(kBatch - 1);
           const uint32_t rel = tile_last - 1 - done_cnt - j;
           av[u] = fminf(0.99f, r1v[u].y * Gv[u]);
@@ -700,7 +695,7 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, uint32_t
         }
       }
 #pragma unroll
-      for (int u = 0; u < 4; u++) {
+      for (int u = 0; u < kGrp; u++) {
         const bool contrib = cv[u];
         // wave-uniform skip of entries without a contributing lane
         const uint64_t bal = __ballot(contrib);
