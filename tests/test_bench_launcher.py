@@ -83,6 +83,8 @@ def test_dist2_roofline_bracket_is_collective_free():
     one, two = run(1), run(2)
     assert one["collective_exposed_ms"] is None
     assert two["collective_exposed_ms"] is not None
-    r1, r2 = one["roofline"], two["roofline"]
-    assert r1["kernel"] == r2["kernel"], (r1, r2)
-    assert r2["avg_ms"] <= 2.0 * r1["avg_ms"], (r1, r2)
+    # the dominant kernel can differ between the two runs on a scene this small: compare the N = 2
+    # bracket with the same kernel's N = 1 launch time
+    r2 = two["roofline"]
+    base = one["kernels"][r2["kernel"]]["avg_ms"]
+    assert r2["avg_ms"] <= 2.0 * base, (r2, one["kernels"])
