@@ -235,7 +235,7 @@ def main():
                          "consecutive chunks, each forward + backward)")
     ap.add_argument("--no-precolor", action="store_true",
                     help="each view evaluates its SH colour itself instead of the step's pre-pass")
-    ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_r05.json"))
+    ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_r06.json"))
     ap.add_argument("--no-extra-legs", action="store_true",
                     help="skip the train-step, reference-cadence and reference-API legs")
     ap.add_argument("--cpu-threads", type=int, default=0,
