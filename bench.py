@@ -240,7 +240,14 @@ def main():
                     help="skip the train-step, reference-cadence and reference-API legs")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="host threads of the CPU baseline (0: OMP_NUM_THREADS or all cores)")
+    ap.add_argument("--cpu-probe", type=int, default=0, help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.cpu_probe:  # child of cpu_baseline: config 1's CPU forward at this many threads (no GPU)
+        from gsr_amd.synthetic import make_cameras, make_gaussians
+        g1 = make_gaussians(10_000, sh_degree=3, seed=0)
+        c1 = make_cameras(1, 400, 400, seed=0)[0]
+        print(json.dumps({"seconds": _torch_cpu_config1(g1, c1, args.cpu_probe)}), flush=True)
+        return
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         rc, line = launch_ranks(sys.argv[1:], args.gpus)
@@ -960,10 +967,13 @@ def cpu_baseline(model, cams, dimg, ddep, dfeat, deg, threads=0):
     if not threads and full > n and out.get("value"):
         _progress(f"CPU baseline: config-1 probe at {n} and {full} threads")
         c1_share = _torch_cpu_config1(g1, c1, n)
-        c1_full = _torch_cpu_config1(g1, c1, full)
-        out["config1_probe_ms_by_threads"] = {str(n): round(1000 * c1_share, 2),
-                                              str(full): round(1000 * c1_full, 2)}
-        if c1_full < c1_share:
+        # the oversubscribed probe in a child process under its own time limit (on the GPU box
+        # 256 threads on a 16-CPU quota ran for minutes); a timeout counts as slower
+        c1_full = _cpu_probe_child(full, limit_s=90.0)
+        out["config1_probe_ms_by_threads"] = {
+            str(n): round(1000 * c1_share, 2),
+            str(full): round(1000 * c1_full, 2) if c1_full is not None else "timed out after 90 s"}
+        if c1_full is not None and c1_full < c1_share:
             alt = torch_cpu_baseline(model, cams[0], dimg, ddep, dfeat, deg, g1, c1, full,
                                      budget_s=60.0)
             by_threads[str(full)] = alt.get("value")
@@ -977,8 +987,9 @@ def cpu_baseline(model, cams, dimg, ddep, dfeat, deg, threads=0):
                     f"os.cpu_count() = {full} threads measured {alt.get('value')} views/s (slower)"]
         else:
             by_threads[str(full)] = None
+            took = f"{1000 * c1_full:.1f} ms" if c1_full is not None else "over 90 s (stopped)"
             out["protocol"] = out.get("protocol", []) + [
-                f"os.cpu_count() = {full} threads: config 1's forward took {1000 * c1_full:.1f} ms "
+                f"os.cpu_count() = {full} threads: config 1's forward took {took} "
                 f"against {1000 * c1_share:.1f} ms at {n} threads (the job's CPU share of the "
                 f"machine's {full} logical CPUs, cpu_share), so the headline view was not re-timed "
                 f"oversubscribed"]
@@ -1007,6 +1018,29 @@ def _torch_cpu_config1(g1, c1, threads, reps=3):
     finally:
         torch.set_num_threads(prev)
     return float(np.median(ts))
+
+
+def _cpu_probe_child(threads, limit_s):
+    """_torch_cpu_config1 at `threads` in a child process (bench.py --cpu-probe): its seconds, or
+    None when it does not finish within limit_s (it is then killed)."""
+    proc = subprocess.Popen([sys.executable, os.path.abspath(__file__), "--cpu-probe", str(threads)],
+                            stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True,
+                            env={**os.environ, "OMP_NUM_THREADS": str(threads)})
+    t0 = last = time.perf_counter()
+    while proc.poll() is None:
+        now = time.perf_counter()
+        if now - t0 > limit_s:
+            proc.kill()
+            proc.wait()
+            return None
+        if now - last > 30.0:
+            last = now
+            _progress(f"CPU baseline: probe at {threads} threads running ({now - t0:.0f} s)")
+        time.sleep(0.5)
+    try:
+        return float(json.loads(proc.stdout.read().strip().splitlines()[-1])["seconds"])
+    except (ValueError, IndexError, KeyError):
+        return None
 
 
 def _cpu_share():
