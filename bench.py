@@ -142,19 +142,25 @@ def _stage_bytes(stage, P, Pv, R, T, HW, D, C, tile_passes, acc, defer_sh, preco
     packed = 0 < tbits <= 16 and P <= (1 << (32 - tbits))
     # the depth sort's values carry the tile counts when id and count fit 32 bits (no gather)
     vsplit = P <= (1 << (32 - max(1, T.bit_length())))
+    # the multi-view duplication counts the tile sort's digit totals (round 6): no totals pass
+    # re-reading the R keys
+    tot_read = 0 if 0 < tbits <= 16 else R * 4
     return {
         # means (all); scale, rot, opacity, SH, language (visible); radii/tiles/key/value (all);
-        # 64-B splat record + clamp bits (visible), the 64-B gradient accumulator row it zeroes (all)
-        "preprocess": P * 12 + Pv * (12 + 16 + 4 + sh_fwd + 12) + P * 16 + Pv * (64 + 1) + P * 64,
+        # 64-B splat record + clamp bits + 8-B binning word (visible), the 64-B gradient
+        # accumulator row it zeroes (all)
+        "preprocess": P * 12 + Pv * (12 + 16 + 4 + sh_fwd + 12) + P * 16 + Pv * (64 + 1 + 8) + P * 64,
         # one-sweep: digit totals read the keys once, each 8-bit pass that runs (the planned
         # sort skips constant digits) reads and writes key+value; the last gathers the tile count
         # unless the values carry it
         "depth_sort": P * 4 + depth_passes * P * 16 + (0 if vsplit else P * 4),
         "scan": P * 12,
-        # offsets (all), order + 48-B record gather (non-empty), R (tile, id) pairs / packed keys
-        "duplicate": P * 8 + Pv * (4 + 48) + R * (4 if packed else 8),
-        "tile_sort": (R * 4 + (tile_passes - 1) * R * 8 + R * 12) if packed
-                     else R * 4 + tile_passes * R * 16,
+        # offsets (all), order + 8-B binning word gather (non-empty; the few Gaussians whose tile
+        # ranges are not packed read 48 B of their record instead, not counted), R (tile, id)
+        # pairs / packed keys
+        "duplicate": P * 8 + Pv * (4 + 8) + R * (4 if packed else 8),
+        "tile_sort": (tot_read + (tile_passes - 1) * R * 8 + R * 12) if packed
+                     else tot_read + tile_passes * R * 16,
         "ranges": R * 4 + T * 8,
         # point_list + 64-B record per instance, ranges/tile_last, C outputs + final_T + n_contrib
         "render_fwd": R * (4 + 64) + T * 12 + HW * (4 * C + 8),

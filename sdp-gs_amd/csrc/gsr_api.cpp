@@ -39,12 +39,14 @@ GeomState carve_geom(char* base, size_t P) {
   g.clamped = c.take<uint8_t>(P);
   g.radii = c.take<int32_t>(P);
   g.rec = c.take<float4>(4 * P);
+  g.bword = c.take<uint2>(P);
   g.tiles_touched = c.take<uint32_t>(P);
   g.offsets = c.take<uint32_t>(P);
   g.acc = c.take<float>((size_t)kAccFloats * P);
   g.ebeg = c.take<uint32_t>(P);
   g.sort = take_sort_scratch(c, P);
   g.scan_status = c.take<uint64_t>(scan_lb_words(P));
+  g.ttot = c.take<uint32_t>(kSortTotTileWords);
   g.scan_parts = c.take<uint32_t>(scan_parts(P) + 1);
   g.pre_parts = c.take<uint32_t>(2 * ((P + 255) / 256) + 1);
   g.bytes = c.size();
@@ -512,8 +514,7 @@ static int fwd_prep(const FwdModel& m, FwdCam& c) {
   pa.pre_color = c.pre_color; pa.pre_clamp = c.pre_clamp;
   // the preprocess grid also zeroes the depth sort's scratch, the look-back scan's status words
   // and (acc_zero) the backward's accumulators
-  pa.clear = SideClear{g.sort.aux, (size_t)((char*)(g.scan_status + scan_lb_words((size_t)P)) -
-                                            (char*)g.sort.aux)};
+  pa.clear = SideClear{g.sort.aux, (size_t)((char*)(g.ttot + kSortTotTileWords) - (char*)g.sort.aux)};
   pa.acc_zero = m.rows ? 0 : 1;  // the rows layout never reads the accumulator rows
   pa.parts = g.pre_parts;
   if (c.defer_pre) {  // the multi-view call launches the views' preprocesses together
@@ -646,7 +647,7 @@ static int fwd_bin(const FwdModel& m, FwdCam& c) {
   GSR_CHECK(launch_duplicate(P, order, g.offsets, c.radii_ptr, g.rec, c.gx, c.gy, b.tkey_a, b.tval_a,
                              (uint32_t)R, SideClear{b.sort.aux, sort_clear_bytes(b.sort, R, tbits)},
                              SideClear{im.ranges, sizeof(uint2) * ntiles}, stream,
-                             m.rows ? b.egid : nullptr, m.rows ? g.ebeg : nullptr));
+                             m.rows ? b.egid : nullptr, m.rows ? g.ebeg : nullptr, g.bword));
   PROF_END(DUPLICATE);
   bool t_in_b = false;
   PROF_BEGIN(TILE_SORT);
@@ -1307,9 +1308,14 @@ int views_forward_batched(const FwdModel& m, std::vector<FwdCam>& cams, gsr_view
                        SideClear{b.sort.aux, sort_clear_bytes(b.sort, R, tbits)},
                        SideClear{c.im.ranges, sizeof(uint2) * ntiles},
                        m.rows ? b.egid : nullptr, m.rows ? g.ebeg : nullptr, b.tag,
-                       bin_layout_tag(m.det, m.rows), pack};
+                       bin_layout_tag(m.det, m.rows), pack, g.bword};
       ts[l] = SortSpec{b.tkey_a, b.tval_a, b.tkey_b, b.tval_b, (size_t)R, b.sort, nullptr};
       ts[l].lo = (int)pack;
+      if (tbits <= 16) {  // the tile sort's digit totals counted by the duplication (no totals launch)
+        dup[l].ttot = g.ttot;
+        dup[l].tbits = tbits;
+        ts[l].totals = g.ttot;
+      }
     }
     PROF_BEGIN(DUPLICATE);
     GSR_CHECK(launch_duplicate_views(dup, nl, stream));

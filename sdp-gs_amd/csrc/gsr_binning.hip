@@ -32,26 +32,25 @@ __device__ __forceinline__ void wave_sync() {
 // its tile ids into a per-wave LDS window, then the wave copies the window out with coalesced
 // stores (each lane storing at its own offsets puts 64 scattered lines in every store
 // instruction).  Each Gaussian's kept range per tile row comes from the preprocess's packed
-// rec[3].w (rectangles of at most 4 rows x 15 tiles), else from band_row_range itself.
-// (body shared by the one-view kernel and the several-views kernel: blk / nblk = this
-// workgroup's index and the workgroup count of its view)
-__device__ __forceinline__ void duplicate_body(int P, const uint32_t* __restrict__ order,
-                                                   const uint32_t* __restrict__ offsets,
-                                                   const float4* __restrict__ rec, uint32_t gx,
-                                                   uint32_t gy, uint32_t* __restrict__ tkey,
-                                                   uint32_t* __restrict__ tval, uint32_t R,
-                                                   SideClear clear0, SideClear clear1,
-                                                   uint32_t* __restrict__ egid,
-                                                   uint32_t* __restrict__ ebeg, uint32_t blk,
-                                                   uint32_t nblk, uint32_t pack = 0) {
-  constexpr int kWin = 256;  // instances per wave window
-  __shared__ uint32_t s_key[kThreads / 64][kWin];
-  __shared__ uint32_t s_val[kThreads / 64][kWin];
-  __shared__ uint32_t s_eg[kThreads / 64][kWin];
-  const int s = (int)(blk * kThreads + threadIdx.x);
-  const size_t nth = (size_t)nblk * kThreads;
-  side_clear(clear0.p, clear0.bytes, (size_t)s, nth);
-  side_clear(clear1.p, clear1.bytes, (size_t)s, nth);
+// ranges (rectangles of at most 4 rows x 15 tiles), else from band_row_range itself.  The packed
+// case reads only the Gaussian's 8-B binning word (bword), the rest its record.
+// With hist (the multi-view forward): every instance's tile digits of the tile sort's passes are
+// counted in the workgroup's LDS histogram hist[tpasses][256] (duplicate_body flushes it), so the
+// tile sort needs no digit-totals launch re-reading the R keys.
+// One chunk of kThreads depth-sorted Gaussians: s0 = its first.
+constexpr int kWin = 256;  // instances per wave window
+__device__ __forceinline__ void duplicate_chunk(int P, int s0, const uint32_t* __restrict__ order,
+                                                const uint32_t* __restrict__ offsets,
+                                                const float4* __restrict__ rec, uint32_t gx,
+                                                uint32_t gy, uint32_t* __restrict__ tkey,
+                                                uint32_t* __restrict__ tval, uint32_t R,
+                                                uint32_t* __restrict__ egid,
+                                                uint32_t* __restrict__ ebeg, uint32_t pack,
+                                                const uint2* __restrict__ bword,
+                                                uint32_t (*s_key)[kWin], uint32_t (*s_val)[kWin],
+                                                uint32_t (*s_eg)[kWin], uint32_t* hist, int tdw,
+                                                int tpasses) {
+  const int s = s0 + (int)threadIdx.x;
   const int lane = (int)(threadIdx.x & 63), wid = (int)(threadIdx.x >> 6);
   const int sw0 = s - lane;
   if (sw0 >= P) return;  // wave-uniform
@@ -76,20 +75,22 @@ __device__ __forceinline__ void duplicate_body(int P, const uint32_t* __restrict
     }
   };
   if (off < end) {
-    float4 r0;
-    float qc, rad;
-    float cc;
     gid = min(order[s], (uint32_t)P - 1u);  // in range unless a sort gave up (reported)
-    r0 = rec[4 * (size_t)gid];
-    const float4 r3 = rec[4 * (size_t)gid + 3];  // {f2, radius, q_cut, rows}
-    qc = r3.z;
-    rad = r3.y;
-    rows = __float_as_uint(r3.w);
-    // conic.c only for the cut itself (rows not packed)
-    cc = rows == kNoRowPack ? rec[4 * (size_t)gid + 1].x : 0.0f;
+    const uint2 bw = bword ? bword[gid] : make_uint2(0u, kNoRowPack);
+    if (bw.y != kNoRowPack) {  // the same x0, y0, y1 and ranges the record path derives
+      x0 = bw.x & 0x3fffu;
+      y0 = (bw.x >> 14) & 0x3fffu;
+      y1 = y0 + (bw.x >> 28);
+      rows = bw.y;
+    } else {
+      const float4 r0 = rec[4 * (size_t)gid];
+      const float4 r3 = rec[4 * (size_t)gid + 3];  // {f2, radius, q_cut, rows}
+      rows = __float_as_uint(r3.w);
+      tile_rect(r0.x, r0.y, (int)r3.y, gx, gy, x0, y0, x1, y1);
+      if (rows == kNoRowPack)  // conic.c only for the cut itself
+        cut = make_band_cut(r0.x, r0.y, r0.z, r0.w, rec[4 * (size_t)gid + 1].x, r3.z);
+    }
     if (egid) ebeg[gid] = off;
-    tile_rect(r0.x, r0.y, (int)rad, gx, gy, x0, y0, x1, y1);
-    if (rows == kNoRowPack) cut = make_band_cut(r0.x, r0.y, r0.z, r0.w, cc, qc);
     y = y0;
     if (y < y1) row_range(y);
     else off = end;
@@ -114,11 +115,63 @@ __device__ __forceinline__ void duplicate_body(int P, const uint32_t* __restrict
     }
     wave_sync();
     for (uint32_t i = (uint32_t)lane; i < wend - wbeg; i += 64) {
-      tkey[wbeg + i] = s_key[wid][i];
+      const uint32_t kk = s_key[wid][i];
+      tkey[wbeg + i] = kk;
       if (!pack) tval[wbeg + i] = s_val[wid][i];
       if (egid) egid[wbeg + i] = s_eg[wid][i];
+      if (hist) {  // the tile's digits (radix_totals_body's, gsr_sort.hip)
+        const uint32_t t = pack ? kk >> pack : kk, dm = (1u << tdw) - 1u;
+        atomicAdd(&hist[t & dm], 1u);
+        if (tpasses > 1) atomicAdd(&hist[256 + ((t >> tdw) & dm)], 1u);
+      }
     }
     wave_sync();
+  }
+}
+
+// Gaussians per duplication workgroup: kDupChunks chunks of kThreads, one after the other (fewer
+// workgroups: fewer histogram flushes, each a set of device-scope atomics on shared lines)
+constexpr int kDupChunks = 4;
+constexpr int kDupPerBlock = kThreads * kDupChunks;
+// (body shared by the one-view kernel and the several-views kernel: blk / nblk = this
+// workgroup's index and the workgroup count of its view)
+__device__ __forceinline__ void duplicate_body(int P, const uint32_t* __restrict__ order,
+                                               const uint32_t* __restrict__ offsets,
+                                               const float4* __restrict__ rec, uint32_t gx,
+                                               uint32_t gy, uint32_t* __restrict__ tkey,
+                                               uint32_t* __restrict__ tval, uint32_t R,
+                                               SideClear clear0, SideClear clear1,
+                                               uint32_t* __restrict__ egid,
+                                               uint32_t* __restrict__ ebeg, uint32_t blk,
+                                               uint32_t nblk, uint32_t pack,
+                                               const uint2* __restrict__ bword,
+                                               uint32_t* __restrict__ ttot, int tbits) {
+  __shared__ uint32_t s_key[kThreads / 64][kWin];
+  __shared__ uint32_t s_val[kThreads / 64][kWin];
+  __shared__ uint32_t s_eg[kThreads / 64][kWin];
+  __shared__ uint32_t s_hist[2 * 256];
+  const size_t tid = (size_t)blk * kThreads + threadIdx.x, nth = (size_t)nblk * kThreads;
+  side_clear(clear0.p, clear0.bytes, tid, nth);
+  side_clear(clear1.p, clear1.bytes, tid, nth);
+  // kernel-argument (grid-uniform) branch; tbits <= 16 (launch_duplicate_views)
+  const int tpasses = ttot ? sort_passes(tbits) : 0, tdw = ttot ? sort_digit_bits(tbits) : 0;
+  if (ttot) {
+    s_hist[threadIdx.x] = 0u;
+    s_hist[256 + threadIdx.x] = 0u;
+    __syncthreads();
+  }
+  for (int c = 0; c < kDupChunks; c++)
+    duplicate_chunk(P, (int)(blk * kDupPerBlock + c * kThreads), order, offsets, rec, gx, gy, tkey,
+                    tval, R, egid, ebeg, pack, bword, s_key, s_val, s_eg, ttot ? s_hist : nullptr,
+                    tdw, tpasses);
+  if (ttot) {
+    __syncthreads();
+    // this workgroup's partial copy of the totals (radix_totals_body's shards)
+    uint32_t* tot = ttot + (size_t)(blk % (uint32_t)kSortTotShards) * kSortMaxPasses * 256;
+    for (int p = 0; p < tpasses; p++) {
+      const uint32_t c = s_hist[p * 256 + threadIdx.x];
+      if (c) atomicAdd(&tot[p * 256 + threadIdx.x], c);
+    }
   }
 }
 
@@ -132,9 +185,10 @@ __global__ __launch_bounds__(kThreads) void duplicate_kernel(int P,
                                                              uint32_t R, SideClear clear0,
                                                              SideClear clear1,
                                                              uint32_t* __restrict__ egid,
-                                                             uint32_t* __restrict__ ebeg) {
+                                                             uint32_t* __restrict__ ebeg,
+                                                             const uint2* __restrict__ bword) {
   duplicate_body(P, order, offsets, rec, gx, gy, tkey, tval, R, clear0, clear1, egid, ebeg,
-                 blockIdx.x, gridDim.x);
+                 blockIdx.x, gridDim.x, 0u, bword, nullptr, 0);
 }
 
 // Instances per lane of the ranges kernel: consecutive keys, one 16-B load when aligned (one
@@ -227,7 +281,7 @@ __global__ __launch_bounds__(kThreads) void duplicate_views_kernel(DupViews m) {
   if (j.tag && blockIdx.x == m.first[k] && threadIdx.x == 0) *j.tag = j.tag_val;
   duplicate_body(j.P, j.order, j.offsets, j.rec, j.gx, j.gy, j.tkey, j.tval, j.R, j.clear0,
                  j.clear1, j.egid, j.ebeg, blockIdx.x - m.first[k], m.first[k + 1] - m.first[k],
-                 j.pack);
+                 j.pack, j.bword, j.ttot, j.tbits);
 }
 
 __global__ __launch_bounds__(kThreads) void tile_ranges_views_kernel(RangesViews m) {
@@ -258,10 +312,12 @@ hipError_t launch_det_gather(size_t R, const uint32_t* einst, const uint32_t* eg
 hipError_t launch_duplicate(int P, const uint32_t* order, const uint32_t* offsets,
                             const int32_t* radii, const float4* rec, uint32_t gx, uint32_t gy,
                             uint32_t* tkey, uint32_t* tval, uint32_t R, SideClear clear0,
-                            SideClear clear1, hipStream_t s, uint32_t* egid, uint32_t* ebeg) {
+                            SideClear clear1, hipStream_t s, uint32_t* egid, uint32_t* ebeg,
+                            const uint2* bword) {
   if (P == 0) return hipSuccess;
-  hipLaunchKernelGGL(duplicate_kernel, dim3((P + kThreads - 1) / kThreads), dim3(kThreads), 0, s,
-                     P, order, offsets, rec, gx, gy, tkey, tval, R, clear0, clear1, egid, ebeg);
+  hipLaunchKernelGGL(duplicate_kernel, dim3((P + kDupPerBlock - 1) / kDupPerBlock), dim3(kThreads), 0, s,
+                     P, order, offsets, rec, gx, gy, tkey, tval, R, clear0, clear1, egid, ebeg,
+                     bword);
   return hipGetLastError();
 }
 
@@ -276,8 +332,10 @@ hipError_t launch_duplicate_views(const DupSpec* v, int V, hipStream_t s) {
     if (d.pack && (d.egid || d.pack >= 32u || (uint64_t)d.P > (1ull << d.pack) ||
                    (uint64_t)d.gx * d.gy > (1ull << (32u - d.pack))))
       return hipErrorInvalidValue;  // tile << pack | gid must fit 32 bits
+    if (d.ttot && (d.tbits <= 0 || d.tbits > 16 || (uint64_t)d.gx * d.gy > (1ull << d.tbits)))
+      return hipErrorInvalidValue;  // two digit passes at most (the LDS histogram's)
     m.j[k] = v[k];
-    m.first[k + 1] = m.first[k] + (uint32_t)((v[k].P + kThreads - 1) / kThreads);
+    m.first[k + 1] = m.first[k] + (uint32_t)((v[k].P + kDupPerBlock - 1) / kDupPerBlock);
   }
   if (m.first[V] == 0) return hipSuccess;
   hipLaunchKernelGGL(duplicate_views_kernel, dim3(m.first[V]), dim3(kThreads), 0, s, m);

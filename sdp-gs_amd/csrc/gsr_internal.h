@@ -57,7 +57,13 @@ constexpr int kSortTile = 256 * GSR_SORT_KPT;  // keys per radix-sort workgroup 
 
 inline size_t scan_parts(size_t n) { return (n + kScanTile - 1) / kScanTile; }
 inline size_t sort_blocks(size_t n) { return (n + kSortTile - 1) / kSortTile; }
-inline int sort_passes(int bits) { return (bits + 7) / 8; }
+constexpr int sort_passes(int bits) { return (bits + 7) / 8; }
+// Digit width of a sort over `bits` key bits: the passes split the bits evenly (12-bit tile ids:
+// 6 + 6 instead of 8 + 4) -- fewer, longer runs per bucket in the scatter of the first pass.  Any
+// split gives the same stable order.  (constexpr: host and device)
+constexpr int sort_digit_bits(int bits) {
+  return (bits + sort_passes(bits) - 1) / sort_passes(bits);
+}
 constexpr int kSortMaxPasses = 4;
 // Partitions per look-back super-partition: besides its own status word, every partition adds its
 // digit counts into its super-partition's word, so a look-back crosses 16 partitions per word.
@@ -72,6 +78,7 @@ inline size_t sort_status_len(size_t n) { return (size_t)kSortMaxPasses * sort_p
 // atomics serialise at the memory side, so one shared copy made ~250-720 workgroups queue on the
 // same 8 lines), sentinel-key counts [shard], partition tickets [kSortMaxPasses][8], error flag
 constexpr int kSortTotShards = 16;
+constexpr size_t kSortTotTileWords = (size_t)kSortTotShards * kSortMaxPasses * 256;
 constexpr size_t kSortAuxTotals = 0,
                  kSortAuxSent = kSortAuxTotals + (size_t)kSortTotShards * kSortMaxPasses * 256,
                  kSortAuxTickets = kSortAuxSent + kSortTotShards,
@@ -157,6 +164,10 @@ struct SortSpec {
   // > 0: the values carry a payload in bits [vsplit, 32); the last pass writes (value >> vsplit)
   // in place of the key and value & (2^vsplit - 1) as the value (no key_payload gather)
   int vsplit = 0;
+  // digit totals formed by an earlier kernel on the stream, laid out as the totals launch's
+  // ([kSortTotShards][kSortMaxPasses][256], the multi-view duplication's GeomState::ttot): the
+  // totals launch is skipped.  All views or none; not with a planned sort, sums or sentinels.
+  const uint32_t* totals = nullptr;
 };
 // sums (one per view, optional): the views' read-back sums formed inside the digit-totals launch
 // (sum_u32_parts_views folded in); after_totals (optional): recorded right after that launch
@@ -213,6 +224,10 @@ struct GeomState {
   uint8_t* clamped;         // [P] bit c set <=> SH colour channel c clamped (forward.cu:67-69)
   int32_t* radii;           // [P] internal radii (used when the caller passes none)
   float4* rec;              // [P*4] splat record for the blend
+  // [P] the duplication's 8-B binning word of a Gaussian with tiles (gsr_preprocess.hip
+  // bin_word): .x = x0 | y0 << 14 | rows << 28 of its tile rectangle, .y = its packed per-row kept
+  // ranges (rec[3].w); .y = kNoRowPack: not packed, the duplication reads the record instead
+  uint2* bword;
   uint32_t* tiles_touched;  // [P]
   uint32_t* offsets;        // [P] inclusive scan of tiles_touched in depth order
   float* acc;               // [P*16] backward accumulators (atomic mode; not the deterministic backward)
@@ -223,6 +238,9 @@ struct GeomState {
   // [scan_lb_words(P)] look-back scan status (the batched forward's scan); follows the sort
   // scratch so that the preprocess's side clear zeroes both (scan_clear_end)
   uint64_t* scan_status;
+  // [kSortTotTileWords] the tile sort's digit totals, added up by the multi-view duplication
+  // (DupSpec::ttot) for its sort (SortSpec::totals); zeroed by the same side clear
+  uint32_t* ttot;
   // [2 * ceil(P/256)] per preprocess workgroup: the sum of its exact tile counts, then (second
   // half) the sum of its full 3-sigma tile rectangles -- the reference's tiles_touched
   // (forward.cu:255), whose total is the num_rendered the boundary returns
@@ -396,7 +414,7 @@ hipError_t launch_duplicate(int P, const uint32_t* order, const uint32_t* offset
                             const int32_t* radii, const float4* rec, uint32_t gx, uint32_t gy,
                             uint32_t* tkey, uint32_t* tval, uint32_t R, SideClear clear0,
                             SideClear clear1, hipStream_t s, uint32_t* egid = nullptr,
-                            uint32_t* ebeg = nullptr);
+                            uint32_t* ebeg = nullptr, const uint2* bword = nullptr);
 // ranges_cleared: the ranges are already zero (duplicate's side clear): no memset launch.
 // Also writes the call's status word from the depth / tile sorts' error words (either may be null).
 // A failed call also or-s its status into `fault` (forward_faults_word(), may be null).
@@ -423,6 +441,11 @@ struct DupSpec {
   // > 0: packed keys tile << pack | gid into tkey for the keys-only tile sort (tval not written;
   // needs gid < 2^pack, no egid)
   uint32_t pack = 0;
+  const uint2* bword = nullptr;  // GeomState::bword (null: every Gaussian's record is read)
+  // non-null: the duplication also adds the digit counts of the tile sort over `tbits` bits
+  // (tbits <= 16) into these zeroed totals (layout of SortSpec::totals)
+  uint32_t* ttot = nullptr;
+  int tbits = 0;
 };
 hipError_t launch_duplicate_views(const DupSpec* v, int V, hipStream_t s);
 struct RangesSpec {

@@ -13,7 +13,10 @@
 //                                        gsr_device.h, computed once here for the binning and blends;
 //                                        rows: the kept tile range of each row, packed (kNoRowPack:
 //                                        not packed), so the duplication does not re-run the cut)
-// so the blend reads one contiguous record per instance instead of five scattered arrays.
+// so the blend reads one contiguous record per instance instead of five scattered arrays.  A
+// Gaussian with tiles also gets its 8-B binning word (GeomState::bword): the duplication, which
+// visits the Gaussians in depth order, gathers that word instead of two 16-B parts of the 64-B
+// record (round 6: the record gather fetched ~2x the duplication's algorithmic bytes).
 #include "gsr_device.h"
 #include "gsr_internal.h"
 #include "gsr_sh.h"
@@ -177,6 +180,10 @@ __device__ __forceinline__ uint32_t preprocess_gaussian(const PreArgs& a, int id
     }
   }
   g.tiles_touched[idx] = count;
+  if (count) {
+    const bool word = pack && x0 < (1u << 14) && y0 < (1u << 14);
+    g.bword[idx] = make_uint2(x0 | (y0 << 14) | ((y1 - y0) << 28), word ? packed : kNoRowPack);
+  }
   g.dkey_a[idx] = __float_as_uint(depth);
   if (a.vpack) g.dval_a[idx] = (uint32_t)idx | (count << a.vpack);
   rec[0 ^ sw] = make_float4(px, py, con_a, con_b);

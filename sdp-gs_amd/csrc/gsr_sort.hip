@@ -230,13 +230,7 @@ constexpr int kTotKPT = 8;
 constexpr size_t kTotGroups = 1024;
 constexpr int kTotTile = kThreads * kTotKPT;
 
-// Digit width of a sort over `bits` key bits: the passes (ceil(bits / 8)) split the bits evenly
-// (12-bit tile ids: 6 + 6 instead of 8 + 4) -- fewer, longer runs per bucket in the scatter of the
-// first pass.  Any split gives the same stable order.
-__host__ __device__ __forceinline__ int sort_digit_width(int bits) {
-  const int passes = (bits + 7) / 8;
-  return (bits + passes - 1) / passes;
-}
+__host__ __device__ __forceinline__ int sort_digit_width(int bits) { return sort_digit_bits(bits); }
 
 // (body shared by the one-sort kernel and the several-sorts kernel: blk / nblk = this
 // workgroup's index and the workgroup count of its sort)
@@ -653,6 +647,7 @@ struct SortPassJob {
   uint32_t *kc, *vc;     // planned sort: (kin, vin) = A, (kout, vout) = B, this = C (else null)
   const uint32_t* kpay;  // last pass: payload gathered in place of the key
   uint32_t* aux;         // totals, sentinel counts, tickets, error word (kSortAux*)
+  const uint32_t* tot;   // the digit totals the passes read (aux's, or SortSpec::totals)
   uint64_t* status;      // this pass's look-back words
   uint32_t n;
   uint32_t ulo;          // keys-only sort, last pass: the value bits to unpack (else 0)
@@ -735,7 +730,7 @@ __global__ __launch_bounds__(NT, NT == 1024 ? 8 : (NT == 512 ? 6 : 1)) void radi
   if (j.kc) {  // planned (workgroup-uniform per view: the view's own plan)
     if (!planned_pass(j.aux[kSortAuxPlan], pass, j.kin, j.vin, j.kout, j.vout, j.kc, j.vc, o)) return;
   }
-  onesweep_body<NT>(o.kin, o.vin, j.n, shift, bits, j.aux + kSortAuxTotals + 256 * pass,
+  onesweep_body<NT>(o.kin, o.vin, j.n, shift, bits, j.tot + 256 * pass,
                     sentinel ? j.aux + kSortAuxSent : nullptr, j.aux + kSortAuxTickets + 8 * pass,
                     j.status, j.aux + kSortAuxErr, o.kout, o.vout, o.last ? j.kpay : nullptr,
                     blockIdx.x - m.first[k], m.first[k + 1] - m.first[k], j.ulo,
@@ -1116,9 +1111,13 @@ hipError_t radix_sort_pairs_views(const SortSpec* v, int V, int bits, bool* resu
     if (v[k].lo != lo || (lo && v[k].key_payload) || v[k].vsplit < 0 || v[k].vsplit >= 32 ||
         (v[k].vsplit && (v[k].key_payload || lo)))
       return hipErrorInvalidValue;
+  // totals formed upstream (the multi-view duplication): no totals launch
+  const bool given = v[0].totals != nullptr;
+  if (given && (planned || sums || after_totals || sentinel_anywhere)) return hipErrorInvalidValue;
   uint32_t tfirst[kMaxBatchViews + 1] = {0}, ofirst[kMaxBatchViews + 1] = {0};
   for (int k = 0; k < V; k++) {
     const size_t n = v[k].n;
+    if ((v[k].totals != nullptr) != given) return hipErrorInvalidValue;
     if (n > 0xffffffffull) return hipErrorInvalidValue;
     if ((v[k].kc != nullptr) != planned || (v[k].kc && !v[k].vc)) return hipErrorInvalidValue;
     if (!precleared && n) {
@@ -1148,6 +1147,7 @@ hipError_t radix_sort_pairs_views(const SortSpec* v, int V, int bits, bool* resu
       j.kpay = (planned || p == passes - 1) ? w.key_payload : nullptr;
       j.vsplit = (planned || p == passes - 1) ? (uint32_t)w.vsplit : 0u;
       j.aux = w.scratch.aux;
+      j.tot = w.totals ? w.totals : w.scratch.aux + kSortAuxTotals;
       j.status = w.scratch.status + (size_t)p * sort_pass_words(w.n);
       j.n = (uint32_t)w.n;
     }
@@ -1162,8 +1162,9 @@ hipError_t radix_sort_pairs_views(const SortSpec* v, int V, int bits, bool* resu
                        (int)sums[k].n};
     }
   }
-  hipLaunchKernelGGL(radix_totals_views_kernel, dim3(tfirst[V]), dim3(kThreads), 0, s, m, bits,
-                     sentinel_anywhere ? 1 : 0, lo, sm);
+  if (!given)
+    hipLaunchKernelGGL(radix_totals_views_kernel, dim3(tfirst[V]), dim3(kThreads), 0, s, m, bits,
+                       sentinel_anywhere ? 1 : 0, lo, sm);
   if (after_totals) {
     const hipError_t e = hipEventRecord(after_totals, s);
     if (e != hipSuccess) return e;
