@@ -1282,7 +1282,9 @@ int views_forward_batched(const FwdModel& m, std::vector<FwdCam>& cams, gsr_view
     // same (tile, gid) pairs the pair sort does -- a stable sort on the tile bits keeps each
     // tile's depth order, so the result is bit-identical.  The deterministic rows path sorts
     // instance indices (egid) and keeps the pair sort.
-    const uint32_t pack = (!m.rows && tbits <= 16 && (uint64_t)P <= (1ull << (32 - tbits)))
+    // (one tile, tbits = 0: no tile sort at all, plain pairs)
+    const uint32_t pack = (!m.rows && tbits > 0 && tbits <= 16 &&
+                           (uint64_t)P <= (1ull << (32 - tbits)))
                               ? (uint32_t)(32 - tbits)
                               : 0u;
     {  // the group's binning buffers in one allocation callback (sizes from the read-back)
@@ -1311,7 +1313,7 @@ int views_forward_batched(const FwdModel& m, std::vector<FwdCam>& cams, gsr_view
                        bin_layout_tag(m.det, m.rows), pack, g.bword};
       ts[l] = SortSpec{b.tkey_a, b.tval_a, b.tkey_b, b.tval_b, (size_t)R, b.sort, nullptr};
       ts[l].lo = (int)pack;
-      if (tbits <= 16) {  // the tile sort's digit totals counted by the duplication (no totals launch)
+      if (tbits > 0 && tbits <= 16) {  // the tile sort's digit totals counted by the duplication (no totals launch)
         dup[l].ttot = g.ttot;
         dup[l].tbits = tbits;
         ts[l].totals = g.ttot;

@@ -58,6 +58,17 @@ def test_batched_forward_wide_ids_equals_single_view():
     assert all(c[1] > 0 for c in counts)
 
 
+def test_batched_forward_one_tile_image():
+    """A 16x12 image is ONE tile: no tile bits, so no keys-only packing (tile << 32 does not fit)
+    and no tile sort at all -- the batched forward keeps the duplication's depth order, bitwise the
+    single-view call (round 6: it used to pick a 32-bit pack shift and the launch refused it)."""
+    W, H = 16, 12
+    m = SplatModel(make_gaussians(3_000, sh_degree=3, seed=11), device="cuda")
+    cams = [c.to("cuda") for c in make_cameras(3, W, H, seed=11, distance=4.0)]
+    counts = _batched_vs_single(m, cams)
+    assert any(c[1] > 0 for c in counts)
+
+
 @pytest.mark.parametrize("nviews,distance", [(1, 4.0), (7, 4.0), (10, 4.0), (5, 1.6)])
 def test_batched_forward_equals_single_view(nviews, distance):
     """(distance 4: every binned depth in [2, 8), one top byte -- the batched depth sort leaves its
