@@ -1,7 +1,7 @@
 """Backward-blend list statistics of the bench scene (CPU, C oracle): per wave half (8x4 pixels),
 how many list entries round 5's conservative test kept (ellipse of alpha >= 1/255 against the
 half's rectangle of pixel centres, without its safety margin; round 6 replaced it by the band form,
-gsr_device.h band_extent, within a few % of the pixel-exact count)
+gsr_device.h band_extent)
 against a pixel-exact test (some pixel centre of the half inside the ellipse) and against the
 entries that actually contribute (the forward's accepted pairs).  Lockstep steps per wave = the
 max over its two halves.  Test-side tool (uses oracle/), not part of the product.
