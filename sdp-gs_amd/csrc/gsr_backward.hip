@@ -240,6 +240,20 @@ __device__ __forceinline__ void bwd_model(const BwdPreArgs& a, size_t i, BwdMode
   md.y = sigmoid_f(a.opacities_raw[i]);
 }
 
+// One view's pre-pass colour Jacobian (planar [9][P]) and clamp bits of one Gaussian, loaded one
+// view ahead by the multi-view kernel with its gradient row
+struct ViewJac {
+  float j[9];
+  uint32_t cl;
+};
+__device__ __forceinline__ void view_jac(const BwdPreArgs& a, size_t i, ViewJac& o) {
+  const float* j = a.pre_jac + i;
+  const size_t P = (size_t)a.P;
+#pragma unroll
+  for (int k = 0; k < 9; k++) o.j[k] = GSR_BWD_NT ? __builtin_nontemporal_load(j + k * P) : j[k * P];
+  o.cl = a.clamped[i];
+}
+
 // Backward of one visible Gaussian.  sh0 / sh1: its rows (coefficient 0 / coefficients 1..) of
 // the LDS staging planes: SH coefficients in, SH gradients out; unused without SH.  The
 // per-view outputs (screen-space gradient, deferred dL/dRGB, SH rows) are written here; the
@@ -248,7 +262,8 @@ __device__ __forceinline__ void bwd_model(const BwdPreArgs& a, size_t i, BwdMode
 template <bool ACC, class Sink>
 __device__ __forceinline__ void gaussian_bwd(const BwdPreArgs& a, size_t i, float* sh0,
                                              float* sh1, Sink& sk, const BwdModel* md = nullptr,
-                                             const float4* row = nullptr) {
+                                             const float4* row = nullptr,
+                                             const ViewJac* vj = nullptr) {
   float4 q0, q1, q2, q3;
   if (row) {
     q0 = row[0]; q1 = row[1]; q2 = row[2]; q3 = row[3];
@@ -362,7 +377,7 @@ __device__ __forceinline__ void gaussian_bwd(const BwdPreArgs& a, size_t i, floa
 
   // ---- SH colour backward (backward.cu:390-391) ----
   if (a.shs || a.fused) {
-    const uint8_t cl = a.clamped[i];
+    const uint32_t cl = vj ? vj->cl : (uint32_t)a.clamped[i];
     V3 dRGB = dL_dcolor;
     dRGB.x *= (cl & 1) ? 0 : 1;
     dRGB.y *= (cl & 2) ? 0 : 1;
@@ -371,11 +386,13 @@ __device__ __forceinline__ void gaussian_bwd(const BwdPreArgs& a, size_t i, floa
     if (a.pre_jac) {  // Jacobian from the multi-view pre-pass; dL/dRGB deferred or to the sink
       if (a.dRGB_out) put3p(a.dRGB_out, (size_t)a.P, i, dRGB);
       sk.rgb(dRGB);
-      const float* j = a.pre_jac + i;  // planar [9][P]
-      const size_t P = (size_t)a.P;
-      auto jl = [&](size_t o) { return GSR_BWD_NT ? __builtin_nontemporal_load(j + o) : j[o]; };
-      const V3 jx = v3(jl(0), jl(P), jl(2 * P)), jy = v3(jl(3 * P), jl(4 * P), jl(5 * P)),
-               jz = v3(jl(6 * P), jl(7 * P), jl(8 * P));
+      ViewJac own;
+      if (!vj) {
+        view_jac(a, i, own);
+        vj = &own;
+      }
+      const V3 jx = v3(vj->j[0], vj->j[1], vj->j[2]), jy = v3(vj->j[3], vj->j[4], vj->j[5]),
+               jz = v3(vj->j[6], vj->j[7], vj->j[8]);
       const V3 dL_ddir = v3(dot3(jx, dRGB), dot3(jy, dRGB), dot3(jz, dRGB));
       dmean = dmean + dnormvdv(dir_orig, dL_ddir);
     } else if (a.dRGB_out) {  // deferred: dL/dsh = basis(dir) x dRGB is formed by the step's flush
@@ -570,8 +587,10 @@ __device__ __forceinline__ void views_body(const BwdPreViews& m, size_t i, float
   BwdModel md;
   bwd_model(a0, i, md);
   float4 cur[4], nxt[4];
+  ViewJac jcur, jnxt;
   int rcur = a0.radii[i], rnxt = 0;
   grad_row(a0, i, cur[0], cur[1], cur[2], cur[3]);
+  view_jac(a0, i, jcur);
 #pragma unroll 1
   for (int v = 0; v < m.V; v++) {
     const BwdPreArgs& a = m.v[v];
@@ -579,6 +598,7 @@ __device__ __forceinline__ void views_body(const BwdPreViews& m, size_t i, float
       const BwdPreArgs& an = m.v[v + 1];
       rnxt = an.radii[i];
       grad_row(an, i, nxt[0], nxt[1], nxt[2], nxt[3]);
+      view_jac(an, i, jnxt);
     }
     sk.rgb_lds = rgb ? rgb + v * 3 * kThreads : nullptr;
     if (a.status && *a.status) {  // this view's forward failed (view-uniform): NaN gradients
@@ -593,7 +613,7 @@ __device__ __forceinline__ void views_body(const BwdPreViews& m, size_t i, float
       touched = true;
     } else if (rcur > 0) {
       const BwdModel mv = opaque(md);
-      gaussian_bwd<true>(a, i, nullptr, nullptr, sk, &mv, cur);
+      gaussian_bwd<true>(a, i, nullptr, nullptr, sk, &mv, cur, &jcur);
       sk.assign = false;
       touched = true;
     } else {
@@ -604,6 +624,7 @@ __device__ __forceinline__ void views_body(const BwdPreViews& m, size_t i, float
     }
 #pragma unroll
     for (int k = 0; k < 4; k++) cur[k] = nxt[k];
+    jcur = jnxt;
     rcur = rnxt;
   }
   if (!touched) return;  // accumulate mode, culled in every view: nothing to add
