@@ -69,6 +69,18 @@ def test_batched_forward_one_tile_image():
     assert any(c[1] > 0 for c in counts)
 
 
+def test_batched_forward_17_tile_bits():
+    """More than 2^16 tiles (4128x4096: 258 x 256 = 66048 tiles, 17 tile bits, 3 tile-sort passes):
+    the duplication does not count the tile sort's digit totals (its LDS histogram holds two
+    passes), the tile sort runs its own totals launch -- still bitwise the single-view call."""
+    W, H = 4128, 4096
+    assert ((W // 16) * (H // 16) - 1).bit_length() == 17
+    m = SplatModel(make_gaussians(20_000, sh_degree=3, seed=17), device="cuda")
+    cams = [c.to("cuda") for c in make_cameras(2, W, H, seed=17)]
+    counts = _batched_vs_single(m, cams)
+    assert all(c[1] > 0 for c in counts)
+
+
 @pytest.mark.parametrize("nviews,distance", [(1, 4.0), (7, 4.0), (10, 4.0), (5, 1.6)])
 def test_batched_forward_equals_single_view(nviews, distance):
     """(distance 4: every binned depth in [2, 8), one top byte -- the batched depth sort leaves its
