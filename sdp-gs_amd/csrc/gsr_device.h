@@ -292,6 +292,40 @@ __device__ __forceinline__ BandCut make_band_cut(float mx, float my, float ca, f
   s.slack = 2e-3f + 4e-6f * fabsf(mx) + 1e-4f * s.hx;
   return s;
 }
+// The blends' form of the same cut: hardware reciprocals (v_rcp_f32, ~1 ulp) in place of the five
+// IEEE divisions (~10 instructions each), on every list entry of every tile of both blends.  Its
+// Q, hx, hy, 1/ca and dyl differ from make_band_cut's by a few ulp, against margins of 2e-2 on Q,
+// 1e-3 px on the half-extents and 2e-3 px of slack (above), so the cells it keeps are still a
+// superset of those any pixel centre can reach with alpha >= 1/255; a non-finite reciprocal (a
+// denormal conic term) falls back to "every cell".  The binning keeps make_band_cut, which the
+// oracle restates operation for operation.
+__device__ __forceinline__ BandCut make_band_cut_fast(float mx, float my, float ca, float cb,
+                                                      float cc, float qc) {
+  BandCut s{};
+  s.mx = mx; s.my = my;
+  if (qc == -2.0f) { s.mode = 0; return s; }
+  s.mode = 1;
+  if (qc < 0.0f) return s;
+  const float det = ca * cc - cb * cb;
+  if (!(det > 0.0f)) return s;
+  const float idet = __builtin_amdgcn_rcpf(det), ica = __builtin_amdgcn_rcpf(ca),
+              icc = __builtin_amdgcn_rcpf(cc);
+  if (!(idet < 3.0e38f && ica < 3.0e38f && icc < 3.0e38f)) return s;
+  const float h2x = cc * idet, h2y = ca * idet;
+  const float ta = ca * h2x + cc * h2y + 2.0f * fabsf(cb) * sqrtf(h2x * h2y);
+  if (!(1e-4f * ta < 0.5f)) return s;
+  const float Q = (qc + 2e-2f) * __builtin_amdgcn_rcpf(1.0f - 1e-4f * ta) * 1.001f;
+  s.mode = 2;
+  s.ica = ica;
+  s.cb = cb;
+  s.det = det;
+  s.caQ = ca * Q;
+  s.hx = sqrtf(Q * h2x) * 1.001f + 1e-3f;
+  s.hy = sqrtf(Q * h2y) * 1.001f + 1e-3f;
+  s.dyl = cb * (s.hx * icc);
+  s.slack = 2e-3f + 4e-6f * fabsf(mx) + 1e-4f * s.hx;
+  return s;
+}
 // The ellipse's x-extent [xl, xr] (relative to mx, slack included) over the pixel-centre rows
 // [y0, y1]; false when it misses the band.
 __device__ __forceinline__ bool band_extent(const BandCut& s, float y0, float y1, float& xl,

@@ -109,7 +109,7 @@ __device__ __forceinline__ void pixel_of(uint32_t tx, uint32_t ty, uint32_t t, u
 // 8-row bands, each quadrant an interval overlap).
 __device__ __forceinline__ uint32_t wave_mask(float4 r0, float4 r1, float qc, uint32_t tx,
                                               uint32_t ty) {
-  const BandCut s = make_band_cut(r0.x, r0.y, r0.z, r0.w, r1.x, qc);
+  const BandCut s = make_band_cut_fast(r0.x, r0.y, r0.z, r0.w, r1.x, qc);
   if (s.mode == 0) return 0u;
   if (s.mode == 1) return 0xfu;
   const float xa = (float)(tx * kTile) - s.mx;
@@ -133,7 +133,7 @@ __device__ __forceinline__ uint32_t wave_mask(float4 r0, float4 r1, float qc, ui
 // x-extent in each band is found once and each (quadrant, half) is an interval overlap.
 __device__ __forceinline__ uint32_t half_mask_bands(float4 r0, float4 r1, float qc, uint32_t tx,
                                                     uint32_t ty, int w0) {
-  const BandCut s = make_band_cut(r0.x, r0.y, r0.z, r0.w, r1.x, qc);
+  const BandCut s = make_band_cut_fast(r0.x, r0.y, r0.z, r0.w, r1.x, qc);
   if (s.mode == 0) return 0u;
   if (s.mode == 1) return 0xffu;
   // the band rows and column starts are re-derived here for each batch: the backend would hoist
@@ -849,7 +849,7 @@ __device__ __forceinline__ void pixel_of_blk(uint32_t tx, uint32_t ty, uint32_t 
 // every block of a quadrant that the box met (and cost four rectangle tests).
 __device__ __forceinline__ uint32_t block_mask(float4 r0, float4 r1, float qc, uint32_t tx,
                                                uint32_t ty) {
-  const BandCut s = make_band_cut(r0.x, r0.y, r0.z, r0.w, r1.x, qc);
+  const BandCut s = make_band_cut_fast(r0.x, r0.y, r0.z, r0.w, r1.x, qc);
   if (s.mode == 0) return 0u;
   if (s.mode == 1) return 0xffffu;
   const float xa = (float)(tx * kTile) - s.mx;  // the tile's first pixel column, relative
