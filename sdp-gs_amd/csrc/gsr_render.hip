@@ -994,6 +994,8 @@ __device__ __forceinline__ void render_fwd_blk_tile(const RenderArgs& a, uint32_
       float pw[4], al[4];
       float4 r1v[4], r2v[4];
       float f2v[4];
+      float Gv[4];
+      float tdist = 1.0f;  // min over the four of |op * G - 1/255| (the exact-path test)
 #pragma unroll
       for (int u = 0; u < 4; u++) {
         jj[u] = (packed >> (8 * u)) & 0xffu;
@@ -1005,10 +1007,20 @@ __device__ __forceinline__ void render_fwd_blk_tile(const RenderArgs& a, uint32_
         const float power = -0.5f * (r0.z * dx * dx + r1v[u].x * dy * dy) - r0.w * dx * dy;
         // entries past the group's list end get power = +1 and are skipped
         pw[u] = (k + u < nl) ? power : 1.0f;
-        float G = __builtin_amdgcn_exp2f(pw[u] * 1.44269504088896341f);
-        if (fabsf(r1v[u].y * G - (1.0f / 255.0f)) <= 2e-6f * (1.0f / 255.0f)) G = splat_exp(pw[u]);
-        al[u] = fminf(0.99f, r1v[u].y * G);
+        Gv[u] = __builtin_amdgcn_exp2f(pw[u] * 1.44269504088896341f);
+        const float d = fabsf(r1v[u].y * Gv[u] - (1.0f / 255.0f));
+        tdist = d < tdist ? d : tdist;
       }
+      // the exact path as one wave-uniform branch per four entries (as the backward's test
+      // phase) instead of a divergent branch per entry; the per-entry condition is unchanged
+      if (__ballot(tdist <= 2e-6f * (1.0f / 255.0f)) != 0ull) {
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+          if (fabsf(r1v[u].y * Gv[u] - (1.0f / 255.0f)) <= 2e-6f * (1.0f / 255.0f))
+            Gv[u] = splat_exp(pw[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u++) al[u] = fminf(0.99f, r1v[u].y * Gv[u]);
 #pragma unroll
       for (int u = 0; u < 4; u++) {
         if (done) continue;
