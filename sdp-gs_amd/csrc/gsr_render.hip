@@ -1023,31 +1023,32 @@ __device__ __forceinline__ void render_fwd_blk_tile(const RenderArgs& a, uint32_
       for (int u = 0; u < 4; u++) al[u] = fminf(0.99f, r1v[u].y * Gv[u]);
 #pragma unroll
       for (int u = 0; u < 4; u++) {
-        if (done) continue;
-        if (pw[u] > 0.0f) continue;
+        // one predicate per entry (the reference's skip / stop / blend decisions, NaN behaviour
+        // included) instead of three nested skips: one exec-mask region per entry
         const float alpha = al[u];
-        if (alpha < 1.0f / 255.0f) continue;
         const float test_T = T * (1 - alpha);
-        if (test_T < 0.0001f) {
-          done = true;
-          continue;
+        const bool take = !done && !(pw[u] > 0.0f) && !(alpha < 1.0f / 255.0f);
+        const bool stop = take && test_T < 0.0001f;
+        done = done || stop;
+        if (take && !stop) {
+          // blend weight alpha * T formed once (the reference forms col * alpha * T per channel,
+          // forward.cu:341-343: same value up to the rounding of one product)
+          const float wgt = alpha * T;
+          C[0] += r1v[u].w * wgt;
+          C[1] += r2v[u].x * wgt;
+          C[2] += r2v[u].y * wgt;
+          C[3] += r1v[u].z * wgt;
+          C[4] += wgt;
+          if (FEAT) {
+            C[5 % NC] += r2v[u].z * wgt;
+            C[6 % NC] += r2v[u].w * wgt;
+            C[7 % NC] += f2v[u] * wgt;
+          }
+          T = test_T;
+          // the reference counts every list position (forward.cu:328); skipped entries cannot
+          // blend
+          last_contributor = rel0 + jj[u] + 1;
         }
-        // blend weight alpha * T formed once (the reference forms col * alpha * T per channel,
-        // forward.cu:341-343: same value up to the rounding of one product)
-        const float wgt = alpha * T;
-        C[0] += r1v[u].w * wgt;
-        C[1] += r2v[u].x * wgt;
-        C[2] += r2v[u].y * wgt;
-        C[3] += r1v[u].z * wgt;
-        C[4] += wgt;
-        if (FEAT) {
-          C[5 % NC] += r2v[u].z * wgt;
-          C[6 % NC] += r2v[u].w * wgt;
-          C[7 % NC] += f2v[u] * wgt;
-        }
-        T = test_T;
-        // the reference counts every list position (forward.cu:328); skipped entries cannot blend
-        last_contributor = rel0 + jj[u] + 1;
       }
     }
   }
