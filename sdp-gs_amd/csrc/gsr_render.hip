@@ -895,12 +895,16 @@ __device__ __forceinline__ uint32_t build_group_lists(const uint16_t* s_mask, ui
   return grp == 0 ? n[0] : grp == 1 ? n[1] : grp == 2 ? n[2] : n[3];
 }
 
-// waves per SIMD the block-list forward is compiled for (VGPR budget 512 / n): 5 (96 VGPRs,
-// 4 spilled) measured 0.262 / 0.263 against 0.275 / 0.276 ms per 3-view launch at the default
-// 104 VGPRs (4 waves), profiles/r04_fwd_occ_ab.txt
+// waves per SIMD the block-list forward is compiled for (VGPR budget 512 / n): 7 (72 VGPRs, no
+// scratch) with its 2-entry steps; with 4-entry steps 5 waves (95 VGPRs) was the best (round 4:
+// 5 against 4, profiles/r04_fwd_occ_ab.txt).  Round 6: 2-entry steps at 7 waves 0.218 -> 0.204 ms
+// per 3-view launch; 1-entry steps at 7 or 8 waves 0.22 (profiles/r06_fwd_group_ab.txt).
 #ifndef GSR_FWD_BLK_WAVES
-#define GSR_FWD_BLK_WAVES 5
+#define GSR_FWD_BLK_WAVES 7
 #endif
+// list entries per step of a 16-lane group: their power -> G -> alpha tests first, then the
+// compositing in list order (2: the registers of a step fit 7 waves per SIMD)
+constexpr int kFG = 2;
 // G by the hardware exp2 (v_exp_f32, 3 instructions instead of the 17 of splat_exp) with
 // splat_exp wherever op * G lies within 2e-6 (relative) of 1/255 -- the alpha >= 1/255 decision
 // stays the oracle's exactly, G differs from splat_exp's by < 1e-6 relative (so the T < 1e-4 stop
@@ -984,20 +988,21 @@ __device__ __forceinline__ void render_fwd_blk_tile(const RenderArgs& a, uint32_
     uint32_t nmax;
     const uint32_t nl = build_group_lists(s_mask, s_list[wid], cnt, wid, lane, grp, nmax);
     const uint32_t rel0 = base - range.x;
-    // four entries of the group's list per iteration: their (independent) Gaussian weights are
+    // kFG entries of the group's list per iteration: their (independent) Gaussian weights are
     // evaluated together, then composited in list order exactly as the reference's per-splat
     // loop -- same operations, same order, per pixel
-    for (uint32_t k = 0; k < nmax; k += 4) {
+    for (uint32_t k = 0; k < nmax; k += kFG) {
       if (__ballot(!done) == 0ull) break;  // wave-uniform
-      const uint32_t packed = *reinterpret_cast<const uint32_t*>(&s_list[wid][grp][k]);
-      uint32_t jj[4];
-      float pw[4], al[4];
-      float4 r1v[4], r2v[4];
-      float f2v[4];
-      float Gv[4];
-      float tdist = 1.0f;  // min over the four of |op * G - 1/255| (the exact-path test)
+      static_assert(kFG == 2, "one 16-bit list read per step");
+      const uint32_t packed = *reinterpret_cast<const uint16_t*>(&s_list[wid][grp][k]);
+      uint32_t jj[kFG];
+      float pw[kFG], al[kFG];
+      float4 r1v[kFG], r2v[kFG];
+      float f2v[kFG];
+      float Gv[kFG];
+      float tdist = 1.0f;  // min over the step's entries of |op * G - 1/255| (exact-path test)
 #pragma unroll
-      for (int u = 0; u < 4; u++) {
+      for (int u = 0; u < kFG; u++) {
         jj[u] = (packed >> (8 * u)) & 0xffu;
         const float4 r0 = s_r0[jj[u]];
         r1v[u] = s_r1[jj[u]];
@@ -1011,18 +1016,18 @@ __device__ __forceinline__ void render_fwd_blk_tile(const RenderArgs& a, uint32_
         const float d = fabsf(r1v[u].y * Gv[u] - (1.0f / 255.0f));
         tdist = d < tdist ? d : tdist;
       }
-      // the exact path as one wave-uniform branch per four entries (as the backward's test
+      // the exact path as one wave-uniform branch per step (as the backward's test
       // phase) instead of a divergent branch per entry; the per-entry condition is unchanged
       if (__ballot(tdist <= 2e-6f * (1.0f / 255.0f)) != 0ull) {
 #pragma unroll
-        for (int u = 0; u < 4; u++)
+        for (int u = 0; u < kFG; u++)
           if (fabsf(r1v[u].y * Gv[u] - (1.0f / 255.0f)) <= 2e-6f * (1.0f / 255.0f))
             Gv[u] = splat_exp(pw[u]);
       }
 #pragma unroll
-      for (int u = 0; u < 4; u++) al[u] = fminf(0.99f, r1v[u].y * Gv[u]);
+      for (int u = 0; u < kFG; u++) al[u] = fminf(0.99f, r1v[u].y * Gv[u]);
 #pragma unroll
-      for (int u = 0; u < 4; u++) {
+      for (int u = 0; u < kFG; u++) {
         // one predicate per entry (the reference's skip / stop / blend decisions, NaN behaviour
         // included) instead of three nested skips: one exec-mask region per entry
         const float alpha = al[u];

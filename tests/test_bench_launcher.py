@@ -84,7 +84,10 @@ def test_dist2_roofline_bracket_is_collective_free():
     assert one["collective_exposed_ms"] is None
     assert two["collective_exposed_ms"] is not None
     # the dominant kernel can differ between the two runs on a scene this small: compare the N = 2
-    # bracket with the same kernel's N = 1 launch time
+    # bracket with the same kernel's N = 1 launch time.  The two ranks' timed regions run at the
+    # same time on the one GPU, so the bracket also holds the other rank's kernels: a fair share
+    # is ~2x, and on this tiny scene a short kernel beside the other rank's wider launches has
+    # measured up to ~3.6x; a bracket that spans the all-reduce read 33x (round 5).
     r2 = two["roofline"]
     base = one["kernels"][r2["kernel"]]["avg_ms"]
-    assert r2["avg_ms"] <= 2.0 * base, (r2, one["kernels"])
+    assert r2["avg_ms"] <= 5.0 * base, (r2["kernel"], r2["avg_ms"], base)
